@@ -1,0 +1,156 @@
+#!/usr/bin/env python
+"""Headline benchmark: train_ffm rows/sec on Criteo-shaped sparse data (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+One process per GPU.  Each rank holds a full FFM model replica in HBM
+(2^20 hashed features x 39 fields x k=4, fp32 V + AdaGrad G + FTRL state, ~1.3 GB) and
+trains on its own shard of synthetic Criteo-shaped rows (weak scaling: per-GPU batch is
+fixed).  A step = one fused ``hm_ffm_step`` launch over ``--batch`` rows per GPU; every
+``--mix-every`` steps the replicas are averaged with a bucketed RCCL all-reduce over xGMI
+(the MixServer replacement) — that mixing cost is inside the timed region.
+
+Timing: W untimed warmup steps, then barrier + synchronize, K timed steps, synchronize +
+barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the
+mixed model on held-out rows and the planted model's logloss (the Bayes floor).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_METRIC = "rows/sec (node) FFM on Criteo-shaped sparse at 1/2/4/8 MI355X; logloss parity"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=262144, help="rows per GPU per step")
+    ap.add_argument("--hash-bits", type=int, default=20)
+    ap.add_argument("--factors", type=int, default=4)
+    ap.add_argument("--mix-every", type=int, default=10)
+    ap.add_argument("--resident-batches", type=int, default=8)
+    ap.add_argument("--eval-rows", type=int, default=262144)
+    ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
+    ap.add_argument("--device", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from hivemall_amd.parallel.dist import init_distributed
+    from hivemall_amd.parallel.mix import ModelMixer
+    from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.ops.ffm import ffm_step
+    from hivemall_amd.io.synthetic import criteo_like
+
+    ctx = init_distributed(device=args.device)
+    dev = ctx.device
+    world, rank = ctx.world_size, ctx.rank
+    if args.gpus != world and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    F = 39
+    NF = 1 << args.hash_bits
+    B = args.batch
+    nres = max(1, args.resident_batches)
+
+    # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
+    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=dev)
+    opts = (f"-classification -factors {args.factors} -feature_hashing {args.hash_bits} "
+            f"-num_fields {F} -seed 31 -batch_size {B}")
+    tr = FFMTrainer(opts, device=dev)
+    tr.init_state(NF, F)
+    st, hyper = tr.state, tr.hyper
+    mixer = ModelMixer(ctx)
+    mix_tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+    grid = args.grid
+
+    def step(i):
+        s = (i % nres) * B
+        ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True, grid=grid)
+        if world > 1 and (i + 1) % args.mix_every == 0:
+            mixer.average(mix_tensors)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        step(i)
+    sync()
+    ctx.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    sync()
+    ctx.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    elapsed = mixer.all_reduce_scalar(elapsed, "max")
+    ms_per_step = 1000.0 * elapsed / max(1, args.steps)
+    rows_total = float(B) * world * args.steps
+    rows_per_s = rows_total / elapsed
+
+    # ---- quality: final mix, then held-out logloss vs the planted-model floor ----
+    if world > 1:
+        mixer.average(mix_tensors)
+    ll = floor = None
+    if rank == 0:
+        eidx, ey, elogit = criteo_like(args.eval_rows, args.hash_bits, seed=999_999, device=dev,
+                                       return_logit=True)
+        pred = torch.empty(args.eval_rows, dtype=torch.float32, device=dev)
+        for s in range(0, args.eval_rows, B):
+            e = min(args.eval_rows, s + B)
+            ffm_step(st, eidx[s:e], None, None, None, hyper, train=False, pred=pred[s:e])
+        yy = (ey > 0).float()
+        ll = torch.nn.functional.binary_cross_entropy_with_logits(pred, yy).item()
+        floor = torch.nn.functional.binary_cross_entropy_with_logits(elogit, yy).item()
+    if rank == 0:
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(rows_per_s, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (Criteo-shaped: 39 fields, Kaggle-DAC cardinalities, power-law "
+                    "values, planted FM logit), random-init weights",
+            "config": {
+                "model": f"train_ffm (k={args.factors}, 2^{args.hash_bits} hashed features, "
+                         f"{F} fields, AdaGrad V + FTRL w, instance L2 norm)",
+                "global_batch": B * world,
+                "seq_len": F,
+                "nnz_per_row": F,
+                "parallelism": f"dp{world}",
+                "mix_every": args.mix_every,
+                "mixed_bytes_per_mix": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
+            },
+            "logloss_heldout": round(ll, 5) if ll is not None else None,
+            "logloss_planted_floor": round(floor, 5) if floor is not None else None,
+            "rows_trained_per_rank": B * (args.steps + args.warmup),
+        }
+        print(json.dumps(out), flush=True)
+    from hivemall_amd.parallel.dist import shutdown
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

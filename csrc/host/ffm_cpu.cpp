@@ -1,0 +1,119 @@
+// CPU engine for FFM: same update rule and layout as csrc/kernels/ffm.hip, processed
+// strictly row by row (Hivemall's per-mapper online semantics, no Hogwild).  Used for CPU
+// runs (world_size=1 plumbing) and as the numerical oracle for the GPU kernel.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#define HM_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+inline float ftrl_weight(float z, float n, float alpha, float beta, float l1, float l2) {
+    if (std::fabs(z) <= l1) return 0.f;
+    const float s = z > 0.f ? 1.f : -1.f;
+    return -(z - s * l1) / ((beta + std::sqrt(n)) / alpha + l2);
+}
+
+inline float ftrl_update(float* z, float* n, float w, float g, float alpha, float beta, float l1,
+                         float l2) {
+    const float n0 = *n, n1 = n0 + g * g;
+    const float sigma = (std::sqrt(n1) - std::sqrt(n0)) / alpha;
+    *z += g - sigma * w;
+    *n = n1;
+    return ftrl_weight(*z, n1, alpha, beta, l1, l2);
+}
+
+inline float log1pexp(float x) { return x > 0.f ? x + std::log1p(std::exp(-x)) : std::log1p(std::exp(x)); }
+
+}  // namespace
+
+HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
+                           const int32_t* fld, const float* val, const float* y, float* V,
+                           float* G, float* w, float* wz, float* wn, float* bias, float* pred,
+                           float* loss) {
+    const int B = ip[0], F = ip[1], NF = ip[2], NFLD = ip[3], Kp = ip[4];
+    const int cls = ip[5], train = ip[6], use_lin = ip[7], use_bias = ip[8], norm = ip[9];
+    const float eta0 = hp[0], eps = hp[1], lv = hp[2], alpha = hp[3], beta = hp[4];
+    const float l1 = hp[5], l2 = hp[6], tmin = hp[7], tmax = hp[8];
+    const size_t fstride = (size_t)NFLD * Kp;
+    std::vector<int> ri(F), rf(F);
+    std::vector<float> rx(F);
+    std::vector<float> snap((size_t)F * F * Kp);
+    for (int r = 0; r < B; ++r) {
+        float sq = 0.f;
+        for (int a = 0; a < F; ++a) {
+            const size_t o = (size_t)r * F + a;
+            int i = idx[o];
+            int f = fld ? fld[o] : a;
+            float x = val ? val[o] : 1.f;
+            if (i < 0 || i >= NF || f < 0 || f >= NFLD) { i = -1; x = 0.f; }
+            ri[a] = i;
+            rf[a] = f < 0 ? 0 : (f >= NFLD ? NFLD - 1 : f);
+            rx[a] = x;
+            sq += x * x;
+        }
+        const float scale = (norm && sq > 0.f) ? 1.f / std::sqrt(sq) : 1.f;
+        // snapshot of the row's slot vectors (matches the LDS staging of the GPU kernel)
+        for (int a = 0; a < F; ++a)
+            for (int b = 0; b < F; ++b) {
+                float* dst = &snap[((size_t)a * F + b) * Kp];
+                if (a != b && ri[a] >= 0 && ri[b] >= 0)
+                    std::memcpy(dst, V + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp, sizeof(float) * Kp);
+                else
+                    std::memset(dst, 0, sizeof(float) * Kp);
+            }
+        double p = 0.0;
+        for (int a = 0; a < F; ++a)
+            for (int b = a + 1; b < F; ++b) {
+                if (ri[a] < 0 || ri[b] < 0) continue;
+                const float* u = &snap[((size_t)a * F + b) * Kp];
+                const float* v = &snap[((size_t)b * F + a) * Kp];
+                float d = 0.f;
+                for (int k = 0; k < Kp; ++k) d += u[k] * v[k];
+                p += (double)d * rx[a] * rx[b] * scale * scale;
+            }
+        if (use_lin)
+            for (int a = 0; a < F; ++a)
+                if (ri[a] >= 0) p += (double)w[ri[a]] * rx[a] * scale;
+        if (use_bias) p += bias[0];
+        const float yy = y ? y[r] : 0.f;
+        float kappa;
+        if (cls) {
+            const float e = yy * (float)p;
+            kappa = -yy / (1.f + std::exp(e));
+            if (loss) loss[r] = log1pexp(-e);
+            if (pred) pred[r] = (float)p;
+        } else {
+            const float pc = std::fmin(std::fmax((float)p, tmin), tmax);
+            kappa = pc - yy;
+            if (loss) loss[r] = 0.5f * kappa * kappa;
+            if (pred) pred[r] = pc;
+        }
+        if (!train) continue;
+        const float ks = kappa * scale * scale;
+        for (int a = 0; a < F; ++a)
+            for (int b = 0; b < F; ++b) {
+                if (a == b || ri[a] < 0 || ri[b] < 0) continue;
+                const float coef = ks * rx[a] * rx[b];
+                float* pv = V + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp;
+                float* pg = G + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp;
+                const float* own = &snap[((size_t)a * F + b) * Kp];
+                const float* par = &snap[((size_t)b * F + a) * Kp];
+                for (int k = 0; k < Kp; ++k) {
+                    const float g = coef * par[k] + lv * own[k];
+                    pg[k] += g * g;
+                    pv[k] = own[k] - eta0 * g / std::sqrt(pg[k] + eps);
+                }
+            }
+        if (use_lin)
+            for (int a = 0; a < F; ++a) {
+                const int i = ri[a];
+                if (i < 0) continue;
+                w[i] = ftrl_update(wz + i, wn + i, w[i], kappa * rx[a] * scale, alpha, beta, l1, l2);
+            }
+        if (use_bias) bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, alpha, beta, 0.f, 0.f);
+    }
+    return 0;
+}

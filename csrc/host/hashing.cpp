@@ -1,0 +1,224 @@
+// Host-side hashing + feature-string data plane (C ABI, loaded via ctypes).
+//
+// * MurmurHash3_x86_32 over UTF-8 bytes.  Hivemall's hivemall.utils.hashing.MurmurHash3
+//   (core/src/main/java/hivemall/utils/hashing/MurmurHash3.java) hashes the
+//   UTF-8 encoding of a CharSequence with seed 0x9747b28c; `mhash` reduces it modulo
+//   num_features (default 2^24), fixes up negatives and returns a value starting from 1.
+// * Feature strings "name:value" / "name" / "field:index:value" are parsed here so the
+//   Python layer never loops over individual features.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#define HM_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+uint32_t murmur3_x86_32(const uint8_t* data, int len, uint32_t seed) {
+    const int nblocks = len / 4;
+    uint32_t h1 = seed;
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    for (int i = 0; i < nblocks; ++i) {
+        uint32_t k1;
+        std::memcpy(&k1, data + 4 * i, 4);  // little-endian host
+        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+        h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+    }
+    const uint8_t* tail = data + nblocks * 4;
+    uint32_t k1 = 0;
+    switch (len & 3) {
+        case 3: k1 ^= (uint32_t)tail[2] << 16; [[fallthrough]];
+        case 2: k1 ^= (uint32_t)tail[1] << 8; [[fallthrough]];
+        case 1: k1 ^= tail[0]; k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint32_t)len;
+    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
+    return h1;
+}
+
+inline int32_t mhash_reduce(uint32_t h, int32_t num_features) {
+    int32_t r = (int32_t)h % num_features;  // Java int % semantics
+    if (r < 0) r += num_features;
+    return r + 1;
+}
+
+// Strict integer parse of [p, p+n) ; returns false if not an integer literal.
+bool parse_int(const char* p, int n, int64_t* out) {
+    if (n <= 0 || n > 19) return false;
+    int i = 0;
+    bool neg = false;
+    if (p[0] == '-' || p[0] == '+') { neg = p[0] == '-'; i = 1; if (n == 1) return false; }
+    int64_t v = 0;
+    for (; i < n; ++i) {
+        const char c = p[i];
+        if (c < '0' || c > '9') return false;
+        v = v * 10 + (c - '0');
+    }
+    *out = neg ? -v : v;
+    return true;
+}
+
+bool parse_float(const char* p, int n, float* out) {
+    if (n <= 0 || n > 63) return false;
+    char tmp[64];
+    std::memcpy(tmp, p, n);
+    tmp[n] = 0;
+    char* end = nullptr;
+    const double d = std::strtod(tmp, &end);
+    if (end != tmp + n) return false;
+    *out = (float)d;
+    return true;
+}
+
+struct Dict {
+    std::unordered_map<std::string, int64_t> map;
+    std::vector<std::string> keys;
+    int64_t encode(std::string_view s, bool add) {
+        auto it = map.find(std::string(s));
+        if (it != map.end()) return it->second;
+        if (!add) return -1;
+        const int64_t id = (int64_t)keys.size();
+        keys.emplace_back(s);
+        map.emplace(keys.back(), id);
+        return id;
+    }
+};
+
+}  // namespace
+
+HM_API uint32_t hm_murmur3(const uint8_t* data, int len, uint32_t seed) {
+    return murmur3_x86_32(data, len, seed);
+}
+
+HM_API void hm_murmur3_batch(const uint8_t* buf, const int64_t* off, int64_t n, uint32_t seed,
+                             uint32_t* out) {
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = murmur3_x86_32(buf + off[i], (int)(off[i + 1] - off[i]), seed);
+}
+
+HM_API void hm_mhash_batch(const uint8_t* buf, const int64_t* off, int64_t n, uint32_t seed,
+                           int32_t num_features, int32_t* out) {
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = mhash_reduce(murmur3_x86_32(buf + off[i], (int)(off[i + 1] - off[i]), seed),
+                              num_features);
+}
+
+// ---------------------------------------------------------------- dictionary
+HM_API void* hm_dict_new() { return new Dict(); }
+HM_API void hm_dict_free(void* d) { delete static_cast<Dict*>(d); }
+HM_API int64_t hm_dict_size(void* d) { return (int64_t)static_cast<Dict*>(d)->keys.size(); }
+HM_API void hm_dict_encode(void* d, const uint8_t* buf, const int64_t* off, int64_t n, int add,
+                           int64_t* out) {
+    Dict* D = static_cast<Dict*>(d);
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = D->encode(std::string_view((const char*)buf + off[i], (size_t)(off[i + 1] - off[i])), add != 0);
+}
+// Two-phase dump: call with buf=null to get total bytes; then with buffers.
+HM_API int64_t hm_dict_dump(void* d, uint8_t* buf, int64_t* off) {
+    Dict* D = static_cast<Dict*>(d);
+    int64_t tot = 0;
+    for (auto& k : D->keys) tot += (int64_t)k.size();
+    if (!buf) return tot;
+    int64_t p = 0;
+    for (size_t i = 0; i < D->keys.size(); ++i) {
+        off[i] = p;
+        std::memcpy(buf + p, D->keys[i].data(), D->keys[i].size());
+        p += (int64_t)D->keys[i].size();
+    }
+    off[D->keys.size()] = p;
+    return tot;
+}
+
+// ---------------------------------------------------------------- feature parsing
+// mode 0: names must be integers (returned as-is)
+// mode 1: names dictionary-encoded through `dict` (new names added when add_new)
+// mode 2: names hashed with mhash(name, num_features) (1-based)
+// mode 3: integer names kept, non-integer names dictionary-encoded and offset by int_base
+// Returns -1 on success, else the index of the first malformed feature.
+HM_API int64_t hm_parse_features(const uint8_t* buf, const int64_t* off, int64_t n, int mode,
+                                 void* dict, int add_new, int32_t num_features, uint32_t seed,
+                                 int64_t int_base, int64_t* idx_out, float* val_out) {
+    Dict* D = static_cast<Dict*>(dict);
+    for (int64_t i = 0; i < n; ++i) {
+        const char* s = (const char*)buf + off[i];
+        const int len = (int)(off[i + 1] - off[i]);
+        const char* colon = (const char*)std::memchr(s, ':', (size_t)len);
+        int nlen = len;
+        float v = 1.f;
+        if (colon) {
+            nlen = (int)(colon - s);
+            if (!parse_float(colon + 1, len - nlen - 1, &v)) return i;
+        }
+        if (nlen <= 0) return i;
+        int64_t id;
+        switch (mode) {
+            case 0:
+                if (!parse_int(s, nlen, &id)) return i;
+                break;
+            case 1:
+                id = D->encode(std::string_view(s, (size_t)nlen), add_new != 0);
+                break;
+            case 2:
+                id = mhash_reduce(murmur3_x86_32((const uint8_t*)s, nlen, seed), num_features);
+                break;
+            default:
+                if (!parse_int(s, nlen, &id)) {
+                    id = D->encode(std::string_view(s, (size_t)nlen), add_new != 0);
+                    if (id >= 0) id += int_base;
+                }
+        }
+        idx_out[i] = id;
+        val_out[i] = v;
+    }
+    return -1;
+}
+
+// FFM features "field:index[:value]".  field: integer (or mhash'd into num_fields when not
+// an integer); index: integer (mod num_features when hash_ints) or mhash'd into num_features.
+HM_API int64_t hm_parse_ffm_features(const uint8_t* buf, const int64_t* off, int64_t n,
+                                     int32_t num_features, int32_t num_fields, int hash_ints,
+                                     uint32_t seed, int32_t* fld_out, int32_t* idx_out,
+                                     float* val_out) {
+    for (int64_t i = 0; i < n; ++i) {
+        const char* s = (const char*)buf + off[i];
+        const int len = (int)(off[i + 1] - off[i]);
+        const char* c1 = (const char*)std::memchr(s, ':', (size_t)len);
+        if (!c1) return i;
+        const int flen = (int)(c1 - s);
+        const char* rest = c1 + 1;
+        const int rlen = len - flen - 1;
+        const char* c2 = (const char*)std::memchr(rest, ':', (size_t)rlen);
+        const int ilen = c2 ? (int)(c2 - rest) : rlen;
+        float v = 1.f;
+        if (c2 && !parse_float(c2 + 1, rlen - ilen - 1, &v)) return i;
+        int64_t f, id;
+        if (!parse_int(s, flen, &f)) {
+            if (flen <= 0) return i;
+            f = mhash_reduce(murmur3_x86_32((const uint8_t*)s, flen, seed), num_fields) - 1;
+        }
+        if (f < 0 || f >= num_fields) return i;
+        if (ilen <= 0) return i;
+        if (parse_int(rest, ilen, &id)) {
+            if (hash_ints) {
+                id %= num_features;
+                if (id < 0) id += num_features;
+            } else if (id < 0 || id >= num_features) {
+                return i;
+            }
+        } else {
+            id = mhash_reduce(murmur3_x86_32((const uint8_t*)rest, ilen, seed), num_features) - 1;
+        }
+        fld_out[i] = (int32_t)f;
+        idx_out[i] = (int32_t)id;
+        val_out[i] = v;
+    }
+    return -1;
+}

@@ -1,0 +1,91 @@
+// Shared device helpers for the hivemall_amd HIP kernel library (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * wave64: lane = threadIdx.x & 63, all warp-level idioms assume 64 lanes.
+//   * Every launcher is an `extern "C" int hm_*(..., hipStream_t)` that returns the
+//     hipError_t of the launch (0 = ok); Python checks it and raises.
+//   * Launchers never allocate or synchronise (they are hipGraph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define HM_WAVE 64
+
+#define HM_API extern "C" __attribute__((visibility("default")))
+
+#define HM_LAUNCH_RET() return (int)hipGetLastError()
+
+namespace hm {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (HM_WAVE - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x / HM_WAVE; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, HM_WAVE);
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, HM_WAVE);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, HM_WAVE));
+    return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `scratch` needs 16 floats.
+// Every thread receives the total.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+    v = wave_sum(v);
+    const int nw = blockDim.x / HM_WAVE;
+    if (lane_id() == 0) scratch[wave_id()] = v;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[i];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// Numerically safe log(1 + exp(x)).
+__device__ __forceinline__ float log1pexp(float x) {
+    return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x));
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+    return __uint_as_float(((uint32_t)h) << 16);
+}
+// Round-to-nearest-even f32 -> bf16 (NaN-preserving path is not needed for weights).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+// XCD-aware bijective remap of a flat block id (cdna_hip_programming.md §5, "XCD swizzle
+// must be bijective"): consecutive logical tiles land on the same XCD / L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int nx = 8;
+    const int xcd = bid % nx;
+    const int q = nwg / nx, r = nwg % nx;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + bid / nx;
+}
+
+// Counter-based RNG (splitmix64 finaliser) — deterministic per (seed, stream, counter).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float u01(uint64_t h) {  // [0,1)
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
+}  // namespace hm

@@ -1,0 +1,109 @@
+"""In-tree build of the native libraries.
+
+Two shared objects are produced under ``hivemall_amd/_lib``:
+
+* ``libhm_hip.so``  — every ``csrc/kernels/*.hip`` compiled by ``hipcc --offload-arch=gfx950``
+  (CDNA4 only; no other targets, no CUDA).  C ABI, launched from Python through ctypes on
+  the current torch HIP stream.
+* ``libhm_host.so`` — ``csrc/host/*.cpp`` (the CPU data plane + CPU learner engine),
+  compiled with g++ -O3 -fopenmp.  Loadable everywhere, needs no GPU.
+
+The build is incremental (per-object mtime check against sources + headers) and runs the
+per-file compiles in parallel.  ``python -m hivemall_amd._build`` builds everything.
+"""
+from __future__ import annotations
+
+import concurrent.futures as _cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "_lib"
+OBJDIR = ROOT / "build" / "obj"
+
+HIP_ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", shutil.which("g++") or "c++")
+
+HIP_FLAGS = [
+    f"--offload-arch={HIP_ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
+    "-munsafe-fp-atomics", "-Wno-unused-result",
+]
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-march=x86-64-v2", "-Wall",
+              "-Wno-unused-function"]
+
+HIP_LIB = LIBDIR / "libhm_hip.so"
+HOST_LIB = LIBDIR / "libhm_host.so"
+
+
+def _headers(d: Path):
+    return [p for p in d.glob("*.h")] + [p for p in d.glob("*.hpp")]
+
+
+def _newest(paths):
+    return max((p.stat().st_mtime for p in paths), default=0.0)
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    return target.stat().st_mtime < _newest(deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), file=sys.stderr)
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed:\n{' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs):
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    hdrs = []
+    for s in srcs:
+        hdrs.extend(_headers(s.parent))
+    objs = []
+    todo = []
+    for s in srcs:
+        o = OBJDIR / (s.parent.name + "_" + s.name + ".o")
+        objs.append(o)
+        if _stale(o, [s] + hdrs):
+            todo.append((s, o))
+    if todo:
+        with _cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_run, [compiler, *flags, "-c", s, "-o", o], verbose) for s, o in todo]
+            for f in futs:
+                f.result()
+    if todo or _stale(lib, objs):
+        tmp = lib.with_suffix(".so.tmp")
+        _run([compiler, "-shared", "-o", tmp, *objs, *link_flags], verbose)
+        os.replace(tmp, lib)
+    return lib
+
+
+def build_host(verbose: bool = False, jobs: int = 8) -> Path:
+    srcs = sorted((CSRC / "host").glob("*.cpp"))
+    return _build_lib(srcs, CXX, HOST_FLAGS, HOST_LIB, ["-fopenmp"], verbose, jobs)
+
+
+def build_hip(verbose: bool = False, jobs: int = 8) -> Path:
+    srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    return _build_lib(srcs, HIPCC, HIP_FLAGS, HIP_LIB, [f"--offload-arch={HIP_ARCH}"], verbose, jobs)
+
+
+def build_all(verbose: bool = False, jobs: int | None = None) -> None:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    build_host(verbose, jobs)
+    build_hip(verbose, jobs)
+
+
+if __name__ == "__main__":
+    build_all(verbose="-v" in sys.argv)
+    print("built:", HOST_LIB, HIP_LIB)

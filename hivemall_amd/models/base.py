@@ -1,0 +1,105 @@
+"""Common learner machinery (the LearnerBaseUDTF / UDTFWithOptions layer).
+
+A learner is created from a Hivemall option string, consumes rows (the UDTF ``process``
+calls, here batched), trains for ``-iters`` epochs with the ``ConversionState`` convergence
+check, and emits its model table (the UDTF ``close``/``forwardModel``) as a pandas frame
+with the upstream column layout.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+from typing import Any
+
+import numpy as np
+import torch
+
+from ..utils.options import Options, opt, flag
+
+log = logging.getLogger("hivemall_amd")
+
+
+def default_device() -> torch.device:
+    env = os.environ.get("HM_DEVICE")
+    if env:
+        return torch.device(env)
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+def resolve_device(device) -> torch.device:
+    if device is None:
+        return default_device()
+    return torch.device(device)
+
+
+class ConversionState:
+    """Epoch-level convergence check (hivemall.common.ConversionState).
+
+    Training stops when the relative decrease of the cumulative loss between two epochs is
+    below ``cv_rate`` (default 0.005), unless ``-disable_cv``.
+    """
+
+    def __init__(self, check: bool = True, cv_rate: float = 0.005):
+        self.check = check
+        self.cv_rate = cv_rate
+        self.prev = math.inf
+        self.curr = 0.0
+        self.epoch = 0
+        self.history: list[float] = []
+
+    def incr_loss(self, v: float) -> None:
+        self.curr += float(v)
+
+    def is_converged(self) -> bool:
+        self.history.append(self.curr)
+        converged = False
+        if self.check and self.prev < math.inf and self.prev > 0:
+            change = (self.prev - self.curr) / self.prev
+            if 0 <= change < self.cv_rate:
+                converged = True
+        self.prev = self.curr
+        self.curr = 0.0
+        self.epoch += 1
+        return converged
+
+
+COMMON_ITER_OPTS = [
+    opt("iters", "iterations", 1, int, "The maximum number of iterations (epochs)", aliases=("iter",)),
+    opt("cv_rate", "convergence_rate", 0.005, float, "Threshold to determine convergence"),
+    flag("disable_cv", "disable_cvtest", "Whether to disable convergence check"),
+    opt("seed", None, -1, int, "Seed value for random number generator"),
+    opt("batch_size", None, 65536, int, "[engine] rows per device kernel launch"),
+    opt("mix_interval", None, 0, int, "[engine] RCCL model-mix every N batches (0 = at end only)"),
+]
+
+
+def parse_labels_binary(y) -> np.ndarray:
+    """0/1 or -1/+1 labels -> float32 {-1,+1} (BinaryOnlineClassifierUDTF label handling)."""
+    a = np.asarray(y, dtype=np.float32).reshape(-1)
+    out = np.where(a > 0, 1.0, -1.0).astype(np.float32)
+    return out
+
+
+class Learner:
+    """Base for all learners; subclasses define OPTIONS, NAME and the train loop."""
+
+    NAME = "learner"
+    OPTIONS: list = []
+
+    @classmethod
+    def options(cls) -> Options:
+        return Options(cls.OPTIONS, cls.NAME)
+
+    def __init__(self, options: str | None = None, device=None, **kw: Any):
+        self.cl = self.options().parse(options)
+        self.device = resolve_device(device)
+        self.seed = self.cl.get("seed")
+        if self.seed is None or self.seed < 0:
+            self.seed = 31
+        self.mixer = kw.pop("mixer", None)
+        self.rank = kw.pop("rank", 0)
+        self.kw = kw
+
+    def opt(self, name: str, default=None):
+        return self.cl.get(name, default)

@@ -1,0 +1,74 @@
+"""FFM train/predict op: gfx950 kernel on ``cuda`` tensors, C++ engine on CPU tensors.
+
+Kernel: ``csrc/kernels/ffm.hip`` (hm_ffm_step).  CPU twin: ``csrc/host/ffm_cpu.cpp``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+
+
+@dataclass
+class FFMHyper:
+    eta0: float = 0.2
+    eps: float = 1.0
+    lambda_v: float = 1e-4
+    alpha: float = 0.2
+    beta: float = 1.0
+    lambda1: float = 1e-3
+    lambda2: float = 1e-4
+    min_target: float = -3.4e38
+    max_target: float = 3.4e38
+    classification: bool = True
+    use_linear: bool = True
+    use_bias: bool = True
+    norm: bool = True
+
+    def hp(self) -> np.ndarray:
+        return np.array([self.eta0, self.eps, self.lambda_v, self.alpha, self.beta, self.lambda1,
+                         self.lambda2, self.min_target, self.max_target], dtype=np.float32)
+
+
+def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
+             y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
+             pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
+             grid: int = 0) -> None:
+    """One fused pass over a padded-ELL batch.
+
+    state: dict with V, G ([NF, NFLD, Kp] f32), w, wz, wn ([NF] f32), bias ([4] f32).
+    idx/fld int32 [B, F]; val f32 [B, F]; y f32 [B] in {-1,+1} (classification) or real.
+    """
+    V = state["V"]
+    B, F = idx.shape
+    NF, NFLD, Kp = V.shape
+    assert idx.dtype == torch.int32 and idx.is_contiguous()
+    for t in (fld, val, y, pred, loss):
+        if t is not None:
+            assert t.device == V.device and t.is_contiguous(), "tensor device/layout mismatch"
+    if fld is not None:
+        assert fld.dtype == torch.int32 and fld.shape == idx.shape
+    if val is not None:
+        assert val.dtype == torch.float32 and val.shape == idx.shape
+    if y is not None:
+        assert y.shape[0] == B
+    if pred is not None:
+        assert pred.shape[0] >= B
+    if loss is not None:
+        assert loss.shape[0] >= B
+    ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
+                   int(hyper.use_bias), int(hyper.norm), int(grid)], dtype=np.int32)
+    hp = hyper.hp()
+    p = _native.ptr
+    args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(state["G"]),
+            p(state["w"]), p(state["wz"]), p(state["wn"]), p(state["bias"]), p(pred), p(loss))
+    if V.is_cuda:
+        rc = _native.hip().hm_ffm_step(*args, _native.stream_of(V.device))
+        _native.check(rc, "hm_ffm_step")
+    else:
+        rc = _native.host().hm_ffm_step_cpu(*args)
+        if rc != 0:
+            raise RuntimeError(f"hm_ffm_step_cpu failed: {rc}")

@@ -1,0 +1,120 @@
+"""Multi-process (gloo, world_size=2) tests of the RCCL mixing layer — the MixServerTest
+analogue: N learners, one mixed model."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import tests.test_dist as T
+    from hivemall_amd.parallel import dist as D
+
+    D._CTX = None
+    ctx = D.init_distributed(backend="gloo", device="cpu")
+    try:
+        q.put((rank, getattr(T, fn_name)(ctx)))
+    finally:
+        D.shutdown()
+
+
+def run_world(fn_name, world=2):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return out
+
+
+def _avg(ctx):
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    m = ModelMixer(ctx, bucket_mb=0.001, small_bytes=64)
+    big = torch.full((10000,), float(ctx.rank + 1))
+    small = torch.tensor([ctx.rank * 2.0, 1.0])
+    m.average([big, small])
+    return big.tolist()[:3] + small.tolist()
+
+
+def _kld(ctx):
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    m = ModelMixer(ctx)
+    w = torch.tensor([1.0, 2.0]) * (ctx.rank + 1)
+    cov = torch.tensor([0.5, 1.0]) * (ctx.rank + 1)
+    m.argmin_kld(w, cov)
+    return w.tolist() + cov.tolist()
+
+
+def _ffm_dp(ctx):
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.models.ffm import FFMBatch, FFMTrainer
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    idx, y = criteo_like(2000, hash_bits=10, seed=100 + ctx.rank)
+    t = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 10 -mix_interval 1 -batch_size 500",
+                   device="cpu", mixer=ModelMixer(ctx), rank=ctx.rank)
+    t.fit(batch=FFMBatch(idx, None, None, y))
+    return float(t.state["V"].sum()), float(t.state["w"].sum())
+
+
+def test_mix_average_bucketed():
+    out = run_world("_avg")
+    for r in (0, 1):
+        assert out[r] == [1.5, 1.5, 1.5, 1.0, 1.0]
+
+
+def test_mix_argmin_kld():
+    out = run_world("_kld")
+    # w_r = (r+1)*w, cov_r = (r+1)*c  ->  sum(w/c) / sum(1/c)
+    import numpy as np
+
+    w = np.array([1.0, 2.0]); c = np.array([0.5, 1.0])
+    num = w / c + 2 * w / (2 * c)
+    inv = 1 / c + 1 / (2 * c)
+    np.testing.assert_allclose(out[0], list(num / inv) + list(1 / inv), rtol=1e-6)
+    assert out[0] == out[1]
+
+
+def test_ffm_data_parallel_replicas_identical():
+    out = run_world("_ffm_dp")
+    assert out[0] == pytest.approx(out[1], rel=1e-6)
+
+
+def test_bench_torchrun_cpu_world2():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "512", "--hash-bits", "10",
+           "--mix-every", "1", "--eval-rows", "512", "--device", "cpu", "--resident-batches", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0

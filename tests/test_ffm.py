@@ -1,0 +1,111 @@
+import numpy as np
+import pytest
+import torch
+
+from hivemall_amd.io.synthetic import criteo_like
+from hivemall_amd.models.ffm import FFMBatch, FFMTrainer, train_ffm
+from hivemall_amd.ops.ffm import ffm_step
+from tests.oracle.ffm_oracle import ffm_train_rows
+
+
+def _trainer(dev, nf=64, nfld=6, k=4, extra=""):
+    t = FFMTrainer(f"-classification -factors {k} -seed 3 {extra}", device=dev)
+    t.init_state(nf, nfld)
+    return t
+
+
+def _np_state(t):
+    return {k: v.detach().cpu().numpy().astype(np.float64).copy() for k, v in t.state.items()}
+
+
+@pytest.mark.parametrize("use_bias", [False, True])
+def test_ffm_cpu_engine_matches_oracle(use_bias):
+    rng = np.random.default_rng(0)
+    B, F, NF = 40, 6, 64
+    idx = rng.integers(0, NF, size=(B, F)).astype(np.int32)
+    val = rng.uniform(0.5, 2.0, size=(B, F)).astype(np.float32)
+    y = np.where(rng.random(B) < 0.4, 1.0, -1.0).astype(np.float32)
+    t = _trainer("cpu", NF, F, extra="-w0" if use_bias else "")
+    ref = _np_state(t)
+    h = t.hyper
+    hp = dict(eta0=h.eta0, eps=h.eps, lambda_v=h.lambda_v, alpha=h.alpha, beta=h.beta,
+              lambda1=h.lambda1, lambda2=h.lambda2)
+    ref_loss, ref_pred = ffm_train_rows(ref, idx, y, hp, val=val, use_bias=use_bias)
+    loss = torch.empty(B)
+    ffm_step(t.state, torch.from_numpy(idx), None, torch.from_numpy(val), torch.from_numpy(y), h,
+             loss=loss)
+    np.testing.assert_allclose(loss.numpy(), ref_loss, rtol=2e-4, atol=2e-5)
+    for k in ("V", "G", "w", "wz", "wn", "bias"):
+        np.testing.assert_allclose(t.state[k].numpy(), ref[k], rtol=2e-4, atol=2e-5, err_msg=k)
+
+
+def test_ffm_fields_and_padding_cpu():
+    rows = [["0:1:1.0", "1:5:0.5", "2:7"], ["0:2", "2:3:2.0"], ["1:1"]]
+    t = FFMTrainer("-c -factors 3 -seed 1", device="cpu")
+    b = t.prepare(rows, [1, 0, 1])
+    assert b.idx.shape == (3, 3) and (b.idx[1:, 2] == -1).all() or b.idx[2, 1] == -1
+    t.fit(batch=b)
+    tab = t.model_table()
+    assert list(tab.columns) == ["model_id", "i", "Wi", "Vi"]
+    assert tab.iloc[0]["i"] == -1
+    assert set(tab["i"].tolist()[1:]) == {1, 2, 3, 5, 7}
+    assert len(tab.iloc[1]["Vi"]) == t.num_fields * 3
+
+
+def test_ffm_learns_criteo_like_cpu():
+    idx, y = criteo_like(20000, hash_bits=16, seed=5)
+    t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 16 -iters 1 -seed 1 -w0",
+                   device="cpu")
+    t.fit(batch=FFMBatch(idx, None, None, y))
+    eidx, ey, elog = criteo_like(5000, hash_bits=16, seed=77, return_logit=True)
+    p = t.predict_raw(batch=FFMBatch(eidx, None, None, None))
+    yy = (ey > 0).float()
+    ll = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+    base = torch.nn.functional.binary_cross_entropy(yy.mean().expand_as(yy), yy).item()
+    assert ll < base, (ll, base)
+    assert len(t.cv.history) >= 1
+
+
+def test_train_ffm_udtf_strings():
+    rows = [["0:a:1", "1:b:1"], ["0:c:1", "1:b:1"], ["0:a:1", "1:d:1"]] * 5
+    tab = train_ffm(rows, [1, 0, 1] * 5, "-c -feature_hashing 8 -num_fields 4 -iters 2", device="cpu")
+    assert len(tab) == 5  # bias row + 4 hashed features (a,b,c,d)
+
+
+@pytest.mark.gpu
+def test_ffm_gpu_matches_cpu_engine():
+    """HIP kernel vs the sequential C++ engine: identical on rows with disjoint features
+    (no Hogwild interaction), and statistically equal on a real stream."""
+    torch.manual_seed(0)
+    B, F, NFLD = 512, 39, 39
+    B_NF = B * F
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)  # all features distinct
+    y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0)
+    val = torch.rand(B, F) + 0.5
+    tc = _trainer("cpu", B_NF, NFLD)
+    tg = _trainer("cuda", B_NF, NFLD)
+    for k in tc.state:
+        tg.state[k].copy_(tc.state[k].cuda())
+    lc = torch.empty(B)
+    lg = torch.empty(B, device="cuda")
+    ffm_step(tc.state, idx, None, val, y, tc.hyper, loss=lc)
+    ffm_step(tg.state, idx.cuda(), None, val.cuda(), y.cuda(), tg.hyper, loss=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=1e-4, atol=1e-5)
+    for k in ("V", "G", "w", "wz", "wn"):
+        np.testing.assert_allclose(tg.state[k].cpu().numpy(), tc.state[k].numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_ffm_gpu_logloss_parity_with_sequential():
+    idx, y = criteo_like(60000, hash_bits=16, seed=5)
+    eidx, ey = criteo_like(20000, hash_bits=16, seed=99)
+    yy = (ey > 0).float()
+    res = {}
+    for dev in ("cpu", "cuda"):
+        t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 16 -iters 2 -seed 1",
+                       device=dev)
+        t.fit(batch=FFMBatch(idx, None, None, y).to(dev))
+        p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
+        res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+    assert abs(res["cpu"] - res["cuda"]) < 5e-3, res
