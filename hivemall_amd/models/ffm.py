@@ -112,6 +112,7 @@ class FFMTrainer(Learner):
         self.state: dict | None = None
         self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
         self.rows_seen = 0
+        self.grid = 0  # kernel grid override (0 = auto); bounds the Hogwild concurrency
 
     # ------------------------------------------------------------------ model state
     def init_state(self, num_features: int, num_fields: int) -> dict:
@@ -168,7 +169,8 @@ class FFMTrainer(Learner):
         for s in range(0, b.n, bs):
             sub = b.slice(s, min(b.n, s + bs))
             lb = None if loss_buf is None else loss_buf[s:s + sub.n]
-            ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True, loss=lb)
+            ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True, loss=lb,
+                     grid=self.grid)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:
