@@ -1,0 +1,366 @@
+// Online linear learner family on gfx950 ("mapper-in-a-wave").
+//
+// Hivemall's linear learners are strictly sequential per example (the PA / CW / AROW / SCW
+// updates depend on the current weights *and* covariance), and Hivemall scales them by
+// running one independent learner per mapper and averaging (GROUP BY feature avg(weight)
+// or argmin_kld) — SURVEY.md §2.4 DP-1/DP-2, §7.4 hard part 1.  This kernel moves that
+// design from nodes to waves:
+//
+//   * replica r = one 64-lane workgroup that runs Hivemall's exact per-row update over its
+//     shard of rows, in order, against its own private model replica (no atomics, no
+//     Hogwild, bitwise deterministic);
+//   * lanes span the non-zeros of a row: one 16-B float4 {w, s1, s2, s3} gather per feature,
+//     xᵀw / xᵀΣx / ‖x‖² reduced with DPP/shuffles, the row rule evaluated wave-uniformly,
+//     then one float4 store per feature;
+//   * small models (a9a: 124 features = 2 KB) are staged in LDS for the whole shard, so the
+//     per-row dependent-load latency is an LDS round trip instead of an L2/HBM one;
+//   * replicas are mixed (average over the replicas that touched the feature, or
+//     argmin-KLD for covariance learners) by ``hm_linear_mix`` and, across GPUs, by an RCCL
+//     all-reduce of the compact sums.
+//
+// Rules live in linear_rules.h (shared with the CPU engine csrc/host/linear_cpu.cpp).
+#include "common.h"
+#include "linear_rules.h"
+
+using namespace hm_lin;
+
+namespace {
+
+struct LinLaunch {
+    int R, dims, L;
+    int64_t n_rows;
+    int mini_batch;
+    int lds_model;       // model replica staged in LDS
+    int touched_cap;     // capacity of the per-replica touched list (mini-batch)
+};
+
+__device__ __forceinline__ F4 ld4(const float4* p) {
+    float4 v = *p;
+    return F4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void st4(float4* p, const F4& s) { *p = make_float4(s.w, s.s1, s.s2, s.s3); }
+
+template <bool LDS>
+__global__ __launch_bounds__(64) void linear_train_kernel(
+    Params P, LinLaunch G, const int64_t* __restrict__ indptr, const int32_t* __restrict__ idx,
+    const float* __restrict__ val, const float* __restrict__ y, const int32_t* __restrict__ order,
+    float4* __restrict__ S, uint8_t* __restrict__ touched, float* __restrict__ RS,
+    double* __restrict__ loss_out, float2* __restrict__ gacc, int32_t* __restrict__ tlist) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_model[];
+    const int r = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int dims = G.dims, L = G.L;
+    const size_t msize = (size_t)L * dims;
+    float4* M = S + (size_t)r * msize;
+    uint8_t* T = touched + (size_t)r * dims;
+    if (LDS) {
+        for (size_t i = lane; i < msize; i += 64) s_model[i] = M[i];
+        __syncthreads();
+        M = s_model;
+    }
+    float rs[HM_REP_SCALARS];
+#pragma unroll
+    for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = RS[r * HM_REP_SCALARS + k];
+    double loss_acc = 0.0;
+
+    const int64_t r0 = G.n_rows * r / G.R, r1 = G.n_rows * (r + 1) / G.R;
+    const bool mc = L > 1;
+    const bool cov = has_covar(P.algo);
+    const bool minib = G.mini_batch > 1 && P.algo == A_GENERAL && !mc;
+    float2* GA = minib ? gacc + (size_t)r * dims : nullptr;
+    int32_t* TL = minib ? tlist + (size_t)r * G.touched_cap : nullptr;
+    int n_touched = 0, in_batch = 0;
+
+    for (int64_t q = r0; q < r1; ++q) {
+        const int64_t row = order ? (int64_t)order[q] : q;
+        const int64_t s = indptr[row], e = indptr[row + 1];
+        const int nnz = (int)(e - s);
+        const float yy = y[row];
+        rs[RS_T] += 1.f;
+        const float t = rs[RS_T];
+        // ---- cached first chunk ----
+        int ci = -1;
+        float cx = 0.f;
+        if (lane < nnz) {
+            ci = idx[s + lane];
+            cx = val ? val[s + lane] : 1.f;
+            if (ci < 0 || ci >= dims) ci = -1;
+            if (ci >= 0) T[ci] = 1;
+        }
+        if (!mc) {
+            F4 cst = {0.f, 0.f, 0.f, 0.f};
+            float p = 0.f, var = 0.f, sq = 0.f;
+            if (ci >= 0) {
+                cst = ld4(M + ci);
+                p = cst.w * cx;
+                var = cst.s1 * cx * cx;
+                sq = cx * cx;
+            }
+            for (int64_t k = s + 64 + lane; k < e; k += 64) {
+                int i = idx[k];
+                const float x = val ? val[k] : 1.f;
+                if (i < 0 || i >= dims) continue;
+                T[i] = 1;
+                const F4 st = ld4(M + i);
+                p += st.w * x;
+                var += st.s1 * x * x;
+                sq += x * x;
+            }
+            p = hm::wave_sum(p);
+            if (cov) var = hm::wave_sum(var);
+            sq = hm::wave_sum(sq);
+            const RowCoef c = row_rule(P, p, yy, var, sq, rs);
+            loss_acc += c.loss;
+            if (minib) {
+                // accumulate dloss * x into the replica's dense gradient buffer
+                if (c.update) {
+                    for (int64_t base = s; base < e; base += 64) {  // wave-uniform trip count
+                        const int64_t k = base + lane;
+                        const int i = k < e ? idx[k] : -1;
+                        const float x = k < e ? (val ? val[k] : 1.f) : 0.f;
+                        bool first = false;
+                        if (i >= 0 && i < dims) {
+                            float2 a = GA[i];
+                            first = a.y == 0.f;
+                            a.x += c.dloss * x;
+                            a.y = 1.f;
+                            GA[i] = a;
+                        }
+                        const uint64_t m = __ballot(first);
+                        const int pos = n_touched + __popcll(m & ((1ull << lane) - 1ull));
+                        if (first && pos < G.touched_cap) TL[pos] = i;
+                        n_touched += __popcll(m);
+                    }
+                }
+                ++in_batch;
+                if (in_batch == G.mini_batch || q + 1 == r1 || n_touched + 64 * 4 > G.touched_cap) {
+                    const float inv = 1.f / (float)in_batch;
+                    const int nt = n_touched < G.touched_cap ? n_touched : G.touched_cap;
+                    for (int k = lane; k < nt; k += 64) {
+                        const int i = TL[k];
+                        F4 st = ld4(M + i);
+                        float2 a = GA[i];
+                        optimizer_update(P, st, a.x * inv, t, rs[RS_EVE_D]);
+                        st4(M + i, st);
+                        GA[i] = make_float2(0.f, 0.f);
+                    }
+                    n_touched = 0;
+                    in_batch = 0;
+                }
+                continue;
+            }
+            if (!c.update) continue;
+            if (ci >= 0) {
+                feature_update(P, c, cst, cx, t, rs[RS_EVE_D]);
+                st4(M + ci, cst);
+            }
+            for (int64_t k = s + 64 + lane; k < e; k += 64) {
+                const int i = idx[k];
+                const float x = val ? val[k] : 1.f;
+                if (i < 0 || i >= dims) continue;
+                F4 st = ld4(M + i);
+                feature_update(P, c, st, x, t, rs[RS_EVE_D]);
+                st4(M + i, st);
+            }
+        } else {
+            // ---- multiclass: scores of every label, actual vs best wrong ----
+            const int act = (int)yy;
+            float sa = 0.f, va = 0.f, sm = -INFINITY, vm = 0.f, sq = 0.f;
+            int miss = -1;
+            float sqp = 0.f;
+            for (int64_t k = s + lane; k < e; k += 64) {
+                const float x = val ? val[k] : 1.f;
+                const int i = idx[k];
+                if (i >= 0 && i < dims) sqp += x * x;
+            }
+            sq = hm::wave_sum(sqp);
+            for (int l = 0; l < L; ++l) {
+                float pl = 0.f, vl = 0.f;
+                for (int64_t k = s + lane; k < e; k += 64) {
+                    const int i = idx[k];
+                    const float x = val ? val[k] : 1.f;
+                    if (i < 0 || i >= dims) continue;
+                    const F4 st = ld4(M + (size_t)l * dims + i);
+                    pl += st.w * x;
+                    vl += st.s1 * x * x;
+                }
+                pl = hm::wave_sum(pl);
+                if (cov) vl = hm::wave_sum(vl);
+                if (l == act) { sa = pl; va = vl; }
+                else if (pl > sm) { sm = pl; vm = vl; miss = l; }
+            }
+            if (miss < 0 || act < 0 || act >= L) continue;
+            const MCCoef c = mc_rule(P, sa, sm, va, vm, sq);
+            loss_acc += c.loss;
+            if (!c.update) continue;
+            for (int64_t k = s + lane; k < e; k += 64) {
+                const int i = idx[k];
+                const float x = val ? val[k] : 1.f;
+                if (i < 0 || i >= dims) continue;
+                float4* pa = M + (size_t)act * dims + i;
+                float4* pm = M + (size_t)miss * dims + i;
+                F4 a = ld4(pa), m = ld4(pm);
+                mc_feature_update(P, c.a_act, c.b, a, x);
+                mc_feature_update(P, c.a_miss, c.b, m, x);
+                st4(pa, a);
+                st4(pm, m);
+            }
+        }
+    }
+    if (LDS) {
+        __syncthreads();
+        float4* Mg = S + (size_t)r * msize;
+        for (size_t i = lane; i < msize; i += 64) Mg[i] = s_model[i];
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < HM_REP_SCALARS; ++k) RS[r * HM_REP_SCALARS + k] = rs[k];
+        loss_out[r] = loss_acc;
+    }
+}
+
+// Replica reduction: per (label, feature) element, over the replicas whose touched byte
+// is set.  Outputs compact sums so several GPUs can add theirs with one all-reduce:
+//   num = Σ w_r            (plain)       or Σ w_r / σ_r   (argmin-KLD)
+//   den = Σ 1              (plain)       or Σ 1 / σ_r
+//   cnt = Σ 1 (touching replicas)
+__global__ __launch_bounds__(256) void linear_mix_reduce_kernel(
+    const float4* __restrict__ S, const uint8_t* __restrict__ touched, int R, int dims, int L,
+    int kld, float* __restrict__ num, float* __restrict__ den, float* __restrict__ cnt) {
+    const size_t n = (size_t)L * dims;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(e % dims);
+        float a = 0.f, b = 0.f, c = 0.f;
+        for (int r = 0; r < R; ++r) {
+            if (!touched[(size_t)r * dims + i]) continue;
+            const float4 v = S[(size_t)r * n + e];
+            if (kld) {
+                const float inv = 1.f / fmaxf(v.y, 1e-12f);
+                a += v.x * inv;
+                b += inv;
+            } else {
+                a += v.x;
+                b += 1.f;
+            }
+            c += 1.f;
+        }
+        num[e] = a;
+        den[e] = b;
+        cnt[e] = c;
+    }
+}
+
+// Write the mixed model back into every replica (optimizer state stays local, as upstream
+// mixes only weights and covariance).  Elements no replica touched are left unchanged.
+__global__ __launch_bounds__(256) void linear_mix_apply_kernel(
+    float4* __restrict__ S, int R, int dims, int L, int kld, const float* __restrict__ num,
+    const float* __restrict__ den, const float* __restrict__ cnt, float* __restrict__ w_out,
+    float* __restrict__ cov_out) {
+    const size_t n = (size_t)L * dims;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const float c = cnt[e];
+        if (c <= 0.f) {
+            if (w_out) w_out[e] = S[e].x;
+            if (cov_out) cov_out[e] = S[e].y;
+            continue;
+        }
+        const float w = num[e] / den[e];
+        const float cv = kld ? c / den[e] : 0.f;
+        for (int r = 0; r < R; ++r) {
+            float4* p = S + (size_t)r * n + e;
+            float4 v = *p;
+            v.x = w;
+            if (kld) v.y = cv;
+            *p = v;
+        }
+        if (w_out) w_out[e] = w;
+        if (cov_out) cov_out[e] = kld ? cv : S[e].y;
+    }
+}
+
+// Batched scoring: out[row * L + l] = Σ_k w[l][idx[k]] * val[k].  One lane per (row, label).
+__global__ __launch_bounds__(256) void linear_predict_kernel(
+    const float* __restrict__ w, int dims, int L, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ idx, const float* __restrict__ val, int64_t n_rows,
+    float* __restrict__ out, const float* __restrict__ cov, float* __restrict__ var_out) {
+    const int64_t total = n_rows * L;
+    for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = g / L;
+        const int l = (int)(g - row * L);
+        const float* wl = w + (size_t)l * dims;
+        float p = 0.f, v = 0.f;
+        for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
+            const int i = idx[k];
+            if (i < 0 || i >= dims) continue;
+            const float x = val ? val[k] : 1.f;
+            p += wl[i] * x;
+            if (cov) v += cov[(size_t)l * dims + i] * x * x;
+        }
+        out[g] = p;
+        if (var_out) var_out[g] = v;
+    }
+}
+
+}  // namespace
+
+// ip: R, dims, L, mini_batch, touched_cap, (n_rows as int64 separately)
+HM_API int hm_linear_train(const Params* P, const int32_t* ip, int64_t n_rows,
+                           const int64_t* indptr, const int32_t* idx, const float* val,
+                           const float* y, const int32_t* order, float* S, uint8_t* touched,
+                           float* RS, double* loss_out, float* gacc, int32_t* tlist,
+                           hipStream_t stream) {
+    LinLaunch G;
+    G.R = ip[0]; G.dims = ip[1]; G.L = ip[2]; G.mini_batch = ip[3]; G.touched_cap = ip[4];
+    G.n_rows = n_rows;
+    if (G.R <= 0 || G.dims <= 0 || G.L <= 0) return (int)hipErrorInvalidValue;
+    if (G.mini_batch > 1 && (gacc == nullptr || tlist == nullptr || G.touched_cap < 64 * 8))
+        return (int)hipErrorInvalidValue;
+    const size_t mbytes = (size_t)G.L * G.dims * sizeof(float4);
+    G.lds_model = mbytes <= 64 * 1024;
+    if (G.lds_model) {
+        hipLaunchKernelGGL((linear_train_kernel<true>), dim3(G.R), dim3(64), mbytes, stream, *P, G,
+                           indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched, RS,
+                           loss_out, reinterpret_cast<float2*>(gacc), tlist);
+    } else {
+        hipLaunchKernelGGL((linear_train_kernel<false>), dim3(G.R), dim3(64), 0, stream, *P, G,
+                           indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched, RS,
+                           loss_out, reinterpret_cast<float2*>(gacc), tlist);
+    }
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_linear_mix_reduce(const float* S, const uint8_t* touched, int R, int dims, int L,
+                                int kld, float* num, float* den, float* cnt, hipStream_t stream) {
+    const size_t n = (size_t)L * dims;
+    int blocks = (int)((n + 255) / 256);
+    blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
+    hipLaunchKernelGGL(linear_mix_reduce_kernel, dim3(blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const float4*>(S), touched, R, dims, L, kld, num, den, cnt);
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_linear_mix_apply(float* S, int R, int dims, int L, int kld, const float* num,
+                               const float* den, const float* cnt, float* w_out, float* cov_out,
+                               hipStream_t stream) {
+    const size_t n = (size_t)L * dims;
+    int blocks = (int)((n + 255) / 256);
+    blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
+    hipLaunchKernelGGL(linear_mix_apply_kernel, dim3(blocks), dim3(256), 0, stream,
+                       reinterpret_cast<float4*>(S), R, dims, L, kld, num, den, cnt, w_out, cov_out);
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_linear_predict(const float* w, int dims, int L, const int64_t* indptr,
+                             const int32_t* idx, const float* val, int64_t n_rows, float* out,
+                             const float* cov, float* var_out, hipStream_t stream) {
+    const int64_t total = n_rows * L;
+    if (total <= 0) return 0;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(linear_predict_kernel, dim3((int)blocks), dim3(256), 0, stream, w, dims, L,
+                       indptr, idx, val, n_rows, out, cov, var_out);
+    HM_LAUNCH_RET();
+}

@@ -66,7 +66,7 @@ def _run(cmd, verbose):
 def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs):
     OBJDIR.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    hdrs = []
+    hdrs = _headers(CSRC / "kernels")  # shared rule headers are used by host code too
     for s in srcs:
         hdrs.extend(_headers(s.parent))
     objs = []

@@ -87,11 +87,14 @@ def criteo_like_strings(n_rows: int, hash_bits: int = 20, seed: int = 7):
     return rows, ((y.numpy() > 0).astype(np.int32))
 
 
-def a9a_like(n_rows: int = 32561, n_features: int = 123, nnz: int = 14, seed: int = 3):
-    """libsvm a9a-shaped binary data: returns (rows as list of int arrays (1-based), labels 0/1)."""
+def a9a_like(n_rows: int = 32561, n_features: int = 123, nnz: int = 14, seed: int = 3,
+             model_seed: int = 123):
+    """libsvm a9a-shaped binary data: returns (rows as list of int arrays (1-based), labels 0/1).
+    The planted model depends only on ``model_seed``; ``seed`` selects the rows."""
+    mrng = np.random.default_rng(model_seed)
+    w = mrng.normal(0, 1.0, n_features + 1)
+    pop = mrng.dirichlet(np.ones(n_features) * 0.3)
     rng = np.random.default_rng(seed)
-    w = rng.normal(0, 1.0, n_features + 1)
-    pop = rng.dirichlet(np.ones(n_features) * 0.3)
     rows = []
     ys = np.empty(n_rows, dtype=np.int32)
     for r in range(n_rows):

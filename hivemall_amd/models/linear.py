@@ -1,0 +1,458 @@
+"""Online linear learners: binary classifiers, regressors, the general (loss x optimizer)
+learners and the multiclass family.
+
+Reference behaviour (upstream
+core/src/main/java/hivemall/{LearnerBaseUDTF,GeneralLearnerBaseUDTF}.java,
+hivemall/classifier/*.java, hivemall/classifier/multiclass/*.java, hivemall/regression/*.java,
+hivemall/optimizer/*.java).  Every SQL function is a subclass that only declares its option
+spec and algorithm id; the update rules are in ``csrc/kernels/linear_rules.h``.
+
+Execution model ("mapper-in-a-wave", see csrc/kernels/linear.hip): ``R`` replicas, each one
+a sequential Hivemall learner over its shard of the rows; after every epoch the replicas are
+mixed (average over the replicas that saw the feature, or argmin-KLD for the covariance
+learners) and, when running distributed, the compact sums are all-reduced over RCCL.  With
+``R = 1`` (the CPU default) this is exactly upstream's single-mapper semantics.
+
+Model tables (docs/compat.md):
+  binary / regression : (feature, weight)            [+ covar for CW/AROW/SCW families]
+  multiclass          : (label, feature, weight)     [+ covar]
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from statistics import NormalDist
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..ops import linear as LO
+from ..utils.features import CSR, FeatureEncoder
+from ..utils.options import UDFArgumentException, flag, opt
+from .base import ConversionState, Learner, log
+
+# ------------------------------------------------------------------ option specs
+LEARNER_BASE_OPTS = [
+    flag("dense", "densemodel", "Use a dense model (always dense on the device; accepted)"),
+    opt("dims", "feature_dimensions", -1, int, "Dimension of the model (default: max index + 1)"),
+    flag("disable_halffloat", None, "Accepted for compatibility (models are fp32)"),
+    opt("mini_batch", "mini_batch_size", 1, int, "Mini-batch size (general learners)"),
+    opt("mix", "mix_servers", None, str, "Mixing: on this engine replicas/ranks are mixed over RCCL"),
+    opt("mix_session", "mix_session_name", None, str, "Accepted for compatibility"),
+    opt("mix_threshold", None, 3, int, "Accepted for compatibility"),
+    flag("mix_cancel", "enable_mix_canceling", "Accepted for compatibility"),
+    flag("ssl", None, "Accepted for compatibility"),
+    opt("loadmodel", None, None, str, "Warm start: path of a model table (TSV/CSV/parquet)"),
+    opt("iters", "iterations", 1, int, "The maximum number of iterations (epochs)", aliases=("iter",)),
+    opt("cv_rate", "convergence_rate", 0.005, float, "Threshold to determine convergence"),
+    flag("disable_cv", "disable_cvtest", "Whether to disable convergence check"),
+    opt("seed", None, -1, int, "Seed value"),
+    opt("replicas", None, 0, int, "[engine] model replicas (0 = auto; CPU default 1)"),
+]
+
+GENERAL_OPTS = [
+    opt("loss", "loss_function", None, str, "Loss function"),
+    opt("opt", "optimizer", "adagrad", str, "Optimizer"),
+    opt("reg", "regularization", "rda", str, "Regularization: no, l1, l2, elasticnet, rda"),
+    opt("eta", None, "inverse", str, "Learning rate scheme: fixed, simple, inverse/inv"),
+    opt("eta0", None, 0.1, float, "Initial learning rate"),
+    opt("t", "total_steps", -1.0, float, "Total of n_samples * epochs (for -eta simple)"),
+    opt("power_t", None, 0.1, float, "Exponent for inverse scaling learning rate"),
+    opt("lambda", None, 1e-4, float, "Regularization term"),
+    opt("l1_ratio", None, 0.5, float, "Elastic-net mixing"),
+    opt("alpha", None, 1.0, float, "Coefficient of learning rate (momentum/Adam family)"),
+    opt("beta1", "momentum", 0.9, float, "Adam beta1 / momentum"),
+    opt("beta2", None, 0.999, float, "Adam beta2"),
+    opt("eps", None, 1e-6, float, "Denominator constant"),
+    opt("decay", None, 0.95, float, "RMSprop decay"),
+    opt("rho", None, 0.95, float, "AdaDelta decay"),
+    opt("beta", None, 1e-6, float, "AdamHD hyper-gradient step"),
+    opt("scale", None, 100.0, float, "Scaling factor (accepted; fp32 accumulators)"),
+    flag("amsgrad", None, "AMSGrad variant of Adam"),
+    flag("inspect_opts", None, "Show the resolved options and raise"),
+    opt("quantile_tau", "tau", 0.5, float, "Quantile loss tau"),
+    opt("huber_c", None, 1.0, float, "Huber loss threshold"),
+    opt("epsilon", None, 0.1, float, "Epsilon of the epsilon-insensitive losses"),
+]
+
+
+@dataclass
+class SparseRows:
+    """Device-resident CSR rows (+ labels)."""
+    indptr: torch.Tensor      # int64 [n+1]
+    idx: torch.Tensor         # int32 [nnz]
+    val: torch.Tensor | None  # f32 [nnz] (None = all ones)
+    y: torch.Tensor | None    # f32 [n]
+
+    @property
+    def n(self) -> int:
+        return self.indptr.numel() - 1
+
+    def to(self, device) -> "SparseRows":
+        f = lambda t: None if t is None else t.to(device).contiguous()
+        return SparseRows(f(self.indptr), f(self.idx), f(self.val), f(self.y))
+
+    @staticmethod
+    def from_csr(csr: CSR, y=None, device="cpu") -> "SparseRows":
+        val = None if csr.nnz and np.all(csr.val == 1.0) else torch.from_numpy(csr.val.astype(np.float32))
+        idx = np.where((csr.idx >= 0) & (csr.idx < 2 ** 31 - 1), csr.idx, -1).astype(np.int32)
+        yy = None if y is None else torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32))
+        return SparseRows(torch.from_numpy(csr.indptr.astype(np.int64)), torch.from_numpy(idx),
+                          val, yy).to(device)
+
+
+def encode_rows(rows, encoder: FeatureEncoder | None, train: bool) -> tuple[CSR, FeatureEncoder]:
+    """Hivemall feature rows -> CSR.  Integer names are used as indices; otherwise names are
+    dictionary-encoded (collision free, decoded again for the model table)."""
+    if isinstance(rows, CSR):
+        return rows, encoder or FeatureEncoder("int")
+    if encoder is None:
+        enc = FeatureEncoder("int")
+        try:
+            return enc.encode(rows), enc
+        except UDFArgumentException:
+            enc = FeatureEncoder("dict")
+            return enc.encode(rows, add_new=True), enc
+    return encoder.encode(rows, add_new=train and encoder.mode == "dict"), encoder
+
+
+class OnlineLinearLearner(Learner):
+    NAME = "train_linear"
+    ALGO = "general"
+    TASK = "binary"           # binary | regression | multiclass
+    OPTIONS = LEARNER_BASE_OPTS
+    DEFAULT_LOSS = "hinge"
+
+    def __init__(self, options: str | None = None, device=None, **kw):
+        super().__init__(options, device, **kw)
+        self.covar = self.ALGO in LO.COVAR_ALGOS
+        self.P = self.make_params()
+        self.encoder: FeatureEncoder | None = None
+        self.state: LO.LinearState | None = None
+        self.labels: list | None = None
+        self.cv = ConversionState(not self.cl["disable_cv"], self.cl["cv_rate"])
+        self._w = self._cov = None
+        self.rows_seen = 0
+        self._warm = None
+        if self.cl["loadmodel"]:
+            from ..io.model_table import read_table
+            self._warm = read_table(self.cl["loadmodel"])
+        if self.cl.has("inspect_opts") and self.cl["inspect_opts"]:
+            raise UDFArgumentException(f"{self.NAME} options: {self.cl.as_dict()}")
+
+    # ------------------------------------------------------------------ params
+    def _opt(self, name, default=None):
+        try:
+            return self.cl[name]
+        except KeyError:
+            return default
+
+    def make_params(self) -> LO.LinParams:
+        P = LO.LinParams()
+        P.algo = LO.ALGOS[self.ALGO]
+        P.n_labels = 1
+        P.eta0 = self._opt("eta0", 0.1) if self._opt("eta0") is not None else 0.1
+        P.power_t = self._opt("power_t", 0.1) or 0.1
+        P.total_steps = self._opt("t", -1.0) or -1.0
+        P.lambda_ = self._opt("lambda", 1e-4) if self._opt("lambda") is not None else 1e-4
+        P.l1_ratio = self._opt("l1_ratio", 0.5) or 0.5
+        P.c = self._opt("c", 1.0) if self._opt("c") is not None else 1.0
+        P.r = self._opt("r", 0.1) if self._opt("r") is not None else 0.1
+        phi = self._opt("phi", None)
+        eta_conf = self._opt("eta", None) if self.ALGO in ("cw", "scw", "scw2") else None
+        if phi is None and eta_conf is not None:
+            phi = NormalDist().inv_cdf(float(eta_conf))
+        P.phi = 1.0 if phi is None else float(phi)
+        P.epsilon = self._opt("epsilon", 0.1) if self._opt("epsilon") is not None else 0.1
+        P.alpha = self._opt("alpha", 1.0) if self._opt("alpha") is not None else 1.0
+        P.beta1 = self._opt("beta1", 0.9) or 0.9
+        P.beta2 = self._opt("beta2", 0.999) or 0.999
+        P.eps = self._opt("eps", 1e-6) if self._opt("eps") is not None else 1e-6
+        P.rho = self._opt("rho", 0.95) or 0.95
+        P.decay = self._opt("decay", 0.95) or 0.95
+        P.beta_hd = self._opt("beta", 1e-6) or 1e-6
+        P.scale = self._opt("scale", 100.0) or 100.0
+        P.quantile_tau = self._opt("quantile_tau", 0.5) or 0.5
+        P.huber_c = self._opt("huber_c", 1.0) or 1.0
+        P.init_covar = 1.0
+        P.eta = LO.ETAS["inverse"]
+        if self.ALGO == "general":
+            loss = (self._opt("loss") or self.DEFAULT_LOSS).lower().replace("-", "_")
+            if loss not in LO.LOSSES:
+                raise UDFArgumentException(f"{self.NAME}: unsupported loss function: {loss}")
+            P.loss = LO.LOSSES[loss]
+            is_cls = P.loss in LO.CLASSIFICATION_LOSSES
+            if (self.TASK == "binary") != is_cls:
+                raise UDFArgumentException(
+                    f"{self.NAME}: loss '{loss}' is not a "
+                    f"{'classification' if self.TASK == 'binary' else 'regression'} loss")
+            o = self._opt("opt").lower()
+            if o not in LO.OPTIMIZERS:
+                raise UDFArgumentException(f"{self.NAME}: unsupported optimizer: {o}")
+            P.opt = LO.OPTIMIZERS[o]
+            r = self._opt("reg").lower()
+            if r not in LO.REGS:
+                raise UDFArgumentException(f"{self.NAME}: unsupported regularization: {r}")
+            P.reg = LO.REGS[r]
+            e = self._opt("eta").lower()
+            if e not in LO.ETAS:
+                raise UDFArgumentException(f"{self.NAME}: unsupported eta scheme: {e}")
+            P.eta = LO.ETAS[e]
+            P.amsgrad = int(bool(self._opt("amsgrad")))
+        elif self.ALGO == "logress":
+            P.eta = LO.ETAS["inverse"] if self._opt("eta") is None else LO.ETAS["fixed"]
+            if self._opt("eta") is not None:
+                P.eta0 = float(self._opt("eta"))
+        elif self.ALGO in ("adagrad_rda", "adagrad_regr"):
+            if self._opt("eta") is not None:
+                P.eta0 = float(self._opt("eta"))
+            if self.ALGO == "adagrad_regr" and self._opt("eps") is None:
+                P.eps = 1.0
+        return P
+
+    # ------------------------------------------------------------------ data
+    def _labels_to_float(self, labels) -> np.ndarray:
+        a = np.asarray(labels)
+        if self.TASK == "binary":
+            return np.where(a.astype(np.float64) > 0, 1.0, -1.0).astype(np.float32)
+        if self.TASK == "multiclass":
+            if self.labels is None:
+                uniq = sorted(set(a.tolist()), key=lambda v: (isinstance(v, str), v))
+                self.labels = uniq
+            lut = {v: i for i, v in enumerate(self.labels)}
+            out = np.array([lut.get(v, -1) for v in a.tolist()], dtype=np.float32)
+            return out
+        return a.astype(np.float32)
+
+    def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
+        if self.encoder is None and self._warm is not None and not isinstance(features, CSR):
+            feats = self._warm["feature"].tolist()
+            if any(isinstance(f, str) and not f.lstrip("-").isdigit() for f in feats):
+                self.encoder = FeatureEncoder("dict")
+                self.encoder.encode([[str(f) for f in feats]], add_new=True)
+        csr, self.encoder = encode_rows(features, self.encoder, train)
+        y = None if labels is None else self._labels_to_float(labels)
+        return SparseRows.from_csr(csr, y, self.device)
+
+    # ------------------------------------------------------------------ state
+    def _auto_replicas(self, n_rows: int) -> int:
+        r = int(self.cl["replicas"])
+        if r > 0:
+            return r
+        if self.device.type != "cuda":
+            return 1
+        return int(max(1, min(1024, n_rows // 4096)))
+
+    def _ensure_state(self, rows: SparseRows) -> None:
+        if self.state is not None:
+            return
+        dims = int(self.cl["dims"])
+        if dims <= 0:
+            dims = int(rows.idx.max().item()) + 1 if rows.idx.numel() else 1
+            if self.encoder is not None and self.encoder.mode == "dict":
+                dims = max(dims, self.encoder.vocab_size())
+            elif self._warm is not None:
+                dims = max(dims, int(np.max(np.asarray(self._warm["feature"], dtype=np.int64))) + 1)
+        L = len(self.labels) if self.TASK == "multiclass" else 1
+        if self.TASK == "multiclass" and L < 2:
+            raise UDFArgumentException(f"{self.NAME}: needs at least two distinct labels")
+        self.P.n_labels = L
+        R = self._auto_replicas(rows.n)
+        mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
+        bytes_ = R * L * dims * 16
+        if bytes_ > (32 << 30):
+            R = max(1, (32 << 30) // (L * dims * 16))
+        self.state = LO.new_state(R, L, dims, self.device, self.covar, self.P.init_covar, mb)
+        if self._warm is not None:
+            self.load_model_table(self._warm)
+
+    # ------------------------------------------------------------------ training
+    def fit(self, features=None, labels=None, rows: SparseRows | None = None) -> "OnlineLinearLearner":
+        rows = rows if rows is not None else self.prepare(features, labels, train=True)
+        if rows.y is None:
+            raise UDFArgumentException(f"{self.NAME}: labels are required")
+        self._ensure_state(rows)
+        if rows.idx.numel() and int(rows.idx.max().item()) >= self.state.dims:
+            log.warning("%s: feature index >= dims (%d) ignored", self.NAME, self.state.dims)
+        mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
+        iters = int(self.cl["iters"])
+        for ep in range(iters):
+            loss = LO.train_pass(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
+                                 None, mb)
+            self.rows_seen += rows.n
+            self.mix()
+            self.cv.incr_loss(float(loss.sum().item()))
+            if self.cv.is_converged():
+                log.info("%s converged at epoch %d", self.NAME, ep + 1)
+                break
+        return self
+
+    def mix(self) -> None:
+        """Mix replicas (and ranks): average, or argmin-KLD for covariance learners."""
+        st = self.state
+        kld = self.covar
+        num, den, cnt = LO.mix_reduce(st, kld)
+        if self.mixer is not None and self.mixer.world > 1:
+            self.mixer.all_reduce_sum([num, den, cnt])
+        self._w, self._cov = LO.mix_apply(st, kld, num, den, cnt)
+
+    # ------------------------------------------------------------------ model
+    def weights(self) -> tuple[torch.Tensor, torch.Tensor | None]:
+        if self._w is None:
+            self.mix()
+        return self._w, self._cov
+
+    def touched_features(self) -> np.ndarray:
+        t = self.state.touched.amax(0) if self.state.R > 1 else self.state.touched[0]
+        return torch.nonzero(t).flatten().cpu().numpy()
+
+    def _feature_names(self, ids: np.ndarray) -> list:
+        if self.encoder is not None and self.encoder.mode == "dict":
+            return self.encoder.decode(ids)
+        return [int(i) for i in ids]
+
+    def model_table(self) -> pd.DataFrame:
+        w, cov = self.weights()
+        ids = self.touched_features()
+        W = w[:, ids].cpu().numpy()
+        names = self._feature_names(ids)
+        C = cov[:, ids].cpu().numpy() if (cov is not None and self.covar) else None
+        if self.TASK == "multiclass":
+            L = len(self.labels)
+            d = {"label": np.repeat(np.array(self.labels, dtype=object), len(ids)),
+                 "feature": names * L, "weight": W.reshape(-1)}
+            if C is not None:
+                d["covar"] = C.reshape(-1)
+            return pd.DataFrame(d)
+        d = {"feature": names, "weight": W[0]}
+        if C is not None:
+            d["covar"] = C[0]
+        return pd.DataFrame(d)
+
+    def load_model_table(self, df: pd.DataFrame) -> None:
+        """Warm start (``-loadmodel``): seed every replica with (feature, weight[, covar])."""
+        st = self.state
+        feats = df["feature"].tolist()
+        if self.encoder is not None and self.encoder.mode == "dict":
+            csr = self.encoder.encode([[str(f)] for f in feats], add_new=False)
+            ids = csr.idx
+        else:
+            ids = np.asarray([int(f) for f in feats], dtype=np.int64)
+        ok = (ids >= 0) & (ids < st.dims)
+        ids_t = torch.from_numpy(ids[ok]).to(st.device)
+        lab = torch.zeros_like(ids_t)
+        if self.TASK == "multiclass" and "label" in df.columns:
+            lut = {v: i for i, v in enumerate(self.labels or [])}
+            lab = torch.tensor([lut.get(v, 0) for v in np.asarray(df["label"])[ok]], device=st.device)
+        wv = torch.tensor(np.asarray(df["weight"], dtype=np.float32)[ok], device=st.device)
+        st.S[:, lab, ids_t, 0] = wv
+        if self.covar and "covar" in df.columns:
+            st.S[:, lab, ids_t, 1] = torch.tensor(np.asarray(df["covar"], dtype=np.float32)[ok],
+                                                  device=st.device)
+        st.touched[:, ids_t] = 1
+
+    # ------------------------------------------------------------------ inference
+    def decision_function(self, features=None, rows: SparseRows | None = None) -> torch.Tensor:
+        rows = rows if rows is not None else self.prepare(features, None, train=False)
+        w, _ = self.weights()
+        out, _ = LO.predict_scores(w, rows.indptr, rows.idx, rows.val)
+        return out if self.TASK == "multiclass" else out[:, 0]
+
+    def predict(self, features=None, rows: SparseRows | None = None) -> np.ndarray:
+        s = self.decision_function(features, rows)
+        if self.TASK == "multiclass":
+            best = s.argmax(1).cpu().numpy()
+            return np.array([self.labels[i] for i in best], dtype=object)
+        if self.ALGO in ("logress", "adagrad_regr", "adadelta_regr") or (
+                self.ALGO == "general" and self.P.loss == LO.LOSSES["log"]):
+            return torch.sigmoid(s).cpu().numpy()
+        return s.cpu().numpy()
+
+
+# ---------------------------------------------------------------- concrete SQL functions
+def _learner(name, algo, task, extra_opts=(), doc="", default_iters=1, default_loss="hinge"):
+    opts = [o for o in LEARNER_BASE_OPTS if not (o.name == "iters" and default_iters != 1)]
+    if default_iters != 1:
+        opts.append(opt("iters", "iterations", default_iters, int,
+                        "The maximum number of iterations (epochs)", aliases=("iter",)))
+    names = {o.name for o in opts}
+    for o in extra_opts:
+        if o.name not in names:
+            opts.append(o)
+            names.add(o.name)
+    cls = type(name.title().replace("_", ""), (OnlineLinearLearner,),
+               {"NAME": name, "ALGO": algo, "TASK": task, "OPTIONS": opts, "__doc__": doc,
+                "DEFAULT_LOSS": default_loss})
+    return cls
+
+
+_C = opt("c", "aggressiveness", 1.0, float, "Aggressiveness parameter C")
+_R = opt("r", "regularization", 0.1, float, "Regularization parameter r")
+_PHI = opt("phi", "confidence", None, float, "Confidence parameter phi")
+_ETA_CONF = opt("eta", "hyper_c", None, float, "Confidence level eta (phi = probit(eta))")
+_EPS_INS = opt("epsilon", None, 0.1, float, "Sensitivity to prediction mistakes")
+
+TrainPerceptron = _learner("train_perceptron", "perceptron", "binary", doc="Rosenblatt perceptron")
+TrainPA = _learner("train_pa", "pa", "binary", doc="Passive-Aggressive (Crammer et al. 2006)")
+TrainPA1 = _learner("train_pa1", "pa1", "binary", [_C], doc="PA-I")
+TrainPA2 = _learner("train_pa2", "pa2", "binary", [_C], doc="PA-II")
+TrainCW = _learner("train_cw", "cw", "binary", [_PHI, _ETA_CONF], doc="Confidence-weighted (Dredze 2008)")
+TrainAROW = _learner("train_arow", "arow", "binary", [_R], doc="AROW (Crammer 2009)")
+TrainAROWh = _learner("train_arowh", "arowh", "binary", [_R, _C], doc="AROW with hinge threshold C")
+TrainSCW = _learner("train_scw", "scw", "binary", [_PHI, _ETA_CONF, _C], doc="SCW-I (Wang 2012)")
+TrainSCW2 = _learner("train_scw2", "scw2", "binary", [_PHI, _ETA_CONF, _C], doc="SCW-II")
+TrainAdaGradRDA = _learner("train_adagrad_rda", "adagrad_rda", "binary", [
+    opt("eta", "eta0", 0.1, float, "Learning rate"),
+    opt("lambda", None, 1e-6, float, "Regularization (RDA L1)"),
+    opt("scale", None, 100.0, float, "Scaling factor (accepted)")], doc="AdaGrad-RDA hinge")
+TrainClassifier = _learner("train_classifier", "general", "binary", GENERAL_OPTS, default_iters=10,
+                           default_loss="hinge", doc="GeneralClassifierUDTF")
+
+_LOGRESS_OPTS = [opt("eta0", None, 0.1, float, "Initial learning rate"),
+                 opt("t", "total_steps", -1.0, float, "Total steps"),
+                 opt("power_t", None, 0.1, float, "Inverse scaling exponent"),
+                 opt("eta", None, None, float, "Fixed learning rate")]
+Logress = _learner("logress", "logress", "regression", _LOGRESS_OPTS, doc="SGD logistic regression")
+TrainLogregr = _learner("train_logregr", "logress", "regression", _LOGRESS_OPTS)
+TrainLogisticRegr = _learner("train_logistic_regr", "logress", "regression", _LOGRESS_OPTS)
+TrainPA1Regr = _learner("train_pa1_regr", "pa1_regr", "regression", [_C, _EPS_INS])
+TrainPA1aRegr = _learner("train_pa1a_regr", "pa1a_regr", "regression", [_C, _EPS_INS])
+TrainPA2Regr = _learner("train_pa2_regr", "pa2_regr", "regression", [_C, _EPS_INS])
+TrainPA2aRegr = _learner("train_pa2a_regr", "pa2a_regr", "regression", [_C, _EPS_INS])
+TrainAROWRegr = _learner("train_arow_regr", "arow_regr", "regression", [_R])
+TrainAROWeRegr = _learner("train_arowe_regr", "arowe_regr", "regression", [_R, _EPS_INS])
+TrainAROWe2Regr = _learner("train_arowe2_regr", "arowe2_regr", "regression", [_R, _EPS_INS])
+TrainAdaGradRegr = _learner("train_adagrad_regr", "adagrad_regr", "regression", [
+    opt("eta", "eta0", 1.0, float, "Learning rate"), opt("eps", None, 1.0, float, "Denominator"),
+    opt("scale", None, 100.0, float, "Scaling factor (accepted)")])
+TrainAdaDeltaRegr = _learner("train_adadelta_regr", "adadelta_regr", "regression", [
+    opt("rho", "decay", 0.95, float, "Decay"), opt("eps", None, 1e-6, float, "Denominator"),
+    opt("scale", None, 100.0, float, "Scaling factor (accepted)")])
+TrainRegressor = _learner("train_regressor", "general", "regression", GENERAL_OPTS, default_iters=10,
+                          default_loss="squared", doc="GeneralRegressorUDTF")
+
+TrainMulticlassPerceptron = _learner("train_multiclass_perceptron", "perceptron", "multiclass")
+TrainMulticlassPA = _learner("train_multiclass_pa", "pa", "multiclass")
+TrainMulticlassPA1 = _learner("train_multiclass_pa1", "pa1", "multiclass", [_C])
+TrainMulticlassPA2 = _learner("train_multiclass_pa2", "pa2", "multiclass", [_C])
+TrainMulticlassCW = _learner("train_multiclass_cw", "cw", "multiclass", [_PHI, _ETA_CONF])
+TrainMulticlassAROW = _learner("train_multiclass_arow", "arow", "multiclass", [_R])
+TrainMulticlassAROWh = _learner("train_multiclass_arowh", "arowh", "multiclass", [_R, _C])
+TrainMulticlassSCW = _learner("train_multiclass_scw", "scw", "multiclass", [_PHI, _ETA_CONF, _C])
+TrainMulticlassSCW2 = _learner("train_multiclass_scw2", "scw2", "multiclass", [_PHI, _ETA_CONF, _C])
+
+LEARNERS = {c.NAME: c for c in [
+    TrainPerceptron, TrainPA, TrainPA1, TrainPA2, TrainCW, TrainAROW, TrainAROWh, TrainSCW,
+    TrainSCW2, TrainAdaGradRDA, TrainClassifier, Logress, TrainLogregr, TrainLogisticRegr,
+    TrainPA1Regr, TrainPA1aRegr, TrainPA2Regr, TrainPA2aRegr, TrainAROWRegr, TrainAROWeRegr,
+    TrainAROWe2Regr, TrainAdaGradRegr, TrainAdaDeltaRegr, TrainRegressor,
+    TrainMulticlassPerceptron, TrainMulticlassPA, TrainMulticlassPA1, TrainMulticlassPA2,
+    TrainMulticlassCW, TrainMulticlassAROW, TrainMulticlassAROWh, TrainMulticlassSCW,
+    TrainMulticlassSCW2]}
+
+
+def train(name: str, features, labels, options: str | None = None, device=None, **kw) -> pd.DataFrame:
+    """Functional UDTF form of any linear learner: returns its model table."""
+    cls = LEARNERS[name]
+    return cls(options, device, **kw).fit(features, labels).model_table()

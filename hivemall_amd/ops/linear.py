@@ -1,0 +1,221 @@
+"""Online linear family ops: gfx950 kernel (``csrc/kernels/linear.hip``) on ``cuda`` tensors,
+OpenMP C++ engine (``csrc/host/linear_cpu.cpp``) on CPU tensors.  Both execute the rules of
+``csrc/kernels/linear_rules.h``.
+
+State layout (``LinearState``):
+  S        f32 [R, L, dims, 4]   per (replica, label, feature): {w, s1, s2, s3}
+  touched  u8  [R, dims]         feature seen by the replica (mix + model-table export)
+  RS       f32 [R, 8]            per-replica scalars (step t, online variance, Eve, ...)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import _native
+
+ALGOS = {
+    "perceptron": 0, "pa": 1, "pa1": 2, "pa2": 3, "cw": 4, "arow": 5, "arowh": 6, "scw": 7,
+    "scw2": 8, "adagrad_rda": 9, "logress": 10, "pa1_regr": 11, "pa2_regr": 12, "pa1a_regr": 13,
+    "pa2a_regr": 14, "arow_regr": 15, "arowe_regr": 16, "arowe2_regr": 17, "adagrad_regr": 18,
+    "adadelta_regr": 19, "general": 20,
+}
+COVAR_ALGOS = {"cw", "arow", "arowh", "scw", "scw2", "arow_regr", "arowe_regr", "arowe2_regr"}
+
+LOSSES = {
+    "hinge": 0, "hingeloss": 0,
+    "log": 1, "logloss": 1, "logistic": 1, "logisticloss": 1,
+    "squaredhinge": 2, "squared_hinge": 2, "squaredhingeloss": 2,
+    "modifiedhuber": 3, "modified_huber": 3, "modifiedhuberloss": 3,
+    "squared": 4, "squaredloss": 4, "squared_loss": 4,
+    "quantile": 5, "quantileloss": 5,
+    "epsilon_insensitive": 6, "epsiloninsensitive": 6, "epsiloninsensitiveloss": 6,
+    "squared_epsilon_insensitive": 7, "squaredepsiloninsensitive": 7,
+    "squaredepsiloninsensitiveloss": 7,
+    "huber": 8, "huberloss": 8,
+}
+CLASSIFICATION_LOSSES = {0, 1, 2, 3}
+OPTIMIZERS = {
+    "sgd": 0, "momentum": 1, "nesterov": 2, "adagrad": 3, "rmsprop": 4, "rmspropgraves": 5,
+    "rmsprop_graves": 5, "adadelta": 6, "adam": 7, "nadam": 8, "eve": 9, "adam_hd": 10,
+    "adamhd": 10,
+}
+REGS = {"no": 0, "none": 0, "l1": 1, "l2": 2, "elasticnet": 3, "elastic_net": 3, "rda": 4}
+ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
+
+
+class LinParams(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("algo", "loss", "opt", "reg", "eta", "amsgrad", "n_labels")] + [
+        (n, C.c_float) for n in ("eta0", "power_t", "total_steps", "lambda_", "l1_ratio", "c", "r",
+                                 "phi", "epsilon", "alpha", "beta1", "beta2", "eps", "rho", "decay",
+                                 "beta_hd", "scale", "quantile_tau", "huber_c", "init_covar")]
+
+
+@dataclass
+class LinearState:
+    S: torch.Tensor
+    touched: torch.Tensor
+    RS: torch.Tensor
+    covar: bool
+    gacc: torch.Tensor | None = None
+    tlist: torch.Tensor | None = None
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def R(self) -> int:
+        return self.S.shape[0]
+
+    @property
+    def L(self) -> int:
+        return self.S.shape[1]
+
+    @property
+    def dims(self) -> int:
+        return self.S.shape[2]
+
+    @property
+    def device(self):
+        return self.S.device
+
+
+def new_state(R: int, L: int, dims: int, device, covar: bool, init_covar: float = 1.0,
+              mini_batch: int = 1) -> LinearState:
+    S = torch.zeros((R, L, dims, 4), dtype=torch.float32, device=device)
+    if covar:
+        S[..., 1] = init_covar
+    st = LinearState(S, torch.zeros((R, dims), dtype=torch.uint8, device=device),
+                     torch.zeros((R, 8), dtype=torch.float32, device=device), covar)
+    if mini_batch > 1 and S.is_cuda:
+        st.gacc = torch.zeros((R, dims, 2), dtype=torch.float32, device=device)
+        cap = max(64 * 8, min(dims, 1 << 22))
+        st.tlist = torch.zeros((R, cap), dtype=torch.int32, device=device)
+        st.meta["touched_cap"] = cap
+    return st
+
+
+def _ip(st: LinearState, mini_batch: int) -> np.ndarray:
+    return np.array([st.R, st.dims, st.L, mini_batch, st.meta.get("touched_cap", 0)], dtype=np.int32)
+
+
+def train_pass(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.Tensor,
+               val: torch.Tensor | None, y: torch.Tensor, order: torch.Tensor | None = None,
+               mini_batch: int = 1) -> torch.Tensor:
+    """One pass over the rows (each replica over its shard).  Returns per-replica loss sums."""
+    n = indptr.numel() - 1
+    dev = st.device
+    for t in (indptr, idx, val, y, order):
+        if t is not None:
+            assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    assert indptr.dtype == torch.int64 and idx.dtype == torch.int32 and y.dtype == torch.float32
+    assert y.numel() >= n
+    if val is not None:
+        assert val.dtype == torch.float32 and val.numel() == idx.numel()
+    if order is not None:
+        assert order.dtype == torch.int32 and order.numel() == n
+    loss = torch.zeros(st.R, dtype=torch.float64, device=dev)
+    ip = _ip(st, mini_batch)
+    p = _native.ptr
+    args = [C.addressof(P), ip.ctypes.data, C.c_int64(n), p(indptr), p(idx), p(val), p(y), p(order),
+            p(st.S), p(st.touched), p(st.RS), p(loss)]
+    if dev.type == "cuda":
+        if mini_batch > 1 and st.gacc is None:
+            st.gacc = torch.zeros((st.R, st.dims, 2), dtype=torch.float32, device=dev)
+            cap = max(64 * 8, min(st.dims, 1 << 22))
+            st.tlist = torch.zeros((st.R, cap), dtype=torch.int32, device=dev)
+            st.meta["touched_cap"] = cap
+            ip = _ip(st, mini_batch)
+            args[1] = ip.ctypes.data
+        rc = _native.hip().hm_linear_train(*args, p(st.gacc), p(st.tlist), _native.stream_of(dev))
+        _native.check(rc, "hm_linear_train")
+    else:
+        rc = _native.host().hm_linear_train_cpu(*args)
+        if rc != 0:
+            raise RuntimeError(f"hm_linear_train_cpu failed: {rc}")
+    return loss
+
+
+def mix_reduce(st: LinearState, kld: bool):
+    """Compact per-element sums (num, den, cnt) over the touching replicas."""
+    R, L, dims = st.R, st.L, st.dims
+    dev = st.device
+    if dev.type == "cuda":
+        num = torch.empty(L * dims, dtype=torch.float32, device=dev)
+        den = torch.empty_like(num)
+        cnt = torch.empty_like(num)
+        rc = _native.hip().hm_linear_mix_reduce(_native.ptr(st.S), _native.ptr(st.touched), R, dims,
+                                                L, int(kld), _native.ptr(num), _native.ptr(den),
+                                                _native.ptr(cnt), _native.stream_of(dev))
+        _native.check(rc, "hm_linear_mix_reduce")
+        return num, den, cnt
+    t = st.touched.to(torch.float32).view(R, 1, dims)          # [R,1,dims]
+    w = st.S[..., 0]
+    if kld:
+        inv = 1.0 / st.S[..., 1].clamp_min(1e-12)
+        num = (w * inv * t).sum(0)
+        den = (inv * t).sum(0)
+    else:
+        num = (w * t).sum(0)
+        den = t.expand(R, L, dims).sum(0)
+    cnt = t.expand(R, L, dims).sum(0)
+    return num.reshape(-1).contiguous(), den.reshape(-1).contiguous(), cnt.reshape(-1).contiguous()
+
+
+def mix_apply(st: LinearState, kld: bool, num, den, cnt):
+    """Write the mixed weights (and covariance) into every replica; return compact (w, cov)."""
+    R, L, dims = st.R, st.L, st.dims
+    dev = st.device
+    w_out = torch.empty(L * dims, dtype=torch.float32, device=dev)
+    cov_out = torch.empty_like(w_out) if st.covar else None
+    if dev.type == "cuda":
+        rc = _native.hip().hm_linear_mix_apply(_native.ptr(st.S), R, dims, L, int(kld),
+                                               _native.ptr(num), _native.ptr(den), _native.ptr(cnt),
+                                               _native.ptr(w_out), _native.ptr(cov_out),
+                                               _native.stream_of(dev))
+        _native.check(rc, "hm_linear_mix_apply")
+        return w_out.view(L, dims), (cov_out.view(L, dims) if cov_out is not None else None)
+    num, den, cnt = (x.view(L, dims) for x in (num, den, cnt))
+    hit = cnt > 0
+    w = torch.where(hit, num / den.clamp_min(1e-30), st.S[0, ..., 0])
+    st.S[..., 0] = torch.where(hit.unsqueeze(0), w.unsqueeze(0), st.S[..., 0])
+    cov = None
+    if st.covar:
+        if kld:
+            cv = torch.where(hit, cnt / den.clamp_min(1e-30), st.S[0, ..., 1])
+            st.S[..., 1] = torch.where(hit.unsqueeze(0), cv.unsqueeze(0), st.S[..., 1])
+            cov = cv
+        else:
+            cov = st.S[0, ..., 1].clone()
+    return w.contiguous(), cov
+
+
+def predict_scores(w: torch.Tensor, indptr: torch.Tensor, idx: torch.Tensor,
+                   val: torch.Tensor | None, cov: torch.Tensor | None = None):
+    """Scores [n, L] (and xᵀΣx variances when ``cov`` is given) for CSR rows."""
+    L, dims = w.shape
+    n = indptr.numel() - 1
+    dev = w.device
+    out = torch.empty((n, L), dtype=torch.float32, device=dev)
+    var = torch.empty((n, L), dtype=torch.float32, device=dev) if cov is not None else None
+    p = _native.ptr
+    w = w.contiguous()
+    cov = cov.contiguous() if cov is not None else None
+    if dev.type == "cuda":
+        rc = _native.hip().hm_linear_predict(p(w), dims, L, p(indptr), p(idx), p(val), C.c_int64(n),
+                                             p(out), p(cov), p(var), _native.stream_of(dev))
+        _native.check(rc, "hm_linear_predict")
+    else:
+        _native.host().hm_linear_predict_cpu(p(w), dims, L, p(indptr), p(idx), p(val), C.c_int64(n),
+                                             p(out), p(cov), p(var))
+    return out, var
+
+
+_P = _native.c_p
+_native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
+_native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
+_native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
+_native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
+_native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])
+_native.register_host("hm_linear_predict_cpu", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P])

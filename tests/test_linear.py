@@ -1,0 +1,180 @@
+import numpy as np
+import pytest
+import torch
+
+from hivemall_amd.io.synthetic import a9a_like
+from hivemall_amd.models import linear as L
+from hivemall_amd.utils.options import UDFArgumentException
+from tests.oracle.linear_oracle import train as oracle_train
+
+
+@pytest.fixture(scope="module")
+def a9a():
+    rows, y = a9a_like(12000)
+    trows, ty = a9a_like(3000, seed=4)
+    return rows, y, trows, ty
+
+
+def _acc(m, trows, ty):
+    return float(((m.decision_function(trows).cpu().numpy() > 0) == (ty > 0)).mean())
+
+
+BINARY = ["train_perceptron", "train_pa", "train_pa1", "train_pa2", "train_cw", "train_arow",
+          "train_arowh", "train_scw", "train_scw2", "train_adagrad_rda"]
+
+
+@pytest.mark.parametrize("name", BINARY)
+def test_binary_learners_learn(a9a, name):
+    rows, y, trows, ty = a9a
+    m = L.LEARNERS[name]("", device="cpu").fit(rows, y)
+    assert _acc(m, trows, ty) > 0.7
+    tab = m.model_table()
+    cols = ["feature", "weight"] + (["covar"] if name in ("train_cw", "train_arow", "train_arowh",
+                                                          "train_scw", "train_scw2") else [])
+    assert list(tab.columns) == cols
+
+
+@pytest.mark.parametrize("opt", ["sgd", "momentum", "nesterov", "adagrad", "rmsprop", "rmspropgraves",
+                                 "adadelta", "adam", "nadam", "eve", "adam_hd"])
+def test_general_classifier_optimizers(a9a, opt):
+    rows, y, trows, ty = a9a
+    m = L.TrainClassifier(f"-loss logloss -opt {opt} -reg no -iters 3", device="cpu").fit(rows, y)
+    assert _acc(m, trows, ty) > 0.7, opt
+
+
+@pytest.mark.parametrize("loss", ["hinge", "logloss", "squared_hinge", "modified_huber"])
+@pytest.mark.parametrize("reg", ["no", "l1", "l2", "elasticnet", "rda"])
+def test_general_classifier_losses_regs(a9a, loss, reg):
+    rows, y, trows, ty = a9a
+    m = L.TrainClassifier(f"-loss {loss} -reg {reg} -iters 2", device="cpu").fit(rows, y)
+    assert _acc(m, trows, ty) > 0.7
+
+
+def test_general_options_validation():
+    with pytest.raises(UDFArgumentException):
+        L.TrainClassifier("-loss squared")          # regression loss on a classifier
+    with pytest.raises(UDFArgumentException):
+        L.TrainRegressor("-loss hinge")
+    with pytest.raises(UDFArgumentException):
+        L.TrainClassifier("-opt foo")
+    with pytest.raises(UDFArgumentException, match="usage"):
+        L.TrainClassifier("-help")
+    with pytest.raises(UDFArgumentException):
+        L.TrainClassifier("-no_such_option 1")
+
+
+def test_mini_batch_and_convergence(a9a):
+    rows, y, trows, ty = a9a
+    m = L.TrainClassifier("-loss logloss -opt sgd -reg no -eta fixed -eta0 0.05 -mini_batch 16 -iters 20",
+                          device="cpu").fit(rows, y)
+    assert _acc(m, trows, ty) > 0.7
+    assert 1 <= m.cv.epoch <= 20
+
+
+@pytest.mark.parametrize("name", ["train_pa1_regr", "train_pa1a_regr", "train_pa2_regr",
+                                  "train_pa2a_regr", "train_arow_regr", "train_arowe_regr",
+                                  "train_arowe2_regr", "train_regressor"])
+def test_regressors(a9a, name):
+    rows, _, trows, _ = a9a
+    yr = np.array([r.sum() / 50.0 for r in rows], dtype=np.float32)
+    tyr = np.array([r.sum() / 50.0 for r in trows], dtype=np.float32)
+    m = L.LEARNERS[name]("", device="cpu").fit(rows, yr)
+    rmse = float(np.sqrt(((m.decision_function(trows).numpy() - tyr) ** 2).mean()))
+    assert rmse < 0.5 * tyr.std(), (name, rmse)
+
+
+@pytest.mark.parametrize("name", ["logress", "train_logregr", "train_logistic_regr",
+                                  "train_adagrad_regr", "train_adadelta_regr"])
+def test_logistic_regressors(a9a, name):
+    rows, y, trows, ty = a9a
+    m = L.LEARNERS[name]("", device="cpu").fit(rows, (y > 0).astype(np.float32))
+    p = m.predict(trows)
+    assert ((p > 0.5) == (ty > 0)).mean() > 0.7 and (p >= 0).all() and (p <= 1).all()
+
+
+@pytest.mark.parametrize("name", [k for k in L.LEARNERS if "multiclass" in k])
+def test_multiclass(a9a, name):
+    rows, _, trows, _ = a9a
+    lab = np.array(["a", "b", "c"])
+    ym = lab[[int(r[0]) % 3 for r in rows]]
+    tym = lab[[int(r[0]) % 3 for r in trows]]
+    m = L.LEARNERS[name]("", device="cpu").fit(rows, ym)
+    assert (m.predict(trows) == tym).mean() > 0.9
+    tab = m.model_table()
+    assert list(tab.columns[:3]) == ["label", "feature", "weight"]
+    assert set(tab["label"]) == {"a", "b", "c"}
+
+
+@pytest.mark.parametrize("algo", ["perceptron", "pa1", "arow", "adagrad_logloss"])
+def test_cpu_engine_matches_numpy_oracle(a9a, algo):
+    rows, y, _, _ = a9a
+    rows, y = rows[:3000], y[:3000]
+    yy = np.where(y > 0, 1.0, -1.0)
+    w_ref, cov_ref = oracle_train(algo, rows, yy, 124)
+    name, opts = {"perceptron": ("train_perceptron", ""), "pa1": ("train_pa1", ""),
+                  "arow": ("train_arow", ""),
+                  "adagrad_logloss": ("train_classifier", "-loss logloss -opt adagrad -reg no -iters 1")}[algo]
+    m = L.LEARNERS[name](opts + " -dims 124", device="cpu").fit(rows, y)
+    w, cov = m.weights()
+    np.testing.assert_allclose(w[0].numpy(), w_ref, rtol=2e-3, atol=2e-4)
+    if algo == "arow":
+        np.testing.assert_allclose(cov[0].numpy(), cov_ref, rtol=2e-3, atol=2e-5)
+
+
+def test_string_features_and_warm_start(tmp_path, a9a):
+    rows, y, _, _ = a9a
+    srows = [[f"f{int(i)}" for i in r] for r in rows[:2000]]
+    m = L.TrainAROW("", device="cpu").fit(srows, y[:2000])
+    tab = m.model_table()
+    assert all(isinstance(f, str) for f in tab["feature"])
+    from hivemall_amd.io.model_table import read_table, write_table
+    p = write_table(tab, str(tmp_path / "arow.tsv"))
+    back = read_table(p)
+    assert list(back.columns) == ["feature", "weight", "covar"]
+    np.testing.assert_allclose(back["weight"].to_numpy(), tab["weight"].to_numpy(), rtol=1e-6)
+    m2 = L.TrainAROW(f"-loadmodel {p}", device="cpu")
+    m2.fit(srows[:10], y[:10])
+    assert len(m2.model_table()) >= len(tab) - 5
+
+
+def test_replicas_cpu_mix_is_deterministic(a9a):
+    rows, y, trows, ty = a9a
+    a = L.TrainAROW("-replicas 4 -iters 2", device="cpu").fit(rows, y)
+    b = L.TrainAROW("-replicas 4 -iters 2", device="cpu").fit(rows, y)
+    assert torch.equal(a.weights()[0], b.weights()[0])
+    assert _acc(a, trows, ty) > 0.7
+
+
+GPU_CASES = [("train_perceptron", ""), ("train_arow", ""), ("train_scw2", ""),
+             ("train_classifier", "-loss logloss -opt adam -reg l2 -iters 2"),
+             ("train_classifier", "-loss logloss -opt sgd -reg no -mini_batch 8 -iters 2"),
+             ("train_multiclass_arow", ""), ("train_pa2a_regr", "")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,opts", GPU_CASES)
+def test_gpu_kernel_matches_cpu_engine(a9a, name, opts):
+    rows, y, trows, ty = a9a
+    if "multiclass" in name:
+        y = np.array([int(r[0]) % 3 for r in rows])
+    elif "regr" in name:
+        y = np.array([r.sum() / 50.0 for r in rows], dtype=np.float32)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = L.LEARNERS[name](opts + " -replicas 3", device=dev).fit(rows, y)
+        res[dev] = m.weights()[0].cpu()
+    np.testing.assert_allclose(res["cuda"].numpy(), res["cpu"].numpy(), rtol=5e-3, atol=5e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_large_model_not_in_lds():
+    """dims > 4096 forces the global-memory replica path."""
+    rng = np.random.default_rng(1)
+    rows = [rng.choice(200000, size=20, replace=False) for _ in range(20000)]
+    wtrue = rng.normal(size=200000)
+    y = np.array([1 if wtrue[r].sum() > 0 else 0 for r in rows])
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = L.TrainClassifier("-loss logloss -iters 2 -replicas 8", device=dev).fit(rows, y)
+        res[dev] = m.weights()[0].cpu().numpy()
+    np.testing.assert_allclose(res["cuda"], res["cpu"], rtol=5e-3, atol=5e-4)
