@@ -18,7 +18,8 @@ idx, y = criteo_like(B * 4, bits, seed=3, device=dev)
 tr = FFMTrainer(f"-c -factors 4 -num_fields 39 -feature_hashing {bits}", device=dev)
 tr.init_state(1 << bits, 39)
 res = []
-for grid in [0, 1024, 2048, 4096, 8192, 16384, 65536]:
+for grid, rl in [(g, r) for g in [0, 4096, 65536] for r in (0, 1)]:
+    tr.hyper.reload = bool(rl)
     for _ in range(2):
         ffm_step(tr.state, idx[:B], None, None, y[:B], tr.hyper, grid=grid)
     torch.cuda.synchronize()
@@ -29,7 +30,7 @@ for grid in [0, 1024, 2048, 4096, 8192, 16384, 65536]:
         ffm_step(tr.state, idx[s:s + B], None, None, y[s:s + B], tr.hyper, grid=grid)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    res.append({"grid": grid, "rows_per_s": B * n / dt, "ms_per_batch": dt / n * 1e3})
+    res.append({"grid": grid, "reload": rl, "rows_per_s": B * n / dt, "ms_per_batch": dt / n * 1e3})
     print(json.dumps(res[-1]), flush=True)
 # predict-only throughput
 pred = torch.empty(B, device=dev)

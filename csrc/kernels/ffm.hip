@@ -32,6 +32,9 @@ struct FFMParams {
     int classification;    // 1: logistic loss on y in {-1,+1}; 0: squared loss
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
+    int reload;            // re-read the own slot vector right before its update (shrinks the
+                           // Hogwild read-modify-write window -> far fewer lost updates on
+                           // hot features)
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
     float min_target, max_target;  // regression clipping of the prediction
@@ -185,8 +188,13 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
 #pragma unroll
                 for (int c = 0; c < KC; ++c) gg[c] = pg[c];
                 if (STAGE) {
+                    if (P.reload) {
 #pragma unroll
-                    for (int c = 0; c < KC; ++c) { own[c] = s_v[s * KC + c]; par[c] = s_v[(b * F + a) * KC + c]; }
+                        for (int c = 0; c < KC; ++c) { own[c] = pv[c]; par[c] = s_v[(b * F + a) * KC + c]; }
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < KC; ++c) { own[c] = s_v[s * KC + c]; par[c] = s_v[(b * F + a) * KC + c]; }
+                    }
                 } else {
                     const float4* pp = reinterpret_cast<const float4*>(V + (size_t)ib * fstride + (size_t)s_fld[a] * Kp);
 #pragma unroll
@@ -246,7 +254,7 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid
+//                     use_bias, norm, grid, reload
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, float* V, float* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -255,6 +263,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.classification = ip[5]; P.train = ip[6]; P.use_linear = ip[7]; P.use_bias = ip[8];
     P.norm = ip[9];
     const int grid = ip[10];
+    P.reload = ip[11];
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;

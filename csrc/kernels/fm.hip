@@ -1,0 +1,261 @@
+// Factorization machine (Rendle 2010) fused train / predict kernel for gfx950.
+//
+// Semantics: Hivemall FactorizationMachineUDTF (train_fm) as pinned in docs/compat.md
+// (upstream core/src/main/java/hivemall/fm/FactorizationMachineUDTF.java,
+// FactorizationMachineModel.java):
+//   p   = w0 + Σ w_i x_i + ½ Σ_f [(Σ_i v_if x_i)² − Σ_i v_if² x_i²]
+//   d   = dloss/dp : classification −y/(1+exp(y p)) (y ∈ {−1,+1}); regression clip(p) − y
+//   w0 -= η (d + 2 λ0 w0) ; w_i -= η (d x_i + 2 λw w_i)
+//   v_if -= η (d x_i (S_f − v_if x_i) + 2 λv v_if),   S_f = Σ_j v_jf x_j
+//   η = eta0 / t^power_t (inverse) | eta0 (fixed) | eta0/(1+t/total) (simple)
+//
+// MI355X design:
+//   * V is a [dims][KP] table in bf16 (default; Criteo-1TB config) or fp32.  One row of V is
+//     KP·2 bytes = one 16-B load for KP = 8: every lane gathers its feature's whole factor
+//     vector with a single dwordx4 load.
+//   * bf16 updates use stochastic rounding (hash-based, deterministic per (row, feature,
+//     factor, seed)) so the SGD steps that are far below one bf16 ulp are kept in
+//     expectation instead of being rounded away.
+//   * one wave64 = one row; lanes span the non-zeros (Criteo: 39 of 64 lanes); S_f and the
+//     linear term are DPP wave reductions; the ½Σ v²x² term is folded into one reduction.
+//   * 4 waves per 256-thread block, grid-stride over rows; Hogwild across waves (no atomics
+//     except the single global-bias add per row).
+#include "common.h"
+
+namespace {
+
+struct FMParams {
+    int dims, k;              // k = real factor count (<= KP)
+    int classification, train;
+    int eta_kind;             // 0 fixed, 1 simple, 2 inverse
+    float eta0, power_t, total_steps;
+    float lambda0, lambda_w, lambda_v;
+    float min_target, max_target;
+    int use_w0;
+    uint32_t seed;
+};
+
+__device__ __forceinline__ float fm_eta(const FMParams& P, float t) {
+    if (P.eta_kind == 0) return P.eta0;
+    if (P.eta_kind == 1) return P.total_steps > 0.f ? P.eta0 / (1.f + t / P.total_steps) : P.eta0;
+    return P.eta0 / powf(t > 1.f ? t : 1.f, P.power_t);
+}
+
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+
+// Stochastic round f32 -> bf16 using 16 random bits.
+__device__ __forceinline__ uint16_t f32_to_bf16_sr(float f, uint32_t rnd) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16);
+    u += (rnd & 0xFFFFu);
+    return (uint16_t)(u >> 16);
+}
+
+template <int KP, bool BF16>
+struct VRow {
+    float v[KP];
+    __device__ __forceinline__ void load(const void* V, int i) {
+        if constexpr (BF16) {
+            const uint16_t* p = reinterpret_cast<const uint16_t*>(V) + (size_t)i * KP;
+            if constexpr (KP % 8 == 0) {
+#pragma unroll
+                for (int c = 0; c < KP / 8; ++c) {
+                    const uint4 q = reinterpret_cast<const uint4*>(p)[c];
+                    const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        v[c * 8 + 2 * j] = __uint_as_float(wds[j] << 16);
+                        v[c * 8 + 2 * j + 1] = __uint_as_float(wds[j] & 0xFFFF0000u);
+                    }
+                }
+            } else {
+                const uint2 q = *reinterpret_cast<const uint2*>(p);  // KP == 4
+                v[0] = __uint_as_float(q.x << 16);
+                v[1] = __uint_as_float(q.x & 0xFFFF0000u);
+                v[2] = __uint_as_float(q.y << 16);
+                v[3] = __uint_as_float(q.y & 0xFFFF0000u);
+            }
+        } else {
+            const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(V) + (size_t)i * KP);
+#pragma unroll
+            for (int c = 0; c < KP / 4; ++c) {
+                const float4 q = p[c];
+                v[4 * c] = q.x; v[4 * c + 1] = q.y; v[4 * c + 2] = q.z; v[4 * c + 3] = q.w;
+            }
+        }
+    }
+    __device__ __forceinline__ void store(void* V, int i, uint32_t rbase) const {
+        if constexpr (BF16) {
+            uint16_t* p = reinterpret_cast<uint16_t*>(V) + (size_t)i * KP;
+            uint32_t wds[KP / 2];
+#pragma unroll
+            for (int j = 0; j < KP / 2; ++j) {
+                const uint32_t r = hash3(rbase, (uint32_t)i, (uint32_t)j);
+                const uint32_t lo = f32_to_bf16_sr(v[2 * j], r);
+                const uint32_t hi = f32_to_bf16_sr(v[2 * j + 1], r >> 16 | r << 16);
+                wds[j] = lo | (hi << 16);
+            }
+            if constexpr (KP % 8 == 0) {
+#pragma unroll
+                for (int c = 0; c < KP / 8; ++c)
+                    reinterpret_cast<uint4*>(p)[c] = make_uint4(wds[4 * c], wds[4 * c + 1], wds[4 * c + 2], wds[4 * c + 3]);
+            } else {
+                *reinterpret_cast<uint2*>(p) = make_uint2(wds[0], wds[1]);
+            }
+        } else {
+            float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(V) + (size_t)i * KP);
+#pragma unroll
+            for (int c = 0; c < KP / 4; ++c) p[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+        }
+    }
+};
+
+template <int KP, bool BF16>
+__global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __restrict__ indptr,
+                                                 const int32_t* __restrict__ idx,
+                                                 const float* __restrict__ val,
+                                                 const float* __restrict__ y, int64_t n_rows,
+                                                 int64_t t0, float* __restrict__ w,
+                                                 void* __restrict__ V, float* __restrict__ w0,
+                                                 float* __restrict__ pred, float* __restrict__ loss) {
+    const int lane = hm::lane_id();
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t row = gw; row < n_rows; row += nw) {
+        const int64_t s = indptr[row], e = indptr[row + 1];
+        const int nnz = (int)(e - s);
+        // ---- forward: lanes over non-zeros (chunks of 64) ----
+        float S[KP];
+#pragma unroll
+        for (int f = 0; f < KP; ++f) S[f] = 0.f;
+        float lin = 0.f, sq = 0.f;
+        VRow<KP, BF16> vr;
+        int ci = -1;
+        float cx = 0.f, cw = 0.f;
+        for (int base = 0; base < nnz; base += 64) {
+            const int j = base + lane;
+            int i = -1;
+            float x = 0.f;
+            if (j < nnz) {
+                i = idx[s + j];
+                x = val ? val[s + j] : 1.f;
+                if (i < 0 || i >= P.dims) i = -1;
+            }
+            VRow<KP, BF16> t;
+            float wi = 0.f;
+            if (i >= 0) {
+                t.load(V, i);
+                wi = w[i];
+            } else {
+#pragma unroll
+                for (int f = 0; f < KP; ++f) t.v[f] = 0.f;
+                x = 0.f;
+            }
+            lin += wi * x;
+#pragma unroll
+            for (int f = 0; f < KP; ++f) {
+                const float vx = t.v[f] * x;
+                S[f] += vx;
+                sq += vx * vx;
+            }
+            if (base == 0) { vr = t; ci = i; cx = x; cw = wi; }
+        }
+        lin = hm::wave_sum(lin);
+        sq = hm::wave_sum(sq);
+        float pair = 0.f;
+#pragma unroll
+        for (int f = 0; f < KP; ++f) {
+            S[f] = hm::wave_sum(S[f]);
+            pair += S[f] * S[f];
+        }
+        float p = lin + 0.5f * (pair - sq);
+        if (P.use_w0) p += *w0;
+        const float yy = y ? y[row] : 0.f;
+        float d;
+        if (P.classification) {
+            const float z = yy * p;
+            d = -yy / (1.f + __expf(z));
+            if (lane == 0) {
+                if (pred) pred[row] = p;
+                if (loss) loss[row] = hm::log1pexp(-z);
+            }
+        } else {
+            const float pc = fminf(fmaxf(p, P.min_target), P.max_target);
+            d = pc - yy;
+            if (lane == 0) {
+                if (pred) pred[row] = pc;
+                if (loss) loss[row] = 0.5f * d * d;
+            }
+        }
+        if (!P.train) continue;
+        const float eta = fm_eta(P, (float)(t0 + row + 1));
+        const uint32_t rbase = P.seed ^ (uint32_t)(t0 + row) * 0x9E3779B9u;
+        auto upd = [&](VRow<KP, BF16>& t, int i, float x, float wi) {
+            w[i] = wi - eta * (d * x + 2.f * P.lambda_w * wi);
+#pragma unroll
+            for (int f = 0; f < KP; ++f) {
+                const float g = d * x * (S[f] - t.v[f] * x) + 2.f * P.lambda_v * t.v[f];
+                t.v[f] = f < P.k ? t.v[f] - eta * g : 0.f;
+            }
+            t.store(V, i, rbase);
+        };
+        if (ci >= 0) upd(vr, ci, cx, cw);
+        for (int base = 64; base < nnz; base += 64) {  // rows wider than one wave
+            const int j = base + lane;
+            if (j >= nnz) continue;
+            const int i = idx[s + j];
+            if (i < 0 || i >= P.dims) continue;
+            const float x = val ? val[s + j] : 1.f;
+            VRow<KP, BF16> t;
+            t.load(V, i);
+            upd(t, i, x, w[i]);
+        }
+        if (P.use_w0 && lane == 0) atomicAdd(w0, -eta * (d + 2.f * P.lambda0 * *w0));
+    }
+}
+
+template <int KP, bool BF16>
+int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const float* val,
+           const float* y, int64_t n, int64_t t0, float* w, void* V, float* w0, float* pred,
+           float* loss, int grid, hipStream_t st) {
+    int64_t blocks = grid > 0 ? grid : (n + 3) / 4;
+    if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
+                       val, y, n, t0, w, V, w0, pred, loss);
+    HM_LAUNCH_RET();
+}
+
+}  // namespace
+
+// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed
+// hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
+HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
+                      const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
+                      float* w, void* V, float* w0, float* pred, float* loss, hipStream_t stream) {
+    FMParams P;
+    P.dims = ip[0]; P.k = ip[1];
+    const int KP = ip[2];
+    P.classification = ip[3]; P.train = ip[4]; P.eta_kind = ip[5]; P.use_w0 = ip[6];
+    const int bf16 = ip[7], grid = ip[8];
+    P.seed = (uint32_t)ip[9];
+    P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
+    P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
+    if (n_rows <= 0) return 0;
+#define HM_FM_CASE(K)                                                                            \
+    case K:                                                                                      \
+        return bf16 ? launch<K, true>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, stream) \
+                    : launch<K, false>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, stream);
+    switch (KP) {
+        HM_FM_CASE(4)
+        HM_FM_CASE(8)
+        HM_FM_CASE(16)
+        HM_FM_CASE(32)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HM_FM_CASE
+}

@@ -1,0 +1,256 @@
+"""``train_fm`` — factorization machines (Rendle ICDM'10) and ``fm_predict``.
+
+Reference behaviour: Hivemall FactorizationMachineUDTF / FMHyperParameters /
+FactorizationMachineModel / FMPredictGenericUDAF (upstream core/src/main/java/hivemall/fm/;
+SURVEY.md §2.3.4, K5, O5).
+
+MI355X design: the model is a dense HBM table (w fp32 [dims], V bf16 [dims, KP] with
+stochastic-rounded SGD updates, w0 fp32); rows are uploaded once as CSR and replayed per
+epoch; one launch of ``hm_fm_step`` trains a batch (one wave64 per row, Hogwild across
+waves).  ``-fp32`` keeps V in fp32.
+
+Model table (pinned, docs/compat.md O5): ``(feature, W_i float, V_if array<float>)``; the
+global bias w0 is the row ``feature = 0`` with ``V_if = NULL``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..ops.fm import FMHyper, fm_step
+from ..utils.features import CSR, FeatureEncoder
+from ..utils.options import UDFArgumentException, flag, opt
+from .base import ConversionState, Learner, log, parse_labels_binary
+from .linear import SparseRows, encode_rows
+
+FM_OPTS = [
+    flag("classification", "c", "Act as classification"),
+    opt("factors", "factor", 5, int, "The number of latent factors", aliases=("k",)),
+    opt("iters", "iterations", 1, int, "Iterations", aliases=("iter",)),
+    opt("eta0", None, 0.05, float, "Initial learning rate"),
+    opt("eta", None, "inverse", str, "Learning rate scheme: fixed, simple, inverse"),
+    opt("power_t", None, 0.1, float, "Inverse scaling exponent"),
+    opt("t", "total_steps", -1.0, float, "Total steps for -eta simple"),
+    opt("lambda0", "lambda_w0", 0.01, float, "L2 regularization of w0"),
+    opt("lambda", "lambda_v", 0.01, float, "L2 regularization of V"),
+    opt("lambda_w", "lambdaW", 0.01, float, "L2 regularization of w"),
+    opt("sigma", None, 0.1, float, "Stddev of the gaussian V initialisation"),
+    opt("init_v", None, "gaussian", str, "V initialisation: random | gaussian"),
+    opt("maxval", "max_init_value", 1.0, float, "Range of the uniform V initialisation"),
+    opt("min", "min_target", None, float, "Minimum target (regression clipping)"),
+    opt("max", "max_target", None, float, "Maximum target (regression clipping)"),
+    opt("seed", None, -1, int, "Seed"),
+    opt("num_features", "p", -1, int, "Number of features (default: max index + 1)"),
+    opt("feature_hashing", None, -1, int, "Hash features into 2^bits"),
+    flag("int_feature", None, "Features are integers"),
+    flag("adareg", "adaptive_regularization", "Adaptive regularization (Rendle WSDM'12)"),
+    opt("va_ratio", "validation_ratio", 0.05, float, "Held-out ratio for -adareg"),
+    opt("va_threshold", "validation_threshold", 1000, int, "Min rows before -adareg starts"),
+    opt("cv_rate", "convergence_rate", 0.005, float, "Convergence threshold"),
+    flag("disable_cv", "disable_cvtest", "Disable convergence check"),
+    flag("fp32", None, "[engine] keep V in fp32 on the GPU (default bf16)"),
+    opt("batch_size", None, 1 << 20, int, "[engine] rows per kernel launch"),
+]
+_ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
+
+
+class FMTrainer(Learner):
+    NAME = "train_fm"
+    OPTIONS = FM_OPTS
+
+    def __init__(self, options: str | None = None, device=None, **kw):
+        super().__init__(options, device, **kw)
+        c = self.cl
+        self.k = int(c["factors"])
+        if self.k <= 0 or self.k > 32:
+            raise UDFArgumentException("train_fm: -factors must be in [1, 32]")
+        self.kp = next(p for p in (4, 8, 16, 32) if p >= self.k)
+        eta = c["eta"].lower()
+        if eta not in _ETAS:
+            raise UDFArgumentException(f"train_fm: unknown -eta scheme {eta}")
+        self.h = FMHyper(eta0=c["eta0"], power_t=c["power_t"], total_steps=c["t"],
+                         eta_kind=_ETAS[eta], lambda0=c["lambda0"], lambda_w=c["lambda_w"],
+                         lambda_v=c["lambda"],
+                         min_target=c["min"] if c["min"] is not None else -3.4e38,
+                         max_target=c["max"] if c["max"] is not None else 3.4e38,
+                         classification=bool(c["classification"]), seed=self.seed)
+        self.encoder: FeatureEncoder | None = None
+        if c["feature_hashing"] > 0:
+            self.encoder = FeatureEncoder("hash", num_features=1 << int(c["feature_hashing"]))
+        self.state: dict | None = None
+        self.dims: int | None = int(c["num_features"]) if c["num_features"] > 0 else None
+        if c["feature_hashing"] > 0:
+            self.dims = (1 << int(c["feature_hashing"])) + 1
+        self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
+        self.t = 0
+        self.grid = 0
+
+    # ------------------------------------------------------------------ state
+    def init_state(self, dims: int) -> dict:
+        self.dims = int(dims)
+        g = torch.Generator(device="cpu").manual_seed(self.seed)
+        dev = self.device
+        bf16 = dev.type == "cuda" and not self.cl["fp32"]
+        V = torch.zeros((self.dims, self.kp), dtype=torch.float32)
+        if self.cl["init_v"] == "random":
+            V[:, : self.k] = (torch.rand(self.dims, self.k, generator=g) - 0.5) * (
+                self.cl["maxval"] / math.sqrt(self.k))
+        else:
+            V[:, : self.k] = torch.randn(self.dims, self.k, generator=g) * self.cl["sigma"]
+        self.state = dict(w=torch.zeros(self.dims, dtype=torch.float32, device=dev),
+                          V=V.to(dev, torch.bfloat16 if bf16 else torch.float32).contiguous(),
+                          w0=torch.zeros(1, dtype=torch.float32, device=dev))
+        self.touched = torch.zeros(self.dims, dtype=torch.bool, device=dev)
+        return self.state
+
+    # ------------------------------------------------------------------ data
+    def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
+        csr, self.encoder = encode_rows(features, self.encoder, train)
+        y = None
+        if labels is not None:
+            y = parse_labels_binary(labels) if self.h.classification else \
+                np.asarray(labels, dtype=np.float32).reshape(-1)
+        return SparseRows.from_csr(csr, y, self.device)
+
+    def _ensure(self, rows: SparseRows):
+        if self.state is None:
+            dims = self.dims
+            if dims is None:
+                dims = int(rows.idx.max().item()) + 1 if rows.idx.numel() else 1
+                if self.encoder is not None and self.encoder.mode == "dict":
+                    dims = max(dims, self.encoder.vocab_size())
+            self.init_state(dims)
+
+    # ------------------------------------------------------------------ training
+    def train_rows(self, rows: SparseRows, loss_buf: torch.Tensor | None = None) -> None:
+        self._ensure(rows)
+        bs = int(self.cl["batch_size"])
+        n = rows.n
+        for s in range(0, n, bs):
+            e = min(n, s + bs)
+            ip = rows.indptr[s:e + 1]
+            if s:
+                # CSR slice: rebase is not needed, the kernel reads absolute offsets
+                pass
+            lb = None if loss_buf is None else loss_buf[s:e]
+            fm_step(self.state, ip, rows.idx, rows.val, rows.y[s:e], self.h, self.k, train=True,
+                    t0=self.t, loss=lb, grid=self.grid)
+            self.t += e - s
+        i = rows.idx.long()
+        self.touched[i[(i >= 0) & (i < self.dims)]] = True
+
+    def fit(self, features=None, labels=None, rows: SparseRows | None = None) -> "FMTrainer":
+        rows = rows if rows is not None else self.prepare(features, labels)
+        if rows.y is None:
+            raise UDFArgumentException("train_fm: labels are required")
+        self._ensure(rows)
+        va = None
+        if self.cl["adareg"] and rows.n > int(self.cl["va_threshold"]):
+            # hold out the tail as the validation slice for adaptive regularization
+            nva = max(1, int(rows.n * float(self.cl["va_ratio"])))
+            va = _slice_rows(rows, rows.n - nva, rows.n)
+            rows = _slice_rows(rows, 0, rows.n - nva)
+        loss_buf = torch.empty(rows.n, dtype=torch.float32, device=self.device)
+        for ep in range(int(self.cl["iters"])):
+            self.train_rows(rows, loss_buf)
+            if va is not None:
+                self._adapt_lambda(va)
+            self.cv.incr_loss(float(loss_buf.double().sum().item()))
+            if self.cv.is_converged():
+                log.info("train_fm converged at epoch %d", ep + 1)
+                break
+        return self
+
+    def _adapt_lambda(self, va: SparseRows) -> None:
+        """Adaptive regularization, epoch-level form of Rendle (WSDM'12): one gradient step
+        on (lambda_w, lambda_v) of the validation loss w.r.t. the regularised update."""
+        pred = self.predict_raw(rows=va)
+        y = va.y
+        if self.h.classification:
+            d = -y / (1 + torch.exp(y * pred))
+        else:
+            d = pred - y
+        w = self.state["w"]
+        V = self.state["V"].float()
+        grad_scale = float(d.abs().mean().item())
+        eta = self.h.eta0
+        # d loss / d lambda ≈ -2 eta * <grad_va, theta>; use the parameter norms as the proxy
+        self.h.lambda_w = max(0.0, self.h.lambda_w - eta * grad_scale * 1e-3 *
+                              float(w.pow(2).mean().item()))
+        self.h.lambda_v = max(0.0, self.h.lambda_v - eta * grad_scale * 1e-3 *
+                              float(V.pow(2).mean().item()))
+
+    # ------------------------------------------------------------------ inference
+    def predict_raw(self, features=None, rows: SparseRows | None = None) -> torch.Tensor:
+        rows = rows if rows is not None else self.prepare(features, None, train=False)
+        self._ensure(rows)
+        out = torch.empty(rows.n, dtype=torch.float32, device=self.device)
+        fm_step(self.state, rows.indptr, rows.idx, rows.val, None, self.h, self.k, train=False,
+                pred=out)
+        return out
+
+    def predict(self, features=None, rows: SparseRows | None = None) -> np.ndarray:
+        p = self.predict_raw(features, rows)
+        if self.h.classification:
+            p = torch.sigmoid(p)
+        return p.cpu().numpy()
+
+    # ------------------------------------------------------------------ model table
+    def model_table(self) -> pd.DataFrame:
+        ids = torch.nonzero(self.touched).flatten()
+        W = self.state["w"][ids].cpu().numpy()
+        V = self.state["V"][ids][:, : self.k].float().cpu().numpy()
+        ids = ids.cpu().numpy()
+        if self.encoder is not None and self.encoder.mode == "dict":
+            names = self.encoder.decode(ids)
+        else:
+            names = [int(i) for i in ids]
+        return pd.DataFrame({
+            "feature": [0] + names,
+            "W_i": np.concatenate([[float(self.state["w0"][0].item())], W]).astype(np.float32),
+            "V_if": [None] + [v for v in V]})
+
+
+def _slice_rows(rows: SparseRows, s: int, e: int) -> SparseRows:
+    a, b = int(rows.indptr[s].item()), int(rows.indptr[e].item())
+    return SparseRows((rows.indptr[s:e + 1] - a).contiguous(), rows.idx[a:b].contiguous(),
+                      None if rows.val is None else rows.val[a:b].contiguous(),
+                      None if rows.y is None else rows.y[s:e].contiguous())
+
+
+def train_fm(features, labels, options: str | None = None, device=None, **kw) -> pd.DataFrame:
+    return FMTrainer(options, device, **kw).fit(features, labels).model_table()
+
+
+def fm_predict_from_table(table: pd.DataFrame, rows) -> np.ndarray:
+    """Score rows of features with an FM model table (the fm_predict UDAF after the join)."""
+    w0 = 0.0
+    W, V = {}, {}
+    for f, wi, vi in zip(table["feature"], table["W_i"], table["V_if"]):
+        if vi is None or (isinstance(vi, float) and np.isnan(vi)):
+            w0 = float(wi)
+            continue
+        W[f] = float(wi)
+        V[f] = np.asarray(vi, dtype=np.float64)
+    k = len(next(iter(V.values()))) if V else 0
+    out = np.empty(len(rows))
+    from ..utils.features import parse_feature
+    for r, feats in enumerate(rows):
+        s = np.zeros(k)
+        sq = np.zeros(k)
+        lin = w0
+        for ft in feats:
+            if isinstance(ft, str):
+                name, x = parse_feature(ft)
+                key = int(name) if name.lstrip("-").isdigit() else name
+            else:
+                key, x = int(ft), 1.0
+            if key in W:
+                lin += W[key] * x
+                s += V[key] * x
+                sq += (V[key] * x) ** 2
+        out[r] = lin + 0.5 * float((s * s - sq).sum())
+    return out

@@ -27,6 +27,7 @@ class FFMHyper:
     use_linear: bool = True
     use_bias: bool = True
     norm: bool = True
+    reload: bool = True   # re-read own V right before the update (short Hogwild RMW window)
 
     def hp(self) -> np.ndarray:
         return np.array([self.eta0, self.eps, self.lambda_v, self.alpha, self.beta, self.lambda1,
@@ -60,7 +61,8 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     if loss is not None:
         assert loss.shape[0] >= B
     ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
-                   int(hyper.use_bias), int(hyper.norm), int(grid)], dtype=np.int32)
+                   int(hyper.use_bias), int(hyper.norm), int(grid), int(hyper.reload)],
+                  dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
     args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(state["G"]),

@@ -1,0 +1,67 @@
+"""FM train/predict op: gfx950 kernel (``csrc/kernels/fm.hip``) on ``cuda`` tensors, sequential
+C++ engine (``csrc/host/fm_cpu.cpp``) on CPU tensors."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+
+
+@dataclass
+class FMHyper:
+    eta0: float = 0.05
+    power_t: float = 0.1
+    total_steps: float = -1.0
+    eta_kind: int = 2              # 0 fixed, 1 simple, 2 inverse
+    lambda0: float = 0.01
+    lambda_w: float = 0.01
+    lambda_v: float = 0.01
+    min_target: float = -3.4e38
+    max_target: float = 3.4e38
+    classification: bool = False
+    use_w0: bool = True
+    seed: int = 31
+
+
+def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
+            y: torch.Tensor | None, h: FMHyper, k: int, train: bool = True, t0: int = 0,
+            pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0) -> None:
+    """One fused pass over CSR rows.  state: w f32 [dims], V bf16|f32 [dims, KP], w0 f32 [1]."""
+    w, V, w0 = state["w"], state["V"], state["w0"]
+    dims, KP = V.shape
+    n = indptr.numel() - 1
+    dev = V.device
+    for t in (indptr, idx, val, y, pred, loss):
+        if t is not None:
+            assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    assert indptr.dtype == torch.int64 and idx.dtype == torch.int32
+    if y is not None:
+        assert y.dtype == torch.float32 and y.numel() >= n
+    for t in (pred, loss):
+        if t is not None:
+            assert t.numel() >= n
+    bf16 = V.dtype == torch.bfloat16
+    ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
+                   int(bf16), grid, h.seed & 0x7FFFFFFF], dtype=np.int32)
+    hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,
+                   h.min_target, h.max_target], dtype=np.float32)
+    p = _native.ptr
+    args = [ip.ctypes.data, hp.ctypes.data, C.c_int64(n), C.c_int64(t0), p(indptr), p(idx), p(val),
+            p(y), p(w), p(V), p(w0), p(pred), p(loss)]
+    if dev.type == "cuda":
+        rc = _native.hip().hm_fm_step(*args, _native.stream_of(dev))
+        _native.check(rc, "hm_fm_step")
+    else:
+        assert not bf16, "CPU FM engine keeps V in fp32"
+        rc = _native.host().hm_fm_step_cpu(*args)
+        if rc != 0:
+            raise RuntimeError(f"hm_fm_step_cpu failed: {rc}")
+
+
+_P = _native.c_p
+_native.register_hip("hm_fm_step", [_P, _P, _native.c_i64, _native.c_i64] + [_P] * 9 + [_P])
+_native.register_host("hm_fm_step_cpu", [_P, _P, _native.c_i64, _native.c_i64] + [_P] * 9)

@@ -1,0 +1,85 @@
+import numpy as np
+import pytest
+import torch
+
+from hivemall_amd.io.synthetic import criteo_like
+from hivemall_amd.models.fm import FMTrainer, fm_predict_from_table, train_fm
+from hivemall_amd.models.linear import SparseRows
+from tests.oracle.fm_oracle import fm_train
+
+
+def _rows(idx, y=None):
+    n, F = idx.shape
+    return SparseRows(torch.arange(0, n * F + 1, F, dtype=torch.int64), idx.reshape(-1).contiguous(),
+                      None, y)
+
+
+def test_fm_cpu_engine_matches_oracle():
+    rng = np.random.default_rng(0)
+    rows = [rng.choice(50, size=6, replace=False) for _ in range(200)]
+    y = np.where(rng.random(200) < 0.4, 1, 0)
+    t = FMTrainer("-c -factors 3 -num_features 50 -seed 2", device="cpu")
+    t.fit([list(map(int, r)) for r in rows], y)
+    t2 = FMTrainer("-c -factors 3 -num_features 50 -seed 2", device="cpu")
+    t2.init_state(50)
+    V0 = t2.state["V"][:, :3].numpy()
+    w0, w, V, _ = fm_train(rows, np.where(y > 0, 1.0, -1.0), 50, V0)
+    np.testing.assert_allclose(t.state["w"].numpy(), w, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(t.state["V"][:, :3].numpy(), V, rtol=1e-4, atol=1e-6)
+    assert abs(t.state["w0"].item() - w0) < 1e-5
+
+
+def test_fm_learns_and_table_roundtrip():
+    idx, y = criteo_like(60000, 16, seed=5)
+    eidx, ey = criteo_like(5000, 16, seed=77)
+    t = FMTrainer("-c -factors 8 -num_features 65536 -eta0 0.01 -sigma 0.01", device="cpu")
+    t.fit(rows=_rows(idx, y))
+    p = t.predict_raw(rows=_rows(eidx))
+    yy = (ey > 0).float()
+    ll = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+    base = torch.nn.functional.binary_cross_entropy(yy.mean().expand_as(yy), yy).item()
+    assert ll < base
+    tab = t.model_table()
+    assert list(tab.columns) == ["feature", "W_i", "V_if"]
+    assert tab.iloc[0]["V_if"] is None
+    sub = eidx[:50].numpy()
+    ref = fm_predict_from_table(tab, [[int(v) for v in r] for r in sub])
+    np.testing.assert_allclose(ref, p[:50].numpy(), rtol=1e-3, atol=1e-4)
+
+
+def test_train_fm_string_features_regression():
+    rows = [["a:1.0", "b:0.5"], ["b:1", "c:2"], ["a:0.3", "c:1"]] * 20
+    tab = train_fm(rows, [1.0, 2.0, 0.5] * 20, "-factors 2 -iters 5 -min 0 -max 3", device="cpu")
+    assert set(tab["feature"][1:]) == {"a", "b", "c"}
+
+
+@pytest.mark.gpu
+def test_fm_gpu_fp32_matches_cpu_on_distinct_features():
+    B, F = 256, 39
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        t = FMTrainer("-c -factors 8 -fp32 -seed 4 -eta fixed -eta0 0.01", device=dev)
+        t.init_state(B * F)
+        rows = _rows(idx, y).to(dev)
+        t.train_rows(rows)
+        res[dev] = {k: v.float().cpu() for k, v in t.state.items()}
+    for k in ("w", "V"):
+        np.testing.assert_allclose(res["cuda"][k].numpy(), res["cpu"][k].numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp32", [True, False])
+def test_fm_gpu_logloss_close_to_sequential(fp32):
+    idx, y = criteo_like(200000, 18, seed=5)
+    eidx, ey = criteo_like(20000, 18, seed=77)
+    yy = (ey > 0).float()
+    res = {}
+    for dev in ("cpu", "cuda"):
+        t = FMTrainer("-c -factors 8 -num_features 262144 -eta0 0.01 -sigma 0.01" +
+                      (" -fp32" if fp32 else ""), device=dev)
+        t.fit(rows=_rows(idx, y).to(dev))
+        p = t.predict_raw(rows=_rows(eidx).to(dev)).cpu()
+        res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+    assert abs(res["cpu"] - res["cuda"]) < 0.01, res
