@@ -1,0 +1,629 @@
+"""Feature engineering functions (upstream core/src/main/java/hivemall/ftvec/
+{AddBiasUDF,AddFeatureIndexUDF,ExtractFeatureUDF,ExtractWeightUDF,FeatureUDF,FeatureIndexUDF,
+SortByFeatureUDF}, ftvec/hashing/*, ftvec/scaling/*, ftvec/amplify/*, ftvec/conv/*,
+ftvec/binning/*, ftvec/pairing/*, ftvec/ranking/*, ftvec/selection/*, ftvec/text/*,
+ftvec/trans/*).
+
+Feature grammar: ``"name:value"`` (split at the last ``:`` for FFM-style strings is NOT done;
+the value is everything after the FIRST ``:`` unless the string has two ``:`` in which case it
+is ``field:index:value``), bare ``"name"`` = value 1.0.  Index 0 is reserved for the bias.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import random
+from collections import Counter, defaultdict
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from ..registry import udaf, udf, udtf
+from ..utils.hashing import DEFAULT_SEED, mhash as _mhash, murmurhash3
+from ..utils.options import Options, UDFArgumentException, flag, opt
+
+
+def _split(f) -> tuple[str, float]:
+    s = str(f)
+    p = s.find(":")
+    if p < 0:
+        return s, 1.0
+    q = s.find(":", p + 1)
+    if q >= 0:  # field:index:value
+        return s[:q], float(s[q + 1:])
+    return s[:p], float(s[p + 1:])
+
+
+def _fmt(v: float) -> str:
+    v = float(v)
+    return repr(v) if v != int(v) or abs(v) > 1e15 else f"{v:.1f}"
+
+
+# ------------------------------------------------------------------ basic
+@udf("add_bias")
+def add_bias(features):
+    """Append the bias feature ``0:1.0`` (index 0 is reserved for the bias)."""
+    if features is None:
+        return None
+    fs = list(features)
+    if fs and isinstance(fs[0], (int, np.integer)):
+        return fs + [0]
+    return fs + ["0:1.0"]
+
+
+@udf("add_feature_index")
+def add_feature_index(values):
+    """[v1, v2, ...] -> ["1:v1", "2:v2", ...]"""
+    if values is None:
+        return None
+    return [f"{i + 1}:{_fmt(v)}" for i, v in enumerate(values) if v is not None]
+
+
+@udf("extract_feature")
+def extract_feature(f):
+    if f is None:
+        return None
+    if isinstance(f, (list, tuple, np.ndarray)):
+        return [_split(x)[0] for x in f]
+    return _split(f)[0]
+
+
+@udf("extract_weight")
+def extract_weight(f):
+    if f is None:
+        return None
+    if isinstance(f, (list, tuple, np.ndarray)):
+        return [_split(x)[1] for x in f]
+    return _split(f)[1]
+
+
+@udf("feature")
+def feature(name, value):
+    if name is None:
+        return None
+    return f"{name}:{_fmt(value) if isinstance(value, float) else value}"
+
+
+@udf("feature_index")
+def feature_index(features):
+    if features is None:
+        return None
+    if isinstance(features, (list, tuple, np.ndarray)):
+        return [int(_split(x)[0]) for x in features]
+    return int(_split(features)[0])
+
+
+@udf("sort_by_feature")
+def sort_by_feature(m):
+    if m is None:
+        return None
+    return dict(sorted(m.items(), key=lambda kv: kv[0]))
+
+
+# ------------------------------------------------------------------ hashing
+@udf("mhash")
+def mhash(word, num_features: int = 1 << 24):
+    """MurmurHash3 x86_32 (seed 0x9747b28c) of the UTF-8 word, mod num_features, 1-based."""
+    if word is None:
+        return None
+    return _mhash(str(word), int(num_features))
+
+
+_FH_OPTS = Options([opt("num_features", "features", 1 << 24, int, "Number of hashed features"),
+                    flag("libsvm", None, "Output libsvm-style index:value (default)")],
+                   "feature_hashing")
+
+
+@udf("feature_hashing")
+def feature_hashing(features, options: str | None = None):
+    """Hash feature names (keeping values): ``"name:v"`` -> ``"mhash(name):v"``."""
+    if features is None:
+        return None
+    n = _FH_OPTS.parse(options)["num_features"]
+
+    def one(f):
+        name, v = _split(f)
+        h = _mhash(name, n)
+        return str(h) if ":" not in str(f) else f"{h}:{str(f)[len(name) + 1:]}"
+    if isinstance(features, (list, tuple, np.ndarray)):
+        return [one(f) for f in features if f is not None]
+    return one(features)
+
+
+@udf("sha1")
+def sha1(word, num_features: int = 1 << 24):
+    """SHA-1 of the UTF-8 word; the first 4 bytes as a signed int, mod num_features, 1-based."""
+    if word is None:
+        return None
+    d = hashlib.sha1(str(word).encode("utf-8")).digest()
+    h = int.from_bytes(d[:4], "big", signed=True)
+    r = h % int(num_features) if h >= 0 else -((-h) % int(num_features))
+    if r < 0:
+        r += int(num_features)
+    return r + 1
+
+
+@udf("array_hash_values")
+def array_hash_values(values, prefix: str | None = None, num_features: int = 1 << 24,
+                      seed: int = DEFAULT_SEED):
+    if values is None:
+        return None
+    p = prefix or ""
+    return [_mhash(p + str(v), int(num_features), seed) for v in values if v is not None]
+
+
+@udf("prefixed_hash_values")
+def prefixed_hash_values(values, prefix: str, use_index_as_prefix: bool = False):
+    if values is None:
+        return None
+    out = []
+    for i, v in enumerate(values):
+        if v is None:
+            continue
+        pre = f"{i}{prefix}" if use_index_as_prefix else prefix
+        out.append(f"{pre}{_mhash(str(v))}")
+    return out
+
+
+# ------------------------------------------------------------------ scaling
+@udf("rescale")
+def rescale(value, mn, mx):
+    """Min-max scaling to [0, 1]; also accepts a ``name:value`` feature string."""
+    if value is None:
+        return None
+    if isinstance(value, str):
+        name, v = _split(value)
+        return f"{name}:{_fmt(rescale(v, mn, mx))}"
+    mn, mx = float(mn), float(mx)
+    if mx == mn:
+        return 0.5
+    return min(1.0, max(0.0, (float(value) - mn) / (mx - mn)))
+
+
+@udf("zscore")
+def zscore(value, mean, stddev):
+    if value is None:
+        return None
+    if isinstance(value, str):
+        name, v = _split(value)
+        return f"{name}:{_fmt(zscore(v, mean, stddev))}"
+    sd = float(stddev)
+    return (float(value) - float(mean)) / sd if sd != 0 else 0.0
+
+
+def _normalize(features, p):
+    if features is None:
+        return None
+    parsed = [_split(f) for f in features]
+    if p == 1:
+        norm = sum(abs(v) for _, v in parsed)
+    else:
+        norm = math.sqrt(sum(v * v for _, v in parsed))
+    if norm == 0:
+        return list(features)
+    return [f"{n}:{_fmt(v / norm)}" for n, v in parsed]
+
+
+@udf("l1_normalize")
+def l1_normalize(features):
+    return _normalize(features, 1)
+
+
+@udf("l2_normalize", "normalize")
+def l2_normalize(features):
+    return _normalize(features, 2)
+
+
+# ------------------------------------------------------------------ amplify
+@udtf("amplify", per_row=True)
+def amplify(xtimes, *cols):
+    """Emit every input row ``xtimes`` times (epoch emulation)."""
+    for _ in range(int(xtimes)):
+        yield tuple(cols)
+
+
+class RandAmplifier:
+    """``rand_amplify(xtimes, num_buffers, *cols)``: rows are amplified and emitted in a
+    shuffled order through a reservoir of ``num_buffers`` rows (seeded)."""
+
+    def __init__(self, xtimes: int, num_buffers: int, seed: int = 43):
+        self.x, self.nb = int(xtimes), int(num_buffers)
+        self.rng = random.Random(seed)
+
+    def run(self, rows: Iterable[tuple]):
+        buf = []
+        for r in rows:
+            for _ in range(self.x):
+                if len(buf) < self.nb:
+                    buf.append(r)
+                else:
+                    i = self.rng.randrange(len(buf))
+                    yield buf[i]
+                    buf[i] = r
+        self.rng.shuffle(buf)
+        yield from buf
+
+
+@udtf("rand_amplify", per_row=False)
+def rand_amplify(xtimes, num_buffers, *cols):
+    x = xtimes[0] if isinstance(xtimes, (list, tuple)) else xtimes
+    nb = num_buffers[0] if isinstance(num_buffers, (list, tuple)) else num_buffers
+    import pandas as pd
+    rows = list(zip(*cols))
+    out = list(RandAmplifier(x, nb).run(rows))
+    return pd.DataFrame(out, columns=[f"c{i}" for i in range(len(cols))])
+
+
+# ------------------------------------------------------------------ conversion
+@udaf("conv2dense")
+def conv2dense(features, weights, n_dims):
+    nd = int(n_dims[0] if isinstance(n_dims, (list, tuple)) else n_dims)
+    out = [0.0] * nd
+    for f, w in zip(features, weights):
+        if f is not None and 0 <= int(f) < nd:
+            out[int(f)] = float(w)
+    return out
+
+
+@udf("to_dense_features", "to_dense")
+def to_dense_features(features, dims):
+    if features is None:
+        return None
+    out = [0.0] * (int(dims) + 1)
+    for f in features:
+        n, v = _split(f)
+        i = int(n)
+        if 0 <= i <= int(dims):
+            out[i] = v
+    return out
+
+
+@udf("to_sparse_features", "to_sparse")
+def to_sparse_features(values):
+    if values is None:
+        return None
+    return [f"{i}:{_fmt(v)}" for i, v in enumerate(values) if v is not None and v != 0]
+
+
+@udtf("quantify", per_row=False)
+def quantify(output_flags, *cols):
+    """Map every non-numeric column value to a dense integer id (first-seen order)."""
+    import pandas as pd
+    out_cols = []
+    for c in cols:
+        vals = list(c)
+        if all(v is None or isinstance(v, (int, float, np.integer, np.floating)) for v in vals):
+            out_cols.append(vals)
+            continue
+        ids = {}
+        out_cols.append([None if v is None else ids.setdefault(v, len(ids)) for v in vals])
+    return pd.DataFrame({f"c{i}": c for i, c in enumerate(out_cols)})
+
+
+# ------------------------------------------------------------------ binning
+@udaf("build_bins")
+def build_bins(values, num_bins, auto_shrink=None):
+    """Quantile bin boundaries [-inf, q1, ..., +inf] (auto_shrink drops duplicates)."""
+    nb = int(num_bins[0] if isinstance(num_bins, (list, tuple)) else num_bins)
+    shrink = bool(auto_shrink[0]) if isinstance(auto_shrink, (list, tuple)) and auto_shrink else False
+    v = np.asarray([x for x in values if x is not None], dtype=np.float64)
+    qs = np.quantile(v, np.linspace(0, 1, nb + 1)[1:-1]) if v.size else np.array([])
+    edges = [-math.inf] + qs.tolist() + [math.inf]
+    if shrink:
+        edges = sorted(set(edges))
+    return edges
+
+
+@udf("feature_binning")
+def feature_binning(features, quantiles):
+    """``feature_binning(array<features>, map<name, bins>)`` -> ``name:bin`` features, or
+    ``feature_binning(double, array<double> bins)`` -> bin index."""
+    if features is None:
+        return None
+    if isinstance(features, (int, float, np.integer, np.floating)):
+        return int(np.searchsorted(np.asarray(quantiles[1:-1]), float(features), side="right"))
+    out = []
+    for f in features:
+        n, v = _split(f)
+        if n in quantiles:
+            b = int(np.searchsorted(np.asarray(quantiles[n][1:-1]), v, side="right"))
+            out.append(f"{n}:{b}")
+        else:
+            out.append(f)
+    return out
+
+
+# ------------------------------------------------------------------ pairing
+@udf("polynomial_features")
+def polynomial_features(features, degree: int = 2, interaction_only: bool = False,
+                        truncate: bool = True):
+    """Products of up to ``degree`` features: ``a^b:v_a*v_b`` (names joined with ``^``)."""
+    if features is None:
+        return None
+    parsed = [_split(f) for f in features]
+    out = list(features)
+    deg = int(degree)
+
+    def rec(start, names, val, d):
+        if d > 1:
+            out.append(f"{'^'.join(names)}:{_fmt(val)}")
+        if d == deg:
+            return
+        for j in range(start, len(parsed)):
+            n, v = parsed[j]
+            if interaction_only and n in names:
+                continue
+            if truncate and (v == 0 or v == 1) and d >= 1 and n in names:
+                continue
+            rec(j if not interaction_only else j + 1, names + [n], val * v, d + 1)
+    for i, (n, v) in enumerate(parsed):
+        rec(i if not interaction_only else i + 1, [n], v, 1)
+    return out
+
+
+@udf("powered_features")
+def powered_features(features, degree: int = 2, truncate: bool = True):
+    if features is None:
+        return None
+    out = list(features)
+    for f in features:
+        n, v = _split(f)
+        if truncate and (v == 0 or v == 1):
+            continue
+        for d in range(2, int(degree) + 1):
+            out.append(f"{n}^{d}:{_fmt(v ** d)}")
+    return out
+
+
+_FP_OPTS = Options([flag("kpa", None, "Emit (h, hk, xh, xk) for kernel-expanded PA"),
+                    flag("ffm", None, "Emit (i, j, xi, xj) pairs for FFM prediction"),
+                    opt("feature_hashing", None, -1, int, "FFM: hash bits"),
+                    opt("num_fields", None, 256, int, "FFM: number of fields"),
+                    flag("no_bias", None, "FFM: omit the bias row")], "feature_pairs")
+
+
+@udtf("feature_pairs", per_row=True, cols=("i", "j", "xi", "xj"))
+def feature_pairs(features, options=None):
+    """``-ffm``: one row (i, NULL, xi, NULL) per linear term and (i, j, xi, xj) per field pair
+    where i/j are the model keys V(feature, field of the partner).  ``-kpa``: (h, hk, xh, xk)."""
+    cl = _FP_OPTS.parse(options)
+    if features is None:
+        return
+    if cl["ffm"]:
+        from ..models.ffm_keys import ffm_pair_rows
+        yield from ffm_pair_rows(features, cl)
+        return
+    parsed = [_split(f) for f in features]
+    for a in range(len(parsed)):
+        ha, xa = parsed[a]
+        yield (ha, None, xa, None)
+        for b in range(a + 1, len(parsed)):
+            hb, xb = parsed[b]
+            yield (ha, hb, xa, xb)
+
+
+# ------------------------------------------------------------------ ranking / sampling
+_BPR_OPTS = Options([opt("sampling_rate", None, 1.0, float, "Sampling rate"),
+                     flag("with_replacement", None, "Sample with replacement"),
+                     flag("without_replacement", None, "Sample without replacement (default)"),
+                     flag("pairwise_sampling", None, "Sample (pos, neg) per positive"),
+                     opt("max_item_id", None, None, int, "Max item id"),
+                     opt("seed", None, 31, int, "Seed")], "bpr_sampling")
+
+
+@udtf("bpr_sampling", per_row=True, cols=("user", "pos_item", "neg_item"))
+def bpr_sampling(user, pos_items, max_item_id=None, options=None):
+    """Negative sampling for BPR: for each positive item of the user draw a negative item
+    uniformly from [0, max_item_id] \\ positives."""
+    if isinstance(max_item_id, str) and options is None:
+        options, max_item_id = max_item_id, None
+    cl = _BPR_OPTS.parse(options)
+    mx = int(max_item_id if max_item_id is not None else (cl["max_item_id"] or max(pos_items)))
+    pos = set(int(p) for p in pos_items)
+    if len(pos) > mx:
+        return
+    rng = random.Random((cl["seed"] * 1000003) ^ hash(user))
+    n = max(1, int(round(len(pos) * cl["sampling_rate"])))
+    plist = sorted(pos)
+    for k in range(n):
+        p = plist[k % len(plist)] if k < len(plist) else rng.choice(plist)
+        while True:
+            j = rng.randint(0, mx)
+            if j not in pos:
+                break
+        yield (user, p, j)
+
+
+@udtf("item_pairs_sampling", per_row=True, cols=("pos_item", "neg_item"))
+def item_pairs_sampling(pos_items, max_item_id, options=None):
+    for user, p, j in bpr_sampling(0, pos_items, max_item_id, options):
+        yield (p, j)
+
+
+@udtf("populate_not_in", per_row=True, cols=("item",))
+def populate_not_in(items, max_item_id, options=None):
+    """Items in [0, max_item_id] not contained in ``items``."""
+    s = set(int(i) for i in items) if items is not None else set()
+    for i in range(int(max_item_id) + 1):
+        if i not in s:
+            yield (i,)
+
+
+# ------------------------------------------------------------------ selection
+@udf("chi2")
+def chi2(observed, expected):
+    """Per-feature chi-square statistic and p-value of observed vs expected counts
+    (rows = classes, columns = features)."""
+    from scipy.stats import chi2 as _chi2
+    O = np.asarray(observed, dtype=np.float64)
+    E = np.asarray(expected, dtype=np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        terms = np.where(E > 0, (O - E) ** 2 / E, 0.0)
+    stat = terms.sum(0)
+    dof = O.shape[0] - 1
+    p = _chi2.sf(stat, dof)
+    return {"chi2": stat.tolist(), "pvalue": p.tolist()}
+
+
+@udaf("snr")
+def snr(features, labels):
+    """Signal-to-noise ratio per feature for one-hot labels: Σ_{pairs of classes}
+    |μ_i − μ_j| / (σ_i + σ_j)."""
+    X = np.asarray([list(f) for f in features], dtype=np.float64)
+    Y = np.asarray([list(l) for l in labels], dtype=np.int64)
+    cls = Y.argmax(1)
+    k = Y.shape[1]
+    out = np.zeros(X.shape[1])
+    stats = []
+    for c in range(k):
+        Xc = X[cls == c]
+        stats.append((Xc.mean(0) if len(Xc) else np.zeros(X.shape[1]),
+                      Xc.std(0) if len(Xc) else np.zeros(X.shape[1])))
+    for a in range(k):
+        for b in range(a + 1, k):
+            den = stats[a][1] + stats[b][1]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                out += np.where(den > 0, np.abs(stats[a][0] - stats[b][0]) / den, 0.0)
+    return out.tolist()
+
+
+# ------------------------------------------------------------------ text
+@udaf("tf")
+def tf(terms):
+    """Term frequency map of the group's terms: count / total."""
+    c = Counter(t for t in terms if t is not None)
+    tot = sum(c.values())
+    return {k: v / tot for k, v in c.items()} if tot else {}
+
+
+@udf("bm25")
+def bm25(term_freq, doc_len, avg_doc_len, num_docs, num_docs_with_term, k1: float = 1.2,
+         b: float = 0.75, delta: float = 0.0):
+    """Okapi BM25 score of one term in one document (BM25+ with delta > 0)."""
+    idf = math.log(1 + (num_docs - num_docs_with_term + 0.5) / (num_docs_with_term + 0.5))
+    tf_ = float(term_freq)
+    norm = tf_ * (k1 + 1) / (tf_ + k1 * (1 - b + b * float(doc_len) / float(avg_doc_len)))
+    return idf * (norm + delta)
+
+
+@udf("tfidf")
+def tfidf(tf_value, df, num_docs):
+    """tf * log10(N / max(1, df)) + 1 (the define-macros.hive ``tfidf`` macro)."""
+    return float(tf_value) * (math.log10(float(num_docs) / max(1.0, float(df))) + 1.0)
+
+
+@udf("idf")
+def idf(df, num_docs):
+    return math.log10(float(num_docs) / max(1.0, float(df))) + 1.0
+
+
+# ------------------------------------------------------------------ transformation
+def _is_num(v):
+    return isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool)
+
+
+@udf("vectorize_features")
+def vectorize_features(names, *values):
+    """Quantitative values -> ``name:value`` (0/NULL dropped); strings -> ``name#value``."""
+    out = []
+    for n, v in zip(names, values):
+        if v is None:
+            continue
+        if _is_num(v):
+            if float(v) != 0:
+                out.append(f"{n}:{_fmt(v)}")
+        elif isinstance(v, bool):
+            if v:
+                out.append(f"{n}")
+        else:
+            out.append(f"{n}#{v}")
+    return out
+
+
+@udf("categorical_features")
+def categorical_features(names, *values):
+    return [f"{n}#{v}" for n, v in zip(names, values) if v is not None]
+
+
+@udf("quantitative_features")
+def quantitative_features(names, *values):
+    return [f"{n}:{_fmt(v)}" for n, v in zip(names, values) if v is not None and float(v) != 0]
+
+
+@udf("indexed_features")
+def indexed_features(*values):
+    return [f"{i + 1}:{_fmt(v)}" for i, v in enumerate(values) if v is not None]
+
+
+@udtf("quantified_features", per_row=False, cols=("features",))
+def quantified_features(output_flags, *cols):
+    import pandas as pd
+    q = quantify(output_flags, *cols)
+    rows = [list(map(lambda x: float(x) if x is not None else None, r)) for r in q.itertuples(index=False)]
+    return pd.DataFrame({"features": rows})
+
+
+@udtf("binarize_label", per_row=True)
+def binarize_label(n_pos, n_neg, *cols):
+    """Emit the row ``n_pos`` times with label 1 and ``n_neg`` times with label 0."""
+    for _ in range(int(n_pos or 0)):
+        yield tuple(cols) + (1,)
+    for _ in range(int(n_neg or 0)):
+        yield tuple(cols) + (0,)
+
+
+@udaf("onehot_encoding")
+def onehot_encoding(*cols):
+    """One map per column: distinct value -> consecutive one-hot index (global across columns,
+    starting at 1)."""
+    out = []
+    nxt = 1
+    for c in cols:
+        m = {}
+        for v in c:
+            if v is not None and v not in m:
+                m[v] = nxt
+                nxt += 1
+        out.append(m)
+    return out
+
+
+_FFMF_OPTS = Options([opt("feature_hashing", None, -1, int, "Hash bits for the index"),
+                      opt("num_fields", None, 256, int, "Number of fields"),
+                      flag("no_hash", None, "Keep indices unhashed (names must be integers)")],
+                     "ffm_features")
+
+
+@udf("ffm_features")
+def ffm_features(names, *values_and_opts):
+    """``ffm_features(array<string> names, v1, v2, ... [, options])`` -> ``field:index:value``.
+    Field = column position; index = mhash("name#value") (categorical) or mhash(name)."""
+    vals = list(values_and_opts)
+    options = None
+    if vals and isinstance(vals[-1], str) and vals[-1].startswith("-") and len(vals) > len(names):
+        options = vals.pop()
+    cl = _FFMF_OPTS.parse(options)
+    nf = (1 << cl["feature_hashing"]) if cl["feature_hashing"] > 0 else (1 << 24)
+    out = []
+    for f, (n, v) in enumerate(zip(names, vals)):
+        if v is None:
+            continue
+        if _is_num(v):
+            if float(v) == 0:
+                continue
+            key = str(n)
+            x = float(v)
+        else:
+            key = f"{n}#{v}"
+            x = 1.0
+        idx = int(key) if cl["no_hash"] else _mhash(key, nf)
+        out.append(f"{f}:{idx}:{_fmt(x)}")
+    return out
+
+
+@udf("add_field_indices")
+def add_field_indices(features):
+    """Prefix each feature with its 1-based position as the field: ``i:feature``."""
+    if features is None:
+        return None
+    return [f"{i + 1}:{f}" for i, f in enumerate(features)]

@@ -1,0 +1,70 @@
+"""Imports every function module (registering its SQL functions) and registers the learners
+as table functions: ``SELECT train_xxx(features, label, '-opts') AS (...) FROM t`` trains on
+the session device and returns the model table (upstream's UDTF ``close()`` -> forwardModel).
+Mirrors ``resources/ddl/define-all.hive``.
+"""
+from __future__ import annotations
+
+import pandas as pd
+
+from . import registry
+from .anomaly import changefinder, sst  # noqa: F401
+from .ensemble import argmin_kld  # noqa: F401
+from .evaluation import metrics  # noqa: F401
+from .ftvec import functions as _ftvec  # noqa: F401
+from .knn import cosine_similarity  # noqa: F401
+from .misc import approx_count_distinct  # noqa: F401
+from .models import ffm_keys  # noqa: F401
+from .tools import functions as _tools  # noqa: F401
+
+
+def _opt_arg(args, k):
+    if len(args) > k and args[k]:
+        v = args[k][0]
+        return None if v is None else str(v)
+    return None
+
+
+def _device(session):
+    return None if session is None else session.device
+
+
+def _learner_udtf(name, cls_getter, n_data_args=2):
+    def impl(*args, session=None):
+        cls = cls_getter()
+        opts = _opt_arg(args, n_data_args)
+        m = cls(opts, device=_device(session))
+        m.fit(*[list(a) for a in args[:n_data_args]])
+        return m.model_table()
+    impl.wants_session = True
+    impl.__doc__ = f"{name}(features, label [, options]) -> model table"
+    registry._register(registry.FunctionDef(name, registry.UDTF, impl, per_row=False,
+                                            doc=impl.__doc__))
+
+
+def _register_learners():
+    from .models import linear as L
+    for n in L.LEARNERS:
+        _learner_udtf(n, lambda n=n: L.LEARNERS[n])
+    from .models.fm import FMTrainer
+    _learner_udtf("train_fm", lambda: FMTrainer)
+    from .models.ffm import FFMTrainer
+    _learner_udtf("train_ffm", lambda: FFMTrainer)
+    _optional_learners()
+
+
+def _optional_learners():
+    import importlib
+    for mod in ("mf", "trees", "topicmodel", "recommend"):
+        try:
+            m = importlib.import_module(f".models.{mod}", __package__)
+        except ModuleNotFoundError as e:
+            if e.name and e.name.endswith(f"models.{mod}"):
+                continue
+            raise
+        reg = getattr(m, "register_sql", None)
+        if reg is not None:
+            reg(_learner_udtf)
+
+
+_register_learners()

@@ -17,8 +17,8 @@ MI355X design:
   replacement).
 
 Model table (pinned, docs/compat.md O4): ``(model_id string, i int, Wi float, Vi array<float>)``
-one row per touched feature ``i`` with ``Vi`` the flattened [num_fields x factors] block, plus
-a row ``i = -1`` carrying the global bias ``w0`` in ``Wi``.
+keyed as in :mod:`models.ffm_keys`: ``i = -1`` bias, ``i = feature`` linear weight,
+``i = NF + feature*F + field`` the latent vector V[feature, field].
 """
 from __future__ import annotations
 
@@ -231,17 +231,22 @@ class FFMTrainer(Learner):
 
     # ------------------------------------------------------------------ model table
     def model_table(self, model_id: str | None = None) -> pd.DataFrame:
+        """Rows keyed as in :mod:`models.ffm_keys` (bias, linear, and V(feature, field))."""
         self._ensure_state()
         mid = model_id or f"ffm-{self.rank}"
         ids = torch.nonzero(self.touched).flatten()
-        V = self.state["V"][ids][:, :, : self.k].reshape(len(ids), -1).cpu().numpy()
+        NF, F, k = self.num_features, self.num_fields, self.k
+        V = self.state["V"][ids][:, :, :k].reshape(len(ids) * F, k).cpu().numpy()
         W = self.state["w"][ids].cpu().numpy()
-        ids = ids.cpu().numpy()
-        rows = {"model_id": [mid] * (len(ids) + 1),
-                "i": np.concatenate([[-1], ids]).astype(np.int64),
-                "Wi": np.concatenate([[float(self.state["bias"][0].item())], W]).astype(np.float32),
-                "Vi": [None] + [v for v in V]}
-        return pd.DataFrame(rows)
+        ids = ids.cpu().numpy().astype(np.int64)
+        vkeys = (NF + ids[:, None] * F + np.arange(F)[None, :]).reshape(-1)
+        n_lin = len(ids)
+        return pd.DataFrame({
+            "model_id": [mid] * (1 + n_lin + len(vkeys)),
+            "i": np.concatenate([[-1], ids, vkeys]).astype(np.int64),
+            "Wi": np.concatenate([[float(self.state["bias"][0].item())], W,
+                                  np.full(len(vkeys), np.nan)]).astype(np.float32),
+            "Vi": [None] * (1 + n_lin) + list(V)})
 
     def state_dict(self) -> dict:
         return {k: v.detach().cpu() for k, v in (self.state or {}).items()} | {

@@ -207,9 +207,11 @@ class FMTrainer(Learner):
         if self.encoder is not None and self.encoder.mode == "dict":
             names = self.encoder.decode(ids)
         else:
-            names = [int(i) for i in ids]
+            as_str = self.encoder is not None and getattr(self.encoder, "string_names", False)
+            names = [str(int(i)) if as_str else int(i) for i in ids]
+        bias_name = "0" if names and isinstance(names[0], str) else 0
         return pd.DataFrame({
-            "feature": [0] + names,
+            "feature": [bias_name] + names,
             "W_i": np.concatenate([[float(self.state["w0"][0].item())], W]).astype(np.float32),
             "V_if": [None] + [v for v in V]})
 
@@ -254,3 +256,28 @@ def fm_predict_from_table(table: pd.DataFrame, rows) -> np.ndarray:
                 sq += (V[key] * x) ** 2
         out[r] = lin + 0.5 * float((s * s - sq).sum())
     return out
+
+
+from ..registry import udaf as _udaf  # noqa: E402
+
+
+@_udaf("fm_predict")
+def fm_predict(Wj, Vjf, Xj):
+    """FMPredictGenericUDAF: Σ W_j·x_j + ½ Σ_f [(Σ_j V_jf x_j)² − Σ_j V_jf² x_j²] over the
+    joined rows of one example (the bias row ``feature 0`` carries w0 with x = 1)."""
+    lin = 0.0
+    S = None
+    sq = None
+    for w, v, x in zip(Wj, Vjf, Xj):
+        if x is None:
+            continue
+        x = float(x)
+        if w is not None and not (isinstance(w, float) and math.isnan(w)):
+            lin += float(w) * x
+        if v is not None and not (isinstance(v, float)):
+            vv = np.asarray(v, dtype=np.float64) * x
+            S = vv.copy() if S is None else S + vv
+            sq = vv * vv if sq is None else sq + vv * vv
+    if S is None:
+        return lin
+    return lin + 0.5 * float((S * S - sq).sum())

@@ -109,6 +109,9 @@ def encode_rows(rows, encoder: FeatureEncoder | None, train: bool) -> tuple[CSR,
         return rows, encoder or FeatureEncoder("int")
     if encoder is None:
         enc = FeatureEncoder("int")
+        # string features that are integer literals keep the string type in the model table
+        first = next((r[0] for r in rows if r is not None and len(r)), None)
+        enc.string_names = isinstance(first, str)
         try:
             return enc.encode(rows), enc
         except UDFArgumentException:
@@ -310,6 +313,8 @@ class OnlineLinearLearner(Learner):
     def _feature_names(self, ids: np.ndarray) -> list:
         if self.encoder is not None and self.encoder.mode == "dict":
             return self.encoder.decode(ids)
+        if self.encoder is not None and getattr(self.encoder, "string_names", False):
+            return [str(int(i)) for i in ids]
         return [int(i) for i in ids]
 
     def model_table(self) -> pd.DataFrame:

@@ -1,1 +1,2 @@
-
+"""HiveQL-subset SQL frontend (N7)."""
+from .executor import Session, SQLError  # noqa: F401

@@ -1,0 +1,143 @@
+"""SQL golden tests: Hivemall's documented HiveQL patterns."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from hivemall_amd.io.synthetic import a9a_like
+from hivemall_amd.sql import Session, SQLError
+
+
+@pytest.fixture
+def sess():
+    rows, y = a9a_like(3000)
+    trows, ty = a9a_like(600, seed=4)
+    s = Session(device="cpu")
+    s.register("train", pd.DataFrame({"rowid": range(len(rows)),
+                                      "features": [[str(int(i)) for i in r] for r in rows], "label": y}))
+    s.register("test", pd.DataFrame({"rowid": range(len(trows)),
+                                     "features": [[str(int(i)) for i in r] for r in trows], "label": ty}))
+    return s
+
+
+def test_a9a_logistic_pipeline(sess):
+    sess.sql("""
+    add jar hivemall-core.jar;
+    source define-all.hive;
+    create temporary function train_classifier as 'hivemall.classifier.GeneralClassifierUDTF';
+    CREATE TABLE model AS
+    SELECT feature, avg(weight) as weight FROM (
+      SELECT train_classifier(add_bias(features), label, '-loss logloss -opt adagrad -reg no -iters 3')
+             AS (feature, weight)
+      FROM train) t GROUP BY feature;
+    CREATE TABLE test_exploded AS
+    SELECT rowid, label, extract_feature(fv) AS feature, extract_weight(fv) AS value
+    FROM test LATERAL VIEW explode(add_bias(features)) t AS fv;
+    CREATE TABLE pred AS
+    SELECT t.rowid, sigmoid(sum(m.weight * t.value)) AS prob, max(t.label) AS label
+    FROM test_exploded t LEFT OUTER JOIN model m ON (t.feature = m.feature)
+    GROUP BY t.rowid;
+    """)
+    r = sess.sql("SELECT auc(prob, label) AS auc, logloss(prob, label) AS ll, count(*) AS n FROM pred")
+    assert r["n"][0] == 600 and r["auc"][0] > 0.8 and r["ll"][0] < 0.6
+    assert list(sess.table("model").columns) == ["feature", "weight"]
+
+
+def test_arow_argmin_kld_mix(sess):
+    m = sess.sql("""
+    SELECT feature, argmin_kld(weight, covar) AS weight FROM (
+      SELECT train_arow(add_bias(features), label) AS (feature, weight, covar) FROM train
+      UNION ALL
+      SELECT train_arow(add_bias(features), label, '-r 0.2') AS (feature, weight, covar) FROM train
+    ) t GROUP BY feature""")
+    assert len(m) >= 100 and m["weight"].notna().all()
+
+
+def test_multiclass_predict_with_maxrow(sess):
+    sess.sql("""
+    CREATE TABLE mtrain AS SELECT rowid, features, CAST(pmod(CAST(features[0] AS int), 3) AS int) AS label FROM train;
+    CREATE TABLE mmodel AS SELECT train_multiclass_scw(features, label) AS (label, feature, weight, covar) FROM mtrain;
+    CREATE TABLE scores AS
+    SELECT t.rowid, m.label, sum(m.weight) AS score
+    FROM (SELECT rowid, fv AS feature FROM mtrain LATERAL VIEW explode(features) e AS fv) t
+    JOIN mmodel m ON (t.feature = m.feature)
+    GROUP BY t.rowid, m.label;
+    """)
+    pred = sess.sql("""
+    SELECT rowid, maxrow(score, label)[1] AS predicted FROM scores GROUP BY rowid""")
+    truth = sess.table("mtrain").set_index("rowid")["label"]
+    acc = np.mean([truth[r] == p for r, p in zip(pred["rowid"], pred["predicted"])])
+    assert acc > 0.9
+
+
+def test_fm_sql_predict_matches_trainer():
+    from hivemall_amd.models.fm import FMTrainer
+    rng = np.random.default_rng(0)
+    # index 0 is reserved for the bias (add_bias), like upstream
+    rows = [[f"{int(i) + 1}:1" for i in rng.choice(100, size=5, replace=False)] for _ in range(400)]
+    y = rng.random(400).astype(np.float32)
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"rowid": range(400), "features": rows, "y": y}))
+    s.sql("CREATE TABLE fm_model AS SELECT train_fm(features, y, '-factors 3 -iters 2') AS (feature, Wi, Vif) FROM t")
+    p = s.sql("""
+    SELECT t.rowid, fm_predict(m.Wi, m.Vif, t.Xi) AS p FROM (
+      SELECT rowid, extract_feature(fv) AS feature, extract_weight(fv) AS Xi
+      FROM t LATERAL VIEW explode(add_bias(features)) e AS fv) t
+    LEFT OUTER JOIN fm_model m ON (t.feature = m.feature)
+    GROUP BY t.rowid ORDER BY rowid""")
+    tr = FMTrainer("-factors 3 -iters 2", device="cpu").fit(rows, y)
+    ref = tr.predict(rows)
+    np.testing.assert_allclose(p["p"].to_numpy(dtype=float), ref, rtol=1e-3, atol=1e-4)
+
+
+def test_ffm_sql_predict_matches_trainer():
+    from hivemall_amd.models.ffm import FFMTrainer
+    rng = np.random.default_rng(1)
+    rows = [[f"{f}:{int(rng.integers(0, 20))}:1" for f in range(4)] for _ in range(300)]
+    y = (rng.random(300) < 0.4).astype(int)
+    opts = "-c -factors 2 -num_fields 4 -feature_hashing 10 -iters 2 -w0"
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"rowid": range(300), "features": rows, "label": y}))
+    s.sql(f"CREATE TABLE ffm_model AS SELECT train_ffm(features, label, '{opts}') AS (model_id, i, Wi, Vi) FROM t")
+    p = s.sql("""
+    SELECT t.rowid, sigmoid(ffm_predict(m1.Wi, m1.Vi, m2.Vi, t.Xi, t.Xj)) AS p FROM (
+      SELECT rowid, i, j, Xi, Xj FROM t
+      LATERAL VIEW feature_pairs(features, '-ffm -feature_hashing 10 -num_fields 4') x AS i, j, Xi, Xj) t
+    LEFT OUTER JOIN ffm_model m1 ON (t.i = m1.i)
+    LEFT OUTER JOIN ffm_model m2 ON (t.j = m2.i)
+    GROUP BY t.rowid ORDER BY rowid""")
+    tr = FFMTrainer(opts, device="cpu").fit(rows, y)
+    ref = tr.predict(rows)
+    np.testing.assert_allclose(p["p"].to_numpy(dtype=float), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_query_features():
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"g": ["a", "a", "b", "b", "b"], "x": [1, 2, 3, 4, 5]}))
+    r = s.sql("""
+    WITH w AS (SELECT g, x, row_number() OVER (PARTITION BY g ORDER BY x DESC) AS rn FROM t)
+    SELECT g, x FROM w WHERE rn = 1 ORDER BY g""")
+    assert r.values.tolist() == [["a", 2], ["b", 5]]
+    r = s.sql("SELECT g, sum(x) s, count(*) c FROM t GROUP BY g HAVING sum(x) > 5 ORDER BY s DESC")
+    assert r.values.tolist() == [["b", 12, 3]]
+    r = s.sql("SELECT CASE WHEN x > 2 THEN 'hi' ELSE 'lo' END AS k, x BETWEEN 2 AND 4 AS b, "
+              "x IN (1, 5) AS i FROM t ORDER BY x")
+    assert r["k"].tolist() == ["lo", "lo", "hi", "hi", "hi"]
+    assert r["b"].tolist() == [False, True, True, True, False]
+    s.sql("CREATE TEMPORARY MACRO max3(a, b, c) max2(max2(a, b), c)")
+    assert s.sql("SELECT max3(1, 7, 3) AS m")["m"][0] == 7
+    s.sql("set hivevar:lim=2")
+    assert len(s.sql("SELECT * FROM t LIMIT ${lim}")) == 2
+    r = s.sql("SELECT x FROM t WHERE g = 'a' UNION ALL SELECT x FROM t WHERE x > 4")
+    assert sorted(r["x"].tolist()) == [1, 2, 5]
+    r = s.sql("SELECT each_top_k(2, g, x, g, x) AS (rank, key, gg, xx) FROM (SELECT * FROM t CLUSTER BY g) t")
+    assert len(r) == 4
+    with pytest.raises(SQLError):
+        s.sql("SELECT nope FROM t")
+    assert "train_ffm" in s.sql("SHOW FUNCTIONS")["tab_name"].tolist()
+
+
+def test_amplify_and_rand_amplify(sess):
+    r = sess.sql("SELECT amplify(3, rowid, label) AS (rowid, label) FROM train")
+    assert len(r) == 9000
+    r = sess.sql("SELECT rand_amplify(2, 100, rowid, label) AS (rowid, label) FROM train")
+    assert len(r) == 6000 and sorted(r["rowid"].tolist()) == sorted(list(range(3000)) * 2)
