@@ -1,0 +1,272 @@
+// Matrix factorization kernels for gfx950: biased MF with SGD / AdaGrad (train_mf_sgd,
+// train_mf_adagrad) and BPR-MF (train_bprmf) with optional fused device-side negative
+// sampling.
+//
+// Semantics (upstream core/src/main/java/hivemall/mf/
+// {OnlineMatrixFactorizationUDTF,MatrixFactorizationSGDUDTF,MatrixFactorizationAdaGradUDTF,
+// BPRMatrixFactorizationUDTF}.java):
+//   MF : r̂ = μ + b_u + b_i + p_u·q_i,  e = r − r̂
+//        p_u += η(e q_i − λ p_u);  q_i += η(e p_u − λ q_i);  b_u += η(e − λ b_u); b_i likewise
+//        AdaGrad: η_x = η0 / sqrt(eps + G_x) per parameter, G_x += g²
+//   BPR: x = b_i − b_j + p_u·(q_i − q_j);  z = dloss  (lnLogistic: σ(−x))
+//        p_u += η(z (q_i − q_j) − λu p_u); q_i += η(z p_u − λi q_i); q_j += η(−z p_u − λj q_j)
+//        b_i += η(z − λb b_i);  b_j += η(−z − λb b_j)
+//
+// MI355X mapping: a "group" of G = next_pow2(k) <= 64 lanes owns one rating/triple (lane f
+// holds factor f), so k = 10 packs 4 ratings per wave64 (16-lane groups) and k = 64 one.  The
+// dot product is a width-G butterfly (__shfl_xor inside the group).  Factor rows are gathered
+// as contiguous k-float segments.  Hogwild across groups, like every GPU MF-SGD.
+#include "common.h"
+
+namespace {
+
+struct MFParams {
+    int k, kp;                 // factors, row stride
+    int n_users, n_items;
+    int adagrad;               // 0 SGD, 1 AdaGrad
+    int use_bias, update_mean;
+    int eta_kind;              // 0 fixed, 1 simple, 2 inverse
+    float eta0, power_t, total_steps;
+    float lambda_u, lambda_i, lambda_j, lambda_b;
+    float eps;
+    int loss;                  // BPR: 0 lnLogistic, 1 logistic, 2 sigmoid
+    uint32_t seed;
+    int max_tries;             // negative-sampling rejection tries
+};
+
+__device__ __forceinline__ float eta_t(const MFParams& P, float t) {
+    if (P.eta_kind == 0) return P.eta0;
+    if (P.eta_kind == 1) return P.total_steps > 0.f ? P.eta0 / (1.f + t / P.total_steps) : P.eta0;
+    return P.eta0 / powf(t > 1.f ? t : 1.f, P.power_t);
+}
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- biased MF (ratings)
+template <int G>
+__global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __restrict__ users,
+                                                 const int32_t* __restrict__ items,
+                                                 const float* __restrict__ ratings, int64_t n,
+                                                 int64_t t0, float* __restrict__ Pu,
+                                                 float* __restrict__ Qi, float* __restrict__ Bu,
+                                                 float* __restrict__ Bi, float* __restrict__ mu,
+                                                 float* __restrict__ GPu, float* __restrict__ GQi,
+                                                 float* __restrict__ GBu, float* __restrict__ GBi,
+                                                 int train, float* __restrict__ pred,
+                                                 float* __restrict__ loss) {
+    constexpr int PER = 64 / G;                       // ratings per wave
+    const int lane = hm::lane_id();
+    const int sub = lane / G, f = lane % G;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t base = wave * PER; base < n; base += nwaves * PER) {
+        const int64_t r = base + sub;
+        const bool act = r < n;
+        int u = act ? users[r] : -1, i = act ? items[r] : -1;
+        const bool ok = act && u >= 0 && u < P.n_users && i >= 0 && i < P.n_items;
+        const bool fa = ok && f < P.k;
+        float pu = 0.f, qi = 0.f;
+        const size_t ou = (size_t)(ok ? u : 0) * P.kp + f, oi = (size_t)(ok ? i : 0) * P.kp + f;
+        if (fa) { pu = Pu[ou]; qi = Qi[oi]; }
+        float dot = group_sum<G>(pu * qi);
+        float bu = 0.f, bi = 0.f;
+        if (ok && P.use_bias) { bu = Bu[u]; bi = Bi[i]; }
+        const float m = *mu;
+        const float rhat = m + bu + bi + dot;
+        const float rr = act ? ratings[r] : 0.f;
+        const float e = rr - rhat;
+        if (ok && f == 0) {
+            if (pred) pred[r] = rhat;
+            if (loss) loss[r] = e * e;
+        }
+        if (!train || !ok) continue;
+        const float t = (float)(t0 + r + 1);
+        if (!P.adagrad) {
+            const float eta = eta_t(P, t);
+            if (fa) {
+                Pu[ou] = pu + eta * (e * qi - P.lambda_u * pu);
+                Qi[oi] = qi + eta * (e * pu - P.lambda_i * qi);
+            }
+            if (P.use_bias && f == 0) {
+                Bu[u] = bu + eta * (e - P.lambda_b * bu);
+                Bi[i] = bi + eta * (e - P.lambda_b * bi);
+            }
+        } else {
+            if (fa) {
+                const float gp = e * qi - P.lambda_u * pu, gq = e * pu - P.lambda_i * qi;
+                const float Gp = GPu[ou] + gp * gp, Gq = GQi[oi] + gq * gq;
+                GPu[ou] = Gp;
+                GQi[oi] = Gq;
+                Pu[ou] = pu + P.eta0 * gp * rsqrtf(P.eps + Gp);
+                Qi[oi] = qi + P.eta0 * gq * rsqrtf(P.eps + Gq);
+            }
+            if (P.use_bias && f == 0) {
+                const float gbu = e - P.lambda_b * bu, gbi = e - P.lambda_b * bi;
+                const float Gu = GBu[u] + gbu * gbu, Gi = GBi[i] + gbi * gbi;
+                GBu[u] = Gu;
+                GBi[i] = Gi;
+                Bu[u] = bu + P.eta0 * gbu * rsqrtf(P.eps + Gu);
+                Bi[i] = bi + P.eta0 * gbi * rsqrtf(P.eps + Gi);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- BPR-MF
+__device__ __forceinline__ uint32_t pcg(uint64_t& s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((-rot) & 31));
+}
+
+// Is item j in the sorted positive list of user u?  (CSR: ptr[u]..ptr[u+1])
+__device__ __forceinline__ bool is_positive(const int64_t* ptr, const int32_t* items, int u, int j) {
+    int64_t lo = ptr[u], hi = ptr[u + 1] - 1;
+    while (lo <= hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int v = items[mid];
+        if (v == j) return true;
+        if (v < j) lo = mid + 1; else hi = mid - 1;
+    }
+    return false;
+}
+
+// Triples either given explicitly (tu/ti/tj) or sampled on the device: a uniformly random
+// positive (u, i) from the user->items CSR and a uniformly random negative j (rejection
+// against u's sorted positives).
+template <int G>
+__global__ __launch_bounds__(256) void bpr_kernel(MFParams P, const int32_t* __restrict__ tu,
+                                                  const int32_t* __restrict__ ti,
+                                                  const int32_t* __restrict__ tj, int64_t n,
+                                                  const int64_t* __restrict__ uptr,
+                                                  const int32_t* __restrict__ uitems,
+                                                  const int32_t* __restrict__ pos_user,
+                                                  int64_t n_pos, int64_t t0,
+                                                  float* __restrict__ Pu, float* __restrict__ Qi,
+                                                  float* __restrict__ Bi, double* __restrict__ loss_sum) {
+    constexpr int PER = 64 / G;
+    const int lane = hm::lane_id();
+    const int sub = lane / G, f = lane % G;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    double lacc = 0.0;
+    for (int64_t base = wave * PER; base < n; base += nwaves * PER) {
+        const int64_t r = base + sub;
+        const bool act = r < n;
+        int u = -1, i = -1, j = -1;
+        if (act) {
+            if (tu) {
+                u = tu[r]; i = ti[r]; j = tj[r];
+            } else {
+                uint64_t s = ((uint64_t)P.seed << 32) ^ (uint64_t)(t0 + r) * 0x9E3779B97F4A7C15ull;
+                pcg(s);
+                const uint64_t pidx = ((uint64_t)pcg(s) << 32 | pcg(s)) % (uint64_t)n_pos;
+                u = pos_user[pidx];
+                i = uitems[pidx];
+                for (int tries = 0; tries < P.max_tries; ++tries) {
+                    j = (int)(pcg(s) % (uint32_t)P.n_items);
+                    if (!is_positive(uptr, uitems, u, j)) break;
+                    j = -1;
+                }
+            }
+        }
+        const bool ok = act && u >= 0 && u < P.n_users && i >= 0 && i < P.n_items && j >= 0 &&
+                        j < P.n_items && i != j;
+        const bool fa = ok && f < P.k;
+        const size_t ou = (size_t)(ok ? u : 0) * P.kp + f;
+        const size_t oi = (size_t)(ok ? i : 0) * P.kp + f, oj = (size_t)(ok ? j : 0) * P.kp + f;
+        float pu = 0.f, qi = 0.f, qj = 0.f;
+        if (fa) { pu = Pu[ou]; qi = Qi[oi]; qj = Qi[oj]; }
+        const float d = group_sum<G>(pu * (qi - qj));
+        float bi = 0.f, bj = 0.f;
+        if (ok && P.use_bias) { bi = Bi[i]; bj = Bi[j]; }
+        const float x = bi - bj + d;
+        float z;
+        if (P.loss == 2) { const float s = hm::sigmoidf_(x); z = s * (1.f - s); }   // sigmoid
+        else z = 1.f / (1.f + __expf(x));                                          // σ(−x)
+        if (ok && f == 0) lacc += (double)hm::log1pexp(-x);
+        if (!ok) continue;
+        const float eta = eta_t(P, (float)(t0 + r + 1));
+        if (fa) {
+            Pu[ou] = pu + eta * (z * (qi - qj) - P.lambda_u * pu);
+            Qi[oi] = qi + eta * (z * pu - P.lambda_i * qi);
+            Qi[oj] = qj + eta * (-z * pu - P.lambda_j * qj);
+        }
+        if (P.use_bias && f == 0) {
+            Bi[i] = bi + eta * (z - P.lambda_b * bi);
+            Bi[j] = bj + eta * (-z - P.lambda_b * bj);
+        }
+    }
+    if (loss_sum) {
+        lacc = hm::wave_sum(lacc);
+        if (lane == 0 && lacc != 0.0) atomicAdd(loss_sum, lacc);
+    }
+}
+
+MFParams unpack(const int32_t* ip, const float* hp) {
+    MFParams P;
+    P.k = ip[0]; P.kp = ip[1]; P.n_users = ip[2]; P.n_items = ip[3]; P.adagrad = ip[4];
+    P.use_bias = ip[5]; P.update_mean = ip[6]; P.eta_kind = ip[7]; P.loss = ip[8];
+    P.seed = (uint32_t)ip[9]; P.max_tries = ip[10] > 0 ? ip[10] : 16;
+    P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda_u = hp[3];
+    P.lambda_i = hp[4]; P.lambda_j = hp[5]; P.lambda_b = hp[6]; P.eps = hp[7];
+    return P;
+}
+
+int grid_for(int64_t n, int per) {
+    int64_t waves = (n + per - 1) / per;
+    int64_t blocks = (waves + 3) / 4;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    return blocks < 1 ? 1 : (int)blocks;
+}
+
+}  // namespace
+
+// ip: k, kp, n_users, n_items, adagrad, use_bias, update_mean, eta_kind, loss, seed, max_tries
+// hp: eta0, power_t, total_steps, lambda_u, lambda_i, lambda_j, lambda_b, eps
+HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
+                      const int32_t* items, const float* ratings, int64_t n, int64_t t0, float* Pu,
+                      float* Qi, float* Bu, float* Bi, float* mu, float* GPu, float* GQi,
+                      float* GBu, float* GBi, int train, float* pred, float* loss,
+                      hipStream_t stream) {
+    const MFParams P = unpack(ip, hp);
+    if (n <= 0) return 0;
+    if (P.k <= 0 || P.k > 64 || P.kp < P.k) return (int)hipErrorInvalidValue;
+    if (P.adagrad && (!GPu || !GQi || !GBu || !GBi)) return (int)hipErrorInvalidValue;
+#define HM_MF(GG)                                                                                  \
+    hipLaunchKernelGGL((mf_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, users,  \
+                       items, ratings, n, t0, Pu, Qi, Bu, Bi, mu, GPu, GQi, GBu, GBi, train, pred,   \
+                       loss)
+    if (P.k <= 8) HM_MF(8);
+    else if (P.k <= 16) HM_MF(16);
+    else if (P.k <= 32) HM_MF(32);
+    else HM_MF(64);
+#undef HM_MF
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, const int32_t* ti,
+                       const int32_t* tj, int64_t n, const int64_t* uptr, const int32_t* uitems,
+                       const int32_t* pos_user, int64_t n_pos, int64_t t0, float* Pu, float* Qi,
+                       float* Bi, double* loss_sum, hipStream_t stream) {
+    const MFParams P = unpack(ip, hp);
+    if (n <= 0) return 0;
+    if (P.k <= 0 || P.k > 64 || P.kp < P.k) return (int)hipErrorInvalidValue;
+    if (!tu && (!uptr || !uitems || !pos_user || n_pos <= 0)) return (int)hipErrorInvalidValue;
+#define HM_BPR(GG)                                                                                 \
+    hipLaunchKernelGGL((bpr_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, tu,    \
+                       ti, tj, n, uptr, uitems, pos_user, n_pos, t0, Pu, Qi, Bi, loss_sum)
+    if (P.k <= 8) HM_BPR(8);
+    else if (P.k <= 16) HM_BPR(16);
+    else if (P.k <= 32) HM_BPR(32);
+    else HM_BPR(64);
+#undef HM_BPR
+    HM_LAUNCH_RET();
+}

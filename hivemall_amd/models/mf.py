@@ -1,0 +1,406 @@
+"""Matrix factorization: ``train_mf_sgd``, ``train_mf_adagrad`` (biased MF), ``train_bprmf``
+(BPR-MF, Rendle UAI'09) and the predictors ``mf_predict`` / ``bprmf_predict``.
+
+Reference behaviour: Hivemall OnlineMatrixFactorizationUDTF, MatrixFactorizationSGDUDTF,
+MatrixFactorizationAdaGradUDTF, BPRMatrixFactorizationUDTF, MFPredictionUDF,
+BPRMFPredictionUDF, FactorizedModel (upstream core/src/main/java/hivemall/mf/; SURVEY.md
+§2.3.5, K7/K8, O7).
+
+MI355X design: P [n_users, kp] and Q [n_items, kp] fp32 tables in HBM; the kernels in
+``csrc/kernels/mf.hip`` pack 64/next_pow2(k) ratings per wave64 and update Hogwild.  BPR can
+sample its negatives on the device (user->items CSR + counter-based RNG), so an epoch is one
+launch with no host round trip.  Bulk scoring (``recommend_topk``) is a bf16 GEMM on the
+matrix cores (torch.matmul -> hipBLASLt) + ``torch.topk``.
+
+Model tables (pinned, docs/compat.md O7):
+  MF : (idx int, Pu array<float>, Qi array<float>, Bu float, Bi float, mu float)
+  BPR: (idx int, Pu array<float>, Qi array<float>, Bi float)
+one row per index that is a user and/or an item (NULL where it is not).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pandas as pd
+import torch
+
+from .. import _native
+from ..registry import udf
+from ..utils.options import UDFArgumentException, flag, opt
+from .base import ConversionState, Learner, log
+
+_ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2, "bolddriver": 0, "bold_driver": 0}
+
+MF_OPTS = [
+    opt("factors", "factor", 10, int, "Number of latent factors", aliases=("k",)),
+    opt("lambda", None, 0.03, float, "Regularization"),
+    opt("mu", "mean_rating", 0.0, float, "Mean rating (initial)"),
+    flag("update_mean", "update_mu", "Update the mean rating from the data"),
+    opt("rankinit", None, "random", str, "Init: random | gaussian"),
+    opt("maxval", "max_init_value", 1.0, float, "Max value for random init"),
+    opt("min_init_stddev", None, 0.1, float, "Stddev for gaussian init"),
+    opt("iters", "iterations", 1, int, "Iterations", aliases=("iter",)),
+    opt("eta0", None, 0.1, float, "Initial learning rate"),
+    opt("eta", None, "fixed", str, "Learning rate scheme: fixed, simple, inverse"),
+    opt("power_t", None, 0.1, float, "Inverse scaling exponent"),
+    opt("t", "total_steps", -1.0, float, "Total steps for -eta simple"),
+    opt("eps", None, 1.0, float, "AdaGrad denominator constant"),
+    opt("scale", None, 100.0, float, "Scaling factor (accepted)"),
+    flag("disable_bias", "no_bias", "Do not learn user/item biases"),
+    opt("cv_rate", "convergence_rate", 0.005, float, "Convergence threshold"),
+    flag("disable_cv", "disable_cvtest", "Disable convergence check"),
+    opt("seed", None, -1, int, "Seed"),
+    opt("grid", None, 0, int, "[engine] kernel grid override"),
+]
+
+BPR_OPTS = [
+    opt("factors", "factor", 10, int, "Number of latent factors", aliases=("k",)),
+    opt("loss", "loss_function", "lnLogistic", str, "lnLogistic | logistic | sigmoid"),
+    opt("iters", "iterations", 30, int, "Iterations", aliases=("iter",)),
+    opt("reg", "lambda", 0.0001, float, "Default regularization"),
+    opt("reg_u", None, None, float, "Regularization of user factors"),
+    opt("reg_i", None, None, float, "Regularization of positive item factors"),
+    opt("reg_j", None, None, float, "Regularization of negative item factors"),
+    opt("reg_bias", None, 0.01, float, "Regularization of item biases"),
+    opt("eta0", None, 0.005, float, "Initial learning rate"),
+    opt("eta", None, "fixed", str, "Learning rate scheme: fixed, simple, inverse, bolddriver"),
+    opt("power_t", None, 0.1, float, "Inverse scaling exponent"),
+    opt("t", "total_steps", -1.0, float, "Total steps"),
+    opt("init", None, "random", str, "Init: random | gaussian"),
+    opt("maxval", "max_init_value", 1.0, float, "Max value for random init"),
+    opt("min_init_stddev", None, 0.1, float, "Stddev for gaussian init"),
+    flag("no_bias", "disable_bias", "Do not learn item biases"),
+    opt("cv_rate", "convergence_rate", 0.005, float, "Convergence threshold"),
+    flag("disable_cv", "disable_cvtest", "Disable convergence check"),
+    opt("seed", None, -1, int, "Seed"),
+    opt("samples_per_epoch", None, 0, int, "[engine] device-sampled triples per epoch (0 = #positives)"),
+    opt("grid", None, 0, int, "[engine] kernel grid override"),
+]
+_BPR_LOSS = {"lnlogistic": 0, "logistic": 1, "sigmoid": 2}
+
+
+def _init_factors(n, k, kp, scheme, maxval, stddev, gen) -> torch.Tensor:
+    T = torch.zeros(n, kp)
+    if scheme == "gaussian":
+        T[:, :k] = torch.randn(n, k, generator=gen) * stddev
+    else:
+        T[:, :k] = torch.rand(n, k, generator=gen) * (maxval / k)
+    return T
+
+
+class _MFBase(Learner):
+    def _factors(self):
+        k = int(self.cl["factors"])
+        if not 0 < k <= 64:
+            raise UDFArgumentException(f"{self.NAME}: -factors must be in [1, 64]")
+        return k
+
+    def _ip(self, loss=0, max_tries=16):
+        c = self.cl
+        eta = str(c["eta"]).lower()
+        if eta not in _ETAS:
+            raise UDFArgumentException(f"{self.NAME}: unknown -eta {eta}")
+        return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
+                         int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries],
+                        dtype=np.int32)
+
+
+class MatrixFactorization(_MFBase):
+    """Biased MF with SGD (``train_mf_sgd``) or AdaGrad (``train_mf_adagrad``)."""
+    NAME = "train_mf_sgd"
+    OPTIONS = MF_OPTS
+    ADAGRAD = False
+
+    def __init__(self, options=None, device=None, **kw):
+        super().__init__(options, device, **kw)
+        self.k = self._factors()
+        self.kp = self.k
+        self.adagrad = self.ADAGRAD
+        self.use_bias = not self.cl["disable_bias"]
+        self.state = None
+        self.t = 0
+        self.cv = ConversionState(not self.cl["disable_cv"], self.cl["cv_rate"])
+
+    def init_state(self, n_users, n_items):
+        self.n_users, self.n_items = int(n_users), int(n_items)
+        g = torch.Generator().manual_seed(self.seed)
+        c = self.cl
+        dev = self.device
+        P = _init_factors(self.n_users, self.k, self.kp, c["rankinit"], c["maxval"], c["min_init_stddev"], g)
+        Q = _init_factors(self.n_items, self.k, self.kp, c["rankinit"], c["maxval"], c["min_init_stddev"], g)
+        st = dict(P=P.to(dev), Q=Q.to(dev), Bu=torch.zeros(self.n_users, device=dev),
+                  Bi=torch.zeros(self.n_items, device=dev),
+                  mu=torch.tensor([float(c["mu"])], device=dev))
+        if self.adagrad:
+            st.update(GP=torch.zeros_like(st["P"]), GQ=torch.zeros_like(st["Q"]),
+                      GBu=torch.zeros_like(st["Bu"]), GBi=torch.zeros_like(st["Bi"]))
+        self.state = st
+        self.seen_u = torch.zeros(self.n_users, dtype=torch.bool, device=dev)
+        self.seen_i = torch.zeros(self.n_items, dtype=torch.bool, device=dev)
+
+    def _hp(self):
+        c = self.cl
+        lam = float(c["lambda"])
+        return np.array([c["eta0"], c["power_t"], c["t"], lam, lam, lam, lam, c["eps"]], dtype=np.float32)
+
+    def _step(self, u, i, r, train=True, pred=None, loss=None):
+        st = self.state
+        p = _native.ptr
+        ip, hp = self._ip(), self._hp()
+        n = u.numel()
+        args = [ip.ctypes.data, hp.ctypes.data, p(u), p(i), p(r), C.c_int64(n), C.c_int64(self.t),
+                p(st["P"]), p(st["Q"]), p(st["Bu"]), p(st["Bi"]), p(st["mu"]), p(st.get("GP")),
+                p(st.get("GQ")), p(st.get("GBu")), p(st.get("GBi")), int(train), p(pred), p(loss)]
+        if u.is_cuda:
+            _native.check(_native.hip().hm_mf_step(*args, _native.stream_of(u.device)), "hm_mf_step")
+        else:
+            _native.host().hm_mf_step_cpu(*args)
+        if train:
+            self.t += n
+
+    def fit(self, users, items, ratings) -> "MatrixFactorization":
+        dev = self.device
+        u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev)
+        i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev)
+        r = torch.as_tensor(np.asarray(ratings, dtype=np.float32)).to(dev)
+        if self.state is None:
+            self.init_state(int(u.max().item()) + 1, int(i.max().item()) + 1)
+            if self.cl["update_mean"]:
+                self.state["mu"].fill_(float(r.mean().item()))
+        self.seen_u[u.long()] = True
+        self.seen_i[i.long()] = True
+        loss = torch.empty(u.numel(), device=dev)
+        for ep in range(int(self.cl["iters"])):
+            self._step(u, i, r, loss=loss)
+            self.cv.incr_loss(float(loss.double().sum().item()))
+            if self.cv.is_converged():
+                log.info("%s converged at epoch %d", self.NAME, ep + 1)
+                break
+        return self
+
+    def predict(self, users, items) -> np.ndarray:
+        dev = self.device
+        u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev)
+        i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev)
+        out = torch.empty(u.numel(), device=dev)
+        self._step(u, i, torch.zeros(u.numel(), device=dev), train=False, pred=out)
+        return out.cpu().numpy()
+
+    def model_table(self) -> pd.DataFrame:
+        st = self.state
+        n = max(self.n_users, self.n_items)
+        su = self.seen_u.cpu().numpy()
+        si = self.seen_i.cpu().numpy()
+        P = st["P"][:, : self.k].cpu().numpy()
+        Q = st["Q"][:, : self.k].cpu().numpy()
+        Bu = st["Bu"].cpu().numpy()
+        Bi = st["Bi"].cpu().numpy()
+        mu = float(st["mu"][0].item())
+        rows = []
+        for idx in range(n):
+            iu = idx < self.n_users and su[idx]
+            ii = idx < self.n_items and si[idx]
+            if not (iu or ii):
+                continue
+            rows.append((idx, P[idx] if iu else None, Q[idx] if ii else None,
+                         float(Bu[idx]) if iu else None, float(Bi[idx]) if ii else None, mu))
+        return pd.DataFrame(rows, columns=["idx", "Pu", "Qi", "Bu", "Bi", "mu"])
+
+
+class MatrixFactorizationAdaGrad(MatrixFactorization):
+    NAME = "train_mf_adagrad"
+    ADAGRAD = True
+
+
+class BPRMF(_MFBase):
+    """BPR-MF.  Input triples (user, pos_item, neg_item) as produced by ``bpr_sampling``, or
+    (``fit_implicit``) the positive pairs only, with negatives sampled on the device."""
+    NAME = "train_bprmf"
+    OPTIONS = BPR_OPTS
+
+    def __init__(self, options=None, device=None, **kw):
+        super().__init__(options, device, **kw)
+        c = self.cl
+        self.k = self._factors()
+        self.kp = self.k
+        self.adagrad = False
+        self.use_bias = not c["no_bias"]
+        loss = str(c["loss"]).lower()
+        if loss not in _BPR_LOSS:
+            raise UDFArgumentException(f"train_bprmf: unknown -loss {c['loss']}")
+        self.loss_id = _BPR_LOSS[loss]
+        self.state = None
+        self.t = 0
+        self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
+        self.grid = int(c["grid"])
+
+    def init_state(self, n_users, n_items):
+        self.n_users, self.n_items = int(n_users), int(n_items)
+        g = torch.Generator().manual_seed(self.seed)
+        c = self.cl
+        dev = self.device
+        self.state = dict(
+            P=_init_factors(self.n_users, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g).to(dev),
+            Q=_init_factors(self.n_items, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g).to(dev),
+            Bi=torch.zeros(self.n_items, device=dev))
+        self.seen_u = torch.zeros(self.n_users, dtype=torch.bool, device=dev)
+        self.seen_i = torch.zeros(self.n_items, dtype=torch.bool, device=dev)
+
+    def _hp(self):
+        c = self.cl
+        reg = float(c["reg"])
+        ru = c["reg_u"] if c["reg_u"] is not None else reg
+        ri = c["reg_i"] if c["reg_i"] is not None else reg
+        rj = c["reg_j"] if c["reg_j"] is not None else reg
+        return np.array([c["eta0"], c["power_t"], c["t"], ru, ri, rj, c["reg_bias"], 1.0], dtype=np.float32)
+
+    def step(self, tu=None, ti=None, tj=None, n=None, csr=None) -> float:
+        """One launch over explicit triples, or ``n`` device-sampled triples from ``csr``."""
+        st = self.state
+        p = _native.ptr
+        ip, hp = self._ip(loss=self.loss_id), self._hp()
+        dev = st["P"].device
+        loss = torch.zeros(1, dtype=torch.float64, device=dev)
+        if tu is not None:
+            n = tu.numel()
+            uptr = uit = pu = None
+            npos = 0
+        else:
+            uptr, uit, pu = csr
+            npos = uit.numel()
+        args = [ip.ctypes.data, hp.ctypes.data, p(tu), p(ti), p(tj), C.c_int64(n), p(uptr), p(uit),
+                p(pu), C.c_int64(npos), C.c_int64(self.t), p(st["P"]), p(st["Q"]), p(st["Bi"]), p(loss)]
+        if dev.type == "cuda":
+            _native.check(_native.hip().hm_bpr_step(*args, _native.stream_of(dev)), "hm_bpr_step")
+        else:
+            _native.host().hm_bpr_step_cpu(*args)
+        self.t += n
+        return float(loss.item())
+
+    def fit(self, users, pos_items, neg_items) -> "BPRMF":
+        dev = self.device
+        tu = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev)
+        ti = torch.as_tensor(np.asarray(pos_items, dtype=np.int32)).to(dev)
+        tj = torch.as_tensor(np.asarray(neg_items, dtype=np.int32)).to(dev)
+        if self.state is None:
+            self.init_state(int(tu.max().item()) + 1, int(max(ti.max().item(), tj.max().item())) + 1)
+        self.seen_u[tu.long()] = True
+        self.seen_i[ti.long()] = True
+        self.seen_i[tj.long()] = True
+        for ep in range(int(self.cl["iters"])):
+            self.cv.incr_loss(self.step(tu, ti, tj))
+            if self.cv.is_converged():
+                break
+        return self
+
+    @staticmethod
+    def build_csr(users: torch.Tensor, items: torch.Tensor, n_users: int):
+        """Positive pairs -> (user ptr int64, items sorted per user int32, user of each pair)."""
+        key = users.long() * (1 << 32) + items.long()
+        key = torch.unique(key)
+        u = (key >> 32).to(torch.int32)
+        it = (key & 0xFFFFFFFF).to(torch.int32)
+        counts = torch.bincount(u.long(), minlength=n_users)
+        ptr = torch.zeros(n_users + 1, dtype=torch.int64, device=users.device)
+        ptr[1:] = torch.cumsum(counts, 0)
+        return ptr.contiguous(), it.contiguous(), u.contiguous()
+
+    def fit_implicit(self, users, items, n_users=None, n_items=None, epochs=None) -> "BPRMF":
+        """Train from positive (user, item) pairs; negatives are sampled on the device."""
+        dev = self.device
+        u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev) if not torch.is_tensor(users) else users.to(dev)
+        i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev) if not torch.is_tensor(items) else items.to(dev)
+        if self.state is None:
+            self.init_state(n_users or int(u.max().item()) + 1, n_items or int(i.max().item()) + 1)
+        csr = self.build_csr(u, i, self.n_users)
+        self.seen_u[u.long()] = True
+        self.seen_i.fill_(True)
+        per = int(self.cl["samples_per_epoch"]) or csr[1].numel()
+        for ep in range(int(epochs or self.cl["iters"])):
+            self.cv.incr_loss(self.step(n=per, csr=csr))
+            if self.cv.is_converged():
+                break
+        return self
+
+    def scores(self, users=None) -> torch.Tensor:
+        st = self.state
+        U = st["P"] if users is None else st["P"][torch.as_tensor(users, device=st["P"].device).long()]
+        dt = torch.bfloat16 if U.is_cuda else torch.float32
+        return (U.to(dt) @ st["Q"].to(dt).T).float() + st["Bi"][None, :]
+
+    def recommend_topk(self, users=None, k: int = 10, exclude: tuple | None = None):
+        """Top-k items per user: bf16 GEMM on the matrix cores + topk (seen items masked)."""
+        S = self.scores(users)
+        if exclude is not None:
+            eu, ei = exclude
+            S[torch.as_tensor(eu, device=S.device).long(), torch.as_tensor(ei, device=S.device).long()] = -float("inf")
+        return torch.topk(S, k, dim=1)
+
+    def model_table(self) -> pd.DataFrame:
+        st = self.state
+        su, si = self.seen_u.cpu().numpy(), self.seen_i.cpu().numpy()
+        P = st["P"][:, : self.k].cpu().numpy()
+        Q = st["Q"][:, : self.k].cpu().numpy()
+        Bi = st["Bi"].cpu().numpy()
+        rows = []
+        for idx in range(max(self.n_users, self.n_items)):
+            iu = idx < self.n_users and su[idx]
+            ii = idx < self.n_items and si[idx]
+            if iu or ii:
+                rows.append((idx, P[idx] if iu else None, Q[idx] if ii else None,
+                             float(Bi[idx]) if ii else None))
+        return pd.DataFrame(rows, columns=["idx", "Pu", "Qi", "Bi"])
+
+
+def auc_implicit(model: BPRMF, test_users, test_items, train_csr=None, n_neg: int = 100, seed: int = 0) -> float:
+    """Sampled AUC: P(score(u, i_test) > score(u, j)) over random negatives j."""
+    dev = model.state["P"].device
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    u = torch.as_tensor(np.asarray(test_users), dtype=torch.long)
+    i = torch.as_tensor(np.asarray(test_items), dtype=torch.long)
+    j = torch.randint(0, model.n_items, (u.numel(), n_neg), generator=g)
+    P, Q, B = model.state["P"], model.state["Q"], model.state["Bi"]
+    u, i, j = u.to(dev), i.to(dev), j.to(dev)
+    si = (P[u] * Q[i]).sum(1) + B[i]
+    sj = (P[u][:, None, :] * Q[j]).sum(2) + B[j]
+    return float((si[:, None] > sj).float().mean().item())
+
+
+@udf("mf_predict")
+def mf_predict(Pu, Qi, Bu=None, Bi=None, mu=None):
+    """μ + b_u + b_i + p_u·q_i (NULL factors -> 0)."""
+    s = 0.0
+    if Pu is not None and Qi is not None:
+        s = float(np.dot(np.asarray(Pu, dtype=np.float64), np.asarray(Qi, dtype=np.float64)))
+    for b in (Bu, Bi, mu):
+        if b is not None and not (isinstance(b, float) and np.isnan(b)):
+            s += float(b)
+    return s
+
+
+@udf("bprmf_predict")
+def bprmf_predict(Pu, Qi, Bi=None):
+    s = 0.0
+    if Pu is not None and Qi is not None:
+        s = float(np.dot(np.asarray(Pu, dtype=np.float64), np.asarray(Qi, dtype=np.float64)))
+    if Bi is not None and not (isinstance(Bi, float) and np.isnan(Bi)):
+        s += float(Bi)
+    return s
+
+
+def register_sql(reg):
+    reg("train_mf_sgd", lambda: MatrixFactorization, n_data_args=3)
+    reg("train_mf_adagrad", lambda: MatrixFactorizationAdaGrad, n_data_args=3)
+    reg("train_bprmf", lambda: BPRMF, n_data_args=3)
+
+
+_P = _native.c_p
+_native.register_hip("hm_mf_step", [_P, _P, _P, _P, _P, _native.c_i64, _native.c_i64] + [_P] * 9 +
+                     [C.c_int, _P, _P, _P])
+_native.register_host("hm_mf_step_cpu", [_P, _P, _P, _P, _P, _native.c_i64, _native.c_i64] + [_P] * 9 +
+                      [C.c_int, _P, _P])
+_native.register_hip("hm_bpr_step", [_P, _P, _P, _P, _P, _native.c_i64, _P, _P, _P, _native.c_i64,
+                                     _native.c_i64, _P, _P, _P, _P, _P])
+_native.register_host("hm_bpr_step_cpu", [_P, _P, _P, _P, _P, _native.c_i64, _P, _P, _P, _native.c_i64,
+                                          _native.c_i64, _P, _P, _P, _P])

@@ -1,0 +1,133 @@
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from hivemall_amd.io.synthetic import movielens_like
+from hivemall_amd.models.mf import (BPRMF, MatrixFactorization, MatrixFactorizationAdaGrad,
+                                    auc_implicit, bprmf_predict, mf_predict)
+from hivemall_amd.sql import Session
+
+
+def _ratings(n=40000, nu=500, ni=300, k=5, seed=0):
+    rng = np.random.default_rng(seed)
+    P = rng.normal(0, 1, (nu, k))
+    Q = rng.normal(0, 1, (ni, k))
+    u = rng.integers(0, nu, n)
+    i = rng.integers(0, ni, n)
+    r = (P[u] * Q[i]).sum(1) + 3 + rng.normal(0, 0.1, n)
+    return u, i, r.astype(np.float32)
+
+
+def _oracle_sgd(u, i, r, P, Q, mu, eta, lam):
+    P, Q = P.astype(np.float64).copy(), Q.astype(np.float64).copy()
+    Bu, Bi = np.zeros(P.shape[0]), np.zeros(Q.shape[0])
+    for a, b, x in zip(u, i, r):
+        e = x - (mu + Bu[a] + Bi[b] + P[a] @ Q[b])
+        pa = P[a].copy()
+        P[a] += eta * (e * Q[b] - lam * P[a])
+        Q[b] += eta * (e * pa - lam * Q[b])
+        Bu[a] += eta * (e - lam * Bu[a])
+        Bi[b] += eta * (e - lam * Bi[b])
+    return P, Q, Bu, Bi
+
+
+def test_mf_sgd_matches_oracle():
+    u, i, r = _ratings(2000)
+    m = MatrixFactorization("-factors 4 -iters 1 -eta0 0.01 -mu 3", device="cpu")
+    m.init_state(500, 300)
+    P0, Q0 = m.state["P"].numpy().copy(), m.state["Q"].numpy().copy()
+    m.fit(u, i, r)
+    P, Q, Bu, Bi = _oracle_sgd(u, i, r, P0, Q0, 3.0, 0.01, 0.03)
+    np.testing.assert_allclose(m.state["P"].numpy(), P, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(m.state["Bi"].numpy(), Bi, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("cls,opts", [(MatrixFactorization, "-eta0 0.01"), (MatrixFactorizationAdaGrad, "-eta0 0.1")])
+def test_mf_learns(cls, opts):
+    u, i, r = _ratings()
+    m = cls(f"-factors 10 -iters 20 -update_mean {opts}", device="cpu").fit(u[:35000], i[:35000], r[:35000])
+    pr = m.predict(u[35000:], i[35000:])
+    assert np.sqrt(((pr - r[35000:]) ** 2).mean()) < 0.3 * r.std()
+    tab = m.model_table()
+    assert list(tab.columns) == ["idx", "Pu", "Qi", "Bu", "Bi", "mu"]
+    row = tab.iloc[3]
+    assert mf_predict(row.Pu, row.Qi, row.Bu, row.Bi, row.mu) == pytest.approx(
+        m.predict([row.idx], [row.idx])[0], rel=1e-4, abs=1e-4)
+
+
+def test_bprmf_triples_and_device_sampling_cpu():
+    us, its = movielens_like(100000, 1000, 500, k=8)
+    m = BPRMF("-factors 16 -iters 10 -eta0 0.05", device="cpu").fit_implicit(us[:95000], its[:95000], 1000, 500)
+    assert auc_implicit(m, us[95000:].numpy(), its[95000:].numpy()) > 0.65
+    rng = np.random.default_rng(0)
+    u = us[:20000].numpy()
+    i = its[:20000].numpy()
+    j = rng.integers(0, 500, 20000)
+    m2 = BPRMF("-factors 8 -iters 3", device="cpu").fit(u, i, j)
+    tab = m2.model_table()
+    assert list(tab.columns) == ["idx", "Pu", "Qi", "Bi"]
+    s, ix = m2.recommend_topk([0, 1], k=5)
+    assert ix.shape == (2, 5)
+    r = tab.iloc[0]
+    assert isinstance(bprmf_predict(r.Pu, r.Qi, r.Bi), float)
+
+
+def test_mf_sql():
+    u, i, r = _ratings(5000)
+    s = Session(device="cpu")
+    s.register("ratings", pd.DataFrame({"userid": u, "itemid": i, "rating": r}))
+    s.sql("CREATE TABLE mf AS SELECT train_mf_sgd(userid, itemid, rating, '-factors 5 -iters 5 -eta0 0.01') "
+          "AS (idx, Pu, Qi, Bu, Bi, mu) FROM ratings")
+    p = s.sql("""SELECT t.rating, mf_predict(p.Pu, q.Qi, p.Bu, q.Bi, p.mu) AS pred FROM ratings t
+                 JOIN mf p ON (t.userid = p.idx) JOIN mf q ON (t.itemid = q.idx)""")
+    assert len(p) == 5000 and np.isfinite(p["pred"].astype(float)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls,opts", [(MatrixFactorization, "-eta0 0.01"), (MatrixFactorizationAdaGrad, "-eta0 0.1")])
+def test_mf_gpu_matches_cpu_on_disjoint_pairs(cls, opts):
+    n = 300
+    u = np.arange(n)
+    i = np.arange(n)
+    r = np.random.default_rng(1).normal(3, 1, n).astype(np.float32)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = cls(f"-factors 10 -iters 1 {opts}", device=dev).fit(u, i, r)
+        res[dev] = {k: v.cpu() for k, v in m.state.items()}
+    for k in ("P", "Q", "Bu", "Bi"):
+        np.testing.assert_allclose(res["cuda"][k].numpy(), res["cpu"][k].numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_mf_gpu_quality():
+    u, i, r = _ratings()
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = MatrixFactorization("-factors 10 -iters 20 -eta0 0.01 -update_mean", device=dev).fit(
+            u[:35000], i[:35000], r[:35000])
+        pr = m.predict(u[35000:], i[35000:])
+        res[dev] = float(np.sqrt(((pr - r[35000:]) ** 2).mean()))
+    assert res["cuda"] < res["cpu"] * 1.5 + 0.05, res
+
+
+@pytest.mark.gpu
+def test_bpr_gpu_explicit_triples_match_cpu():
+    n = 200
+    u, i, j = np.arange(n), np.arange(n), np.arange(n, 2 * n)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = BPRMF("-factors 16 -iters 1 -eta0 0.05", device=dev).fit(u, i, j)
+        res[dev] = {k: v.cpu() for k, v in m.state.items()}
+    for k in ("P", "Q", "Bi"):
+        np.testing.assert_allclose(res["cuda"][k].numpy(), res["cpu"][k].numpy(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_bpr_gpu_device_sampling_quality():
+    us, its = movielens_like(400000, 5000, 2000, k=8)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = BPRMF("-factors 32 -iters 10 -eta0 0.05", device=dev).fit_implicit(us[:380000], its[:380000], 5000, 2000)
+        res[dev] = auc_implicit(m, us[380000:].numpy(), its[380000:].numpy())
+    assert res["cuda"] > res["cpu"] - 0.03, res
