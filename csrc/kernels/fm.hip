@@ -125,6 +125,11 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
     const int lane = hm::lane_id();
     const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    // w0 is touched by every row: each wave keeps its pending w0 delta in a register and
+    // publishes it every 64 rows (one atomic per 64 rows instead of one per row; a single
+    // contended address would otherwise serialise the whole chip).
+    float w0_pending = 0.f;
+    int w0_rows = 0;
     for (int64_t row = gw; row < n_rows; row += nw) {
         const int64_t s = indptr[row], e = indptr[row + 1];
         const int nnz = (int)(e - s);
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             pair += S[f] * S[f];
         }
         float p = lin + 0.5f * (pair - sq);
-        if (P.use_w0) p += *w0;
+        if (P.use_w0) p += *w0 + w0_pending;
         const float yy = y ? y[row] : 0.f;
         float d;
         if (P.classification) {
@@ -214,15 +219,27 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             t.load(V, i);
             upd(t, i, x, w[i]);
         }
-        if (P.use_w0 && lane == 0) atomicAdd(w0, -eta * (d + 2.f * P.lambda0 * *w0));
+        if (P.use_w0) {
+            w0_pending -= eta * (d + 2.f * P.lambda0 * (*w0 + w0_pending));
+            if (++w0_rows == 64) {
+                if (lane == 0) atomicAdd(w0, w0_pending);
+                w0_pending = 0.f;
+                w0_rows = 0;
+            }
+        }
     }
+    if (P.use_w0 && lane == 0 && w0_pending != 0.f) atomicAdd(w0, w0_pending);
 }
 
 template <int KP, bool BF16>
 int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const float* val,
            const float* y, int64_t n, int64_t t0, float* w, void* V, float* w0, float* pred,
            float* loss, int grid, hipStream_t st) {
-    int64_t blocks = grid > 0 ? grid : (n + 3) / 4;
+    // Default: 64 blocks x 4 waves.  Measured on MI355X (profiles/fm_sweep_r1.log): more
+    // concurrent rows only add Hogwild contention on the hot Criteo features (slower AND a
+    // worse logloss); 256 waves already saturate the memory pipes for FM-sized rows.
+    int64_t blocks = grid > 0 ? grid : 64;
+    if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,

@@ -220,7 +220,13 @@ MFParams unpack(const int32_t* ip, const float* hp) {
     return P;
 }
 
+int g_grid_override = 0;
+
 int grid_for(int64_t n, int per) {
+    if (g_grid_override > 0) {
+        const int64_t need = ((n + per - 1) / per + 3) / 4;
+        return (int)(g_grid_override < need ? g_grid_override : (need < 1 ? 1 : need));
+    }
     int64_t waves = (n + per - 1) / per;
     int64_t blocks = (waves + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
@@ -237,6 +243,7 @@ HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
                       float* GBu, float* GBi, int train, float* pred, float* loss,
                       hipStream_t stream) {
     const MFParams P = unpack(ip, hp);
+    g_grid_override = ip[11];  // concurrency cap chosen by the host (Hogwild contention policy)
     if (n <= 0) return 0;
     if (P.k <= 0 || P.k > 64 || P.kp < P.k) return (int)hipErrorInvalidValue;
     if (P.adagrad && (!GPu || !GQi || !GBu || !GBi)) return (int)hipErrorInvalidValue;
@@ -257,6 +264,7 @@ HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, co
                        const int32_t* pos_user, int64_t n_pos, int64_t t0, float* Pu, float* Qi,
                        float* Bi, double* loss_sum, hipStream_t stream) {
     const MFParams P = unpack(ip, hp);
+    g_grid_override = ip[11];  // concurrency cap chosen by the host (Hogwild contention policy)
     if (n <= 0) return 0;
     if (P.k <= 0 || P.k > 64 || P.kp < P.k) return (int)hipErrorInvalidValue;
     if (!tu && (!uptr || !uitems || !pos_user || n_pos <= 0)) return (int)hipErrorInvalidValue;

@@ -102,8 +102,17 @@ class _MFBase(Learner):
         if eta not in _ETAS:
             raise UDFArgumentException(f"{self.NAME}: unknown -eta {eta}")
         return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
-                         int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries],
-                        dtype=np.int32)
+                         int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
+                         self._grid()], dtype=np.int32)
+
+    def _grid(self) -> int:
+        """Hogwild concurrency cap: keep the number of ratings in flight well below the number
+        of distinct rows they update (plain SGD diverges when many stale gradients of one
+        popular item are summed).  ~1 block (4 waves) per 256 items/users, >= 1."""
+        g = int(self.cl["grid"])
+        if g > 0:
+            return g
+        return int(max(1, min(4096, min(self.n_users, self.n_items) // 256)))
 
 
 class MatrixFactorization(_MFBase):

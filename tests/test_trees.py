@@ -1,0 +1,117 @@
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+from sklearn.metrics import roc_auc_score
+
+from hivemall_amd.io.synthetic import higgs_like
+from hivemall_amd.models.trees import (GradientTreeBoostingClassifier, RandomForestClassifier,
+                                       RandomForestRegressor, Tree, decision_path, quantize,
+                                       rf_ensemble, tree_export, tree_predict)
+from hivemall_amd.sql import Session
+
+
+@pytest.fixture(scope="module")
+def higgs():
+    X, y = higgs_like(30000)
+    Xt, yt = higgs_like(6000, seed=9)
+    return X, y.long(), Xt, yt.long()
+
+
+def test_quantize_bins_monotone():
+    X = torch.randn(5000, 3)
+    q = quantize(X, 16)
+    assert q.bins.dtype == torch.uint8 and int(q.bins[:, :3].max()) <= 15
+    o = torch.argsort(X[:, 0])
+    assert (q.bins[o, 0].diff().to(torch.int64) >= 0).all()
+
+
+def test_random_forest_classifier(higgs):
+    X, y, Xt, yt = higgs
+    rf = RandomForestClassifier("-trees 10 -max_depth 10 -seed 3", device="cpu").fit(X, y)
+    auc = roc_auc_score(yt.numpy(), rf.predict_proba(Xt)[:, 1])
+    assert auc > 0.72
+    tab = rf.model_table()
+    assert list(tab.columns) == ["model_id", "model_weight", "model", "var_importance", "oob_errors", "oob_tests"]
+    assert (tab["oob_tests"] > 0).all()
+    r = tree_predict(tab.iloc[0]["model_id"], tab.iloc[0]["model"], Xt[0].tolist(), "-classification")
+    assert set(r) == {"value", "posteriori"}
+    assert "digraph" in tree_export(tab.iloc[0]["model"])
+    assert decision_path(tab.iloc[0]["model_id"], tab.iloc[0]["model"], Xt[0].tolist())[-1].startswith("value=")
+
+
+def test_gbt_matches_sklearn_quality(higgs):
+    from sklearn.ensemble import HistGradientBoostingClassifier
+    X, y, Xt, yt = higgs
+    gb = GradientTreeBoostingClassifier("-trees 40 -eta 0.1 -max_depth 6 -seed 3", device="cpu").fit(X, y)
+    auc = roc_auc_score(yt.numpy(), gb.predict_proba(Xt)[:, 1])
+    ref = HistGradientBoostingClassifier(max_iter=40, learning_rate=0.1, max_depth=6).fit(X.numpy(), y.numpy())
+    auc_ref = roc_auc_score(yt.numpy(), ref.predict_proba(Xt.numpy())[:, 1])
+    assert auc > auc_ref - 0.015, (auc, auc_ref)
+    tab = gb.model_table()
+    assert list(tab.columns) == ["iteration", "pred_models", "intercept", "shrinkage", "var_importance", "oob_error_rate"]
+
+
+def test_gbt_multiclass():
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(6000, 5)).astype(np.float32)
+    y = (X[:, 0] > 0).astype(int) + (X[:, 1] > 0.5).astype(int)
+    gb = GradientTreeBoostingClassifier("-trees 20 -eta 0.2 -max_depth 4", device="cpu").fit(X, y)
+    assert (gb.predict(X) == y).mean() > 0.9
+
+
+def test_rf_regressor():
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(8000, 4)).astype(np.float32)
+    y = 2 * X[:, 0] + np.sin(X[:, 1])
+    rr = RandomForestRegressor("-trees 10", device="cpu").fit(X, y)
+    assert np.sqrt(((rr.predict(X) - y) ** 2).mean()) < 0.5
+
+
+def test_tree_serialization_roundtrip():
+    t = Tree([0, -1, -1], [0.5, float("inf"), float("inf")], [1, -1, -1], [2, -1, -1],
+             [None, [1.0, 0.0], [0.0, 1.0]], 2)
+    t2 = Tree.deserialize(t.serialize())
+    assert t2.predict_one([0.2]) == [1.0, 0.0] and t2.predict_one([0.9]) == [0.0, 1.0]
+
+
+def test_rf_sql_pipeline(higgs):
+    X, y, Xt, yt = higgs
+    s = Session(device="cpu")
+    s.register("train", pd.DataFrame({"features": [list(map(float, r)) for r in X[:5000].tolist()],
+                                      "label": y[:5000].numpy()}))
+    s.register("test", pd.DataFrame({"rowid": range(500), "features": [list(map(float, r)) for r in Xt[:500].tolist()],
+                                     "label": yt[:500].numpy()}))
+    s.sql("CREATE TABLE rf AS SELECT train_randomforest_classifier(features, label, '-trees 5 -seed 71') "
+          "AS (model_id, model_weight, model, var_importance, oob_errors, oob_tests) FROM train")
+    p = s.sql("""
+    SELECT rowid, rf_ensemble(predicted.value, predicted.posteriori, model_weight) AS predicted FROM (
+      SELECT t.rowid, m.model_weight, tree_predict(m.model_id, m.model, t.features, '-classification') AS predicted
+      FROM rf m CROSS JOIN test t) x GROUP BY rowid""")
+    assert len(p) == 500
+    acc = np.mean([d["label"] == lab for d, lab in zip(p["predicted"], yt[:500].numpy()[p["rowid"].to_numpy()])])
+    assert acc > 0.6
+
+
+@pytest.mark.gpu
+def test_hist_kernel_matches_cpu(higgs):
+    X, y, _, _ = higgs
+    res = {}
+    for dev in ("cpu", "cuda"):
+        gb = GradientTreeBoostingClassifier("-trees 3 -eta 0.1 -max_depth 5 -subsample 1.0 -seed 3", device=dev).fit(X, y)
+        res[dev] = gb
+    a = res["cpu"].iters[0][0]
+    b = res["cuda"].iters[0][0]
+    assert a.feature == b.feature
+    np.testing.assert_allclose(res["cpu"].decision_function(X[:2000]), res["cuda"].decision_function(X[:2000]),
+                               rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_rf_gpu_quality(higgs):
+    X, y, Xt, yt = higgs
+    aucs = {}
+    for dev in ("cpu", "cuda"):
+        rf = RandomForestClassifier("-trees 10 -max_depth 10 -seed 3", device=dev).fit(X, y)
+        aucs[dev] = roc_auc_score(yt.numpy(), rf.predict_proba(Xt)[:, 1])
+    assert abs(aucs["cpu"] - aucs["cuda"]) < 0.01, aucs
