@@ -12,16 +12,20 @@
 //   w,w0 <- FTRL-proximal (alpha, beta, lambda1, lambda2) on g = kappa x
 //
 // Layout (MI355X-first):
-//   * V, G   : [num_features][num_fields][Kp] fp32, Kp = K rounded up to 4 so every field
-//              vector is a whole number of 16-B float4 chunks (padding stays exactly 0).
+//   * V, G   : [num_features][num_fields][Kp], Kp = K rounded up to 4 (padding stays 0).
+//              Stored fp32, or bf16 (BF = true, ``-bf16_state``) with stochastic rounding on
+//              every write: the kernel is HBM-bound (~95 KB of V/G traffic per Criteo row in
+//              fp32), so halving the state bytes is the throughput lever; stochastic rounding
+//              keeps the sub-ulp AdaGrad steps and G increments unbiased.
 //   * batch  : padded-ELL [B][F] (idx, fld, val), idx < 0 marks padding.
 //   * One 256-thread block per row (grid-stride over rows).  Ordered slot s = a*F + b owns
-//     the vector V[i_a, f_b]; consecutive threads read consecutive 16-B chunks of the same
-//     feature block, so every gather is fully coalesced.  The whole row's F*F*Kp slot
-//     vectors are staged in LDS (24 KB at F=39, K=4) so the partner read for the pair dot
-//     and for the gradient never goes back to L2.  6 blocks/CU fit in the 160 KB LDS.
+//     the vector V[i_a, f_b]; consecutive threads read consecutive slot vectors of the same
+//     feature block, so every gather is coalesced.  The row's F*F*Kp slot vectors are staged
+//     in LDS as fp32 (24 KB at F=39, K=4) so the partner read for the pair dot and for the
+//     gradient never goes back to L2.
 //   * Updates are Hogwild across rows (no atomics); each slot vector has a single writer
-//     within a row.  This is the GPU analogue of Hivemall's per-mapper online SGD.
+//     within a row.  ``reload`` re-reads the own slot right before its update (shorter
+//     read-modify-write window -> fewer lost updates on hot features).
 #include "common.h"
 
 namespace {
@@ -32,9 +36,8 @@ struct FFMParams {
     int classification;    // 1: logistic loss on y in {-1,+1}; 0: squared loss
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
-    int reload;            // re-read the own slot vector right before its update (shrinks the
-                           // Hogwild read-modify-write window -> far fewer lost updates on
-                           // hot features)
+    int reload;
+    uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
     float min_target, max_target;  // regression clipping of the prediction
@@ -60,11 +63,47 @@ __device__ __forceinline__ float ftrl_update(float* __restrict__ z, float* __res
     return ftrl_weight(z1, n1, alpha, beta, l1, l2);
 }
 
-template <int KC, bool STAGE>
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t bf16_sr(float f, uint32_t rnd) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7F800000u) == 0x7F800000u) return u >> 16;
+    return (u + (rnd & 0xFFFFu)) >> 16;
+}
+
+// 4-element chunk of a slot vector, at element offset `off` (a multiple of 4).
+template <bool BF>
+__device__ __forceinline__ float4 ld_chunk(const void* base, size_t off) {
+    if constexpr (BF) {
+        const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + off);
+        return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u));
+    } else {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + off);
+    }
+}
+
+template <bool BF>
+__device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint32_t rnd) {
+    if constexpr (BF) {
+        const uint32_t r2 = rnd * 0x9E3779B1u + 0x632BE5ABu;
+        const uint32_t lo = bf16_sr(v.x, rnd) | (bf16_sr(v.y, rnd >> 16) << 16);
+        const uint32_t hi = bf16_sr(v.z, r2) | (bf16_sr(v.w, r2 >> 16) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + off) = make_uint2(lo, hi);
+    } else {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + off) = v;
+    }
+}
+
+template <int KC, bool STAGE, bool BF>
 __global__ __launch_bounds__(256) void ffm_row_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y,
-    float* __restrict__ V, float* __restrict__ G,
+    void* __restrict__ V, void* __restrict__ G,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias,        // [4] = {w0, z0, n0, _}
     float* __restrict__ pred_out,    // [B] or null: raw score p
@@ -82,7 +121,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
 
     const int tid = threadIdx.x;
     const int Kp = P.Kp;
-    const size_t fstride = (size_t)P.num_fields * Kp;  // floats per feature block
+    const size_t fstride = (size_t)P.num_fields * Kp;  // elements per feature block
 
     for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
@@ -111,18 +150,11 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 const int ia = s_idx[a];
-                float4 v[KC];
-                if (a != b && ia >= 0 && s_idx[b] >= 0) {
-                    const float4* src = reinterpret_cast<const float4*>(
-                        V + (size_t)ia * fstride + (size_t)s_fld[b] * Kp);
+                const bool live = a != b && ia >= 0 && s_idx[b] >= 0;
+                const size_t off = live ? (size_t)ia * fstride + (size_t)s_fld[b] * Kp : 0;
 #pragma unroll
-                    for (int c = 0; c < KC; ++c) v[c] = src[c];
-                } else {
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-#pragma unroll
-                for (int c = 0; c < KC; ++c) s_v[s * KC + c] = v[c];
+                for (int c = 0; c < KC; ++c)
+                    s_v[s * KC + c] = live ? ld_chunk<BF>(V, off + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             __syncthreads();
         }
@@ -139,10 +171,10 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
 #pragma unroll
                 for (int c = 0; c < KC; ++c) { u[c] = s_v[s * KC + c]; v[c] = s_v[(b * F + a) * KC + c]; }
             } else {
-                const float4* pu = reinterpret_cast<const float4*>(V + (size_t)ia * fstride + (size_t)s_fld[b] * Kp);
-                const float4* pv = reinterpret_cast<const float4*>(V + (size_t)ib * fstride + (size_t)s_fld[a] * Kp);
+                const size_t ou = (size_t)ia * fstride + (size_t)s_fld[b] * Kp;
+                const size_t ov = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
 #pragma unroll
-                for (int c = 0; c < KC; ++c) { u[c] = pu[c]; v[c] = pv[c]; }
+                for (int c = 0; c < KC; ++c) { u[c] = ld_chunk<BF>(V, ou + 4 * c); v[c] = ld_chunk<BF>(V, ov + 4 * c); }
             }
             float d = 0.f;
 #pragma unroll
@@ -176,29 +208,27 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         // ---- 5. updates (Hogwild) ----
         if (P.train) {
             const float ks = kappa * scale * scale;
+            const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 if (a == b) continue;
                 const int ia = s_idx[a], ib = s_idx[b];
                 if (ia < 0 || ib < 0) continue;
                 const float coef = ks * s_x[a] * s_x[b];
-                float4* pv = reinterpret_cast<float4*>(V + (size_t)ia * fstride + (size_t)s_fld[b] * Kp);
-                float4* pg = reinterpret_cast<float4*>(G + (size_t)ia * fstride + (size_t)s_fld[b] * Kp);
+                const size_t ov = (size_t)ia * fstride + (size_t)s_fld[b] * Kp;
                 float4 own[KC], par[KC], gg[KC];
 #pragma unroll
-                for (int c = 0; c < KC; ++c) gg[c] = pg[c];
+                for (int c = 0; c < KC; ++c) gg[c] = ld_chunk<BF>(G, ov + 4 * c);
                 if (STAGE) {
-                    if (P.reload) {
 #pragma unroll
-                        for (int c = 0; c < KC; ++c) { own[c] = pv[c]; par[c] = s_v[(b * F + a) * KC + c]; }
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < KC; ++c) { own[c] = s_v[s * KC + c]; par[c] = s_v[(b * F + a) * KC + c]; }
+                    for (int c = 0; c < KC; ++c) {
+                        own[c] = P.reload ? ld_chunk<BF>(V, ov + 4 * c) : s_v[s * KC + c];
+                        par[c] = s_v[(b * F + a) * KC + c];
                     }
                 } else {
-                    const float4* pp = reinterpret_cast<const float4*>(V + (size_t)ib * fstride + (size_t)s_fld[a] * Kp);
+                    const size_t op = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
 #pragma unroll
-                    for (int c = 0; c < KC; ++c) { own[c] = pv[c]; par[c] = pp[c]; }
+                    for (int c = 0; c < KC; ++c) { own[c] = ld_chunk<BF>(V, ov + 4 * c); par[c] = ld_chunk<BF>(V, op + 4 * c); }
                 }
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
@@ -212,8 +242,9 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                     own[c].y -= P.eta0 * g.y * rsqrtf(gg[c].y + P.eps);
                     own[c].z -= P.eta0 * g.z * rsqrtf(gg[c].z + P.eps);
                     own[c].w -= P.eta0 * g.w * rsqrtf(gg[c].w + P.eps);
-                    pv[c] = own[c];
-                    pg[c] = gg[c];
+                    const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
+                    st_chunk<BF>(V, ov + 4 * c, own[c], rnd);
+                    st_chunk<BF>(G, ov + 4 * c, gg[c], rnd ^ 0xA5A5A5A5u);
                 }
             }
             if (P.use_linear && tid < F) {
@@ -231,32 +262,46 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     }
 }
 
-template <int KC>
+template <int KC, bool BF>
 int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-               const float* y, float* V, float* G, float* w, float* wz, float* wn, float* bias,
+               const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
                float* pred, float* loss, int grid, hipStream_t stream) {
     const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
     const size_t stage = (size_t)P.F * P.F * KC * 16;
-    const bool use_stage = stage + meta <= 48 * 1024;
+    const bool use_stage = stage + meta <= 64 * 1024;
     const int blocks = grid > 0 ? grid : (P.B < 256 * 6 * 4 ? P.B : 256 * 6 * 4);
     if (blocks <= 0) return 0;
     if (use_stage) {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, true>), dim3(blocks), dim3(256), stage + meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     } else {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, false>), dim3(blocks), dim3(256), meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF>), dim3(blocks), dim3(256), meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     }
     HM_LAUNCH_RET();
+}
+
+template <bool BF>
+int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+             const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
+             float* pred, float* loss, int grid, hipStream_t stream) {
+    switch (P.Kp / 4) {
+        case 1: return launch_ffm<1, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 2: return launch_ffm<2, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 3: return launch_ffm<3, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 4: return launch_ffm<4, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 8: return launch_ffm<8, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        default: return (int)hipErrorInvalidValue;
+    }
 }
 
 }  // namespace
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload
+//                     use_bias, norm, grid, reload, bf16_state, seed
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
-                       const float* val, const float* y, float* V, float* G, float* w, float* wz,
+                       const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
     FFMParams P;
     P.B = ip[0]; P.F = ip[1]; P.num_features = ip[2]; P.num_fields = ip[3]; P.Kp = ip[4];
@@ -264,15 +309,11 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.norm = ip[9];
     const int grid = ip[10];
     P.reload = ip[11];
+    const int bf16 = ip[12];
+    P.seed = (uint32_t)ip[13];
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
-    switch (P.Kp / 4) {
-        case 1: return launch_ffm<1>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 2: return launch_ffm<2>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 3: return launch_ffm<3>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 4: return launch_ffm<4>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 8: return launch_ffm<8>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        default: return (int)hipErrorInvalidValue;
-    }
+    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream)
+                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
 }

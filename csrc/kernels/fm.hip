@@ -125,11 +125,6 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
     const int lane = hm::lane_id();
     const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
-    // w0 is touched by every row: each wave keeps its pending w0 delta in a register and
-    // publishes it every 64 rows (one atomic per 64 rows instead of one per row; a single
-    // contended address would otherwise serialise the whole chip).
-    float w0_pending = 0.f;
-    int w0_rows = 0;
     for (int64_t row = gw; row < n_rows; row += nw) {
         const int64_t s = indptr[row], e = indptr[row + 1];
         const int nnz = (int)(e - s);
@@ -178,7 +173,7 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             pair += S[f] * S[f];
         }
         float p = lin + 0.5f * (pair - sq);
-        if (P.use_w0) p += *w0 + w0_pending;
+        if (P.use_w0) p += *w0;
         const float yy = y ? y[row] : 0.f;
         float d;
         if (P.classification) {
@@ -219,16 +214,10 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             t.load(V, i);
             upd(t, i, x, w[i]);
         }
-        if (P.use_w0) {
-            w0_pending -= eta * (d + 2.f * P.lambda0 * (*w0 + w0_pending));
-            if (++w0_rows == 64) {
-                if (lane == 0) atomicAdd(w0, w0_pending);
-                w0_pending = 0.f;
-                w0_rows = 0;
-            }
-        }
+        // per-row atomic: batching w0 deltas per wave was measured to diverge (every wave's
+        // locally-converged delta is summed -> ~#waves x overshoot on the hottest parameter)
+        if (P.use_w0 && lane == 0) atomicAdd(w0, -eta * (d + 2.f * P.lambda0 * *w0));
     }
-    if (P.use_w0 && lane == 0 && w0_pending != 0.f) atomicAdd(w0, w0_pending);
 }
 
 template <int KP, bool BF16>

@@ -76,6 +76,8 @@ class FFMTrainer(Learner):
         flag("global_bias", "w0", "Include the global bias term w0"),
         flag("disable_wi", "no_coeff", "Do not include the linear term w_i"),
         flag("no_norm", "disable_norm", "Disable instance-wise L2 normalization"),
+        flag("bf16_state", None, "[engine] keep V and the AdaGrad state in bf16 on the GPU "
+                                 "(stochastic rounding); halves the HBM traffic"),
         opt("feature_hashing", None, -1, int, "Hash feature indices into 2^bits"),
         opt("num_features", None, -1, int, "Number of (hashed) features; inferred when -1"),
         opt("num_fields", None, -1, int, "Number of fields; inferred from data when -1"),
@@ -131,9 +133,10 @@ class FFMTrainer(Learner):
             e = min(self.num_features, s + rows_per)
             chunk = init((e - s) * self.num_fields * self.k).view(e - s, self.num_fields, self.k)
             V[s:e, :, : self.k].copy_(chunk.to(dev))
+        sdt = torch.bfloat16 if (self.cl["bf16_state"] and dev.type == "cuda") else torch.float32
         self.state = dict(
-            V=V,
-            G=torch.zeros(shape, dtype=torch.float32, device=dev),
+            V=V.to(sdt),
+            G=torch.zeros(shape, dtype=sdt, device=dev),
             w=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
             wz=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
             wn=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
@@ -236,7 +239,7 @@ class FFMTrainer(Learner):
         mid = model_id or f"ffm-{self.rank}"
         ids = torch.nonzero(self.touched).flatten()
         NF, F, k = self.num_features, self.num_fields, self.k
-        V = self.state["V"][ids][:, :, :k].reshape(len(ids) * F, k).cpu().numpy()
+        V = self.state["V"][ids][:, :, :k].float().reshape(len(ids) * F, k).cpu().numpy()
         W = self.state["w"][ids].cpu().numpy()
         ids = ids.cpu().numpy().astype(np.int64)
         vkeys = (NF + ids[:, None] * F + np.arange(F)[None, :]).reshape(-1)

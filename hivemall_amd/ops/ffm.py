@@ -28,10 +28,14 @@ class FFMHyper:
     use_bias: bool = True
     norm: bool = True
     reload: bool = True   # re-read own V right before the update (short Hogwild RMW window)
+    seed: int = 31        # stochastic-rounding stream (bf16 state)
 
     def hp(self) -> np.ndarray:
         return np.array([self.eta0, self.eps, self.lambda_v, self.alpha, self.beta, self.lambda1,
                          self.lambda2, self.min_target, self.max_target], dtype=np.float32)
+
+
+_CALLS = 0  # per-launch counter mixed into the stochastic-rounding seed
 
 
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
@@ -60,9 +64,14 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
         assert pred.shape[0] >= B
     if loss is not None:
         assert loss.shape[0] >= B
+    bf16 = V.dtype == torch.bfloat16
+    assert state["G"].dtype == V.dtype, "V and G must share the storage dtype"
+    assert not bf16 or V.is_cuda, "bf16 FFM state is a device-only layout"
+    global _CALLS
+    _CALLS += 1
     ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
-                   int(hyper.use_bias), int(hyper.norm), int(grid), int(hyper.reload)],
-                  dtype=np.int32)
+                   int(hyper.use_bias), int(hyper.norm), int(grid), int(hyper.reload), int(bf16),
+                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF], dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
     args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(state["G"]),
