@@ -44,6 +44,8 @@ def parse_args(argv=None):
     ap.add_argument("--resident-batches", type=int, default=8)
     ap.add_argument("--eval-rows", type=int, default=262144)
     ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
+    ap.add_argument("--state", choices=("bf16", "fp32"), default="bf16",
+                    help="V / AdaGrad state storage (bf16 = stochastic-rounded, fp32 accumulate)")
     ap.add_argument("--device", default=None)
     return ap.parse_args(argv)
 
@@ -69,7 +71,8 @@ def main(argv=None):
     # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
     idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=dev)
     opts = (f"-classification -factors {args.factors} -feature_hashing {args.hash_bits} "
-            f"-num_fields {F} -seed 31 -batch_size {B}")
+            f"-num_fields {F} -seed 31 -batch_size {B}" +
+            (" -bf16_state" if args.state == "bf16" and dev.type == "cuda" else ""))
     tr = FFMTrainer(opts, device=dev)
     tr.init_state(NF, F)
     st, hyper = tr.state, tr.hyper
@@ -130,7 +133,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "bf16" if (args.state == "bf16" and dev.type == "cuda") else "fp32",
             "data": "synthetic (Criteo-shaped: 39 fields, Kaggle-DAC cardinalities, power-law "
                     "values, planted FM logit), random-init weights",
             "config": {

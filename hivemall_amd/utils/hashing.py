@@ -117,3 +117,39 @@ def murmur3_batch(words: Iterable[str], seed: int = DEFAULT_SEED) -> np.ndarray:
         _native.host().hm_murmur3_batch(b.ctypes.data, off.ctypes.data, len(words), seed,
                                         out.ctypes.data)
     return out.view(np.int32)
+
+
+def mhash_device(words: Iterable[str], num_features: int = DEFAULT_NUM_FEATURES,
+                 seed: int = DEFAULT_SEED, device="cuda") -> "torch.Tensor":
+    """Batched mhash on the GPU (csrc/kernels/hashing.hip): strings are packed on the host,
+    copied once, and hashed by the gfx950 kernel (bytes staged in LDS).  ``num_features <= 0``
+    returns the raw signed 32-bit hashes.  Bit-exact with :func:`mhash_batch`."""
+    import torch
+
+    from .. import _native
+
+    words = list(words)
+    buf, off = pack_strings(words)
+    dev = torch.device(device)
+    out = torch.empty(len(words), dtype=torch.int32, device=dev)
+    if not words:
+        return out
+    b = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy() if buf else np.zeros(16, np.uint8))
+    # pad so the kernel's 16-B staging loads never run past the allocation
+    b = torch.cat([b, torch.zeros(16, dtype=torch.uint8)]).to(dev)
+    o = torch.from_numpy(off.astype(np.int64)).to(dev)
+    rc = _native.hip().hm_mhash(_native.ptr(b), _native.ptr(o), len(words), seed, int(num_features),
+                                _native.ptr(out), _native.stream_of(dev))
+    _native.check(rc, "hm_mhash")
+    return out
+
+
+def _register():
+    import ctypes as C
+
+    from .. import _native
+    _native.register_hip("hm_mhash", [_native.c_p, _native.c_p, _native.c_i64, C.c_uint32, C.c_int32,
+                                      _native.c_p, _native.c_p])
+
+
+_register()

@@ -182,3 +182,16 @@ def test_anomaly_detects_level_shift():
     x2 = np.where(t < 300, np.sin(t / 3.0), np.sin(t / 1.2)) + rng.normal(0, 0.1, 600)
     s = np.array([c[0] for c in sst(x2, "-w 20")])
     assert 300 <= s.argmax() <= 360 and s[:290].max() < 0.1 * s.max()
+
+
+@pytest.mark.gpu
+def test_mhash_kernel_bit_exact():
+    import random
+    from hivemall_amd.utils.hashing import mhash_batch, mhash_device, murmur3_batch
+    rng = random.Random(0)
+    words = ["", "a", "ab", "abc", "abcd", "feature_name_42", "日本語", "x" * 5000] + \
+        ["".join(rng.choice("abcdefghij:0123456789_") for _ in range(rng.randint(1, 40))) for _ in range(20000)]
+    for nf in (1 << 24, 1000, 0):
+        got = mhash_device(words, nf).cpu().numpy()
+        ref = murmur3_batch(words) if nf == 0 else mhash_batch(words, nf)
+        assert (got == ref).all(), nf
