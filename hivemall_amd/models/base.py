@@ -94,7 +94,10 @@ class Learner:
     def __init__(self, options: str | None = None, device=None, **kw: Any):
         self.cl = self.options().parse(options)
         self.device = resolve_device(device)
-        self.seed = self.cl.get("seed")
+        try:
+            self.seed = self.cl.get("seed")
+        except KeyError:  # learners without a -seed option
+            self.seed = None
         if self.seed is None or self.seed < 0:
             self.seed = 31
         self.mixer = kw.pop("mixer", None)

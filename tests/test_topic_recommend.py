@@ -1,0 +1,68 @@
+import numpy as np
+import pandas as pd
+import pytest
+
+from hivemall_amd.models.recommend import KPA, SLIM
+from hivemall_amd.models.topicmodel import LDA, PLSA, lda_predict, plsa_predict
+from hivemall_amd.sql import Session
+
+
+def _docs(n=300, seed=0):
+    rng = np.random.default_rng(seed)
+    A = [f"a{i}" for i in range(20)]
+    B = [f"b{i}" for i in range(20)]
+    return [list(rng.choice(A if d % 2 == 0 else B, 30)) for d in range(n)]
+
+
+def test_lda_separates_topics():
+    docs = _docs()
+    m = LDA("-topics 2 -iters 5", device="cpu").fit(docs)
+    th = m.transform(docs[:10])
+    lab = th.argmax(1)
+    assert (lab[0::2] == lab[0]).all() and (lab[1::2] != lab[0]).all() and th.max(1).min() > 0.8
+    tab = m.model_table()
+    assert list(tab.columns) == ["label", "word", "lambda"]
+    sub = tab[tab.word.isin(docs[0])]
+    pred = lda_predict(sub.word.tolist(), [1] * len(sub), sub.label.tolist(), sub["lambda"].tolist(), "-topics 2")
+    assert pred[0][0] == lab[0] and pred[0][1] > 0.8
+
+
+def test_plsa_separates_topics():
+    docs = _docs()
+    m = PLSA("-topics 2 -iters 5", device="cpu").fit(docs)
+    th = m.transform(docs[:10])
+    assert (th.argmax(1)[0::2] == th.argmax(1)[0]).all() and (th.argmax(1)[1::2] != th.argmax(1)[0]).all()
+    tab = m.model_table()
+    sub = tab[tab.word.isin(docs[1])]
+    p = plsa_predict(sub.word.tolist(), [1] * len(sub), sub.label.tolist(), sub["prob"].tolist())
+    assert p[0][0] == th.argmax(1)[1]
+
+
+def test_lda_sql():
+    s = Session(device="cpu")
+    s.register("docs", pd.DataFrame({"docid": range(100), "words": _docs(100)}))
+    t = s.sql("SELECT train_lda(words, '-topics 2 -iters 3') AS (label, word, lambda) FROM docs")
+    assert set(t.columns) == {"label", "word", "lambda"} and len(t) == 80
+
+
+def test_slim_recovers_item_relation():
+    rng = np.random.default_rng(0)
+    users = range(50)
+    r0 = {u: float(rng.integers(1, 5)) for u in users}
+    r1 = {u: 2 * v for u, v in r0.items()}            # item 1 = 2 x item 0
+    r2 = {u: float(rng.integers(1, 5)) for u in users}  # unrelated
+    m = SLIM("-l1 0.0 -l2 0.0 -iters 100", device="cpu").fit([0, 0], [r0, r0], [None, None], [1, 2], [r1, r2])
+    tab = m.model_table()
+    w = {(int(a), int(b)): v for a, b, v in tab.itertuples(index=False)}
+    assert w[(0, 1)] == pytest.approx(0.5, rel=0.05) and w.get((0, 2), 0.0) < 0.05
+
+
+def test_kpa_learns_xor():
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(2000, 2))
+    y = (X[:, 0] * X[:, 1] > 0).astype(int)
+    feats = [[f"a:{a}", f"b:{b}"] for a, b in X]
+    m = KPA("-iters 3", device="cpu").fit(feats, y)
+    acc = ((m.decision_function(feats) > 0) == (y > 0)).mean()
+    assert acc > 0.9
+    assert list(m.model_table().columns) == ["h", "hk", "w0", "w1", "w2", "w3"]
