@@ -37,6 +37,7 @@ struct FFMParams {
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
     int reload;
+    int batched;           // J-slot batched gathers (more HBM requests in flight per lane)
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -99,7 +100,8 @@ __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint3
     }
 }
 
-template <int KC, bool STAGE, bool BF>
+// J > 0: every thread owns J slots (tid + 256 j) and issues their gathers together.
+template <int KC, bool STAGE, bool BF, int J>
 __global__ __launch_bounds__(256) void ffm_row_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y,
@@ -119,6 +121,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     float* s_x = reinterpret_cast<float*>(s_fld + F);                    // F
     float* s_red = s_x + F;                                              // 16 (+pad)
 
+    constexpr int JA = J > 0 ? J : 1;
     const int tid = threadIdx.x;
     const int Kp = P.Kp;
     const size_t fstride = (size_t)P.num_fields * Kp;  // elements per feature block
@@ -146,7 +149,30 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         }
 
         // ---- 2. gather the row's slot vectors (coalesced) ----
-        if (STAGE) {
+        if constexpr (STAGE && J > 0) {
+            // issue all J gathers of this thread before the first LDS store: J independent
+            // HBM round trips in flight per lane instead of one
+            float4 buf[JA][KC];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int s = tid + j * 256;
+                const int a = s / F, b = s - (s / F) * F;
+                const bool live = s < FF && a != b && s_idx[a] >= 0 && s_idx[b] >= 0;
+                const size_t off = live ? (size_t)s_idx[a] * fstride + (size_t)s_fld[b] * Kp : 0;
+#pragma unroll
+                for (int c = 0; c < KC; ++c)
+                    buf[j][c] = live ? ld_chunk<BF>(V, off + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int s = tid + j * 256;
+                if (s < FF) {
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) s_v[s * KC + c] = buf[j][c];
+                }
+            }
+            __syncthreads();
+        } else if (STAGE) {
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 const int ia = s_idx[a];
@@ -209,6 +235,49 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         if (P.train) {
             const float ks = kappa * scale * scale;
             const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
+            if constexpr (STAGE && J > 0) {
+                // batched: all J slots' G (and reloaded V) loads in flight, then the math
+                float4 own[JA][KC], gg[JA][KC];
+                size_t ovs[JA];
+                bool live[JA];
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int s = tid + j * 256;
+                    const int a = s / F, b = s - (s / F) * F;
+                    live[j] = s < FF && a != b && s_idx[a] >= 0 && s_idx[b] >= 0;
+                    ovs[j] = live[j] ? (size_t)s_idx[a] * fstride + (size_t)s_fld[b] * Kp : 0;
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) {
+                        gg[j][c] = live[j] ? ld_chunk<BF>(G, ovs[j] + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        own[j][c] = live[j] ? (P.reload ? ld_chunk<BF>(V, ovs[j] + 4 * c) : s_v[s * KC + c])
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    if (!live[j]) continue;
+                    const int s = tid + j * 256;
+                    const int a = s / F, b = s - (s / F) * F;
+                    const float coef = ks * s_x[a] * s_x[b];
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) {
+                        const float4 par = s_v[(b * F + a) * KC + c];
+                        float4 o = own[j][c], q = gg[j][c], g;
+                        g.x = coef * par.x + P.lambda_v * o.x;
+                        g.y = coef * par.y + P.lambda_v * o.y;
+                        g.z = coef * par.z + P.lambda_v * o.z;
+                        g.w = coef * par.w + P.lambda_v * o.w;
+                        q.x += g.x * g.x; q.y += g.y * g.y; q.z += g.z * g.z; q.w += g.w * g.w;
+                        o.x -= P.eta0 * g.x * rsqrtf(q.x + P.eps);
+                        o.y -= P.eta0 * g.y * rsqrtf(q.y + P.eps);
+                        o.z -= P.eta0 * g.z * rsqrtf(q.z + P.eps);
+                        o.w -= P.eta0 * g.w * rsqrtf(q.w + P.eps);
+                        const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
+                        st_chunk<BF>(V, ovs[j] + 4 * c, o, rnd);
+                        st_chunk<BF>(G, ovs[j] + 4 * c, q, rnd ^ 0xA5A5A5A5u);
+                    }
+                }
+            } else
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 if (a == b) continue;
@@ -271,13 +340,22 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
     const bool use_stage = stage + meta <= 64 * 1024;
     const int blocks = grid > 0 ? grid : (P.B < 256 * 6 * 4 ? P.B : 256 * 6 * 4);
     if (blocks <= 0) return 0;
-    if (use_stage) {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
-                           P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
+    const int FF = P.F * P.F;
+#define HM_FFM_J(JJ)                                                                               \
+    hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF, JJ>), dim3(blocks), dim3(256), stage + meta,    \
+                       stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+    if (use_stage && P.batched && KC == 1 && FF <= 8 * 256) {
+        if (FF <= 2 * 256) HM_FFM_J(2);
+        else if (FF <= 4 * 256) HM_FFM_J(4);
+        else if (FF <= 6 * 256) HM_FFM_J(6);
+        else HM_FFM_J(8);
+    } else if (use_stage) {
+        HM_FFM_J(0);
     } else {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF>), dim3(blocks), dim3(256), meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF, 0>), dim3(blocks), dim3(256), meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     }
+#undef HM_FFM_J
     HM_LAUNCH_RET();
 }
 
@@ -299,7 +377,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload, bf16_state, seed
+//                     use_bias, norm, grid, reload, bf16_state, seed, batched
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -311,6 +389,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.reload = ip[11];
     const int bf16 = ip[12];
     P.seed = (uint32_t)ip[13];
+    P.batched = ip[14];
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
