@@ -26,6 +26,8 @@
 //   * Updates are Hogwild across rows (no atomics); each slot vector has a single writer
 //     within a row.  ``reload`` re-reads the own slot right before its update (shorter
 //     read-modify-write window -> fewer lost updates on hot features).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -37,7 +39,6 @@ struct FFMParams {
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
     int reload;
-    int batched;           // J-slot batched gathers (more HBM requests in flight per lane)
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -88,6 +89,23 @@ __device__ __forceinline__ float4 ld_chunk(const void* base, size_t off) {
     }
 }
 
+// Raw storage-format chunk (no conversion) and its fp32 view.
+template <bool BF>
+__device__ __forceinline__ typename std::conditional<BF, uint2, float4>::type ld_raw(const void* base, size_t off) {
+    if constexpr (BF) return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + off);
+    else return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + off);
+}
+
+template <bool BF, typename T>
+__device__ __forceinline__ float4 to_f4(const T& q) {
+    if constexpr (BF) {
+        return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u));
+    } else {
+        return q;
+    }
+}
+
 template <bool BF>
 __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint32_t rnd) {
     if constexpr (BF) {
@@ -100,8 +118,7 @@ __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint3
     }
 }
 
-// J > 0: every thread owns J slots (tid + 256 j) and issues their gathers together.
-template <int KC, bool STAGE, bool BF, int J>
+template <int KC, bool STAGE, bool BF>
 __global__ __launch_bounds__(256) void ffm_row_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y,
@@ -114,14 +131,17 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int F = P.F;
     const int FF = F * F;
-    float4* s_v = reinterpret_cast<float4*>(smem);                       // STAGE: FF*KC
-    const size_t vbytes = STAGE ? (size_t)FF * KC * sizeof(float4) : 0;
+    // The LDS image keeps the storage format (bf16 state -> 8 B per 4-vector): half the LDS per
+    // block at bf16, so 8 instead of 6 blocks fit per CU (measured: occupancy, not bytes, is
+    // what limits this kernel once the state is bf16 — profiles/ffm_kernel_ab_r1.log).
+    using SV = typename std::conditional<BF, uint2, float4>::type;
+    SV* s_v = reinterpret_cast<SV*>(smem);                               // STAGE: FF*KC
+    const size_t vbytes = STAGE ? (size_t)FF * KC * sizeof(SV) : 0;
     int* s_idx = reinterpret_cast<int*>(smem + vbytes);                  // F
     int* s_fld = s_idx + F;                                              // F
     float* s_x = reinterpret_cast<float*>(s_fld + F);                    // F
     float* s_red = s_x + F;                                              // 16 (+pad)
 
-    constexpr int JA = J > 0 ? J : 1;
     const int tid = threadIdx.x;
     const int Kp = P.Kp;
     const size_t fstride = (size_t)P.num_fields * Kp;  // elements per feature block
@@ -149,30 +169,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         }
 
         // ---- 2. gather the row's slot vectors (coalesced) ----
-        if constexpr (STAGE && J > 0) {
-            // issue all J gathers of this thread before the first LDS store: J independent
-            // HBM round trips in flight per lane instead of one
-            float4 buf[JA][KC];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const int s = tid + j * 256;
-                const int a = s / F, b = s - (s / F) * F;
-                const bool live = s < FF && a != b && s_idx[a] >= 0 && s_idx[b] >= 0;
-                const size_t off = live ? (size_t)s_idx[a] * fstride + (size_t)s_fld[b] * Kp : 0;
-#pragma unroll
-                for (int c = 0; c < KC; ++c)
-                    buf[j][c] = live ? ld_chunk<BF>(V, off + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const int s = tid + j * 256;
-                if (s < FF) {
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) s_v[s * KC + c] = buf[j][c];
-                }
-            }
-            __syncthreads();
-        } else if (STAGE) {
+        if (STAGE) {
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 const int ia = s_idx[a];
@@ -180,7 +177,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 const size_t off = live ? (size_t)ia * fstride + (size_t)s_fld[b] * Kp : 0;
 #pragma unroll
                 for (int c = 0; c < KC; ++c)
-                    s_v[s * KC + c] = live ? ld_chunk<BF>(V, off + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    s_v[s * KC + c] = live ? ld_raw<BF>(V, off + 4 * c) : SV{};
             }
             __syncthreads();
         }
@@ -195,7 +192,10 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
             float4 u[KC], v[KC];
             if (STAGE) {
 #pragma unroll
-                for (int c = 0; c < KC; ++c) { u[c] = s_v[s * KC + c]; v[c] = s_v[(b * F + a) * KC + c]; }
+                for (int c = 0; c < KC; ++c) {
+                    u[c] = to_f4<BF>(s_v[s * KC + c]);
+                    v[c] = to_f4<BF>(s_v[(b * F + a) * KC + c]);
+                }
             } else {
                 const size_t ou = (size_t)ia * fstride + (size_t)s_fld[b] * Kp;
                 const size_t ov = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
@@ -235,49 +235,6 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         if (P.train) {
             const float ks = kappa * scale * scale;
             const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
-            if constexpr (STAGE && J > 0) {
-                // batched: all J slots' G (and reloaded V) loads in flight, then the math
-                float4 own[JA][KC], gg[JA][KC];
-                size_t ovs[JA];
-                bool live[JA];
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    const int s = tid + j * 256;
-                    const int a = s / F, b = s - (s / F) * F;
-                    live[j] = s < FF && a != b && s_idx[a] >= 0 && s_idx[b] >= 0;
-                    ovs[j] = live[j] ? (size_t)s_idx[a] * fstride + (size_t)s_fld[b] * Kp : 0;
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) {
-                        gg[j][c] = live[j] ? ld_chunk<BF>(G, ovs[j] + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-                        own[j][c] = live[j] ? (P.reload ? ld_chunk<BF>(V, ovs[j] + 4 * c) : s_v[s * KC + c])
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    if (!live[j]) continue;
-                    const int s = tid + j * 256;
-                    const int a = s / F, b = s - (s / F) * F;
-                    const float coef = ks * s_x[a] * s_x[b];
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) {
-                        const float4 par = s_v[(b * F + a) * KC + c];
-                        float4 o = own[j][c], q = gg[j][c], g;
-                        g.x = coef * par.x + P.lambda_v * o.x;
-                        g.y = coef * par.y + P.lambda_v * o.y;
-                        g.z = coef * par.z + P.lambda_v * o.z;
-                        g.w = coef * par.w + P.lambda_v * o.w;
-                        q.x += g.x * g.x; q.y += g.y * g.y; q.z += g.z * g.z; q.w += g.w * g.w;
-                        o.x -= P.eta0 * g.x * rsqrtf(q.x + P.eps);
-                        o.y -= P.eta0 * g.y * rsqrtf(q.y + P.eps);
-                        o.z -= P.eta0 * g.z * rsqrtf(q.z + P.eps);
-                        o.w -= P.eta0 * g.w * rsqrtf(q.w + P.eps);
-                        const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
-                        st_chunk<BF>(V, ovs[j] + 4 * c, o, rnd);
-                        st_chunk<BF>(G, ovs[j] + 4 * c, q, rnd ^ 0xA5A5A5A5u);
-                    }
-                }
-            } else
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 if (a == b) continue;
@@ -291,8 +248,8 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 if (STAGE) {
 #pragma unroll
                     for (int c = 0; c < KC; ++c) {
-                        own[c] = P.reload ? ld_chunk<BF>(V, ov + 4 * c) : s_v[s * KC + c];
-                        par[c] = s_v[(b * F + a) * KC + c];
+                        own[c] = P.reload ? ld_chunk<BF>(V, ov + 4 * c) : to_f4<BF>(s_v[s * KC + c]);
+                        par[c] = to_f4<BF>(s_v[(b * F + a) * KC + c]);
                     }
                 } else {
                     const size_t op = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
@@ -336,26 +293,17 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
                const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
                float* pred, float* loss, int grid, hipStream_t stream) {
     const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
-    const size_t stage = (size_t)P.F * P.F * KC * 16;
+    const size_t stage = (size_t)P.F * P.F * KC * (BF ? 8 : 16);
     const bool use_stage = stage + meta <= 64 * 1024;
     const int blocks = grid > 0 ? grid : (P.B < 256 * 6 * 4 ? P.B : 256 * 6 * 4);
     if (blocks <= 0) return 0;
-    const int FF = P.F * P.F;
-#define HM_FFM_J(JJ)                                                                               \
-    hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF, JJ>), dim3(blocks), dim3(256), stage + meta,    \
-                       stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-    if (use_stage && P.batched && KC == 1 && FF <= 8 * 256) {
-        if (FF <= 2 * 256) HM_FFM_J(2);
-        else if (FF <= 4 * 256) HM_FFM_J(4);
-        else if (FF <= 6 * 256) HM_FFM_J(6);
-        else HM_FFM_J(8);
-    } else if (use_stage) {
-        HM_FFM_J(0);
+    if (use_stage) {
+        hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
+                           P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     } else {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF, 0>), dim3(blocks), dim3(256), meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF>), dim3(blocks), dim3(256), meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     }
-#undef HM_FFM_J
     HM_LAUNCH_RET();
 }
 
@@ -377,7 +325,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload, bf16_state, seed, batched
+//                     use_bias, norm, grid, reload, bf16_state, seed
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -389,7 +337,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.reload = ip[11];
     const int bf16 = ip[12];
     P.seed = (uint32_t)ip[13];
-    P.batched = ip[14];
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;

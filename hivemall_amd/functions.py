@@ -15,6 +15,7 @@ from .ftvec import functions as _ftvec  # noqa: F401
 from .knn import cosine_similarity  # noqa: F401
 from .misc import approx_count_distinct  # noqa: F401
 from .models import ffm_keys  # noqa: F401
+from .nlp import tokenize_ja  # noqa: F401
 from .tools import functions as _tools  # noqa: F401
 
 
@@ -55,7 +56,7 @@ def _register_learners():
 
 def _optional_learners():
     import importlib
-    for mod in ("mf", "trees", "topicmodel", "recommend"):
+    for mod in ("mf", "trees", "topicmodel", "recommend", "fm"):
         try:
             m = importlib.import_module(f".models.{mod}", __package__)
         except ModuleNotFoundError as e:
