@@ -1,0 +1,157 @@
+"""Checkpoint / resume of any learner.
+
+Upstream the model table *is* the checkpoint (plus ``-loadmodel`` warm start); multi-epoch
+state lives in a task-local spill file and is not resumable.  Here a checkpoint directory holds
+
+* ``model.parquet``  — the learner's model table (Hivemall layout; loadable by SQL / -loadmodel),
+* ``state.pt``       — every device tensor of the learner (weights *and* optimizer state:
+                       AdaGrad G, FTRL z/n, Adam moments, covariances, touched masks, replica
+                       scalars), saved with ``torch.save`` and read back with
+                       ``torch.load(weights_only=True)`` (tensors and primitives only),
+* ``meta.json``      — learner class, option string, counters (step t, rows seen, epoch,
+                       convergence history), label / vocabulary encoders and the RNG cursor.
+
+``save(learner, dir)`` / ``load(dir, device)`` round-trip bit-exactly; writes are atomic
+(temp directory + rename) so a rank killed mid-write never leaves a torn checkpoint.
+"""
+from __future__ import annotations
+
+import dataclasses
+import importlib
+import json
+import os
+import shutil
+import tempfile
+
+import numpy as np
+import torch
+
+_SCALARS = ("t", "rows_seen", "num_features", "num_fields", "dims", "n_users", "n_items", "labels",
+            "classes", "k", "kp", "grid", "K")
+
+
+def _collect_tensors(learner) -> dict:
+    out = {}
+    st = getattr(learner, "state", None)
+    if isinstance(st, dict):
+        for k, v in st.items():
+            if torch.is_tensor(v):
+                out[f"state.{k}"] = v
+    elif dataclasses.is_dataclass(st):
+        for f in dataclasses.fields(st):
+            v = getattr(st, f.name)
+            if torch.is_tensor(v):
+                out[f"state.{f.name}"] = v
+    for k, v in vars(learner).items():
+        if torch.is_tensor(v) and not k.startswith("_"):
+            out[f"attr.{k}"] = v
+    return out
+
+
+def _encoder_meta(enc):
+    if enc is None:
+        return None
+    return {"mode": enc.mode, "num_features": enc.num_features, "seed": enc.seed,
+            "int_base": enc.int_base, "vocab": enc.vocab() if enc.mode in ("dict", "auto") else [],
+            "string_names": bool(getattr(enc, "string_names", False))}
+
+
+def _restore_encoder(m):
+    if m is None:
+        return None
+    from ..utils.features import FeatureEncoder
+    enc = FeatureEncoder(m["mode"], m["num_features"], m["int_base"], m["seed"])
+    enc.string_names = m.get("string_names", False)
+    if m["vocab"]:
+        enc.encode([m["vocab"]], add_new=True)
+    return enc
+
+
+def _jsonable(v):
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    if isinstance(v, (list, tuple)):
+        return [_jsonable(x) for x in v]
+    return v
+
+
+def save(learner, path: str, model_table: bool = True) -> str:
+    parent = os.path.dirname(os.path.abspath(path)) or "."
+    os.makedirs(parent, exist_ok=True)
+    tmp = tempfile.mkdtemp(prefix=".ckpt-", dir=parent)
+    try:
+        tensors = {k: v.detach().cpu() for k, v in _collect_tensors(learner).items()}
+        torch.save(tensors, os.path.join(tmp, "state.pt"))
+        st = getattr(learner, "state", None)
+        meta = {
+            "class": f"{type(learner).__module__}:{type(learner).__qualname__}",
+            "name": getattr(learner, "NAME", None),
+            "options": getattr(learner, "options_str", ""),
+            "scalars": {k: _jsonable(getattr(learner, k)) for k in _SCALARS
+                        if hasattr(learner, k) and isinstance(getattr(learner, k), (int, float, str, list, tuple, type(None), np.integer, np.floating))},
+            "state_kind": "dataclass" if dataclasses.is_dataclass(st) else ("dict" if isinstance(st, dict) else None),
+            "state_meta": dict(st.meta) if dataclasses.is_dataclass(st) and hasattr(st, "meta") else None,
+            "state_covar": bool(getattr(st, "covar", False)) if dataclasses.is_dataclass(st) else None,
+            "encoder": _encoder_meta(getattr(learner, "encoder", None)),
+            "cv": vars(learner.cv) if hasattr(learner, "cv") else None,
+            "hyper": dataclasses.asdict(learner.hyper) if dataclasses.is_dataclass(getattr(learner, "hyper", None)) else None,
+            "torch_rng": torch.get_rng_state().tolist(),
+        }
+        with open(os.path.join(tmp, "meta.json"), "w") as f:
+            json.dump(meta, f, default=lambda o: None)
+        if model_table and hasattr(learner, "model_table"):
+            try:
+                from .model_table import write_table
+                write_table(learner.model_table(), os.path.join(tmp, "model.parquet"))
+            except Exception:  # pragma: no cover - the tensors are the authoritative state
+                pass
+        if os.path.exists(path):
+            shutil.rmtree(path)
+        os.replace(tmp, path)
+    except BaseException:
+        shutil.rmtree(tmp, ignore_errors=True)
+        raise
+    return path
+
+
+def load(path: str, device=None, **kw):
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    mod, qual = meta["class"].split(":")
+    m = importlib.import_module(mod)
+    try:
+        cls = m
+        for part in qual.split("."):
+            cls = getattr(cls, part)
+    except AttributeError:  # classes generated per SQL function (models.linear.LEARNERS)
+        cls = getattr(m, "LEARNERS")[meta["name"]]
+    learner = cls(meta["options"] or None, device=device, **kw)
+    tensors = torch.load(os.path.join(path, "state.pt"), weights_only=True)
+    dev = learner.device
+    for k, v in meta["scalars"].items():
+        setattr(learner, k, v)
+    kind = meta["state_kind"]
+    st_t = {k[6:]: v.to(dev) for k, v in tensors.items() if k.startswith("state.")}
+    if kind == "dict":
+        learner.state = st_t
+    elif kind == "dataclass":
+        from ..ops.linear import LinearState
+        learner.state = LinearState(st_t["S"], st_t["touched"], st_t["RS"], bool(meta["state_covar"]),
+                                    st_t.get("gacc"), st_t.get("tlist"), meta.get("state_meta") or {})
+    for k, v in tensors.items():
+        if k.startswith("attr."):
+            setattr(learner, k[5:], v.to(dev))
+    if meta.get("encoder") is not None:
+        learner.encoder = _restore_encoder(meta["encoder"])
+    if meta.get("cv") is not None and hasattr(learner, "cv"):
+        for k, v in meta["cv"].items():
+            setattr(learner.cv, k, v if v is not None else float("inf"))
+    if meta.get("hyper") is not None and hasattr(learner, "hyper"):
+        for k, v in meta["hyper"].items():
+            setattr(learner.hyper, k, v)
+    if getattr(learner, "labels", None) is not None and hasattr(learner, "P"):
+        learner.P.n_labels = len(learner.labels)
+    torch.set_rng_state(torch.tensor(meta["torch_rng"], dtype=torch.uint8))
+    return learner

@@ -92,6 +92,7 @@ class Learner:
         return Options(cls.OPTIONS, cls.NAME)
 
     def __init__(self, options: str | None = None, device=None, **kw: Any):
+        self.options_str = options or ""
         self.cl = self.options().parse(options)
         self.device = resolve_device(device)
         try:

@@ -1,0 +1,69 @@
+"""Checkpoint/resume round trips and fault injection + resume."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from hivemall_amd.io import checkpoint
+from hivemall_amd.io.synthetic import a9a_like, criteo_like
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_checkpoint_roundtrip_linear(tmp_path):
+    from hivemall_amd.models.linear import TrainAROW
+    rows, y = a9a_like(2000)
+    srows = [[f"f{int(i)}" for i in r] for r in rows]
+    a = TrainAROW("-replicas 2 -iters 1", device="cpu").fit(srows, y)
+    checkpoint.save(a, str(tmp_path / "ck"))
+    b = checkpoint.load(str(tmp_path / "ck"), device="cpu")
+    assert torch.equal(a.state.S, b.state.S)
+    a.fit(srows, y)
+    b.fit(srows, y)
+    assert torch.equal(a.weights()[0], b.weights()[0])
+    assert a.model_table().equals(b.model_table())
+    assert os.path.exists(tmp_path / "ck" / "model.parquet")
+
+
+def test_checkpoint_roundtrip_ffm_and_fm(tmp_path):
+    from hivemall_amd.models.ffm import FFMBatch, FFMTrainer
+    from hivemall_amd.models.fm import FMTrainer
+    idx, y = criteo_like(3000, 12, seed=1)
+    a = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 12", device="cpu")
+    a.fit(batch=FFMBatch(idx, None, None, y))
+    checkpoint.save(a, str(tmp_path / "ffm"))
+    b = checkpoint.load(str(tmp_path / "ffm"), device="cpu")
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k
+    rows = [[f"{int(i) + 1}:1" for i in r[:5]] for r in idx[:500].numpy()]
+    f = FMTrainer("-factors 3 -iters 2", device="cpu").fit(rows, y[:500].numpy())
+    checkpoint.save(f, str(tmp_path / "fm"))
+    g = checkpoint.load(str(tmp_path / "fm"), device="cpu")
+    np.testing.assert_array_equal(f.predict(rows[:20]), g.predict(rows[:20]))
+
+
+def _run_job(ckpt, fault=None, world=2, steps=6):
+    env = dict(os.environ, PYTHONPATH=ROOT, HM_CKPT=str(ckpt), HM_STEPS=str(steps),
+               MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("HM_FAULT", None)
+    if fault:
+        env["HM_FAULT"] = fault
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000 + (7 if fault else 0)),
+           os.path.join(ROOT, "tests", "elastic_job.py")]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_fault_injection_and_resume(tmp_path):
+    ref = _run_job(tmp_path / "ref")
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    crashed = _run_job(tmp_path / "job", fault="1:3")
+    assert crashed.returncode != 0
+    resumed = _run_job(tmp_path / "job")
+    assert resumed.returncode == 0, resumed.stderr[-2000:]
+    a = torch.load(tmp_path / "ref" / "final_rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "job" / "final_rank0.pt", weights_only=True)
+    assert torch.equal(a, b)
