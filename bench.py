@@ -41,6 +41,8 @@ def parse_args(argv=None):
     ap.add_argument("--hash-bits", type=int, default=20)
     ap.add_argument("--factors", type=int, default=4)
     ap.add_argument("--mix-every", type=int, default=10)
+    ap.add_argument("--mix-overlap", type=int, default=1,
+                    help="1: stale-by-one mixing overlapped with compute (async MixServer semantics)")
     ap.add_argument("--resident-batches", type=int, default=8)
     ap.add_argument("--eval-rows", type=int, default=262144)
     ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
@@ -53,7 +55,7 @@ def parse_args(argv=None):
 def main(argv=None):
     args = parse_args(argv)
     from hivemall_amd.parallel.dist import init_distributed
-    from hivemall_amd.parallel.mix import ModelMixer
+    from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
     from hivemall_amd.models.ffm import FFMTrainer
     from hivemall_amd.ops.ffm import ffm_step
     from hivemall_amd.io.synthetic import criteo_like
@@ -80,11 +82,16 @@ def main(argv=None):
     mix_tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
     grid = args.grid
 
+    overlap = OverlappedMixer(mixer) if args.mix_overlap else None
+
     def step(i):
         s = (i % nres) * B
         ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True, grid=grid)
         if world > 1 and (i + 1) % args.mix_every == 0:
-            mixer.average(mix_tensors)
+            if overlap is not None:
+                overlap.start(mix_tensors)   # finishes the previous mix, launches this one
+            else:
+                mixer.average(mix_tensors)
 
     def sync():
         if dev.type == "cuda":
@@ -98,6 +105,8 @@ def main(argv=None):
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
+    if overlap is not None:
+        overlap.finish()   # the last in-flight mix is applied inside the timed region
     sync()
     ctx.barrier()
     t1 = time.perf_counter()

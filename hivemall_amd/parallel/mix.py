@@ -103,3 +103,69 @@ class ModelMixer:
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                                "min": dist.ReduceOp.MIN}[op])
         return float(t.item())
+
+
+class OverlappedMixer:
+    """Stale-by-one model averaging whose all-reduce runs behind the training kernels.
+
+    ``start(tensors)`` snapshots the replicas (one device copy on the compute stream) and
+    launches the bucketed all-reduce of the snapshot asynchronously (RCCL's own stream);
+    training continues.  ``finish()`` (at the next mix point) waits for the collective on the
+    device — not on the host — and merges it without discarding the local progress made in the
+    meantime:
+
+        x  <-  x + (mean_r(snapshot_r) - snapshot_local)
+
+    i.e. every rank moves by the consensus correction of the snapshot.  This is the
+    asynchronous MixServer semantics (replies arrive while the learner keeps training) on
+    xGMI, and it hides the collective completely when one mix interval of compute takes longer
+    than the all-reduce.  Buffers are allocated once (2x the mixed bytes).
+    """
+
+    def __init__(self, mixer: ModelMixer):
+        self.m = mixer
+        self.snap: list[torch.Tensor] | None = None
+        self.buf: list[torch.Tensor] | None = None
+        self.works: list = []
+        self.targets: list[torch.Tensor] = []
+
+    def pending(self) -> bool:
+        return bool(self.works)
+
+    def start(self, tensors: list[torch.Tensor]) -> None:
+        if not self.m._active():
+            return
+        if self.works:
+            self.finish()
+        if self.snap is None:
+            # bf16 replicas are reduced in fp32: an 8-way sum rounded to 8 mantissa bits would
+            # inject noise into every mix (the wire cost is hidden behind compute anyway)
+            wide = lambda t: torch.empty(t.shape, dtype=torch.float32 if t.dtype in (
+                torch.bfloat16, torch.float16) else t.dtype, device=t.device)
+            self.snap = [wide(t) for t in tensors]
+            self.buf = [wide(t) for t in tensors]
+        self.targets = tensors
+        for s, b, t in zip(self.snap, self.buf, tensors):
+            s.copy_(t)
+            b.copy_(t)
+        self.works = []
+        for b in self.buf:
+            v = b.view(-1)
+            step = max(1, self.m.bucket_bytes // b.element_size())
+            for s0 in range(0, v.numel(), step):
+                self.works.append(dist.all_reduce(v[s0:s0 + step], async_op=True))
+        self.m.calls += 1
+        self.m.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
+
+    def finish(self) -> None:
+        if not self.works:
+            return
+        for w in self.works:
+            w.wait()
+        self.works = []
+        inv = 1.0 / self.m.world
+        for t, s, b in zip(self.targets, self.snap, self.buf):
+            if t.dtype in (torch.bfloat16, torch.float16):
+                t.copy_((t.float() + (b * inv - s)).to(t.dtype))
+            else:
+                t.add_(b, alpha=inv).sub_(s)

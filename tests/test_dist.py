@@ -32,7 +32,13 @@ def _worker(rank, world, port, fn_name, q):
     D._CTX = None
     ctx = D.init_distributed(backend="gloo", device="cpu")
     try:
-        q.put((rank, getattr(T, fn_name)(ctx)))
+        if ":" in fn_name:
+            import importlib
+            mod, fn = fn_name.split(":")
+            f = getattr(importlib.import_module(mod), fn)
+        else:
+            f = getattr(T, fn_name)
+        q.put((rank, f(ctx)))
     finally:
         D.shutdown()
 
