@@ -19,9 +19,9 @@ for state in ("bf16", "fp32"):
     t = FFMTrainer(f"-c -factors 4 -num_fields 39 -feature_hashing {bits}" +
                    (" -bf16_state" if state == "bf16" else ""), device=dev)
     t.init_state(1 << bits, 39)
-    for batched in (False, True):
+    for batched in (False, True):  # batched -> pair kernel (True) vs staged kernel (False)
         for reload in (True, False):
-            t.hyper.batched, t.hyper.reload = batched, reload
+            t.hyper.pairs, t.hyper.reload = batched, reload
             for i in range(3):
                 ffm_step(t.state, idx[:B], None, None, y[:B], t.hyper)
             torch.cuda.synchronize()
@@ -32,6 +32,6 @@ for state in ("bf16", "fp32"):
                 ffm_step(t.state, idx[s:s + B], None, None, y[s:s + B], t.hyper)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"state": state, "batched": batched, "reload": reload,
+            print(json.dumps({"state": state, "pairs": batched, "reload": reload,
                               "rows_per_s": round(B * n / dt), "ms_per_step": round(dt / n * 1e3, 3)}),
                   flush=True)
