@@ -21,7 +21,7 @@ for state in ("bf16", "fp32"):
     t.init_state(1 << bits, 39)
     for batched in (False, True):  # batched -> pair kernel (True) vs staged kernel (False)
         for reload in (True, False):
-            t.hyper.pairs, t.hyper.reload = batched, reload
+            t.hyper.reload = reload
             for i in range(3):
                 ffm_step(t.state, idx[:B], None, None, y[:B], t.hyper)
             torch.cuda.synchronize()

@@ -39,7 +39,6 @@ struct FFMParams {
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
     int reload;
-    int pairs;             // pair-ownership kernel (no LDS staging); 0 = staged kernel
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -133,8 +132,8 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     const int F = P.F;
     const int FF = F * F;
     // The LDS image keeps the storage format (bf16 state -> 8 B per 4-vector): half the LDS per
-    // block at bf16, so 8 instead of 6 blocks fit per CU (measured: occupancy, not bytes, is
-    // what limits this kernel once the state is bf16 — profiles/ffm_kernel_ab_r1.log).
+    // block at bf16, so up to 8 blocks fit per CU.  Measured variants (profiles/ffm_kernel_ab*):
+    // J-slot batched gathers and a register-only pair-ownership kernel were both slower.
     using SV = typename std::conditional<BF, uint2, float4>::type;
     SV* s_v = reinterpret_cast<SV*>(smem);                               // STAGE: FF*KC
     const size_t vbytes = STAGE ? (size_t)FF * KC * sizeof(SV) : 0;
@@ -289,174 +288,6 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     }
 }
 
-// Pair-ownership variant (default): thread t owns the field pairs p = t + 256 j (a < b).  The
-// two slot vectors of a pair, V[i_a, f_b] and V[i_b, f_a], are exactly what both the forward
-// dot product and the two AdaGrad updates of that pair need, so they are loaded once into
-// registers and never staged: no LDS image, no staging barrier, every gather of the thread
-// in flight at once, occupancy bounded by VGPRs only.  (PMC of the staged kernel:
-// 64 % of wave cycles in s_waitcnt/barrier waits, profiles/ffm_pmc/.)
-template <int KC, bool BF, int JP>
-__global__ __launch_bounds__(256) void ffm_pair_kernel(
-    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
-    const float* __restrict__ val, const float* __restrict__ y,
-    void* __restrict__ V, void* __restrict__ G,
-    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
-    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out) {
-    using SV = typename std::conditional<BF, uint2, float4>::type;
-    __shared__ int s_idx[256];
-    __shared__ int s_fld[256];
-    __shared__ float s_x[256];
-    __shared__ float s_red[16];
-    __shared__ uint16_t s_pa[JP * 256], s_pb[JP * 256];
-    const int F = P.F;
-    const int NP = F * (F - 1) / 2;
-    const int tid = threadIdx.x;
-    const int Kp = P.Kp;
-    const size_t fstride = (size_t)P.num_fields * Kp;
-    // pair table p -> (a, b), a < b (row-major upper triangle), built once per block
-    for (int p = tid; p < NP; p += 256) {
-        int a = 0, rem = p;
-        while (rem >= F - 1 - a) { rem -= F - 1 - a; ++a; }
-        s_pa[p] = (uint16_t)a;
-        s_pb[p] = (uint16_t)(a + 1 + rem);
-    }
-    __syncthreads();
-
-    for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
-        float sq = 0.f;
-        if (tid < F) {
-            const size_t o = (size_t)row * F + tid;
-            int i = idx[o];
-            int f = fld ? fld[o] : tid;
-            float x = val ? val[o] : 1.f;
-            if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; }
-            s_idx[tid] = i;
-            s_fld[tid] = f < 0 ? 0 : (f >= P.num_fields ? P.num_fields - 1 : f);
-            s_x[tid] = x;
-            sq = x * x;
-        }
-        float scale = 1.f;
-        if (P.norm) {
-            const float tot = hm::block_sum(sq, s_red);
-            scale = tot > 0.f ? rsqrtf(tot) : 1.f;
-        } else {
-            __syncthreads();
-        }
-        // ---- gathers: both slot vectors of every owned pair, all in flight together ----
-        SV u[JP][KC], v[JP][KC];
-        size_t ou[JP], ov[JP];
-        bool live[JP];
-#pragma unroll
-        for (int j = 0; j < JP; ++j) {
-            const int p = tid + 256 * j;
-            live[j] = false;
-            ou[j] = ov[j] = 0;
-            if (p < NP) {
-                const int a = s_pa[p], b = s_pb[p];
-                const int ia = s_idx[a], ib = s_idx[b];
-                live[j] = ia >= 0 && ib >= 0;
-                ou[j] = (size_t)(ia < 0 ? 0 : ia) * fstride + (size_t)s_fld[b] * Kp;
-                ov[j] = (size_t)(ib < 0 ? 0 : ib) * fstride + (size_t)s_fld[a] * Kp;
-            }
-#pragma unroll
-            for (int c = 0; c < KC; ++c) {
-                u[j][c] = live[j] ? ld_raw<BF>(V, ou[j] + 4 * c) : SV{};
-                v[j][c] = live[j] ? ld_raw<BF>(V, ov[j] + 4 * c) : SV{};
-            }
-        }
-        float part = 0.f;
-#pragma unroll
-        for (int j = 0; j < JP; ++j) {
-            if (!live[j]) continue;
-            const int p = tid + 256 * j;
-            float d = 0.f;
-#pragma unroll
-            for (int c = 0; c < KC; ++c) {
-                const float4 a4 = to_f4<BF>(u[j][c]), b4 = to_f4<BF>(v[j][c]);
-                d += a4.x * b4.x + a4.y * b4.y + a4.z * b4.z + a4.w * b4.w;
-            }
-            part += d * s_x[s_pa[p]] * s_x[s_pb[p]];
-        }
-        part *= scale * scale;
-        if (P.use_linear && tid < F && s_idx[tid] >= 0) part += w[s_idx[tid]] * s_x[tid] * scale;
-        float pv = hm::block_sum(part, s_red);
-        if (P.use_bias) pv += bias[0];
-        const float yy = y ? y[row] : 0.f;
-        float kappa;
-        if (P.classification) {
-            const float e = yy * pv;
-            kappa = -yy / (1.f + __expf(e));
-            if (tid == 0) {
-                if (loss_out) loss_out[row] = hm::log1pexp(-e);
-                if (pred_out) pred_out[row] = pv;
-            }
-        } else {
-            const float pc = fminf(fmaxf(pv, P.min_target), P.max_target);
-            kappa = pc - yy;
-            if (tid == 0) {
-                if (loss_out) loss_out[row] = 0.5f * kappa * kappa;
-                if (pred_out) pred_out[row] = pc;
-            }
-        }
-        if (P.train) {
-            const float ks = kappa * scale * scale;
-            const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
-            SV gu[JP][KC], gv[JP][KC];
-#pragma unroll
-            for (int j = 0; j < JP; ++j) {
-#pragma unroll
-                for (int c = 0; c < KC; ++c) {
-                    gu[j][c] = live[j] ? ld_raw<BF>(G, ou[j] + 4 * c) : SV{};
-                    gv[j][c] = live[j] ? ld_raw<BF>(G, ov[j] + 4 * c) : SV{};
-                    if (P.reload && live[j]) {
-                        u[j][c] = ld_raw<BF>(V, ou[j] + 4 * c);
-                        v[j][c] = ld_raw<BF>(V, ov[j] + 4 * c);
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < JP; ++j) {
-                if (!live[j]) continue;
-                const int p = tid + 256 * j;
-                const float coef = ks * s_x[s_pa[p]] * s_x[s_pb[p]];
-#pragma unroll
-                for (int c = 0; c < KC; ++c) {
-                    float4 a4 = to_f4<BF>(u[j][c]), b4 = to_f4<BF>(v[j][c]);
-                    float4 ga = to_f4<BF>(gu[j][c]), gb = to_f4<BF>(gv[j][c]);
-                    float4 da, db;  // gradients of V[i_a,f_b] (partner b4) and V[i_b,f_a] (partner a4)
-                    da.x = coef * b4.x + P.lambda_v * a4.x; db.x = coef * a4.x + P.lambda_v * b4.x;
-                    da.y = coef * b4.y + P.lambda_v * a4.y; db.y = coef * a4.y + P.lambda_v * b4.y;
-                    da.z = coef * b4.z + P.lambda_v * a4.z; db.z = coef * a4.z + P.lambda_v * b4.z;
-                    da.w = coef * b4.w + P.lambda_v * a4.w; db.w = coef * a4.w + P.lambda_v * b4.w;
-                    ga.x += da.x * da.x; ga.y += da.y * da.y; ga.z += da.z * da.z; ga.w += da.w * da.w;
-                    gb.x += db.x * db.x; gb.y += db.y * db.y; gb.z += db.z * db.z; gb.w += db.w * db.w;
-                    a4.x -= P.eta0 * da.x * rsqrtf(ga.x + P.eps); b4.x -= P.eta0 * db.x * rsqrtf(gb.x + P.eps);
-                    a4.y -= P.eta0 * da.y * rsqrtf(ga.y + P.eps); b4.y -= P.eta0 * db.y * rsqrtf(gb.y + P.eps);
-                    a4.z -= P.eta0 * da.z * rsqrtf(ga.z + P.eps); b4.z -= P.eta0 * db.z * rsqrtf(gb.z + P.eps);
-                    a4.w -= P.eta0 * da.w * rsqrtf(ga.w + P.eps); b4.w -= P.eta0 * db.w * rsqrtf(gb.w + P.eps);
-                    const uint32_t r1 = BF ? hash3(rrow, (uint32_t)p, (uint32_t)c) : 0u;
-                    const uint32_t r2 = BF ? hash3(rrow ^ 0x5bd1e995u, (uint32_t)p, (uint32_t)c) : 0u;
-                    st_chunk<BF>(V, ou[j] + 4 * c, a4, r1);
-                    st_chunk<BF>(G, ou[j] + 4 * c, ga, r1 ^ 0xA5A5A5A5u);
-                    st_chunk<BF>(V, ov[j] + 4 * c, b4, r2);
-                    st_chunk<BF>(G, ov[j] + 4 * c, gb, r2 ^ 0xA5A5A5A5u);
-                }
-            }
-            if (P.use_linear && tid < F) {
-                const int i = s_idx[tid];
-                if (i >= 0) {
-                    const float g = kappa * s_x[tid] * scale;
-                    w[i] = ftrl_update(wz + i, wn + i, w[i], g, P.alpha, P.beta, P.lambda1, P.lambda2);
-                }
-            }
-            if (P.use_bias && tid == 0) {
-                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
-            }
-        }
-        __syncthreads();  // s_idx / s_x reuse by the next row
-    }
-}
-
 template <int KC, bool BF>
 int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
@@ -466,20 +297,6 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
     const bool use_stage = stage + meta <= 64 * 1024;
     const int blocks = grid > 0 ? grid : (P.B < 256 * 8 * 4 ? P.B : 256 * 8 * 4);
     if (blocks <= 0) return 0;
-    const int NP = P.F * (P.F - 1) / 2;
-    if (P.pairs && NP <= 16 * 256) {
-#define HM_FFM_P(JJ)                                                                               \
-    hipLaunchKernelGGL((ffm_pair_kernel<KC, BF, JJ>), dim3(blocks), dim3(256), 0, stream, P, idx,   \
-                       fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (NP <= 256) HM_FFM_P(1);
-        else if (NP <= 512) HM_FFM_P(2);
-        else if (NP <= 768) HM_FFM_P(3);
-        else if (NP <= 1024) HM_FFM_P(4);
-        else if (NP <= 2048) HM_FFM_P(8);
-        else HM_FFM_P(16);
-#undef HM_FFM_P
-        HM_LAUNCH_RET();
-    }
     if (use_stage) {
         hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
@@ -520,7 +337,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.reload = ip[11];
     const int bf16 = ip[12];
     P.seed = (uint32_t)ip[13];
-    P.pairs = ip[14];
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;

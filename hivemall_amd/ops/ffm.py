@@ -29,7 +29,6 @@ class FFMHyper:
     norm: bool = True
     reload: bool = True   # re-read own V right before the update (short Hogwild RMW window)
     seed: int = 31        # stochastic-rounding stream (bf16 state)
-    pairs: bool = True    # pair-ownership kernel (registers, no LDS staging)
 
     def hp(self) -> np.ndarray:
         return np.array([self.eta0, self.eps, self.lambda_v, self.alpha, self.beta, self.lambda1,
@@ -72,7 +71,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     _CALLS += 1
     ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
                    int(hyper.use_bias), int(hyper.norm), int(grid), int(hyper.reload), int(bf16),
-                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(hyper.pairs)], dtype=np.int32)
+                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF], dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
     args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(state["G"]),
