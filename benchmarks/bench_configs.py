@@ -1,0 +1,165 @@
+"""Throughput + quality for the BASELINE.json configs other than the headline FFM bench:
+
+  classifier : train_classifier (AdaGrad logistic) on a9a-shaped libsvm rows (CPU engine, ws=1)
+  linear_gpu : the same learner on 8M a9a-shaped rows on the GPU (replica-per-wave kernel)
+  fm         : train_fm on Criteo-1TB-shaped rows (2^24 hashed features, bf16 V), 1 GPU
+  gbdt       : GBT classifier on HIGGS-shaped dense rows (11M x 28, histogram kernel), 1 GPU
+  rf         : random forest on the same data
+  bprmf      : BPR-MF on MovieLens-20M-shaped implicit feedback (device negative sampling)
+
+    python benchmarks/bench_configs.py [names...]      # one JSON line per config
+Synthetic data of the named shapes (no datasets offline), random-init weights.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
+
+
+def bench_classifier(dev="cpu"):
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import a9a_like
+    from hivemall_amd.models.linear import TrainClassifier
+    rows, y = a9a_like(32561)
+    trows, ty = a9a_like(16281, seed=4)
+    m = TrainClassifier("-loss logloss -opt adagrad -reg no -iters 10 -disable_cv", device=dev)
+    r = m.prepare(rows, y)
+    t0 = time.perf_counter()
+    m.fit(rows=r)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    p = 1 / (1 + np.exp(-m.decision_function(trows).cpu().numpy()))
+    from sklearn.metrics import log_loss
+    return {"config": "train_classifier adagrad logistic, a9a-shaped (32561 x 123, ~14 nnz), 10 epochs",
+            "device": dev, "rows_per_s": round(32561 * 10 / dt), "seconds": round(dt, 3),
+            "test_auc": round(roc_auc_score(ty, p), 4), "test_logloss": round(log_loss(ty, p), 4)}
+
+
+def bench_linear_gpu(dev="cuda", n=8_000_000):
+    from hivemall_amd.models.linear import SparseRows, TrainClassifier
+    g = torch.Generator(device=dev).manual_seed(0)
+    nnz = 14
+    idx = torch.randint(1, 124, (n, nnz), generator=g, device=dev, dtype=torch.int32)
+    wtrue = torch.randn(124, generator=g, device=dev)
+    logit = wtrue[idx.long()].sum(1) * 0.5
+    y = torch.where(torch.rand(n, generator=g, device=dev) < torch.sigmoid(logit), 1.0, -1.0)
+    rows = SparseRows(torch.arange(0, n * nnz + 1, nnz, dtype=torch.int64, device=dev),
+                      idx.reshape(-1).contiguous(), None, y)
+    m = TrainClassifier("-loss logloss -opt adagrad -reg no -iters 1 -dims 124", device=dev)
+    m.fit(rows=rows)  # warm (allocations, replicas)
+    _sync(dev)
+    t0 = time.perf_counter()
+    m.fit(rows=rows)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    s = m.decision_function(rows=rows).float()
+    acc = float(((s > 0) == (y > 0)).float().mean().item())
+    return {"config": f"train_classifier adagrad logistic, {n} a9a-shaped rows, GPU replica-per-wave",
+            "device": dev, "replicas": m.state.R, "rows_per_s": round(n / dt), "train_acc": round(acc, 4)}
+
+
+def bench_fm(dev="cuda", n_rows=8 * 262144, bits=24):
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.models.fm import FMTrainer
+    from hivemall_amd.models.linear import SparseRows
+    idx, y = criteo_like(n_rows, bits, seed=5, device=dev)
+    rows = SparseRows(torch.arange(0, n_rows * 39 + 1, 39, dtype=torch.int64, device=dev),
+                      idx.reshape(-1).contiguous(), None, y)
+    t = FMTrainer(f"-c -factors 8 -num_features {1 << bits} -eta0 0.01 -sigma 0.01", device=dev)
+    t.fit(rows=rows)
+    _sync(dev)
+    t0 = time.perf_counter()
+    t.train_rows(rows)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    eidx, ey = criteo_like(200000, bits, seed=77, device=dev)
+    er = SparseRows(torch.arange(0, 200000 * 39 + 1, 39, dtype=torch.int64, device=dev),
+                    eidx.reshape(-1).contiguous(), None, None)
+    ll = torch.nn.functional.binary_cross_entropy_with_logits(t.predict_raw(rows=er), (ey > 0).float()).item()
+    return {"config": f"train_fm k=8, Criteo-1TB-shaped (39 fields, 2^{bits} hashed features), bf16 V",
+            "device": dev, "rows_per_s": round(n_rows / dt), "heldout_logloss_after_2_epochs": round(ll, 5)}
+
+
+def bench_gbdt(dev="cuda", n=11_000_000, trees=20):
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import GradientTreeBoostingClassifier
+    X, y = higgs_like(n, device=dev)
+    Xt, yt = higgs_like(500000, seed=9, device=dev)
+    gb = GradientTreeBoostingClassifier(f"-trees {trees} -eta 0.1 -max_depth 8 -subsample 1.0", device=dev)
+    _sync(dev)
+    t0 = time.perf_counter()
+    gb.fit(X, y.long())
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    auc = roc_auc_score(yt.cpu().numpy(), gb.predict_proba(Xt)[:, 1])
+    return {"config": f"GBT classifier, HIGGS-shaped {n} x 28, depth 8, {trees} trees, 256-bin histograms",
+            "device": dev, "seconds": round(dt, 3), "row_trees_per_s": round(n * trees / dt),
+            "test_auc": round(float(auc), 4)}
+
+
+def bench_rf(dev="cuda", n=11_000_000, trees=10):
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import RandomForestClassifier
+    X, y = higgs_like(n, device=dev)
+    Xt, yt = higgs_like(500000, seed=9, device=dev)
+    rf = RandomForestClassifier(f"-trees {trees} -max_depth 12", device=dev)
+    _sync(dev)
+    t0 = time.perf_counter()
+    rf.fit(X, y.long())
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    auc = roc_auc_score(yt.cpu().numpy(), rf.predict_proba(Xt)[:, 1])
+    return {"config": f"RandomForest classifier, HIGGS-shaped {n} x 28, depth 12, {trees} trees",
+            "device": dev, "seconds": round(dt, 3), "row_trees_per_s": round(n * trees / dt),
+            "test_auc": round(float(auc), 4)}
+
+
+def bench_bprmf(dev="cuda", k=64, epochs=3):
+    from hivemall_amd.io.synthetic import movielens_like
+    from hivemall_amd.models.mf import BPRMF, auc_implicit
+    us, its = movielens_like(device=dev, k=16)
+    n = us.numel()
+    ntest = 200000
+    m = BPRMF(f"-factors {k} -iters 1 -eta0 0.05", device=dev)
+    m.fit_implicit(us[:-ntest], its[:-ntest], 138493, 27278, epochs=1)
+    _sync(dev)
+    t0 = time.perf_counter()
+    m.fit_implicit(us[:-ntest], its[:-ntest], 138493, 27278, epochs=epochs)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    auc = auc_implicit(m, us[-ntest:].cpu().numpy(), its[-ntest:].cpu().numpy())
+    return {"config": f"BPR-MF k={k}, MovieLens-20M-shaped ({n} interactions, 138493 users, 27278 items), "
+                      f"device negative sampling", "device": dev,
+            "triples_per_s": round((n - ntest) * epochs / dt), "sampled_auc": round(auc, 4)}
+
+
+ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "fm": bench_fm,
+       "gbdt": bench_gbdt, "rf": bench_rf, "bprmf": bench_bprmf}
+
+SMALL = {"linear_gpu": dict(n=20000), "fm": dict(n_rows=20000, bits=16),
+         "gbdt": dict(n=20000, trees=4), "rf": dict(n=20000, trees=2), "bprmf": dict(k=16, epochs=1)}
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    small = "--small" in sys.argv  # CPU smoke of the harness itself (tiny shapes)
+    names = args or list(ALL)
+    for name in names:
+        kw = dict(SMALL.get(name, {})) if small else {}
+        if small:
+            kw["dev"] = "cpu"
+        res = ALL[name](**kw)
+        for r in (res if isinstance(res, list) else [res]):
+            r["bench"] = name
+            print(json.dumps(r), flush=True)

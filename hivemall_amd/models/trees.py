@@ -378,6 +378,12 @@ def _to_dense(features, d=None) -> np.ndarray:
     return np.asarray([list(r) for r in rows], dtype=np.float32)
 
 
+def _encode_classes(yl: np.ndarray):
+    """Sorted distinct labels (python scalars) and the int64 class index of every row."""
+    cls, inv = np.unique(np.asarray(yl).reshape(-1), return_inverse=True)
+    return cls.tolist(), torch.from_numpy(inv.astype(np.int64))
+
+
 class _ForestBase(Learner):
     OPTIONS = TREE_OPTS
     TASK = "classification"
@@ -404,10 +410,9 @@ class _ForestBase(Learner):
         n, d = X.shape
         c = self.cl
         if self.TASK == "classification":
-            yl = y.cpu().numpy()
-            self.classes = sorted(set(yl.tolist()))
-            lut = {v: i for i, v in enumerate(self.classes)}
-            yi = torch.as_tensor([lut[v] for v in yl.tolist()], device=self.device)
+            cls, yi = _encode_classes(y.cpu().numpy())
+            self.classes = cls
+            yi = yi.to(self.device)
             onehot = torch.nn.functional.one_hot(yi, len(self.classes)).float()
             crit = "entropy" if str(c["splits"]).upper() == "ENTROPY" else "gini"
             mtry = c["mtry"] or max(1, int(math.floor(math.sqrt(d))))
@@ -519,10 +524,9 @@ class GradientTreeBoostingClassifier(Learner):
         X = features if torch.is_tensor(features) else torch.from_numpy(_to_dense(features))
         X = X.float().to(self.device)
         yl = labels.cpu().numpy() if torch.is_tensor(labels) else np.asarray(labels)
-        self.classes = sorted(set(yl.tolist()))
+        self.classes, yi = _encode_classes(yl)
+        yi = yi.to(self.device)
         K = len(self.classes)
-        lut = {v: i for i, v in enumerate(self.classes)}
-        yi = torch.as_tensor([lut[v] for v in yl.tolist()], device=self.device)
         n, d = X.shape
         q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed)
         self.importance = np.zeros(d)
