@@ -154,12 +154,21 @@ SMALL = {"linear_gpu": dict(n=20000), "fm": dict(n_rows=20000, bits=16),
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     small = "--small" in sys.argv  # CPU smoke of the harness itself (tiny shapes)
+    prof = "--profile" in sys.argv  # per-kernel device-time table via torch.profiler
     names = args or list(ALL)
     for name in names:
         kw = dict(SMALL.get(name, {})) if small else {}
         if small:
             kw["dev"] = "cpu"
-        res = ALL[name](**kw)
+        if prof:
+            from torch.profiler import ProfilerActivity, profile
+            with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as pr:
+                res = ALL[name](**kw)
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open(f"gpurun_out/torchprof_{name}.txt", "w") as f:
+                f.write(pr.key_averages().table(sort_by="self_cuda_time_total", row_limit=40))
+        else:
+            res = ALL[name](**kw)
         for r in (res if isinstance(res, list) else [res]):
             r["bench"] = name
             print(json.dumps(r), flush=True)

@@ -6,18 +6,16 @@
 
 #define HM_API extern "C" __attribute__((visibility("default")))
 
-HM_API int hm_hist_build_cpu(const uint8_t* bins, int64_t n, int d, int dpad, int B,
-                             const int32_t* rows, const int64_t* seg, const int32_t* node_ids,
-                             int n_nodes, int64_t max_seg, const float* stats, int NS, int FG,
+HM_API int hm_hist_build_cpu(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
+                             const int64_t* seg, int n_seg, const float* stats, int NS, int FG,
                              float* hist) {
-    (void)n; (void)max_seg; (void)FG;
+    (void)FG;
 #pragma omp parallel for schedule(dynamic, 1) collapse(2)
-    for (int node = 0; node < n_nodes; ++node) {
+    for (int node = 0; node < n_seg; ++node) {
         for (int f = 0; f < d; ++f) {
-            const int out_node = node_ids ? node_ids[node] : node;
-            float* h = hist + (((size_t)out_node * d + f) * B) * NS;
+            float* h = hist + (((size_t)node * d + f) * B) * NS;
             for (int64_t q = seg[node]; q < seg[node + 1]; ++q) {
-                const int64_t r = rows ? rows[q] : q;
+                const int64_t r = rows[q];
                 const int b = bins[r * dpad + f];
                 const float* st = stats + r * NS;
                 for (int s = 0; s < NS; ++s) h[b * NS + s] += st[s];
@@ -41,7 +39,7 @@ HM_API int hm_tree_predict_cpu(const float* X, int64_t n, int d, const int32_t* 
                 const int f = feature[k];
                 if (f < 0) break;
                 const float v = x[f];
-                k = (v <= threshold[k] || std::isnan(v)) ? left[k] : right[k];
+                k = v <= threshold[k] ? left[k] : right[k];  // NaN goes right
             }
             const float* val = values + voff[k];
             if (sum_trees) {

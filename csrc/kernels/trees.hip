@@ -9,11 +9,17 @@
 // feature, bin) sums of NS statistics (GBT: residual, hessian, count; RF: per-class
 // bootstrap-weighted counts; regression: w·y, w).
 //
-// hist_build: block (tile t, node n, feature group g) walks TILE rows of node n's segment,
-//   privatises the group's histogram [FG][B][NS] in LDS (ds_add_f32 float atomics; rows of
-//   one node contend only on equal bins), then adds it to the global histogram with one
-//   pass of global float atomics (skipping zero bins).  Feature groups keep the LDS image
-//   small (FG=8, B=256, NS=3 -> 24 KB) so several blocks share a CU.
+// hist_build: the level's rows are grouped by node (rows[seg[k] .. seg[k+1]) belong to output
+//   node k).  A fixed grid of blocks splits the position range [seg[0], seg[S]) into equal
+//   chunks (the host never has to know the row count: no sync before the launch); a block walks
+//   the node segments its chunk overlaps.  Per (block, node) piece: a large piece privatises the
+//   feature group's histogram in LDS, laid out [f][s][b] so the 64 lanes of one ds_add_f32 hit
+//   banks by bin, and flushes the non-zero bins with global float atomics; a small piece (deep
+//   levels: few rows per node) adds straight to global memory, so zeroing and scanning a 48 KB
+//   LDS image is not paid for a handful of rows.  Feature groups (FG a multiple of 4) keep the
+//   LDS image <= 48 KB so three blocks share a CU; bins are read as 32-bit words.
+//   The tree builder only histograms the smaller child of every split and derives the sibling
+//   as parent - child (models/trees.py).
 // tree_predict: one lane per (row, tree); trees are flattened SoA arrays
 //   (feature, threshold, left, right, value offset) so a traversal is a chain of coalesced-ish
 //   16-B loads that stay in L2 for forests of a few MB.
@@ -21,52 +27,115 @@
 
 namespace {
 
-constexpr int TILE = 4096;
 
-template <int NS>
-__global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ bins, int64_t n,
-                                                   int d, int dpad, int B,
-                                                   const int32_t* __restrict__ rows,
-                                                   const int64_t* __restrict__ seg,
-                                                   const int32_t* __restrict__ node_ids,
-                                                   const float* __restrict__ stats, int FG,
-                                                   float* __restrict__ hist) {
-    extern __shared__ __attribute__((aligned(16))) float s_hist[];
-    const int node = blockIdx.y;
-    const int g = blockIdx.z;
-    const int f0 = g * FG;
-    const int nf = min(FG, d - f0);
-    if (nf <= 0) return;
-    const int64_t beg = seg[node], end = seg[node + 1];
-    const int64_t t0 = beg + (int64_t)blockIdx.x * TILE;
-    if (t0 >= end) return;
-    const int64_t t1 = min(end, t0 + TILE);
-    const int hsz = nf * B * NS;
-    for (int i = threadIdx.x; i < hsz; i += blockDim.x) s_hist[i] = 0.f;
-    __syncthreads();
-    for (int64_t q = t0 + threadIdx.x; q < t1; q += blockDim.x) {
-        const int64_t r = rows ? rows[q] : q;
-        float st[NS];
+template <int FGW> struct BinWords;
+template <> struct BinWords<1> { using T = uint32_t; };
+template <> struct BinWords<2> { using T = uint2; };
+template <> struct BinWords<4> { using T = uint4; };
+
+// Rows handled per thread per step: all their loads are issued before the first atomic, so a
+// wave keeps HIST_U row gathers (index -> stats + bin words) in flight instead of one.
+constexpr int HIST_U = 4;
+
+template <int NS, int FGW, bool GLOBAL>
+__device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int dpad, int f0, int nf,
+                                          int B, const int32_t* __restrict__ rows,
+                                          const float* __restrict__ stats, int64_t s0, int64_t s1,
+                                          float* __restrict__ h) {
+    using W = typename BinWords<FGW>::T;
+    for (int64_t q0 = s0 + threadIdx.x; q0 < s1; q0 += (int64_t)blockDim.x * HIST_U) {
+        int64_t r[HIST_U];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) st[s] = stats[r * NS + s];
-        bool zero = true;
+        for (int u = 0; u < HIST_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            r[u] = q < s1 ? (int64_t)rows[q] : -1;
+        }
+        float st[HIST_U][NS];
+        uint32_t w[HIST_U][FGW];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) zero = zero && st[s] == 0.f;
-        if (zero) continue;  // out-of-bag / zero-weight rows add nothing
-        const uint8_t* br = bins + r * dpad + f0;
-        for (int f = 0; f < nf; ++f) {
-            const int b = br[f];
-            float* h = s_hist + (f * B + b) * NS;
+        for (int u = 0; u < HIST_U; ++u) {
+            if (r[u] >= 0) {
 #pragma unroll
-            for (int s = 0; s < NS; ++s) atomicAdd(h + s, st[s]);
+                for (int s = 0; s < NS; ++s) st[u][s] = stats[r[u] * NS + s];
+                const W v = *reinterpret_cast<const W*>(bins + r[u] * dpad + f0);
+                if constexpr (FGW == 1) {
+                    w[u][0] = v;
+                } else if constexpr (FGW == 2) {
+                    w[u][0] = v.x; w[u][1] = v.y;
+                } else {
+                    w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < HIST_U; ++u) {
+            if (r[u] < 0) continue;
+#pragma unroll
+            for (int j = 0; j < FGW * 4; ++j) {
+                if (j < nf) {
+                    const int bin = (w[u][j >> 2] >> (8 * (j & 3))) & 0xff;
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        if constexpr (GLOBAL) {
+                            if (st[u][s] != 0.f) atomicAdd(h + ((size_t)j * B + bin) * NS + s, st[u][s]);
+                        } else {
+                            atomicAdd(h + (j * NS + s) * B + bin, st[u][s]);
+                        }
+                    }
+                }
+            }
         }
     }
-    __syncthreads();
-    const int out_node = node_ids ? node_ids[node] : node;
-    float* gh = hist + ((size_t)out_node * d + f0) * B * NS;
-    for (int i = threadIdx.x; i < hsz; i += blockDim.x) {
-        const float v = s_hist[i];
-        if (v != 0.f) atomicAdd(gh + i, v);
+}
+
+template <int NS, int FGW>
+__global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ bins, int d, int dpad,
+                                                   int B, const int32_t* __restrict__ rows,
+                                                   const int64_t* __restrict__ seg, int n_seg,
+                                                   const float* __restrict__ stats,
+                                                   float* __restrict__ hist) {
+    constexpr int FG = FGW * 4;
+    extern __shared__ __attribute__((aligned(16))) float s_hist[];
+    const int f0 = blockIdx.y * FG;
+    const int nf = min(FG, d - f0);
+    if (nf <= 0) return;
+    const int64_t nblk = gridDim.x;
+    const int64_t lo = seg[0], hi = seg[n_seg];
+    const int64_t chunk = ((hi - lo + nblk - 1) / nblk + 255) / 256 * 256;
+    const int64_t p0 = lo + (int64_t)blockIdx.x * chunk;
+    const int64_t p1 = min(hi, p0 + chunk);
+    if (p0 >= p1) return;
+    // first node whose segment ends after p0
+    int a = 0, b = n_seg - 1;
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if (seg[m + 1] <= p0) a = m + 1; else b = m;
+    }
+    const int hsz = nf * NS * B;
+    for (int k = a; k < n_seg; ++k) {
+        if (seg[k] >= p1) break;
+        const int64_t s0 = max(p0, seg[k]), s1 = min(p1, seg[k + 1]);
+        if (s0 >= s1) continue;
+        float* gh = hist + ((size_t)k * d + f0) * B * NS;
+        if ((s1 - s0) * nf * 4 < hsz) {  // few rows: straight to global memory
+            hist_rows<NS, FGW, true>(bins, dpad, f0, nf, B, rows, stats, s0, s1, gh);
+            continue;
+        }
+        for (int i = threadIdx.x; i < hsz; i += blockDim.x) s_hist[i] = 0.f;
+        __syncthreads();
+        hist_rows<NS, FGW, false>(bins, dpad, f0, nf, B, rows, stats, s0, s1, s_hist);
+        __syncthreads();
+        for (int i = threadIdx.x; i < hsz; i += blockDim.x) {
+            const float v = s_hist[i];
+            if (v != 0.f) {
+                const int f = i / (NS * B);
+                const int rem = i - f * NS * B;
+                const int s = rem / B;
+                const int bin = rem - s * B;
+                atomicAdd(gh + ((size_t)f * B + bin) * NS + s, v);
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -91,7 +160,7 @@ __global__ __launch_bounds__(256) void tree_predict_kernel(
             const int f = feature[k];
             if (f < 0) break;
             const float v = x[f];
-            k = (v <= threshold[k] || v != v) ? left[k] : right[k];
+            k = v <= threshold[k] ? left[k] : right[k];  // NaN goes right (Smile: x <= t ? true : false)
         }
         const float* val = values + voff[k];
         if (sum_trees) {
@@ -150,23 +219,30 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
 
 }  // namespace
 
-HM_API int hm_hist_build(const uint8_t* bins, int64_t n, int d, int dpad, int B,
-                         const int32_t* rows, const int64_t* seg, const int32_t* node_ids,
-                         int n_nodes, int64_t max_seg, const float* stats, int NS, int FG,
-                         float* hist, hipStream_t stream) {
-    if (n_nodes <= 0 || max_seg <= 0) return 0;
-    if (B > 256 || NS <= 0 || NS > 8 || FG <= 0) return (int)hipErrorInvalidValue;
+// hist [n_seg, d, B, NS] (zeroed by the caller) += statistics of rows[seg[k]..seg[k+1]) for
+// every node k.  seg lives on the device.  FG (features per group) is 4, 8 or 16 and bins rows
+// are padded to a multiple of 16 bytes, so a row's group is one aligned 4/8/16-byte load.
+HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
+                         const int64_t* seg, int n_seg, const float* stats, int NS, int FG,
+                         float* hist, int nblk, hipStream_t stream) {
+    if (n_seg <= 0) return 0;
+    if (nblk <= 0) nblk = 1024;
+    if (B > 256 || NS <= 0 || NS > 8 || (FG != 4 && FG != 8 && FG != 16) || (dpad & 15))
+        return (int)hipErrorInvalidValue;
     const size_t lds = (size_t)FG * B * NS * sizeof(float);
     if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-    const dim3 grid((unsigned)((max_seg + TILE - 1) / TILE), (unsigned)n_nodes, (unsigned)((d + FG - 1) / FG));
-#define HM_H(K)                                                                                     \
-    case K:                                                                                         \
-        hipLaunchKernelGGL((hist_kernel<K>), grid, dim3(256), lds, stream, bins, n, d, dpad, B, rows, \
-                           seg, node_ids, stats, FG, hist);                                         \
+    const dim3 grid((unsigned)nblk, (unsigned)((d + FG - 1) / FG));
+#define HM_H(K, W)                                                                                  \
+    case K * 100 + W:                                                                               \
+        hipLaunchKernelGGL((hist_kernel<K, W>), grid, dim3(256), lds, stream, bins, d, dpad, B, rows, \
+                           seg, n_seg, stats, hist);                                                \
         break;
-    switch (NS) {
-        HM_H(1) HM_H(2) HM_H(3) HM_H(4) HM_H(5) HM_H(6) HM_H(7) HM_H(8)
+#define HM_HN(K) HM_H(K, 1) HM_H(K, 2) HM_H(K, 4)
+    switch (NS * 100 + FG / 4) {
+        HM_HN(1) HM_HN(2) HM_HN(3) HM_HN(4) HM_HN(5) HM_HN(6) HM_HN(7) HM_HN(8)
+        default: return (int)hipErrorInvalidValue;
     }
+#undef HM_HN
 #undef HM_H
     HM_LAUNCH_RET();
 }

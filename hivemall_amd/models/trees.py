@@ -34,6 +34,7 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import Learner, log
 
 MODEL_VERSION = 1
+HIST_BLOCKS = 1024   # histogram grid (blocks per feature group); see benchmarks/hist_sweep.py
 
 
 # ------------------------------------------------------------------ quantisation
@@ -64,7 +65,7 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
         E = torch.nan_to_num(E, nan=float("inf"))
         # strictly increasing edges (ties collapse to the same bin)
         edges = E.contiguous()
-    dpad = (d + 3) // 4 * 4
+    dpad = (d + 15) // 16 * 16   # 16-byte rows: a feature group is one aligned load
     bins = torch.zeros((n, dpad), dtype=torch.uint8, device=X.device)
     p = _native.ptr
     args = (p(X), C.c_int64(n), d, dpad, p(edges), edges.shape[1], p(bins))
@@ -106,8 +107,8 @@ class Tree:
         k = 0
         while self.feature[k] >= 0:
             v = x[self.feature[k]]
-            k = self.left[k] if (v is None or (isinstance(v, float) and math.isnan(v)) or
-                                 v <= self.threshold[k]) else self.right[k]
+            # missing / NaN goes right, as in Smile's `x <= t ? trueChild : falseChild`
+            k = self.left[k] if (v is not None and v <= self.threshold[k]) else self.right[k]
         return self.value[k]
 
     def depth(self) -> int:
@@ -202,26 +203,31 @@ class HistTreeBuilder:
             return S[..., 1]
         return S[..., 2]
 
-    def _leaf_value(self, S: np.ndarray) -> list:
+    def _leaf_values(self, S: torch.Tensor) -> torch.Tensor:
+        """Leaf outputs for node statistics S [L, NS] -> [L, n_out]."""
         c = self.criterion
         if c in ("gini", "entropy"):
-            w = S.sum()
-            return (S / w).tolist() if w > 0 else [1.0 / len(S)] * len(S)
+            w = S.sum(1, keepdim=True)
+            return torch.where(w > 0, S / w.clamp_min(1e-30), torch.full_like(S, 1.0 / S.shape[1]))
         if c == "variance":
-            return [float(S[0] / S[1]) if S[1] > 0 else 0.0]
-        return [float(S[0] / S[1]) if abs(S[1]) > 1e-12 else 0.0]
+            return torch.where(S[:, 1:2] > 0, S[:, 0:1] / S[:, 1:2].clamp_min(1e-30), torch.zeros_like(S[:, :1]))
+        ok = S[:, 1:2].abs() > 1e-12
+        return torch.where(ok, S[:, 0:1] / torch.where(ok, S[:, 1:2], torch.ones_like(S[:, 1:2])),
+                           torch.zeros_like(S[:, :1]))
 
-    def _hist(self, rows, seg, n_nodes, max_seg, stats):
+    def _hist(self, rows, seg, n_seg, stats):
+        """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
         q = self.q
         NS = stats.shape[1]
         dev = stats.device
-        hist = torch.zeros((n_nodes, q.d, q.B, NS), dtype=torch.float32, device=dev)
-        FG = max(1, min(q.d, (48 * 1024) // (q.B * NS * 4)))
+        hist = torch.zeros((n_seg, q.d, q.B, NS), dtype=torch.float32, device=dev)
+        # feature groups: multiple of 4 features, LDS image <= 48 KB, balanced over the groups
+        # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB
+        FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
         p = _native.ptr
-        args = (p(q.bins), C.c_int64(q.bins.shape[0]), q.d, q.dpad, q.B, p(rows), p(seg), None,
-                n_nodes, C.c_int64(max_seg), p(stats), NS, FG, p(hist))
+        args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), NS, FG, p(hist))
         if dev.type == "cuda":
-            _native.check(_native.hip().hm_hist_build(*args, _native.stream_of(dev)), "hm_hist_build")
+            _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)), "hm_hist_build")
         else:
             _native.host().hm_hist_build_cpu(*args)
         if self.mixer is not None and self.mixer.world > 1:
@@ -229,110 +235,125 @@ class HistTreeBuilder:
         return hist
 
     def build(self, stats: torch.Tensor, active: torch.Tensor | None = None) -> Tree:
-        """stats: f32 [n, NS] per-row statistics (zero rows are ignored)."""
+        """Grow one tree level by level.  stats: f32 [n, NS] per-row statistics.
+
+        Every level: split search on the device over the level's histograms; one host sync
+        (the number of splits); rows routed by the bins; the next level histograms only the
+        smaller child of each split (sibling = parent - child).  After the call
+        ``self.leaf_of_row`` holds the leaf node id of every row (-1: inactive)."""
         q = self.q
         dev = stats.device
-        n = stats.shape[0]
+        n, NS = stats.shape
+        d, B = q.d, q.B
         stats = stats.contiguous()
         node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
+        act = (stats != 0).any(1)
         if active is not None:
             node_of_row[~active] = -1
-        tree = Tree(n_out=stats.shape[1] if self.criterion in ("gini", "entropy") else 1)
-        tree.feature.append(-1)
-        tree.threshold.append(math.inf)
-        tree.left.append(-1)
-        tree.right.append(-1)
-        tree.value.append(None)
-        level = [0]
-        totals = {0: stats[node_of_row >= 0].sum(0).double().cpu().numpy()}
-        n_leaves = 1
-        for depth in range(self.max_depth + 1):
-            if not level:
+            act &= active
+        act_rows = torch.nonzero(act).flatten().to(torch.int32)
+        gen = torch.Generator(device=dev).manual_seed(int(self.gen.initial_seed()))
+        edges = q.edges.to(dev)
+        n_out = NS if self.criterion in ("gini", "entropy") else 1
+        imp = torch.zeros(d, dtype=torch.float64, device=dev)
+        # level 0: the root histogram over every active row
+        seg = torch.stack([torch.zeros((), dtype=torch.int64, device=dev),
+                           torch.full((), act_rows.numel(), dtype=torch.int64, device=dev)])
+        H = self._hist(act_rows, seg, 1, stats)
+        base, L = 0, 1
+        n_leaves = torch.ones((), dtype=torch.int64, device=dev)
+        feats, thrs, lefts, rights, vals = [], [], [], [], []
+        sf_all = torch.zeros(0, dtype=torch.int32, device=dev)
+        sb_all, lc_all, rc_all = sf_all.clone(), sf_all.clone(), sf_all.clone()
+        depth = 0
+        while True:
+            tot = H[:, 0].sum(1)                                               # [L, NS]
+            vals.append(self._leaf_values(tot))
+            lidx = torch.arange(L, device=dev)
+            if depth >= self.max_depth:
+                feats.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
+                thrs.append(torch.full((L,), math.inf, device=dev))
+                lefts.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
+                rights.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 break
-            if depth == self.max_depth:
-                for nd in level:
-                    tree.value[nd] = self._leaf_value(totals[nd])
+            cum = torch.cumsum(H, dim=2)
+            right = tot[:, None, None, :] - cum
+            gain = self._score(cum) + self._score(right) - self._score(tot)[:, None, None]
+            cnt_ok = (self._weight(cum) >= self.min_leaf) & (self._weight(right) >= self.min_leaf)
+            gain = torch.where(cnt_ok, gain, torch.full_like(gain, -math.inf))
+            if self.mtry is not None and self.mtry < d:
+                pick = torch.rand((L, d), generator=gen, device=dev).topk(self.mtry, 1).indices
+                fm = torch.zeros((L, d), dtype=torch.bool, device=dev).scatter_(1, pick, True)
+                gain = torch.where(fm[:, :, None], gain, torch.full_like(gain, -math.inf))
+            best_gain, best = gain.reshape(L, -1).max(1)
+            ok = (best_gain > 1e-12) & torch.isfinite(best_gain) & (self._weight(tot) >= self.min_split)
+            if self.max_leaves is not None:
+                ok &= torch.cumsum(ok.long(), 0) <= (int(self.max_leaves) - n_leaves)
+            n_split = int(ok.sum().item())                                     # the level's one sync
+            bf = (best // B).to(torch.int32)
+            bb = (best % B).to(torch.int32)
+            rank = torch.cumsum(ok.int(), 0) - 1
+            nb = base + L
+            lc = torch.where(ok, nb + 2 * rank, torch.full_like(rank, -1)).to(torch.int32)
+            rc = torch.where(ok, lc + 1, lc).to(torch.int32)
+            thr = torch.where(bb < edges.shape[1], edges[bf.long(), bb.clamp(max=edges.shape[1] - 1).long()],
+                              torch.full_like(best_gain, math.inf))
+            feats.append(torch.where(ok, bf, torch.full_like(bf, -1)))
+            thrs.append(torch.where(ok, thr, torch.full_like(thr, math.inf)))
+            lefts.append(lc)
+            rights.append(rc)
+            if n_split == 0:
                 break
-            # group the level's rows by node
-            lut = torch.full((len(tree.feature),), -1, dtype=torch.int64, device=dev)
-            lut[torch.tensor(level, device=dev)] = torch.arange(len(level), device=dev)
-            loc = torch.where(node_of_row >= 0, lut[node_of_row.clamp_min(0).long()],
-                              torch.full_like(node_of_row, -1, dtype=torch.int64))
-            sel = torch.nonzero(loc >= 0).flatten()
-            order = torch.argsort(loc[sel], stable=True)
-            rows = sel[order].to(torch.int32).contiguous()
-            counts = torch.bincount(loc[sel], minlength=len(level))
-            seg = torch.zeros(len(level) + 1, dtype=torch.int64, device=dev)
-            seg[1:] = torch.cumsum(counts, 0)
-            max_seg = int(counts.max().item()) if counts.numel() else 0
-            hist = self._hist(rows, seg, len(level), max_seg, stats)       # [L, d, B, NS]
-            cum = torch.cumsum(hist, dim=2)
-            tot = cum[:, :, -1:, :]
-            left, right = cum, tot - cum
-            parent = self._score(tot[:, 0, 0, :])                           # [L]
-            gain = self._score(left) + self._score(right) - parent[:, None, None]
-            wl, wr = self._weight(left), self._weight(right)
-            cnt_ok = (wl >= self.min_leaf) & (wr >= self.min_leaf)
-            gain = torch.where(cnt_ok, gain, torch.full_like(gain, -float("inf")))
-            if self.mtry is not None and self.mtry < q.d:
-                fm = torch.zeros((len(level), q.d), dtype=torch.bool)
-                for li in range(len(level)):
-                    fm[li, torch.randperm(q.d, generator=self.gen)[: self.mtry]] = True
-                gain = torch.where(fm.to(dev)[:, :, None], gain, torch.full_like(gain, -float("inf")))
-            flat = gain.reshape(len(level), -1)
-            best_gain, best = flat.max(1)
-            best_gain = best_gain.cpu().numpy()
-            best = best.cpu().numpy()
-            node_tot = tot[:, 0, 0, :].double().cpu().numpy()
-            node_w = self._weight(tot[:, 0, 0, :]).cpu().numpy()
-            # children statistics of the chosen splits
-            li = torch.arange(len(level), device=dev)
-            bf = torch.as_tensor(best // q.B, device=dev)
-            bb = torch.as_tensor(best % q.B, device=dev)
-            left_tot = left[li, bf, bb].double().cpu().numpy()
-            split_feat = torch.full((len(tree.feature) + 2 * len(level),), -1, dtype=torch.int32)
-            split_bin = torch.zeros_like(split_feat)
-            lch = torch.zeros_like(split_feat)
-            rch = torch.zeros_like(split_feat)
-            nxt = []
-            for k, nd in enumerate(level):
-                ok = (best_gain[k] > 1e-12 and np.isfinite(best_gain[k]) and node_w[k] >= self.min_split
-                      and (self.max_leaves is None or n_leaves < self.max_leaves))
-                if not ok:
-                    tree.value[nd] = self._leaf_value(node_tot[k])
-                    continue
-                f, b = int(best[k] // q.B), int(best[k] % q.B)
-                thr = float(q.edges[f, b].item()) if b < q.edges.shape[1] else math.inf
-                tree.feature[nd] = f
-                tree.threshold[nd] = thr
-                self.importance[f] += float(best_gain[k])
-                for side in ("l", "r"):
-                    tree.feature.append(-1)
-                    tree.threshold.append(math.inf)
-                    tree.left.append(-1)
-                    tree.right.append(-1)
-                    tree.value.append(None)
-                lc, rc = len(tree.feature) - 2, len(tree.feature) - 1
-                tree.left[nd], tree.right[nd] = lc, rc
-                totals[lc] = left_tot[k]
-                totals[rc] = node_tot[k] - left_tot[k]
-                split_feat[nd], split_bin[nd], lch[nd], rch[nd] = f, b, lc, rc
-                nxt += [lc, rc]
-                n_leaves += 1
-            if not nxt:
-                break
-            n_all = len(tree.feature)
-            sf, sb, lc_, rc_ = (t[:n_all].to(dev).contiguous() for t in (split_feat, split_bin, lch, rch))
+            imp.index_add_(0, bf[ok].long(), best_gain[ok].double())
+            n_leaves = n_leaves + n_split
+            # route every row one level down (leaves keep their id: split_feat < 0)
+            sf_all = torch.cat([sf_all, feats[-1]])
+            sb_all = torch.cat([sb_all, bb])
+            lc_all = torch.cat([lc_all, lc])
+            rc_all = torch.cat([rc_all, rc])
             p = _native.ptr
-            args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf), p(sb), p(lc_), p(rc_))
+            args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all))
             if dev.type == "cuda":
                 _native.check(_native.hip().hm_route_rows(*args, _native.stream_of(dev)), "hm_route_rows")
             else:
                 _native.host().hm_route_rows_cpu(*args)
-            level = nxt
-        for k in range(len(tree.feature)):
-            if tree.feature[k] < 0 and tree.value[k] is None:
-                tree.value[k] = self._leaf_value(totals.get(k, np.zeros(stats.shape[1])))
+            # next level: histogram the smaller child of every split, derive the sibling
+            li = lidx[ok]
+            left_tot = cum[li, bf[ok].long(), bb[ok].long()]                   # [S, NS]
+            right_tot = tot[ok] - left_tot
+            small_right = self._weight(right_tot) < self._weight(left_tot)     # [S]
+            small_id = torch.where(small_right, rc[ok], lc[ok]) - nb           # local child id
+            lut = torch.full((2 * n_split,), 32767, dtype=torch.int16, device=dev)
+            lut[small_id.long()] = torch.arange(n_split, device=dev, dtype=torch.int16)
+            nr = node_of_row[act_rows.long()] - nb
+            key = torch.where(nr >= 0, lut[nr.clamp_min(0).long()], torch.full_like(nr, 32767, dtype=torch.int16))
+            skey, order = torch.sort(key, stable=True)
+            rows = act_rows[order].contiguous()
+            seg = torch.searchsorted(skey, torch.arange(n_split + 1, device=dev, dtype=torch.int16)).to(torch.int64)
+            Hs = self._hist(rows, seg.contiguous(), n_split, stats)
+            Hp = H[li]
+            Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
+            sr = small_right.long()
+            j2 = 2 * torch.arange(n_split, device=dev)
+            Hn[j2 + sr] = Hs
+            Hn[j2 + 1 - sr] = Hp - Hs
+            H = Hn
+            base, L = nb, 2 * n_split
+            depth += 1
+        self.importance = self.importance + imp.cpu().numpy()
+        self.leaf_of_row = node_of_row
+        F = torch.cat(feats).cpu().numpy()
+        T = torch.cat(thrs).cpu().numpy()
+        Lc = torch.cat(lefts).cpu().numpy()
+        Rc = torch.cat(rights).cpu().numpy()
+        V = torch.cat(vals).double().cpu().numpy()
+        self.node_values = torch.cat(vals)
+        tree = Tree(n_out=n_out)
+        tree.feature = [int(f) for f in F]
+        tree.threshold = [float(t) for t in T]
+        tree.left = [int(x) for x in Lc]
+        tree.right = [int(x) for x in Rc]
+        tree.value = [None if F[k] >= 0 else V[k].tolist() for k in range(len(F))]
         return tree
 
 
@@ -378,8 +399,12 @@ def _to_dense(features, d=None) -> np.ndarray:
     return np.asarray([list(r) for r in rows], dtype=np.float32)
 
 
-def _encode_classes(yl: np.ndarray):
-    """Sorted distinct labels (python scalars) and the int64 class index of every row."""
+def _encode_classes(yl):
+    """Sorted distinct labels (python scalars) and the int64 class index of every row
+    (on the labels' device when given a tensor)."""
+    if torch.is_tensor(yl):
+        cls, inv = torch.unique(yl.reshape(-1), sorted=True, return_inverse=True)
+        return cls.cpu().tolist(), inv.to(torch.int64)
     cls, inv = np.unique(np.asarray(yl).reshape(-1), return_inverse=True)
     return cls.tolist(), torch.from_numpy(inv.astype(np.int64))
 
@@ -410,7 +435,7 @@ class _ForestBase(Learner):
         n, d = X.shape
         c = self.cl
         if self.TASK == "classification":
-            cls, yi = _encode_classes(y.cpu().numpy())
+            cls, yi = _encode_classes(y)
             self.classes = cls
             yi = yi.to(self.device)
             onehot = torch.nn.functional.one_hot(yi, len(self.classes)).float()
@@ -420,14 +445,15 @@ class _ForestBase(Learner):
             yf = y.float()
             crit = "variance"
             mtry = c["mtry"] or max(1, d // 3)
-        g = torch.Generator(device="cpu").manual_seed(self.seed)
+        g = torch.Generator(device=self.device).manual_seed(self.seed)
         world = self.mixer.world if self.mixer is not None else 1
         rank = self.rank
         T = int(c["trees"])
         my = [t for t in range(T) if t % world == rank]
         for t in my:
             m = max(1, int(round(n * float(c["subsample"]))))
-            draw = torch.randint(0, n, (m,), generator=g).to(self.device)
+            g.manual_seed(self.seed * 1000003 + t)   # tree t's bootstrap does not depend on the rank split
+            draw = torch.randint(0, n, (m,), generator=g, device=self.device)
             w = torch.bincount(draw, minlength=n).float()
             if self.TASK == "classification":
                 if onehot.shape[1] > 8:
@@ -440,10 +466,11 @@ class _ForestBase(Learner):
             tree = b.build(stats)
             self.trees.append(tree)
             self.importances.append(b.importance)
+            # out-of-bag error from the leaf every row was routed to while growing
             oob = w == 0
             no = int(oob.sum().item())
             if no:
-                out = predict_forest([tree], X[oob])
+                out = b.node_values[b.leaf_of_row[oob].long()]
                 if self.TASK == "classification":
                     err = int((out.argmax(1) != yi[oob]).sum().item())
                 else:
@@ -523,14 +550,13 @@ class GradientTreeBoostingClassifier(Learner):
         c = self.cl
         X = features if torch.is_tensor(features) else torch.from_numpy(_to_dense(features))
         X = X.float().to(self.device)
-        yl = labels.cpu().numpy() if torch.is_tensor(labels) else np.asarray(labels)
-        self.classes, yi = _encode_classes(yl)
+        self.classes, yi = _encode_classes(labels if torch.is_tensor(labels) else np.asarray(labels))
         yi = yi.to(self.device)
         K = len(self.classes)
         n, d = X.shape
         q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed)
         self.importance = np.zeros(d)
-        g = torch.Generator(device="cpu").manual_seed(self.seed)
+        g = torch.Generator(device=self.device).manual_seed(self.seed)
         eta = float(c["eta"])
         if K == 2:
             pos = float((yi == 1).float().mean().item())
@@ -547,9 +573,12 @@ class GradientTreeBoostingClassifier(Learner):
             P = torch.sigmoid(F) if K == 2 else torch.softmax(F, 1)
             R = Y - P
             H = (R.abs() * (1 - R.abs())) if K == 2 else P * (1 - P)
-            sel = torch.randperm(n, generator=g)[:m_sub].to(self.device)
-            mask = torch.zeros(n, dtype=torch.bool, device=self.device)
-            mask[sel] = True
+            if m_sub >= n:
+                mask = torch.ones(n, dtype=torch.bool, device=self.device)
+            else:
+                sel = torch.randperm(n, generator=g, device=self.device)[:m_sub]
+                mask = torch.zeros(n, dtype=torch.bool, device=self.device)
+                mask[sel] = True
             trees = []
             for k in range(R.shape[1]):
                 stats = torch.stack([R[:, k], H[:, k], torch.ones(n, device=self.device)], 1)
@@ -562,7 +591,8 @@ class GradientTreeBoostingClassifier(Learner):
                     tree.value = [[v[0] * (K - 1) / K] if v is not None else None for v in tree.value]
                 trees.append(tree)
                 self.importance += b.importance
-                F[:, k] += eta * predict_forest([tree], X)[:, 0]
+                # every row (sampled or not) was routed to its leaf while the tree grew
+                F[:, k] += eta * b.node_values[b.leaf_of_row.long(), 0] * ((K - 1) / K if K > 2 else 1.0)
             self.iters.append(trees)
             oob = ~mask
             if oob.any():
@@ -735,10 +765,10 @@ def register_sql(reg):
 
 _P = _native.c_p
 _I64 = _native.c_i64
-_native.register_hip("hm_hist_build", [_P, _I64, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int, _I64,
-                                       _P, C.c_int, C.c_int, _P, _P])
-_native.register_host("hm_hist_build_cpu", [_P, _I64, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int,
-                                            _I64, _P, C.c_int, C.c_int, _P])
+_native.register_hip("hm_hist_build", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, C.c_int, C.c_int,
+                                       _P, C.c_int, _P])
+_native.register_host("hm_hist_build_cpu", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, C.c_int,
+                                            C.c_int, _P])
 _native.register_hip("hm_tree_predict", [_P, _I64, C.c_int] + [_P] * 7 + [C.c_int, C.c_int, _P, C.c_int,
                                                                           _P, _P])
 _native.register_host("hm_tree_predict_cpu", [_P, _I64, C.c_int] + [_P] * 7 + [C.c_int, C.c_int, _P,

@@ -115,3 +115,77 @@ def test_rf_gpu_quality(higgs):
         rf = RandomForestClassifier("-trees 10 -max_depth 10 -seed 3", device=dev).fit(X, y)
         aucs[dev] = roc_auc_score(yt.numpy(), rf.predict_proba(Xt)[:, 1])
     assert abs(aucs["cpu"] - aucs["cuda"]) < 0.01, aucs
+
+
+def _leaf_vs_predict(dev):
+    from hivemall_amd.models.trees import HistTreeBuilder, predict_forest
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(20000, 9, generator=g)
+    X[torch.rand(20000, 9, generator=g) < 0.05] = float("nan")          # missing values go right
+    y = (torch.nan_to_num(X[:, 0]) * torch.nan_to_num(X[:, 1]) > 0).float()
+    X = X.to(dev)
+    q = quantize(X, 64)
+    st = torch.stack([y - 0.5, torch.full_like(y, 0.25), torch.ones_like(y)], 1).to(dev)
+    st[::7] = 0                                                           # unsampled rows are routed too
+    b = HistTreeBuilder(q, "gbt", max_depth=6, seed=1)
+    tree = b.build(st)
+    via_leaf = b.node_values[b.leaf_of_row.long(), 0]
+    via_pred = predict_forest([tree], X)[:, 0]
+    torch.testing.assert_close(via_leaf, via_pred)
+    assert tree.depth() == 6
+
+
+def test_builder_leaf_routing_matches_predict():
+    _leaf_vs_predict("cpu")
+
+
+@pytest.mark.gpu
+def test_builder_leaf_routing_matches_predict_gpu():
+    _leaf_vs_predict("cuda")
+
+
+def _hist_case():
+    g = torch.Generator().manual_seed(1)
+    n, d, dpad, B, NS = 300000, 27, 32, 256, 3
+    bins = torch.zeros(n, dpad, dtype=torch.uint8)
+    bins[:, :d] = torch.randint(0, B, (n, d), generator=g, dtype=torch.uint8)
+    stats = torch.randn(n, NS, generator=g)
+    sizes = torch.tensor([150000, 3, 0, 70, 100000, 1, 500, 20000])
+    rows = torch.randperm(n, generator=g)[: int(sizes.sum())].to(torch.int32)
+    seg = torch.zeros(len(sizes) + 1, dtype=torch.int64)
+    seg[1:] = torch.cumsum(sizes, 0)
+    S = len(sizes)
+    ref = torch.zeros(S * d * B * NS, dtype=torch.float64)
+    node = torch.repeat_interleave(torch.arange(S), sizes)
+    for f in range(d):
+        for s in range(NS):
+            idx = ((node * d + f) * B + bins[rows.long(), f].long()) * NS + s
+            ref.index_add_(0, idx, stats[rows.long(), s].double())
+    return (bins, rows, seg, stats), ref.view(S, d, B, NS), (d, dpad, B, NS, S)
+
+
+def _run_hist(dev, FG):
+    from hivemall_amd import _native
+    (bins, rows, seg, stats), ref, (d, dpad, B, NS, S) = _hist_case()
+    hb, hr, hs, hst = (t.to(dev) for t in (bins, rows, seg, stats))
+    out = torch.zeros(S, d, B, NS, device=dev)
+    p = _native.ptr
+    args = (p(hb), d, dpad, B, p(hr), p(hs), S, p(hst), NS, FG, p(out))
+    gargs = args + (0,)
+    if dev == "cuda":
+        _native.check(_native.hip().hm_hist_build(*gargs, _native.stream_of(torch.device(dev))), "hm_hist_build")
+    else:
+        assert _native.host().hm_hist_build_cpu(*args) == 0
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-4, atol=2e-3)
+
+
+def test_hist_cpu_segments_vs_torch():
+    _run_hist("cpu", 16)
+
+
+@pytest.mark.gpu
+def test_hist_kernel_segments_vs_torch():
+    """Segmented histogram kernel (LDS path for large segments, global path for small ones)
+    against a torch fp64 scatter-add reference; two feature-group widths."""
+    for FG in (16, 8, 4):
+        _run_hist("cuda", FG)
