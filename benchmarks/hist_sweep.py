@@ -20,6 +20,7 @@ def run(n=11_000_000, d=28, NS=3, B=256):
     dpad = (d + 15) // 16 * 16
     bins = torch.randint(0, B, (n, dpad), generator=g, device=dev, dtype=torch.uint8)
     stats = torch.randn(n, NS, generator=g, device=dev)
+    smax = stats.abs().amax(0).contiguous()
     rows_all = torch.arange(n, dtype=torch.int32, device=dev)
     cases = {"root": (rows_all, torch.tensor([0, n], device=dev), 1)}
     S = 256
@@ -34,7 +35,7 @@ def run(n=11_000_000, d=28, NS=3, B=256):
         for FG in (16, 8):
             for nblk in (128, 256, 512, 768, 1024, 2048, 4096):
                 out = torch.zeros(ns, d, B, NS, device=dev)
-                args = (p(bins), d, dpad, B, p(r), p(sg), ns, p(stats), NS, FG, p(out), nblk,
+                args = (p(bins), d, dpad, B, p(r), p(sg), ns, p(stats), p(smax), NS, FG, p(out), nblk,
                         _native.stream_of(dev))
                 for _ in range(2):
                     _native.check(_native.hip().hm_hist_build(*args), "hist")

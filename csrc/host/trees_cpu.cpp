@@ -7,9 +7,9 @@
 #define HM_API extern "C" __attribute__((visibility("default")))
 
 HM_API int hm_hist_build_cpu(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
-                             const int64_t* seg, int n_seg, const float* stats, int NS, int FG,
-                             float* hist) {
-    (void)FG;
+                             const int64_t* seg, int n_seg, const float* stats, const float* smax,
+                             int NS, int FG, float* hist) {
+    (void)FG; (void)smax;  // exact fp32 sums on the host
 #pragma omp parallel for schedule(dynamic, 1) collapse(2)
     for (int node = 0; node < n_seg; ++node) {
         for (int f = 0; f < d; ++f) {

@@ -13,16 +13,18 @@
 //   node k).  A fixed grid of blocks splits the position range [seg[0], seg[S]) into equal
 //   chunks (the host never has to know the row count: no sync before the launch); a block walks
 //   the node segments its chunk overlaps.  Per (block, node) piece: a large piece privatises the
-//   feature group's histogram in LDS, laid out [f][s][b] so the 64 lanes of one ds_add_f32 hit
-//   banks by bin, and flushes the non-zero bins with global float atomics; a small piece (deep
-//   levels: few rows per node) adds straight to global memory, so zeroing and scanning a 48 KB
-//   LDS image is not paid for a handful of rows.  Feature groups (FG a multiple of 4) keep the
-//   LDS image <= 48 KB so three blocks share a CU; bins are read as 32-bit words.
-//   The tree builder only histograms the smaller child of every split and derives the sibling
-//   as parent - child (models/trees.py).
-// tree_predict: one lane per (row, tree); trees are flattened SoA arrays
-//   (feature, threshold, left, right, value offset) so a traversal is a chain of coalesced-ish
-//   16-B loads that stay in L2 for forests of a few MB.
+//   feature group's histogram in LDS, laid out [f][s][b], as 32-bit FIXED-POINT sums
+//   (ds_add_u32), and flushes the non-zero bins to the fp32 global histogram with float atomics;
+//   a small piece (deep levels: few rows per node) adds straight to global memory.
+//   Why fixed point: on gfx950 ds_add_f32 retires 0.33 lane-ops per CU-clock whatever the
+//   address pattern, ds_add_u32 3.5 (random bins) to 8.4 (distinct addresses) — measured by
+//   benchmarks/probes/lds_atomic_probe.hip (profiles/lds_atomic_probe_r1.jsonl).  The scale per
+//   statistic is a power of two chosen in-kernel from the block's chunk length and max|stat|
+//   (device array), so a block's partial sum cannot overflow 2^31; quantisation error per row
+//   is <= max|stat| * 2^-17 at the root of an 11M-row HIGGS level.
+//   Feature groups (4/8/16 features, one aligned load of the row's bins) keep the LDS image
+//   <= 48 KB so three blocks share a CU.  The tree builder only histograms the smaller child of
+//   every split and derives the sibling as parent - child (models/trees.py).
 #include "common.h"
 
 namespace {
@@ -41,7 +43,7 @@ template <int NS, int FGW, bool GLOBAL>
 __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int dpad, int f0, int nf,
                                           int B, const int32_t* __restrict__ rows,
                                           const float* __restrict__ stats, int64_t s0, int64_t s1,
-                                          float* __restrict__ h) {
+                                          float* __restrict__ h, const float* scale) {
     using W = typename BinWords<FGW>::T;
     for (int64_t q0 = s0 + threadIdx.x; q0 < s1; q0 += (int64_t)blockDim.x * HIST_U) {
         int64_t r[HIST_U];
@@ -79,7 +81,8 @@ __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int 
                         if constexpr (GLOBAL) {
                             if (st[u][s] != 0.f) atomicAdd(h + ((size_t)j * B + bin) * NS + s, st[u][s]);
                         } else {
-                            atomicAdd(h + (j * NS + s) * B + bin, st[u][s]);
+                            atomicAdd(reinterpret_cast<int*>(h) + (j * NS + s) * B + bin,
+                                      __float2int_rn(st[u][s] * scale[s]));
                         }
                     }
                 }
@@ -93,6 +96,7 @@ __global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ b
                                                    int B, const int32_t* __restrict__ rows,
                                                    const int64_t* __restrict__ seg, int n_seg,
                                                    const float* __restrict__ stats,
+                                                   const float* __restrict__ smax,
                                                    float* __restrict__ hist) {
     constexpr int FG = FGW * 4;
     extern __shared__ __attribute__((aligned(16))) float s_hist[];
@@ -105,6 +109,15 @@ __global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ b
     const int64_t p0 = lo + (int64_t)blockIdx.x * chunk;
     const int64_t p1 = min(hi, p0 + chunk);
     if (p0 >= p1) return;
+    // fixed-point scale per statistic: chunk * max|stat| * scale <= 2^30
+    float scale[NS], inv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const float m = fmaxf(smax[s], 1e-30f) * (float)chunk;
+        const float e = fminf(fmaxf(floorf(log2f(1073741824.f / m)), -60.f), 60.f);
+        scale[s] = exp2f(e);
+        inv[s] = exp2f(-e);
+    }
     // first node whose segment ends after p0
     int a = 0, b = n_seg - 1;
     while (a < b) {
@@ -112,30 +125,55 @@ __global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ b
         if (seg[m + 1] <= p0) a = m + 1; else b = m;
     }
     const int hsz = nf * NS * B;
+    int* s_int = reinterpret_cast<int*>(s_hist);
     for (int k = a; k < n_seg; ++k) {
         if (seg[k] >= p1) break;
         const int64_t s0 = max(p0, seg[k]), s1 = min(p1, seg[k + 1]);
         if (s0 >= s1) continue;
         float* gh = hist + ((size_t)k * d + f0) * B * NS;
         if ((s1 - s0) * nf * 4 < hsz) {  // few rows: straight to global memory
-            hist_rows<NS, FGW, true>(bins, dpad, f0, nf, B, rows, stats, s0, s1, gh);
+            hist_rows<NS, FGW, true>(bins, dpad, f0, nf, B, rows, stats, s0, s1, gh, scale);
             continue;
         }
-        for (int i = threadIdx.x; i < hsz; i += blockDim.x) s_hist[i] = 0.f;
+        for (int i = threadIdx.x; i < hsz; i += blockDim.x) s_int[i] = 0;
         __syncthreads();
-        hist_rows<NS, FGW, false>(bins, dpad, f0, nf, B, rows, stats, s0, s1, s_hist);
+        hist_rows<NS, FGW, false>(bins, dpad, f0, nf, B, rows, stats, s0, s1, s_hist, scale);
         __syncthreads();
         for (int i = threadIdx.x; i < hsz; i += blockDim.x) {
-            const float v = s_hist[i];
-            if (v != 0.f) {
+            const int v = s_int[i];
+            if (v != 0) {
                 const int f = i / (NS * B);
                 const int rem = i - f * NS * B;
                 const int s = rem / B;
                 const int bin = rem - s * B;
-                atomicAdd(gh + ((size_t)f * B + bin) * NS + s, v);
+                float iv = inv[0];
+#pragma unroll
+                for (int t = 1; t < NS; ++t) iv = s == t ? inv[t] : iv;
+                atomicAdd(gh + ((size_t)f * B + bin) * NS + s, (float)v * iv);
             }
         }
         __syncthreads();
+    }
+}
+
+// out[s] = max_r |stats[r, s]| (out zeroed by the caller): non-negative floats order like their
+// bit patterns, so a block max finishes with one integer atomicMax per column.
+template <int NS>
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ stats, int64_t n,
+                                                     float* __restrict__ out) {
+    float m[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) m[s] = 0.f;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) m[s] = fmaxf(m[s], fabsf(stats[r * NS + s]));
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        float v = m[s];
+        for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+        if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(out) + s, __float_as_int(v));
     }
 }
 
@@ -222,9 +260,10 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
 // hist [n_seg, d, B, NS] (zeroed by the caller) += statistics of rows[seg[k]..seg[k+1]) for
 // every node k.  seg lives on the device.  FG (features per group) is 4, 8 or 16 and bins rows
 // are padded to a multiple of 16 bytes, so a row's group is one aligned 4/8/16-byte load.
+// smax: device [NS] upper bounds of |stats[:, s]| (fixed-point scaling of the LDS sums).
 HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
-                         const int64_t* seg, int n_seg, const float* stats, int NS, int FG,
-                         float* hist, int nblk, hipStream_t stream) {
+                         const int64_t* seg, int n_seg, const float* stats, const float* smax,
+                         int NS, int FG, float* hist, int nblk, hipStream_t stream) {
     if (n_seg <= 0) return 0;
     if (nblk <= 0) nblk = 1024;
     if (B > 256 || NS <= 0 || NS > 8 || (FG != 4 && FG != 8 && FG != 16) || (dpad & 15))
@@ -235,7 +274,7 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
 #define HM_H(K, W)                                                                                  \
     case K * 100 + W:                                                                               \
         hipLaunchKernelGGL((hist_kernel<K, W>), grid, dim3(256), lds, stream, bins, d, dpad, B, rows, \
-                           seg, n_seg, stats, hist);                                                \
+                           seg, n_seg, stats, smax, hist);                                          \
         break;
 #define HM_HN(K) HM_H(K, 1) HM_H(K, 2) HM_H(K, 4)
     switch (NS * 100 + FG / 4) {
@@ -244,6 +283,20 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
     }
 #undef HM_HN
 #undef HM_H
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_absmax_cols(const float* stats, int64_t n, int NS, float* out, hipStream_t stream) {
+    if (n <= 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+#define HM_A(K) \
+    case K: hipLaunchKernelGGL((absmax_kernel<K>), dim3((int)blocks), dim3(256), 0, stream, stats, n, out); break;
+    switch (NS) {
+        HM_A(1) HM_A(2) HM_A(3) HM_A(4) HM_A(5) HM_A(6) HM_A(7) HM_A(8)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HM_A
     HM_LAUNCH_RET();
 }
 

@@ -34,7 +34,7 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import Learner, log
 
 MODEL_VERSION = 1
-HIST_BLOCKS = 1024   # histogram grid (blocks per feature group); see benchmarks/hist_sweep.py
+HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
 
 
 # ------------------------------------------------------------------ quantisation
@@ -58,7 +58,7 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
     B = int(num_bins)
     if edges is None:
         g = torch.Generator(device="cpu").manual_seed(seed)
-        idx = torch.randperm(n, generator=g)[: min(n, sample)].to(X.device)
+        idx = (torch.arange(n) if n <= sample else torch.randint(0, n, (sample,), generator=g)).to(X.device)
         S = X[idx]
         qs = torch.linspace(0, 1, B + 1, device=X.device)[1:-1]
         E = torch.quantile(S.T.contiguous(), qs, dim=1).T.contiguous()     # [d, B-1]
@@ -215,7 +215,7 @@ class HistTreeBuilder:
         return torch.where(ok, S[:, 0:1] / torch.where(ok, S[:, 1:2], torch.ones_like(S[:, 1:2])),
                            torch.zeros_like(S[:, :1]))
 
-    def _hist(self, rows, seg, n_seg, stats):
+    def _hist(self, rows, seg, n_seg, stats, smax):
         """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
         q = self.q
         NS = stats.shape[1]
@@ -225,7 +225,7 @@ class HistTreeBuilder:
         # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB
         FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
         p = _native.ptr
-        args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), NS, FG, p(hist))
+        args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), p(smax), NS, FG, p(hist))
         if dev.type == "cuda":
             _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)), "hm_hist_build")
         else:
@@ -259,7 +259,13 @@ class HistTreeBuilder:
         # level 0: the root histogram over every active row
         seg = torch.stack([torch.zeros((), dtype=torch.int64, device=dev),
                            torch.full((), act_rows.numel(), dtype=torch.int64, device=dev)])
-        H = self._hist(act_rows, seg, 1, stats)
+        if dev.type == "cuda" and NS <= 8:                # fixed-point range of the LDS sums
+            smax = torch.zeros(NS, dtype=torch.float32, device=dev)
+            _native.check(_native.hip().hm_absmax_cols(_native.ptr(stats), C.c_int64(n), NS, _native.ptr(smax),
+                                                        _native.stream_of(dev)), "hm_absmax_cols")
+        else:
+            smax = stats.abs().amax(0).contiguous()
+        H = self._hist(act_rows, seg, 1, stats, smax)
         base, L = 0, 1
         n_leaves = torch.ones((), dtype=torch.int64, device=dev)
         feats, thrs, lefts, rights, vals = [], [], [], [], []
@@ -269,7 +275,6 @@ class HistTreeBuilder:
         while True:
             tot = H[:, 0].sum(1)                                               # [L, NS]
             vals.append(self._leaf_values(tot))
-            lidx = torch.arange(L, device=dev)
             if depth >= self.max_depth:
                 feats.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 thrs.append(torch.full((L,), math.inf, device=dev))
@@ -289,7 +294,8 @@ class HistTreeBuilder:
             ok = (best_gain > 1e-12) & torch.isfinite(best_gain) & (self._weight(tot) >= self.min_split)
             if self.max_leaves is not None:
                 ok &= torch.cumsum(ok.long(), 0) <= (int(self.max_leaves) - n_leaves)
-            n_split = int(ok.sum().item())                                     # the level's one sync
+            li = torch.nonzero(ok).flatten()                                   # the level's one sync
+            n_split = li.numel()
             bf = (best // B).to(torch.int32)
             bb = (best % B).to(torch.int32)
             rank = torch.cumsum(ok.int(), 0) - 1
@@ -304,7 +310,7 @@ class HistTreeBuilder:
             rights.append(rc)
             if n_split == 0:
                 break
-            imp.index_add_(0, bf[ok].long(), best_gain[ok].double())
+            imp.index_add_(0, bf[li].long(), best_gain[li].double())
             n_leaves = n_leaves + n_split
             # route every row one level down (leaves keep their id: split_feat < 0)
             sf_all = torch.cat([sf_all, feats[-1]])
@@ -318,11 +324,10 @@ class HistTreeBuilder:
             else:
                 _native.host().hm_route_rows_cpu(*args)
             # next level: histogram the smaller child of every split, derive the sibling
-            li = lidx[ok]
-            left_tot = cum[li, bf[ok].long(), bb[ok].long()]                   # [S, NS]
-            right_tot = tot[ok] - left_tot
+            left_tot = cum[li, bf[li].long(), bb[li].long()]                   # [S, NS]
+            right_tot = tot[li] - left_tot
             small_right = self._weight(right_tot) < self._weight(left_tot)     # [S]
-            small_id = torch.where(small_right, rc[ok], lc[ok]) - nb           # local child id
+            small_id = torch.where(small_right, rc[li], lc[li]) - nb           # local child id
             lut = torch.full((2 * n_split,), 32767, dtype=torch.int16, device=dev)
             lut[small_id.long()] = torch.arange(n_split, device=dev, dtype=torch.int16)
             nr = node_of_row[act_rows.long()] - nb
@@ -330,7 +335,7 @@ class HistTreeBuilder:
             skey, order = torch.sort(key, stable=True)
             rows = act_rows[order].contiguous()
             seg = torch.searchsorted(skey, torch.arange(n_split + 1, device=dev, dtype=torch.int16)).to(torch.int64)
-            Hs = self._hist(rows, seg.contiguous(), n_split, stats)
+            Hs = self._hist(rows, seg.contiguous(), n_split, stats, smax)
             Hp = H[li]
             Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
             sr = small_right.long()
@@ -765,9 +770,9 @@ def register_sql(reg):
 
 _P = _native.c_p
 _I64 = _native.c_i64
-_native.register_hip("hm_hist_build", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, C.c_int, C.c_int,
-                                       _P, C.c_int, _P])
-_native.register_host("hm_hist_build_cpu", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, C.c_int,
+_native.register_hip("hm_hist_build", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, _P, C.c_int,
+                                       C.c_int, _P, C.c_int, _P])
+_native.register_host("hm_hist_build_cpu", [_P, C.c_int, C.c_int, C.c_int, _P, _P, C.c_int, _P, _P, C.c_int,
                                             C.c_int, _P])
 _native.register_hip("hm_tree_predict", [_P, _I64, C.c_int] + [_P] * 7 + [C.c_int, C.c_int, _P, C.c_int,
                                                                           _P, _P])
@@ -775,5 +780,6 @@ _native.register_host("hm_tree_predict_cpu", [_P, _I64, C.c_int] + [_P] * 7 + [C
                                                                                C.c_int, _P])
 _native.register_hip("hm_quantize", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P, _P])
 _native.register_host("hm_quantize_cpu", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P])
+_native.register_hip("hm_absmax_cols", [_P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [_P])
 _native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5)

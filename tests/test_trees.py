@@ -170,7 +170,8 @@ def _run_hist(dev, FG):
     hb, hr, hs, hst = (t.to(dev) for t in (bins, rows, seg, stats))
     out = torch.zeros(S, d, B, NS, device=dev)
     p = _native.ptr
-    args = (p(hb), d, dpad, B, p(hr), p(hs), S, p(hst), NS, FG, p(out))
+    smax = stats.abs().amax(0).to(dev)
+    args = (p(hb), d, dpad, B, p(hr), p(hs), S, p(hst), p(smax), NS, FG, p(out))
     gargs = args + (0,)
     if dev == "cuda":
         _native.check(_native.hip().hm_hist_build(*gargs, _native.stream_of(torch.device(dev))), "hm_hist_build")
