@@ -56,7 +56,7 @@ def _register_learners():
 
 def _optional_learners():
     import importlib
-    for mod in ("mf", "trees", "topicmodel", "recommend", "fm"):
+    for mod in ("mf", "trees", "xgboost", "topicmodel", "recommend", "fm"):
         try:
             m = importlib.import_module(f".models.{mod}", __package__)
         except ModuleNotFoundError as e:

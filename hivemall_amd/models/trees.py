@@ -163,12 +163,21 @@ class HistTreeBuilder:
 
     def __init__(self, q: Quantized, criterion: str, max_depth: int = 12,
                  min_samples_split: int = 2, min_samples_leaf: int = 1, mtry: int | None = None,
-                 max_leaf_nodes: int | None = None, seed: int = 0, mixer=None, lam: float = 0.0):
+                 max_leaf_nodes: int | None = None, seed: int = 0, mixer=None, lam: float = 0.0,
+                 alpha: float = 0.0, min_gain: float = 0.0, feature_mask: torch.Tensor | None = None):
         self.q = q
         self.criterion = criterion
         self.max_depth = max_depth
-        self.min_split = max(2, int(min_samples_split))
-        self.min_leaf = max(1, int(min_samples_leaf))
+        if criterion == "xgb":
+            # second-order statistics (g, h): min_samples_* are hessian weights (min_child_weight)
+            self.min_split = float(min_samples_split)
+            self.min_leaf = float(min_samples_leaf)
+        else:
+            self.min_split = max(2, int(min_samples_split))
+            self.min_leaf = max(1, int(min_samples_leaf))
+        self.alpha = float(alpha)
+        self.min_gain = float(min_gain)
+        self.feature_mask = feature_mask
         self.mtry = mtry
         self.max_leaves = max_leaf_nodes
         self.gen = torch.Generator(device="cpu").manual_seed(int(seed))
@@ -193,13 +202,22 @@ class HistTreeBuilder:
         if c == "gbt":           # S = (Σr, Σh, n): least squares on the residual
             return torch.where(S[..., 2] > 0, S[..., 0] ** 2 / (S[..., 2] + self.lam),
                                torch.zeros_like(S[..., 0]))
+        if c == "xgb":           # S = (Σg, Σh): T_alpha(G)^2 / (H + lambda)
+            G = self._soft(S[..., 0])
+            return torch.where(S[..., 1] > 0, G * G / (S[..., 1] + self.lam), torch.zeros_like(G))
         raise ValueError(c)
+
+    def _soft(self, G: torch.Tensor) -> torch.Tensor:
+        """L1 soft threshold of the gradient sum (XGBoost's alpha)."""
+        if self.alpha <= 0:
+            return G
+        return torch.sign(G) * (G.abs() - self.alpha).clamp_min(0)
 
     def _weight(self, S: torch.Tensor) -> torch.Tensor:
         c = self.criterion
         if c in ("gini", "entropy"):
             return S.sum(-1)
-        if c == "variance":
+        if c in ("variance", "xgb"):
             return S[..., 1]
         return S[..., 2]
 
@@ -211,6 +229,9 @@ class HistTreeBuilder:
             return torch.where(w > 0, S / w.clamp_min(1e-30), torch.full_like(S, 1.0 / S.shape[1]))
         if c == "variance":
             return torch.where(S[:, 1:2] > 0, S[:, 0:1] / S[:, 1:2].clamp_min(1e-30), torch.zeros_like(S[:, :1]))
+        if c == "xgb":           # Newton step -T(G) / (H + lambda)
+            den = S[:, 1:2] + self.lam
+            return torch.where(den > 0, -self._soft(S[:, 0:1]) / den.clamp_min(1e-30), torch.zeros_like(S[:, :1]))
         ok = S[:, 1:2].abs() > 1e-12
         return torch.where(ok, S[:, 0:1] / torch.where(ok, S[:, 1:2], torch.ones_like(S[:, 1:2])),
                            torch.zeros_like(S[:, :1]))
@@ -286,12 +307,15 @@ class HistTreeBuilder:
             gain = self._score(cum) + self._score(right) - self._score(tot)[:, None, None]
             cnt_ok = (self._weight(cum) >= self.min_leaf) & (self._weight(right) >= self.min_leaf)
             gain = torch.where(cnt_ok, gain, torch.full_like(gain, -math.inf))
+            if self.feature_mask is not None:
+                gain = torch.where(self.feature_mask.to(dev)[None, :, None], gain, torch.full_like(gain, -math.inf))
             if self.mtry is not None and self.mtry < d:
                 pick = torch.rand((L, d), generator=gen, device=dev).topk(self.mtry, 1).indices
                 fm = torch.zeros((L, d), dtype=torch.bool, device=dev).scatter_(1, pick, True)
                 gain = torch.where(fm[:, :, None], gain, torch.full_like(gain, -math.inf))
             best_gain, best = gain.reshape(L, -1).max(1)
-            ok = (best_gain > 1e-12) & torch.isfinite(best_gain) & (self._weight(tot) >= self.min_split)
+            ok = (best_gain > max(1e-12, self.min_gain)) & torch.isfinite(best_gain) & \
+                (self._weight(tot) >= self.min_split)
             if self.max_leaves is not None:
                 ok &= torch.cumsum(ok.long(), 0) <= (int(self.max_leaves) - n_leaves)
             li = torch.nonzero(ok).flatten()                                   # the level's one sync
@@ -764,8 +788,6 @@ def register_sql(reg):
     reg("train_randomforest_regressor", lambda: RandomForestRegressor)
     reg("train_randomforest_regr", lambda: RandomForestRegressor)
     reg("train_gradient_tree_boosting_classifier", lambda: GradientTreeBoostingClassifier)
-    reg("train_xgboost_classifier", lambda: GradientTreeBoostingClassifier)
-    reg("train_xgboost", lambda: GradientTreeBoostingClassifier)
 
 
 _P = _native.c_p

@@ -1,0 +1,99 @@
+"""train_xgboost family (second-order histogram boosting) vs scikit-learn's histogram GBM and
+hand-computed Newton leaves; SQL train -> xgboost_predict_* pipeline."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+from sklearn.ensemble import HistGradientBoostingClassifier, HistGradientBoostingRegressor
+from sklearn.metrics import roc_auc_score
+
+from hivemall_amd.io.synthetic import higgs_like
+from hivemall_amd.models.xgboost import XGBoostMulticlass, XGBoostRegressor, XGBoostTrainer
+from hivemall_amd.sql import Session
+
+
+@pytest.fixture(scope="module")
+def higgs():
+    X, y = higgs_like(30000)
+    Xt, yt = higgs_like(6000, seed=9)
+    return X, y, Xt, yt
+
+
+def test_binary_matches_sklearn_hgb(higgs):
+    X, y, Xt, yt = higgs
+    m = XGBoostTrainer("-objective binary:logistic -num_round 40 -eta 0.3 -max_depth 6 -lambda 1",
+                       device="cpu").fit(X, y)
+    auc = roc_auc_score(yt.numpy(), m.predict_proba(Xt)[:, 0])
+    ref = HistGradientBoostingClassifier(max_iter=40, learning_rate=0.3, max_depth=6, l2_regularization=1.0,
+                                         early_stopping=False, max_leaf_nodes=None, min_samples_leaf=1)
+    ref.fit(X.numpy(), y.numpy())
+    auc_ref = roc_auc_score(yt.numpy(), ref.predict_proba(Xt.numpy())[:, 1])
+    assert auc > auc_ref - 0.01, (auc, auc_ref)
+
+
+def test_regression_matches_sklearn_hgb():
+    g = np.random.default_rng(0)
+    X = g.normal(size=(20000, 8)).astype(np.float32)
+    y = (np.sin(X[:, 0]) * 2 + X[:, 1] * X[:, 2] + 0.1 * g.normal(size=20000)).astype(np.float32)
+    m = XGBoostRegressor("-num_round 60 -eta 0.2 -max_depth 5", device="cpu").fit(X[:15000], y[:15000])
+    rmse = float(np.sqrt(np.mean((m.predict(X[15000:]) - y[15000:]) ** 2)))
+    ref = HistGradientBoostingRegressor(max_iter=60, learning_rate=0.2, max_depth=5, l2_regularization=1.0,
+                                        early_stopping=False, max_leaf_nodes=None, min_samples_leaf=1)
+    ref.fit(X[:15000], y[:15000])
+    rmse_ref = float(np.sqrt(np.mean((ref.predict(X[15000:]) - y[15000:]) ** 2)))
+    assert rmse < rmse_ref * 1.1, (rmse, rmse_ref)
+
+
+def test_multiclass_softprob():
+    g = np.random.default_rng(1)
+    X = g.normal(size=(9000, 5)).astype(np.float32)
+    lab = np.where(X[:, 0] > 0.5, 2, np.where(X[:, 1] > 0, 1, 0))
+    m = XGBoostMulticlass("-num_round 20 -max_depth 4 -num_class 3", device="cpu").fit(X[:6000], lab[:6000])
+    P = m.predict_proba(X[6000:])
+    assert P.shape == (3000, 3) and np.allclose(P.sum(1), 1, atol=1e-5)
+    assert (m.predict(X[6000:]) == lab[6000:]).mean() > 0.95
+
+
+def test_newton_leaf_values_and_gamma():
+    """One stump: leaf = -eta * G / (H + lambda) with logistic g = p - y, h = p(1-p) at p = 0.5."""
+    X = torch.tensor([[0.0], [0.0], [1.0], [1.0], [1.0]])
+    y = torch.tensor([0.0, 0.0, 1.0, 1.0, 0.0])
+    m = XGBoostTrainer("-num_round 1 -max_depth 1 -eta 0.5 -lambda 1 -min_child_weight 0", device="cpu").fit(X, y)
+    t = m.trees[0][0]
+    assert t.feature[0] == 0
+    left = [v[0] for k, v in enumerate(t.value) if v is not None and k == t.left[0]][0]
+    right = [v[0] for k, v in enumerate(t.value) if v is not None and k == t.right[0]][0]
+    # left: g = 0.5, 0.5 -> G = 1, H = 0.5 ; right: g = -0.5, -0.5, 0.5 -> G = -0.5, H = 0.75
+    assert left == pytest.approx(-0.5 * 1.0 / 1.5, rel=1e-5)
+    assert right == pytest.approx(-0.5 * -0.5 / 1.75, rel=1e-5)
+    big_gamma = XGBoostTrainer("-num_round 1 -max_depth 1 -gamma 10 -min_child_weight 0", device="cpu").fit(X, y)
+    assert big_gamma.trees[0][0].feature[0] == -1          # split not worth 2*gamma
+
+
+def test_sql_pipeline(higgs):
+    X, y, Xt, yt = higgs
+    s = Session(device="cpu")
+    s.register("train", pd.DataFrame({"features": [[f"{j}:{v:.5f}" for j, v in enumerate(r)] for r in X[:8000].tolist()],
+                                      "label": y[:8000].numpy().astype(int)}))
+    s.register("test", pd.DataFrame({"rowid": range(1000),
+                                     "features": [[f"{j}:{v:.5f}" for j, v in enumerate(r)] for r in Xt[:1000].tolist()]}))
+    s.sql("CREATE TABLE m AS SELECT train_xgboost(features, label, '-objective binary:logistic -num_round 20') "
+          "AS (model_id, model) FROM train")
+    p = s.sql("SELECT xgboost_predict_one(t.rowid, t.features, m.model_id, m.model) AS (rowid, predicted) "
+              "FROM m CROSS JOIN test t")
+    assert len(p) == 1000
+    auc = roc_auc_score(yt[:1000].numpy()[p["rowid"].to_numpy()], p["predicted"].to_numpy())
+    assert auc > 0.75
+    tri = s.sql("SELECT xgboost_predict_triple(t.rowid, t.features, m.model_id, m.model) AS (rowid, label, prob) "
+                "FROM m CROSS JOIN test t")
+    assert len(tri) == 2000 and set(tri["label"]) == {"0", "1"}
+
+
+@pytest.mark.gpu
+def test_binary_gpu_matches_cpu(higgs):
+    X, y, Xt, yt = higgs
+    aucs = {}
+    for dev in ("cpu", "cuda"):
+        m = XGBoostTrainer("-num_round 20 -max_depth 6", device=dev).fit(X, y)
+        aucs[dev] = roc_auc_score(yt.numpy(), m.predict_proba(Xt)[:, 0])
+    assert abs(aucs["cpu"] - aucs["cuda"]) < 0.005, aucs
