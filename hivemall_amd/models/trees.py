@@ -51,15 +51,25 @@ class Quantized:
 
 
 def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: int = 0,
-             edges: torch.Tensor | None = None) -> Quantized:
-    """Per-feature quantile edges (from a row sample) and uint8 bins on X's device."""
+             edges: torch.Tensor | None = None, mixer=None) -> Quantized:
+    """Per-feature quantile edges (from a row sample) and uint8 bins on X's device.
+
+    With a mixer over several ranks every rank contributes an equal-size sample of its shard and
+    the edges are computed from the all-gathered sample, so all ranks bin identically (required
+    by the histogram all-reduce of data-parallel boosting)."""
     X = X.float().contiguous()
     n, d = X.shape
     B = int(num_bins)
     if edges is None:
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        idx = (torch.arange(n) if n <= sample else torch.randint(0, n, (sample,), generator=g)).to(X.device)
-        S = X[idx]
+        world = mixer.world if mixer is not None else 1
+        g = torch.Generator(device="cpu").manual_seed(seed + 7919 * (mixer.ctx.rank if world > 1 else 0))
+        if world > 1:
+            m = max(1, sample // world)
+            idx = torch.randint(0, n, (m,), generator=g).to(X.device)
+            S = mixer.all_gather_cat(X[idx])
+        else:
+            idx = (torch.arange(n) if n <= sample else torch.randint(0, n, (sample,), generator=g)).to(X.device)
+            S = X[idx]
         qs = torch.linspace(0, 1, B + 1, device=X.device)[1:-1]
         E = torch.quantile(S.T.contiguous(), qs, dim=1).T.contiguous()     # [d, B-1]
         E = torch.nan_to_num(E, nan=float("inf"))
@@ -583,12 +593,16 @@ class GradientTreeBoostingClassifier(Learner):
         yi = yi.to(self.device)
         K = len(self.classes)
         n, d = X.shape
-        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed)
+        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer)
         self.importance = np.zeros(d)
         g = torch.Generator(device=self.device).manual_seed(self.seed)
         eta = float(c["eta"])
         if K == 2:
-            pos = float((yi == 1).float().mean().item())
+            pos = float((yi == 1).float().sum().item())
+            if self.mixer is not None:     # the global positive rate, so every rank starts alike
+                pos = self.mixer.all_reduce_scalar(pos) / self.mixer.all_reduce_scalar(float(n))
+            else:
+                pos /= n
             pos = min(max(pos, 1e-6), 1 - 1e-6)
             self.intercepts = [math.log(pos / (1 - pos))]
             F = torch.full((n, 1), self.intercepts[0], device=self.device)

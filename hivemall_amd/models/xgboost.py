@@ -120,7 +120,7 @@ class XGBoostTrainer(Learner):
                 self.base_margin = [math.log(bs / (1 - bs))]
             else:
                 self.base_margin = [bs]
-        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed)
+        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer)
         F = torch.tensor(self.base_margin, device=dev).repeat(n, 1)
         g = torch.Generator(device=dev).manual_seed(self.seed)
         gcpu = torch.Generator().manual_seed(self.seed)

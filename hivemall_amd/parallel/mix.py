@@ -96,6 +96,14 @@ class ModelMixer:
         for w in works:
             w.wait()
 
+    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenation (dim 0, rank order) of an equally-shaped tensor from every rank."""
+        if not self._active():
+            return t
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous())
+        return torch.cat(out, 0)
+
     def all_reduce_scalar(self, x: float, op: str = "sum") -> float:
         if not self._active():
             return x

@@ -89,6 +89,29 @@ def _ffm_dp(ctx):
     return float(t.state["V"].sum()), float(t.state["w"].sum())
 
 
+def _gbt_dp(ctx):
+    """Data-parallel boosting: each rank holds half the rows; histograms are all-reduced per
+    level, so both ranks must grow the same trees."""
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import GradientTreeBoostingClassifier
+    from hivemall_amd.models.xgboost import XGBoostTrainer
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    X, y = higgs_like(8000, seed=40 + ctx.rank)
+    gb = GradientTreeBoostingClassifier("-trees 3 -max_depth 4 -subsample 1.0 -seed 5", device="cpu",
+                                        mixer=ModelMixer(ctx), rank=ctx.rank).fit(X, y.long())
+    xg = XGBoostTrainer("-num_round 3 -max_depth 4", device="cpu", mixer=ModelMixer(ctx),
+                        rank=ctx.rank).fit(X, y)
+    return (list(gb.model_table()["pred_models"].map(tuple)), gb.intercepts,
+            xg.model_table()["model"].iloc[0])
+
+
+def test_boosting_data_parallel_identical_trees():
+    out = run_world("_gbt_dp")
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    assert out[0][2] == out[1][2]
+
+
 def test_mix_average_bucketed():
     out = run_world("_avg")
     for r in (0, 1):
