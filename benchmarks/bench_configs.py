@@ -86,7 +86,7 @@ def bench_fm(dev="cuda", n_rows=8 * 262144, bits=24):
     er = SparseRows(torch.arange(0, 200000 * 39 + 1, 39, dtype=torch.int64, device=dev),
                     eidx.reshape(-1).contiguous(), None, None)
     ll = torch.nn.functional.binary_cross_entropy_with_logits(t.predict_raw(rows=er), (ey > 0).float()).item()
-    return {"config": f"train_fm k=8, Criteo-1TB-shaped (39 fields, 2^{bits} hashed features), bf16 V",
+    return {"config": f"train_fm k=8, Criteo-1TB-shaped (39 fields, 2^{bits} hashed features), " + ("bf16 V" if dev == "cuda" else "fp32 V"),
             "device": dev, "rows_per_s": round(n_rows / dt), "heldout_logloss_after_2_epochs": round(ll, 5)}
 
 
@@ -154,14 +154,19 @@ ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "fm": ben
 SMALL = {"linear_gpu": dict(n=20000), "fm": dict(n_rows=20000, bits=16),
          "gbdt": dict(n=20000, trees=4), "rf": dict(n=20000, trees=2), "bprmf": dict(k=16, epochs=1)}
 
+# CPU reference-class points (8-core host): same code paths on the C++/OpenMP engines
+CPU = {"linear_gpu": dict(n=1_000_000), "fm": dict(n_rows=262144, bits=20),
+       "gbdt": dict(n=1_000_000, trees=10), "rf": dict(n=1_000_000, trees=4), "bprmf": dict(k=64, epochs=1)}
+
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     small = "--small" in sys.argv  # CPU smoke of the harness itself (tiny shapes)
+    cpu = "--cpu" in sys.argv      # reference-class CPU measurement
     prof = "--profile" in sys.argv  # per-kernel device-time table via torch.profiler
     names = args or list(ALL)
     for name in names:
-        kw = dict(SMALL.get(name, {})) if small else {}
-        if small:
+        kw = dict(SMALL.get(name, {})) if small else dict(CPU.get(name, {})) if cpu else {}
+        if small or cpu:
             kw["dev"] = "cpu"
         if prof:
             from torch.profiler import ProfilerActivity, profile
