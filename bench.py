@@ -48,6 +48,11 @@ def parse_args(argv=None):
     ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
     ap.add_argument("--state", choices=("bf16", "fp32"), default="bf16",
                     help="V / AdaGrad state storage (bf16 = stochastic-rounded, fp32 accumulate)")
+    ap.add_argument("--layout", choices=("packed", "split"), default="packed",
+                    help="V/G state layout: packed V|G slots (one 16-B access per slot) or split tables")
+    ap.add_argument("--reload", type=int, default=-1,
+                    help="1: re-read the own slot right before its update (short Hogwild window); "
+                         "0: keep the gathered slot in registers; -1: by layout (packed -> 0)")
     ap.add_argument("--device", default=None)
     return ap.parse_args(argv)
 
@@ -74,10 +79,12 @@ def main(argv=None):
     idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=dev)
     opts = (f"-classification -factors {args.factors} -feature_hashing {args.hash_bits} "
             f"-num_fields {F} -seed 31 -batch_size {B}" +
-            (" -bf16_state" if args.state == "bf16" and dev.type == "cuda" else ""))
+            (" -bf16_state" if args.state == "bf16" and dev.type == "cuda" else "") +
+            (" -split_state" if args.layout == "split" else ""))
     tr = FFMTrainer(opts, device=dev)
     tr.init_state(NF, F)
     st, hyper = tr.state, tr.hyper
+    hyper.reload = None if args.reload < 0 else bool(args.reload)
     mixer = ModelMixer(ctx)
     mix_tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
     grid = args.grid
@@ -153,6 +160,8 @@ def main(argv=None):
                 "nnz_per_row": F,
                 "parallelism": f"dp{world}",
                 "mix_every": args.mix_every,
+                "state_layout": args.layout if dev.type == "cuda" else "split",
+                "reload": (args.layout == "split") if args.reload < 0 else bool(args.reload),
                 "mixed_bytes_per_mix": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
             },
             "logloss_heldout": round(ll, 5) if ll is not None else None,

@@ -37,7 +37,8 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
     const int cls = ip[5], train = ip[6], use_lin = ip[7], use_bias = ip[8], norm = ip[9];
     const float eta0 = hp[0], eps = hp[1], lv = hp[2], alpha = hp[3], beta = hp[4];
     const float l1 = hp[5], l2 = hp[6], tmin = hp[7], tmax = hp[8];
-    const size_t fstride = (size_t)NFLD * Kp;
+    // slot stride: Kp (separate V / G tables) or 2*Kp (packed [NF][NFLD][2][Kp], G = V + Kp)
+    const size_t ss = ip[14] ? (size_t)2 * Kp : (size_t)Kp;
     std::vector<int> ri(F), rf(F);
     std::vector<float> rx(F);
     std::vector<float> snap((size_t)F * F * Kp);
@@ -60,7 +61,7 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
             for (int b = 0; b < F; ++b) {
                 float* dst = &snap[((size_t)a * F + b) * Kp];
                 if (a != b && ri[a] >= 0 && ri[b] >= 0)
-                    std::memcpy(dst, V + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp, sizeof(float) * Kp);
+                    std::memcpy(dst, V + ((size_t)ri[a] * NFLD + rf[b]) * ss, sizeof(float) * Kp);
                 else
                     std::memset(dst, 0, sizeof(float) * Kp);
             }
@@ -97,8 +98,8 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
             for (int b = 0; b < F; ++b) {
                 if (a == b || ri[a] < 0 || ri[b] < 0) continue;
                 const float coef = ks * rx[a] * rx[b];
-                float* pv = V + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp;
-                float* pg = G + (size_t)ri[a] * fstride + (size_t)rf[b] * Kp;
+                float* pv = V + ((size_t)ri[a] * NFLD + rf[b]) * ss;
+                float* pg = G + ((size_t)ri[a] * NFLD + rf[b]) * ss;
                 const float* own = &snap[((size_t)a * F + b) * Kp];
                 const float* par = &snap[((size_t)b * F + a) * Kp];
                 for (int k = 0; k < Kp; ++k) {

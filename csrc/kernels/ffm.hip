@@ -12,17 +12,25 @@
 //   w,w0 <- FTRL-proximal (alpha, beta, lambda1, lambda2) on g = kappa x
 //
 // Layout (MI355X-first):
-//   * V, G   : [num_features][num_fields][Kp], Kp = K rounded up to 4 (padding stays 0).
-//              Stored fp32, or bf16 (BF = true, ``-bf16_state``) with stochastic rounding on
-//              every write: the kernel is HBM-bound (~95 KB of V/G traffic per Criteo row in
-//              fp32), so halving the state bytes is the throughput lever; stochastic rounding
-//              keeps the sub-ulp AdaGrad steps and G increments unbiased.
+//   * A "slot" is the (feature, field) pair; it owns the latent vector V[i, f] (Kp elements,
+//     Kp = K rounded up to 4, padding stays 0) and its AdaGrad accumulator G[i, f].
+//     Two layouts, selected per call by the strides of the V / G tensors:
+//       - packed (default on the GPU): VG[feature][field] = {V[0..Kp) | G[0..Kp)}, slot stride
+//         2*Kp.  One 16-B access (bf16, K=4) moves a slot's V and G together and a feature's
+//         39-field block is 624 contiguous bytes.  gfx950 serves 8-B lanes at 0.54-0.70x the
+//         16-B rate (MI355X_MICROARCH.md, global_load flavours) and the split layout needs four
+//         8-B accesses per slot (V read, G read, V write, G write) against two 16-B ones here.
+//       - split: V and G are separate [feature][field][Kp] tables, slot stride Kp.
+//   * State is stored fp32, or bf16 (``-bf16_state``) with stochastic rounding on every write:
+//     the kernel is bound by HBM / memory instructions, so halving the state bytes is the
+//     throughput lever; stochastic rounding keeps the sub-ulp AdaGrad steps and G increments
+//     unbiased.
 //   * batch  : padded-ELL [B][F] (idx, fld, val), idx < 0 marks padding.
 //   * One 256-thread block per row (grid-stride over rows).  Ordered slot s = a*F + b owns
 //     the vector V[i_a, f_b]; consecutive threads read consecutive slot vectors of the same
-//     feature block, so every gather is coalesced.  The row's F*F*Kp slot vectors are staged
-//     in LDS as fp32 (24 KB at F=39, K=4) so the partner read for the pair dot and for the
-//     gradient never goes back to L2.
+//     feature block, so every gather is coalesced.  The row's F*F slot vectors are staged in
+//     LDS in the storage format (12 KB at F=39, K=4, bf16 -> 8 blocks/CU) so the partner read
+//     for the pair dot and for the gradient never goes back to L2.
 //   * Updates are Hogwild across rows (no atomics); each slot vector has a single writer
 //     within a row.  ``reload`` re-reads the own slot right before its update (shorter
 //     read-modify-write window -> fewer lost updates on hot features).
@@ -39,6 +47,7 @@ struct FFMParams {
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
     int reload;
+    int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -118,6 +127,80 @@ __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint3
     }
 }
 
+// Row metadata -> LDS and the instance-wise L2 normalisation factor (shared by both kernels;
+// contains the block barrier that publishes s_idx / s_fld / s_x).
+__device__ __forceinline__ float load_row_meta(const FFMParams& P, int row,
+                                               const int32_t* __restrict__ idx,
+                                               const int32_t* __restrict__ fld,
+                                               const float* __restrict__ val, int* s_idx,
+                                               int* s_fld, float* s_x, float* s_red) {
+    const int tid = threadIdx.x;
+    const int F = P.F;
+    float sq = 0.f;
+    if (tid < F) {
+        const size_t o = (size_t)row * F + tid;
+        int i = idx[o];
+        int f = fld ? fld[o] : tid;
+        float x = val ? val[o] : 1.f;
+        if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; }
+        s_idx[tid] = i;
+        s_fld[tid] = f < 0 ? 0 : (f >= P.num_fields ? P.num_fields - 1 : f);
+        s_x[tid] = x;
+        sq = x * x;
+    }
+    if (P.norm) {
+        const float tot = hm::block_sum(sq, s_red);
+        return tot > 0.f ? rsqrtf(tot) : 1.f;
+    }
+    __syncthreads();
+    return 1.f;
+}
+
+// Loss of the row's score p; writes pred/loss (thread 0) and returns kappa = dloss/dp.
+__device__ __forceinline__ float row_loss(const FFMParams& P, int row, float p,
+                                          const float* __restrict__ y,
+                                          float* __restrict__ pred_out,
+                                          float* __restrict__ loss_out) {
+    const float yy = y ? y[row] : 0.f;
+    float kappa;
+    if (P.classification) {
+        const float e = yy * p;
+        kappa = -yy / (1.f + __expf(e));
+        if (threadIdx.x == 0) {
+            if (loss_out) loss_out[row] = hm::log1pexp(-e);
+            if (pred_out) pred_out[row] = p;
+        }
+    } else {
+        const float pc = fminf(fmaxf(p, P.min_target), P.max_target);
+        kappa = pc - yy;
+        if (threadIdx.x == 0) {
+            if (loss_out) loss_out[row] = 0.5f * kappa * kappa;
+            if (pred_out) pred_out[row] = pc;
+        }
+    }
+    return kappa;
+}
+
+// FTRL updates of the linear terms and the global bias (after the V updates of a row).
+__device__ __forceinline__ void linear_updates(const FFMParams& P, float kappa, float scale,
+                                               const int* s_idx, const float* s_x,
+                                               float* __restrict__ w, float* __restrict__ wz,
+                                               float* __restrict__ wn, float* __restrict__ bias) {
+    const int tid = threadIdx.x;
+    if (P.use_linear && tid < P.F) {
+        const int i = s_idx[tid];
+        if (i >= 0) {
+            const float g = kappa * s_x[tid] * scale;
+            w[i] = ftrl_update(wz + i, wn + i, w[i], g, P.alpha, P.beta, P.lambda1, P.lambda2);
+        }
+    }
+    if (P.use_bias && tid == 0) {
+        bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic kernel: any K, either layout (slot stride P.sstride), LDS staging when it fits.
 template <int KC, bool STAGE, bool BF>
 __global__ __launch_bounds__(256) void ffm_row_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -143,30 +226,13 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     float* s_red = s_x + F;                                              // 16 (+pad)
 
     const int tid = threadIdx.x;
-    const int Kp = P.Kp;
-    const size_t fstride = (size_t)P.num_fields * Kp;  // elements per feature block
+    const size_t nfld = (size_t)P.num_fields;
+    const size_t ss = (size_t)P.sstride;
+    auto slot_off = [&](int i, int f) -> size_t { return ((size_t)i * nfld + (size_t)f) * ss; };
 
     for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
-        float sq = 0.f;
-        if (tid < F) {
-            const size_t o = (size_t)row * F + tid;
-            int i = idx[o];
-            int f = fld ? fld[o] : tid;
-            float x = val ? val[o] : 1.f;
-            if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; }
-            s_idx[tid] = i;
-            s_fld[tid] = f < 0 ? 0 : (f >= P.num_fields ? P.num_fields - 1 : f);
-            s_x[tid] = x;
-            sq = x * x;
-        }
-        float scale = 1.f;
-        if (P.norm) {
-            const float tot = hm::block_sum(sq, s_red);
-            scale = tot > 0.f ? rsqrtf(tot) : 1.f;
-        } else {
-            __syncthreads();
-        }
+        const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);
 
         // ---- 2. gather the row's slot vectors (coalesced) ----
         if (STAGE) {
@@ -174,7 +240,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 const int a = s / F, b = s - (s / F) * F;
                 const int ia = s_idx[a];
                 const bool live = a != b && ia >= 0 && s_idx[b] >= 0;
-                const size_t off = live ? (size_t)ia * fstride + (size_t)s_fld[b] * Kp : 0;
+                const size_t off = live ? slot_off(ia, s_fld[b]) : 0;
 #pragma unroll
                 for (int c = 0; c < KC; ++c)
                     s_v[s * KC + c] = live ? ld_raw<BF>(V, off + 4 * c) : SV{};
@@ -197,8 +263,8 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                     v[c] = to_f4<BF>(s_v[(b * F + a) * KC + c]);
                 }
             } else {
-                const size_t ou = (size_t)ia * fstride + (size_t)s_fld[b] * Kp;
-                const size_t ov = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
+                const size_t ou = slot_off(ia, s_fld[b]);
+                const size_t ov = slot_off(ib, s_fld[a]);
 #pragma unroll
                 for (int c = 0; c < KC; ++c) { u[c] = ld_chunk<BF>(V, ou + 4 * c); v[c] = ld_chunk<BF>(V, ov + 4 * c); }
             }
@@ -213,23 +279,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         if (P.use_bias) p += bias[0];
 
         // ---- 4. loss ----
-        const float yy = y ? y[row] : 0.f;
-        float kappa;
-        if (P.classification) {
-            const float e = yy * p;
-            kappa = -yy / (1.f + __expf(e));
-            if (tid == 0) {
-                if (loss_out) loss_out[row] = hm::log1pexp(-e);
-                if (pred_out) pred_out[row] = p;
-            }
-        } else {
-            const float pc = fminf(fmaxf(p, P.min_target), P.max_target);
-            kappa = pc - yy;
-            if (tid == 0) {
-                if (loss_out) loss_out[row] = 0.5f * kappa * kappa;
-                if (pred_out) pred_out[row] = pc;
-            }
-        }
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- 5. updates (Hogwild) ----
         if (P.train) {
@@ -241,7 +291,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 const int ia = s_idx[a], ib = s_idx[b];
                 if (ia < 0 || ib < 0) continue;
                 const float coef = ks * s_x[a] * s_x[b];
-                const size_t ov = (size_t)ia * fstride + (size_t)s_fld[b] * Kp;
+                const size_t ov = slot_off(ia, s_fld[b]);
                 float4 own[KC], par[KC], gg[KC];
 #pragma unroll
                 for (int c = 0; c < KC; ++c) gg[c] = ld_chunk<BF>(G, ov + 4 * c);
@@ -252,7 +302,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                         par[c] = to_f4<BF>(s_v[(b * F + a) * KC + c]);
                     }
                 } else {
-                    const size_t op = (size_t)ib * fstride + (size_t)s_fld[a] * Kp;
+                    const size_t op = slot_off(ib, s_fld[a]);
 #pragma unroll
                     for (int c = 0; c < KC; ++c) { own[c] = ld_chunk<BF>(V, ov + 4 * c); par[c] = ld_chunk<BF>(V, op + 4 * c); }
                 }
@@ -273,19 +323,236 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                     st_chunk<BF>(G, ov + 4 * c, gg[c], rnd ^ 0xA5A5A5A5u);
                 }
             }
-            if (P.use_linear && tid < F) {
-                const int i = s_idx[tid];
-                if (i >= 0) {
-                    const float g = kappa * s_x[tid] * scale;
-                    w[i] = ftrl_update(wz + i, wn + i, w[i], g, P.alpha, P.beta, P.lambda1, P.lambda2);
-                }
-            }
-            if (P.use_bias && tid == 0) {
-                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
-            }
+            linear_updates(P, kappa, scale, s_idx, s_x, w, wz, wn, bias);
         }
         __syncthreads();  // LDS reuse by the next row
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Packed-layout kernel (K <= 8, F*F <= 2048): each thread owns NS = ceil(F*F / 256) slots,
+// decodes their (a, b) once per launch, and moves a slot's V and G with the same 16-B
+// accesses.  RELOAD = false keeps the gathered raw V/G words in registers until the update
+// (two memory instructions per slot in total: gather, store); RELOAD = true re-reads the packed
+// slot right before the update (an L2 hit: the gather brought the line in a few microseconds
+// earlier), as short a Hogwild read-modify-write window as the split kernel's.
+template <int KC, bool BF>
+struct SlotIO {
+    using SV = typename std::conditional<BF, uint2, float4>::type;
+    // slot index -> raw V and G chunks (Kp = 4*KC elements per half)
+    __device__ static __forceinline__ void load(const void* VG, uint32_t slot, SV (&v)[KC], SV (&g)[KC]) {
+        if constexpr (BF) {
+            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(VG) + (size_t)slot * (8 * KC));
+            uint2 u[2 * KC];
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const uint4 q = p[c];
+                u[2 * c] = make_uint2(q.x, q.y);
+                u[2 * c + 1] = make_uint2(q.z, q.w);
+            }
+#pragma unroll
+            for (int c = 0; c < KC; ++c) { v[c] = u[c]; g[c] = u[KC + c]; }
+        } else {
+            const float4* p = reinterpret_cast<const float4*>(VG) + (size_t)slot * (2 * KC);
+#pragma unroll
+            for (int c = 0; c < KC; ++c) { v[c] = p[c]; g[c] = p[KC + c]; }
+        }
+    }
+    __device__ static __forceinline__ void store(void* VG, uint32_t slot, const float4 (&v)[KC],
+                                                 const float4 (&g)[KC], uint32_t rnd0) {
+        if constexpr (BF) {
+            uint2 u[2 * KC];
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const uint32_t r1 = hash3(rnd0, (uint32_t)c, 0x51u);
+                const uint32_t r2 = r1 * 0x9E3779B1u + 0x632BE5ABu;
+                const uint32_t r3 = r2 * 0x85EBCA77u + 0x27D4EB2Fu;
+                const uint32_t r4 = r3 * 0xC2B2AE3Du + 0x165667B1u;
+                u[c] = make_uint2(bf16_sr(v[c].x, r1) | (bf16_sr(v[c].y, r1 >> 16) << 16),
+                                  bf16_sr(v[c].z, r2) | (bf16_sr(v[c].w, r2 >> 16) << 16));
+                u[KC + c] = make_uint2(bf16_sr(g[c].x, r3) | (bf16_sr(g[c].y, r3 >> 16) << 16),
+                                       bf16_sr(g[c].z, r4) | (bf16_sr(g[c].w, r4 >> 16) << 16));
+            }
+            uint4* p = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(VG) + (size_t)slot * (8 * KC));
+#pragma unroll
+            for (int c = 0; c < KC; ++c)
+                p[c] = make_uint4(u[2 * c].x, u[2 * c].y, u[2 * c + 1].x, u[2 * c + 1].y);
+        } else {
+            float4* p = reinterpret_cast<float4*>(VG) + (size_t)slot * (2 * KC);
+#pragma unroll
+            for (int c = 0; c < KC; ++c) { p[c] = v[c]; p[KC + c] = g[c]; }
+        }
+    }
+};
+
+template <int KC, bool BF, int NS, bool RELOAD>
+__global__ __launch_bounds__(256) void ffm_packed_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
+    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    using IO = SlotIO<KC, BF>;
+    using SV = typename IO::SV;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int F = P.F;
+    const int FF = F * F;
+    SV* s_v = reinterpret_cast<SV*>(smem);                                      // FF*KC
+    int* s_idx = reinterpret_cast<int*>(smem + (size_t)FF * KC * sizeof(SV));   // F
+    int* s_fld = s_idx + F;
+    float* s_x = reinterpret_cast<float*>(s_fld + F);
+    float* s_red = s_x + F;
+    const int tid = threadIdx.x;
+    const uint32_t nfld = (uint32_t)P.num_fields;
+
+    // slot -> (a, b) is row-invariant: decoded once as a | b << 16 (-1 past the end)
+    int ab[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        ab[j] = s < FF ? ((s / F) | ((s % F) << 16)) : -1;
+    }
+
+    for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
+        // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
+        const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);
+
+        // ---- 2. gather own packed slots: V -> LDS image (+ registers), G -> registers ----
+        SV ov[NS][KC], og[NS][KC];
+        uint32_t slot[NS];
+        uint32_t live = 0u;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            slot[j] = 0u;
+            if (ab[j] >= 0) {
+                const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
+                const int ia = s_idx[a];
+                SV v[KC], g[KC];
+                if (a != b && ia >= 0 && s_idx[b] >= 0) {
+                    slot[j] = (uint32_t)ia * nfld + (uint32_t)s_fld[b];
+                    IO::load(VG, slot[j], v, g);
+                    live |= 1u << j;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) { v[c] = SV{}; g[c] = SV{}; }
+                }
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    s_v[(a * F + b) * KC + c] = v[c];
+                    if (!RELOAD) { ov[j][c] = v[c]; og[j][c] = g[c]; }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- 3. forward: pairs a < b ----
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            if (!(live >> j & 1u)) continue;
+            const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
+            if (a >= b) continue;
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const float4 u = to_f4<BF>(RELOAD ? s_v[(a * F + b) * KC + c] : ov[j][c]);
+                const float4 v = to_f4<BF>(s_v[(b * F + a) * KC + c]);
+                d += u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w;
+            }
+            part += d * s_x[a] * s_x[b];
+        }
+        part *= scale * scale;
+        if (P.use_linear && tid < F && s_idx[tid] >= 0) part += w[s_idx[tid]] * s_x[tid] * scale;
+        float p = hm::block_sum(part, s_red);
+        if (P.use_bias) p += bias[0];
+
+        // ---- 4. loss ----
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- 5. AdaGrad(V) update on the packed slots (Hogwild) ----
+        if (P.train) {
+            const float ks = kappa * scale * scale;
+            const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (!(live >> j & 1u)) continue;
+                const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
+                const float coef = ks * s_x[a] * s_x[b];
+                SV rv[KC], rg[KC];
+                if (RELOAD) {
+                    IO::load(VG, slot[j], rv, rg);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) { rv[c] = ov[j][c]; rg[c] = og[j][c]; }
+                }
+                float4 own[KC], gg[KC];
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    own[c] = to_f4<BF>(rv[c]);
+                    gg[c] = to_f4<BF>(rg[c]);
+                    const float4 par = to_f4<BF>(s_v[(b * F + a) * KC + c]);
+                    float4 g;
+                    g.x = coef * par.x + P.lambda_v * own[c].x;
+                    g.y = coef * par.y + P.lambda_v * own[c].y;
+                    g.z = coef * par.z + P.lambda_v * own[c].z;
+                    g.w = coef * par.w + P.lambda_v * own[c].w;
+                    gg[c].x += g.x * g.x; gg[c].y += g.y * g.y; gg[c].z += g.z * g.z; gg[c].w += g.w * g.w;
+                    own[c].x -= P.eta0 * g.x * rsqrtf(gg[c].x + P.eps);
+                    own[c].y -= P.eta0 * g.y * rsqrtf(gg[c].y + P.eps);
+                    own[c].z -= P.eta0 * g.z * rsqrtf(gg[c].z + P.eps);
+                    own[c].w -= P.eta0 * g.w * rsqrtf(gg[c].w + P.eps);
+                }
+                IO::store(VG, slot[j], own, gg, BF ? hash3(rrow, (uint32_t)(a * F + b), 0x3u) : 0u);
+            }
+            linear_updates(P, kappa, scale, s_idx, s_x, w, wz, wn, bias);
+        }
+        __syncthreads();  // LDS reuse by the next row
+    }
+}
+
+int default_blocks(int B, int grid) {
+    return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
+}
+
+// Occupancy: the NS loops are fully unrolled so every owned slot's load is in flight at once;
+// that costs 110-127 VGPRs (4 waves/SIMD).  Capping the registers for 6 waves/SIMD spilled
+// (124-192 B/lane of scratch) and ran 22-44 % slower (profiles/ffm_layout_ab_r1.log); a cap for
+// 5 waves/SIMD still spills (36-104 B/lane).
+template <int KC, bool BF, int NS, bool RELOAD>
+int launch_packed_w(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                    const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                    float* pred, float* loss, int blocks, size_t shmem, hipStream_t stream) {
+    hipLaunchKernelGGL((ffm_packed_kernel<KC, BF, NS, RELOAD>), dim3(blocks), dim3(256), shmem, stream,
+                       P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss);
+    HM_LAUNCH_RET();
+}
+
+template <int KC, bool BF, int NS>
+int launch_packed(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                  float* pred, float* loss, int blocks, size_t shmem, hipStream_t stream) {
+    if (P.reload)
+        return launch_packed_w<KC, BF, NS, true>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, shmem, stream);
+    return launch_packed_w<KC, BF, NS, false>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, shmem, stream);
+}
+
+// Packed dispatch; returns -1 when the shape needs the generic kernel instead.
+template <int KC, bool BF>
+int dispatch_packed(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                    const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                    float* pred, float* loss, int grid, hipStream_t stream) {
+    const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
+    const size_t stage = (size_t)P.F * P.F * KC * (BF ? 8 : 16);
+    if (stage + meta > 64 * 1024) return -1;
+    const int need = (P.F * P.F + 255) / 256;
+    const int blocks = default_blocks(P.B, grid);
+    if (blocks <= 0) return 0;
+    const size_t sh = stage + meta;
+    if (need <= 2) return launch_packed<KC, BF, 2>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
+    if (need <= 4) return launch_packed<KC, BF, 4>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
+    if (need <= 6) return launch_packed<KC, BF, 6>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
+    if (need <= 8) return launch_packed<KC, BF, 8>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
+    return -1;
 }
 
 template <int KC, bool BF>
@@ -295,7 +562,7 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
     const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
     const size_t stage = (size_t)P.F * P.F * KC * (BF ? 8 : 16);
     const bool use_stage = stage + meta <= 64 * 1024;
-    const int blocks = grid > 0 ? grid : (P.B < 256 * 8 * 4 ? P.B : 256 * 8 * 4);
+    const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
     if (use_stage) {
         hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
@@ -310,7 +577,14 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
 template <bool BF>
 int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
-             float* pred, float* loss, int grid, hipStream_t stream) {
+             float* pred, float* loss, int grid, int packed, hipStream_t stream) {
+    if (packed) {
+        int rc = -1;
+        if (P.Kp == 4) rc = dispatch_packed<1, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+        else if (P.Kp == 8) rc = dispatch_packed<2, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+        if (rc != -1) return rc;
+        // other shapes: the generic kernel handles the packed strides too (G = V + Kp)
+    }
     switch (P.Kp / 4) {
         case 1: return launch_ffm<1, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
         case 2: return launch_ffm<2, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
@@ -325,7 +599,9 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload, bf16_state, seed
+//                     use_bias, norm, grid, reload, bf16_state, seed, packed
+// packed = 1: V and G are the two halves of one [num_features][num_fields][2][Kp] table
+//             (G == V + Kp elements, slot stride 2*Kp); 0: separate [.][.][Kp] tables.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -337,9 +613,19 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.reload = ip[11];
     const int bf16 = ip[12];
     P.seed = (uint32_t)ip[13];
+    const int packed = ip[14];
+    P.sstride = packed ? 2 * P.Kp : P.Kp;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
-    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream)
-                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+    if (packed) {
+        // G must be the second half of every packed slot
+        const size_t es = bf16 ? 2 : 4;
+        if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.Kp * es)
+            return (int)hipErrorInvalidValue;
+        // 32-bit slot indices in the packed kernel
+        if ((size_t)P.num_features * (size_t)P.num_fields >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
+    }
+    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, stream)
+                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, stream);
 }

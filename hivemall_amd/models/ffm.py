@@ -29,7 +29,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from ..ops.ffm import FFMHyper, ffm_step
+from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
 from .base import COMMON_ITER_OPTS, ConversionState, Learner, log, parse_labels_binary
@@ -78,6 +78,8 @@ class FFMTrainer(Learner):
         flag("no_norm", "disable_norm", "Disable instance-wise L2 normalization"),
         flag("bf16_state", None, "[engine] keep V and the AdaGrad state in bf16 on the GPU "
                                  "(stochastic rounding); halves the HBM traffic"),
+        flag("split_state", None, "[engine] separate V and G tables on the GPU instead of the "
+                                  "packed V|G slot layout (A/B)"),
         opt("feature_hashing", None, -1, int, "Hash feature indices into 2^bits"),
         opt("num_features", None, -1, int, "Number of (hashed) features; inferred when -1"),
         opt("num_fields", None, -1, int, "Number of fields; inferred from data when -1"),
@@ -121,8 +123,10 @@ class FFMTrainer(Learner):
         self.num_features, self.num_fields = int(num_features), int(num_fields)
         g = torch.Generator(device="cpu").manual_seed(self.seed)
         dev = self.device
-        shape = (self.num_features, self.num_fields, self.kp)
-        V = torch.zeros(shape, dtype=torch.float32, device=dev)
+        sdt = torch.bfloat16 if (self.cl["bf16_state"] and dev.type == "cuda") else torch.float32
+        # packed V|G slots on the GPU (csrc/kernels/ffm.hip); split tables on the CPU engine
+        V, G = new_state_tables(self.num_features, self.num_fields, self.kp, sdt, dev,
+                                packed=dev.type == "cuda" and not self.cl["split_state"])
         if self.cl["init_v"] == "gaussian":
             init = lambda n: torch.randn(n, generator=g) * self.cl["sigma"]
         else:
@@ -133,10 +137,9 @@ class FFMTrainer(Learner):
             e = min(self.num_features, s + rows_per)
             chunk = init((e - s) * self.num_fields * self.k).view(e - s, self.num_fields, self.k)
             V[s:e, :, : self.k].copy_(chunk.to(dev))
-        sdt = torch.bfloat16 if (self.cl["bf16_state"] and dev.type == "cuda") else torch.float32
         self.state = dict(
-            V=V.to(sdt),
-            G=torch.zeros(shape, dtype=sdt, device=dev),
+            V=V,
+            G=G,
             w=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
             wz=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
             wn=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
@@ -252,7 +255,7 @@ class FFMTrainer(Learner):
             "Vi": [None] * (1 + n_lin) + list(V)})
 
     def state_dict(self) -> dict:
-        return {k: v.detach().cpu() for k, v in (self.state or {}).items()} | {
+        return {k: v.detach().cpu().contiguous() for k, v in (self.state or {}).items()} | {
             "meta": torch.tensor([self.num_features, self.num_fields, self.k, self.kp])}
 
     def load_state_dict(self, sd: dict) -> None:
@@ -260,7 +263,20 @@ class FFMTrainer(Learner):
         assert k == self.k, "factor mismatch"
         self.num_features, self.num_fields = nf, nfld
         self.state = {k2: v.to(self.device) for k2, v in sd.items() if k2 != "meta"}
+        self.pack_state()
         self.touched = torch.ones(nf, dtype=torch.bool, device=self.device)
+
+    def pack_state(self) -> None:
+        """Move split V/G tables into the packed GPU layout (after a load)."""
+        st = self.state
+        if (st is None or self.device.type != "cuda" or self.cl["split_state"]
+                or is_packed(st["V"], st["G"])):
+            return
+        NF, NFLD, kp = st["V"].shape
+        V, G = new_state_tables(NF, NFLD, kp, st["V"].dtype, st["V"].device, packed=True)
+        V.copy_(st["V"])
+        G.copy_(st["G"])
+        st["V"], st["G"] = V, G
 
 
 def train_ffm(features, labels, options: str | None = None, device=None, **kw) -> pd.DataFrame:

@@ -44,7 +44,8 @@ class ModelMixer:
         return self.ctx.is_dist and self.world > 1
 
     def all_reduce_sum(self, tensors: list[torch.Tensor]) -> None:
-        """In-place SUM all-reduce of a list of contiguous tensors (bucketed, async)."""
+        """In-place SUM all-reduce of a list of tensors (bucketed, async; non-contiguous views
+        are reduced through a contiguous copy)."""
         if not self._active():
             return
         small = [t for t in tensors if t.numel() * t.element_size() <= self.small_bytes]
@@ -54,14 +55,19 @@ class ModelMixer:
         if small:
             flat = torch.cat([t.reshape(-1).to(torch.float32) for t in small])
             works.append(dist.all_reduce(flat, async_op=True))
+        staged = []   # strided views (e.g. the V half of the packed FFM table) go via a copy
         for t in big:
-            assert t.is_contiguous()
-            v = t.view(-1)
-            step = max(1, self.bucket_bytes // t.element_size())
+            buf = t if t.is_contiguous() else t.contiguous()
+            if buf is not t:
+                staged.append((t, buf))
+            v = buf.view(-1)
+            step = max(1, self.bucket_bytes // buf.element_size())
             for s in range(0, v.numel(), step):
                 works.append(dist.all_reduce(v[s:s + step], async_op=True))
         for w in works:
             w.wait()
+        for t, buf in staged:
+            t.copy_(buf)
         if flat is not None:
             off = 0
             for t in small:

@@ -67,6 +67,18 @@ def _avg(ctx):
     return big.tolist()[:3] + small.tolist()
 
 
+def _avg_strided(ctx):
+    """A non-contiguous view (the V half of the packed FFM table) mixes like a plain tensor."""
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    m = ModelMixer(ctx, bucket_mb=0.001, small_bytes=64)
+    VG = torch.zeros(50, 3, 2, 4)
+    VG[:, :, 0] = float(ctx.rank + 1)
+    VG[:, :, 1] = 7.0 * (ctx.rank + 1)       # G: optimizer state, stays local
+    m.average([VG[:, :, 0, :]])
+    return [float(VG[:, :, 0].mean()), float(VG[:, :, 1].mean())]
+
+
 def _kld(ctx):
     from hivemall_amd.parallel.mix import ModelMixer
 
@@ -116,6 +128,12 @@ def test_mix_average_bucketed():
     out = run_world("_avg")
     for r in (0, 1):
         assert out[r] == [1.5, 1.5, 1.5, 1.0, 1.0]
+
+
+def test_mix_average_strided_view():
+    out = run_world("_avg_strided")
+    assert out[0][0] == 1.5 and out[1][0] == 1.5
+    assert out[0][1] == 7.0 and out[1][1] == 14.0
 
 
 def test_mix_argmin_kld():

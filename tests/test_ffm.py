@@ -4,7 +4,7 @@ import torch
 
 from hivemall_amd.io.synthetic import criteo_like
 from hivemall_amd.models.ffm import FFMBatch, FFMTrainer, train_ffm
-from hivemall_amd.ops.ffm import ffm_step
+from hivemall_amd.ops.ffm import ffm_step, is_packed, new_state_tables
 from tests.oracle.ffm_oracle import ffm_train_rows
 
 
@@ -37,6 +37,36 @@ def test_ffm_cpu_engine_matches_oracle(use_bias):
     np.testing.assert_allclose(loss.numpy(), ref_loss, rtol=2e-4, atol=2e-5)
     for k in ("V", "G", "w", "wz", "wn", "bias"):
         np.testing.assert_allclose(t.state[k].numpy(), ref[k], rtol=2e-4, atol=2e-5, err_msg=k)
+
+
+def _to_packed(t):
+    """Copy a trainer's split V/G tables into the packed [NF, NFLD, 2, Kp] layout."""
+    NF, NFLD, kp = t.state["V"].shape
+    V, G = new_state_tables(NF, NFLD, kp, t.state["V"].dtype, t.state["V"].device, packed=True)
+    V.copy_(t.state["V"])
+    G.copy_(t.state["G"])
+    t.state["V"], t.state["G"] = V, G
+    assert is_packed(V, G)
+
+
+@pytest.mark.parametrize("k", [4, 8])
+def test_ffm_packed_layout_matches_split_cpu(k):
+    """The packed V|G slot layout (GPU default) runs the same arithmetic as split tables."""
+    rng = np.random.default_rng(2)
+    B, F, NF = 64, 6, 48
+    idx = torch.from_numpy(rng.integers(0, NF, size=(B, F)).astype(np.int32))
+    val = torch.from_numpy(rng.uniform(0.5, 2.0, size=(B, F)).astype(np.float32))
+    y = torch.from_numpy(np.where(rng.random(B) < 0.4, 1.0, -1.0).astype(np.float32))
+    a = _trainer("cpu", NF, F, k=k, extra="-w0")
+    b = _trainer("cpu", NF, F, k=k, extra="-w0")
+    _to_packed(b)
+    la, lb = torch.empty(B), torch.empty(B)
+    ffm_step(a.state, idx, None, val, y, a.hyper, loss=la)
+    ffm_step(b.state, idx, None, val, y, b.hyper, loss=lb)
+    assert torch.equal(la, lb)
+    for key in ("V", "G", "w", "wz", "wn", "bias"):
+        assert torch.equal(a.state[key], b.state[key].contiguous()), key
+    assert b.state_dict()["V"].is_contiguous()
 
 
 def test_ffm_fields_and_padding_cpu():
@@ -75,27 +105,55 @@ def test_train_ffm_udtf_strings():
 
 
 @pytest.mark.gpu
-def test_ffm_gpu_matches_cpu_engine():
-    """HIP kernel vs the sequential C++ engine: identical on rows with disjoint features
-    (no Hogwild interaction), and statistically equal on a real stream."""
+@pytest.mark.parametrize("layout,reload,k", [("packed", True, 4), ("packed", False, 4),
+                                             ("split", True, 4), ("packed", True, 8),
+                                             ("packed", False, 8)])
+def test_ffm_gpu_matches_cpu_engine(layout, reload, k):
+    """HIP kernels (packed-slot and split-table layouts, with and without the reload) vs the
+    sequential C++ engine: identical on rows with disjoint features (no Hogwild interaction)."""
     torch.manual_seed(0)
     B, F, NFLD = 512, 39, 39
     B_NF = B * F
     idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)  # all features distinct
     y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0)
     val = torch.rand(B, F) + 0.5
-    tc = _trainer("cpu", B_NF, NFLD)
-    tg = _trainer("cuda", B_NF, NFLD)
-    for k in tc.state:
-        tg.state[k].copy_(tc.state[k].cuda())
+    tc = _trainer("cpu", B_NF, NFLD, k=k)
+    tg = _trainer("cuda", B_NF, NFLD, k=k, extra="-split_state" if layout == "split" else "")
+    assert is_packed(tg.state["V"], tg.state["G"]) == (layout == "packed")
+    tg.hyper.reload = reload
+    for key in tc.state:
+        tg.state[key].copy_(tc.state[key].cuda())
     lc = torch.empty(B)
     lg = torch.empty(B, device="cuda")
     ffm_step(tc.state, idx, None, val, y, tc.hyper, loss=lc)
     ffm_step(tg.state, idx.cuda(), None, val.cuda(), y.cuda(), tg.hyper, loss=lg)
     torch.cuda.synchronize()
     np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=1e-4, atol=1e-5)
-    for k in ("V", "G", "w", "wz", "wn"):
-        np.testing.assert_allclose(tg.state[k].cpu().numpy(), tc.state[k].numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+    for key in ("V", "G", "w", "wz", "wn"):
+        np.testing.assert_allclose(tg.state[key].cpu().numpy(), tc.state[key].numpy(), rtol=1e-4, atol=1e-5,
+                                   err_msg=key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["packed", "split"])
+def test_ffm_gpu_bf16_state_close_to_fp32_engine(layout):
+    """bf16 stochastic-rounded state (both layouts) tracks the fp32 sequential engine."""
+    torch.manual_seed(1)
+    B, F = 256, 39
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0)
+    tc = _trainer("cpu", B * F, F)
+    tg = _trainer("cuda", B * F, F, extra="-bf16_state" + (" -split_state" if layout == "split" else ""))
+    assert tg.state["V"].dtype == torch.bfloat16
+    for key in tc.state:
+        tg.state[key].copy_(tc.state[key].cuda())
+    lc = torch.empty(B)
+    lg = torch.empty(B, device="cuda")
+    ffm_step(tc.state, idx, None, None, y, tc.hyper, loss=lc)
+    ffm_step(tg.state, idx.cuda(), None, None, y.cuda(), tg.hyper, loss=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=2e-2, atol=2e-3)
+    np.testing.assert_allclose(tg.state["V"].float().cpu().numpy(), tc.state["V"].numpy(), rtol=2e-2, atol=2e-3)
 
 
 @pytest.mark.gpu
