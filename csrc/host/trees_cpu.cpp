@@ -5,6 +5,7 @@
 #include <vector>
 
 #define HM_API extern "C" __attribute__((visibility("default")))
+#define HM_TREE_CAT 0x40000000  // nominal split flag (csrc/kernels/trees.hip)
 
 HM_API int hm_hist_build_cpu(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
                              const int64_t* seg, int n_seg, const float* stats, const float* smax,
@@ -36,10 +37,12 @@ HM_API int hm_tree_predict_cpu(const float* X, int64_t n, int d, const int32_t* 
         for (int t = 0; t < n_trees; ++t) {
             int k = roots[t];
             for (int depth = 0; depth < 64; ++depth) {
-                const int f = feature[k];
+                int f = feature[k];
                 if (f < 0) break;
+                const bool cat = f & HM_TREE_CAT;
+                f &= ~HM_TREE_CAT;
                 const float v = x[f];
-                k = v <= threshold[k] ? left[k] : right[k];  // NaN goes right
+                k = (cat ? v == threshold[k] : v <= threshold[k]) ? left[k] : right[k];  // NaN goes right
             }
             const float* val = values + voff[k];
             if (sum_trees) {
@@ -81,9 +84,12 @@ HM_API int hm_route_rows_cpu(const uint8_t* bins, int64_t n, int dpad, int32_t* 
     for (int64_t r = 0; r < n; ++r) {
         const int nd = node_of_row[r];
         if (nd < 0) continue;
-        const int f = split_feat[nd];
+        int f = split_feat[nd];
         if (f < 0) continue;
-        node_of_row[r] = bins[r * dpad + f] <= split_bin[nd] ? left_child[nd] : right_child[nd];
+        const bool cat = f & HM_TREE_CAT;
+        f &= ~HM_TREE_CAT;
+        const int b = bins[r * dpad + f];
+        node_of_row[r] = (cat ? b == split_bin[nd] : b <= split_bin[nd]) ? left_child[nd] : right_child[nd];
     }
     return 0;
 }

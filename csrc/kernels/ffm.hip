@@ -127,21 +127,36 @@ __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint3
     }
 }
 
-// Row metadata -> LDS and the instance-wise L2 normalisation factor (shared by both kernels;
-// contains the block barrier that publishes s_idx / s_fld / s_x).
-__device__ __forceinline__ float load_row_meta(const FFMParams& P, int row,
-                                               const int32_t* __restrict__ idx,
-                                               const int32_t* __restrict__ fld,
-                                               const float* __restrict__ val, int* s_idx,
-                                               int* s_fld, float* s_x, float* s_red) {
+// Row metadata of one slot (thread tid < F) from the padded-ELL batch.
+struct SlotMeta {
+    int i, f;
+    float x;
+};
+
+__device__ __forceinline__ SlotMeta fetch_row_meta(const FFMParams& P, int row,
+                                                   const int32_t* __restrict__ idx,
+                                                   const int32_t* __restrict__ fld,
+                                                   const float* __restrict__ val) {
+    SlotMeta m{-1, 0, 0.f};
     const int tid = threadIdx.x;
-    const int F = P.F;
+    if (tid < P.F && row < P.B) {
+        const size_t o = (size_t)row * P.F + tid;
+        m.i = idx[o];
+        m.f = fld ? fld[o] : tid;
+        m.x = val ? val[o] : 1.f;
+    }
+    return m;
+}
+
+// Metadata -> LDS and the instance-wise L2 normalisation factor (contains the block barrier
+// that publishes s_idx / s_fld / s_x).
+__device__ __forceinline__ float publish_row_meta(const FFMParams& P, SlotMeta m, int* s_idx,
+                                                  int* s_fld, float* s_x, float* s_red) {
+    const int tid = threadIdx.x;
     float sq = 0.f;
-    if (tid < F) {
-        const size_t o = (size_t)row * F + tid;
-        int i = idx[o];
-        int f = fld ? fld[o] : tid;
-        float x = val ? val[o] : 1.f;
+    if (tid < P.F) {
+        int i = m.i, f = m.f;
+        float x = m.x;
         if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; }
         s_idx[tid] = i;
         s_fld[tid] = f < 0 ? 0 : (f >= P.num_fields ? P.num_fields - 1 : f);
@@ -154,6 +169,14 @@ __device__ __forceinline__ float load_row_meta(const FFMParams& P, int row,
     }
     __syncthreads();
     return 1.f;
+}
+
+__device__ __forceinline__ float load_row_meta(const FFMParams& P, int row,
+                                               const int32_t* __restrict__ idx,
+                                               const int32_t* __restrict__ fld,
+                                               const float* __restrict__ val, int* s_idx,
+                                               int* s_fld, float* s_x, float* s_red) {
+    return publish_row_meta(P, fetch_row_meta(P, row, idx, fld, val), s_idx, s_fld, s_x, s_red);
 }
 
 // Loss of the row's score p; writes pred/loss (thread 0) and returns kappa = dloss/dp.
@@ -413,6 +436,8 @@ __global__ __launch_bounds__(256) void ffm_packed_kernel(
         ab[j] = s < FF ? ((s / F) | ((s % F) << 16)) : -1;
     }
 
+    // (Prefetching the next row's metadata during the gather was measured 15 % slower: the three
+    // extra VGPRs cross the 128-register line, 4 -> 3 waves/SIMD; profiles/ffm_layout_ab_r1.log.)
     for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
         const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);

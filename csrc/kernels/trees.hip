@@ -27,6 +27,10 @@
 //   every split and derives the sibling as parent - child (models/trees.py).
 #include "common.h"
 
+// Split-feature flag of a nominal (one-vs-rest) node: go left when x == threshold (prediction)
+// or bin == split bin (training); ordinal nodes go left when x <= threshold / bin <= split bin.
+#define HM_TREE_CAT 0x40000000
+
 namespace {
 
 
@@ -195,10 +199,14 @@ __global__ __launch_bounds__(256) void tree_predict_kernel(
         int k = roots[t];
         const float* x = X + row * d;
         for (int depth = 0; depth < 64; ++depth) {
-            const int f = feature[k];
+            int f = feature[k];
             if (f < 0) break;
+            const bool cat = f & HM_TREE_CAT;
+            f &= ~HM_TREE_CAT;
             const float v = x[f];
-            k = v <= threshold[k] ? left[k] : right[k];  // NaN goes right (Smile: x <= t ? true : false)
+            const float t = threshold[k];
+            // NaN goes right (Smile: x <= t ? true : false; nominal: x == t ? true : false)
+            k = (cat ? v == t : v <= t) ? left[k] : right[k];
         }
         const float* val = values + voff[k];
         if (sum_trees) {
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 }
 
 // Row routing after a level's splits: node_of_row[r] -> child id (or stays when the node
-// became a leaf).  split_feat[node] < 0 means leaf.
+// became a leaf).  split_feat[node] < 0 means leaf; HM_TREE_CAT marks a nominal split.
 __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ bins, int64_t n,
                                                     int dpad, int32_t* __restrict__ node_of_row,
                                                     const int32_t* __restrict__ split_feat,
@@ -248,10 +256,13 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
          r += (int64_t)gridDim.x * blockDim.x) {
         const int nd = node_of_row[r];
         if (nd < 0) continue;
-        const int f = split_feat[nd];
+        int f = split_feat[nd];
         if (f < 0) continue;
+        const bool cat = f & HM_TREE_CAT;
+        f &= ~HM_TREE_CAT;
         const int b = bins[r * dpad + f];
-        node_of_row[r] = b <= split_bin[nd] ? left_child[nd] : right_child[nd];
+        const int sb = split_bin[nd];
+        node_of_row[r] = (cat ? b == sb : b <= sb) ? left_child[nd] : right_child[nd];
     }
 }
 

@@ -34,16 +34,31 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import Learner, log
 
 MODEL_VERSION = 1
+CAT_FLAG = 1 << 30   # nominal split flag in flattened node arrays (HM_TREE_CAT in trees.hip)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
 
 
 # ------------------------------------------------------------------ quantisation
+def parse_attrs(spec, d: int) -> torch.Tensor | None:
+    """``-attrs Q,C,Q`` (or ``QCQ``; Q = quantitative, C = categorical/nominal) -> bool [d] mask
+    of the nominal columns, None when every column is quantitative (Smile's attribute types,
+    SURVEY.md §2.3.6)."""
+    if not spec:
+        return None
+    t = str(spec).replace(",", "").replace(" ", "").upper()
+    if len(t) != d or any(c not in "QC" for c in t):
+        raise UDFArgumentException(f"-attrs needs one of Q/C for each of the {d} columns: {spec!r}")
+    m = torch.tensor([c == "C" for c in t])
+    return m if bool(m.any()) else None
+
+
 @dataclass
 class Quantized:
     bins: torch.Tensor        # uint8 [n, dpad]
     edges: torch.Tensor       # f32 [d, B-1]
     d: int
     B: int
+    cat: torch.Tensor | None = None   # bool [d]: nominal columns (bin = category index)
 
     @property
     def dpad(self) -> int:
@@ -51,12 +66,17 @@ class Quantized:
 
 
 def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: int = 0,
-             edges: torch.Tensor | None = None, mixer=None) -> Quantized:
+             edges: torch.Tensor | None = None, mixer=None,
+             categorical: torch.Tensor | None = None) -> Quantized:
     """Per-feature quantile edges (from a row sample) and uint8 bins on X's device.
 
     With a mixer over several ranks every rank contributes an equal-size sample of its shard and
     the edges are computed from the all-gathered sample, so all ranks bin identically (required
-    by the histogram all-reduce of data-parallel boosting)."""
+    by the histogram all-reduce of data-parallel boosting).
+
+    Nominal columns (``categorical`` mask) get their sorted distinct values as edges, so a
+    category's bin is its index (exact, at most ``num_bins - 1`` categories; NaN takes the last
+    bin)."""
     X = X.float().contiguous()
     n, d = X.shape
     B = int(num_bins)
@@ -74,6 +94,21 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
         E = torch.quantile(S.T.contiguous(), qs, dim=1).T.contiguous()     # [d, B-1]
         E = torch.nan_to_num(E, nan=float("inf"))
         # strictly increasing edges (ties collapse to the same bin)
+        if categorical is not None:
+            for j in torch.nonzero(categorical).flatten().tolist():
+                col = X[:, j]
+                u = torch.unique(col[~torch.isnan(col)])
+                if world > 1:      # every rank needs the union of the categories
+                    pad = torch.full((1, B - 1), float("inf"), device=X.device)
+                    pad[0, : min(B - 1, u.numel())] = u[: B - 1]
+                    u = torch.unique(mixer.all_gather_cat(pad))
+                    u = u[torch.isfinite(u)]
+                if u.numel() > B - 1:
+                    raise UDFArgumentException(
+                        f"nominal column {j} has {u.numel()} distinct values (at most {B - 1})")
+                row = torch.full((B - 1,), float("inf"), device=X.device)
+                row[: u.numel()] = u
+                E[j] = row
         edges = E.contiguous()
     dpad = (d + 15) // 16 * 16   # 16-byte rows: a feature group is one aligned load
     bins = torch.zeros((n, dpad), dtype=torch.uint8, device=X.device)
@@ -83,7 +118,8 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
         _native.check(_native.hip().hm_quantize(*args, _native.stream_of(X.device)), "hm_quantize")
     else:
         _native.host().hm_quantize_cpu(*args)
-    return Quantized(bins, edges, d, B)
+    cat = None if categorical is None else categorical.to(torch.bool).cpu()
+    return Quantized(bins, edges, d, B, cat)
 
 
 # ------------------------------------------------------------------ trees
@@ -95,16 +131,29 @@ class Tree:
     right: list = field(default_factory=list)
     value: list = field(default_factory=list)       # list of floats per node (leaf output)
     n_out: int = 1
+    cat: list = field(default_factory=list)         # 1 = nominal node: left when x == threshold
+
+    def is_cat(self, k: int) -> bool:
+        return bool(self.cat) and bool(self.cat[k])
+
+    def goes_left(self, k: int, v) -> bool:
+        """Smile's test: ``x <= t`` (ordinal) / ``x == t`` (nominal); missing/NaN goes right."""
+        if v is None:
+            return False
+        return v == self.threshold[k] if self.is_cat(k) else v <= self.threshold[k]
 
     def to_json(self) -> dict:
-        return {"v": MODEL_VERSION, "f": self.feature,
-                "t": [None if not math.isfinite(x) else x for x in self.threshold],
-                "l": self.left, "r": self.right, "val": self.value, "o": self.n_out}
+        j = {"v": MODEL_VERSION, "f": self.feature,
+             "t": [None if not math.isfinite(x) else x for x in self.threshold],
+             "l": self.left, "r": self.right, "val": self.value, "o": self.n_out}
+        if any(self.cat):
+            j["c"] = self.cat
+        return j
 
     @staticmethod
     def from_json(j: dict) -> "Tree":
         return Tree(j["f"], [math.inf if x is None else x for x in j["t"]], j["l"], j["r"], j["val"],
-                    j["o"])
+                    j["o"], list(j.get("c", [])))
 
     def serialize(self) -> str:
         return base91.encode(zlib.compress(json.dumps(self.to_json(), separators=(",", ":")).encode()))
@@ -116,9 +165,8 @@ class Tree:
     def predict_one(self, x) -> list:
         k = 0
         while self.feature[k] >= 0:
-            v = x[self.feature[k]]
             # missing / NaN goes right, as in Smile's `x <= t ? trueChild : falseChild`
-            k = self.left[k] if (v is not None and v <= self.threshold[k]) else self.right[k]
+            k = self.left[k] if self.goes_left(k, x[self.feature[k]]) else self.right[k]
         return self.value[k]
 
     def depth(self) -> int:
@@ -133,7 +181,7 @@ def flatten(trees: list[Tree], device) -> dict:
     for t in trees:
         roots.append(base)
         for k in range(len(t.feature)):
-            feat.append(t.feature[k])
+            feat.append(t.feature[k] | CAT_FLAG if (t.feature[k] >= 0 and t.is_cat(k)) else t.feature[k])
             thr.append(t.threshold[k] if math.isfinite(t.threshold[k]) else 3.4e38)
             lft.append(t.left[k] + base if t.feature[k] >= 0 else 0)
             rgt.append(t.right[k] + base if t.feature[k] >= 0 else 0)
@@ -176,6 +224,7 @@ class HistTreeBuilder:
                  max_leaf_nodes: int | None = None, seed: int = 0, mixer=None, lam: float = 0.0,
                  alpha: float = 0.0, min_gain: float = 0.0, feature_mask: torch.Tensor | None = None):
         self.q = q
+        self.cat = q.cat                          # nominal columns: one-vs-rest splits
         self.criterion = criterion
         self.max_depth = max_depth
         if criterion == "xgb":
@@ -285,6 +334,7 @@ class HistTreeBuilder:
         act_rows = torch.nonzero(act).flatten().to(torch.int32)
         gen = torch.Generator(device=dev).manual_seed(int(self.gen.initial_seed()))
         edges = q.edges.to(dev)
+        cat_dev = None if self.cat is None else self.cat.to(dev)
         n_out = NS if self.criterion in ("gini", "entropy") else 1
         imp = torch.zeros(d, dtype=torch.float64, device=dev)
         # level 0: the root histogram over every active row
@@ -316,6 +366,16 @@ class HistTreeBuilder:
             right = tot[:, None, None, :] - cum
             gain = self._score(cum) + self._score(right) - self._score(tot)[:, None, None]
             cnt_ok = (self._weight(cum) >= self.min_leaf) & (self._weight(right) >= self.min_leaf)
+            if cat_dev is not None:
+                # nominal columns: "x == category b" vs the rest (Smile's nominal split); the
+                # left child holds bin b's own statistics.  The last bin (NaN / beyond the
+                # category list) is never a category.
+                rest = tot[:, None, None, :] - H
+                g_eq = self._score(H) + self._score(rest) - self._score(tot)[:, None, None]
+                ok_eq = (self._weight(H) >= self.min_leaf) & (self._weight(rest) >= self.min_leaf)
+                ok_eq[:, :, edges.shape[1]:] = False
+                gain = torch.where(cat_dev[None, :, None], g_eq, gain)
+                cnt_ok = torch.where(cat_dev[None, :, None], ok_eq, cnt_ok)
             gain = torch.where(cnt_ok, gain, torch.full_like(gain, -math.inf))
             if self.feature_mask is not None:
                 gain = torch.where(self.feature_mask.to(dev)[None, :, None], gain, torch.full_like(gain, -math.inf))
@@ -338,7 +398,8 @@ class HistTreeBuilder:
             rc = torch.where(ok, lc + 1, lc).to(torch.int32)
             thr = torch.where(bb < edges.shape[1], edges[bf.long(), bb.clamp(max=edges.shape[1] - 1).long()],
                               torch.full_like(best_gain, math.inf))
-            feats.append(torch.where(ok, bf, torch.full_like(bf, -1)))
+            bflag = bf if cat_dev is None else bf | (cat_dev[bf.long()].to(torch.int32) * CAT_FLAG)
+            feats.append(torch.where(ok, bflag, torch.full_like(bf, -1)))
             thrs.append(torch.where(ok, thr, torch.full_like(thr, math.inf)))
             lefts.append(lc)
             rights.append(rc)
@@ -359,6 +420,9 @@ class HistTreeBuilder:
                 _native.host().hm_route_rows_cpu(*args)
             # next level: histogram the smaller child of every split, derive the sibling
             left_tot = cum[li, bf[li].long(), bb[li].long()]                   # [S, NS]
+            if cat_dev is not None:
+                left_eq = H[li, bf[li].long(), bb[li].long()]
+                left_tot = torch.where(cat_dev[bf[li].long()][:, None], left_eq, left_tot)
             right_tot = tot[li] - left_tot
             small_right = self._weight(right_tot) < self._weight(left_tot)     # [S]
             small_id = torch.where(small_right, rc[li], lc[li]) - nb           # local child id
@@ -388,7 +452,9 @@ class HistTreeBuilder:
         V = torch.cat(vals).double().cpu().numpy()
         self.node_values = torch.cat(vals)
         tree = Tree(n_out=n_out)
-        tree.feature = [int(f) for f in F]
+        cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
+        tree.cat = cflag if any(cflag) else []
+        tree.feature = [int(f) & ~CAT_FLAG if f >= 0 else int(f) for f in F]
         tree.threshold = [float(t) for t in T]
         tree.left = [int(x) for x in Lc]
         tree.right = [int(x) for x in Rc]
@@ -406,9 +472,12 @@ TREE_OPTS = [
     opt("min_split", "min_samples_split", 2, int, "Minimum rows to split a node"),
     opt("min_samples_leaf", None, 1, int, "Minimum rows in a leaf"),
     opt("seed", None, -1, int, "Seed"),
-    opt("attrs", "attribute_types", None, str, "Attribute types (Q/C per column; C treated as ordinal bins)"),
+    opt("attrs", "attribute_types", None, str,
+        "Attribute types, Q (quantitative) or C (categorical) per column, e.g. Q,C,Q; categorical "
+        "columns get one-vs-rest 'x == v' splits"),
     opt("subsample", None, 1.0, float, "Bootstrap sampling rate"),
-    flag("stratified", "stratified_sampling", "Stratified bootstrap (accepted)"),
+    flag("stratified", "stratified_sampling", "Stratified bootstrap: sample every class at the "
+                                              "-subsample rate"),
     opt("splits", "split_rule", "GINI", str, "GINI | ENTROPY"),
     opt("num_bins", None, 256, int, "[engine] histogram bins (<= 256)"),
 ]
@@ -470,9 +539,9 @@ class _ForestBase(Learner):
 
     def fit(self, features, labels):
         X, y = self._prep(features, labels)
-        q = quantize(X, self.num_bins, seed=self.seed)
         n, d = X.shape
         c = self.cl
+        q = quantize(X, self.num_bins, seed=self.seed, categorical=parse_attrs(c["attrs"], d))
         if self.TASK == "classification":
             cls, yi = _encode_classes(y)
             self.classes = cls
@@ -489,11 +558,10 @@ class _ForestBase(Learner):
         rank = self.rank
         T = int(c["trees"])
         my = [t for t in range(T) if t % world == rank]
+        strat = yi if (self.TASK == "classification" and c["stratified"]) else None
         for t in my:
-            m = max(1, int(round(n * float(c["subsample"]))))
             g.manual_seed(self.seed * 1000003 + t)   # tree t's bootstrap does not depend on the rank split
-            draw = torch.randint(0, n, (m,), generator=g, device=self.device)
-            w = torch.bincount(draw, minlength=n).float()
+            w = bootstrap_weights(n, float(c["subsample"]), g, self.device, strat)
             if self.TASK == "classification":
                 if onehot.shape[1] > 8:
                     raise UDFArgumentException("train_randomforest_classifier: > 8 classes not supported on this engine")
@@ -545,6 +613,24 @@ class _ForestBase(Learner):
         return p[:, 0]
 
 
+def bootstrap_weights(n: int, rate: float, gen: torch.Generator, device,
+                      strata: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-row multiplicities of a bootstrap sample of round(n * rate) rows with replacement;
+    with ``strata`` (class index per row) every class is sampled at that rate separately
+    (``-stratified``), so rare classes keep their share in every tree."""
+    if strata is None:
+        m = max(1, int(round(n * rate)))
+        draw = torch.randint(0, n, (m,), generator=gen, device=device)
+        return torch.bincount(draw, minlength=n).float()
+    w = torch.zeros(n, dtype=torch.float32, device=device)
+    for k in torch.unique(strata).tolist():
+        rows = torch.nonzero(strata == k).flatten()
+        m = max(1, int(round(rows.numel() * rate)))
+        pick = rows[torch.randint(0, rows.numel(), (m,), generator=gen, device=device)]
+        w += torch.bincount(pick, minlength=n).float()
+    return w
+
+
 class RandomForestClassifier(_ForestBase):
     NAME = "train_randomforest_classifier"
     TASK = "classification"
@@ -565,7 +651,8 @@ GBT_OPTS = [
     opt("min_samples_leaf", None, 1, int, "Minimum rows in a leaf"),
     opt("mtry", "vars", None, int, "Random features per split (default: all)"),
     opt("seed", None, -1, int, "Seed"),
-    opt("attrs", "attribute_types", None, str, "Attribute types (accepted)"),
+    opt("attrs", "attribute_types", None, str,
+        "Attribute types, Q or C per column (C: one-vs-rest 'x == v' splits)"),
     opt("num_bins", None, 256, int, "[engine] histogram bins"),
     opt("lambda", None, 0.0, float, "[engine] L2 on leaf values (0 = Friedman's least squares)"),
 ]
@@ -593,7 +680,8 @@ class GradientTreeBoostingClassifier(Learner):
         yi = yi.to(self.device)
         K = len(self.classes)
         n, d = X.shape
-        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer)
+        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer,
+                     categorical=parse_attrs(c["attrs"], d))
         self.importance = np.zeros(d)
         g = torch.Generator(device=self.device).manual_seed(self.seed)
         eta = float(c["eta"])
@@ -761,7 +849,8 @@ def tree_export(model, options: str = "-type graphviz", feature_names=None, clas
             if tree.feature[k] < 0:
                 v = tree.value[k]
                 return f"{ind}return {int(np.argmax(v)) if len(v) > 1 else v[0]};\n"
-            return (f"{ind}if ({fname(tree.feature[k])} <= {tree.threshold[k]}) {{\n" +
+            op = "==" if tree.is_cat(k) else "<="
+            return (f"{ind}if ({fname(tree.feature[k])} {op} {tree.threshold[k]}) {{\n" +
                     rec(tree.left[k], ind + "  ") + f"{ind}}} else {{\n" + rec(tree.right[k], ind + "  ") +
                     f"{ind}}}\n")
         return "function predict(x) {\n" + rec(0, "  ") + "}"
@@ -772,7 +861,8 @@ def tree_export(model, options: str = "-type graphviz", feature_names=None, clas
             lab = (class_names[int(np.argmax(v))] if class_names else int(np.argmax(v))) if len(v) > 1 else v[0]
             lines.append(f' {k} [label="{lab}"];')
         else:
-            lines.append(f' {k} [label="{fname(tree.feature[k])} <= {tree.threshold[k]:.6g}"];')
+            op = "==" if tree.is_cat(k) else "<="
+            lines.append(f' {k} [label="{fname(tree.feature[k])} {op} {tree.threshold[k]:.6g}"];')
             lines.append(f" {k} -> {tree.left[k]} [label=\"yes\"];")
             lines.append(f" {k} -> {tree.right[k]} [label=\"no\"];")
     lines.append("}")
@@ -790,8 +880,11 @@ def decision_path(model_id, model, features, options=None):
     k = 0
     while tree.feature[k] >= 0:
         f, t = tree.feature[k], tree.threshold[k]
-        go_left = x[f] <= t
-        path.append(f"{f} {'<=' if go_left else '>'} {t:.6g}")
+        go_left = tree.goes_left(k, x[f])
+        if tree.is_cat(k):
+            path.append(f"{f} {'==' if go_left else '!='} {t:.6g}")
+        else:
+            path.append(f"{f} {'<=' if go_left else '>'} {t:.6g}")
         k = tree.left[k] if go_left else tree.right[k]
     path.append(f"value={tree.value[k]}")
     return path
