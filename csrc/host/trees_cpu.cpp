@@ -93,3 +93,105 @@ HM_API int hm_route_rows_cpu(const uint8_t* bins, int64_t n, int dpad, int32_t* 
     }
     return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Host twin of split_find_kernel (csrc/kernels/trees.hip): same criteria, candidate-feature
+// draw (feat_key ranking) and tie-break (larger gain, then smaller feature*B + bin).
+namespace {
+
+inline uint32_t feat_key(uint32_t seed, uint32_t node, uint32_t f) {
+    uint32_t h = seed * 0x9E3779B1u ^ (node + 0x7F4A7C15u) * 0x85EBCA77u ^ (f + 1u) * 0xC2B2AE3Du;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+
+inline float split_weight(const float* S, int NS, int crit) {
+    if (crit <= 1) { float w = 0.f; for (int s = 0; s < NS; ++s) w += S[s]; return w; }
+    if (crit == 3) return NS > 2 ? S[2] : 0.f;
+    return NS > 1 ? S[1] : 0.f;
+}
+
+inline float split_score(const float* S, int NS, int crit, float lam, float alpha) {
+    if (crit == 0) {
+        float w = 0.f, q = 0.f;
+        for (int s = 0; s < NS; ++s) { w += S[s]; q += S[s] * S[s]; }
+        return w > 0.f ? q / std::fmax(w, 1e-30f) : 0.f;
+    }
+    if (crit == 1) {
+        float w = 0.f;
+        for (int s = 0; s < NS; ++s) w += S[s];
+        const float iw = 1.f / std::fmax(w, 1e-30f);
+        float e = 0.f;
+        for (int s = 0; s < NS; ++s) e += S[s] * std::log(std::fmax(S[s] * iw, 1e-30f));
+        return e;
+    }
+    const float s0 = S[0];
+    if (crit == 2) { const float s1 = S[NS > 1 ? 1 : 0]; return s1 > 0.f ? s0 * s0 / std::fmax(s1, 1e-30f) : 0.f; }
+    if (crit == 3) { const float s2 = S[NS > 2 ? 2 : 0]; return s2 > 0.f ? s0 * s0 / (s2 + lam) : 0.f; }
+    const float s1 = S[NS > 1 ? 1 : 0];
+    float g = s0;
+    if (alpha > 0.f) { const float m = std::fabs(g) - alpha; g = m > 0.f ? std::copysign(m, g) : 0.f; }
+    return s1 > 0.f ? g * g / (s1 + lam) : 0.f;
+}
+
+}  // namespace
+
+HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* fp, const uint8_t* cat,
+                             const uint8_t* fmask, float* gain, int32_t* feat, int32_t* bin, float* left,
+                             float* tot) {
+    const int L = ip[0], d = ip[1], B = ip[2], NS = ip[3], n_edges = ip[4], crit = ip[5];
+    const int mtry = ip[6], node_base = ip[7];
+    const uint32_t seed = (uint32_t)ip[8];
+    const float lam = fp[0], alpha = fp[1], min_leaf = fp[2];
+    if (B <= 0 || B > 256 || NS <= 0 || NS > 8 || crit < 0 || crit > 4) return 1;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int node = 0; node < L; ++node) {
+        const float* hn = hist + (size_t)node * d * B * NS;
+        float T[8] = {0}, Lb[8] = {0}, run[8], lf[8], rt[8];
+        for (int b = 0; b < B; ++b)
+            for (int s = 0; s < NS; ++s) T[s] += hn[(size_t)b * NS + s];
+        const float parent = split_score(T, NS, crit, lam, alpha);
+        float best = -INFINITY;
+        int best_i = 0x7FFFFFFF;
+        for (int f = 0; f < d; ++f) {
+            if (fmask && !fmask[f]) continue;
+            if (mtry > 0 && mtry < d) {
+                const uint32_t kf = feat_key(seed, (uint32_t)(node_base + node), (uint32_t)f);
+                int before = 0;
+                for (int g = 0; g < d; ++g) {
+                    const uint32_t kg = feat_key(seed, (uint32_t)(node_base + node), (uint32_t)g);
+                    before += (kg < kf || (kg == kf && g < f)) ? 1 : 0;
+                }
+                if (before >= mtry) continue;
+            }
+            const bool is_cat = cat && cat[f];
+            const float* hf = hn + (size_t)f * B * NS;
+            for (int s = 0; s < NS; ++s) run[s] = 0.f;
+            for (int b = 0; b < B; ++b) {
+                for (int s = 0; s < NS; ++s) {
+                    run[s] += hf[(size_t)b * NS + s];
+                    lf[s] = is_cat ? hf[(size_t)b * NS + s] : run[s];
+                    rt[s] = T[s] - lf[s];
+                }
+                if (split_weight(lf, NS, crit) < min_leaf || split_weight(rt, NS, crit) < min_leaf) continue;
+                if (is_cat && b >= n_edges) continue;
+                const float g = split_score(lf, NS, crit, lam, alpha) + split_score(rt, NS, crit, lam, alpha) - parent;
+                const int i = f * B + b;
+                if (g > best || (g == best && i < best_i)) {
+                    best = g;
+                    best_i = i;
+                    for (int s = 0; s < NS; ++s) Lb[s] = lf[s];
+                }
+            }
+        }
+        const bool found = best_i != 0x7FFFFFFF;
+        gain[node] = found ? best : -INFINITY;
+        feat[node] = found ? best_i / B : 0;
+        bin[node] = found ? best_i % B : 0;
+        for (int s = 0; s < NS; ++s) {
+            left[node * NS + s] = Lb[s];
+            tot[node * NS + s] = T[s];
+        }
+    }
+    return 0;
+}

@@ -266,6 +266,213 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Fused split search of one tree level (replaces ~30 tensor ops over [L, d, B, NS] per level).
+// One 256-thread block per node; each wave takes features f = wave, wave + 4, ...; a lane owns
+// ceil(B / 64) consecutive bins, the bin prefix sums are a wave scan, the best bin is a wave
+// argmax and the best feature a block argmax.  Criteria (split gain = score(L) + score(R) -
+// score(parent), children need weight >= min_leaf):
+//   0 gini     S = class counts        score = sum S^2 / W              W = sum S
+//   1 entropy  S = class counts        score = sum S log(S / W)         W = sum S
+//   2 variance S = (sum w y, sum w)    score = S0^2 / S1                W = S1
+//   3 gbt      S = (sum r, sum h, n)   score = S0^2 / (S2 + lambda)     W = S2
+//   4 xgb      S = (sum g, sum h)      score = T(S0)^2 / (S1 + lambda)  W = S1 (T: L1 soft threshold)
+// Nominal columns (cat[f]) score "bin == b" against the rest, never the last bin (NaN / beyond
+// the category list).  mtry < d draws the node's candidate features by ranking a counter hash
+// of (seed, node, feature) — the same draw on the host engine (trees_cpu.cpp).
+struct SplitParams {
+    int L, d, B, NS, n_edges;
+    int crit, mtry, node_base;
+    float lam, alpha, min_leaf;
+    uint32_t seed;
+};
+
+__host__ __device__ __forceinline__ uint32_t feat_key(uint32_t seed, uint32_t node, uint32_t f) {
+    uint32_t h = seed * 0x9E3779B1u ^ (node + 0x7F4A7C15u) * 0x85EBCA77u ^ (f + 1u) * 0xC2B2AE3Du;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+
+__device__ __forceinline__ float soft_thr(float g, float a) {
+    if (a <= 0.f) return g;
+    const float m = fabsf(g) - a;
+    return m > 0.f ? copysignf(m, g) : 0.f;
+}
+
+template <int NS>
+__device__ __forceinline__ float split_weight(const float* S, int crit) {
+    if (crit <= 1) { float w = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) w += S[s];
+        return w; }
+    if (crit == 3) return NS > 2 ? S[NS > 2 ? 2 : 0] : 0.f;
+    return NS > 1 ? S[NS > 1 ? 1 : 0] : 0.f;
+}
+
+template <int NS>
+__device__ __forceinline__ float split_score(const float* S, int crit, float lam, float alpha) {
+    if (crit == 0) {
+        float w = 0.f, q = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { w += S[s]; q += S[s] * S[s]; }
+        return w > 0.f ? q / fmaxf(w, 1e-30f) : 0.f;
+    }
+    if (crit == 1) {
+        float w = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) w += S[s];
+        const float iw = 1.f / fmaxf(w, 1e-30f);
+        float e = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) e += S[s] * logf(fmaxf(S[s] * iw, 1e-30f));
+        return e;
+    }
+    const float s0 = S[0];
+    if (crit == 2) { const float s1 = S[NS > 1 ? 1 : 0]; return s1 > 0.f ? s0 * s0 / fmaxf(s1, 1e-30f) : 0.f; }
+    if (crit == 3) { const float s2 = S[NS > 2 ? 2 : 0]; return s2 > 0.f ? s0 * s0 / (s2 + lam) : 0.f; }
+    const float s1 = S[NS > 1 ? 1 : 0];
+    const float g = soft_thr(s0, alpha);
+    return s1 > 0.f ? g * g / (s1 + lam) : 0.f;
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const float* __restrict__ hist,
+                                                         const uint8_t* __restrict__ cat,
+                                                         const uint8_t* __restrict__ fmask,
+                                                         float* __restrict__ out_gain,
+                                                         int32_t* __restrict__ out_feat,
+                                                         int32_t* __restrict__ out_bin,
+                                                         float* __restrict__ out_left,
+                                                         float* __restrict__ out_tot) {
+    __shared__ float s_gain[4];
+    __shared__ int s_idx[4];
+    __shared__ float s_left[4][NS];
+    const int node = blockIdx.x;
+    const int lane = hm::lane_id(), wave = hm::wave_id();
+    const int B = P.B, d = P.d;
+    const int bpl = (B + 63) / 64;              // bins per lane (<= 4)
+    const int b0 = lane * bpl;
+    const float* hn = hist + (size_t)node * d * B * NS;
+    // parent totals (feature 0's histogram), identical in every wave
+    float tot[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) tot[s] = 0.f;
+    for (int k = 0; k < bpl; ++k)
+        if (b0 + k < B)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) tot[s] += hn[(size_t)(b0 + k) * NS + s];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) tot[s] = hm::wave_sum(tot[s]);
+    const float parent = split_score<NS>(tot, P.crit, P.lam, P.alpha);
+
+    float best = -INFINITY;
+    int best_i = 0x7FFFFFFF;
+    float best_left[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) best_left[s] = 0.f;
+    for (int f = wave; f < d; f += 4) {
+        if (fmask && !fmask[f]) continue;
+        if (P.mtry > 0 && P.mtry < d) {
+            // candidate iff fewer than mtry features rank before f (wave-uniform loop)
+            const uint32_t kf = feat_key(P.seed, (uint32_t)(P.node_base + node), (uint32_t)f);
+            int before = 0;
+            for (int g = lane; g < d; g += 64) {
+                const uint32_t kg = feat_key(P.seed, (uint32_t)(P.node_base + node), (uint32_t)g);
+                before += (kg < kf || (kg == kf && g < f)) ? 1 : 0;
+            }
+            for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+            if (before >= P.mtry) continue;
+        }
+        const bool is_cat = cat && cat[f];
+        const float* hf = hn + (size_t)f * B * NS;
+        float h[4][NS];
+        float lsum[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) lsum[s] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool in = k < bpl && b0 + k < B;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                h[k][s] = in ? hf[(size_t)(b0 + k) * NS + s] : 0.f;
+                lsum[s] += h[k][s];
+            }
+        }
+        // exclusive wave scan of the lane sums -> running left statistics
+        float run[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            float v = lsum[s];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const float t = __shfl_up(v, o, 64);
+                if (lane >= o) v += t;
+            }
+            run[s] = v - lsum[s];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k >= bpl || b0 + k >= B) break;
+            const int b = b0 + k;
+            float left[NS], right[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                run[s] += h[k][s];
+                left[s] = is_cat ? h[k][s] : run[s];
+                right[s] = tot[s] - left[s];
+            }
+            bool ok = split_weight<NS>(left, P.crit) >= P.min_leaf &&
+                      split_weight<NS>(right, P.crit) >= P.min_leaf;
+            if (is_cat && b >= P.n_edges) ok = false;
+            if (!ok) continue;
+            const float g = split_score<NS>(left, P.crit, P.lam, P.alpha) +
+                            split_score<NS>(right, P.crit, P.lam, P.alpha) - parent;
+            const int i = f * B + b;
+            if (g > best || (g == best && i < best_i)) {
+                best = g;
+                best_i = i;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) best_left[s] = left[s];
+            }
+        }
+    }
+    // wave argmax (ties -> smaller flattened (feature, bin) index)
+    for (int o = 32; o > 0; o >>= 1) {
+        const float og = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(best_i, o, 64);
+        float ol[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) ol[s] = __shfl_xor(best_left[s], o, 64);
+        if (og > best || (og == best && oi < best_i)) {
+            best = og;
+            best_i = oi;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) best_left[s] = ol[s];
+        }
+    }
+    if (lane == 0) {
+        s_gain[wave] = best;
+        s_idx[wave] = best_i;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) s_left[wave][s] = best_left[s];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int w = 0;
+        for (int k = 1; k < 4; ++k)
+            if (s_gain[k] > s_gain[w] || (s_gain[k] == s_gain[w] && s_idx[k] < s_idx[w])) w = k;
+        const bool found = s_idx[w] != 0x7FFFFFFF;
+        out_gain[node] = found ? s_gain[w] : -INFINITY;
+        out_feat[node] = found ? s_idx[w] / B : 0;
+        out_bin[node] = found ? s_idx[w] % B : 0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            out_left[node * NS + s] = s_left[w][s];
+            out_tot[node * NS + s] = tot[s];
+        }
+    }
+}
 }  // namespace
 
 // hist [n_seg, d, B, NS] (zeroed by the caller) += statistics of rows[seg[k]..seg[k+1]) for
@@ -345,5 +552,28 @@ HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int32_t* node
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(route_kernel, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
                        node_of_row, split_feat, split_bin, left_child, right_child);
+    HM_LAUNCH_RET();
+}
+
+// Best split of every node of a level: hist [L, d, B, NS] -> gain [L] (-inf: none), feature,
+// bin, left-child statistics [L, NS] and node totals [L, NS].  cat / fmask: [d] bytes or null.
+// ip: L, d, B, NS, n_edges, crit, mtry, node_base, seed;  fp: lambda, alpha, min_leaf
+HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, const uint8_t* cat,
+                         const uint8_t* fmask, float* gain, int32_t* feat, int32_t* bin, float* left,
+                         float* tot, hipStream_t stream) {
+    SplitParams P;
+    P.L = ip[0]; P.d = ip[1]; P.B = ip[2]; P.NS = ip[3]; P.n_edges = ip[4]; P.crit = ip[5];
+    P.mtry = ip[6]; P.node_base = ip[7]; P.seed = (uint32_t)ip[8];
+    P.lam = fp[0]; P.alpha = fp[1]; P.min_leaf = fp[2];
+    if (P.L <= 0) return 0;
+    if (P.B <= 0 || P.B > 256 || P.d <= 0 || P.crit < 0 || P.crit > 4) return (int)hipErrorInvalidValue;
+#define HM_SF(K) \
+    case K: hipLaunchKernelGGL((split_find_kernel<K>), dim3(P.L), dim3(256), 0, stream, P, hist, cat, fmask, \
+                               gain, feat, bin, left, tot); break;
+    switch (P.NS) {
+        HM_SF(1) HM_SF(2) HM_SF(3) HM_SF(4) HM_SF(5) HM_SF(6) HM_SF(7) HM_SF(8)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HM_SF
     HM_LAUNCH_RET();
 }

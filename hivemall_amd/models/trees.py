@@ -243,6 +243,8 @@ class HistTreeBuilder:
         self.mixer = mixer
         self.lam = lam
         self.importance = np.zeros(q.d)
+        self._seed32 = int(seed) & 0x7FFFFFFF      # candidate-feature draw (mtry) of hm_split_find
+        self._masks = None
 
     # -- statistics -> impurity / gain
     def _score(self, S: torch.Tensor) -> torch.Tensor:
@@ -295,6 +297,38 @@ class HistTreeBuilder:
         return torch.where(ok, S[:, 0:1] / torch.where(ok, S[:, 1:2], torch.ones_like(S[:, 1:2])),
                            torch.zeros_like(S[:, :1]))
 
+    _CRIT = {"gini": 0, "entropy": 1, "variance": 2, "gbt": 3, "xgb": 4}
+
+    def _split_find(self, H: torch.Tensor, node_base: int):
+        """Best split of every node of the level (csrc hm_split_find: one fused kernel instead
+        of ~30 tensor ops over [L, d, B, NS]).  Returns gain [L] (-inf: no valid split), feature
+        and bin (int32), left-child statistics [L, NS] and node totals [L, NS]."""
+        L, d, B, NS = H.shape
+        dev = H.device
+        H = H.contiguous()
+        gain = torch.empty(L, dtype=torch.float32, device=dev)
+        feat = torch.empty(L, dtype=torch.int32, device=dev)
+        bins = torch.empty(L, dtype=torch.int32, device=dev)
+        left = torch.empty((L, NS), dtype=torch.float32, device=dev)
+        tot = torch.empty((L, NS), dtype=torch.float32, device=dev)
+        mtry = int(self.mtry) if (self.mtry is not None and self.mtry < d) else 0
+        ip = np.array([L, d, B, NS, self.q.edges.shape[1], self._CRIT[self.criterion], mtry,
+                       node_base, self._seed32], dtype=np.int32)
+        fp = np.array([self.lam, self.alpha, float(self.min_leaf)], dtype=np.float32)
+        if self._masks is None or self._masks[0] != dev:
+            u8 = lambda m: None if m is None else m.to(device=dev, dtype=torch.uint8).contiguous()
+            self._masks = (dev, u8(self.cat), u8(self.feature_mask))
+        _, cat, fm = self._masks
+        p = _native.ptr
+        args = (p(H), ip.ctypes.data, fp.ctypes.data, p(cat), p(fm), p(gain), p(feat), p(bins),
+                p(left), p(tot))
+        if dev.type == "cuda":
+            _native.check(_native.hip().hm_split_find(*args, _native.stream_of(dev)), "hm_split_find")
+        else:
+            if _native.host().hm_split_find_cpu(*args) != 0:
+                raise RuntimeError("hm_split_find_cpu: invalid arguments")
+        return gain, feat, bins, left, tot
+
     def _hist(self, rows, seg, n_seg, stats, smax):
         """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
         q = self.q
@@ -332,7 +366,6 @@ class HistTreeBuilder:
             node_of_row[~active] = -1
             act &= active
         act_rows = torch.nonzero(act).flatten().to(torch.int32)
-        gen = torch.Generator(device=dev).manual_seed(int(self.gen.initial_seed()))
         edges = q.edges.to(dev)
         cat_dev = None if self.cat is None else self.cat.to(dev)
         n_out = NS if self.criterion in ("gini", "entropy") else 1
@@ -354,44 +387,21 @@ class HistTreeBuilder:
         sb_all, lc_all, rc_all = sf_all.clone(), sf_all.clone(), sf_all.clone()
         depth = 0
         while True:
-            tot = H[:, 0].sum(1)                                               # [L, NS]
-            vals.append(self._leaf_values(tot))
             if depth >= self.max_depth:
+                vals.append(self._leaf_values(H[:, 0].sum(1)))
                 feats.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 thrs.append(torch.full((L,), math.inf, device=dev))
                 lefts.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 rights.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 break
-            cum = torch.cumsum(H, dim=2)
-            right = tot[:, None, None, :] - cum
-            gain = self._score(cum) + self._score(right) - self._score(tot)[:, None, None]
-            cnt_ok = (self._weight(cum) >= self.min_leaf) & (self._weight(right) >= self.min_leaf)
-            if cat_dev is not None:
-                # nominal columns: "x == category b" vs the rest (Smile's nominal split); the
-                # left child holds bin b's own statistics.  The last bin (NaN / beyond the
-                # category list) is never a category.
-                rest = tot[:, None, None, :] - H
-                g_eq = self._score(H) + self._score(rest) - self._score(tot)[:, None, None]
-                ok_eq = (self._weight(H) >= self.min_leaf) & (self._weight(rest) >= self.min_leaf)
-                ok_eq[:, :, edges.shape[1]:] = False
-                gain = torch.where(cat_dev[None, :, None], g_eq, gain)
-                cnt_ok = torch.where(cat_dev[None, :, None], ok_eq, cnt_ok)
-            gain = torch.where(cnt_ok, gain, torch.full_like(gain, -math.inf))
-            if self.feature_mask is not None:
-                gain = torch.where(self.feature_mask.to(dev)[None, :, None], gain, torch.full_like(gain, -math.inf))
-            if self.mtry is not None and self.mtry < d:
-                pick = torch.rand((L, d), generator=gen, device=dev).topk(self.mtry, 1).indices
-                fm = torch.zeros((L, d), dtype=torch.bool, device=dev).scatter_(1, pick, True)
-                gain = torch.where(fm[:, :, None], gain, torch.full_like(gain, -math.inf))
-            best_gain, best = gain.reshape(L, -1).max(1)
+            best_gain, bf, bb, left_all, tot = self._split_find(H, base)
+            vals.append(self._leaf_values(tot))
             ok = (best_gain > max(1e-12, self.min_gain)) & torch.isfinite(best_gain) & \
                 (self._weight(tot) >= self.min_split)
             if self.max_leaves is not None:
                 ok &= torch.cumsum(ok.long(), 0) <= (int(self.max_leaves) - n_leaves)
             li = torch.nonzero(ok).flatten()                                   # the level's one sync
             n_split = li.numel()
-            bf = (best // B).to(torch.int32)
-            bb = (best % B).to(torch.int32)
             rank = torch.cumsum(ok.int(), 0) - 1
             nb = base + L
             lc = torch.where(ok, nb + 2 * rank, torch.full_like(rank, -1)).to(torch.int32)
@@ -419,10 +429,7 @@ class HistTreeBuilder:
             else:
                 _native.host().hm_route_rows_cpu(*args)
             # next level: histogram the smaller child of every split, derive the sibling
-            left_tot = cum[li, bf[li].long(), bb[li].long()]                   # [S, NS]
-            if cat_dev is not None:
-                left_eq = H[li, bf[li].long(), bb[li].long()]
-                left_tot = torch.where(cat_dev[bf[li].long()][:, None], left_eq, left_tot)
+            left_tot = left_all[li]                                            # [S, NS]
             right_tot = tot[li] - left_tot
             small_right = self._weight(right_tot) < self._weight(left_tot)     # [S]
             small_id = torch.where(small_right, rc[li], lc[li]) - nb           # local child id
@@ -912,3 +919,5 @@ _native.register_host("hm_quantize_cpu", [_P, _I64, C.c_int, C.c_int, _P, C.c_in
 _native.register_hip("hm_absmax_cols", [_P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [_P])
 _native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5)
+_native.register_hip("hm_split_find", [_P] * 10 + [_P])
+_native.register_host("hm_split_find_cpu", [_P] * 10)
