@@ -473,6 +473,95 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
         }
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Level row partition (replaces a full 16-bit key sort of the active rows per level): the rows
+// of the smaller child of every split, grouped by child, as the next level's histogram input.
+// key(r) = lut[node_of_row[r] - nb] (32767 / out of range: not histogrammed).  Two passes over
+// fixed row chunks (one per block): count per (key, block) in LDS, a device-wide inclusive scan
+// of the key-major counts (torch.cumsum), then scatter with LDS rank counters.  Order inside a
+// (key, block) cell is arbitrary; the histogram sums do not depend on it (32-bit fixed point).
+__device__ __forceinline__ int part_key(const int32_t* __restrict__ node_of_row,
+                                        const int16_t* __restrict__ lut, int row, int nb, int nlut,
+                                        int nkeys) {
+    const int c = node_of_row[row] - nb;
+    if (c < 0 || c >= nlut) return -1;
+    const int k = lut[c];
+    return k < nkeys ? k : -1;
+}
+
+__global__ __launch_bounds__(256) void part_count_kernel(const int32_t* __restrict__ rows, int64_t m,
+                                                         const int32_t* __restrict__ node_of_row,
+                                                         const int16_t* __restrict__ lut, int nb,
+                                                         int nlut, int nkeys,
+                                                         int32_t* __restrict__ counts /* [nkeys][G] */) {
+    extern __shared__ int s_cnt[];
+    const int G = gridDim.x;
+    for (int k = threadIdx.x; k < nkeys; k += blockDim.x) s_cnt[k] = 0;
+    __syncthreads();
+    const int64_t chunk = (m + G - 1) / G;
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(m, r0 + chunk);
+    for (int64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) {
+        const int k = part_key(node_of_row, lut, rows[q], nb, nlut, nkeys);
+        if (k >= 0) atomicAdd(&s_cnt[k], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nkeys; k += blockDim.x) counts[(size_t)k * G + blockIdx.x] = s_cnt[k];
+}
+
+__global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __restrict__ rows, int64_t m,
+                                                           const int32_t* __restrict__ node_of_row,
+                                                           const int16_t* __restrict__ lut, int nb,
+                                                           int nlut, int nkeys,
+                                                           const int32_t* __restrict__ counts,
+                                                           const int64_t* __restrict__ incl,
+                                                           int32_t* __restrict__ out,
+                                                           int64_t* __restrict__ seg /* [nkeys+1] */) {
+    extern __shared__ int64_t s_pos[];
+    const int G = gridDim.x;
+    for (int k = threadIdx.x; k < nkeys; k += blockDim.x) {
+        const size_t c = (size_t)k * G + blockIdx.x;
+        s_pos[k] = incl[c] - counts[c];               // first slot of this (key, block) cell
+    }
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k <= nkeys; k += blockDim.x)
+            seg[k] = k == 0 ? 0 : incl[(size_t)k * G - 1];
+    }
+    __syncthreads();
+    const int64_t chunk = (m + G - 1) / G;
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(m, r0 + chunk);
+    for (int64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) {
+        const int row = rows[q];
+        const int k = part_key(node_of_row, lut, row, nb, nlut, nkeys);
+        if (k >= 0) {
+            const int64_t pos = atomicAdd(reinterpret_cast<unsigned long long*>(&s_pos[k]), 1ull);
+            out[pos] = row;
+        }
+    }
+}
+
+// Next-level histograms from the parents' and the smaller children's: for split i (parent
+// node li[i]), child 2i+sr[i] gets Hs[i] and child 2i+1-sr[i] gets H[li[i]] - Hs[i].
+__global__ __launch_bounds__(256) void hist_sibling_kernel(const float* __restrict__ H,
+                                                           const float* __restrict__ Hs,
+                                                           const int64_t* __restrict__ li,
+                                                           const uint8_t* __restrict__ small_right,
+                                                           int64_t per, int n_split,
+                                                           float* __restrict__ Hn) {
+    const int i = blockIdx.y;
+    if (i >= n_split) return;
+    const float4* hp = reinterpret_cast<const float4*>(H + (size_t)li[i] * per);
+    const float4* hs = reinterpret_cast<const float4*>(Hs + (size_t)i * per);
+    const int sr = small_right[i] ? 1 : 0;
+    float4* dsmall = reinterpret_cast<float4*>(Hn + (size_t)(2 * i + sr) * per);
+    float4* dbig = reinterpret_cast<float4*>(Hn + (size_t)(2 * i + 1 - sr) * per);
+    const int64_t n4 = per / 4;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = hp[e], b = hs[e];
+        dsmall[e] = b;
+        dbig[e] = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+    }
+}
 }  // namespace
 
 // hist [n_seg, d, B, NS] (zeroed by the caller) += statistics of rows[seg[k]..seg[k+1]) for
@@ -575,5 +664,39 @@ HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, 
         default: return (int)hipErrorInvalidValue;
     }
 #undef HM_SF
+    HM_LAUNCH_RET();
+}
+
+// Row partition of a level, pass 1: counts [nkeys][G] (int32, G = grid) of the active rows per
+// small-child key.  Pass 2 (after incl = inclusive cumsum of the flattened counts, int64):
+// rows grouped by key into out[0 .. seg[nkeys]), segment starts seg [nkeys + 1].
+HM_API int hm_partition_count(const int32_t* rows, int64_t m, const int32_t* node_of_row,
+                              const int16_t* lut, int nb, int nlut, int nkeys, int grid,
+                              int32_t* counts, hipStream_t stream) {
+    if (nkeys <= 0 || nkeys > 8192 || grid <= 0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
+                       rows, m, node_of_row, lut, nb, nlut, nkeys, counts);
+    HM_LAUNCH_RET();
+}
+
+HM_API int hm_partition_scatter(const int32_t* rows, int64_t m, const int32_t* node_of_row,
+                                const int16_t* lut, int nb, int nlut, int nkeys, int grid,
+                                const int32_t* counts, const int64_t* incl, int32_t* out,
+                                int64_t* seg, hipStream_t stream) {
+    if (nkeys <= 0 || nkeys > 8192 || grid <= 0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int64_t), stream,
+                       rows, m, node_of_row, lut, nb, nlut, nkeys, counts, incl, out, seg);
+    HM_LAUNCH_RET();
+}
+
+// Hn [2 * n_split, per] from H [L, per], Hs [n_split, per] (per = d * B * NS, a multiple of 4).
+HM_API int hm_hist_sibling(const float* H, const float* Hs, const int64_t* li, const uint8_t* small_right,
+                           int64_t per, int n_split, float* Hn, hipStream_t stream) {
+    if (n_split <= 0) return 0;
+    if (per % 4) return (int)hipErrorInvalidValue;
+    int64_t bx = (per / 4 + 255) / 256;
+    if (bx > 64) bx = 64;
+    hipLaunchKernelGGL(hist_sibling_kernel, dim3((unsigned)bx, (unsigned)n_split), dim3(256), 0, stream,
+                       H, Hs, li, small_right, per, n_split, Hn);
     HM_LAUNCH_RET();
 }

@@ -329,6 +329,25 @@ class HistTreeBuilder:
                 raise RuntimeError("hm_split_find_cpu: invalid arguments")
         return gain, feat, bins, left, tot
 
+    @staticmethod
+    def _partition_gpu(act_rows, node_of_row, nb: int, lut, n_keys: int):
+        """Rows of the small children grouped by child (csrc hm_partition_count / _scatter: a
+        counting sort of the level's keys instead of a full radix sort of every active row)."""
+        dev = act_rows.device
+        m = act_rows.numel()
+        G = int(max(1, min(1024, (m + 4095) // 4096)))
+        counts = torch.empty(n_keys * G, dtype=torch.int32, device=dev)
+        p, st = _native.ptr, _native.stream_of(dev)
+        _native.check(_native.hip().hm_partition_count(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
+                                                       lut.numel(), n_keys, G, p(counts), st), "hm_partition_count")
+        incl = torch.cumsum(counts, 0)                     # int64
+        rows = torch.empty(max(1, m), dtype=torch.int32, device=dev)
+        seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+        _native.check(_native.hip().hm_partition_scatter(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
+                                                         lut.numel(), n_keys, G, p(counts), p(incl), p(rows),
+                                                         p(seg), st), "hm_partition_scatter")
+        return rows, seg
+
     def _hist(self, rows, seg, n_seg, stats, smax):
         """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
         q = self.q
@@ -435,18 +454,26 @@ class HistTreeBuilder:
             small_id = torch.where(small_right, rc[li], lc[li]) - nb           # local child id
             lut = torch.full((2 * n_split,), 32767, dtype=torch.int16, device=dev)
             lut[small_id.long()] = torch.arange(n_split, device=dev, dtype=torch.int16)
-            nr = node_of_row[act_rows.long()] - nb
-            key = torch.where(nr >= 0, lut[nr.clamp_min(0).long()], torch.full_like(nr, 32767, dtype=torch.int16))
-            skey, order = torch.sort(key, stable=True)
-            rows = act_rows[order].contiguous()
-            seg = torch.searchsorted(skey, torch.arange(n_split + 1, device=dev, dtype=torch.int16)).to(torch.int64)
+            if dev.type == "cuda" and n_split <= 8192:
+                rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, n_split)
+            else:
+                nr = node_of_row[act_rows.long()] - nb
+                key = torch.where(nr >= 0, lut[nr.clamp_min(0).long()], torch.full_like(nr, 32767, dtype=torch.int16))
+                skey, order = torch.sort(key, stable=True)
+                rows = act_rows[order].contiguous()
+                seg = torch.searchsorted(skey, torch.arange(n_split + 1, device=dev, dtype=torch.int16)).to(torch.int64)
             Hs = self._hist(rows, seg.contiguous(), n_split, stats, smax)
-            Hp = H[li]
             Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
-            sr = small_right.long()
-            j2 = 2 * torch.arange(n_split, device=dev)
-            Hn[j2 + sr] = Hs
-            Hn[j2 + 1 - sr] = Hp - Hs
+            if dev.type == "cuda":
+                sr8 = small_right.to(torch.uint8)
+                _native.check(_native.hip().hm_hist_sibling(
+                    _native.ptr(H), _native.ptr(Hs), _native.ptr(li), _native.ptr(sr8), C.c_int64(d * B * NS),
+                    n_split, _native.ptr(Hn), _native.stream_of(dev)), "hm_hist_sibling")
+            else:
+                sr = small_right.long()
+                j2 = 2 * torch.arange(n_split, device=dev)
+                Hn[j2 + sr] = Hs
+                Hn[j2 + 1 - sr] = H[li] - Hs
             H = Hn
             base, L = nb, 2 * n_split
             depth += 1
@@ -921,3 +948,7 @@ _native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [_P])
 _native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5)
 _native.register_hip("hm_split_find", [_P] * 10 + [_P])
 _native.register_host("hm_split_find_cpu", [_P] * 10)
+_native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P])
+_native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
+                                              _P, _P, _P])
+_native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])

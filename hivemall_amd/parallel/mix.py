@@ -153,15 +153,16 @@ class OverlappedMixer:
             self.finish()
         if self.snap is None:
             # bf16 replicas are reduced in fp32: an 8-way sum rounded to 8 mantissa bits would
-            # inject noise into every mix (the wire cost is hidden behind compute anyway)
+            # inject noise into every mix (the wire cost is hidden behind compute anyway).  The
+            # snapshot keeps the replica's own dtype (an exact copy), which halves its bytes.
             wide = lambda t: torch.empty(t.shape, dtype=torch.float32 if t.dtype in (
                 torch.bfloat16, torch.float16) else t.dtype, device=t.device)
-            self.snap = [wide(t) for t in tensors]
+            self.snap = [torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in tensors]
             self.buf = [wide(t) for t in tensors]
         self.targets = tensors
         for s, b, t in zip(self.snap, self.buf, tensors):
-            s.copy_(t)
-            b.copy_(t)
+            s.copy_(t)          # one strided read of the replica (e.g. the V half of packed VG)
+            b.copy_(s)
         self.works = []
         for b in self.buf:
             v = b.view(-1)
@@ -179,7 +180,6 @@ class OverlappedMixer:
         self.works = []
         inv = 1.0 / self.m.world
         for t, s, b in zip(self.targets, self.snap, self.buf):
-            if t.dtype in (torch.bfloat16, torch.float16):
-                t.copy_((t.float() + (b * inv - s)).to(t.dtype))
-            else:
-                t.add_(b, alpha=inv).sub_(s)
+            # x <- x + (mean - snapshot): in place, fp32 math, one rounding to t's dtype
+            b.mul_(inv).sub_(s)
+            t.add_(b)

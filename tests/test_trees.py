@@ -326,3 +326,26 @@ def test_split_find_kernel_matches_host(crit, NS, cat):
     torch.testing.assert_close(dev[0].cpu(), host[0], rtol=1e-4, atol=1e-5)
     assert torch.equal(dev[1].cpu(), host[1]) and torch.equal(dev[2].cpu(), host[2])
     torch.testing.assert_close(dev[3].cpu(), host[3], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_partition_kernel_groups_rows_like_sort():
+    """Counting-sort partition of a level == stable key sort, as sets per segment."""
+    from hivemall_amd.models.trees import HistTreeBuilder
+    g = torch.Generator().manual_seed(3)
+    n, nb, n_split = 300000, 15, 40
+    node = torch.randint(nb - 5, nb + 2 * n_split, (n,), generator=g, dtype=torch.int32)
+    act = torch.nonzero(torch.rand(n, generator=g) < 0.7).flatten().to(torch.int32)
+    lut = torch.full((2 * n_split,), 32767, dtype=torch.int16)
+    pick = torch.randperm(2 * n_split, generator=g)[:n_split]
+    lut[pick] = torch.arange(n_split, dtype=torch.int16)
+    rows, seg = HistTreeBuilder._partition_gpu(act.cuda(), node.cuda(), nb, lut.cuda(), n_split)
+    rows, seg = rows.cpu(), seg.cpu()
+    nr = node[act.long()] - nb
+    key = torch.where((nr >= 0) & (nr < 2 * n_split), lut[nr.clamp(0, 2 * n_split - 1).long()],
+                      torch.full_like(nr, 32767, dtype=torch.int16))
+    for k in range(n_split):
+        want = set(act[key == k].tolist())
+        got = rows[seg[k]:seg[k + 1]].tolist()
+        assert len(got) == len(want) and set(got) == want, k
+    assert int(seg[n_split]) == int((key < n_split).sum())
