@@ -37,7 +37,13 @@ HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-march=x86-64-v2", "-Wa
               "-Wno-unused-function"]
 
 HIP_LIB = LIBDIR / "libhm_hip.so"
-HOST_LIB = LIBDIR / "libhm_host.so"
+HOST_LIB = Path(os.environ["HM_HOST_LIB"]) if os.environ.get("HM_HOST_LIB") else LIBDIR / "libhm_host.so"
+# host library built with AddressSanitizer + UBSan (sanitizer runs on host code only; the GPU
+# pool has no GPU ASan / XNACK): build_host_sanitized(), used by tests/test_sanitizers.py
+ASAN_HOST_LIB = ROOT / "build" / "asan" / "libhm_host_asan.so"
+SAN_FLAGS = ["-O1", "-g", "-std=c++17", "-fPIC", "-fopenmp", "-fno-omit-frame-pointer",
+             "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-Wall",
+             "-Wno-unused-function"]
 
 
 def _headers(d: Path):
@@ -63,16 +69,16 @@ def _run(cmd, verbose):
     return r
 
 
-def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs):
-    OBJDIR.mkdir(parents=True, exist_ok=True)
-    LIBDIR.mkdir(parents=True, exist_ok=True)
+def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs, objdir: Path = OBJDIR):
+    objdir.mkdir(parents=True, exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
     hdrs = _headers(CSRC / "kernels")  # shared rule headers are used by host code too
     for s in srcs:
         hdrs.extend(_headers(s.parent))
     objs = []
     todo = []
     for s in srcs:
-        o = OBJDIR / (s.parent.name + "_" + s.name + ".o")
+        o = objdir / (s.parent.name + "_" + s.name + ".o")
         objs.append(o)
         if _stale(o, [s] + hdrs):
             todo.append((s, o))
@@ -91,6 +97,13 @@ def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs):
 def build_host(verbose: bool = False, jobs: int = 8) -> Path:
     srcs = sorted((CSRC / "host").glob("*.cpp"))
     return _build_lib(srcs, CXX, HOST_FLAGS, HOST_LIB, ["-fopenmp"], verbose, jobs)
+
+
+def build_host_sanitized(verbose: bool = False, jobs: int = 8) -> Path:
+    """CPU library with ASan + UBSan (load it with libasan preloaded: tests/test_sanitizers.py)."""
+    srcs = sorted((CSRC / "host").glob("*.cpp"))
+    return _build_lib(srcs, CXX, SAN_FLAGS, ASAN_HOST_LIB, ["-fopenmp", "-fsanitize=address,undefined"],
+                      verbose, jobs, objdir=ROOT / "build" / "asan" / "obj")
 
 
 def build_hip(verbose: bool = False, jobs: int = 8) -> Path:

@@ -255,6 +255,12 @@ def topk_similar(X: torch.Tensor, Y: torch.Tensor | None = None, k: int = 10):
     for every row of X (self-matches excluded when Y is None)."""
     Xn = torch.nn.functional.normalize(X.float(), dim=1)
     Yn = Xn if Y is None else torch.nn.functional.normalize(Y.float(), dim=1)
+    if k <= 64 and Xn.shape[1] <= 256:
+        # fused MFMA similarity + running top-k (ops/topk_mips.py): no N x N matrix in HBM
+        from ..ops.topk_mips import mips_topk
+
+        ix, sc = mips_topk(Xn, Yn, min(k, Yn.shape[0]), exclude_self_offset=0 if Y is None else None)
+        return sc, ix
     dt = torch.bfloat16 if X.is_cuda else torch.float32
     S = (Xn.to(dt) @ Yn.to(dt).T).float()
     if Y is None:

@@ -26,6 +26,7 @@ import pandas as pd
 import torch
 
 from .. import _native
+from ..ops import topk_mips
 from ..registry import udf
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import ConversionState, Learner, log
@@ -196,6 +197,23 @@ class MatrixFactorization(_MFBase):
         self._step(u, i, torch.zeros(u.numel(), device=dev), train=False, pred=out)
         return out.cpu().numpy()
 
+    def recommend_topk(self, users=None, k: int = 10, exclude: tuple | None = None):
+        """Top-k items by mf_predict (mu + b_u + b_i + p_u.q_i) per user, best first:
+        (scores [U,k], items [U,k]).  ``exclude`` = (row positions into ``users``, items).
+        Fused MFMA score + top-k on the GPU (``ops/topk_mips.py``); k <= 64.
+        (Predictions are not clipped to -min/-max here: clipping would only create ties.)"""
+        st = self.state
+        dev = st["P"].device
+        uu = (torch.arange(self.n_users, device=dev) if users is None
+              else torch.as_tensor(users, device=dev).long())
+        ex = None
+        if exclude is not None:
+            ex = topk_mips.exclusion_csr(exclude[0], exclude[1], uu.numel(), device=dev)
+        ix, sc = topk_mips.mips_topk(st["P"][uu][:, : self.k], st["Q"][:, : self.k], k,
+                                     item_bias=st["Bi"], row_bias=st["Bu"][uu] + st["mu"][0],
+                                     exclude=ex)
+        return sc, ix
+
     def model_table(self) -> pd.DataFrame:
         st = self.state
         n = max(self.n_users, self.n_items)
@@ -339,7 +357,20 @@ class BPRMF(_MFBase):
         return (U.to(dt) @ st["Q"].to(dt).T).float() + st["Bi"][None, :]
 
     def recommend_topk(self, users=None, k: int = 10, exclude: tuple | None = None):
-        """Top-k items per user: bf16 GEMM on the matrix cores + topk (seen items masked)."""
+        """Top-k items per user, best first: (scores [U,k], items [U,k]).
+
+        ``exclude`` = (row positions into ``users``, items) pairs to skip (already-seen items).
+        On the GPU this is the fused MFMA score + top-k kernel (``ops/topk_mips.py``): the
+        user x item score matrix is never materialised.  k > 64 falls back to GEMM + topk."""
+        st = self.state
+        U = st["P"] if users is None else st["P"][torch.as_tensor(users, device=st["P"].device).long()]
+        if k <= topk_mips.KMAX:
+            ex = None
+            if exclude is not None:
+                ex = topk_mips.exclusion_csr(exclude[0], exclude[1], U.shape[0], device=U.device)
+            ix, sc = topk_mips.mips_topk(U[:, : self.k], st["Q"][:, : self.k], k,
+                                         item_bias=st["Bi"], exclude=ex)
+            return sc, ix
         S = self.scores(users)
         if exclude is not None:
             eu, ei = exclude

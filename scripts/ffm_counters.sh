@@ -9,4 +9,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_AN
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/ffm_pmc/p$i -o run -- python3 benchmarks/ffm_prof_target.py > gpurun_out/ffm_pmc_p$i.log 2>&1 || { echo "pass $i failed: $?"; tail -5 gpurun_out/ffm_pmc_p$i.log; exit 1; }
 done
-find gpurun_out/ffm_pmc -name "*counter_collection*"
+python scripts/pmc_summary.py gpurun_out/ffm_pmc ffm_packed > gpurun_out/ffm_pmc_summary.json
+cat gpurun_out/ffm_pmc_summary.json
