@@ -375,8 +375,12 @@ int launch(const MipsParams& P, const void* Q, const void* I, const float* bias,
 // top-KTC list in VGPRs (insertion = a compare/select network, no memory, no cross-lane
 // coordination) and its threshold is always exact, so after the first tiles nearly every score
 // fails one compare.  The two half-lists of a query are merged by shuffles at the end.
-// Measured against the LDS-candidate-buffer kernel above on the ML-20M all-users top-10 sweep:
-// that one spends 4+ ms in ballots, appends and compactions.
+// Measured on the ML-20M all-users top-10 sweep (profiles/mips/): 3.7 ms against 5-7 ms for the
+// LDS-candidate-buffer kernel above (ballots, appends, compactions) and 46 ms for GEMM + topk.
+// Counters: ~237K VALU instructions per wave, most of them in insertions (about one network
+// pass per 32-item tile per wave, although typically one or two of the 64 lanes insert);
+// prefetching the next tile's A fragments from LDS changed nothing at k = 10 and cost 55 % at
+// k = 32 (VGPRs).
 template <int KS2, int KTC, bool EXCL>
 __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
     MipsParams P, const bf16x8* __restrict__ Q, const bf16x8* __restrict__ I,
@@ -486,9 +490,16 @@ __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
                 acc[4 * j] += bb.x; acc[4 * j + 1] += bb.y; acc[4 * j + 2] += bb.z; acc[4 * j + 3] += bb.w;
             }
             const int nb = n0 + 4 * h;
+            if (n0 + 32 > n_end) {                       // tail tile only (uniform branch)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (nb + (r & 3) + 8 * (r >> 2) >= n_end) acc[r] = -INFINITY;
+            }
+            // fast path: 16 compares against the exact threshold (their lane masks OR-ed on
+            // the scalar unit); per-register bit masks are built only when something passes
             bool any = false;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) any |= (nb + (r & 3) + 8 * (r >> 2) < n_end) & (acc[r] > thr);
+            for (int r = 0; r < 16; ++r) any |= acc[r] > thr;
             if (!__builtin_amdgcn_ballot_w64(any)) continue;
             // pending candidates of this lane as a bit mask; one insertion site (a copy of the
             // network per register made the compile run for tens of minutes)
@@ -496,7 +507,7 @@ __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = nb + (r & 3) + 8 * (r >> 2);
-                bool c = (n < n_end) & (acc[r] > thr);
+                bool c = acc[r] > thr;
                 if (EXCL) {
                     if (c && P.use_self && n == q + P.self_offset) c = false;
                     if (c && ex_ptr && q < P.M) c = !is_excluded(ex_ptr, ex_idx, q, n);
