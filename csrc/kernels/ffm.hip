@@ -408,8 +408,10 @@ struct SlotIO {
     }
 };
 
+// bf16 K=4 (the bench shape) is register-allocated for 4 waves/SIMD (<= 128 VGPRs); the other
+// shapes keep the compiler's choice.
 template <int KC, bool BF, int NS, bool RELOAD>
-__global__ __launch_bounds__(256) void ffm_packed_kernel(
+__global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_packed_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
@@ -442,7 +444,11 @@ __global__ __launch_bounds__(256) void ffm_packed_kernel(
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
         const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);
 
-        // ---- 2. gather own packed slots: V -> LDS image (+ registers), G -> registers ----
+        // ---- 2. gather own packed slots: V -> LDS image (+ registers), G -> registers; the
+        //         linear weight is fetched alongside, so the forward waits on no further global
+        //         round trip ----
+        float lw = 0.f;
+        if (P.use_linear && tid < F && s_idx[tid] >= 0) lw = w[s_idx[tid]];
         SV ov[NS][KC], og[NS][KC];
         uint32_t slot[NS];
         uint32_t live = 0u;
@@ -487,7 +493,7 @@ __global__ __launch_bounds__(256) void ffm_packed_kernel(
             part += d * s_x[a] * s_x[b];
         }
         part *= scale * scale;
-        if (P.use_linear && tid < F && s_idx[tid] >= 0) part += w[s_idx[tid]] * s_x[tid] * scale;
+        if (P.use_linear && tid < F) part += lw * s_x[tid] * scale;   // lw = 0 for padding
         float p = hm::block_sum(part, s_red);
         if (P.use_bias) p += bias[0];
 
@@ -496,6 +502,8 @@ __global__ __launch_bounds__(256) void ffm_packed_kernel(
 
         // ---- 5. AdaGrad(V) update on the packed slots (Hogwild) ----
         if (P.train) {
+            float lz = 0.f, ln = 0.f;     // FTRL state of the linear term: in flight during the V updates
+            if (P.use_linear && tid < F && s_idx[tid] >= 0) { lz = wz[s_idx[tid]]; ln = wn[s_idx[tid]]; }
             const float ks = kappa * scale * scale;
             const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
 #pragma unroll
@@ -529,7 +537,19 @@ __global__ __launch_bounds__(256) void ffm_packed_kernel(
                 }
                 IO::store(VG, slot[j], own, gg, BF ? hash3(rrow, (uint32_t)(a * F + b), 0x3u) : 0u);
             }
-            linear_updates(P, kappa, scale, s_idx, s_x, w, wz, wn, bias);
+            if (P.use_linear && tid < F) {
+                const int i = s_idx[tid];
+                if (i >= 0) {   // FTRL-proximal on the prefetched (w, z, n)
+                    const float g = kappa * s_x[tid] * scale;
+                    const float n1 = ln + g * g;
+                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                    wz[i] = z1;
+                    wn[i] = n1;
+                    w[i] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                }
+            }
+            if (P.use_bias && tid == 0)
+                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
         }
         __syncthreads();  // LDS reuse by the next row
     }

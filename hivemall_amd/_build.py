@@ -36,7 +36,7 @@ HIP_FLAGS = [
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-march=x86-64-v2", "-Wall",
               "-Wno-unused-function"]
 
-HIP_LIB = LIBDIR / "libhm_hip.so"
+HIP_LIB = Path(os.environ["HM_HIP_LIB"]) if os.environ.get("HM_HIP_LIB") else LIBDIR / "libhm_hip.so"
 HOST_LIB = Path(os.environ["HM_HOST_LIB"]) if os.environ.get("HM_HOST_LIB") else LIBDIR / "libhm_host.so"
 # host library built with AddressSanitizer + UBSan (sanitizer runs on host code only; the GPU
 # pool has no GPU ASan / XNACK): build_host_sanitized(), used by tests/test_sanitizers.py
