@@ -122,6 +122,16 @@ def main(argv=None):
     ms_per_step = 1000.0 * elapsed / max(1, args.steps)
     rows_total = float(B) * world * args.steps
     rows_per_s = rows_total / elapsed
+    if os.environ.get("HM_TRACE"):
+        # host + device timeline of a few extra steps (outside the timed region)
+        from hivemall_amd.prof import host_trace
+
+        with host_trace(os.environ["HM_TRACE"], name="bench_ffm", rank=ctx.rank):
+            for i in range(3):
+                step(args.warmup + args.steps + i)
+            if overlap is not None:
+                overlap.finish()
+            sync()
 
     # ---- quality: final mix, then held-out logloss vs the planted-model floor ----
     if world > 1:

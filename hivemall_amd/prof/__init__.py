@@ -8,6 +8,8 @@
 * :func:`kernel_stats` / :func:`counter_summary` — parse rocprofv3's CSV output into
   per-kernel tables (what ``profiles/`` holds).
 * :class:`MetricsWriter` — per-step JSONL metrics stream (rows/s, loss, bytes mixed, GB/s).
+* :func:`host_trace`    — torch.profiler host + device timeline of a region, exported as a
+  Chrome trace (``HM_TRACE=<dir>`` makes ``bench.py`` write one per rank) plus a per-op table.
 """
 from __future__ import annotations
 
@@ -101,3 +103,44 @@ class MetricsWriter:
         rec.update({k: (float(v) if isinstance(v, torch.Tensor) else v) for k, v in kv.items()})
         with open(self.path, "a") as f:
             f.write(json.dumps(rec) + "\n")
+
+
+class host_trace:
+    """``with host_trace("out_dir", name="ffm"):`` — torch.profiler over CPU + GPU activity of
+    the region; writes ``<out_dir>/<name>.rank<r>.json`` (chrome://tracing / Perfetto) and
+    ``<name>.rank<r>.txt`` (the ``key_averages`` table sorted by device time).  A no-op when
+    ``out_dir`` is empty, so call sites can pass ``os.environ.get("HM_TRACE")``."""
+
+    def __init__(self, out_dir: str | None, name: str = "trace", rank: int = 0, row_limit: int = 30):
+        self.out_dir, self.name, self.rank, self.row_limit = out_dir, name, rank, row_limit
+        self.prof = None
+
+    def __enter__(self):
+        if not self.out_dir:
+            return self
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU]
+        if torch.cuda.is_available():
+            acts.append(ProfilerActivity.CUDA)
+        self.prof = profile(activities=acts, record_shapes=False)
+        self.prof.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.prof is None:
+            return False
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self.prof.__exit__(*exc)
+        os.makedirs(self.out_dir, exist_ok=True)
+        base = os.path.join(self.out_dir, f"{self.name}.rank{self.rank}")
+        self.prof.export_chrome_trace(base + ".json")
+        key = "self_cuda_time_total" if torch.cuda.is_available() else "self_cpu_time_total"
+        try:
+            table = self.prof.key_averages().table(sort_by=key, row_limit=self.row_limit)
+        except Exception:  # pragma: no cover - sort key naming differs across versions
+            table = self.prof.key_averages().table(row_limit=self.row_limit)
+        with open(base + ".txt", "w") as f:
+            f.write(table)
+        return False
