@@ -56,7 +56,9 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0,
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if use_gpu else "gloo")
+    # HM_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on one card
+    # (RCCL refuses two ranks on the same GPU); production runs use RCCL
+    be = backend or os.environ.get("HM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
