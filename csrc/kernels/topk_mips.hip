@@ -375,7 +375,8 @@ int launch(const MipsParams& P, const void* Q, const void* I, const float* bias,
 // top-KTC list in VGPRs (insertion = a compare/select network, no memory, no cross-lane
 // coordination) and its threshold is always exact, so after the first tiles nearly every score
 // fails one compare.  The two half-lists of a query are merged by shuffles at the end.
-// Measured on the ML-20M all-users top-10 sweep (profiles/mips/): 3.7 ms against 5-7 ms for the
+// Measured on the ML-20M all-users top-10 sweep (profiles/mips/): 2.8 ms (3.7 ms before the
+// per-lane candidate queue) against 5-7 ms for the
 // LDS-candidate-buffer kernel above (ballots, appends, compactions) and 46 ms for GEMM + topk.
 // Counters: ~237K VALU instructions per wave, most of them in insertions (about one network
 // pass per 32-item tile per wave, although typically one or two of the 64 lanes insert);
@@ -462,6 +463,18 @@ __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
         return t;
     };
 
+    // per-lane queue of candidates not yet in the sorted list
+    float qs0 = 0.f, qs1 = 0.f, qs2 = 0.f, qs3 = 0.f;
+    int qi0 = 0, qi1 = 0, qi2 = 0, qi3 = 0, qn = 0;
+    auto flush_queue = [&]() {
+        if (qn > 0) insert(qs0, qi0);
+        if (qn > 1) insert(qs1, qi1);
+        if (qn > 2) insert(qs2, qi2);
+        if (qn > 3) insert(qs3, qi3);
+        qn = 0;
+        thr = kth();
+    };
+
     if (n_begin < n_end) MIPS_FETCH(n_begin);
     __syncthreads();
     if (n_begin < n_end) MIPS_COMMIT();
@@ -514,17 +527,29 @@ __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
                 }
                 pend |= (uint32_t)c << r;
             }
+            // append to the lane's 4-entry queue (~30 VALU per lockstep pass); the sorted lists
+            // are updated only when some lane's queue is full — late in the sweep one or two of
+            // the 64 lanes have a candidate per tile, and a full insertion pass per tile for the
+            // whole wave was most of the kernel's VALU work
             while (__builtin_amdgcn_ballot_w64(pend != 0u)) {
-                if (pend) {
+                if (pend && qn < 4) {
                     const int r = __builtin_ctz(pend);
                     pend &= pend - 1u;
                     float sv = acc[0];
 #pragma unroll
                     for (int k = 1; k < 16; ++k) sv = r == k ? acc[k] : sv;
-                    if (sv > thr) {
-                        insert(sv, nb + (r & 3) + 8 * (r >> 2));
-                        thr = kth();
-                    }
+                    const int nv = nb + (r & 3) + 8 * (r >> 2);
+                    qs0 = qn == 0 ? sv : qs0; qi0 = qn == 0 ? nv : qi0;
+                    qs1 = qn == 1 ? sv : qs1; qi1 = qn == 1 ? nv : qi1;
+                    qs2 = qn == 2 ? sv : qs2; qi2 = qn == 2 ? nv : qi2;
+                    qs3 = qn == 3 ? sv : qs3; qi3 = qn == 3 ? nv : qi3;
+                    ++qn;
+                }
+                if (__builtin_amdgcn_ballot_w64(qn == 4 && pend != 0u)) {
+                    flush_queue();
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (!(acc[r] > thr)) pend &= ~(1u << r);
                 }
             }
         }
@@ -533,6 +558,7 @@ __global__ __launch_bounds__(NT) void mips_topk_reg_kernel(
         __syncthreads();
     }
 
+    flush_queue();
     // merge the two half-lists of each query: lanes l + 32 publish theirs through LDS (the
     // stage buffer is free now), lanes l insert them
     float2* s_half = reinterpret_cast<float2*>(s_tile) + (size_t)w * 32 * KTC;
