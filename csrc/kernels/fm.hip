@@ -24,6 +24,9 @@
 
 namespace {
 
+// w0 shard i lives at w0[i * W0_STRIDE] (its own 128-B line: atomics to one line serialise)
+constexpr int W0_STRIDE = 32;
+
 struct FMParams {
     int dims, k;              // k = real factor count (<= KP)
     int classification, train;
@@ -32,6 +35,7 @@ struct FMParams {
     float lambda0, lambda_w, lambda_v;
     float min_target, max_target;
     int use_w0;
+    int w0_shards;            // w0 = sum of w0[0..w0_shards) (<= 64)
     uint32_t seed;
 };
 
@@ -128,6 +132,9 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
     for (int64_t row = gw; row < n_rows; row += nw) {
         const int64_t s = indptr[row], e = indptr[row + 1];
         const int nnz = (int)(e - s);
+        // global-bias shards (one 128-B line each) are read at the top of the row, in flight
+        // with the feature gathers instead of after the reductions
+        const float w0part = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
         // ---- forward: lanes over non-zeros (chunks of 64) ----
         float S[KP];
 #pragma unroll
@@ -173,7 +180,8 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             pair += S[f] * S[f];
         }
         float p = lin + 0.5f * (pair - sq);
-        if (P.use_w0) p += *w0;
+        const float w0v = P.use_w0 ? hm::wave_sum(w0part) : 0.f;
+        p += w0v;
         const float yy = y ? y[row] : 0.f;
         float d;
         if (P.classification) {
@@ -214,9 +222,13 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             t.load(V, i);
             upd(t, i, x, w[i]);
         }
-        // per-row atomic: batching w0 deltas per wave was measured to diverge (every wave's
-        // locally-converged delta is summed -> ~#waves x overshoot on the hottest parameter)
-        if (P.use_w0 && lane == 0) atomicAdd(w0, -eta * (d + 2.f * P.lambda0 * *w0));
+        // per-row atomic (batching w0 deltas per wave was measured to diverge: every wave's
+        // locally-converged delta is summed -> ~#waves x overshoot on the hottest parameter),
+        // into one of w0_shards addresses: a single address serialised every row of the chip
+        // (~40 M rows/s at any grid, profiles/fm_grid_probe_r1.log); the sum of the shards
+        // receives exactly the same per-row deltas
+        if (P.use_w0 && lane == 0)
+            atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, -eta * (d + 2.f * P.lambda0 * w0v));
     }
 }
 
@@ -224,10 +236,15 @@ template <int KP, bool BF16>
 int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const float* val,
            const float* y, int64_t n, int64_t t0, float* w, void* V, float* w0, float* pred,
            float* loss, int grid, hipStream_t st) {
-    // Default: 64 blocks x 4 waves.  Measured on MI355X (profiles/fm_sweep_r1.log): more
-    // concurrent rows only add Hogwild contention on the hot Criteo features (slower AND a
-    // worse logloss); 256 waves already saturate the memory pipes for FM-sized rows.
-    int64_t blocks = grid > 0 ? grid : 64;
+    // Default: 256 blocks x 4 waves.  With the global bias behind ONE atomic address every
+    // grid topped out near 40 M rows/s (64 blocks was best; profiles/fm_sweep_r1.log); with 64
+    // line-padded shards (profiles/fm_grid_probe_r1.log, 2M rows, 2^24 features, k=8 bf16):
+    //   blocks  64: 58.7 M rows/s, held-out logloss 0.4749   128: 95.6 M, 0.4742
+    //          256: 117.0 M, 0.4759                          512: 122.9 M, 0.4787
+    // (single address, 64 blocks: 38.7 M, 0.4730).  256 keeps the logloss within 0.003 of the
+    // single-address run at 3x the rows/s; more Hogwild concurrency costs more logloss than it
+    // buys.
+    int64_t blocks = grid > 0 ? grid : 256;
     if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;
@@ -238,7 +255,7 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 
 }  // namespace
 
-// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed
+// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards
 // hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
                       const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
@@ -249,6 +266,8 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     P.classification = ip[3]; P.train = ip[4]; P.eta_kind = ip[5]; P.use_w0 = ip[6];
     const int bf16 = ip[7], grid = ip[8];
     P.seed = (uint32_t)ip[9];
+    P.w0_shards = ip[10];
+    if (P.w0_shards < 1 || P.w0_shards > 64) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
     if (n_rows <= 0) return 0;

@@ -21,6 +21,11 @@ import pandas as pd
 import torch
 
 from ..ops.fm import FMHyper, fm_step
+
+# global-bias shards on the GPU (see ops/fm.py): one same-address atomic per row capped train_fm
+# at ~40 M rows/s on MI355X whatever the grid (profiles/fm_grid_probe_r1.log)
+W0_SHARDS = 64
+W0_STRIDE = 32      # floats between shards: one 128-B line each
 from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import ConversionState, Learner, log, parse_labels_binary
@@ -102,7 +107,8 @@ class FMTrainer(Learner):
             V[:, : self.k] = torch.randn(self.dims, self.k, generator=g) * self.cl["sigma"]
         self.state = dict(w=torch.zeros(self.dims, dtype=torch.float32, device=dev),
                           V=V.to(dev, torch.bfloat16 if bf16 else torch.float32).contiguous(),
-                          w0=torch.zeros(1, dtype=torch.float32, device=dev))
+                          w0=torch.zeros(W0_SHARDS * W0_STRIDE if dev.type == "cuda" else 1,
+                                         dtype=torch.float32, device=dev))
         self.touched = torch.zeros(self.dims, dtype=torch.bool, device=dev)
         return self.state
 
@@ -212,7 +218,7 @@ class FMTrainer(Learner):
         bias_name = "0" if names and isinstance(names[0], str) else 0
         return pd.DataFrame({
             "feature": [bias_name] + names,
-            "W_i": np.concatenate([[float(self.state["w0"][0].item())], W]).astype(np.float32),
+            "W_i": np.concatenate([[float(self.state["w0"].double().sum().item())], W]).astype(np.float32),
             "V_if": [None] + [v for v in V]})
 
 

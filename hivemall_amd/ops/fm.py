@@ -30,7 +30,10 @@ class FMHyper:
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
             y: torch.Tensor | None, h: FMHyper, k: int, train: bool = True, t0: int = 0,
             pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0) -> None:
-    """One fused pass over CSR rows.  state: w f32 [dims], V bf16|f32 [dims, KP], w0 f32 [1]."""
+    """One fused pass over CSR rows.  state: w f32 [dims], V bf16|f32 [dims, KP], w0 f32:
+    on the GPU the global bias is the SUM of S = numel/32 shards at stride 32 floats (every
+    row's update is an atomic add into shard (wave % S) instead of one contended address);
+    the CPU engine keeps a single w0 (numel 1)."""
     w, V, w0 = state["w"], state["V"], state["w0"]
     dims, KP = V.shape
     n = indptr.numel() - 1
@@ -46,7 +49,8 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
             assert t.numel() >= n
     bf16 = V.dtype == torch.bfloat16
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
-                   int(bf16), grid, h.seed & 0x7FFFFFFF], dtype=np.int32)
+                   int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32)], dtype=np.int32)
+    assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,
                    h.min_target, h.max_target], dtype=np.float32)
     p = _native.ptr
