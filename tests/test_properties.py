@@ -118,3 +118,32 @@ def test_mhash_kernel_bit_exact(ws, nf):
     got = mhash_device(ws, num_features=nf, device="cuda").cpu().tolist()
     want = mhash_batch(ws, num_features=nf).tolist() if nf > 0 else murmur3_batch(ws).tolist()
     assert got == want
+
+
+@SETTINGS
+@given(st.lists(st.integers(-(2**63), 2**63 - 1), max_size=200))
+def test_zigzag_leb128_roundtrip(vals):
+    from hivemall_amd.utils.codec import zigzag_leb128_decode, zigzag_leb128_encode
+
+    enc = zigzag_leb128_encode(vals)
+    assert zigzag_leb128_decode(enc).tolist() == vals
+    # small magnitudes of either sign take one byte
+    if vals and all(-64 <= v < 64 for v in vals):
+        assert len(enc) == len(vals)
+
+
+@SETTINGS
+@given(st.lists(st.integers(0, 2**64 - 1), max_size=200))
+def test_vbyte_roundtrip_and_layout(vals):
+    from hivemall_amd.utils.codec import vbyte_decode, vbyte_encode
+
+    enc = vbyte_encode(vals)
+    assert vbyte_decode(enc).tolist() == vals
+    assert len(enc) == sum(max(1, (v.bit_length() + 6) // 7) for v in vals)
+
+
+def test_vbyte_known_bytes():
+    from hivemall_amd.utils.codec import vbyte_encode, zigzag_encode
+
+    assert vbyte_encode([0, 1, 127, 128, 300]) == bytes([0, 1, 0x7F, 0x80, 0x01, 0xAC, 0x02])
+    assert [zigzag_encode(v) for v in (0, -1, 1, -2, 2)] == [0, 1, 2, 3, 4]
