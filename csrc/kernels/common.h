@@ -67,6 +67,21 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     return (uint16_t)(u >> 16);
 }
 
+// Two floats -> packed bf16x2 with stochastic rounding on gfx950's v_cvt_sr_bf16_f32.
+// Bit-identical to the software rule (bits + (r & 0xFFFF)) >> 16 per value: the instruction
+// adds the HIGH 16 bits of its random operand (benchmarks/probes/sr_probe.hip: 0 mismatches in
+// 2^20 random inputs against that rule), hence the << 16.  One instruction per value instead of
+// the and/add/shift/pack sequence (and no Inf/NaN special case to carry by hand).
+__device__ __forceinline__ uint32_t pack_bf16x2_sr(float lo, uint32_t r_lo, float hi, uint32_t r_hi) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+    bf16x2_t v = {};
+    v = __builtin_amdgcn_cvt_sr_bf16_f32(v, lo, r_lo << 16, false);
+    v = __builtin_amdgcn_cvt_sr_bf16_f32(v, hi, r_hi << 16, true);
+    uint32_t u;
+    __builtin_memcpy(&u, &v, 4);
+    return u;
+}
+
 // XCD-aware bijective remap of a flat block id (cdna_hip_programming.md §5, "XCD swizzle
 // must be bijective"): consecutive logical tiles land on the same XCD / L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

@@ -80,12 +80,6 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     return h;
 }
 
-__device__ __forceinline__ uint32_t bf16_sr(float f, uint32_t rnd) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7F800000u) == 0x7F800000u) return u >> 16;
-    return (u + (rnd & 0xFFFFu)) >> 16;
-}
-
 // 4-element chunk of a slot vector, at element offset `off` (a multiple of 4).
 template <bool BF>
 __device__ __forceinline__ float4 ld_chunk(const void* base, size_t off) {
@@ -119,8 +113,8 @@ template <bool BF>
 __device__ __forceinline__ void st_chunk(void* base, size_t off, float4 v, uint32_t rnd) {
     if constexpr (BF) {
         const uint32_t r2 = rnd * 0x9E3779B1u + 0x632BE5ABu;
-        const uint32_t lo = bf16_sr(v.x, rnd) | (bf16_sr(v.y, rnd >> 16) << 16);
-        const uint32_t hi = bf16_sr(v.z, r2) | (bf16_sr(v.w, r2 >> 16) << 16);
+        const uint32_t lo = hm::pack_bf16x2_sr(v.x, rnd, v.y, rnd >> 16);
+        const uint32_t hi = hm::pack_bf16x2_sr(v.z, r2, v.w, r2 >> 16);
         *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + off) = make_uint2(lo, hi);
     } else {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + off) = v;
@@ -391,10 +385,10 @@ struct SlotIO {
                 const uint32_t r2 = r1 * 0x9E3779B1u + 0x632BE5ABu;
                 const uint32_t r3 = r2 * 0x85EBCA77u + 0x27D4EB2Fu;
                 const uint32_t r4 = r3 * 0xC2B2AE3Du + 0x165667B1u;
-                u[c] = make_uint2(bf16_sr(v[c].x, r1) | (bf16_sr(v[c].y, r1 >> 16) << 16),
-                                  bf16_sr(v[c].z, r2) | (bf16_sr(v[c].w, r2 >> 16) << 16));
-                u[KC + c] = make_uint2(bf16_sr(g[c].x, r3) | (bf16_sr(g[c].y, r3 >> 16) << 16),
-                                       bf16_sr(g[c].z, r4) | (bf16_sr(g[c].w, r4 >> 16) << 16));
+                u[c] = make_uint2(hm::pack_bf16x2_sr(v[c].x, r1, v[c].y, r1 >> 16),
+                                  hm::pack_bf16x2_sr(v[c].z, r2, v[c].w, r2 >> 16));
+                u[KC + c] = make_uint2(hm::pack_bf16x2_sr(g[c].x, r3, g[c].y, r3 >> 16),
+                                       hm::pack_bf16x2_sr(g[c].z, r4, g[c].w, r4 >> 16));
             }
             uint4* p = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(VG) + (size_t)slot * (8 * KC));
 #pragma unroll

@@ -51,14 +51,6 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     return h;
 }
 
-// Stochastic round f32 -> bf16 using 16 random bits.
-__device__ __forceinline__ uint16_t f32_to_bf16_sr(float f, uint32_t rnd) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16);
-    u += (rnd & 0xFFFFu);
-    return (uint16_t)(u >> 16);
-}
-
 template <int KP, bool BF16>
 struct VRow {
     float v[KP];
@@ -99,9 +91,7 @@ struct VRow {
 #pragma unroll
             for (int j = 0; j < KP / 2; ++j) {
                 const uint32_t r = hash3(rbase, (uint32_t)i, (uint32_t)j);
-                const uint32_t lo = f32_to_bf16_sr(v[2 * j], r);
-                const uint32_t hi = f32_to_bf16_sr(v[2 * j + 1], r >> 16 | r << 16);
-                wds[j] = lo | (hi << 16);
+                wds[j] = hm::pack_bf16x2_sr(v[2 * j], r, v[2 * j + 1], r >> 16 | r << 16);
             }
             if constexpr (KP % 8 == 0) {
 #pragma unroll
