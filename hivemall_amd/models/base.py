@@ -71,6 +71,8 @@ COMMON_ITER_OPTS = [
     opt("seed", None, -1, int, "Seed value for random number generator"),
     opt("batch_size", None, 65536, int, "[engine] rows per device kernel launch"),
     opt("mix_interval", None, 0, int, "[engine] RCCL model-mix every N batches (0 = at end only)"),
+    flag("mix_sparse", None, "[engine] mix only the rows touched since the last mix: all-gather "
+         "of (index, delta) instead of a dense all-reduce (parallel.mix.SparseDeltaMixer)"),
 ]
 
 

@@ -153,6 +153,34 @@ def test_ffm_data_parallel_replicas_identical():
     assert out[0] == pytest.approx(out[1], rel=1e-6)
 
 
+def _ffm_dp_sparse(ctx):
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.models.ffm import FFMBatch, FFMTrainer
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    res = []
+    for extra in ("", " -mix_sparse"):
+        idx, y = criteo_like(1200, hash_bits=16, seed=100 + ctx.rank)
+        t = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 16 -mix_interval 1 "
+                       "-batch_size 200 -seed 7" + extra,
+                       device="cpu", mixer=ModelMixer(ctx), rank=ctx.rank)
+        t.fit(batch=FFMBatch(idx, None, None, y))
+        res.append([float(t.state["V"].double().sum()), float(t.state["w"].double().sum())])
+    sm = t._sparse_mixer
+    res.append([sm.sparse_rows, sm.dense_mixes])
+    return res
+
+
+def test_ffm_sparse_mixing_matches_dense_mixing():
+    """-mix_sparse (touched-row all-gather) trains the same replicas as the dense all-reduce."""
+    out = run_world("_ffm_dp_sparse")
+    for r in (0, 1):
+        dense, sparse, (rows, dense_mixes) = out[r]
+        assert sparse == pytest.approx(dense, rel=1e-4, abs=1e-3)
+        assert rows > 0 and dense_mixes >= 1
+    assert out[0][1] == pytest.approx(out[1][1], rel=1e-6)
+
+
 def test_bench_torchrun_cpu_world2():
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
