@@ -75,6 +75,9 @@ COMMON_ITER_OPTS = [
          "of (index, delta) instead of a dense all-reduce (parallel.mix.SparseDeltaMixer)"),
 ]
 
+# data-parallel mixing options of the learners that do not take COMMON_ITER_OPTS
+MIX_OPTS = [COMMON_ITER_OPTS[-2], COMMON_ITER_OPTS[-1]]
+
 
 def parse_labels_binary(y) -> np.ndarray:
     """0/1 or -1/+1 labels -> float32 {-1,+1} (BinaryOnlineClassifierUDTF label handling)."""
@@ -109,3 +112,27 @@ class Learner:
 
     def opt(self, name: str, default=None):
         return self.cl.get(name, default)
+
+    # ------------------------------------------------------------------ data parallel
+    def _dp(self) -> bool:
+        return self.mixer is not None and self.mixer.world > 1
+
+    def mix_tensors(self, tensors: list, flags: list = ()) -> None:
+        """Average this rank's replica with the other ranks' (the ``GROUP BY feature
+        avg(weight)`` / MixServer step): a dense bucketed all-reduce, or the
+        touched-row all-gather with ``-mix_sparse``.  ``flags`` (bool "seen" masks) are OR-ed
+        over ranks so every rank emits the same model table."""
+        if not self._dp():
+            return
+        if self.cl.get("mix_sparse", False):
+            if getattr(self, "_sparse_mixer", None) is None:
+                from ..parallel.mix import SparseDeltaMixer
+                self._sparse_mixer = SparseDeltaMixer(self.mixer)
+            self._sparse_mixer.mix(list(tensors))
+        else:
+            self.mixer.average(list(tensors))
+        if flags:
+            f = [m.to(torch.float32) for m in flags]
+            self.mixer.all_reduce_sum(f)
+            for m, v in zip(flags, f):
+                m.copy_(v > 0)

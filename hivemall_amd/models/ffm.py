@@ -191,16 +191,8 @@ class FFMTrainer(Learner):
         self.touched[i] = True
 
     def mix(self) -> None:
-        if self.mixer is not None:
-            ts = [self.state["V"], self.state["wz"], self.state["wn"], self.state["w"],
-                  self.state["bias"]]
-            if self.cl.get("mix_sparse"):
-                if getattr(self, "_sparse_mixer", None) is None:
-                    from ..parallel.mix import SparseDeltaMixer
-                    self._sparse_mixer = SparseDeltaMixer(self.mixer)
-                self._sparse_mixer.mix(ts)
-            else:
-                self.mixer.average(ts)
+        self.mix_tensors([self.state["V"], self.state["wz"], self.state["wn"], self.state["w"],
+                          self.state["bias"]], [self.touched])
 
     def fit(self, features=None, labels=None, batch: FFMBatch | None = None) -> "FFMTrainer":
         b = batch if batch is not None else self.prepare(features, labels)

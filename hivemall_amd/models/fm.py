@@ -28,7 +28,7 @@ W0_SHARDS = 64
 W0_STRIDE = 32      # floats between shards: one 128-B line each
 from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
-from .base import ConversionState, Learner, log, parse_labels_binary
+from .base import MIX_OPTS, ConversionState, Learner, log, parse_labels_binary
 from .linear import SparseRows, encode_rows
 
 FM_OPTS = [
@@ -58,7 +58,7 @@ FM_OPTS = [
     flag("disable_cv", "disable_cvtest", "Disable convergence check"),
     flag("fp32", None, "[engine] keep V in fp32 on the GPU (default bf16)"),
     opt("batch_size", None, 1 << 20, int, "[engine] rows per kernel launch"),
-]
+] + MIX_OPTS
 _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
 
 
@@ -145,8 +145,17 @@ class FMTrainer(Learner):
             fm_step(self.state, ip, rows.idx, rows.val, rows.y[s:e], self.h, self.k, train=True,
                     t0=self.t, loss=lb, grid=self.grid)
             self.t += e - s
+            mi = int(self.cl["mix_interval"])
+            if mi > 0 and self._dp():
+                self._nbatches = getattr(self, "_nbatches", 0) + 1
+                if self._nbatches % mi == 0:
+                    self.mix()
         i = rows.idx.long()
         self.touched[i[(i >= 0) & (i < self.dims)]] = True
+
+    def mix(self) -> None:
+        """Replica averaging over the ranks (w, V, w0; the SGD state has no optimizer slots)."""
+        self.mix_tensors([self.state["w"], self.state["V"], self.state["w0"]], [self.touched])
 
     def fit(self, features=None, labels=None, rows: SparseRows | None = None) -> "FMTrainer":
         rows = rows if rows is not None else self.prepare(features, labels)
@@ -168,6 +177,7 @@ class FMTrainer(Learner):
             if self.cv.is_converged():
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
+        self.mix()
         return self
 
     def _adapt_lambda(self, va: SparseRows) -> None:

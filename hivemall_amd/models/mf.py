@@ -29,7 +29,7 @@ from .. import _native
 from ..ops import topk_mips
 from ..registry import udf
 from ..utils.options import UDFArgumentException, flag, opt
-from .base import ConversionState, Learner, log
+from .base import MIX_OPTS, ConversionState, Learner, log
 
 _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2, "bolddriver": 0, "bold_driver": 0}
 
@@ -53,7 +53,7 @@ MF_OPTS = [
     flag("disable_cv", "disable_cvtest", "Disable convergence check"),
     opt("seed", None, -1, int, "Seed"),
     opt("grid", None, 0, int, "[engine] kernel grid override"),
-]
+] + MIX_OPTS
 
 BPR_OPTS = [
     opt("factors", "factor", 10, int, "Number of latent factors", aliases=("k",)),
@@ -77,7 +77,7 @@ BPR_OPTS = [
     opt("seed", None, -1, int, "Seed"),
     opt("samples_per_epoch", None, 0, int, "[engine] device-sampled triples per epoch (0 = #positives)"),
     opt("grid", None, 0, int, "[engine] kernel grid override"),
-]
+] + MIX_OPTS
 _BPR_LOSS = {"lnlogistic": 0, "logistic": 1, "sigmoid": 2}
 
 
@@ -91,6 +91,19 @@ def _init_factors(n, k, kp, scheme, maxval, stddev, gen) -> torch.Tensor:
 
 
 class _MFBase(Learner):
+    def mix(self) -> None:
+        """Replica averaging of the factor tables over the ranks (SURVEY.md §2.6 BPR/MF row);
+        AdaGrad accumulators stay local, as each upstream mapper keeps its own."""
+        if self.state is None:
+            return
+        ts = [self.state[k] for k in ("P", "Q", "Bu", "Bi", "mu") if k in self.state]
+        self.mix_tensors(ts, [self.seen_u, self.seen_i])
+
+    def _epoch_mix(self, ep: int) -> None:
+        mi = int(self.cl["mix_interval"])
+        if mi > 0 and (ep + 1) % mi == 0:
+            self.mix()
+
     def _factors(self):
         k = int(self.cl["factors"])
         if not 0 < k <= 64:
@@ -183,10 +196,12 @@ class MatrixFactorization(_MFBase):
         loss = torch.empty(u.numel(), device=dev)
         for ep in range(int(self.cl["iters"])):
             self._step(u, i, r, loss=loss)
+            self._epoch_mix(ep)
             self.cv.incr_loss(float(loss.double().sum().item()))
             if self.cv.is_converged():
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
+        self.mix()
         return self
 
     def predict(self, users, items) -> np.ndarray:
@@ -317,8 +332,10 @@ class BPRMF(_MFBase):
         self.seen_i[tj.long()] = True
         for ep in range(int(self.cl["iters"])):
             self.cv.incr_loss(self.step(tu, ti, tj))
+            self._epoch_mix(ep)
             if self.cv.is_converged():
                 break
+        self.mix()
         return self
 
     @staticmethod
@@ -346,8 +363,10 @@ class BPRMF(_MFBase):
         per = int(self.cl["samples_per_epoch"]) or csr[1].numel()
         for ep in range(int(epochs or self.cl["iters"])):
             self.cv.incr_loss(self.step(n=per, csr=csr))
+            self._epoch_mix(ep)
             if self.cv.is_converged():
                 break
+        self.mix()
         return self
 
     def scores(self, users=None) -> torch.Tensor:

@@ -193,3 +193,39 @@ def test_bench_torchrun_cpu_world2():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+
+
+def _fm_mf_bpr_dp(ctx):
+    import numpy as np
+
+    from hivemall_amd.models.fm import FMTrainer
+    from hivemall_amd.models.mf import BPRMF, MatrixFactorization
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    rng = np.random.default_rng(50 + ctx.rank)
+    out = {}
+    for extra in ("", " -mix_sparse"):
+        feats = [[f"{j}:1.0" for j in rng.choice(3000, 8, replace=False)] for _ in range(300)]
+        y = rng.integers(0, 2, 300)
+        fm = FMTrainer("-c -factors 4 -iters 2 -num_features 3001 -seed 3 -mix_interval 1"
+                       " -batch_size 100" + extra, device="cpu", mixer=ModelMixer(ctx),
+                       rank=ctx.rank).fit(feats, y)
+        u, i = rng.integers(0, 50, 400), rng.integers(0, 80, 400)
+        mf = MatrixFactorization("-factors 4 -iters 3 -seed 3 -mix_interval 1" + extra,
+                                 device="cpu", mixer=ModelMixer(ctx), rank=ctx.rank)
+        mf.fit(u, i, rng.random(400) * 5)
+        bp = BPRMF("-factors 4 -iters 3 -seed 3" + extra, device="cpu", mixer=ModelMixer(ctx),
+                   rank=ctx.rank).fit(u, i, rng.integers(0, 80, 400))
+        out[extra or "dense"] = [float(fm.state["V"].double().sum()), float(fm.state["w"].sum()),
+                                 int(fm.touched.sum()), float(mf.state["P"].double().sum()),
+                                 float(mf.state["Q"].double().sum()),
+                                 float(bp.state["Q"].double().sum()), int(mf.seen_u.sum())]
+    return out
+
+
+def test_fm_mf_bpr_data_parallel_replicas_identical():
+    """FM / MF / BPR replicas agree after mixing (dense and touched-row modes), and the "seen"
+    masks are the union over ranks (one model table per job)."""
+    out = run_world("_fm_mf_bpr_dp")
+    for mode in ("dense", " -mix_sparse"):
+        assert out[0][mode] == pytest.approx(out[1][mode], rel=1e-5, abs=1e-5)
