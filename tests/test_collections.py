@@ -105,3 +105,15 @@ def test_vectors():
     assert list(a.each()) == [(0, 1.0), (2, 2.0)]
     s.set(2, 0.0)
     assert s.size() == 1
+
+
+def test_function_catalogue_covers_registry():
+    """docs/funcs.md analogue (upstream hivemall-docs): every registered name is described."""
+    from hivemall_amd import registry
+    from hivemall_amd.ddl import function_catalogue
+
+    text = function_catalogue()
+    registry.load_all()
+    for name in registry.names():
+        assert f"| `{name}`" in text
+    assert "(see hivemall" not in text
