@@ -129,13 +129,13 @@ def bench_rf(dev="cuda", n=11_000_000, trees=50):
             "row_trees_per_s": round(n * trees / dt), "test_auc": round(float(auc), 4)}
 
 
-def bench_bprmf(dev="cuda", k=64, epochs=3):
+def bench_bprmf(dev="cuda", k=64, epochs=3, opts=""):
     from hivemall_amd.io.synthetic import movielens_like
     from hivemall_amd.models.mf import BPRMF, auc_implicit
     us, its = movielens_like(device=dev, k=16)
     n = us.numel()
     ntest = 200000
-    m = BPRMF(f"-factors {k} -iters 1 -eta0 0.05", device=dev)
+    m = BPRMF(f"-factors {k} -iters 1 -eta0 0.05 {opts}", device=dev)
     m.fit_implicit(us[:-ntest], its[:-ntest], 138493, 27278, epochs=1)
     _sync(dev)
     t0 = time.perf_counter()
@@ -145,7 +145,8 @@ def bench_bprmf(dev="cuda", k=64, epochs=3):
     auc = auc_implicit(m, us[-ntest:].cpu().numpy(), its[-ntest:].cpu().numpy())
     return {"config": f"BPR-MF k={k}, MovieLens-20M-shaped ({n} interactions, 138493 users, 27278 items), "
                       f"device negative sampling", "device": dev,
-            "triples_per_s": round((n - ntest) * epochs / dt), "sampled_auc": round(auc, 4)}
+            "triples_per_s": round((n - ntest) * epochs / dt), "sampled_auc": round(auc, 4),
+            "opts": opts, "grid": m._grid()}
 
 
 ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "fm": bench_fm,

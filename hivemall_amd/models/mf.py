@@ -90,6 +90,13 @@ def _init_factors(n, k, kp, scheme, maxval, stddev, gen) -> torch.Tensor:
     return T
 
 
+def _dev(x, dtype, dev) -> torch.Tensor:
+    """Host arrays or (device) tensors -> contiguous ``dtype`` tensor on ``dev``."""
+    if torch.is_tensor(x):
+        return x.to(dev, dtype).contiguous()
+    return torch.as_tensor(np.asarray(x, dtype=torch.empty(0, dtype=dtype).numpy().dtype)).to(dev)
+
+
 class _MFBase(Learner):
     def mix(self) -> None:
         """Replica averaging of the factor tables over the ranks (SURVEY.md §2.6 BPR/MF row);
@@ -119,14 +126,22 @@ class _MFBase(Learner):
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
                          self._grid()], dtype=np.int32)
 
+    # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Squared-loss
+    # SGD has unbounded per-rating steps: 32 rows/block diverged on a small dense catalogue
+    # (300 items, tests/test_mf.py::test_mf_gpu_quality, RMSE 2.24 vs 0.14) although the
+    # ML-20M-shaped sweep (profiles/mf_grid_r1.log) showed no loss up to grid 1696, so explicit
+    # MF keeps 256 (pass -grid to raise it on large catalogues).
+    ROWS_PER_BLOCK = 256
+
     def _grid(self) -> int:
         """Hogwild concurrency cap: keep the number of ratings in flight well below the number
         of distinct rows they update (plain SGD diverges when many stale gradients of one
-        popular item are summed).  ~1 block (4 waves) per 256 items/users, >= 1."""
+        popular item are summed).  ~1 block (4 waves) per ``ROWS_PER_BLOCK`` items/users,
+        >= 1."""
         g = int(self.cl["grid"])
         if g > 0:
             return g
-        return int(max(1, min(4096, min(self.n_users, self.n_items) // 256)))
+        return int(max(1, min(4096, min(self.n_users, self.n_items) // self.ROWS_PER_BLOCK)))
 
 
 class MatrixFactorization(_MFBase):
@@ -184,9 +199,8 @@ class MatrixFactorization(_MFBase):
 
     def fit(self, users, items, ratings) -> "MatrixFactorization":
         dev = self.device
-        u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev)
-        i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev)
-        r = torch.as_tensor(np.asarray(ratings, dtype=np.float32)).to(dev)
+        u, i, r = _dev(users, torch.int32, dev), _dev(items, torch.int32, dev), \
+            _dev(ratings, torch.float32, dev)
         if self.state is None:
             self.init_state(int(u.max().item()) + 1, int(i.max().item()) + 1)
             if self.cl["update_mean"]:
@@ -258,6 +272,10 @@ class MatrixFactorizationAdaGrad(MatrixFactorization):
 class BPRMF(_MFBase):
     """BPR-MF.  Input triples (user, pos_item, neg_item) as produced by ``bpr_sampling``, or
     (``fit_implicit``) the positive pairs only, with negatives sampled on the device."""
+    # BPR's sigmoid-bounded pairwise steps tolerate 8x the concurrency: ML-20M-shaped k=64
+    # sweep on MI355X (profiles/bpr_grid_r1.log): grid 106 -> 852 blocks = 170M -> 966M
+    # triples/s at sampled AUC 0.7103 -> 0.7101 (sequential CPU engine 0.7105).
+    ROWS_PER_BLOCK = 32
     NAME = "train_bprmf"
     OPTIONS = BPR_OPTS
 
