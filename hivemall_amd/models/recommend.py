@@ -26,6 +26,50 @@ SLIM_OPTS = [
 ]
 
 
+def slim_cd_batched(Gs, bs, l1: float, l2: float, iters: int, eps: float, device=None):
+    """Non-negative elastic-net coordinate descent for every item at once, in Gram form.
+
+    Per item the problem is min_w ½||y − Xw||² + ½λ2||w||² + λ1||w||₁, w ≥ 0 with
+    G = XᵀX, b = Xᵀy.  A coordinate step is ρ_k = b_k − Σ_{m≠k} G_km w_m,
+    w_k = max(0, ρ_k − λ1) / (G_kk + λ2) — the same update and coordinate order as the
+    per-item residual loop of upstream SlimUDTF, so the result matches it to rounding.  All
+    items (padded to the largest neighbourhood K) advance together: one [items, K] mat-vec
+    row per coordinate, on the learner's device; an item stops when its largest change in a
+    sweep falls below ``eps`` (the per-item convergence test).  Returns an [items, K] numpy
+    array (padding columns are zero).
+    """
+    import torch
+
+    dev = device if device is not None else torch.device("cpu")
+    n = len(Gs)
+    K = max(g.shape[0] for g in Gs)
+    G = torch.zeros((n, K, K), dtype=torch.float64)
+    b = torch.zeros((n, K), dtype=torch.float64)
+    for t, (g, v) in enumerate(zip(Gs, bs)):
+        m = g.shape[0]
+        G[t, :m, :m] = torch.from_numpy(np.asarray(g, dtype=np.float64))
+        b[t, :m] = torch.from_numpy(np.asarray(v, dtype=np.float64))
+    G, b = G.to(dev), b.to(dev)
+    w = torch.zeros((n, K), dtype=torch.float64, device=dev)
+    diag = torch.diagonal(G, dim1=1, dim2=2)
+    live = diag > 0                                   # sq[k] == 0 columns are skipped
+    active = torch.ones(n, dtype=torch.bool, device=dev)
+    for _ in range(iters):
+        dmax = torch.zeros(n, dtype=torch.float64, device=dev)
+        for k in range(K):
+            gk = G[:, k, :]
+            rho = b[:, k] - (gk * w).sum(1) + diag[:, k] * w[:, k]
+            nw = torch.clamp(rho - l1, min=0.0) / (diag[:, k] + l2)
+            upd = active & live[:, k]
+            nw = torch.where(upd, nw, w[:, k])
+            dmax = torch.maximum(dmax, (nw - w[:, k]).abs())
+            w[:, k] = nw
+        active = active & (dmax >= eps)
+        if not bool(active.any()):
+            break
+    return w.cpu().numpy()
+
+
 class SLIM(Learner):
     """For every item i: min_w ½||r_i − Σ_j w_j r_j||² + ½λ2||w||² + λ1||w||₁, w ≥ 0, over the
     item's kNN neighbours j (coordinate descent with soft thresholding)."""
@@ -44,7 +88,7 @@ class SLIM(Learner):
             if knn:
                 for jj, rr in dict(knn).items():
                     g["nb"].setdefault(jj, dict(rr))
-        rows = []
+        items, nbl, Gs, bs = [], [], [], []
         for i, g in groups.items():
             ri = g["ri"] or {}
             nbs = [j for j in g["nb"] if j != i]
@@ -59,26 +103,18 @@ class SLIM(Learner):
             for col, j in enumerate(nbs):
                 for u, v in g["nb"][j].items():
                     X[uix[u], col] = v
-            w = np.zeros(len(nbs))
-            resid = y.copy()
-            sq = (X * X).sum(0)
-            for _ in range(int(c["iters"])):
-                dmax = 0.0
-                for k in range(len(nbs)):
-                    if sq[k] == 0:
-                        continue
-                    rho = X[:, k] @ resid + sq[k] * w[k]
-                    nw = max(0.0, rho - c["l1"]) / (sq[k] + c["l2"])
-                    d = nw - w[k]
-                    if d != 0:
-                        resid -= d * X[:, k]
-                        w[k] = nw
-                        dmax = max(dmax, abs(d))
-                if dmax < c["eps"]:
-                    break
-            for k, j in enumerate(nbs):
-                if w[k] != 0:
-                    rows.append((i, j, float(w[k])))
+            items.append(i)
+            nbl.append(nbs)
+            Gs.append(X.T @ X)
+            bs.append(X.T @ y)
+        rows = []
+        if items:
+            W = slim_cd_batched(Gs, bs, float(c["l1"]), float(c["l2"]), int(c["iters"]),
+                                float(c["eps"]), self.device)
+            for n, (i, nbs) in enumerate(zip(items, nbl)):
+                for k, j in enumerate(nbs):
+                    if W[n, k] != 0:
+                        rows.append((i, j, float(W[n, k])))
         self.table = pd.DataFrame(rows, columns=["i", "nn", "w"])
         return self
 
