@@ -126,11 +126,10 @@ class _MFBase(Learner):
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
                          self._grid()], dtype=np.int32)
 
-    # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Squared-loss
-    # SGD has unbounded per-rating steps: 32 rows/block diverged on a small dense catalogue
-    # (300 items, tests/test_mf.py::test_mf_gpu_quality, RMSE 2.24 vs 0.14) although the
-    # ML-20M-shaped sweep (profiles/mf_grid_r1.log) showed no loss up to grid 1696, so explicit
-    # MF keeps 256 (pass -grid to raise it on large catalogues).
+    # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
+    # keeps 256: on the tests/test_mf.py fixture SGD learns the factors only at grid 1 and stays
+    # at the bias-only RMSE from grid 3 up (profiles/mf_staleness_probe_r1.log,
+    # docs/perf_notes.md); pass -grid to override.
     ROWS_PER_BLOCK = 256
 
     def _grid(self) -> int:
