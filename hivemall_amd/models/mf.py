@@ -127,9 +127,9 @@ class _MFBase(Learner):
                          self._grid()], dtype=np.int32)
 
     # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
-    # keeps 256: on the tests/test_mf.py fixture SGD learns the factors only at grid 1 and stays
-    # at the bias-only RMSE from grid 3 up (profiles/mf_staleness_probe_r1.log,
-    # docs/perf_notes.md); pass -grid to override.
+    # keeps 256: on a small catalogue, concurrent stale updates slow the escape from the
+    # near-zero factor init (300 items: 20-epoch RMSE 0.14 at grid 1, 1.40 at grid 3, 2.24 at
+    # grid 9; profiles/mf_staleness_probe23_r1.log, docs/perf_notes.md); -grid overrides.
     ROWS_PER_BLOCK = 256
 
     def _grid(self) -> int:
