@@ -2,8 +2,11 @@
 """Headline benchmark: train_ffm rows/sec on Criteo-shaped sparse data (BASELINE.json).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
-          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+N>1 without a launcher: the parent process starts ``torch.distributed.run`` with N ranks on
+127.0.0.1 itself (before it touches the GPU) and exits with the launcher's code; under a
+launcher (``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``) every
+rank checks WORLD_SIZE == N and that the process group really holds N ranks, else exits 2.
 
 One process per GPU.  Each rank holds a full FFM model replica in HBM
 (2^20 hashed features x 39 fields x k=4, fp32 V + AdaGrad G + FTRL state, ~1.3 GB) and
@@ -54,11 +57,61 @@ def parse_args(argv=None):
                     help="1: re-read the own slot right before its update (short Hogwild window); "
                          "0: keep the gathered slot in registers; -1: by layout (packed -> 0)")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--mix-probe", type=int, default=3,
+                    help="synchronous mixes timed after the run (ms, wire bytes, bus GB/s)")
     return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args, argv) -> int | None:
+    """--gpus N > 1 outside a launcher: run N ranks under torch.distributed.run as a CHILD
+    process (this process never initialises the GPU, so nothing is exec'd over a HIP context)
+    and return its exit code.  None when this process is itself a rank."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args, ctx) -> None:
+    """Every rank: the job must really be N ranks (driver contract: value = whole-job rate)."""
+    import torch.distributed as dist
+
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    pg_world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+    bad = []
+    if env_world != args.gpus:
+        bad.append(f"WORLD_SIZE={env_world}")
+    if pg_world != args.gpus or ctx.world_size != args.gpus:
+        bad.append(f"process group world={pg_world}")
+    if ctx.device.type == "cuda" and torch.cuda.device_count() < args.gpus:
+        bad.append(f"only {torch.cuda.device_count()} visible GPUs")
+    if bad:
+        print(f"[bench] --gpus {args.gpus} but " + ", ".join(bad), file=sys.stderr, flush=True)
+        sys.exit(2)
 
 
 def main(argv=None):
     args = parse_args(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        sys.exit(rc)
     from hivemall_amd.parallel.dist import init_distributed
     from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
     from hivemall_amd.models.ffm import FFMTrainer
@@ -68,8 +121,7 @@ def main(argv=None):
     ctx = init_distributed(device=args.device)
     dev = ctx.device
     world, rank = ctx.world_size, ctx.rank
-    if args.gpus != world and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    check_world(args, ctx)
     F = 39
     NF = 1 << args.hash_bits
     B = args.batch
@@ -109,6 +161,7 @@ def main(argv=None):
     sync()
     ctx.barrier()
     sync()
+    calls0 = mixer.calls
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
@@ -117,6 +170,7 @@ def main(argv=None):
     sync()
     ctx.barrier()
     t1 = time.perf_counter()
+    mixes_timed = mixer.calls - calls0
     elapsed = t1 - t0
     elapsed = mixer.all_reduce_scalar(elapsed, "max")
     ms_per_step = 1000.0 * elapsed / max(1, args.steps)
@@ -133,6 +187,8 @@ def main(argv=None):
                 overlap.finish()
             sync()
 
+    # ---- mix cost on its own (synchronous, outside the timed region); leaves the model mixed ----
+    probe = mixer.probe(mix_tensors, args.mix_probe) if world > 1 else {}
     # ---- quality: final mix, then held-out logloss vs the planted-model floor ----
     if world > 1:
         mixer.average(mix_tensors)
@@ -173,7 +229,13 @@ def main(argv=None):
                 "state_layout": args.layout if dev.type == "cuda" else "split",
                 "reload": (args.layout == "split") if args.reload < 0 else bool(args.reload),
                 "mixed_bytes_per_mix": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
+                "mixes_in_timed_region": mixes_timed,
+                "mix_overlapped": bool(overlap is not None),
             },
+            "rccl_world": world if ctx.backend == "nccl" else None,
+            "dist_backend": ctx.backend,
+            "world": world,
+            **probe,
             "logloss_heldout": round(ll, 5) if ll is not None else None,
             "logloss_planted_floor": round(floor, 5) if floor is not None else None,
             "rows_trained_per_rank": B * (args.steps + args.warmup),

@@ -7,23 +7,127 @@ Upstream (reference hivemall/mix/**, mixserv/*
   value (``PartialAverage`` / ``PartialArgminKLD``).
 
 MI355X-native: every rank holds the whole (hashed, dense) model in HBM, so mixing is a
-collective on dense tensors:
-* AVERAGE    = all_reduce(SUM) / world
-* ARGMIN_KLD = all_reduce over the interleaved pair [w/σ, 1/σ] -> w = Σ(w/σ)/Σ(1/σ),
-               σ = 1/Σ(1/σ)
-Bucketing: small tensors are coalesced into one flat buffer; big ones are reduced in
-place in ``bucket_mb`` chunks, all issued asynchronously so RCCL keeps several rings'
-worth of work in flight over the 7 xGMI links.  Chunks default to 64 MB (a single ring
-step then moves 8 MB per link; big enough to be bandwidth-bound, small enough for ≥7
-chunks on any model over 448 MB).  Optimizer state stays local by default (upstream only
-mixes weights/covariance).
+collective on dense tensors.
+
+AVERAGE (:meth:`ModelMixer.average`) is a *shard mean*, not a ring all-reduce:
+
+    all_to_all(flat)  ->  fp32 sum of the world's copies of my 1/world shard, one rounding
+                      ->  all_gather(shard means)
+
+* the wire carries the replica's storage dtype (bf16 state: half the bytes of an fp32 wire),
+  yet the sum is formed in fp32 (``csrc/kernels/mix.hip``) — a bf16 ring all-reduce would
+  round the partial sum at every hop;
+* wire bytes per rank are 2(N-1)/N of the payload, the same as a ring all-reduce;
+* the all-to-all sends to all N-1 peers at once: on a fully connected xGMI node that is all 7
+  point-to-point links of a GPU busy together, where one ring uses two of them;
+* every rank computes its shard's mean once and gathers the others, so all replicas are
+  bit-identical after a mix (the order of the fp32 sum is fixed: rank 0..N-1).
+
+Tensors are grouped by dtype into one flat, world-padded wire buffer per group (allocated once
+per tensor list), so a model of five tensors costs two collectives per dtype, never a small
+all-reduce per tensor.  Strided views (the V half of the packed FFM V|G table) are packed by one
+strided copy; only the weights travel (AdaGrad/FTRL state stays local, as upstream).
+
+ARGMIN_KLD = SUM all-reduce over [w/σ, 1/σ] -> w = Σ(w/σ)/Σ(1/σ), σ = 1/Σ(1/σ) (fp32).
+SUM (:meth:`ModelMixer.all_reduce_sum`, histograms / counters) widens bf16/fp16 to fp32.
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
 
+from .. import _native
 from .dist import DistContext, context
+
+_native.register_hip("hm_mix_shard_mean", [_native.c_p, _native.c_int, _native.c_i64,
+                                           _native.c_int, _native.c_p, _native.c_p])
+_native.register_hip("hm_mix_merge", [_native.c_p, _native.c_p, _native.c_p, _native.c_i64,
+                                      _native.c_int, _native.c_i64, _native.c_int, _native.c_p])
+
+_LOWP = (torch.bfloat16, torch.float16)
+
+
+def _dtype_code(dt: torch.dtype) -> int | None:
+    return {torch.float32: 0, torch.bfloat16: 1}.get(dt)
+
+
+def _row_view(t: torch.Tensor):
+    """(rows, inner, row_stride) when ``t`` is rows of ``inner`` contiguous elements at a uniform
+    stride (contiguous tensors and the packed V half), else None."""
+    if t.is_contiguous():
+        return (t.numel() // 4, 4, 4) if t.numel() % 4 == 0 else None
+    if t.dim() < 2 or t.stride(-1) != 1:
+        return None
+    for i in range(t.dim() - 2):
+        if t.stride(i) != t.shape[i + 1] * t.stride(i + 1):
+            return None
+    rows = t.numel() // t.shape[-1]
+    inner, rs = t.shape[-1], t.stride(-2)
+    if inner % 4 or rs % 4:
+        return None
+    return rows, inner, rs
+
+
+class _FlatGroup:
+    """Same-dtype tensors packed into one flat wire buffer, padded to a multiple of 4*world."""
+
+    def __init__(self, tensors: list[torch.Tensor], world: int):
+        self.tensors = tensors
+        self.dtype = tensors[0].dtype
+        dev = tensors[0].device
+        self.offs = []
+        off = 0
+        for t in tensors:
+            self.offs.append(off)
+            off += (t.numel() + 3) // 4 * 4          # 16-B / 8-B aligned segments
+        q = 4 * world
+        self.n = (off + q - 1) // q * q
+        self.shard = self.n // world
+        self.send = torch.zeros(self.n, dtype=self.dtype, device=dev)   # = the snapshot
+        self.recv = torch.empty(self.n, dtype=self.dtype, device=dev)
+        self.mean = torch.empty(self.shard, dtype=self.dtype, device=dev)
+        self.out = torch.empty(self.n, dtype=self.dtype, device=dev)
+        self.nbytes = self.n * self.send.element_size()
+
+    def seg(self, buf: torch.Tensor, k: int) -> torch.Tensor:
+        t = self.tensors[k]
+        return buf[self.offs[k]:self.offs[k] + t.numel()].view(t.shape)
+
+    def pack(self) -> None:
+        for k, t in enumerate(self.tensors):
+            self.seg(self.send, k).copy_(t)
+
+    def unpack(self) -> None:
+        for k, t in enumerate(self.tensors):
+            t.copy_(self.seg(self.out, k))
+
+    def shard_mean(self, world: int) -> None:
+        """mean = fp32 sum over ranks of recv[r] / world, rounded once to the wire dtype."""
+        code = _dtype_code(self.dtype)
+        if self.recv.is_cuda and code is not None:
+            rc = _native.hip().hm_mix_shard_mean(self.recv.data_ptr(), world, self.shard, code,
+                                                 self.mean.data_ptr(),
+                                                 _native.stream_of(self.recv.device))
+            _native.check(rc, "hm_mix_shard_mean")
+        else:
+            s = self.recv.view(world, self.shard).sum(0, dtype=torch.float32)
+            self.mean.copy_(s.mul_(1.0 / world))
+
+    def merge(self) -> None:
+        """t <- t + (mean - snapshot), fp32 math, one rounding (overlapped mixing)."""
+        code = _dtype_code(self.dtype)
+        for k, t in enumerate(self.tensors):
+            m, s = self.seg(self.out, k), self.seg(self.send, k)
+            rv = _row_view(t) if t.is_cuda else None
+            if rv is not None and code is not None and t.data_ptr() % 16 == 0:
+                rows, inner, rs = rv
+                rc = _native.hip().hm_mix_merge(t.data_ptr(), m.data_ptr(), s.data_ptr(), rows,
+                                                inner, rs, code, _native.stream_of(t.device))
+                _native.check(rc, "hm_mix_merge")
+            else:
+                t.copy_(t.to(torch.float32) + (m.to(torch.float32) - s.to(torch.float32)))
 
 
 class ModelMixer:
@@ -33,8 +137,10 @@ class ModelMixer:
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.small_bytes = small_bytes
         self.wire_dtype = wire_dtype
-        self.bytes_reduced = 0
+        self.bytes_reduced = 0       # payload bytes mixed (sum over calls)
+        self.wire_bytes = 0          # bytes this rank sent over the fabric (sum over calls)
         self.calls = 0
+        self._plans: dict = {}
 
     @property
     def world(self) -> int:
@@ -43,9 +149,50 @@ class ModelMixer:
     def _active(self) -> bool:
         return self.ctx.is_dist and self.world > 1
 
+    # ---------------------------------------------------------------- shard-mean plan
+    def plan(self, tensors: list[torch.Tensor]) -> list[_FlatGroup]:
+        """Flat wire groups for this exact tensor list (cached by identity and shape)."""
+        key = tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) for t in tensors)
+        p = self._plans.get(key)
+        if p is None:
+            by_dt: dict = {}
+            for t in tensors:
+                by_dt.setdefault(t.dtype, []).append(t)
+            p = [_FlatGroup(ts, self.world) for ts in by_dt.values()]
+            if len(self._plans) >= 4:                # one-off lists must not pin buffers
+                self._plans.pop(next(iter(self._plans)))
+            self._plans[key] = p
+        return p
+
+    def _count(self, groups: list[_FlatGroup], tensors) -> None:
+        self.calls += 1
+        self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
+        self.wire_bytes += sum(2 * (self.world - 1) * g.nbytes // self.world for g in groups)
+
+    def _a2a(self, g: _FlatGroup, async_op: bool = False):
+        return dist.all_to_all_single(g.recv, g.send, async_op=async_op)
+
+    def _gather(self, g: _FlatGroup, async_op: bool = False):
+        return dist.all_gather_into_tensor(g.out, g.mean, async_op=async_op)
+
+    def average(self, tensors: list[torch.Tensor]) -> None:
+        """In-place replica mean (shard-mean collective, see the module docstring)."""
+        if not self._active():
+            return
+        groups = self.plan(tensors)
+        for g in groups:
+            g.pack()
+        for g in groups:
+            self._a2a(g)
+            g.shard_mean(self.world)
+            self._gather(g)
+            g.unpack()
+        self._count(groups, tensors)
+
+    # ---------------------------------------------------------------- sum all-reduce
     def all_reduce_sum(self, tensors: list[torch.Tensor]) -> None:
-        """In-place SUM all-reduce of a list of tensors (bucketed, async; non-contiguous views
-        are reduced through a contiguous copy)."""
+        """In-place SUM all-reduce of a list of tensors (bucketed, async).  bf16/fp16 tensors are
+        summed in fp32 (an N-way sum rounded at every ring hop would lose their low bits)."""
         if not self._active():
             return
         small = [t for t in tensors if t.numel() * t.element_size() <= self.small_bytes]
@@ -55,9 +202,13 @@ class ModelMixer:
         if small:
             flat = torch.cat([t.reshape(-1).to(torch.float32) for t in small])
             works.append(dist.all_reduce(flat, async_op=True))
-        staged = []   # strided views (e.g. the V half of the packed FFM table) go via a copy
+        staged = []   # strided views and low-precision tensors go via an fp32/contiguous copy
         for t in big:
-            buf = t if t.is_contiguous() else t.contiguous()
+            buf = t
+            if t.dtype in _LOWP:
+                buf = t.to(torch.float32)
+            elif not t.is_contiguous():
+                buf = t.contiguous()
             if buf is not t:
                 staged.append((t, buf))
             v = buf.view(-1)
@@ -75,15 +226,9 @@ class ModelMixer:
                 t.copy_(flat[off:off + n].view_as(t).to(t.dtype))
                 off += n
         self.calls += 1
-        self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
-
-    def average(self, tensors: list[torch.Tensor]) -> None:
-        if not self._active():
-            return
-        self.all_reduce_sum(tensors)
-        inv = 1.0 / self.world
-        for t in tensors:
-            t.mul_(inv)
+        nb = sum(t.numel() * t.element_size() for t in tensors)
+        self.bytes_reduced += nb
+        self.wire_bytes += 2 * (self.world - 1) * nb // self.world
 
     def argmin_kld(self, w: torch.Tensor, covar: torch.Tensor, eps: float = 1e-12) -> None:
         """Mix (w, covar) in place with the argmin-KLD rule (PartialArgminKLD)."""
@@ -118,30 +263,62 @@ class ModelMixer:
                                "min": dist.ReduceOp.MIN}[op])
         return float(t.item())
 
+    # ---------------------------------------------------------------- measurement
+    def probe(self, tensors: list[torch.Tensor], reps: int = 3) -> dict:
+        """Time ``reps`` synchronous shard-mean mixes of ``tensors`` (device events on the GPU,
+        after a barrier); returns ms per mix, wire bytes per rank and bus GB/s (nccl-tests
+        convention: 2(N-1)/N * payload / time).  The tensors are left mixed."""
+        if not self._active() or reps <= 0:
+            return {}
+        groups = self.plan(tensors)
+        payload = sum(g.nbytes for g in groups)
+        wire = sum(2 * (self.world - 1) * g.nbytes // self.world for g in groups)
+        self.average(tensors)                      # warm the communicators / buffers
+        self.ctx.barrier()
+        cuda = tensors[0].is_cuda
+        if cuda:
+            torch.cuda.synchronize(tensors[0].device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.average(tensors)
+        if cuda:
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+        else:
+            ms = 1000.0 * (time.perf_counter() - t0) / reps
+        ms = self.all_reduce_scalar(ms, "max")
+        return {"mix_ms": round(ms, 4), "mix_payload_bytes": int(payload),
+                "mix_wire_bytes_per_rank": int(wire),
+                "mix_bus_gbps": round(wire / (ms * 1e-3) / 1e9, 2) if ms > 0 else None,
+                "mix_algo": "all_to_all + fp32 shard mean + all_gather"}
+
 
 class OverlappedMixer:
-    """Stale-by-one model averaging whose all-reduce runs behind the training kernels.
+    """Stale-by-one model averaging whose collectives run behind the training kernels.
 
-    ``start(tensors)`` snapshots the replicas (one device copy on the compute stream) and
-    launches the bucketed all-reduce of the snapshot asynchronously (RCCL's own stream);
-    training continues.  ``finish()`` (at the next mix point) waits for the collective on the
-    device — not on the host — and merges it without discarding the local progress made in the
-    meantime:
+    ``start(tensors)`` snapshots the replicas into the flat wire buffers (one strided copy on the
+    compute stream) and launches the shard-mean collective (all-to-all -> fp32 shard mean ->
+    all-gather) on a side stream; training continues.  ``finish()`` (at the next mix point)
+    makes the compute stream wait for the all-gather — on the device, not the host — and merges
+    without discarding the local progress made in the meantime:
 
         x  <-  x + (mean_r(snapshot_r) - snapshot_local)
 
     i.e. every rank moves by the consensus correction of the snapshot.  This is the
     asynchronous MixServer semantics (replies arrive while the learner keeps training) on
     xGMI, and it hides the collective completely when one mix interval of compute takes longer
-    than the all-reduce.  Buffers are allocated once (2x the mixed bytes).
+    than the collective.  The wire carries the storage dtype (bf16 V: half the bytes) and the
+    sum is still exact fp32 (the shard mean).  Buffers: 3x the mixed bytes, allocated once.
     """
 
     def __init__(self, mixer: ModelMixer):
         self.m = mixer
-        self.snap: list[torch.Tensor] | None = None
-        self.buf: list[torch.Tensor] | None = None
+        self.groups: list[_FlatGroup] | None = None
         self.works: list = []
-        self.targets: list[torch.Tensor] = []
+        self.side = None
 
     def pending(self) -> bool:
         return bool(self.works)
@@ -151,26 +328,27 @@ class OverlappedMixer:
             return
         if self.works:
             self.finish()
-        if self.snap is None:
-            # bf16 replicas are reduced in fp32: an 8-way sum rounded to 8 mantissa bits would
-            # inject noise into every mix (the wire cost is hidden behind compute anyway).  The
-            # snapshot keeps the replica's own dtype (an exact copy), which halves its bytes.
-            wide = lambda t: torch.empty(t.shape, dtype=torch.float32 if t.dtype in (
-                torch.bfloat16, torch.float16) else t.dtype, device=t.device)
-            self.snap = [torch.empty(t.shape, dtype=t.dtype, device=t.device) for t in tensors]
-            self.buf = [wide(t) for t in tensors]
-        self.targets = tensors
-        for s, b, t in zip(self.snap, self.buf, tensors):
-            s.copy_(t)          # one strided read of the replica (e.g. the V half of packed VG)
-            b.copy_(s)
-        self.works = []
-        for b in self.buf:
-            v = b.view(-1)
-            step = max(1, self.m.bucket_bytes // b.element_size())
-            for s0 in range(0, v.numel(), step):
-                self.works.append(dist.all_reduce(v[s0:s0 + step], async_op=True))
-        self.m.calls += 1
-        self.m.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
+        self.groups = self.m.plan(tensors)
+        for g in self.groups:
+            g.pack()                                 # the snapshot (exact copy of the replica)
+        world = self.m.world
+        if tensors[0].is_cuda:
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=tensors[0].device)
+            self.side.wait_stream(torch.cuda.current_stream(tensors[0].device))
+            with torch.cuda.stream(self.side):
+                for g in self.groups:
+                    self.m._a2a(g, async_op=True).wait()    # side stream waits, host does not
+                    g.shard_mean(world)
+                    self.works.append(self.m._gather(g, async_op=True))
+        else:
+            # gloo: the shard mean needs the all-to-all's data on the host, so the first half
+            # runs synchronously; the all-gather stays in flight behind the caller's compute
+            for g in self.groups:
+                self.m._a2a(g)
+                g.shard_mean(world)
+                self.works.append(self.m._gather(g, async_op=True))
+        self.m._count(self.groups, tensors)
 
     def finish(self) -> None:
         if not self.works:
@@ -178,11 +356,8 @@ class OverlappedMixer:
         for w in self.works:
             w.wait()
         self.works = []
-        inv = 1.0 / self.m.world
-        for t, s, b in zip(self.targets, self.snap, self.buf):
-            # x <- x + (mean - snapshot): in place, fp32 math, one rounding to t's dtype
-            b.mul_(inv).sub_(s)
-            t.add_(b)
+        for g in self.groups:
+            g.merge()
 
 
 class SparseDeltaMixer:
@@ -190,8 +365,9 @@ class SparseDeltaMixer:
     all-reduce (SURVEY.md §5.8 "sparse alternative"; upstream's MixClient likewise only pushes
     the features a learner updated, reference hivemall/mix/client/MixClient.java).
 
-    Every rank keeps ``base`` = the last mixed model.  Rows that a rank did not touch since then
-    equal ``base`` on that rank, so the replica mean is exactly
+    Every rank keeps ``base`` = the last mixed model (as stored: a bf16 replica's base is the
+    bf16 value widened, so untouched rows compare equal).  Rows that a rank did not touch since
+    then equal ``base`` on that rank, so the replica mean is exactly
 
         mean_r(x_r) = base + Σ_r Δ_r / world,   Δ_r = x_r - base  (non-zero on touched rows only)
 
@@ -200,7 +376,7 @@ class SparseDeltaMixer:
     fp32) and copies the result back — bit-for-bit the dense average up to summation order.
     Wire bytes per rank are ``world · touched · (row_bytes + 8)`` against ``≈2 · rows ·
     row_bytes`` for a ring all-reduce, so when the touched fraction exceeds ``dense_fraction``
-    (default ``1 / world``) the step falls back to the dense bucketed all-reduce of
+    (default ``1 / world``) the step falls back to the dense shard mean of
     :class:`ModelMixer` — decided collectively (max over ranks) so every rank takes the same
     path.  Costs one fp32 copy of the mixed tensors for ``base``.
     """
@@ -241,7 +417,7 @@ class SparseDeltaMixer:
         for k, (t, b, ix) in enumerate(zip(tensors, self.base, idx)):
             if t.dim() == 0:
                 self.m.average([t])
-                b.copy_(t)
+                b.copy_(t.to(torch.float32))
                 continue
             rows = t.shape[0]
             if maxc[k] == 0:
@@ -249,7 +425,7 @@ class SparseDeltaMixer:
                 continue
             if maxc[k] > frac * rows:
                 self.m.average([t])
-                b.copy_(t)
+                b.copy_(t.to(torch.float32))
                 self.dense_mixes += 1
                 continue
             n = maxc[k]
@@ -269,6 +445,11 @@ class SparseDeltaMixer:
             keep = gi >= 0
             b.index_add_(0, gi[keep], gd[keep], alpha=1.0 / world)
             t.copy_(b)
+            if t.dtype != torch.float32:
+                # the replica now holds base rounded to its dtype: keep base equal to what is
+                # stored, or every mixed row would look touched at the next mix
+                b.copy_(t.to(torch.float32))
             self.sparse_rows += int(allc[:, k].sum())
             self.m.bytes_reduced += n * world * (delta[0].numel() * 4 + 8)
+            self.m.wire_bytes += n * (world - 1) * (delta[0].numel() * 4 + 8)
         self.m.calls += 1

@@ -195,6 +195,36 @@ def test_bench_torchrun_cpu_world2():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
 
 
+def test_bench_self_launch_cpu_world2():
+    """`python bench.py --gpus 2` with no launcher starts 2 ranks itself (the driver contract:
+    the JSON's value is the whole-job rate of N ranks), and reports the mix cost."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", "512", "--hash-bits", "10", "--mix-every", "1",
+           "--eval-rows", "512", "--device", "cpu", "--resident-batches", "2", "--mix-probe", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["dist_backend"] == "gloo" and d["rccl_world"] is None
+    assert d["config"]["mixes_in_timed_region"] == 2
+    assert d["mix_ms"] > 0 and d["mix_wire_bytes_per_rank"] > 0 and d["mix_bus_gbps"] > 0
+
+
+def test_bench_refuses_world_mismatch():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "3", "--steps", "1", "--warmup", "0", "--batch", "256", "--hash-bits", "10",
+           "--eval-rows", "256", "--device", "cpu", "--resident-batches", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0
+    assert "--gpus 3 but" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def _fm_mf_bpr_dp(ctx):
     import numpy as np
 
