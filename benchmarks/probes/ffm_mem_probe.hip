@@ -1,0 +1,80 @@
+// Roofline probe for the FFM slot traffic: the exact per-row access pattern of ffm_*_kernel
+// (1,482 live 16-B packed V|G slots gathered at (i_a * num_fields + f_b) * 16, each written
+// back once) with no arithmetic, LDS image or reductions.  Tells how fast the memory system
+// serves this pattern on MI355X, i.e. the ceiling for the real kernel.
+//
+//   mode 0: gather only (registers), one float per row written
+//   mode 1: gather + write back every live slot (the training kernel's traffic)
+//   mode 2: mode 1 with 2 rows per block iteration in flight (loads of both issued first)
+//   mode 3: 128-B aligned feature blocks (field stride 40 slots = 640 B = 5 lines) and the
+//           diagonal + pad slot written too: every written line is written in full
+//   mode 4: the aligned layout of mode 3, live slots only (partial lines)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+template <int NS, int MODE, int STRIDE>
+__global__ __launch_bounds__(256) void probe_kernel(const int32_t* __restrict__ idx, int B, int F, int nfld,
+                                                    char* __restrict__ vg, float* __restrict__ out) {
+    __shared__ int s_i[2][64];
+    const int tid = threadIdx.x;
+    const int FF = F * F;
+    constexpr int R = MODE == 2 ? 2 : 1;
+    for (int row0 = blockIdx.x * R; row0 < B; row0 += gridDim.x * R) {
+        for (int r = 0; r < R; ++r)
+            if (tid < F) s_i[r][tid] = row0 + r < B ? idx[(size_t)(row0 + r) * F + tid] : -1;
+        __syncthreads();
+        uint4 q[R][NS];
+        uint32_t off[R][NS];
+        bool live[R][NS];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const int s = tid + j * 256;
+                const int a = s < FF ? s / F : 0, b = s < FF ? s % F : 0;
+                const int ia = s_i[r][a], ib = s_i[r][b];
+                live[r][j] = a != b && ia >= 0 && ib >= 0;
+                if (MODE == 3) live[r][j] = s < FF && ia >= 0 && ib >= 0;
+                off[r][j] = live[r][j] ? ((uint32_t)ia * (uint32_t)STRIDE + (uint32_t)b) * 16u : 0u;
+                q[r][j] = *reinterpret_cast<const uint4*>(vg + off[r][j]);
+            }
+        }
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (MODE == 0) {
+                    acc += __uint_as_float(q[r][j].x) + __uint_as_float(q[r][j].w);
+                } else if (live[r][j]) {
+                    uint4 v = q[r][j];
+                    v.x ^= 1u;
+                    *reinterpret_cast<uint4*>(vg + off[r][j]) = v;
+                }
+            }
+        }
+        if (MODE == 0 && acc == 1234.5f) out[row0] = acc;
+        if (MODE == 3 && tid < F && s_i[0][tid] >= 0)
+            *reinterpret_cast<uint4*>(vg + ((size_t)s_i[0][tid] * STRIDE + (STRIDE - 1)) * 16u) = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" int hm_probe_ffm_mem(const int32_t* idx, int B, int F, int nfld, void* vg, float* out, int mode,
+                                int blocks, hipStream_t stream) {
+    if (F * F > 1536) return (int)hipErrorInvalidValue;
+#define L(M, S) hipLaunchKernelGGL((probe_kernel<6, M, S>), dim3(blocks), dim3(256), 0, stream, idx, B, F, nfld, \
+                                   (char*)vg, out)
+    if (F != 39) return (int)hipErrorInvalidValue;
+    if (mode == 0) L(0, 39);
+    else if (mode == 1) L(1, 39);
+    else if (mode == 2) L(2, 39);
+    else if (mode == 3) L(3, 40);
+    else L(1, 40);
+#undef L
+    return (int)hipGetLastError();
+}

@@ -39,6 +39,9 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
     const float l1 = hp[5], l2 = hp[6], tmin = hp[7], tmax = hp[8];
     // slot stride: Kp (separate V / G tables) or 2*Kp (packed [NF][NFLD][2][Kp], G = V + Kp)
     const size_t ss = ip[14] ? (size_t)2 * Kp : (size_t)Kp;
+    // slots between consecutive features (>= NFLD: the GPU's packed table pads each feature
+    // block to whole 128-B lines)
+    const size_t FS = ip[16] > 0 ? (size_t)ip[16] : (size_t)NFLD;
     std::vector<int> ri(F), rf(F);
     std::vector<float> rx(F);
     std::vector<float> snap((size_t)F * F * Kp);
@@ -61,7 +64,7 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
             for (int b = 0; b < F; ++b) {
                 float* dst = &snap[((size_t)a * F + b) * Kp];
                 if (a != b && ri[a] >= 0 && ri[b] >= 0)
-                    std::memcpy(dst, V + ((size_t)ri[a] * NFLD + rf[b]) * ss, sizeof(float) * Kp);
+                    std::memcpy(dst, V + ((size_t)ri[a] * FS + rf[b]) * ss, sizeof(float) * Kp);
                 else
                     std::memset(dst, 0, sizeof(float) * Kp);
             }
@@ -98,8 +101,8 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
             for (int b = 0; b < F; ++b) {
                 if (a == b || ri[a] < 0 || ri[b] < 0) continue;
                 const float coef = ks * rx[a] * rx[b];
-                float* pv = V + ((size_t)ri[a] * NFLD + rf[b]) * ss;
-                float* pg = G + ((size_t)ri[a] * NFLD + rf[b]) * ss;
+                float* pv = V + ((size_t)ri[a] * FS + rf[b]) * ss;
+                float* pg = G + ((size_t)ri[a] * FS + rf[b]) * ss;
                 const float* own = &snap[((size_t)a * F + b) * Kp];
                 const float* par = &snap[((size_t)b * F + a) * Kp];
                 for (int k = 0; k < Kp; ++k) {

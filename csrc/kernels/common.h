@@ -52,9 +52,13 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// Numerically safe log(1 + exp(x)).
+// Numerically safe log(1 + exp(x)) on the hardware exp/log (v_exp_f32 / v_log_f32): per-row
+// loss reporting only.  libm's log1pf cost ~40 VALU and enough registers to push the FFM row
+// loop into scratch spills; the absolute error here is < 1e-7 (1 + e^x rounds to 1 below
+// x ~ -16.6, where the true value is < 6e-8).
 __device__ __forceinline__ float log1pexp(float x) {
-    return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x));
+    const float t = __logf(1.f + __expf(-fabsf(x)));
+    return x > 0.f ? x + t : t;
 }
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
@@ -80,6 +84,15 @@ __device__ __forceinline__ uint32_t pack_bf16x2_sr(float lo, uint32_t r_lo, floa
     uint32_t u;
     __builtin_memcpy(&u, &v, 4);
     return u;
+}
+
+// Load that bypasses the CU's L1 (agent-scope relaxed atomic load -> `sc1` global load on
+// gfx950).  The vector L1 is not coherent with other CUs' stores: a Hogwild kernel whose rows
+// are small enough to stay L1-resident would otherwise keep reading its own stale copy of a
+// row that other CUs keep updating in L2 for the whole launch.
+template <typename T>
+__device__ __forceinline__ T ld_coherent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // XCD-aware bijective remap of a flat block id (cdna_hip_programming.md §5, "XCD swizzle

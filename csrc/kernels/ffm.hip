@@ -48,6 +48,8 @@ struct FFMParams {
     int use_linear, use_bias, norm;
     int reload;
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
+    int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
+                           // table pads each feature block to whole 128-B lines)
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     float* s_red = s_x + F;                                              // 16 (+pad)
 
     const int tid = threadIdx.x;
-    const size_t nfld = (size_t)P.num_fields;
+    const size_t nfld = (size_t)P.fstride;
     const size_t ss = (size_t)P.sstride;
     auto slot_off = [&](int i, int f) -> size_t { return ((size_t)i * nfld + (size_t)f) * ss; };
 
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_p
     float* s_x = reinterpret_cast<float*>(s_fld + F);
     float* s_red = s_x + F;
     const int tid = threadIdx.x;
-    const uint32_t nfld = (uint32_t)P.num_fields;
+    const uint32_t nfld = (uint32_t)P.fstride;
 
     // slot -> (a, b) is row-invariant: decoded once as a | b << 16 (-1 past the end)
     int ab[NS];
@@ -549,6 +551,526 @@ __global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_p
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lean packed kernel (K <= 4, packed V|G slots): the shipped kernel for the headline shape.
+//
+// Counters of ffm_packed_kernel on MI355X (profiles/ffm_pmc_packed_r2b.json) show the row loop
+// is bound by vector-instruction ISSUE, not by memory: 3,976 VALU wave-instructions per row
+// (~166 per slot and wave), 22 % of wave-cycles issuing with 4 waves/SIMD (the SIMDs ~90 %
+// busy), HBM-side traffic only 3.7 TB/s.  The VALU went to bf16 unpacking, 13 quarter-rate
+// v_mul_lo_u32 per slot for the stochastic-rounding hash chain, 64-bit address math and
+// register shuffles around the per-slot branches.  This kernel does the same arithmetic with:
+//   * the forward pair dot as two v_dot2c_f32_bf16 on the raw bf16 words (no unpack);
+//   * the update in packed fp32 (v_pk_mul/fma/add_f32: two elements per instruction);
+//   * ONE 32-bit hash per slot (row seed + a per-thread constant, one multiply) whose rotated
+//     16-bit windows feed all eight v_cvt_sr_bf16_f32 (each window uniform -> unbiased);
+//   * a transposed LDS image: slot s = (a, b) writes its own V to T[b*F + a], so the partner
+//     V[i_b, f_a] of slot s is T[s] — both partner reads (forward, update) are contiguous;
+//   * 32-bit slot byte offsets (tables < 4 GiB) from one uniform base;
+//   * x_a * x_b per slot cached in a register for the forward and the update.
+// Arithmetic order matches the CPU engine up to fp32 contraction / dot2 association.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 bf2_to_f2(uint32_t u) {
+    return f2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+}
+
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+    bf16x2_t va, vb;
+    __builtin_memcpy(&va, &a, 4);
+    __builtin_memcpy(&vb, &b, 4);
+    return __builtin_amdgcn_fdot2_f32_bf16(va, vb, c, false);
+}
+
+// Two floats -> bf16x2 with stochastic rounding; ra / rb are used as is (the instruction adds
+// the HIGH 16 bits of its random operand, see hm::pack_bf16x2_sr).
+__device__ __forceinline__ uint32_t pack_sr_hi(f2 v, uint32_t ra, uint32_t rb) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+    bf16x2_t o = __builtin_bit_cast(bf16x2_t, ra);   // both halves are overwritten
+    o = __builtin_amdgcn_cvt_sr_bf16_f32(o, v.x, ra, false);
+    o = __builtin_amdgcn_cvt_sr_bf16_f32(o, v.y, rb, true);
+    uint32_t u;
+    __builtin_memcpy(&u, &o, 4);
+    return u;
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+
+template <bool BF>
+struct LeanIO {
+    // raw slot: bf16 -> uint4 {v01, v23, g01, g23}; fp32 -> V float4 + G float4
+    using Raw = typename std::conditional<BF, uint4, float4[2]>::type;
+    using Img = typename std::conditional<BF, uint2, float4>::type;   // V in the LDS image
+};
+
+template <bool BF, int NS>
+__global__ __launch_bounds__(256) void ffm_lean_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
+    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    using Img = typename LeanIO<BF>::Img;
+    constexpr uint32_t SLOT_B = BF ? 16u : 32u;          // bytes per packed slot
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int F = P.F;
+    const int FF = F * F;
+    Img* s_t = reinterpret_cast<Img*>(smem);                                     // FF (transposed)
+    int4* s_m = reinterpret_cast<int4*>(smem + (size_t)FF * sizeof(Img));      // F x {i, f, x, -}
+    float* s_red = reinterpret_cast<float*>(s_m + F);                           // 16
+    const int tid = threadIdx.x;
+    const uint32_t nfld = (uint32_t)P.fstride;
+    char* vg = reinterpret_cast<char*>(VG);
+
+    // row-invariant slot decode; slots past F*F become (0, 0): a diagonal slot, i.e. dead
+    int sa[NS], sb[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        sa[j] = s < FF ? s / F : 0;
+        sb[j] = s < FF ? s % F : 0;
+    }
+    const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
+
+    for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
+        // ---- row metadata -> LDS {i, f, x}; instance-wise L2 norm (the block sum's barrier
+        //      publishes s_m).  Padding / out-of-range entries get i = -1, x = 0. ----
+        float sq = 0.f;
+        int mi = -1;
+        float mx = 0.f;
+        if (tid < F) {
+            const size_t o = (size_t)row * F + tid;
+            int i = idx[o];
+            int f = fld ? fld[o] : tid;
+            float x = val ? val[o] : 1.f;
+            if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; f = 0; }
+            s_m[tid] = make_int4(i, f, __float_as_int(x), 0);
+            mi = i;
+            mx = x;
+            sq = x * x;
+        }
+        float scale = 1.f;
+        if (P.norm) {
+            const float tot = hm::block_sum(sq, s_red);
+            scale = tot > 0.f ? rsqrtf(tot) : 1.f;
+        } else {
+            __syncthreads();
+        }
+        float lw = 0.f;
+        if (P.use_linear && mi >= 0) lw = w[mi];
+
+        // ---- gather (branch-free): own raw slot -> registers, own V -> transposed LDS image.
+        //      Dead slots (a == b, padding) load slot 0 and get x_a x_b = 0. ----
+        uint4 q[NS];
+        float4 qv[NS], qg[NS];
+        uint32_t off[NS];
+        float xab[NS];
+        bool live[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int4 ma = s_m[sa[j]], mb = s_m[sb[j]];
+            live[j] = sa[j] != sb[j] && ma.x >= 0 && mb.x >= 0;
+            off[j] = live[j] ? ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * SLOT_B : 0u;
+            xab[j] = live[j] ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+            if constexpr (BF) {
+                q[j] = *reinterpret_cast<const uint4*>(vg + off[j]);
+                s_t[sb[j] * F + sa[j]] = make_uint2(q[j].x, q[j].y);
+            } else {
+                qv[j] = *reinterpret_cast<const float4*>(vg + off[j]);
+                qg[j] = *reinterpret_cast<const float4*>(vg + off[j] + 16u);
+                s_t[sb[j] * F + sa[j]] = qv[j];
+            }
+        }
+        __syncthreads();
+
+        // ---- forward: every slot (a, b) adds its pair dot weighted by x_a x_b (0 if dead); the
+        //      sum over ordered pairs counts each unordered pair twice -> halved ----
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int s = tid + j * 256;
+            float d;
+            if constexpr (BF) {
+                const uint2 pv = s_t[s < FF ? s : 0];
+                d = dot2_bf16(q[j].x, pv.x, dot2_bf16(q[j].y, pv.y, 0.f));
+            } else {
+                const float4 pv = s_t[s < FF ? s : 0];
+                d = qv[j].x * pv.x + qv[j].y * pv.y + qv[j].z * pv.z + qv[j].w * pv.w;
+            }
+            part += d * xab[j];
+        }
+        part *= 0.5f * scale * scale;
+        part += lw * mx * scale;                       // mx = 0 for tid >= F / padding
+        float p = hm::block_sum(part, s_red);
+        if (P.use_bias) p += bias[0];
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- AdaGrad(V) update (Hogwild), packed fp32 math; only the store is predicated ----
+        if (P.train) {
+            float lz = 0.f, ln = 0.f;
+            if (P.use_linear && mi >= 0) { lz = wz[mi]; ln = wn[mi]; }
+            const float ks = kappa * scale * scale;
+            const f2 lam = {P.lambda_v, P.lambda_v}, eps = {P.eps, P.eps};
+            const f2 meta = {-P.eta0, -P.eta0};
+            const uint32_t hrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const int s = tid + j * 256;
+                const f2 coef = {ks * xab[j], ks * xab[j]};
+                f2 o0, o1, g0, g1, p0, p1;
+                if constexpr (BF) {
+                    const uint2 pv = s_t[s < FF ? s : 0];
+                    o0 = bf2_to_f2(q[j].x); o1 = bf2_to_f2(q[j].y);
+                    g0 = bf2_to_f2(q[j].z); g1 = bf2_to_f2(q[j].w);
+                    p0 = bf2_to_f2(pv.x);   p1 = bf2_to_f2(pv.y);
+                } else {
+                    const float4 pv = s_t[s < FF ? s : 0];
+                    o0 = f2{qv[j].x, qv[j].y}; o1 = f2{qv[j].z, qv[j].w};
+                    g0 = f2{qg[j].x, qg[j].y}; g1 = f2{qg[j].z, qg[j].w};
+                    p0 = f2{pv.x, pv.y};       p1 = f2{pv.z, pv.w};
+                }
+                const f2 d0 = coef * p0 + lam * o0, d1 = coef * p1 + lam * o1;
+                g0 = g0 + d0 * d0;
+                g1 = g1 + d1 * d1;
+                const f2 t0 = g0 + eps, t1 = g1 + eps;
+                const f2 r0 = {__builtin_amdgcn_rsqf(t0.x), __builtin_amdgcn_rsqf(t0.y)};
+                const f2 r1 = {__builtin_amdgcn_rsqf(t1.x), __builtin_amdgcn_rsqf(t1.y)};
+                o0 = o0 + meta * d0 * r0;
+                o1 = o1 + meta * d1 * r1;
+                if constexpr (BF) {
+                    // one hash per slot, full-rate 24-bit multiply; 8 rotated 16-bit windows
+                    uint32_t h = hrow + tid_h + (uint32_t)j * 0x6A09E667u;
+                    h ^= h >> 16;
+                    h = __umul24(h, 0x2C1B3Du) ^ (h >> 11);
+                    h ^= h >> 15;
+                    const uint4 st = make_uint4(pack_sr_hi(o0, h, rotl32(h, 16)),
+                                                pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
+                                                pack_sr_hi(g0, rotl32(h, 4), rotl32(h, 20)),
+                                                pack_sr_hi(g1, rotl32(h, 12), rotl32(h, 28)));
+                    if (live[j]) *reinterpret_cast<uint4*>(vg + off[j]) = st;
+                } else {
+                    if (live[j]) {
+                        *reinterpret_cast<float4*>(vg + off[j]) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                        *reinterpret_cast<float4*>(vg + off[j] + 16u) = make_float4(g0.x, g0.y, g1.x, g1.y);
+                    }
+                }
+            }
+            if (P.use_linear && mi >= 0) {
+                const float g = kappa * mx * scale;
+                const float n1 = ln + g * g;
+                const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                wz[mi] = z1;
+                wn[mi] = n1;
+                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+            }
+            if (P.use_bias && tid == 0)
+                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined kernel (bf16 packed V|G, K <= 4): the next row's 1,482 slot gathers fly into LDS by
+// LDS-DMA (global_load_lds_dwordx4: no VGPR destination) while the current row computes.
+//
+// The lean kernel above still waits on two dependent global round trips per row (row metadata,
+// then the slot gather) with nothing else to do: per CU only ~4 rows' gathers are ever in flight,
+// and only during their gather phase (HBM-side 3.7-3.9 TB/s).  Here a block's loop iteration
+// for row r is
+//   A  wait for DMA(r) (own wave: vmcnt(0)), barrier
+//   B  own raw slots LDS -> registers, own V -> transposed image T; publish meta(r+G) (loaded
+//      into registers one iteration earlier) and its L2-norm scale; barrier
+//   C  issue DMA(r+G) from meta(r+G) (offsets, x_a x_b, linear-term ids kept in registers);
+//      issue the loads of meta(r+2G)
+//   D  forward(r), block sum (raw s_barrier: a __syncthreads() fence would drain the DMA)
+//   E  AdaGrad / FTRL updates of r (stores)
+//   F  load w, z, n of r+G's linear terms (after E's stores: same-thread order keeps the FTRL
+//      read-modify-write of a feature shared by consecutive rows exact)
+// so each block keeps one row's 24 KB gather in flight behind its compute (4 blocks/CU: ~96 KB
+// in flight per CU).  Staleness: row r+G's slots are read before row r's updates land — the
+// same one-row Hogwild window the other ~1,000 rows in flight already impose.
+__device__ __forceinline__ void bar_raw() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_s_barrier();
+    __asm__ __volatile__("" ::: "memory");
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
+    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256];   // slot DMA landing zone
+    __shared__ __attribute__((aligned(16))) uint2 s_t[NS * 256];     // transposed V image
+    // F <= 45 (F*F <= 2048): per-field arrays of 48; total LDS 40,736 B at NS = 6 -> 4 blocks/CU
+    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
+    __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
+    __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
+    __shared__ float s_red[8];                                        // [0..3] sums, [4+b] scale
+    const int F = P.F;
+    const int FF = F * F;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // per-row bookkeeping is spread over the waves so no wave works alone before a barrier:
+    // wave 1 validates / publishes meta, wave 2 owns the linear (FTRL) terms, wave 3 DMAs meta
+    constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
+    const uint32_t nfld = (uint32_t)P.fstride;
+    const int G = gridDim.x;
+    char* vg = reinterpret_cast<char*>(VG);
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef const __attribute__((address_space(1))) void* glb_ptr_t;
+
+    // row-invariant slot decode, packed a | b << 8 (one register per slot; F <= 45)
+    int ab[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
+    }
+#define SA(j) (ab[j] & 0xFF)
+#define SB(j) (ab[j] >> 8)
+    const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
+    if (wave == W_LIN && lane < 48) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { s_lin[0][k][lane] = 0.f; s_lin[1][k][lane] = 0.f; }
+    }
+
+    // wave W_DMA, lanes < F: DMA of one row's raw meta into s_mr[bf] (no registers held)
+    auto dma_meta = [&](int bf, int row) {
+        if (wave == W_DMA && lane < F && row < P.B) {
+            const size_t o = (size_t)row * F + lane;
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(idx + o), (lds_ptr_t)&s_mr[bf][0][0], 4, 0, 0);
+            if (fld) __builtin_amdgcn_global_load_lds((glb_ptr_t)(fld + o), (lds_ptr_t)&s_mr[bf][1][0], 4, 0, 0);
+            if (val) __builtin_amdgcn_global_load_lds((glb_ptr_t)(val + o), (lds_ptr_t)&s_mr[bf][2][0], 4, 0, 0);
+        }
+    };
+    // wave W_META: raw meta of buffer bf (landed) -> validated s_m[bf] + the L2-norm scale
+    auto publish_meta = [&](int bf) {
+        if (wave == W_META) {
+            float sq = 0.f;
+            if (lane < F) {
+                int ri = s_mr[bf][0][lane];
+                int rf = fld ? s_mr[bf][1][lane] : lane;
+                float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
+                if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
+                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
+                sq = rx * rx;
+            }
+            const float tot = hm::wave_sum(sq);
+            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+        }
+    };
+    // slot j of the row in buffer bf: byte offset, x_a x_b; returns 1 = live (updated),
+    // 2 = diagonal (a == b: written back unchanged, so a row rewrites whole 128-B lines of its
+    // features' line-padded blocks), 0 = dead (padding, past F*F)
+    auto slot = [&](int bf, int j, uint32_t& off, float& xab) -> uint32_t {
+        const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
+        const bool ok = ma.x >= 0 && mb.x >= 0 && tid + j * 256 < FF;
+        const bool live = ok && SA(j) != SB(j);
+        off = ok ? ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * 16u : 0u;
+        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+        return live ? 1u : (ok ? 2u : 0u);
+    };
+    // DMA of the slots of the row in buffer bf (dead slots fetch slot 0; never read back)
+    auto dma_slots = [&](int bf) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t off;
+            float xab;
+            slot(bf, j, off, xab);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + off),
+                                             (lds_ptr_t)(s_raw + j * 256 + wave * 64), 16, 0, 0);
+        }
+    };
+    // wave W_LIN, lanes < F with a valid feature: DMA of w, z, n of the row in buffer bf
+    // (issued after this wave's FTRL stores: same-wave order keeps a shared feature's update exact)
+    auto dma_lin = [&](int bf) {
+        if (P.use_linear && wave == W_LIN && lane < F) {
+            const int i = s_m[bf][lane].x;
+            if (i >= 0) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                if (P.train) {
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                }
+            }
+        }
+    };
+
+    int row = blockIdx.x;
+    if (row >= P.B) return;
+    // ---- prologue: meta(row) -> s_m[0]; DMA of its slots and linear state; meta(row + G) ----
+    dma_meta(0, row);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    bar_raw();
+    publish_meta(0);
+    bar_raw();
+    dma_slots(0);
+    dma_lin(0);
+    dma_meta(1, row + G);
+
+    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
+        const int nxt = cur ^ 1;
+        const bool more = row + G < P.B;
+
+        // ---- A: every DMA of this wave has landed (slots + lin of this row, meta of the
+        //      next), then every wave's ----
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+        bar_raw();
+        // ---- B: raw -> registers, V -> transposed image; meta(row + G) -> s_m[nxt] ----
+        uint4 q[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            q[j] = s_raw[j * 256 + tid];
+            s_t[SB(j) * F + SA(j)] = make_uint2(q[j].x, q[j].y);
+        }
+        uint32_t off[NS];
+        float xab[NS];
+        uint32_t live = 0u, wr = 0u;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const uint32_t k = slot(cur, j, off[j], xab[j]);
+            live |= (k & 1u) << j;
+            wr |= (uint32_t)(k != 0u) << j;
+        }
+        if (more) publish_meta(nxt);
+        bar_raw();
+        // ---- C: next row's slot DMA, then the raw meta of the row after it ----
+        if (more) {
+            dma_slots(nxt);
+            dma_meta(cur, row + 2 * G);    // s_mr[cur] was consumed at this row's B
+        }
+        const float scale = s_red[4 + cur];
+        int mi = -1;
+        float mx = 0.f, lw = 0.f;
+        if (wave == W_LIN && lane < F) {
+            const int4 m = s_m[cur][lane];
+            mi = m.x;
+            mx = __int_as_float(m.z);
+            lw = s_lin[cur][0][lane];
+        }
+        // ---- D: forward ----
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int s = tid + j * 256;
+            const uint2 pv = s_t[s < FF ? s : 0];
+            const float d = dot2_bf16(q[j].x, pv.x, dot2_bf16(q[j].y, pv.y, 0.f));
+            part += d * xab[j];
+        }
+        part *= 0.5f * scale * scale;
+        part += lw * mx * scale;
+        part = hm::wave_sum(part);
+        if ((tid & 63) == 0) s_red[wave] = part;
+        bar_raw();
+        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        if (P.use_bias) p += bias[0];
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- E: updates ----
+        if (P.train) {
+            const float ks = kappa * scale * scale;
+            const f2 eps = {P.eps, P.eps};
+            const f2 meta = {-P.eta0, -P.eta0};
+            uint32_t hrow = (P.seed ^ ((uint32_t)row * 0x85EBCA77u)) + tid_h;
+            hrow ^= hrow >> 16;
+            hrow *= 0x7FEB352Du;
+            hrow ^= hrow >> 15;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const int s = tid + j * 256;
+                const f2 coef = {ks * xab[j], ks * xab[j]};
+                const uint2 pv = s_t[s < FF ? s : 0];
+                f2 o0 = bf2_to_f2(q[j].x), o1 = bf2_to_f2(q[j].y);
+                f2 g0 = bf2_to_f2(q[j].z), g1 = bf2_to_f2(q[j].w);
+                const f2 p0 = bf2_to_f2(pv.x), p1 = bf2_to_f2(pv.y);
+                // diagonal slots: coef = 0 and lambda = 0 -> d = 0, V and G unchanged, and the
+                // stochastic rounding of a value already in bf16 is exact
+                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
+                const f2 lamj = {lj, lj};
+                const f2 d0 = coef * p0 + lamj * o0, d1 = coef * p1 + lamj * o1;
+                g0 = g0 + d0 * d0;
+                g1 = g1 + d1 * d1;
+                const f2 t0 = g0 + eps, t1 = g1 + eps;
+                const f2 r0 = {__builtin_amdgcn_rsqf(t0.x), __builtin_amdgcn_rsqf(t0.y)};
+                const f2 r1 = {__builtin_amdgcn_rsqf(t1.x), __builtin_amdgcn_rsqf(t1.y)};
+                o0 = o0 + meta * d0 * r0;
+                o1 = o1 + meta * d1 * r1;
+                // this thread's row hash, re-keyed per slot: each 16-bit window stays uniform
+                const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
+                const uint4 st = make_uint4(pack_sr_hi(o0, h, rotl32(h, 16)),
+                                            pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
+                                            pack_sr_hi(g0, rotl32(h, 4), rotl32(h, 20)),
+                                            pack_sr_hi(g1, rotl32(h, 12), rotl32(h, 28)));
+                if (wr >> j & 1u) *reinterpret_cast<uint4*>(vg + off[j]) = st;
+            }
+            if (mi >= 0) {
+                // the feature block's pad slots (never read): zeros, completing its last line
+                for (int f = P.num_fields; f < (int)nfld; ++f)
+                    *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * 16u) = make_uint4(0u, 0u, 0u, 0u);
+                if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
+                    const float lz = s_lin[cur][1][lane], ln = s_lin[cur][2][lane];
+                    const float g = kappa * mx * scale;
+                    const float n1 = ln + g * g;
+                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                    wz[mi] = z1;
+                    wn[mi] = n1;
+                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                }
+            }
+            if (P.use_bias && tid == 0)
+                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+        }
+        // ---- F: linear state of the next row (after this row's FTRL stores) ----
+        if (more) dma_lin(nxt);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
+#undef SA
+#undef SB
+}
+
+int default_blocks(int B, int grid);
+
+// Lean dispatch (Kp == 4, packed, table < 4 GiB, F*F <= 2048); -1 when the shape needs another kernel.
+template <bool BF>
+int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                  float* pred, float* loss, int grid, int variant, hipStream_t stream) {
+    const size_t slot_b = BF ? 16 : 32;
+    if (P.Kp != 4 || P.F > 45) return -1;
+    if ((size_t)P.num_features * (size_t)P.fstride * slot_b >= ((size_t)1 << 32)) return -1;
+    const size_t meta = (size_t)P.F * 16 + 16 * 4;
+    const size_t sh = (size_t)P.F * P.F * (BF ? 8 : 16) + meta;
+    const int need = (P.F * P.F + 255) / 256;
+    const int blocks = default_blocks(P.B, grid);
+    if (blocks <= 0) return 0;
+    if constexpr (BF) {
+        if (variant == 0) {   // LDS-DMA pipelined kernel (static LDS)
+#define HM_PIPE(NSV)                                                                                \
+    hipLaunchKernelGGL((ffm_pipe_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, fld, val, \
+                       y, VG, w, wz, wn, bias, pred, loss)
+            if (need <= 2) HM_PIPE(2);
+            else if (need <= 4) HM_PIPE(4);
+            else if (need <= 6) HM_PIPE(6);
+            else HM_PIPE(8);
+#undef HM_PIPE
+            HM_LAUNCH_RET();
+        }
+    }
+#define HM_LEAN(NSV)                                                                                \
+    hipLaunchKernelGGL((ffm_lean_kernel<BF, NSV>), dim3(blocks), dim3(256), sh, stream, P, idx, fld, \
+                       val, y, VG, w, wz, wn, bias, pred, loss)
+    if (need <= 2) HM_LEAN(2);
+    else if (need <= 4) HM_LEAN(4);
+    else if (need <= 6) HM_LEAN(6);
+    else HM_LEAN(8);
+#undef HM_LEAN
+    HM_LAUNCH_RET();
+}
+
 int default_blocks(int B, int grid) {
     return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
 }
@@ -616,9 +1138,13 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
 template <bool BF>
 int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
-             float* pred, float* loss, int grid, int packed, hipStream_t stream) {
+             float* pred, float* loss, int grid, int packed, int variant, hipStream_t stream) {
     if (packed) {
         int rc = -1;
+        if (variant == 0 || variant == 2) {
+            rc = dispatch_lean<BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
+            if (rc != -1) return rc;
+        }
         if (P.Kp == 4) rc = dispatch_packed<1, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
         else if (P.Kp == 8) rc = dispatch_packed<2, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
         if (rc != -1) return rc;
@@ -638,7 +1164,9 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload, bf16_state, seed, packed
+//                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride
+// variant (Kp == 4, packed, F <= 45, table < 4 GiB): 0 = auto (bf16: ffm_pipe_kernel, fp32:
+// ffm_lean_kernel), 1 = ffm_packed_kernel (round 1), 2 = ffm_lean_kernel (A/B)
 // packed = 1: V and G are the two halves of one [num_features][num_fields][2][Kp] table
 //             (G == V + Kp elements, slot stride 2*Kp); 0: separate [.][.][Kp] tables.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
@@ -653,7 +1181,10 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     const int bf16 = ip[12];
     P.seed = (uint32_t)ip[13];
     const int packed = ip[14];
+    const int variant = ip[15];
     P.sstride = packed ? 2 * P.Kp : P.Kp;
+    P.fstride = ip[16] > 0 ? ip[16] : P.num_fields;
+    if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
@@ -663,8 +1194,8 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
         if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.Kp * es)
             return (int)hipErrorInvalidValue;
         // 32-bit slot indices in the packed kernel
-        if ((size_t)P.num_features * (size_t)P.num_fields >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
+        if ((size_t)P.num_features * (size_t)P.fstride >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
     }
-    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, stream)
-                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, stream);
+    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, variant, stream)
+                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, variant, stream);
 }

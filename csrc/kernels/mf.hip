@@ -32,7 +32,13 @@ struct MFParams {
     int loss;                  // BPR: 0 lnLogistic, 1 logistic, 2 sigmoid
     uint32_t seed;
     int max_tries;             // negative-sampling rejection tries
+    int coherent;              // 1: factor/bias/state loads bypass L1 (hm::ld_coherent)
 };
+
+// Shared-model load: L1-bypassing unless disabled for an A/B (HM_MF_PLAIN_LOADS=1).
+__device__ __forceinline__ float ldm(const MFParams& P, const float* p) {
+    return P.coherent ? hm::ld_coherent(p) : *p;
+}
 
 __device__ __forceinline__ float eta_t(const MFParams& P, float t) {
     if (P.eta_kind == 0) return P.eta0;
@@ -72,11 +78,11 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
         const bool fa = ok && f < P.k;
         float pu = 0.f, qi = 0.f;
         const size_t ou = (size_t)(ok ? u : 0) * P.kp + f, oi = (size_t)(ok ? i : 0) * P.kp + f;
-        if (fa) { pu = Pu[ou]; qi = Qi[oi]; }
+        if (fa) { pu = ldm(P, Pu + ou); qi = ldm(P, Qi + oi); }
         float dot = group_sum<G>(pu * qi);
         float bu = 0.f, bi = 0.f;
-        if (ok && P.use_bias) { bu = Bu[u]; bi = Bi[i]; }
-        const float m = *mu;
+        if (ok && P.use_bias) { bu = ldm(P, Bu + u); bi = ldm(P, Bi + i); }
+        const float m = ldm(P, mu);
         const float rhat = m + bu + bi + dot;
         const float rr = act ? ratings[r] : 0.f;
         const float e = rr - rhat;
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
         } else {
             if (fa) {
                 const float gp = e * qi - P.lambda_u * pu, gq = e * pu - P.lambda_i * qi;
-                const float Gp = GPu[ou] + gp * gp, Gq = GQi[oi] + gq * gq;
+                const float Gp = ldm(P, GPu + ou) + gp * gp, Gq = ldm(P, GQi + oi) + gq * gq;
                 GPu[ou] = Gp;
                 GQi[oi] = Gq;
                 Pu[ou] = pu + P.eta0 * gp * rsqrtf(P.eps + Gp);
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
             }
             if (P.use_bias && f == 0) {
                 const float gbu = e - P.lambda_b * bu, gbi = e - P.lambda_b * bi;
-                const float Gu = GBu[u] + gbu * gbu, Gi = GBi[i] + gbi * gbi;
+                const float Gu = ldm(P, GBu + u) + gbu * gbu, Gi = ldm(P, GBi + i) + gbi * gbi;
                 GBu[u] = Gu;
                 GBi[i] = Gi;
                 Bu[u] = bu + P.eta0 * gbu * rsqrtf(P.eps + Gu);
@@ -183,10 +189,10 @@ __global__ __launch_bounds__(256) void bpr_kernel(MFParams P, const int32_t* __r
         const size_t ou = (size_t)(ok ? u : 0) * P.kp + f;
         const size_t oi = (size_t)(ok ? i : 0) * P.kp + f, oj = (size_t)(ok ? j : 0) * P.kp + f;
         float pu = 0.f, qi = 0.f, qj = 0.f;
-        if (fa) { pu = Pu[ou]; qi = Qi[oi]; qj = Qi[oj]; }
+        if (fa) { pu = ldm(P, Pu + ou); qi = ldm(P, Qi + oi); qj = ldm(P, Qi + oj); }
         const float d = group_sum<G>(pu * (qi - qj));
         float bi = 0.f, bj = 0.f;
-        if (ok && P.use_bias) { bi = Bi[i]; bj = Bi[j]; }
+        if (ok && P.use_bias) { bi = ldm(P, Bi + i); bj = ldm(P, Bi + j); }
         const float x = bi - bj + d;
         float z;
         if (P.loss == 2) { const float s = hm::sigmoidf_(x); z = s * (1.f - s); }   // sigmoid
@@ -215,6 +221,7 @@ MFParams unpack(const int32_t* ip, const float* hp) {
     P.k = ip[0]; P.kp = ip[1]; P.n_users = ip[2]; P.n_items = ip[3]; P.adagrad = ip[4];
     P.use_bias = ip[5]; P.update_mean = ip[6]; P.eta_kind = ip[7]; P.loss = ip[8];
     P.seed = (uint32_t)ip[9]; P.max_tries = ip[10] > 0 ? ip[10] : 16;
+    P.coherent = ip[12] == 0;  // ip[12] = 1: plain (L1-cached) loads, A/B only
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda_u = hp[3];
     P.lambda_i = hp[4]; P.lambda_j = hp[5]; P.lambda_b = hp[6]; P.eps = hp[7];
     return P;
@@ -235,7 +242,8 @@ int grid_for(int64_t n, int per) {
 
 }  // namespace
 
-// ip: k, kp, n_users, n_items, adagrad, use_bias, update_mean, eta_kind, loss, seed, max_tries
+// ip: k, kp, n_users, n_items, adagrad, use_bias, update_mean, eta_kind, loss, seed, max_tries,
+//     grid, plain_loads
 // hp: eta0, power_t, total_steps, lambda_u, lambda_i, lambda_j, lambda_b, eps
 HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
                       const int32_t* items, const float* ratings, int64_t n, int64_t t0, float* Pu,

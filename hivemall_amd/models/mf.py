@@ -20,6 +20,7 @@ one row per index that is a user and/or an item (NULL where it is not).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import pandas as pd
@@ -124,7 +125,8 @@ class _MFBase(Learner):
             raise UDFArgumentException(f"{self.NAME}: unknown -eta {eta}")
         return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
-                         self._grid()], dtype=np.int32)
+                         self._grid(), int(os.environ.get("HM_MF_PLAIN_LOADS", "0") == "1")],
+                        dtype=np.int32)
 
     # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
     # keeps 256: on a small catalogue, concurrent stale updates slow the escape from the

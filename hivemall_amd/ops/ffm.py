@@ -4,6 +4,7 @@ Kernel: ``csrc/kernels/ffm.hip`` (hm_ffm_step).  CPU twin: ``csrc/host/ffm_cpu.c
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -39,25 +40,47 @@ class FFMHyper:
 
 
 _CALLS = 0  # per-launch counter mixed into the stochastic-rounding seed
+# kernel variant (A/B only), K <= 4 packed: 0 = auto (bf16 state: LDS-DMA pipelined
+# ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the round-1 ffm_packed_kernel, 2 = ffm_lean_kernel
+_VARIANT = int(os.environ.get("HM_FFM_VARIANT", "0"))
 
 
 def is_packed(V: torch.Tensor, G: torch.Tensor) -> bool:
-    """True when V and G are the two halves of one [NF, NFLD, 2, Kp] table (the packed slot
-    layout of csrc/kernels/ffm.hip: one 16-B access moves a slot's V and G)."""
+    """True when V and G are the two halves of one [NF, FS, 2, Kp] table, FS >= NFLD (the packed
+    slot layout of csrc/kernels/ffm.hip: one 16-B access moves a slot's V and G)."""
     if V.dim() != 3 or G.shape != V.shape or G.dtype != V.dtype or G.device != V.device:
         return False
     _, NFLD, Kp = V.shape
-    st = (NFLD * 2 * Kp, 2 * Kp, 1)
-    return (V.stride() == st and G.stride() == st
+    fs = V.stride(0) // (2 * Kp)
+    st = (fs * 2 * Kp, 2 * Kp, 1)
+    return (fs >= NFLD and V.stride() == st and G.stride() == st
             and G.data_ptr() == V.data_ptr() + Kp * V.element_size())
+
+
+def field_stride(V: torch.Tensor) -> int:
+    """Slots between consecutive features of the V table (NFLD, or the padded FS)."""
+    return V.stride(0) // V.stride(1) if V.dim() == 3 and V.stride(1) > 0 else V.shape[1]
+
+
+def padded_fields(num_fields: int, kp: int, dtype) -> int:
+    """Field count of a packed table padded so every feature block is whole 128-B lines (39
+    fields of 16-B bf16 slots -> 40 = 640 B = 5 lines).  Measured on MI355X with the bench's
+    access pattern (benchmarks/ffm_mem_roofline.py, profiles/ffm_roofline_r2.log): gather +
+    write-back of the row's slots 127M rows/s unaligned -> 141M aligned -> 146M aligned with the
+    whole block written (diagonal + pad slots)."""
+    slot_b = 2 * kp * torch.empty(0, dtype=dtype).element_size()
+    per_line = max(1, 128 // slot_b) if 128 % slot_b == 0 else 1
+    return (num_fields + per_line - 1) // per_line * per_line
 
 
 def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
                      packed: bool) -> tuple[torch.Tensor, torch.Tensor]:
-    """Zeroed (V, G): views of one packed [NF, NFLD, 2, Kp] table, or two split tables."""
+    """Zeroed (V, G): views of one packed [NF, FS, 2, Kp] table (FS = line-padded field count),
+    or two split tables."""
     if packed:
-        VG = torch.zeros((num_features, num_fields, 2, kp), dtype=dtype, device=device)
-        return VG[:, :, 0, :], VG[:, :, 1, :]
+        fs = padded_fields(num_fields, kp, dtype)
+        VG = torch.zeros((num_features, fs, 2, kp), dtype=dtype, device=device)
+        return VG[:, :num_fields, 0, :], VG[:, :num_fields, 1, :]
     shape = (num_features, num_fields, kp)
     return (torch.zeros(shape, dtype=dtype, device=device),
             torch.zeros(shape, dtype=dtype, device=device))
@@ -104,7 +127,9 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
                    int(hyper.use_bias), int(hyper.norm), int(grid),
                    int((not packed) if hyper.reload is None else hyper.reload), int(bf16),
-                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed)], dtype=np.int32)
+                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed), _VARIANT,
+                   field_stride(V)],
+                  dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
     args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(G),
