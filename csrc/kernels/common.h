@@ -31,6 +31,23 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, HM_WAVE);
     return v;
 }
+// Full-wave sum on DPP lane permutes (quad_perm x2, row half-mirror, row mirror, row_bcast15,
+// row_bcast31), total read from lane 63 -> a wave-uniform value.  ~8 instructions against ~36 for
+// the ds_bpermute butterfly of __shfl_xor.  EXEC must be full.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_take(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_uniform(float v) {
+    v += dpp_take<0xB1>(v);          // quad_perm [1,0,3,2]
+    v += dpp_take<0x4E>(v);          // quad_perm [2,3,0,1]
+    v += dpp_take<0x141>(v);         // row_half_mirror
+    v += dpp_take<0x140>(v);         // row_mirror
+    v += dpp_take<0x142, 0xA>(v);    // row_bcast:15 into rows 1, 3
+    v += dpp_take<0x143, 0xC>(v);    // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, HM_WAVE));

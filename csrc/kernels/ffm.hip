@@ -859,7 +859,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
                 sq = rx * rx;
             }
-            const float tot = hm::wave_sum(sq);
+            const float tot = hm::wave_sum_uniform(sq);
             if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
         }
     };
@@ -868,10 +868,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     // features' line-padded blocks), 0 = dead (padding, past F*F)
     auto slot = [&](int bf, int j, uint32_t& off, float& xab) -> uint32_t {
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
-        const bool ok = ma.x >= 0 && mb.x >= 0 && tid + j * 256 < FF;
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
         const bool live = ok && SA(j) != SB(j);
-        off = ok ? ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * 16u : 0u;
-        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+        const uint32_t o = ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * 16u;   // branch-free
+        const float x = __int_as_float(ma.z) * __int_as_float(mb.z);
+        off = ok ? o : 0u;
+        xab = live ? x : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
     // DMA of the slots of the row in buffer bf (dead slots fetch slot 0; never read back)
@@ -963,8 +965,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         }
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;
-        part = hm::wave_sum(part);
-        if ((tid & 63) == 0) s_red[wave] = part;
+        part = hm::wave_sum_uniform(part);
+        if (lane == 0) s_red[wave] = part;
         bar_raw();
         float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
         if (P.use_bias) p += bias[0];

@@ -135,7 +135,8 @@ _SST_OPTS = Options([
     opt("r", "n_component", 3, int, "Rank of the past subspace"),
     opt("k", "n_dim", 5, int, "Rank of the current subspace"),
     opt("th", "threshold", -1.0, float, "Change-point threshold"),
-    flag("ika", None, "Use the implicit Krylov approximation (accepted; SVD is used)")], "sst")
+    flag("ika", None, "Use the implicit Krylov approximation",
+         inert="SST uses an exact (batched) SVD")], "sst")
 
 
 @udf("sst", vectorized=True)

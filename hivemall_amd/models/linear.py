@@ -33,16 +33,21 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import ConversionState, Learner, log
 
 # ------------------------------------------------------------------ option specs
+_MIX_INERT = ("mixing is a collective between the job's ranks over RCCL (-mix_interval), "
+              "there is no MixServer")
+_SCALE_INERT = "AdaGrad accumulators are fp32 (no half-float scaling)"
 LEARNER_BASE_OPTS = [
-    flag("dense", "densemodel", "Use a dense model (always dense on the device; accepted)"),
+    flag("dense", "densemodel", "Use a dense model",
+         inert="models are always dense tables on the device"),
     opt("dims", "feature_dimensions", -1, int, "Dimension of the model (default: max index + 1)"),
-    flag("disable_halffloat", None, "Accepted for compatibility (models are fp32)"),
+    flag("disable_halffloat", None, "Disable half-float weights",
+         inert="linear models are fp32"),
     opt("mini_batch", "mini_batch_size", 1, int, "Mini-batch size (general learners)"),
-    opt("mix", "mix_servers", None, str, "Mixing: on this engine replicas/ranks are mixed over RCCL"),
-    opt("mix_session", "mix_session_name", None, str, "Accepted for compatibility"),
-    opt("mix_threshold", None, 3, int, "Accepted for compatibility"),
-    flag("mix_cancel", "enable_mix_canceling", "Accepted for compatibility"),
-    flag("ssl", None, "Accepted for compatibility"),
+    opt("mix", "mix_servers", None, str, "MixServer addresses", inert=_MIX_INERT),
+    opt("mix_session", "mix_session_name", None, str, "MixServer session", inert=_MIX_INERT),
+    opt("mix_threshold", None, 3, int, "MixServer update threshold", inert=_MIX_INERT),
+    flag("mix_cancel", "enable_mix_canceling", "MixServer cancel", inert=_MIX_INERT),
+    flag("ssl", None, "MixServer SSL", inert=_MIX_INERT),
     opt("loadmodel", None, None, str, "Warm start: path of a model table (TSV/CSV/parquet)"),
     opt("iters", "iterations", 1, int, "The maximum number of iterations (epochs)", aliases=("iter",)),
     opt("cv_rate", "convergence_rate", 0.005, float, "Threshold to determine convergence"),
@@ -68,7 +73,7 @@ GENERAL_OPTS = [
     opt("decay", None, 0.95, float, "RMSprop decay"),
     opt("rho", None, 0.95, float, "AdaDelta decay"),
     opt("beta", None, 1e-6, float, "AdamHD hyper-gradient step"),
-    opt("scale", None, 100.0, float, "Scaling factor (accepted; fp32 accumulators)"),
+    opt("scale", None, 100.0, float, "Scaling factor", inert=_SCALE_INERT),
     flag("amsgrad", None, "AMSGrad variant of Adam"),
     flag("inspect_opts", None, "Show the resolved options and raise"),
     opt("quantile_tau", "tau", 0.5, float, "Quantile loss tau"),
@@ -410,7 +415,7 @@ TrainSCW2 = _learner("train_scw2", "scw2", "binary", [_PHI, _ETA_CONF, _C], doc=
 TrainAdaGradRDA = _learner("train_adagrad_rda", "adagrad_rda", "binary", [
     opt("eta", "eta0", 0.1, float, "Learning rate"),
     opt("lambda", None, 1e-6, float, "Regularization (RDA L1)"),
-    opt("scale", None, 100.0, float, "Scaling factor (accepted)")], doc="AdaGrad-RDA hinge")
+    opt("scale", None, 100.0, float, "Scaling factor", inert=_SCALE_INERT)], doc="AdaGrad-RDA hinge")
 TrainClassifier = _learner("train_classifier", "general", "binary", GENERAL_OPTS, default_iters=10,
                            default_loss="hinge", doc="GeneralClassifierUDTF")
 
@@ -430,10 +435,10 @@ TrainAROWeRegr = _learner("train_arowe_regr", "arowe_regr", "regression", [_R, _
 TrainAROWe2Regr = _learner("train_arowe2_regr", "arowe2_regr", "regression", [_R, _EPS_INS])
 TrainAdaGradRegr = _learner("train_adagrad_regr", "adagrad_regr", "regression", [
     opt("eta", "eta0", 1.0, float, "Learning rate"), opt("eps", None, 1.0, float, "Denominator"),
-    opt("scale", None, 100.0, float, "Scaling factor (accepted)")])
+    opt("scale", None, 100.0, float, "Scaling factor", inert=_SCALE_INERT)])
 TrainAdaDeltaRegr = _learner("train_adadelta_regr", "adadelta_regr", "regression", [
     opt("rho", "decay", 0.95, float, "Decay"), opt("eps", None, 1e-6, float, "Denominator"),
-    opt("scale", None, 100.0, float, "Scaling factor (accepted)")])
+    opt("scale", None, 100.0, float, "Scaling factor", inert=_SCALE_INERT)])
 TrainRegressor = _learner("train_regressor", "general", "regression", GENERAL_OPTS, default_iters=10,
                           default_loss="squared", doc="GeneralRegressorUDTF")
 

@@ -33,6 +33,34 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import MIX_OPTS, ConversionState, Learner, log
 
 _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2, "bolddriver": 0, "bold_driver": 0}
+_BOLD = ("bolddriver", "bold_driver")
+
+
+class BoldDriverEta:
+    """``-eta bolddriver``: Hivemall's AdjustingEtaEstimator driven by the epoch loss
+    (hivemall.common.EtaEstimator.AdjustingEtaEstimator).
+
+    The rate is constant within an epoch; after each epoch whose loss is known against the
+    previous one it is multiplied by 1.05 when the loss decreased and by 0.5 when it increased,
+    capped at MAX_ETA = 1.0, and a non-finite product leaves it unchanged."""
+
+    MAX_ETA = 1.0
+    UP, DOWN = 1.05, 0.5
+
+    def __init__(self, eta0: float):
+        self.eta = float(eta0)
+        self.prev_loss: float | None = None
+        self.history = [self.eta]
+
+    def epoch_end(self, loss: float) -> float:
+        if self.prev_loss is not None:
+            mult = self.DOWN if loss > self.prev_loss else self.UP
+            new = self.eta * mult
+            if np.isfinite(new):
+                self.eta = min(self.MAX_ETA, new)
+        self.prev_loss = float(loss)
+        self.history.append(self.eta)
+        return self.eta
 
 MF_OPTS = [
     opt("factors", "factor", 10, int, "Number of latent factors", aliases=("k",)),
@@ -44,11 +72,12 @@ MF_OPTS = [
     opt("min_init_stddev", None, 0.1, float, "Stddev for gaussian init"),
     opt("iters", "iterations", 1, int, "Iterations", aliases=("iter",)),
     opt("eta0", None, 0.1, float, "Initial learning rate"),
-    opt("eta", None, "fixed", str, "Learning rate scheme: fixed, simple, inverse"),
+    opt("eta", None, "fixed", str, "Learning rate scheme: fixed, simple, inverse, bolddriver"),
     opt("power_t", None, 0.1, float, "Inverse scaling exponent"),
     opt("t", "total_steps", -1.0, float, "Total steps for -eta simple"),
     opt("eps", None, 1.0, float, "AdaGrad denominator constant"),
-    opt("scale", None, 100.0, float, "Scaling factor (accepted)"),
+    opt("scale", None, 100.0, float, "Scaling factor",
+        inert="factor accumulators are fp32 (no half-float scaling)"),
     flag("disable_bias", "no_bias", "Do not learn user/item biases"),
     opt("cv_rate", "convergence_rate", 0.005, float, "Convergence threshold"),
     flag("disable_cv", "disable_cvtest", "Disable convergence check"),
@@ -106,6 +135,18 @@ class _MFBase(Learner):
             return
         ts = [self.state[k] for k in ("P", "Q", "Bu", "Bi", "mu") if k in self.state]
         self.mix_tensors(ts, [self.seen_u, self.seen_i])
+
+    def _eta0(self) -> float:
+        """Learning rate of the current epoch: -eta0, or the bold driver's adjusted rate."""
+        if str(self.cl["eta"]).lower() in _BOLD:
+            if getattr(self, "bold", None) is None:
+                self.bold = BoldDriverEta(float(self.cl["eta0"]))
+            return self.bold.eta
+        return float(self.cl["eta0"])
+
+    def _epoch_end(self, loss: float) -> None:
+        if getattr(self, "bold", None) is not None:
+            self.bold.epoch_end(loss)
 
     def _epoch_mix(self, ep: int) -> None:
         mi = int(self.cl["mix_interval"])
@@ -181,7 +222,7 @@ class MatrixFactorization(_MFBase):
     def _hp(self):
         c = self.cl
         lam = float(c["lambda"])
-        return np.array([c["eta0"], c["power_t"], c["t"], lam, lam, lam, lam, c["eps"]], dtype=np.float32)
+        return np.array([self._eta0(), c["power_t"], c["t"], lam, lam, lam, lam, c["eps"]], dtype=np.float32)
 
     def _step(self, u, i, r, train=True, pred=None, loss=None):
         st = self.state
@@ -212,7 +253,9 @@ class MatrixFactorization(_MFBase):
         for ep in range(int(self.cl["iters"])):
             self._step(u, i, r, loss=loss)
             self._epoch_mix(ep)
-            self.cv.incr_loss(float(loss.double().sum().item()))
+            el = float(loss.double().sum().item())
+            self._epoch_end(el)
+            self.cv.incr_loss(el)
             if self.cv.is_converged():
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
@@ -314,7 +357,7 @@ class BPRMF(_MFBase):
         ru = c["reg_u"] if c["reg_u"] is not None else reg
         ri = c["reg_i"] if c["reg_i"] is not None else reg
         rj = c["reg_j"] if c["reg_j"] is not None else reg
-        return np.array([c["eta0"], c["power_t"], c["t"], ru, ri, rj, c["reg_bias"], 1.0], dtype=np.float32)
+        return np.array([self._eta0(), c["power_t"], c["t"], ru, ri, rj, c["reg_bias"], 1.0], dtype=np.float32)
 
     def step(self, tu=None, ti=None, tj=None, n=None, csr=None) -> float:
         """One launch over explicit triples, or ``n`` device-sampled triples from ``csr``."""
@@ -350,7 +393,9 @@ class BPRMF(_MFBase):
         self.seen_i[ti.long()] = True
         self.seen_i[tj.long()] = True
         for ep in range(int(self.cl["iters"])):
-            self.cv.incr_loss(self.step(tu, ti, tj))
+            el = self.step(tu, ti, tj)
+            self._epoch_end(el)
+            self.cv.incr_loss(el)
             self._epoch_mix(ep)
             if self.cv.is_converged():
                 break
@@ -381,7 +426,9 @@ class BPRMF(_MFBase):
         self.seen_i.fill_(True)
         per = int(self.cl["samples_per_epoch"]) or csr[1].numel()
         for ep in range(int(epochs or self.cl["iters"])):
-            self.cv.incr_loss(self.step(n=per, csr=csr))
+            el = self.step(n=per, csr=csr)
+            self._epoch_end(el)
+            self.cv.incr_loss(el)
             self._epoch_mix(ep)
             if self.cv.is_converged():
                 break

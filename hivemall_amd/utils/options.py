@@ -36,6 +36,7 @@ class Opt:
     type: Callable[[str], Any] = str
     help: str = ""
     aliases: tuple = ()
+    inert: str = ""                # non-empty: accepted for compatibility, has no effect (why)
 
     def names(self) -> list[str]:
         out = [self.name]
@@ -49,13 +50,31 @@ def _bool(s: str) -> bool:
     return str(s).lower() in ("1", "true", "yes", "on")
 
 
-def flag(name: str, long: str | None = None, help: str = "", aliases: tuple = ()) -> Opt:
-    return Opt(name, long, has_arg=False, default=False, type=_bool, help=help, aliases=aliases)
+def flag(name: str, long: str | None = None, help: str = "", aliases: tuple = (),
+         inert: str = "") -> Opt:
+    return Opt(name, long, has_arg=False, default=False, type=_bool, help=help, aliases=aliases,
+               inert=inert)
 
 
 def opt(name: str, long: str | None = None, default: Any = None, type: Callable = str,
-        help: str = "", aliases: tuple = ()) -> Opt:
-    return Opt(name, long, has_arg=True, default=default, type=type, help=help, aliases=aliases)
+        help: str = "", aliases: tuple = (), inert: str = "") -> Opt:
+    return Opt(name, long, has_arg=True, default=default, type=type, help=help, aliases=aliases,
+               inert=inert)
+
+
+_warned: set = set()
+
+
+def warn_inert(func_name: str, o: Opt) -> None:
+    """Log (once per function and option) that an accepted option has no effect here."""
+    key = (func_name, o.name)
+    if key in _warned:
+        return
+    _warned.add(key)
+    import logging
+
+    logging.getLogger("hivemall_amd").warning("%s: option -%s is accepted for compatibility but "
+                                              "has no effect: %s", func_name, o.name, o.inert)
 
 
 class Options:
@@ -97,7 +116,8 @@ class Options:
             if o.has_arg:
                 spell += f" <arg>"
             d = f" (default: {o.default})" if o.has_arg and o.default is not None else ""
-            lines.append(f" {spell:<32} {o.help}{d}")
+            inert = f" [no effect: {o.inert}]" if o.inert else ""
+            lines.append(f" {spell:<32} {o.help}{d}{inert}")
         return "\n".join(lines)
 
     def parse(self, optstr: str | None) -> "CommandLine":
@@ -121,6 +141,8 @@ class Options:
             if o.name == "help":
                 raise UDFArgumentException(self.usage())
             present.add(o.name)
+            if o.inert:
+                warn_inert(self.func_name, o)
             if o.has_arg:
                 if val_inline is not None:
                     raw = val_inline

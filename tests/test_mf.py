@@ -131,3 +131,40 @@ def test_bpr_gpu_device_sampling_quality():
         m = BPRMF("-factors 32 -iters 10 -eta0 0.05", device=dev).fit_implicit(us[:380000], its[:380000], 5000, 2000)
         res[dev] = auc_implicit(m, us[380000:].numpy(), its[380000:].numpy())
     assert res["cuda"] > res["cpu"] - 0.03, res
+
+
+@pytest.mark.parametrize("cls", ["bpr", "mf"])
+def test_bold_driver_eta_follows_the_rule(cls):
+    """-eta bolddriver (AdjustingEtaEstimator): x1.05 after a loss decrease, x0.5 after an
+    increase, capped at 1.0; the kernel is fed the adjusted rate every epoch."""
+    from hivemall_amd.models.mf import BPRMF, MatrixFactorization
+
+    rng = np.random.default_rng(0)
+    u, i, j = rng.integers(0, 40, 600), rng.integers(0, 60, 600), rng.integers(0, 60, 600)
+    if cls == "bpr":
+        m = BPRMF("-factors 4 -iters 6 -disable_cv -eta bolddriver -eta0 0.3", device="cpu")
+        m.fit(u, i, j)
+    else:
+        m = MatrixFactorization("-factors 4 -iters 6 -disable_cv -eta bold_driver -eta0 0.9",
+                                device="cpu")
+        m.fit(u, i, rng.random(600) * 5)
+    losses = m.cv.history
+    etas = m.bold.history
+    assert len(etas) == len(losses) + 1 and len(losses) == 6
+    for k in range(1, len(losses)):
+        mult = 0.5 if losses[k] > losses[k - 1] else 1.05
+        assert etas[k + 1] == pytest.approx(min(1.0, etas[k] * mult), rel=1e-12)
+    assert etas[1] == etas[0]             # no previous loss after the first epoch
+    assert max(etas) <= 1.0
+
+
+def test_inert_option_warns(caplog):
+    import logging
+
+    from hivemall_amd.models.mf import MatrixFactorization
+    from hivemall_amd.utils import options as O
+
+    O._warned.clear()
+    with caplog.at_level(logging.WARNING, logger="hivemall_amd"):
+        MatrixFactorization("-factors 4 -scale 10", device="cpu")
+    assert any("-scale" in r.getMessage() and "no effect" in r.getMessage() for r in caplog.records)
