@@ -1,4 +1,5 @@
 // CPU twins of csrc/kernels/trees.hip (same layouts and semantics), OpenMP-parallel.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -134,6 +135,89 @@ inline float split_score(const float* S, int NS, int crit, float lam, float alph
     return s1 > 0.f ? g * g / (s1 + lam) : 0.f;
 }
 
+inline float wide_term(float S, float W, int crit) {
+    return crit == 0 ? S * S : S * std::log(std::fmax(S / std::fmax(W, 1e-30f), 1e-30f));
+}
+inline float wide_score(float W, float T, int crit) {
+    if (W <= 0.f) return 0.f;
+    return crit == 0 ? T / std::fmax(W, 1e-30f) : T;
+}
+
+// NS > 8 (many classes, gini / entropy): the class-decomposed scores of split_find_wide_kernel,
+// same accumulation order (classes 0..NS-1 per candidate bin).
+void split_find_wide(const float* hist, int L, int d, int B, int NS, int n_edges, int crit, int mtry,
+                     int node_base, uint32_t seed, float min_leaf, const uint8_t* cat, const uint8_t* fmask,
+                     float* gain, int32_t* feat, int32_t* bin, float* left, float* tot) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int node = 0; node < L; ++node) {
+        const float* hn = hist + (size_t)node * d * B * NS;
+        std::vector<float> T(NS, 0.f);
+        for (int c = 0; c < NS; ++c)
+            for (int b = 0; b < B; ++b) T[c] += hn[(size_t)b * NS + c];
+        float pw = 0.f, pt = 0.f;
+        for (int c = 0; c < NS; ++c) pw += T[c];
+        for (int c = 0; c < NS; ++c) pt += wide_term(T[c], pw, crit);
+        const float parent = wide_score(pw, pt, crit);
+        std::vector<float> wl(B), tl(B), wr(B), tr(B);
+        float best = -INFINITY;
+        int best_i = 0x7FFFFFFF;
+        for (int f = 0; f < d; ++f) {
+            if (fmask && !fmask[f]) continue;
+            if (mtry > 0 && mtry < d) {
+                const uint32_t kf = feat_key(seed, (uint32_t)(node_base + node), (uint32_t)f);
+                int before = 0;
+                for (int g = 0; g < d; ++g) {
+                    const uint32_t kg = feat_key(seed, (uint32_t)(node_base + node), (uint32_t)g);
+                    before += (kg < kf || (kg == kf && g < f)) ? 1 : 0;
+                }
+                if (before >= mtry) continue;
+            }
+            const bool is_cat = cat && cat[f];
+            const float* hf = hn + (size_t)f * B * NS;
+            std::fill(wl.begin(), wl.end(), 0.f); std::fill(tl.begin(), tl.end(), 0.f);
+            std::fill(wr.begin(), wr.end(), 0.f); std::fill(tr.begin(), tr.end(), 0.f);
+            for (int pass = crit == 1 ? 0 : 1; pass < 2; ++pass) {
+                for (int c = 0; c < NS; ++c) {
+                    float tc = 0.f;
+                    for (int b = 0; b < B; ++b) tc += hf[(size_t)b * NS + c];
+                    float run = 0.f;
+                    for (int b = 0; b < B; ++b) {
+                        const float h = hf[(size_t)b * NS + c];
+                        run += h;
+                        const float l = is_cat ? h : run;
+                        const float r = tc - l;
+                        if (pass == 0 || crit == 0) { wl[b] += l; wr[b] += r; }
+                        if (pass == 1) { tl[b] += wide_term(l, wl[b], crit); tr[b] += wide_term(r, wr[b], crit); }
+                    }
+                }
+            }
+            for (int b = 0; b < B; ++b) {
+                if (wl[b] < min_leaf || wr[b] < min_leaf) continue;
+                if (is_cat && b >= n_edges) continue;
+                const float g = wide_score(wl[b], tl[b], crit) + wide_score(wr[b], tr[b], crit) - parent;
+                const int i = f * B + b;
+                if (g > best || (g == best && i < best_i)) { best = g; best_i = i; }
+            }
+        }
+        const bool found = best_i != 0x7FFFFFFF;
+        gain[node] = found ? best : -INFINITY;
+        feat[node] = found ? best_i / B : 0;
+        bin[node] = found ? best_i % B : 0;
+        const int bf = found ? best_i / B : 0, bb = found ? best_i % B : -1;
+        const bool bcat = found && cat && cat[bf];
+        for (int c = 0; c < NS; ++c) {
+            float t = 0.f, l = 0.f;
+            for (int b = 0; b < B; ++b) {
+                t += hn[(size_t)b * NS + c];
+                const float hv = hn[((size_t)bf * B + b) * NS + c];
+                if (bcat ? b == bb : b <= bb) l += hv;
+            }
+            tot[(size_t)node * NS + c] = t;
+            left[(size_t)node * NS + c] = found ? l : 0.f;
+        }
+    }
+}
+
 }  // namespace
 
 HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* fp, const uint8_t* cat,
@@ -143,7 +227,13 @@ HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* 
     const int mtry = ip[6], node_base = ip[7];
     const uint32_t seed = (uint32_t)ip[8];
     const float lam = fp[0], alpha = fp[1], min_leaf = fp[2];
-    if (B <= 0 || B > 256 || NS <= 0 || NS > 8 || crit < 0 || crit > 4) return 1;
+    if (B <= 0 || B > 256 || NS <= 0 || crit < 0 || crit > 4) return 1;
+    if (NS > 8) {
+        if (crit > 1) return 1;
+        split_find_wide(hist, L, d, B, NS, n_edges, crit, mtry, node_base, seed, min_leaf, cat, fmask, gain,
+                        feat, bin, left, tot);
+        return 0;
+    }
 #pragma omp parallel for schedule(dynamic, 1)
     for (int node = 0; node < L; ++node) {
         const float* hn = hist + (size_t)node * d * B * NS;

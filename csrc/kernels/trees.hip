@@ -475,6 +475,140 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
 }
 
 // ---------------------------------------------------------------------------------------------
+// Split search for class-count statistics with more classes than the register kernel holds
+// (NS > 8: RandomForest with up to 256 classes).  Gini and entropy scores decompose over the
+// classes (gini = sum S^2 / W, entropy = sum S log S - W log W), so the kernel walks the classes
+// one at a time and keeps, per candidate bin, only (W, sum f(S)) of the left and right child: 4
+// bins x 4 floats per lane whatever NS is.  Same candidates, mtry draw, nominal rule and
+// tie-break as split_find_kernel; the left statistics of the winning split are re-summed per
+// class at the end (thread per class).
+// gini: term S^2, score T / W.  entropy: term S log(S / W) with the child weight W known from a
+// first pass over the classes (no T - W log W cancellation), score T.
+__device__ __forceinline__ float wide_term(float S, float W, int crit) {
+    return crit == 0 ? S * S : S * logf(fmaxf(S / fmaxf(W, 1e-30f), 1e-30f));
+}
+__device__ __forceinline__ float wide_score(float W, float T, int crit) {
+    if (W <= 0.f) return 0.f;
+    return crit == 0 ? T / fmaxf(W, 1e-30f) : T;
+}
+
+__global__ __launch_bounds__(256) void split_find_wide_kernel(SplitParams P, const float* __restrict__ hist,
+                                                              const uint8_t* __restrict__ cat,
+                                                              const uint8_t* __restrict__ fmask,
+                                                              float* __restrict__ out_gain,
+                                                              int32_t* __restrict__ out_feat,
+                                                              int32_t* __restrict__ out_bin,
+                                                              float* __restrict__ out_left,
+                                                              float* __restrict__ out_tot) {
+    __shared__ float s_gain[4];
+    __shared__ int s_idx[4];
+    const int node = blockIdx.x;
+    const int lane = hm::lane_id(), wave = hm::wave_id();
+    const int B = P.B, d = P.d, NS = P.NS;
+    const int bpl = (B + 63) / 64;
+    const int b0 = lane * bpl;
+    const float* hn = hist + (size_t)node * d * B * NS;
+    // parent score from feature 0's histogram (class order 0..NS-1, as the host engine)
+    auto node_class = [&](int c) {
+        float v = 0.f;
+        for (int k = 0; k < bpl; ++k)
+            if (b0 + k < B) v += hn[(size_t)(b0 + k) * NS + c];
+        return hm::wave_sum(v);
+    };
+    float pw = 0.f, pt = 0.f;
+    for (int c = 0; c < NS; ++c) pw += node_class(c);
+    for (int c = 0; c < NS; ++c) pt += wide_term(node_class(c), pw, P.crit);
+    const float parent = wide_score(pw, pt, P.crit);
+
+    float best = -INFINITY;
+    int best_i = 0x7FFFFFFF;
+    for (int f = wave; f < d; f += 4) {
+        if (fmask && !fmask[f]) continue;
+        if (P.mtry > 0 && P.mtry < d) {
+            const uint32_t kf = feat_key(P.seed, (uint32_t)(P.node_base + node), (uint32_t)f);
+            int before = 0;
+            for (int g = lane; g < d; g += 64) {
+                const uint32_t kg = feat_key(P.seed, (uint32_t)(P.node_base + node), (uint32_t)g);
+                before += (kg < kf || (kg == kf && g < f)) ? 1 : 0;
+            }
+            for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+            if (before >= P.mtry) continue;
+        }
+        const bool is_cat = cat && cat[f];
+        const float* hf = hn + (size_t)f * B * NS;
+        float wl[4] = {0.f, 0.f, 0.f, 0.f}, tl[4] = {0.f, 0.f, 0.f, 0.f};
+        float wr[4] = {0.f, 0.f, 0.f, 0.f}, tr[4] = {0.f, 0.f, 0.f, 0.f};
+        // pass 0 (entropy only): child weights; pass 1: the score terms
+        for (int pass = P.crit == 1 ? 0 : 1; pass < 2; ++pass) {
+            for (int c = 0; c < NS; ++c) {
+                float h[4];
+                float lsum = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    h[k] = (k < bpl && b0 + k < B) ? hf[(size_t)(b0 + k) * NS + c] : 0.f;
+                    lsum += h[k];
+                }
+                float v = lsum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const float t = __shfl_up(v, o, 64);
+                    if (lane >= o) v += t;
+                }
+                const float tc = hm::wave_sum(lsum);
+                float run = v - lsum;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    run += h[k];
+                    const float l = is_cat ? h[k] : run;
+                    const float r = tc - l;
+                    if (pass == 0 || P.crit == 0) { wl[k] += l; wr[k] += r; }
+                    if (pass == 1) { tl[k] += wide_term(l, wl[k], P.crit); tr[k] += wide_term(r, wr[k], P.crit); }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int b = b0 + k;
+            if (k >= bpl || b >= B) break;
+            if (wl[k] < P.min_leaf || wr[k] < P.min_leaf) continue;
+            if (is_cat && b >= P.n_edges) continue;
+            const float g = wide_score(wl[k], tl[k], P.crit) + wide_score(wr[k], tr[k], P.crit) - parent;
+            const int i = f * B + b;
+            if (g > best || (g == best && i < best_i)) { best = g; best_i = i; }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float og = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(best_i, o, 64);
+        if (og > best || (og == best && oi < best_i)) { best = og; best_i = oi; }
+    }
+    if (lane == 0) { s_gain[wave] = best; s_idx[wave] = best_i; }
+    __syncthreads();
+    int w = 0;
+    for (int k = 1; k < 4; ++k)
+        if (s_gain[k] > s_gain[w] || (s_gain[k] == s_gain[w] && s_idx[k] < s_idx[w])) w = k;
+    const bool found = s_idx[w] != 0x7FFFFFFF;
+    if (threadIdx.x == 0) {
+        out_gain[node] = found ? s_gain[w] : -INFINITY;
+        out_feat[node] = found ? s_idx[w] / B : 0;
+        out_bin[node] = found ? s_idx[w] % B : 0;
+    }
+    // per class: node total (feature 0) and the winning split's left statistics
+    const int bf = found ? s_idx[w] / B : 0, bb = found ? s_idx[w] % B : -1;
+    const bool bcat = found && cat && cat[bf];
+    for (int c = threadIdx.x; c < NS; c += blockDim.x) {
+        float t = 0.f, l = 0.f;
+        for (int b = 0; b < B; ++b) {
+            t += hn[(size_t)b * NS + c];
+            const float hv = hn[((size_t)bf * B + b) * NS + c];
+            if (bcat ? b == bb : b <= bb) l += hv;
+        }
+        out_tot[(size_t)node * NS + c] = t;
+        out_left[(size_t)node * NS + c] = found ? l : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Level row partition (replaces a full 16-bit key sort of the active rows per level): the rows
 // of the smaller child of every split, grouped by child, as the next level's histogram input.
 // key(r) = lut[node_of_row[r] - nb] (32767 / out of range: not histogrammed).  Two passes over
@@ -656,6 +790,12 @@ HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, 
     P.lam = fp[0]; P.alpha = fp[1]; P.min_leaf = fp[2];
     if (P.L <= 0) return 0;
     if (P.B <= 0 || P.B > 256 || P.d <= 0 || P.crit < 0 || P.crit > 4) return (int)hipErrorInvalidValue;
+    if (P.NS > 8) {   // many classes: gini / entropy only, classes walked one at a time
+        if (P.crit > 1 || P.NS > 4096) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(split_find_wide_kernel, dim3(P.L), dim3(256), 0, stream, P, hist, cat, fmask,
+                           gain, feat, bin, left, tot);
+        HM_LAUNCH_RET();
+    }
 #define HM_SF(K) \
     case K: hipLaunchKernelGGL((split_find_kernel<K>), dim3(P.L), dim3(256), 0, stream, P, hist, cat, fmask, \
                                gain, feat, bin, left, tot); break;

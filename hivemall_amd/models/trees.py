@@ -354,15 +354,28 @@ class HistTreeBuilder:
         NS = stats.shape[1]
         dev = stats.device
         hist = torch.zeros((n_seg, q.d, q.B, NS), dtype=torch.float32, device=dev)
-        # feature groups: multiple of 4 features, LDS image <= 48 KB, balanced over the groups
-        # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB
-        FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
         p = _native.ptr
-        args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), p(smax), NS, FG, p(hist))
-        if dev.type == "cuda":
-            _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)), "hm_hist_build")
+        if dev.type == "cuda" and NS > 8:
+            # many classes: the LDS kernel sums <= 8 statistics per pass -> class tiles of 8
+            for c0 in range(0, NS, 8):
+                c1 = min(NS, c0 + 8)
+                sub = torch.zeros((n_seg, q.d, q.B, c1 - c0), dtype=torch.float32, device=dev)
+                st = stats[:, c0:c1].contiguous()
+                sm = smax[c0:c1].contiguous()
+                FG = next((f for f in (16, 8) if f * q.B * (c1 - c0) * 4 <= 48 * 1024), 4)
+                args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(st), p(sm), c1 - c0, FG, p(sub))
+                _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)),
+                              "hm_hist_build")
+                hist[..., c0:c1] = sub
         else:
-            _native.host().hm_hist_build_cpu(*args)
+            # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB
+            FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
+            args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), p(smax), NS, FG, p(hist))
+            if dev.type == "cuda":
+                _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)),
+                              "hm_hist_build")
+            else:
+                _native.host().hm_hist_build_cpu(*args)
         if self.mixer is not None and self.mixer.world > 1:
             self.mixer.all_reduce_sum([hist])
         return hist
@@ -597,9 +610,7 @@ class _ForestBase(Learner):
             g.manual_seed(self.seed * 1000003 + t)   # tree t's bootstrap does not depend on the rank split
             w = bootstrap_weights(n, float(c["subsample"]), g, self.device, strat)
             if self.TASK == "classification":
-                if onehot.shape[1] > 8:
-                    raise UDFArgumentException("train_randomforest_classifier: > 8 classes not supported on this engine")
-                stats = onehot * w[:, None]
+                stats = onehot * w[:, None]       # > 8 classes: class-tiled histograms
             else:
                 stats = torch.stack([w * yf, w], 1)
             b = HistTreeBuilder(q, crit, int(c["max_depth"]), c["min_split"], c["min_samples_leaf"],

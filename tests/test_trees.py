@@ -349,3 +349,84 @@ def test_partition_kernel_groups_rows_like_sort():
         got = rows[seg[k]:seg[k + 1]].tolist()
         assert len(got) == len(want) and set(got) == want, k
     assert int(seg[n_split]) == int((key < n_split).sum())
+
+
+# ---------------------------------------------------------------- many classes (NS > 8)
+def _int_split_case(crit, NS, cat=False, seed=0):
+    """Integer class-count histograms (exact in fp32) for the class-decomposed split search."""
+    b, _, cm = _split_case(crit, 2, cat, seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    L, d, B = 5, 7, 64
+    rows = torch.randint(0, NS, (L, 4000), generator=g)
+    binsel = torch.randint(0, B, (L, d, 4000), generator=g)
+    H = torch.zeros(L, d, B, NS)
+    for l in range(L):
+        for f in range(d):
+            H[l, f].index_put_((binsel[l, f], rows[l]), torch.ones(4000), accumulate=True)
+    return b, H, cm
+
+
+@pytest.mark.parametrize("crit,cat", [("gini", False), ("entropy", True)])
+def test_split_find_many_classes_matches_tensor_formulation(crit, cat):
+    b, H, cm = _int_split_case(crit, 11, cat)
+    gain, feat, bins, left, tot = b._split_find(H, 0)
+    bg, bi, rtot = _split_ref(b, H, cm)
+    torch.testing.assert_close(tot, rtot)
+    torch.testing.assert_close(gain, bg, rtol=1e-4, atol=1e-3)
+    assert torch.equal(feat.long() * H.shape[2] + bins.long(), bi)
+    # left statistics of the chosen split
+    for l in range(H.shape[0]):
+        f, bb = int(feat[l]), int(bins[l])
+        want = H[l, f, bb] if (cm is not None and bool(cm[f])) else H[l, f, :bb + 1].sum(0)
+        torch.testing.assert_close(left[l], want)
+
+
+def _ten_class_data(n=6000, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 6)).astype(np.float32)
+    y = (np.floor((X[:, 0] + 3) * 10 / 6).clip(0, 9)).astype(int)   # 10 bands of feature 0
+    return X, y
+
+
+def test_rf_ten_classes_cpu():
+    X, y = _ten_class_data()
+    rf = RandomForestClassifier("-trees 8 -max_depth 8 -seed 3", device="cpu").fit(X, y)
+    assert len(rf.classes) == 10
+    assert (rf.predict(X) == y).mean() > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crit,cat", [("gini", False), ("entropy", True), ("gini", True)])
+def test_split_find_many_classes_kernel_matches_host(crit, cat):
+    b, H, cm = _int_split_case(crit, 10, cat, seed=4)
+    b.mtry = 4
+    host = b._split_find(H, 7)
+    b._masks = None
+    dev = b._split_find(H.cuda(), 7)
+    # gains: hardware logf vs libm log over ~10^4-sized terms -> 1e-3 relative for entropy
+    torch.testing.assert_close(dev[0].cpu(), host[0], rtol=1e-3 if crit == "entropy" else 1e-5, atol=1e-4)
+    assert torch.equal(dev[1].cpu(), host[1]) and torch.equal(dev[2].cpu(), host[2])
+    assert torch.equal(dev[3].cpu(), host[3]) and torch.equal(dev[4].cpu(), host[4])
+
+
+@pytest.mark.gpu
+def test_rf_ten_classes_gpu_matches_cpu():
+    """10 classes: class-tiled LDS histograms + the class-decomposed split kernel grow the same
+    tree as the host engine from the same (integer) statistics."""
+    from hivemall_amd.models.trees import HistTreeBuilder, Quantized
+
+    X, y = _ten_class_data(n=20000, seed=1)
+    q = quantize(torch.from_numpy(X), 64)
+    w = torch.from_numpy(np.random.default_rng(2).integers(0, 3, len(y)).astype(np.float32))
+    stats = torch.nn.functional.one_hot(torch.from_numpy(y), 10).float() * w[:, None]
+    trees = []
+    for dev in ("cpu", "cuda"):
+        qd = q if dev == "cpu" else Quantized(q.bins.to(dev), q.edges, q.d, q.B, q.cat)
+        b = HistTreeBuilder(qd, "gini", 6, 2.0, 1.0, mtry=3, seed=11)
+        trees.append(b.build(stats.to(dev)))
+    tc, tg = trees
+    assert list(tc.feature) == list(tg.feature)
+    np.testing.assert_allclose(np.asarray(tc.threshold, dtype=np.float64),
+                               np.asarray(tg.threshold, dtype=np.float64))
+    rf = RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device="cuda").fit(X, y)
+    assert (rf.predict(X) == y).mean() > 0.9
