@@ -30,15 +30,51 @@ def _device(session):
     return None if session is None else session.device
 
 
-def _learner_udtf(name, cls_getter, n_data_args=2):
+def _dist(session):
+    ctx = getattr(session, "ctx", None)
+    return ctx if (ctx is not None and ctx.world_size > 1) else None
+
+
+def _learner_udtf(name, cls_getter, n_data_args=2, signature=None):
+    """Register learner ``name`` as a table function.  In a distributed session the learner's
+    ``SQL_DP`` mode decides how the ranks share the work (models/base.py Learner.SQL_DP):
+
+    * ``shard``: rank r trains on input rows r, r + world, ... with a ModelMixer (replicas mixed
+      over RCCL; all ranks end with the same model table);
+    * ``union``: every rank sees all rows and builds its share of an ensemble (RandomForest
+      trees t with t % world == rank); the table is the union of the ranks' tables;
+    * ``replicate``: learners without a data-parallel formulation train on all rows on every
+      rank (identical tables, no speed-up)."""
     def impl(*args, session=None):
         cls = cls_getter()
         opts = _opt_arg(args, n_data_args)
-        m = cls(opts, device=_device(session))
-        m.fit(*[list(a) for a in args[:n_data_args]])
-        return m.model_table()
+        data = [list(a) for a in args[:n_data_args]]
+        ctx = _dist(session)
+        if ctx is None:
+            m = cls(opts, device=_device(session))
+            m.fit(*data)
+            return m.model_table()
+        from .parallel.mix import ModelMixer
+
+        mode = getattr(cls, "SQL_DP", "replicate")
+        kw = {}
+        if mode == "shard":
+            data = [d[ctx.rank::ctx.world_size] for d in data]
+            kw = dict(mixer=ModelMixer(ctx), rank=ctx.rank)
+        elif mode == "union":
+            kw = dict(mixer=ModelMixer(ctx), rank=ctx.rank)
+        m = cls(opts, device=_device(session), **kw)
+        m.fit(*data)
+        tab = m.model_table()
+        if mode == "union":
+            import torch.distributed as tdist
+
+            parts = [None] * ctx.world_size
+            tdist.all_gather_object(parts, tab)
+            tab = pd.concat(parts, ignore_index=True)
+        return tab
     impl.wants_session = True
-    impl.__doc__ = f"{name}(features, label [, options]) -> model table"
+    impl.__doc__ = f"{name}({signature or 'features, label'} [, options]) -> model table"
     registry._register(registry.FunctionDef(name, registry.UDTF, impl, per_row=False,
                                             doc=impl.__doc__))
 

@@ -91,6 +91,10 @@ class Learner:
 
     NAME = "learner"
     OPTIONS: list = []
+    # data parallelism of the SQL UDTF in a distributed session (functions._learner_udtf):
+    # "shard" (rows split over the ranks + RCCL mixing), "union" (ensemble members split over the
+    # ranks) or "replicate" (no data-parallel formulation: every rank trains on all rows)
+    SQL_DP = "replicate"
 
     @classmethod
     def options(cls) -> Options:

@@ -63,6 +63,7 @@ def csr_to_ffm_batch(csr: CSR, y: np.ndarray | None, width: int | None = None) -
 
 class FFMTrainer(Learner):
     NAME = "train_ffm"
+    SQL_DP = "shard"
     OPTIONS = COMMON_ITER_OPTS + [
         flag("classification", "c", "Act as classification (logistic loss); labels 0/1 or -1/1"),
         opt("factors", "factor", 4, int, "The number of latent factors k", aliases=("k",)),
@@ -238,7 +239,8 @@ class FFMTrainer(Learner):
     def model_table(self, model_id: str | None = None) -> pd.DataFrame:
         """Rows keyed as in :mod:`models.ffm_keys` (bias, linear, and V(feature, field))."""
         self._ensure_state()
-        mid = model_id or f"ffm-{self.rank}"
+        # a mixed data-parallel model is one model: same id on every rank
+        mid = model_id or f"ffm-{0 if self._dp() else self.rank}"
         ids = torch.nonzero(self.touched).flatten()
         NF, F, k = self.num_features, self.num_fields, self.k
         V = self.state["V"][ids][:, :, :k].float().reshape(len(ids) * F, k).cpu().numpy()

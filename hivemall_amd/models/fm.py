@@ -63,6 +63,7 @@ _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
 
 
 class FMTrainer(Learner):
+    SQL_DP = "shard"
     NAME = "train_fm"
     OPTIONS = FM_OPTS
 

@@ -126,6 +126,7 @@ def encode_rows(rows, encoder: FeatureEncoder | None, train: bool) -> tuple[CSR,
 
 
 class OnlineLinearLearner(Learner):
+    SQL_DP = "shard"
     NAME = "train_linear"
     ALGO = "general"
     TASK = "binary"           # binary | regression | multiclass
@@ -259,9 +260,15 @@ class OnlineLinearLearner(Learner):
         if dims <= 0:
             dims = int(rows.idx.max().item()) + 1 if rows.idx.numel() else 1
             if self.encoder is not None and self.encoder.mode == "dict":
+                if self._dp():
+                    raise UDFArgumentException(
+                        f"{self.NAME}: data-parallel training needs integer feature indices or "
+                        "-feature_hashing (a per-rank string dictionary gives every rank its own ids)")
                 dims = max(dims, self.encoder.vocab_size())
             elif self._warm is not None:
                 dims = max(dims, int(np.max(np.asarray(self._warm["feature"], dtype=np.int64))) + 1)
+            if self._dp():   # every rank's replica must have the same shape
+                dims = int(self.mixer.all_reduce_scalar(float(dims), "max"))
         L = len(self.labels) if self.TASK == "multiclass" else 1
         if self.TASK == "multiclass" and L < 2:
             raise UDFArgumentException(f"{self.NAME}: needs at least two distinct labels")
@@ -313,6 +320,10 @@ class OnlineLinearLearner(Learner):
 
     def touched_features(self) -> np.ndarray:
         t = self.state.touched.amax(0) if self.state.R > 1 else self.state.touched[0]
+        if self._dp():   # one model table on every rank: features seen by any rank
+            f = t.to(torch.float32)
+            self.mixer.all_reduce_sum([f])
+            t = f > 0
         return torch.nonzero(t).flatten().cpu().numpy()
 
     def _feature_names(self, ids: np.ndarray) -> list:

@@ -128,6 +128,7 @@ def _dev(x, dtype, dev) -> torch.Tensor:
 
 
 class _MFBase(Learner):
+    SQL_DP = "shard"
     def mix(self) -> None:
         """Replica averaging of the factor tables over the ranks (SURVEY.md §2.6 BPR/MF row);
         AdaGrad accumulators stay local, as each upstream mapper keeps its own."""

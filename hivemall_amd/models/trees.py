@@ -565,6 +565,7 @@ def _encode_classes(yl):
 
 
 class _ForestBase(Learner):
+    SQL_DP = "union"     # trees t with t % world == rank, over all rows
     OPTIONS = TREE_OPTS
     TASK = "classification"
 
@@ -704,6 +705,7 @@ GBT_OPTS = [
 
 
 class GradientTreeBoostingClassifier(Learner):
+    SQL_DP = "shard"     # rows split over the ranks, histograms all-reduced
     """Friedman's gradient boosting with logistic loss (binary) or softmax (K classes):
     regression trees on the pseudo-residuals, Newton leaf values Σr / Σ|r|(1-|r|)."""
     NAME = "train_gradient_tree_boosting_classifier"

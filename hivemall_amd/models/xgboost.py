@@ -62,6 +62,7 @@ _OBJ_ALIASES = {"reg:linear": "reg:squarederror", "binary:logitraw": "binary:log
 
 
 class XGBoostTrainer(Learner):
+    SQL_DP = "shard"
     NAME = "train_xgboost"
     OPTIONS = XGB_OPTS
     DEFAULT_OBJECTIVE = None
@@ -181,7 +182,7 @@ class XGBoostTrainer(Learner):
 
     def model_table(self) -> pd.DataFrame:
         s = base91.encode(zlib.compress(json.dumps(self._model_dict(), separators=(",", ":")).encode()))
-        return pd.DataFrame([(f"xgb-{self.rank}-{self.seed}", s)], columns=["model_id", "model"])
+        return pd.DataFrame([(f"xgb-{0 if self._dp() else self.rank}-{self.seed}", s)], columns=["model_id", "model"])
 
 
 class XGBoostClassifier(XGBoostTrainer):

@@ -215,7 +215,24 @@ def _expr_name(e, i: int) -> str:
 
 # ------------------------------------------------------------------ session
 class Session:
-    def __init__(self, device=None):
+    """A HiveQL session.  Under ``torch.distributed`` (one process per GPU, world > 1) every rank
+    runs the same script over the same (replicated) tables, and the learner UDTFs train data-
+    parallel: each rank takes its 1/world of the UDTF's input rows and the replicas are mixed over
+    RCCL (the mappers + MixServer of a Hive job), so every rank materialises the same model table
+    and every later query returns the same global result on every rank.
+    ``distributed=False`` keeps a session rank-local."""
+
+    def __init__(self, device=None, distributed: bool | None = None):
+        self.ctx = None
+        if distributed is not False:
+            import torch.distributed as tdist
+
+            if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1:
+                from ..parallel.dist import context
+
+                self.ctx = context()
+            elif distributed:
+                raise SQLError("Session(distributed=True) needs an initialised process group")
         self.tables: dict[str, pd.DataFrame] = {}
         self.views: dict[str, Query] = {}
         self.vars: dict[str, str] = {}
