@@ -30,12 +30,48 @@ def _device(session):
     return None if session is None else session.device
 
 
+# learner UDTF signatures for the catalogue / DESCRIBE FUNCTION: (inputs, output columns)
+_LIN_BIN = ("features, label", "feature, weight[, covar]")
+_LIN_MC = ("features, label", "label, feature, weight[, covar]")
+_FOREST = ("features, label", "model_id, model_weight, model, var_importance, oob_errors, oob_tests")
+SIGNATURES = {
+    "train_fm": ("features, target", "feature, Wi, Vif"),
+    "train_ffm": ("features, label", "model_id, i, Wi, Vi"),
+    "train_mf_sgd": ("user, item, rating", "idx, Pu, Qi, Bu, Bi, mu"),
+    "train_mf_adagrad": ("user, item, rating", "idx, Pu, Qi, Bu, Bi, mu"),
+    "train_bprmf": ("user, pos_item, neg_item", "idx, Pu, Qi, Bi"),
+    "train_slim": ("i, r_i, topKRatesOfI, j, r_j", "i, nn, w"),
+    "train_kpa": ("features, label", "h, hk, w0, w1, w2, w3"),
+    "train_lda": ("words", "label, word, lambda"),
+    "train_plsa": ("words", "label, word, prob"),
+    "train_randomforest_classifier": _FOREST,
+    "train_randomforest_regressor": _FOREST,
+    "train_randomforest_regr": _FOREST,
+    "train_gradient_tree_boosting_classifier": (
+        "features, label", "iteration, pred_models, intercept, shrinkage, var_importance, oob_error_rate"),
+    "train_xgboost": ("features, label", "model_id, model"),
+    "train_xgboost_classifier": ("features, label", "model_id, model"),
+    "train_xgboost_regr": ("features, target", "model_id, model"),
+    "train_multiclass_xgboost_classifier": ("features, label", "model_id, model"),
+}
+
+
+def _signature(name: str):
+    if name in SIGNATURES:
+        return SIGNATURES[name]
+    if "multiclass" in name:
+        return _LIN_MC
+    if name.endswith("_regr") or name in ("logress", "train_regressor"):
+        return ("features, target", "feature, weight[, covar]")
+    return _LIN_BIN
+
+
 def _dist(session):
     ctx = getattr(session, "ctx", None)
     return ctx if (ctx is not None and ctx.world_size > 1) else None
 
 
-def _learner_udtf(name, cls_getter, n_data_args=2, signature=None):
+def _learner_udtf(name, cls_getter, n_data_args=2):
     """Register learner ``name`` as a table function.  In a distributed session the learner's
     ``SQL_DP`` mode decides how the ranks share the work (models/base.py Learner.SQL_DP):
 
@@ -74,7 +110,8 @@ def _learner_udtf(name, cls_getter, n_data_args=2, signature=None):
             tab = pd.concat(parts, ignore_index=True)
         return tab
     impl.wants_session = True
-    impl.__doc__ = f"{name}({signature or 'features, label'} [, options]) -> model table"
+    ins, outs = _signature(name)
+    impl.__doc__ = f"{name}({ins} [, const string options]) -> table ({outs})"
     registry._register(registry.FunctionDef(name, registry.UDTF, impl, per_row=False,
                                             doc=impl.__doc__))
 
