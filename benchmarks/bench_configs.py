@@ -68,6 +68,34 @@ def bench_linear_gpu(dev="cuda", n=8_000_000):
             "device": dev, "replicas": m.state.R, "rows_per_s": round(n / dt), "train_acc": round(acc, 4)}
 
 
+def bench_linear_hashed(dev="cuda", n_rows=8 * 262144, bits=24, epochs=2):
+    """train_classifier -loss logloss -opt adagrad at Hivemall's default -dims 2^24 on
+    Criteo-shaped hashed rows (39 nnz): the shared-table Hogwild engine on the GPU, the
+    sequential engine on the CPU."""
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.models.linear import SparseRows, TrainClassifier
+    idx, y = criteo_like(n_rows, bits, seed=5, device=dev)
+    rows = SparseRows(torch.arange(0, n_rows * 39 + 1, 39, dtype=torch.int64, device=dev),
+                      idx.reshape(-1).contiguous(), None, y)
+    m = TrainClassifier(f"-loss logloss -opt adagrad -dims {1 << bits} -iters 1", device=dev)
+    m.fit(rows=rows)                                   # epoch 1 (state allocation, code load)
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(epochs - 1):
+        m.fit(rows=rows)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    eidx, ey = criteo_like(200000, bits, seed=77, device=dev)
+    er = SparseRows(torch.arange(0, 200000 * 39 + 1, 39, dtype=torch.int64, device=dev),
+                    eidx.reshape(-1).contiguous(), None, None)
+    ll = torch.nn.functional.binary_cross_entropy_with_logits(m.decision_function(rows=er),
+                                                              (ey > 0).float()).item()
+    eng = "shared-table Hogwild" if m.state.meta.get("shared") else f"{m.state.R} replicas"
+    return {"config": f"train_classifier adagrad logistic, Criteo-shaped {n_rows} x 39 nnz, -dims 2^{bits}",
+            "device": dev, "engine": eng, "rows_per_s": round(n_rows * (epochs - 1) / dt),
+            "heldout_logloss_after_epochs": round(ll, 5), "epochs": epochs}
+
+
 def bench_fm(dev="cuda", n_rows=8 * 262144, bits=24):
     from hivemall_amd.io.synthetic import criteo_like
     from hivemall_amd.models.fm import FMTrainer
@@ -149,14 +177,15 @@ def bench_bprmf(dev="cuda", k=64, epochs=3, opts=""):
             "opts": opts, "grid": m._grid()}
 
 
-ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "fm": bench_fm,
+ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "linear_hashed": bench_linear_hashed,
+       "fm": bench_fm,
        "gbdt": bench_gbdt, "rf": bench_rf, "bprmf": bench_bprmf}
 
-SMALL = {"linear_gpu": dict(n=20000), "fm": dict(n_rows=20000, bits=16),
+SMALL = {"linear_gpu": dict(n=20000), "linear_hashed": dict(n_rows=20000, bits=16), "fm": dict(n_rows=20000, bits=16),
          "gbdt": dict(n=20000, trees=4), "rf": dict(n=20000, trees=2), "bprmf": dict(k=16, epochs=1)}
 
 # CPU reference-class points (8-core host): same code paths on the C++/OpenMP engines
-CPU = {"linear_gpu": dict(n=1_000_000), "fm": dict(n_rows=262144, bits=20),
+CPU = {"linear_gpu": dict(n=1_000_000), "linear_hashed": dict(n_rows=8 * 262144, bits=24),"fm": dict(n_rows=262144, bits=20),
        "gbdt": dict(n=1_000_000, trees=10), "rf": dict(n=1_000_000, trees=4), "bprmf": dict(k=64, epochs=1)}
 
 if __name__ == "__main__":

@@ -76,6 +76,26 @@ __device__ __forceinline__ float ftrl_update(float* __restrict__ z, float* __res
     return ftrl_weight(z1, n1, alpha, beta, l1, l2);
 }
 
+// Global bias w0 (-w0): bias = {w0, z0, n0, _}.  Every block updates it, so its FTRL state
+// (z0, n0) is accumulated with atomics and w0 is derived from (z0, n0) where it is read;
+// bias[0] is only a cached copy for the host.  Sequentially this is exactly ftrl_update.
+__device__ __forceinline__ float bias_w0(const FFMParams& P, const float* bias) {
+    const float z = __hip_atomic_load(bias + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float n = __hip_atomic_load(bias + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ftrl_weight(z, n, P.alpha, P.beta, 0.f, 0.f);
+}
+
+__device__ __forceinline__ void bias_update(const FFMParams& P, float g, float* bias) {
+    const float z0 = __hip_atomic_load(bias + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float n0 = __hip_atomic_load(bias + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float w = ftrl_weight(z0, n0, P.alpha, P.beta, 0.f, 0.f);
+    const float sigma = (sqrtf(n0 + g * g) - sqrtf(n0)) / P.alpha;
+    const float dz = g - sigma * w;
+    atomicAdd(bias + 1, dz);
+    atomicAdd(bias + 2, g * g);
+    bias[0] = ftrl_weight(z0 + dz, n0 + g * g, P.alpha, P.beta, 0.f, 0.f);
+}
+
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
     h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
@@ -213,9 +233,7 @@ __device__ __forceinline__ void linear_updates(const FFMParams& P, float kappa, 
             w[i] = ftrl_update(wz + i, wn + i, w[i], g, P.alpha, P.beta, P.lambda1, P.lambda2);
         }
     }
-    if (P.use_bias && tid == 0) {
-        bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
-    }
+    if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -295,7 +313,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         part *= scale * scale;
         if (P.use_linear && tid < F && s_idx[tid] >= 0) part += w[s_idx[tid]] * s_x[tid] * scale;
         float p = hm::block_sum(part, s_red);
-        if (P.use_bias) p += bias[0];
+        if (P.use_bias) p += bias_w0(P, bias);
 
         // ---- 4. loss ----
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
@@ -491,7 +509,7 @@ __global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_p
         part *= scale * scale;
         if (P.use_linear && tid < F) part += lw * s_x[tid] * scale;   // lw = 0 for padding
         float p = hm::block_sum(part, s_red);
-        if (P.use_bias) p += bias[0];
+        if (P.use_bias) p += bias_w0(P, bias);
 
         // ---- 4. loss ----
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
@@ -544,8 +562,7 @@ __global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_p
                     w[i] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
-            if (P.use_bias && tid == 0)
-                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
         __syncthreads();  // LDS reuse by the next row
     }
@@ -703,7 +720,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;                       // mx = 0 for tid >= F / padding
         float p = hm::block_sum(part, s_red);
-        if (P.use_bias) p += bias[0];
+        if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- AdaGrad(V) update (Hogwild), packed fp32 math; only the store is predicated ----
@@ -764,8 +781,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
                 wn[mi] = n1;
                 w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
             }
-            if (P.use_bias && tid == 0)
-                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
         __syncthreads();
     }
@@ -969,7 +985,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         if (lane == 0) s_red[wave] = part;
         bar_raw();
         float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-        if (P.use_bias) p += bias[0];
+        if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- E: updates ----
@@ -1023,8 +1039,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                     w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
-            if (P.use_bias && tid == 0)
-                bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, P.alpha, P.beta, 0.f, 0.f);
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
         if (more) dma_lin(nxt);

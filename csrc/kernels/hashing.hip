@@ -9,35 +9,11 @@
 // window are hashed straight from global memory).  Output = raw hash (uint32) or mhash
 // ((int)h % num_features, negatives fixed up, +1) — bit-exact with the Java/C++ versions.
 #include "common.h"
+#include "murmur3.h"
 
 namespace {
 
 constexpr int HASH_LDS = 16 * 1024;
-
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-
-template <typename LoadByte>
-__device__ __forceinline__ uint32_t murmur3(LoadByte at, int len, uint32_t seed) {
-    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
-    uint32_t h1 = seed;
-    const int nblocks = len >> 2;
-    for (int i = 0; i < nblocks; ++i) {
-        uint32_t k1 = (uint32_t)at(4 * i) | ((uint32_t)at(4 * i + 1) << 8) |
-                      ((uint32_t)at(4 * i + 2) << 16) | ((uint32_t)at(4 * i + 3) << 24);
-        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
-        h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
-    }
-    uint32_t k1 = 0;
-    const int t = nblocks * 4;
-    switch (len & 3) {
-        case 3: k1 ^= (uint32_t)at(t + 2) << 16; [[fallthrough]];
-        case 2: k1 ^= (uint32_t)at(t + 1) << 8; [[fallthrough]];
-        case 1: k1 ^= (uint32_t)at(t); k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
-    }
-    h1 ^= (uint32_t)len;
-    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu; h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u; h1 ^= h1 >> 16;
-    return h1;
-}
 
 __global__ __launch_bounds__(256) void mhash_kernel(const uint8_t* __restrict__ buf,
                                                     const int64_t* __restrict__ off, int64_t n,
@@ -74,10 +50,10 @@ __global__ __launch_bounds__(256) void mhash_kernel(const uint8_t* __restrict__ 
             const int len = (int)(e - b);
             uint32_t h;
             if (e <= staged) {
-                h = murmur3([&](int i) { return s_buf[b + i]; }, len, seed);
+                h = hm::murmur3([&](int i) { return s_buf[b + i]; }, len, seed);
             } else {
                 const uint8_t* g = buf + span0 + b;
-                h = murmur3([&](int i) { return g[i]; }, len, seed);
+                h = hm::murmur3([&](int i) { return g[i]; }, len, seed);
             }
             if (num_features > 0) {
                 int32_t r = (int32_t)h % num_features;

@@ -66,6 +66,28 @@ def _signature(name: str):
     return _LIN_BIN
 
 
+def _column(a, arrow_ok: bool):
+    """A UDTF argument column: Arrow-backed columns stay Arrow for learners that ingest Arrow
+    buffers on the device (``ARROW_INPUT``, e.g. train_ffm), everything else becomes a list."""
+    import pandas as pd
+
+    if arrow_ok and isinstance(a, pd.Series) and isinstance(a.dtype, pd.ArrowDtype):
+        arr = a.array._pa_array
+        return arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
+    if isinstance(a, pd.Series) and isinstance(a.dtype, pd.ArrowDtype):
+        return a.array._pa_array.to_pylist()
+    return list(a)
+
+
+def _rows(d, rank: int, world: int):
+    """Rows rank, rank + world, ... of a list or an Arrow array."""
+    if isinstance(d, list):
+        return d[rank::world]
+    import pyarrow as pa
+
+    return d.take(pa.array(range(rank, len(d), world), type=pa.int64()))
+
+
 def _dist(session):
     ctx = getattr(session, "ctx", None)
     return ctx if (ctx is not None and ctx.world_size > 1) else None
@@ -84,7 +106,7 @@ def _learner_udtf(name, cls_getter, n_data_args=2):
     def impl(*args, session=None):
         cls = cls_getter()
         opts = _opt_arg(args, n_data_args)
-        data = [list(a) for a in args[:n_data_args]]
+        data = [_column(a, getattr(cls, "ARROW_INPUT", False)) for a in args[:n_data_args]]
         ctx = _dist(session)
         if ctx is None:
             m = cls(opts, device=_device(session))
@@ -95,7 +117,7 @@ def _learner_udtf(name, cls_getter, n_data_args=2):
         mode = getattr(cls, "SQL_DP", "replicate")
         kw = {}
         if mode == "shard":
-            data = [d[ctx.rank::ctx.world_size] for d in data]
+            data = [_rows(d, ctx.rank, ctx.world_size) for d in data]
             kw = dict(mixer=ModelMixer(ctx), rank=ctx.rank)
         elif mode == "union":
             kw = dict(mixer=ModelMixer(ctx), rank=ctx.rank)

@@ -30,6 +30,7 @@ import pandas as pd
 import torch
 
 from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
+from ..io.ingest import is_arrow_like as ingest_is_arrow
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
 from .base import COMMON_ITER_OPTS, ConversionState, Learner, log, parse_labels_binary
@@ -64,6 +65,7 @@ def csr_to_ffm_batch(csr: CSR, y: np.ndarray | None, width: int | None = None) -
 class FFMTrainer(Learner):
     NAME = "train_ffm"
     SQL_DP = "shard"
+    ARROW_INPUT = True      # Arrow list<string> feature columns are parsed on the device
     OPTIONS = COMMON_ITER_OPTS + [
         flag("classification", "c", "Act as classification (logistic loss); labels 0/1 or -1/1"),
         opt("factors", "factor", 4, int, "The number of latent factors k", aliases=("k",)),
@@ -151,18 +153,35 @@ class FFMTrainer(Learner):
 
     # ------------------------------------------------------------------ data
     def prepare(self, features, labels=None) -> FFMBatch:
-        """Rows of ``field:index[:value]`` strings -> device-resident padded-ELL batch."""
+        """Rows of ``field:index[:value]`` strings -> device-resident padded-ELL batch.
+
+        On the GPU the strings are parsed and hashed there (io/ingest.py: Arrow buffers ->
+        pinned double-buffered H2D -> hm_ffm_parse); on the CPU by the host parser."""
         nf = self.num_features if self.num_features is not None else (1 << 24)
         nfld = self.num_fields if self.num_fields is not None else 1 << 15
+        y = None
+        if labels is not None:
+            y = parse_labels_binary(labels) if self.hyper.classification else \
+                np.asarray(labels, dtype=np.float32).reshape(-1)
+        if self.device.type == "cuda":
+            from ..io import ingest
+
+            idx, fld, val = ingest.ffm_ell_device(features, nf, nfld,
+                                                  hash_ints=self.cl["feature_hashing"] > 0,
+                                                  device=self.device)[:3]
+            if self.num_features is None:
+                self.num_features = int(idx.max().item()) + 1 if idx.numel() else 1
+            if self.num_fields is None:
+                self.num_fields = int(fld.max().item()) + 1 if fld.numel() else 1
+            yt = None if y is None else torch.from_numpy(y).to(self.device)
+            return FFMBatch(idx, fld, val, yt)
+        if ingest_is_arrow(features):
+            features = features.to_pylist() if hasattr(features, "to_pylist") else list(features)
         csr = parse_ffm_rows(features, nf, nfld, hash_ints=self.cl["feature_hashing"] > 0)
         if self.num_features is None:
             self.num_features = int(csr.idx.max()) + 1 if csr.nnz else 1
         if self.num_fields is None:
             self.num_fields = int(csr.fld.max()) + 1 if csr.nnz else 1
-        y = None
-        if labels is not None:
-            y = parse_labels_binary(labels) if self.hyper.classification else \
-                np.asarray(labels, dtype=np.float32).reshape(-1)
         return csr_to_ffm_batch(csr, y).to(self.device)
 
     def _ensure_state(self):

@@ -31,6 +31,26 @@ from ..utils.options import UDFArgumentException, flag, opt
 from .base import MIX_OPTS, ConversionState, Learner, log, parse_labels_binary
 from .linear import SparseRows, encode_rows
 
+
+def _is_arrow(x) -> bool:
+    from ..io.ingest import is_arrow_like
+
+    return is_arrow_like(x)
+
+
+def _string_rows(rows) -> bool:
+    """Rows of feature strings (Arrow list<string>, or Python lists whose first row holds str)."""
+    if _is_arrow(rows):
+        import pyarrow as pa
+
+        t = rows.dtype.pyarrow_dtype if hasattr(rows, "dtype") and hasattr(rows.dtype, "pyarrow_dtype") \
+            else rows.type
+        return (pa.types.is_list(t) or pa.types.is_large_list(t)) and \
+            (pa.types.is_string(t.value_type) or pa.types.is_large_string(t.value_type))
+    first = next((r for r in rows if r is not None and len(r)), None)
+    return first is not None and all(isinstance(v, str) for v in first)
+
+
 FM_OPTS = [
     flag("classification", "c", "Act as classification"),
     opt("factors", "factor", 5, int, "The number of latent factors", aliases=("k",)),
@@ -64,6 +84,7 @@ _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
 
 class FMTrainer(Learner):
     SQL_DP = "shard"
+    ARROW_INPUT = True      # Arrow list<string> rows are parsed on the device (-feature_hashing)
     NAME = "train_fm"
     OPTIONS = FM_OPTS
 
@@ -115,11 +136,23 @@ class FMTrainer(Learner):
 
     # ------------------------------------------------------------------ data
     def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
-        csr, self.encoder = encode_rows(features, self.encoder, train)
+        """Feature rows -> device CSR.  With -feature_hashing on the GPU, string rows are parsed
+        and mhash'd there (io/ingest.py, hm_feat_parse); otherwise by the host encoder."""
         y = None
         if labels is not None:
             y = parse_labels_binary(labels) if self.h.classification else \
                 np.asarray(labels, dtype=np.float32).reshape(-1)
+        if (self.device.type == "cuda" and self.encoder is not None and self.encoder.mode == "hash"
+                and not isinstance(features, CSR) and _string_rows(features)):
+            from ..io import ingest
+
+            ip, idx, val, _ = ingest.csr_device(features, "hash", self.encoder.num_features,
+                                                device=self.device, seed=self.encoder.seed)
+            yt = None if y is None else torch.from_numpy(y).to(self.device)
+            return SparseRows(ip, idx.to(torch.int32), val, yt)
+        if not isinstance(features, (list, CSR)) and _is_arrow(features):
+            features = features.to_pylist()
+        csr, self.encoder = encode_rows(features, self.encoder, train)
         return SparseRows.from_csr(csr, y, self.device)
 
     def _ensure(self, rows: SparseRows):

@@ -54,6 +54,13 @@ LEARNER_BASE_OPTS = [
     flag("disable_cv", "disable_cvtest", "Whether to disable convergence check"),
     opt("seed", None, -1, int, "Seed value"),
     opt("replicas", None, 0, int, "[engine] model replicas (0 = auto; CPU default 1)"),
+    opt("engine", None, "auto", str,
+        "[engine] GPU execution: replica (private model per wave, mixed), shared (one Hogwild "
+        "table for the whole chip, large -dims), auto (shared when the replicas would exceed "
+        "2 GiB)"),
+    opt("shared_replicas", None, 8, int,
+        "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
+        "after every pass"),
 ]
 
 GENERAL_OPTS = [
@@ -275,12 +282,36 @@ class OnlineLinearLearner(Learner):
         self.P.n_labels = L
         R = self._auto_replicas(rows.n)
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
+        if self._use_shared(R, L, dims, mb):
+            try:
+                self.state = LO.new_shared_state(dims, self.device, rows.n,
+                                                 replicas=int(self.cl["shared_replicas"]))
+            except ValueError as e:
+                raise UDFArgumentException(f"{self.NAME}: {e}") from None
+            if self._warm is not None:
+                self.load_model_table(self._warm)
+            return
         bytes_ = R * L * dims * 16
         if bytes_ > (32 << 30):
             R = max(1, (32 << 30) // (L * dims * 16))
         self.state = LO.new_state(R, L, dims, self.device, self.covar, self.P.init_covar, mb)
         if self._warm is not None:
             self.load_model_table(self._warm)
+
+    def _use_shared(self, R: int, L: int, dims: int, mb: int) -> bool:
+        """Shared-table Hogwild engine: device only, binary/regression rules
+        without covariance, per-row updates.  auto picks it when R private replicas of
+        ``dims x 16 B`` would exceed 2 GiB (e.g. Hivemall's default 2^24 hashed dims)."""
+        eng = str(self.cl["engine"]).lower()
+        if eng not in ("auto", "replica", "shared"):
+            raise UDFArgumentException(f"{self.NAME}: -engine must be auto, replica or shared")
+        ok = (self.device.type == "cuda" and not self.covar and L == 1 and mb == 1)
+        if eng == "shared" and not ok:
+            raise UDFArgumentException(f"{self.NAME}: -engine shared needs a GPU, a rule without "
+                                       "covariance, a binary/regression task and -mini_batch 1")
+        if eng == "replica" or not ok or int(self.cl["replicas"]) > 0:
+            return eng == "shared"
+        return eng == "shared" or R * dims * 16 > (2 << 30)
 
     # ------------------------------------------------------------------ training
     def fit(self, features=None, labels=None, rows: SparseRows | None = None) -> "OnlineLinearLearner":
@@ -292,9 +323,14 @@ class OnlineLinearLearner(Learner):
             log.warning("%s: feature index >= dims (%d) ignored", self.NAME, self.state.dims)
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         iters = int(self.cl["iters"])
+        shared = self.state.meta.get("shared", False)
         for ep in range(iters):
-            loss = LO.train_pass(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
-                                 None, mb)
+            if shared:
+                loss = LO.train_pass_shared(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
+                                            self.rows_seen)
+            else:
+                loss = LO.train_pass(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
+                                     None, mb)
             self.rows_seen += rows.n
             self.mix()
             self.cv.incr_loss(float(loss.sum().item()))

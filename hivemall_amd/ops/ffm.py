@@ -137,6 +137,11 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     if V.is_cuda:
         rc = _native.hip().hm_ffm_step(*args, _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
+        if train and hyper.use_bias:
+            # w0 = f(z0, n0): the kernel accumulates z0/n0 atomically and its cached bias[0] is
+            # whichever block wrote last; refresh it (FTRL weight with l1 = l2 = 0)
+            b = state["bias"]
+            b[0] = -b[1] / ((hyper.beta + b[2].sqrt()) / hyper.alpha)
     else:
         rc = _native.host().hm_ffm_step_cpu(*args)
         if rc != 0:

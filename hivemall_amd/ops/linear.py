@@ -137,6 +137,57 @@ def train_pass(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.T
     return loss
 
 
+SHARED_WAVES = 8192      # 256 CUs x 4 SIMDs x 8 waves: every wave slot of an MI355X
+
+
+def shared_waves(n_rows: int) -> int:
+    """Waves of a shared-table pass: enough rows per wave to amortise its scalars, at most one
+    full chip of wave slots."""
+    return int(max(1, min(SHARED_WAVES, n_rows // 8)))
+
+
+def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, replicas: int = 8,
+                     reload: bool = False) -> LinearState:
+    """Shared-table Hogwild state (csrc/kernels/linear.hip linear_shared_kernel): ``replicas``
+    tables S [R, 1, dims, 4] each shared by the waves of one XCD (R = 1 or a multiple of 8),
+    touched [R, dims], per-wave scalars RS [W, 8]."""
+    W = int(waves) if waves else shared_waves(n_rows)
+    R = int(replicas)
+    if R != 1 and (R % 8 or (W + 3) // 4 < R):
+        raise ValueError(f"shared engine: replicas must be 1 or a multiple of 8 with >= 4 * R waves "
+                         f"(R={R}, W={W})")
+    st = LinearState(torch.zeros((R, 1, dims, 4), dtype=torch.float32, device=device),
+                     torch.zeros((R, dims), dtype=torch.uint8, device=device),
+                     torch.zeros((W, 8), dtype=torch.float32, device=device), False)
+    st.meta["shared"] = True
+    st.meta["reload"] = bool(reload)
+    return st
+
+
+def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.Tensor,
+                      val: torch.Tensor | None, y: torch.Tensor, t0: int,
+                      order: torch.Tensor | None = None) -> torch.Tensor:
+    """One Hogwild pass of the shared tables over the rows; step of row q = t0 + q + 1.  Returns
+    per-wave loss sums."""
+    n = indptr.numel() - 1
+    dev = st.device
+    assert dev.type == "cuda", "the shared-table engine is a device engine"
+    assert indptr.dtype == torch.int64 and idx.dtype == torch.int32 and y.dtype == torch.float32
+    assert y.numel() >= n and (val is None or val.numel() == idx.numel())
+    for t in (indptr, idx, val, y, order):
+        if t is not None:
+            assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    W = st.RS.shape[0]
+    loss = torch.zeros(W, dtype=torch.float64, device=dev)
+    p = _native.ptr
+    rc = _native.hip().hm_linear_train_shared(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
+                                              st.R, int(st.meta.get("reload", False)),
+                                              p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
+                                              p(st.touched), p(st.RS), p(loss), _native.stream_of(dev))
+    _native.check(rc, "hm_linear_train_shared")
+    return loss
+
+
 def mix_reduce(st: LinearState, kld: bool):
     """Compact per-element sums (num, den, cnt) over the touching replicas."""
     R, L, dims = st.R, st.L, st.dims
@@ -215,6 +266,8 @@ def predict_scores(w: torch.Tensor, indptr: torch.Tensor, idx: torch.Tensor,
 _P = _native.c_p
 _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
+_native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
+                                              C.c_int] + [_P] * 9 + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
 _native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])

@@ -174,6 +174,26 @@ def test_ffm_gpu_single_block_is_exactly_sequential():
 
 
 @pytest.mark.gpu
+def test_ffm_gpu_global_bias_loses_no_updates():
+    """-w0: every block updates the one global bias; its FTRL state (z0, n0) is accumulated
+    atomically, so n0 = sum over rows of the squared row gradient |kappa| = 1 - exp(-loss)
+    (a plain read-modify-write from thousands of blocks loses most of them), and the cached
+    w0 = f(z0, n0)."""
+    torch.manual_seed(0)
+    B, F = 4096, 8
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F).cuda()   # only the bias is shared
+    y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0).cuda()
+    t = _trainer("cuda", B * F, F, extra="-w0")
+    loss = torch.empty(B, device="cuda")
+    ffm_step(t.state, idx, None, None, y, t.hyper, loss=loss)
+    b = t.state["bias"].cpu().double()
+    n_rows = ((1 - torch.exp(-loss.double())) ** 2).sum().item()
+    assert n_rows > 100 and abs(b[2].item() - n_rows) / n_rows < 1e-3, (b[2].item(), n_rows)
+    w0 = -b[1].item() / ((t.hyper.beta + b[2].sqrt().item()) / t.hyper.alpha)
+    assert abs(b[0].item() - w0) < 1e-5
+
+
+@pytest.mark.gpu
 def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
     """Full-chip Hogwild vs the sequential engine at 500K rows (measured gap ~0.01, shrinking
     with data: profiles/ffm_parity_r1.log)."""

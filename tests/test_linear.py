@@ -178,3 +178,73 @@ def test_gpu_large_model_not_in_lds():
         m = L.TrainClassifier("-loss logloss -iters 2 -replicas 8", device=dev).fit(rows, y)
         res[dev] = m.weights()[0].cpu().numpy()
     np.testing.assert_allclose(res["cuda"], res["cpu"], rtol=5e-3, atol=5e-4)
+
+
+def _criteo_rows(n, bits, seed, distinct=False):
+    """Criteo-shaped hashed rows as SparseRows; ``distinct``: field j maps into its own index
+    range, so no row holds a feature twice (sequential and per-lane updates then agree)."""
+    from hivemall_amd.io.synthetic import criteo_like
+
+    idx, y = criteo_like(n, hash_bits=bits, seed=seed)
+    F = idx.shape[1]
+    if distinct:
+        span = (1 << bits) // F
+        idx = (torch.arange(F, dtype=torch.int32) * span + idx % span).to(torch.int32)
+    return L.SparseRows(torch.arange(0, n * F + 1, F, dtype=torch.int64), idx.reshape(-1).contiguous(),
+                        None, y.contiguous())
+
+
+def test_shared_engine_selection_rules():
+    """auto keeps replicas on CPU / for covariance rules; -engine shared is refused where the
+    shared-table kernel cannot run."""
+    m = L.TrainClassifier("-loss logloss -dims 16777216", device="cpu")
+    assert not m._use_shared(1, 1, 1 << 24, 1)
+    with pytest.raises(UDFArgumentException):
+        L.TrainClassifier("-engine shared", device="cpu")._use_shared(1, 1, 100, 1)
+    with pytest.raises(UDFArgumentException):
+        L.TrainClassifier("-engine bogus", device="cpu")._use_shared(1, 1, 100, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reload", [True, False])
+@pytest.mark.parametrize("name,opts", [("train_classifier", "-loss logloss -opt adagrad"),
+                                       ("train_classifier", "-loss hinge -opt adam -reg l2"),
+                                       ("train_pa1", ""), ("train_logregr", ""),
+                                       ("train_pa2a_regr", "")])
+def test_gpu_shared_engine_one_wave_is_sequential(name, opts, reload):
+    """The shared-table kernel with ONE wave walks the rows in order with step t0 + q + 1: the
+    sequential learner, i.e. the CPU engine with one replica (two passes: t0 carries over)."""
+    from hivemall_amd.ops import linear as LO
+
+    rows = _criteo_rows(3000, 12, seed=3, distinct=True)
+    if "regr" in name:
+        rows.y = (rows.idx.view(-1, 39)[:, :4].float().sum(1) / 8192.0).contiguous()
+    cpu = L.LEARNERS[name](opts + " -replicas 1", device="cpu")
+    cpu._ensure_state(rows)
+    st = LO.new_shared_state(cpu.state.dims, "cuda", rows.n, waves=1, replicas=1, reload=reload)
+    rg = rows.to("cuda")
+    for ep in range(2):
+        LO.train_pass(cpu.state, cpu.P, rows.indptr, rows.idx, rows.val, rows.y)
+        LO.train_pass_shared(st, cpu.P, rg.indptr, rg.idx, rg.val, rg.y, t0=ep * rows.n)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(st.S[0, 0].cpu().numpy(), cpu.state.S[0, 0].numpy(), rtol=2e-4, atol=2e-5)
+    assert torch.equal(st.touched[0].cpu(), cpu.state.touched[0])
+
+
+@pytest.mark.gpu
+def test_gpu_shared_engine_hashed_2p24_logloss_parity():
+    """Hivemall's default -dims 2^24 (hashed Criteo-shaped rows, 39 nnz): auto picks the shared
+    table; full-chip Hogwild (XCD-local replicas, averaged) held-out logloss within 0.01 of the
+    sequential CPU engine."""
+    rows = _criteo_rows(200000, 24, seed=5)
+    test = _criteo_rows(50000, 24, seed=99)
+    yy = (test.y > 0).float()
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = L.TrainClassifier("-loss logloss -opt adagrad -dims 16777216", device=dev)
+        m.fit(rows=rows.to(dev))
+        if dev == "cuda":
+            assert m.state.meta.get("shared") and m.state.RS.shape[0] > 1000
+        s = m.decision_function(rows=test.to(dev)).cpu()
+        res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
+    assert abs(res["cpu"] - res["cuda"]) < 0.01, res
