@@ -37,20 +37,20 @@ def main():
         print(json.dumps({"engine": "cpu sequential", "rows": N, "rows_per_s": round(N / dt),
                           "heldout_logloss": round(heldout(m, te_c), 5)}), flush=True)
     tr, te = tr_c.to("cuda"), te_c.to("cuda")
-    grid = [(R, W, rl) for R in (1, 8, 32, 64, 128) for W in (8192, 2048) for rl in (False, True)
-            if (W + 3) // 4 >= R]
-    for R, W, reload in grid:
+    grid = [(R, W, rl, nt) for nt in (True, False) for R in (1, 8, 32) for W in (8192, 2048, 512)
+            for rl in (False, True) if (W + 3) // 4 >= R and not (not nt and W == 512)]
+    for R, W, reload, nt in grid:
         m = L.TrainClassifier(f"-loss logloss -opt adagrad -dims {1 << BITS} -engine shared", device="cuda")
         m._ensure_state(tr)
-        m.state = LO.new_shared_state(1 << BITS, "cuda", N, waves=W, replicas=R, reload=reload)
+        m.state = LO.new_shared_state(1 << BITS, "cuda", N, waves=W, replicas=R, reload=reload, nt=nt)
         LO.train_pass_shared(m.state, m.P, tr.indptr, tr.idx, tr.val, tr.y, 0)     # warm (code load)
-        m.state = LO.new_shared_state(1 << BITS, "cuda", N, waves=W, replicas=R, reload=reload)
+        m.state = LO.new_shared_state(1 << BITS, "cuda", N, waves=W, replicas=R, reload=reload, nt=nt)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         m.fit(rows=tr)                      # one pass + the replica mix
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"engine": "shared", "replicas": R, "waves": W, "reload": reload, "rows": N,
+        print(json.dumps({"engine": "shared", "replicas": R, "waves": W, "reload": reload, "nt": nt, "rows": N,
                           "rows_per_s": round(N / dt), "heldout_logloss": round(heldout(m, te), 5)}),
               flush=True)
         del m

@@ -20,7 +20,7 @@ from .tools import functions as _tools  # noqa: F401
 
 
 def _opt_arg(args, k):
-    if len(args) > k and args[k]:
+    if len(args) > k and len(args[k]):
         v = args[k][0]
         return None if v is None else str(v)
     return None
@@ -76,7 +76,7 @@ def _column(a, arrow_ok: bool):
         return arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
     if isinstance(a, pd.Series) and isinstance(a.dtype, pd.ArrowDtype):
         return a.array._pa_array.to_pylist()
-    return list(a)
+    return a.tolist() if isinstance(a, pd.Series) else list(a)
 
 
 def _rows(d, rank: int, world: int):
@@ -132,6 +132,7 @@ def _learner_udtf(name, cls_getter, n_data_args=2):
             tab = pd.concat(parts, ignore_index=True)
         return tab
     impl.wants_session = True
+    impl.accepts_series = True      # argument columns arrive as Series (Arrow buffers kept)
     ins, outs = _signature(name)
     impl.__doc__ = f"{name}({ins} [, const string options]) -> table ({outs})"
     registry._register(registry.FunctionDef(name, registry.UDTF, impl, per_row=False,

@@ -267,12 +267,24 @@ class FFMTrainer(Learner):
         ids = ids.cpu().numpy().astype(np.int64)
         vkeys = (NF + ids[:, None] * F + np.arange(F)[None, :]).reshape(-1)
         n_lin = len(ids)
+        n = 1 + n_lin + len(vkeys)
+        # columnar build (tens of millions of rows at 2^20 features x 39 fields): model_id is a
+        # one-category categorical, Vi an Arrow list<float> over the V buffer (NULL for the bias
+        # and linear rows) — no per-row Python objects
+        import pyarrow as pa
+
+        offs = np.concatenate([np.zeros(1 + n_lin, np.int32),
+                               np.arange(1, len(vkeys) + 1, dtype=np.int64).astype(np.int32) * k])
+        offs = np.concatenate([[0], offs]).astype(np.int32)
+        valid = np.concatenate([np.zeros(1 + n_lin, bool), np.ones(len(vkeys), bool)])
+        vi = pa.ListArray.from_arrays(pa.array(offs), pa.array(V.reshape(-1).astype(np.float32)),
+                                      mask=pa.array(~valid))
         return pd.DataFrame({
-            "model_id": [mid] * (1 + n_lin + len(vkeys)),
+            "model_id": pd.Categorical.from_codes(np.zeros(n, np.int8), [mid]),
             "i": np.concatenate([[-1], ids, vkeys]).astype(np.int64),
             "Wi": np.concatenate([[float(self.state["bias"][0].item())], W,
                                   np.full(len(vkeys), np.nan)]).astype(np.float32),
-            "Vi": [None] * (1 + n_lin) + list(V)})
+            "Vi": pd.Series(vi, dtype=pd.ArrowDtype(vi.type))})
 
     def state_dict(self) -> dict:
         return {k: v.detach().cpu().contiguous() for k, v in (self.state or {}).items()} | {

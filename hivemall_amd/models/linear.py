@@ -58,9 +58,11 @@ LEARNER_BASE_OPTS = [
         "[engine] GPU execution: replica (private model per wave, mixed), shared (one Hogwild "
         "table for the whole chip, large -dims), auto (shared when the replicas would exceed "
         "2 GiB)"),
-    opt("shared_replicas", None, 8, int,
+    opt("shared_replicas", None, 1, int,
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
+    opt("shared_waves", None, 512, int,
+        "[engine] shared engine: rows in flight (more = faster, staler hot features)"),
 ]
 
 GENERAL_OPTS = [
@@ -284,8 +286,9 @@ class OnlineLinearLearner(Learner):
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         if self._use_shared(R, L, dims, mb):
             try:
-                self.state = LO.new_shared_state(dims, self.device, rows.n,
-                                                 replicas=int(self.cl["shared_replicas"]))
+                self.state = LO.new_shared_state(
+                    dims, self.device, rows.n, replicas=int(self.cl["shared_replicas"]),
+                    waves=LO.shared_waves(rows.n, max(1, int(self.cl["shared_waves"]))))
             except ValueError as e:
                 raise UDFArgumentException(f"{self.NAME}: {e}") from None
             if self._warm is not None:

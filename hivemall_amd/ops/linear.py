@@ -137,17 +137,22 @@ def train_pass(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.T
     return loss
 
 
-SHARED_WAVES = 8192      # 256 CUs x 4 SIMDs x 8 waves: every wave slot of an MI355X
+# Rows in flight = waves.  The Hogwild quality knob: a hot feature of a Zipf stream is read and
+# rewritten by every concurrent row that holds it, so the fraction of its updates that survive
+# falls with concurrency.  Measured on 2M Criteo-shaped rows at 2^24 dims, one AdaGrad epoch
+# (sequential CPU engine: held-out logloss 0.4789; profiles/linear_shared_r2o_nt.log):
+#   8192 waves 0.623-0.670 @ 65-230 M rows/s, 2048: 0.513-0.553 @ 108-183 M, 512: 0.4985 @ 47-56 M
+SHARED_WAVES = 512
 
 
-def shared_waves(n_rows: int) -> int:
-    """Waves of a shared-table pass: enough rows per wave to amortise its scalars, at most one
-    full chip of wave slots."""
-    return int(max(1, min(SHARED_WAVES, n_rows // 8)))
+def shared_waves(n_rows: int, cap: int = SHARED_WAVES) -> int:
+    """Waves of a shared-table pass: enough rows per wave to amortise its scalars, at most
+    ``cap`` rows in flight."""
+    return int(max(1, min(cap, n_rows // 8)))
 
 
-def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, replicas: int = 8,
-                     reload: bool = False) -> LinearState:
+def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, replicas: int = 1,
+                     reload: bool = True, nt: bool = True) -> LinearState:
     """Shared-table Hogwild state (csrc/kernels/linear.hip linear_shared_kernel): ``replicas``
     tables S [R, 1, dims, 4] each shared by the waves of one XCD (R = 1 or a multiple of 8),
     touched [R, dims], per-wave scalars RS [W, 8]."""
@@ -161,6 +166,7 @@ def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, r
                      torch.zeros((W, 8), dtype=torch.float32, device=device), False)
     st.meta["shared"] = True
     st.meta["reload"] = bool(reload)
+    st.meta["nt"] = bool(nt)
     return st
 
 
@@ -182,6 +188,7 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     p = _native.ptr
     rc = _native.hip().hm_linear_train_shared(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
                                               st.R, int(st.meta.get("reload", False)),
+                                              int(st.meta.get("nt", True)),
                                               p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
                                               p(st.touched), p(st.RS), p(loss), _native.stream_of(dev))
     _native.check(rc, "hm_linear_train_shared")
@@ -267,7 +274,7 @@ _P = _native.c_p
 _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
-                                              C.c_int] + [_P] * 9 + [_P])
+                                              C.c_int, C.c_int] + [_P] * 9 + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
 _native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])

@@ -679,7 +679,12 @@ class Session:
     def _select_udtf(self, item: SelectItem, src: Frame, ctes) -> Frame:
         f = item.expr
         impl, per_row, default_cols = self._table_fn(f.name)
-        args = [_ser(self.eval(a, src, ctes), src.n).tolist() for a in f.args]
+        if not per_row and getattr(impl, "accepts_series", False):
+            # learner UDTFs take whole columns; an Arrow-backed column reaches the device
+            # ingest as its buffers instead of millions of Python lists
+            args = [_ser(self.eval(a, src, ctes), src.n).reset_index(drop=True) for a in f.args]
+        else:
+            args = [_ser(self.eval(a, src, ctes), src.n).tolist() for a in f.args]
         if per_row:
             rows = []
             for r in range(src.n):
