@@ -57,6 +57,9 @@ def parse_args(argv=None):
                     help="1: re-read the own slot right before its update (short Hogwild window); "
                          "0: keep the gathered slot in registers; -1: by layout (packed -> 0)")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--gen-device", choices=("auto", "cpu"), default="auto",
+                    help="where the synthetic rows are drawn (cpu = the exact stream of "
+                         "benchmarks/ffm_parity_bench_scale.py, copied to the GPU before timing)")
     ap.add_argument("--mix-probe", type=int, default=3,
                     help="synchronous mixes timed after the run (ms, wire bytes, bus GB/s)")
     return ap.parse_args(argv)
@@ -128,7 +131,9 @@ def main(argv=None):
     nres = max(1, args.resident_batches)
 
     # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
-    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=dev)
+    gdev = torch.device("cpu") if args.gen_device == "cpu" else dev
+    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=gdev)
+    idx, y = idx.to(dev), y.to(dev)
     opts = (f"-classification -factors {args.factors} -feature_hashing {args.hash_bits} "
             f"-num_fields {F} -seed 31 -batch_size {B}" +
             (" -bf16_state" if args.state == "bf16" and dev.type == "cuda" else "") +
@@ -194,8 +199,9 @@ def main(argv=None):
         mixer.average(mix_tensors)
     ll = floor = None
     if rank == 0:
-        eidx, ey, elogit = criteo_like(args.eval_rows, args.hash_bits, seed=999_999, device=dev,
+        eidx, ey, elogit = criteo_like(args.eval_rows, args.hash_bits, seed=999_999, device=gdev,
                                        return_logit=True)
+        eidx, ey, elogit = eidx.to(dev), ey.to(dev), elogit.to(dev)
         pred = torch.empty(args.eval_rows, dtype=torch.float32, device=dev)
         for s in range(0, args.eval_rows, B):
             e = min(args.eval_rows, s + B)

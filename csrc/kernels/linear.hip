@@ -321,9 +321,24 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
 // 0.479 at 8192 waves); float-atomic deltas lose nothing but serialise on the hot addresses
 // (1.7 M rows/s) and diverge from stale AdaGrad state.
 // RELOAD re-reads a feature's state right before updating it (shorter read-modify-write window).
+// NT reads the model with non-temporal loads, which bypass the CU's L1: a CU's L1 is never
+// refreshed by other CUs' stores, so plain loads of a hot feature keep returning the copy the
+// CU first cached while the other CUs of the XCD update it in L2.
 // Per-wave scalars (online target variance, Eve) live in RSW [W][8].  Non-covariance binary /
 // regression rules only (covariance learners keep one replica per wave, mixed by argmin-KLD).
-template <bool RELOAD>
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ F4 ld4m(const float4* p) {
+    if constexpr (NT) {
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        return F4{v.x, v.y, v.z, v.w};
+    } else {
+        return ld4(p);
+    }
+}
+
+template <bool RELOAD, bool NT>
 __global__ __launch_bounds__(256) void linear_shared_kernel(
     Params P, int64_t n_rows, int dims, int64_t t0, int W, int R, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
@@ -357,7 +372,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
         F4 cst = {0.f, 0.f, 0.f, 0.f};
         float p = 0.f, sq = 0.f;
         if (ci >= 0) {
-            cst = ld4(S + ci);
+            cst = ld4m<NT>(S + ci);
             p = cst.w * cx;
             sq = cx * cx;
         }
@@ -365,7 +380,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             const int i = idx[k];
             const float x = val ? val[k] : 1.f;
             if (i < 0 || i >= dims) continue;
-            p += ld4(S + i).w * x;
+            p += ld4m<NT>(S + i).w * x;
             sq += x * x;
         }
         p = hm::wave_sum(p);
@@ -375,7 +390,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
         if (ci >= 0) {
             touched[ci] = 1;
             if (c.update) {
-                if (RELOAD) cst = ld4(S + ci);
+                if (RELOAD) cst = ld4m<NT>(S + ci);
                 feature_update(P, c, cst, cx, t, rs[RS_EVE_D]);
                 st4(S + ci, cst);
             }
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             if (i < 0 || i >= dims) continue;
             touched[i] = 1;
             if (!c.update) continue;
-            F4 st = ld4(S + i);
+            F4 st = ld4m<NT>(S + i);
             feature_update(P, c, st, x, t, rs[RS_EVE_D]);
             st4(S + i, st);
         }
@@ -463,19 +478,20 @@ HM_API int hm_linear_predict(const float* w, int dims, int L, const int64_t* ind
 // [R][dims]; W waves (RSW f32 [W][8], loss_out f64 [W]); R = 1 or a multiple of 8 with W / 4 >= R
 // workgroups so that every replica gets waves.
 HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int64_t t0, int W, int R,
-                                  int reload, const int64_t* indptr, const int32_t* idx, const float* val,
+                                  int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,
                                   float* RSW, double* loss_out, hipStream_t stream) {
     if (n_rows <= 0) return 0;
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
-    if (reload)
-        hipLaunchKernelGGL(linear_shared_kernel<true>, dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows,
-                           dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,
-                           RSW, loss_out);
-    else
-        hipLaunchKernelGGL(linear_shared_kernel<false>, dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows,
-                           dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,
-                           RSW, loss_out);
+#define HM_SHARED_LAUNCH(RL, NTT)                                                                      \
+    hipLaunchKernelGGL((linear_shared_kernel<RL, NTT>), dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows, \
+                       dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
+                       RSW, loss_out)
+    if (reload && nt) HM_SHARED_LAUNCH(true, true);
+    else if (reload) HM_SHARED_LAUNCH(true, false);
+    else if (nt) HM_SHARED_LAUNCH(false, true);
+    else HM_SHARED_LAUNCH(false, false);
+#undef HM_SHARED_LAUNCH
     HM_LAUNCH_RET();
 }

@@ -59,8 +59,49 @@ def add_feature_index(values):
     return [f"{i + 1}:{_fmt(v)}" for i, v in enumerate(values) if v is not None]
 
 
-@udf("extract_feature")
-def extract_feature(f):
+_FV_RE = r"^([^:]*:[^:]*|[^:]*):(.*)$"     # _split: value after the 2nd ':' when there is one
+
+
+def _vec_split(col):
+    """Vectorised _split over a Series of feature strings (Arrow compute, C++ regex): (names
+    Series, values Series), or None when the column holds anything but strings (the per-row
+    path handles those)."""
+    import pandas as pd
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    try:
+        arr = pa.array(col.to_numpy(dtype=object), type=pa.string(), from_pandas=True)
+    except (pa.ArrowInvalid, pa.ArrowTypeError):
+        return None
+    sp = pc.split_pattern(arr, ":", max_splits=2)          # <=3 parts: name | f:i | value
+    lens = pc.fill_null(pc.list_value_length(sp), 0).to_numpy()
+    offs = sp.offsets.to_numpy()[:-1].astype(np.int64)
+    flat = pc.list_flatten(sp)
+    last = max(len(flat) - 1, 0)
+
+    def part(j):
+        return flat.take(pa.array(np.minimum(offs + j, last))) if len(flat) else pa.nulls(len(arr), pa.string())
+    three, two = pa.array(lens == 3), pa.array(lens == 2)
+    name = pc.if_else(three, pc.binary_join_element_wise(part(0), part(1), ":"),
+                      pc.if_else(two, part(0), arr))
+    vs = pc.if_else(three, part(2), pc.if_else(two, part(1), pa.scalar("1")))
+    try:
+        val = pc.cast(pc.if_else(pc.is_valid(arr), vs, pa.scalar(None, pa.string())), pa.float64())
+    except pa.ArrowInvalid as e:
+        raise ValueError(f"could not convert feature value to float: {e}") from None
+    names = pd.Series(name.to_numpy(zero_copy_only=False), index=col.index, dtype=object)
+    vals = pd.Series(val.to_numpy(zero_copy_only=False), index=col.index, dtype=np.float64)
+    return names, vals
+
+
+def _rowwise(fn, col):
+    import pandas as pd
+
+    return pd.Series([fn(v) for v in col.tolist()], dtype=object).infer_objects()
+
+
+def _extract_feature1(f):
     if f is None:
         return None
     if isinstance(f, (list, tuple, np.ndarray)):
@@ -68,13 +109,34 @@ def extract_feature(f):
     return _split(f)[0]
 
 
-@udf("extract_weight")
-def extract_weight(f):
+def _extract_weight1(f):
     if f is None:
         return None
     if isinstance(f, (list, tuple, np.ndarray)):
         return [_split(x)[1] for x in f]
     return _split(f)[1]
+
+
+@udf("extract_feature", vectorized=True)
+def extract_feature(f):
+    import pandas as pd
+
+    if isinstance(f, pd.Series):
+        sp = _vec_split(f)
+        return sp[0] if sp is not None else _rowwise(_extract_feature1, f)
+    return _extract_feature1(f)
+
+
+@udf("extract_weight", vectorized=True)
+def extract_weight(f):
+    import pandas as pd
+
+    if isinstance(f, pd.Series):
+        sp = _vec_split(f)
+        if sp is None:
+            return _rowwise(_extract_weight1, f)
+        return sp[1].where(f.notna(), None) if f.isna().any() else sp[1]
+    return _extract_weight1(f)
 
 
 @udf("feature")

@@ -224,6 +224,8 @@ class Session:
 
     def __init__(self, device=None, distributed: bool | None = None):
         self.ctx = None
+        self._prebuilt = {}          # Join id -> (L, R) frames already built by the fused path
+        self.last_plan = None        # "fused_join_predict" when the last GROUP BY ran fused
         if distributed is not False:
             import torch.distributed as tdist
 
@@ -431,8 +433,11 @@ class Session:
         return all(self._refs_only(c, fr) for c in ch) if ch else not isinstance(e, SubqueryExpr)
 
     def _join(self, j: Join, ctes) -> Frame:
-        L = self._source(j.left, ctes)
-        R = self._source(j.right, ctes)
+        if id(j) in self._prebuilt:
+            L, R = self._prebuilt.pop(id(j))
+        else:
+            L = self._source(j.left, ctes)
+            R = self._source(j.right, ctes)
         if j.kind == "cross" or j.on is None:
             li = np.repeat(np.arange(L.n), R.n)
             ri = np.tile(np.arange(R.n), L.n)
@@ -548,6 +553,10 @@ class Session:
         src = self._source(lv.source, ctes)
         impl, per_row, default_cols = self._table_fn(lv.func.name)
         args = [_ser(self.eval(a, src, ctes), src.n).tolist() for a in lv.func.args]
+        if impl is B.explode and len(args) == 1:
+            fast = self._explode_lists(src, lv, args[0])
+            if fast is not None:
+                return fast
         rows_idx, out_rows = [], []
         if per_row:
             for r in range(src.n):
@@ -571,8 +580,39 @@ class Session:
                     [(lv.table_alias, n) for n in names])
         return Frame.concat_cols(src.take(np.asarray(rows_idx, dtype=np.int64)), new)
 
+    def _explode_lists(self, src: Frame, lv: LateralView, vals: list) -> Frame | None:
+        """explode() of an array column without a Python generator per row: one flat list in C
+        (itertools.chain) and a repeat of the source row index.  Maps / non-list cells -> None
+        (the generic path handles them)."""
+        import itertools
+
+        lens = np.empty(len(vals), dtype=np.int64)
+        for i, v in enumerate(vals):
+            if isinstance(v, (list, tuple, np.ndarray)):
+                lens[i] = len(v)
+            elif v is None or (isinstance(v, float) and math.isnan(v)):
+                lens[i] = 0
+            else:
+                return None
+        if lv.outer:
+            return None
+        rows_idx = np.repeat(np.arange(len(vals), dtype=np.int64), lens)
+        flat = list(itertools.chain.from_iterable(v for v in vals if isinstance(v, (list, tuple, np.ndarray))))
+        names = lv.col_aliases or ["col"]
+        if len(names) != 1:
+            return None
+        col = pd.Series(flat, dtype=object).infer_objects() if flat else pd.Series([], dtype=object)
+        new = Frame(pd.DataFrame({"c0": col}), [(lv.table_alias, names[0])])
+        return Frame.concat_cols(src.take(rows_idx), new)
+
     # -- select
     def run_select(self, s: Select, ctes) -> Frame:
+        if isinstance(s.source, Join) and s.group_by:
+            from .fused import try_fused
+
+            fused = try_fused(self, s, ctes)
+            if fused is not None:
+                return fused
         src = self._source(s.source, ctes)
         if s.where is not None:
             src = src.take(np.nonzero(_truthy(_ser(self.eval(s.where, src, ctes), src.n)))[0])
