@@ -15,14 +15,20 @@ Model tables: LDA ``(label int, word string, lambda float)``; pLSA ``(label, wor
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import pandas as pd
 import torch
 
+from .. import _native
 from ..registry import udaf
 from ..utils.options import UDFArgumentException, opt
 from .base import Learner, log
+
+_native.register_hip("hm_lda_estep", [_native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_int,
+                                      _native.c_int, _native.c_f32, _native.c_f32, _native.c_int,
+                                      _native.c_p, _native.c_p, _native.c_p, _native.c_p])
 
 LDA_OPTS = [
     opt("topics", "k", 10, int, "Number of topics"),
@@ -120,22 +126,49 @@ class LDA(Learner):
         return torch.digamma(x) - torch.digamma(x.sum(dim, keepdim=True))
 
     def e_step(self, doc, w, c, B, expElogbeta):
+        """Per-document fixed point of gamma (upstream OnlineLDAModel.eStep: each document
+        iterates until mean |Δγ| < -delta).  GPU: one fused gfx950 kernel for the whole loop
+        (csrc/kernels/lda.hip); CPU: the same iteration as torch ops with a per-document
+        convergence mask."""
         c_ = self.cl
         gamma = torch.distributions.Gamma(100.0, 100.0).sample((B, self.K)).to(self.device)
+        if self.device.type == "cuda" and self.K <= 256 and os.environ.get("HM_LDA_TORCH", "0") != "1":
+            return self._e_step_kernel(doc, w, c, B, expElogbeta, gamma)
         Eb = expElogbeta[:, w].T                                  # [N, K]
+        active = torch.ones(B, dtype=torch.bool, device=self.device)
         for _ in range(int(c_["max_inner_iters"])):
             Et = torch.exp(self._elog(gamma, 1))                  # [B, K]
-            phinorm = (Et[doc] * Eb).sum(1) + 1e-100              # [N]
+            phinorm = (Et[doc] * Eb).sum(1) + 1e-30               # [N]
             contrib = Et[doc] * Eb * (c / phinorm)[:, None]       # [N, K]
             new = torch.full((B, self.K), float(self.alpha), device=self.device)
             new.index_add_(0, doc, contrib)
-            change = float((new - gamma).abs().mean().item())
-            gamma = new
-            if change < c_["delta"]:
+            change = (new - gamma).abs().mean(1)
+            gamma = torch.where(active[:, None], new, gamma)
+            active &= change >= c_["delta"]
+            if not bool(active.any()):
                 break
         Et = torch.exp(self._elog(gamma, 1))
-        phinorm = (Et[doc] * Eb).sum(1) + 1e-100
+        phinorm = (Et[doc] * Eb).sum(1) + 1e-30
         contrib = Et[doc] * Eb * (c / phinorm)[:, None]
+        return gamma, contrib
+
+    def _e_step_kernel(self, doc, w, c, B, expElogbeta, gamma):
+        from .. import _native
+
+        dev = self.device
+        off = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        off[1:] = torch.cumsum(torch.bincount(doc, minlength=B), 0).to(torch.int32)
+        EbT = expElogbeta.T.contiguous()                          # [V, K]: a word's row contiguous
+        wid = w.to(torch.int32).contiguous()
+        cc = c.to(torch.float32).contiguous()
+        gamma = gamma.contiguous()
+        contrib = torch.empty((w.numel(), self.K), dtype=torch.float32, device=dev)
+        self.inner_iters = torch.zeros(B, dtype=torch.int32, device=dev)
+        p = _native.ptr
+        rc = _native.hip().hm_lda_estep(p(off), p(wid), p(cc), p(EbT), B, self.K, float(self.alpha),
+                                        float(self.cl["delta"]), int(self.cl["max_inner_iters"]), p(gamma),
+                                        p(contrib), p(self.inner_iters), _native.stream_of(dev))
+        _native.check(rc, "hm_lda_estep")
         return gamma, contrib
 
     def fit(self, docs) -> "LDA":

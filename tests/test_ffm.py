@@ -195,8 +195,9 @@ def test_ffm_gpu_global_bias_loses_no_updates():
 
 @pytest.mark.gpu
 def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
-    """Full-chip Hogwild vs the sequential engine at 500K rows (measured gap ~0.01, shrinking
-    with data: profiles/ffm_parity_r1.log)."""
+    """Full-chip Hogwild vs the sequential engine at 500K rows: measured gap 0.011-0.014 here
+    (profiles/ffm_parity_r1.log), 5e-4 (fp32) / 1.3e-3 (bf16) at the bench's 12.6M rows on the
+    same stream (profiles/ffm_parity_bench_scale.log); the bound is the 500K measurement + margin."""
     idx, y = criteo_like(500000, hash_bits=20, seed=5)
     eidx, ey = criteo_like(100000, hash_bits=20, seed=99)
     yy = (ey > 0).float()
@@ -207,4 +208,4 @@ def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
         t.fit(batch=FFMBatch(idx, None, None, y).to(dev))
         p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
-    assert abs(res["cpu"] - res["cuda"]) < 0.02, res
+    assert abs(res["cpu"] - res["cuda"]) < 0.016, res
