@@ -37,14 +37,14 @@ def main():
         os.environ["HM_LDA_TORCH"] = "1" if torch_path else "0"
         m = LDA(f"-topics {K} -iters 1 -mini_batch_size 256", device="cuda")
         m.fit(docs[:256])                                      # warm-up (code load)
-        m = LDA(f"-topics {K} -iters 1 -mini_batch_size 256", device="cuda")
+        m = LDA(f"-topics {K} -iters 5 -eps 0 -mini_batch_size 256", device="cuda")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         m.fit(docs)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         print(json.dumps({"estep": "torch" if torch_path else "kernel", "docs": D, "topics": K,
-                          "epoch_s": round(dt, 3), "docs_per_s": round(D / dt),
+                          "fit_5_epochs_s": round(dt, 3), "docs_epochs_per_s": round(5 * D / dt),
                           "perplexity": round(float(m.perplexity or 0), 3)}), flush=True)
 
 

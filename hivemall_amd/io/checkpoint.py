@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import dataclasses
 import importlib
+import glob
 import json
 import os
 import shutil
@@ -107,16 +108,56 @@ def save(learner, path: str, model_table: bool = True) -> str:
                 write_table(learner.model_table(), os.path.join(tmp, "model.parquet"))
             except Exception:  # pragma: no cover - the tensors are the authoritative state
                 pass
+        for name in os.listdir(tmp):
+            _fsync_file(os.path.join(tmp, name))
+        _fsync_dir(tmp)
+        # swap: the old checkpoint is renamed aside (never deleted first), the new one moved in,
+        # the parent directory synced, and only then the old one removed — a crash at any point
+        # leaves a complete checkpoint at ``path`` or at ``path``.old-*
+        old = None
         if os.path.exists(path):
-            shutil.rmtree(path)
+            old = tempfile.mkdtemp(prefix=os.path.basename(path) + ".old-", dir=parent)
+            os.rmdir(old)
+            os.replace(path, old)
         os.replace(tmp, path)
+        _fsync_dir(parent)
+        if old is not None:
+            shutil.rmtree(old, ignore_errors=True)
     except BaseException:
         shutil.rmtree(tmp, ignore_errors=True)
         raise
     return path
 
 
-def load(path: str, device=None, **kw):
+def _fsync_file(p: str) -> None:
+    if os.path.isfile(p):
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+        finally:
+            os.close(fd)
+
+
+def _fsync_dir(d: str) -> None:
+    try:
+        fd = os.open(d, os.O_RDONLY)
+    except OSError:  # pragma: no cover - platforms without directory fds
+        return
+    try:
+        os.fsync(fd)
+    except OSError:  # pragma: no cover
+        pass
+    finally:
+        os.close(fd)
+
+
+def load(path: str, device=None, restore_rng: bool = False, **kw):
+    """Rebuild a learner from ``save``.  ``restore_rng``: also restore the process-global torch
+    CPU RNG to its state at save time (off by default: loading must not reseed the caller)."""
+    if not os.path.exists(os.path.join(path, "meta.json")):
+        olds = sorted(glob.glob(path.rstrip("/") + ".old-*"))
+        if olds:                     # a crash between the two renames of save(): take the old one
+            path = olds[-1]
     with open(os.path.join(path, "meta.json")) as f:
         meta = json.load(f)
     mod, qual = meta["class"].split(":")
@@ -153,5 +194,6 @@ def load(path: str, device=None, **kw):
             setattr(learner.hyper, k, v)
     if getattr(learner, "labels", None) is not None and hasattr(learner, "P"):
         learner.P.n_labels = len(learner.labels)
-    torch.set_rng_state(torch.tensor(meta["torch_rng"], dtype=torch.uint8))
+    if restore_rng:
+        torch.set_rng_state(torch.tensor(meta["torch_rng"], dtype=torch.uint8))
     return learner

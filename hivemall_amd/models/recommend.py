@@ -38,6 +38,33 @@ def slim_cd_batched(Gs, bs, l1: float, l2: float, iters: int, eps: float, device
     sweep falls below ``eps`` (the per-item convergence test).  Returns an [items, K] numpy
     array (padding columns are zero).
     """
+    n = len(Gs)
+    Kmax = max(g.shape[0] for g in Gs)
+    out = np.zeros((n, Kmax))
+    # items sorted by neighbourhood size and solved in chunks of bounded n_chunk * K_chunk^2 Gram
+    # bytes: padding to one item's huge kNN union no longer sizes every item's Gram matrix
+    order = np.argsort([g.shape[0] for g in Gs], kind="stable")
+    s = 0
+    while s < n:
+        e = s + 1
+        kc = Gs[order[s]].shape[0]
+        while e < n:
+            k_next = max(kc, Gs[order[e]].shape[0])
+            if (e + 1 - s) * k_next * k_next * 8 > _SLIM_CHUNK_BYTES:
+                break
+            kc = k_next
+            e += 1
+        idx = order[s:e]
+        w = _slim_cd_chunk([Gs[i] for i in idx], [bs[i] for i in idx], l1, l2, iters, eps, device)
+        out[idx, :w.shape[1]] = w
+        s = e
+    return out
+
+
+_SLIM_CHUNK_BYTES = 256 << 20
+
+
+def _slim_cd_chunk(Gs, bs, l1: float, l2: float, iters: int, eps: float, device=None):
     import torch
 
     dev = device if device is not None else torch.device("cpu")

@@ -87,14 +87,15 @@ class _Vocab:
 
 
 def _flatten(rows, device):
-    doc, w, c = [], [], []
-    for d, r in enumerate(rows):
-        for i, x in r:
-            doc.append(d)
-            w.append(i)
-            c.append(x)
-    t = lambda a, dt: torch.tensor(a, dtype=dt, device=device)
-    return t(doc, torch.long), t(w, torch.long), t(c, torch.float32)
+    """[(word id, count)] rows -> (doc, word, count) tensors, built with numpy (no per-token
+    torch calls)."""
+    lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=len(rows))
+    n = int(lens.sum())
+    doc = np.repeat(np.arange(len(rows), dtype=np.int64), lens)
+    w = np.fromiter((i for r in rows for i, _ in r), dtype=np.int64, count=n)
+    c = np.fromiter((x for r in rows for _, x in r), dtype=np.float32, count=n)
+    t = lambda a: torch.from_numpy(a).to(device)
+    return t(doc), t(w), t(c)
 
 
 class LDA(Learner):
@@ -179,11 +180,18 @@ class LDA(Learner):
         D = c["num_docs"] if c["num_docs"] > 0 else len(rows)
         bs = int(c["mini_batch_size"])
         prev = None
+        # the corpus flattened ONCE to device CSR (doc, word, count); mini-batches are slices
+        doc_all, w_all, c_all = _flatten(rows, self.device)
+        ptr = np.zeros(len(rows) + 1, dtype=np.int64)
+        np.cumsum([len(r) for r in rows], out=ptr[1:])
+        total = float(c_all.sum().item()) if c_all.numel() else 0.0
         for ep in range(int(c["iters"])):
-            bound = 0.0
+            bound = torch.zeros((), dtype=torch.float64, device=self.device)
             for s in range(0, len(rows), bs):
-                batch = rows[s:s + bs]
-                doc, w, cnt = _flatten(batch, self.device)
+                e = min(len(rows), s + bs)
+                a, b = int(ptr[s]), int(ptr[e])
+                batch = rows[s:e]
+                doc, w, cnt = doc_all[a:b] - s, w_all[a:b], c_all[a:b]
                 if doc.numel() == 0:
                     continue
                 expElogbeta = torch.exp(self._elog(self.lam, 1))
@@ -193,9 +201,9 @@ class LDA(Learner):
                 rho = (c["tau0"] + self.t) ** (-c["kappa"])
                 self.lam = (1 - rho) * self.lam + rho * (self.eta + D / len(batch) * sstats)
                 self.t += 1
-                bound += float(-(cnt * torch.log((torch.exp(self._elog(gamma, 1))[doc] *
-                                                   expElogbeta[:, w].T).sum(1) + 1e-100)).sum().item())
-            ppl = math.exp(bound / max(1.0, sum(x for r in rows for _, x in r)))
+                bound -= (cnt * torch.log((torch.exp(self._elog(gamma, 1))[doc] *
+                                           expElogbeta[:, w].T).sum(1) + 1e-100)).sum().double()
+            ppl = math.exp(float(bound.item()) / max(1.0, total))       # one sync per epoch
             log.info("train_lda epoch %d perplexity %.3f", ep + 1, ppl)
             if prev is not None and abs(prev - ppl) < c["eps"]:
                 break

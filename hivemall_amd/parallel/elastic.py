@@ -79,7 +79,8 @@ class ResumableLoop:
             return 0
         path = os.path.join(self.rank_dir, f"step{step}")
         mixer, rank = getattr(self.learner, "mixer", None), getattr(self.learner, "rank", 0)
-        self.learner = checkpoint.load(path, device=device or self.learner.device, mixer=mixer, rank=rank)
+        self.learner = checkpoint.load(path, device=device or self.learner.device, restore_rng=True,
+                                       mixer=mixer, rank=rank)
         return step + 1
 
     def save(self, step: int) -> None:

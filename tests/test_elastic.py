@@ -67,3 +67,25 @@ def test_fault_injection_and_resume(tmp_path):
     a = torch.load(tmp_path / "ref" / "final_rank0.pt", weights_only=True)
     b = torch.load(tmp_path / "job" / "final_rank0.pt", weights_only=True)
     assert torch.equal(a, b)
+
+
+def test_checkpoint_save_replaces_atomically_and_keeps_rng(tmp_path):
+    import torch
+
+    from hivemall_amd.io import checkpoint
+    from hivemall_amd.models.linear import TrainClassifier
+    from hivemall_amd.io.synthetic import a9a_like
+    rows, y = a9a_like(500)
+    m = TrainClassifier("-loss logloss", device="cpu").fit(rows, y)
+    p = str(tmp_path / "ck")
+    checkpoint.save(m, p)
+    checkpoint.save(m, p)                       # overwrite: old renamed aside, then removed
+    assert sorted(os.listdir(tmp_path)) == ["ck"]
+    torch.manual_seed(123)
+    before = torch.get_rng_state()
+    checkpoint.load(p, device="cpu")
+    assert torch.equal(torch.get_rng_state(), before)   # load does not reseed the caller
+    # a crash between the renames leaves only <path>.old-*: load() falls back to it
+    os.replace(p, p + ".old-x1")
+    b = checkpoint.load(p, device="cpu")
+    assert torch.equal(b.weights()[0], m.weights()[0])

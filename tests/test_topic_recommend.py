@@ -102,6 +102,23 @@ def test_slim_batched_cd_matches_scalar_loop():
         assert (W[t, len(b):] == 0).all()
 
 
+def test_slim_batched_cd_chunks_by_neighbourhood_size(monkeypatch):
+    """Items are solved in size-sorted chunks of bounded Gram bytes; the result is the one-shot
+    padded solve's (one large kNN union must not size every item's Gram matrix)."""
+    from hivemall_amd.models import recommend as R
+
+    rng = np.random.default_rng(5)
+    Gs, bs = [], []
+    for m in list(rng.integers(1, 6, size=40)) + [30]:
+        X = rng.random((50, m)) * (rng.random((50, m)) < 0.4)
+        Gs.append(X.T @ X)
+        bs.append(X.T @ rng.random(50))
+    full = R.slim_cd_batched(Gs, bs, 0.01, 0.05, 40, 1e-8)
+    monkeypatch.setattr(R, "_SLIM_CHUNK_BYTES", 4 * 6 * 6 * 8)      # <= 4 small items per chunk
+    chunked = R.slim_cd_batched(Gs, bs, 0.01, 0.05, 40, 1e-8)
+    np.testing.assert_allclose(chunked, full, rtol=1e-12, atol=1e-14)
+
+
 @pytest.mark.gpu
 def test_slim_batched_cd_gpu_matches_cpu():
     import torch
