@@ -6,7 +6,8 @@
 #include <vector>
 
 #define HM_API extern "C" __attribute__((visibility("default")))
-#define HM_TREE_CAT 0x40000000  // nominal split flag (csrc/kernels/trees.hip)
+#define HM_TREE_CAT 0x40000000    // nominal split flag (csrc/kernels/trees.hip)
+#define HM_TREE_DLEFT 0x20000000  // missing values go left (learned default direction)
 
 HM_API int hm_hist_build_cpu(const uint8_t* bins, int d, int dpad, int B, const int32_t* rows,
                              const int64_t* seg, int n_seg, const float* stats, const float* smax,
@@ -41,9 +42,12 @@ HM_API int hm_tree_predict_cpu(const float* X, int64_t n, int d, const int32_t* 
                 int f = feature[k];
                 if (f < 0) break;
                 const bool cat = f & HM_TREE_CAT;
-                f &= ~HM_TREE_CAT;
+                const bool dl = f & HM_TREE_DLEFT;
+                f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
                 const float v = x[f];
-                k = (cat ? v == threshold[k] : v <= threshold[k]) ? left[k] : right[k];  // NaN goes right
+                // NaN goes right unless the split learned a default direction
+                k = std::isnan(v) ? (dl ? left[k] : right[k])
+                                  : ((cat ? v == threshold[k] : v <= threshold[k]) ? left[k] : right[k]);
             }
             const float* val = values + voff[k];
             if (sum_trees) {
@@ -80,7 +84,7 @@ HM_API int hm_quantize_cpu(const float* X, int64_t n, int d, int dpad, const flo
 
 HM_API int hm_route_rows_cpu(const uint8_t* bins, int64_t n, int dpad, int32_t* node_of_row,
                              const int32_t* split_feat, const int32_t* split_bin,
-                             const int32_t* left_child, const int32_t* right_child) {
+                             const int32_t* left_child, const int32_t* right_child, int miss_bin) {
 #pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < n; ++r) {
         const int nd = node_of_row[r];
@@ -88,9 +92,11 @@ HM_API int hm_route_rows_cpu(const uint8_t* bins, int64_t n, int dpad, int32_t* 
         int f = split_feat[nd];
         if (f < 0) continue;
         const bool cat = f & HM_TREE_CAT;
-        f &= ~HM_TREE_CAT;
+        const bool dl = f & HM_TREE_DLEFT;
+        f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
         const int b = bins[r * dpad + f];
-        node_of_row[r] = (cat ? b == split_bin[nd] : b <= split_bin[nd]) ? left_child[nd] : right_child[nd];
+        const bool go_left = b == miss_bin ? dl : (cat ? b == split_bin[nd] : b <= split_bin[nd]);
+        node_of_row[r] = go_left ? left_child[nd] : right_child[nd];
     }
     return 0;
 }
@@ -226,10 +232,11 @@ HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* 
     const int L = ip[0], d = ip[1], B = ip[2], NS = ip[3], n_edges = ip[4], crit = ip[5];
     const int mtry = ip[6], node_base = ip[7];
     const uint32_t seed = (uint32_t)ip[8];
+    const int miss = ip[9];
     const float lam = fp[0], alpha = fp[1], min_leaf = fp[2];
     if (B <= 0 || B > 256 || NS <= 0 || crit < 0 || crit > 4) return 1;
     if (NS > 8) {
-        if (crit > 1) return 1;
+        if (crit > 1 || miss) return 1;
         split_find_wide(hist, L, d, B, NS, n_edges, crit, mtry, node_base, seed, min_leaf, cat, fmask, gain,
                         feat, bin, left, tot);
         return 0;
@@ -256,6 +263,10 @@ HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* 
             }
             const bool is_cat = cat && cat[f];
             const float* hf = hn + (size_t)f * B * NS;
+            const bool fmiss = miss && !is_cat;
+            float M[8] = {0};
+            if (fmiss)
+                for (int s = 0; s < NS; ++s) M[s] = hf[(size_t)(B - 1) * NS + s];
             for (int s = 0; s < NS; ++s) run[s] = 0.f;
             for (int b = 0; b < B; ++b) {
                 for (int s = 0; s < NS; ++s) {
@@ -263,21 +274,27 @@ HM_API int hm_split_find_cpu(const float* hist, const int32_t* ip, const float* 
                     lf[s] = is_cat ? hf[(size_t)b * NS + s] : run[s];
                     rt[s] = T[s] - lf[s];
                 }
-                if (split_weight(lf, NS, crit) < min_leaf || split_weight(rt, NS, crit) < min_leaf) continue;
-                if (is_cat && b >= n_edges) continue;
-                const float g = split_score(lf, NS, crit, lam, alpha) + split_score(rt, NS, crit, lam, alpha) - parent;
-                const int i = f * B + b;
-                if (g > best || (g == best && i < best_i)) {
-                    best = g;
-                    best_i = i;
-                    for (int s = 0; s < NS; ++s) Lb[s] = lf[s];
+                if (fmiss && b == B - 1) break;
+                for (int v = 0; v < (fmiss ? 2 : 1); ++v) {
+                    if (v == 1)
+                        for (int s = 0; s < NS; ++s) { lf[s] += M[s]; rt[s] -= M[s]; }
+                    if (split_weight(lf, NS, crit) < min_leaf || split_weight(rt, NS, crit) < min_leaf) continue;
+                    if (is_cat && b >= n_edges) continue;
+                    const float g = split_score(lf, NS, crit, lam, alpha) + split_score(rt, NS, crit, lam, alpha) - parent;
+                    const int i = (f * B + b) * 2 + v;
+                    if (g > best || (g == best && i < best_i)) {
+                        best = g;
+                        best_i = i;
+                        for (int s = 0; s < NS; ++s) Lb[s] = lf[s];
+                    }
                 }
             }
         }
         const bool found = best_i != 0x7FFFFFFF;
+        const int fb = best_i >> 1;
         gain[node] = found ? best : -INFINITY;
-        feat[node] = found ? best_i / B : 0;
-        bin[node] = found ? best_i % B : 0;
+        feat[node] = found ? fb / B : 0;
+        bin[node] = found ? (fb % B) | ((best_i & 1) << 16) : 0;
         for (int s = 0; s < NS; ++s) {
             left[node * NS + s] = Lb[s];
             tot[node * NS + s] = T[s];

@@ -30,6 +30,7 @@
 // Split-feature flag of a nominal (one-vs-rest) node: go left when x == threshold (prediction)
 // or bin == split bin (training); ordinal nodes go left when x <= threshold / bin <= split bin.
 #define HM_TREE_CAT 0x40000000
+#define HM_TREE_DLEFT 0x20000000   // learned default direction: missing (NaN) goes left
 
 namespace {
 
@@ -202,11 +203,13 @@ __global__ __launch_bounds__(256) void tree_predict_kernel(
             int f = feature[k];
             if (f < 0) break;
             const bool cat = f & HM_TREE_CAT;
-            f &= ~HM_TREE_CAT;
+            const bool dl = f & HM_TREE_DLEFT;
+            f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
             const float v = x[f];
             const float t = threshold[k];
-            // NaN goes right (Smile: x <= t ? true : false; nominal: x == t ? true : false)
-            k = (cat ? v == t : v <= t) ? left[k] : right[k];
+            // NaN goes right (Smile: x <= t ? true : false; nominal: x == t ? true : false) unless
+            // the split learned a default direction (XGBoost's sparsity-aware splits)
+            k = (v != v) ? (dl ? left[k] : right[k]) : ((cat ? v == t : v <= t) ? left[k] : right[k]);
         }
         const float* val = values + voff[k];
         if (sum_trees) {
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
                                                     const int32_t* __restrict__ split_feat,
                                                     const int32_t* __restrict__ split_bin,
                                                     const int32_t* __restrict__ left_child,
-                                                    const int32_t* __restrict__ right_child) {
+                                                    const int32_t* __restrict__ right_child, int miss_bin) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         const int nd = node_of_row[r];
@@ -259,10 +262,12 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
         int f = split_feat[nd];
         if (f < 0) continue;
         const bool cat = f & HM_TREE_CAT;
-        f &= ~HM_TREE_CAT;
+        const bool dl = f & HM_TREE_DLEFT;
+        f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
         const int b = bins[r * dpad + f];
         const int sb = split_bin[nd];
-        node_of_row[r] = (cat ? b == sb : b <= sb) ? left_child[nd] : right_child[nd];
+        const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
+        node_of_row[r] = go_left ? left_child[nd] : right_child[nd];
     }
 }
 
@@ -286,6 +291,8 @@ struct SplitParams {
     int crit, mtry, node_base;
     float lam, alpha, min_leaf;
     uint32_t seed;
+    int miss;     // 1: bin B-1 holds the missing values; each ordinal candidate is scored with
+                  // them on the right and on the left, the better one is the default direction
 };
 
 __host__ __device__ __forceinline__ uint32_t feat_key(uint32_t seed, uint32_t node, uint32_t f) {
@@ -386,6 +393,10 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
         }
         const bool is_cat = cat && cat[f];
         const float* hf = hn + (size_t)f * B * NS;
+        const bool fmiss = P.miss && !is_cat;
+        float M[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) M[s] = fmiss ? hf[(size_t)(B - 1) * NS + s] : 0.f;
         float h[4][NS];
         float lsum[NS];
 #pragma unroll
@@ -422,18 +433,28 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
                 left[s] = is_cat ? h[k][s] : run[s];
                 right[s] = tot[s] - left[s];
             }
-            bool ok = split_weight<NS>(left, P.crit) >= P.min_leaf &&
-                      split_weight<NS>(right, P.crit) >= P.min_leaf;
-            if (is_cat && b >= P.n_edges) ok = false;
-            if (!ok) continue;
-            const float g = split_score<NS>(left, P.crit, P.lam, P.alpha) +
-                            split_score<NS>(right, P.crit, P.lam, P.alpha) - parent;
-            const int i = f * B + b;
-            if (g > best || (g == best && i < best_i)) {
-                best = g;
-                best_i = i;
+            if (fmiss && b == B - 1) break;         // the missing bin is not a threshold
+            for (int v = 0; v < (fmiss ? 2 : 1); ++v) {
+                if (v == 1) {                        // the missing rows on the left
 #pragma unroll
-                for (int s = 0; s < NS; ++s) best_left[s] = left[s];
+                    for (int s = 0; s < NS; ++s) {
+                        left[s] += M[s];
+                        right[s] -= M[s];
+                    }
+                }
+                bool ok = split_weight<NS>(left, P.crit) >= P.min_leaf &&
+                          split_weight<NS>(right, P.crit) >= P.min_leaf;
+                if (is_cat && b >= P.n_edges) ok = false;
+                if (!ok) continue;
+                const float g = split_score<NS>(left, P.crit, P.lam, P.alpha) +
+                                split_score<NS>(right, P.crit, P.lam, P.alpha) - parent;
+                const int i = (f * B + b) * 2 + v;   // ties: smaller (feature, bin), missing right
+                if (g > best || (g == best && i < best_i)) {
+                    best = g;
+                    best_i = i;
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) best_left[s] = left[s];
+                }
             }
         }
     }
@@ -463,9 +484,11 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
         for (int k = 1; k < 4; ++k)
             if (s_gain[k] > s_gain[w] || (s_gain[k] == s_gain[w] && s_idx[k] < s_idx[w])) w = k;
         const bool found = s_idx[w] != 0x7FFFFFFF;
+        const int fb = s_idx[w] >> 1;
         out_gain[node] = found ? s_gain[w] : -INFINITY;
-        out_feat[node] = found ? s_idx[w] / B : 0;
-        out_bin[node] = found ? s_idx[w] % B : 0;
+        out_feat[node] = found ? fb / B : 0;
+        // bit 16 of the bin: the missing values go left at this split
+        out_bin[node] = found ? (fb % B) | ((s_idx[w] & 1) << 16) : 0;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             out_left[node * NS + s] = s_left[w][s];
@@ -767,31 +790,35 @@ HM_API int hm_quantize(const float* X, int64_t n, int d, int dpad, const float* 
     HM_LAUNCH_RET();
 }
 
+// miss_bin: the bin of missing values (rows there follow the split's HM_TREE_DLEFT flag), or -1.
 HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int32_t* node_of_row,
                          const int32_t* split_feat, const int32_t* split_bin,
-                         const int32_t* left_child, const int32_t* right_child, hipStream_t stream) {
+                         const int32_t* left_child, const int32_t* right_child, int miss_bin,
+                         hipStream_t stream) {
     if (n <= 0) return 0;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(route_kernel, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
-                       node_of_row, split_feat, split_bin, left_child, right_child);
+                       node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
     HM_LAUNCH_RET();
 }
 
 // Best split of every node of a level: hist [L, d, B, NS] -> gain [L] (-inf: none), feature,
 // bin, left-child statistics [L, NS] and node totals [L, NS].  cat / fmask: [d] bytes or null.
-// ip: L, d, B, NS, n_edges, crit, mtry, node_base, seed;  fp: lambda, alpha, min_leaf
+// ip: L, d, B, NS, n_edges, crit, mtry, node_base, seed, miss;  fp: lambda, alpha, min_leaf.
+// With miss (NS <= 8 kernel) bin B-1 holds the missing values and bit 16 of the returned bin
+// says they go left at that split.
 HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, const uint8_t* cat,
                          const uint8_t* fmask, float* gain, int32_t* feat, int32_t* bin, float* left,
                          float* tot, hipStream_t stream) {
     SplitParams P;
     P.L = ip[0]; P.d = ip[1]; P.B = ip[2]; P.NS = ip[3]; P.n_edges = ip[4]; P.crit = ip[5];
-    P.mtry = ip[6]; P.node_base = ip[7]; P.seed = (uint32_t)ip[8];
+    P.mtry = ip[6]; P.node_base = ip[7]; P.seed = (uint32_t)ip[8]; P.miss = ip[9];
     P.lam = fp[0]; P.alpha = fp[1]; P.min_leaf = fp[2];
     if (P.L <= 0) return 0;
     if (P.B <= 0 || P.B > 256 || P.d <= 0 || P.crit < 0 || P.crit > 4) return (int)hipErrorInvalidValue;
     if (P.NS > 8) {   // many classes: gini / entropy only, classes walked one at a time
-        if (P.crit > 1 || P.NS > 4096) return (int)hipErrorInvalidValue;
+        if (P.crit > 1 || P.NS > 4096 || P.miss) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL(split_find_wide_kernel, dim3(P.L), dim3(256), 0, stream, P, hist, cat, fmask,
                            gain, feat, bin, left, tot);
         HM_LAUNCH_RET();

@@ -35,6 +35,7 @@ from .base import Learner, log
 
 MODEL_VERSION = 1
 CAT_FLAG = 1 << 30   # nominal split flag in flattened node arrays (HM_TREE_CAT in trees.hip)
+DLEFT_FLAG = 1 << 29  # missing values go left at this split (HM_TREE_DLEFT)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
 
 
@@ -59,6 +60,7 @@ class Quantized:
     d: int
     B: int
     cat: torch.Tensor | None = None   # bool [d]: nominal columns (bin = category index)
+    missing: bool = False             # bin B-1 holds exactly the NaN values
 
     @property
     def dpad(self) -> int:
@@ -67,7 +69,7 @@ class Quantized:
 
 def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: int = 0,
              edges: torch.Tensor | None = None, mixer=None,
-             categorical: torch.Tensor | None = None) -> Quantized:
+             categorical: torch.Tensor | None = None, missing: bool = False) -> Quantized:
     """Per-feature quantile edges (from a row sample) and uint8 bins on X's device.
 
     With a mixer over several ranks every rank contributes an equal-size sample of its shard and
@@ -90,9 +92,12 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
         else:
             idx = (torch.arange(n) if n <= sample else torch.randint(0, n, (sample,), generator=g)).to(X.device)
             S = X[idx]
-        qs = torch.linspace(0, 1, B + 1, device=X.device)[1:-1]
-        E = torch.quantile(S.T.contiguous(), qs, dim=1).T.contiguous()     # [d, B-1]
+        qs = torch.linspace(0, 1, (B if missing else B + 1), device=X.device)[1:-1]
+        St = S.T.contiguous()
+        E = (torch.nanquantile(St, qs, dim=1) if missing else torch.quantile(St, qs, dim=1)).T.contiguous()
         E = torch.nan_to_num(E, nan=float("inf"))
+        if missing:                      # [d, B-2] edges + inf: finite values never reach bin B-1
+            E = torch.cat([E, torch.full((d, 1), float("inf"), device=X.device)], 1)
         # strictly increasing edges (ties collapse to the same bin)
         if categorical is not None:
             for j in torch.nonzero(categorical).flatten().tolist():
@@ -119,7 +124,7 @@ def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: 
     else:
         _native.host().hm_quantize_cpu(*args)
     cat = None if categorical is None else categorical.to(torch.bool).cpu()
-    return Quantized(bins, edges, d, B, cat)
+    return Quantized(bins, edges, d, B, cat, bool(missing) and edges.shape[1] == B - 1)
 
 
 # ------------------------------------------------------------------ trees
@@ -132,14 +137,16 @@ class Tree:
     value: list = field(default_factory=list)       # list of floats per node (leaf output)
     n_out: int = 1
     cat: list = field(default_factory=list)         # 1 = nominal node: left when x == threshold
+    dleft: list = field(default_factory=list)       # 1 = missing (NaN) goes left (learned default)
 
     def is_cat(self, k: int) -> bool:
         return bool(self.cat) and bool(self.cat[k])
 
     def goes_left(self, k: int, v) -> bool:
-        """Smile's test: ``x <= t`` (ordinal) / ``x == t`` (nominal); missing/NaN goes right."""
-        if v is None:
-            return False
+        """Smile's test: ``x <= t`` (ordinal) / ``x == t`` (nominal); missing/NaN goes right
+        unless the split learned a default direction (XGBoost-style, ``dleft``)."""
+        if v is None or (isinstance(v, float) and math.isnan(v)):
+            return bool(self.dleft) and bool(self.dleft[k])
         return v == self.threshold[k] if self.is_cat(k) else v <= self.threshold[k]
 
     def to_json(self) -> dict:
@@ -148,12 +155,14 @@ class Tree:
              "l": self.left, "r": self.right, "val": self.value, "o": self.n_out}
         if any(self.cat):
             j["c"] = self.cat
+        if any(self.dleft):
+            j["m"] = self.dleft
         return j
 
     @staticmethod
     def from_json(j: dict) -> "Tree":
         return Tree(j["f"], [math.inf if x is None else x for x in j["t"]], j["l"], j["r"], j["val"],
-                    j["o"], list(j.get("c", [])))
+                    j["o"], list(j.get("c", [])), list(j.get("m", [])))
 
     def serialize(self) -> str:
         return base91.encode(zlib.compress(json.dumps(self.to_json(), separators=(",", ":")).encode()))
@@ -165,7 +174,8 @@ class Tree:
     def predict_one(self, x) -> list:
         k = 0
         while self.feature[k] >= 0:
-            # missing / NaN goes right, as in Smile's `x <= t ? trueChild : falseChild`
+            # missing / NaN goes right, as in Smile's `x <= t ? trueChild : falseChild`, unless
+            # the split learned a default direction
             k = self.left[k] if self.goes_left(k, x[self.feature[k]]) else self.right[k]
         return self.value[k]
 
@@ -181,7 +191,10 @@ def flatten(trees: list[Tree], device) -> dict:
     for t in trees:
         roots.append(base)
         for k in range(len(t.feature)):
-            feat.append(t.feature[k] | CAT_FLAG if (t.feature[k] >= 0 and t.is_cat(k)) else t.feature[k])
+            fk = t.feature[k]
+            if fk >= 0:
+                fk |= (CAT_FLAG if t.is_cat(k) else 0) | (DLEFT_FLAG if (t.dleft and t.dleft[k]) else 0)
+            feat.append(fk)
             thr.append(t.threshold[k] if math.isfinite(t.threshold[k]) else 3.4e38)
             lft.append(t.left[k] + base if t.feature[k] >= 0 else 0)
             rgt.append(t.right[k] + base if t.feature[k] >= 0 else 0)
@@ -224,6 +237,7 @@ class HistTreeBuilder:
                  max_leaf_nodes: int | None = None, seed: int = 0, mixer=None, lam: float = 0.0,
                  alpha: float = 0.0, min_gain: float = 0.0, feature_mask: torch.Tensor | None = None):
         self.q = q
+        self.missing = bool(getattr(q, "missing", False))   # learn default directions for NaN
         self.cat = q.cat                          # nominal columns: one-vs-rest splits
         self.criterion = criterion
         self.max_depth = max_depth
@@ -312,8 +326,9 @@ class HistTreeBuilder:
         left = torch.empty((L, NS), dtype=torch.float32, device=dev)
         tot = torch.empty((L, NS), dtype=torch.float32, device=dev)
         mtry = int(self.mtry) if (self.mtry is not None and self.mtry < d) else 0
+        miss = int(self.missing and NS <= 8)
         ip = np.array([L, d, B, NS, self.q.edges.shape[1], self._CRIT[self.criterion], mtry,
-                       node_base, self._seed32], dtype=np.int32)
+                       node_base, self._seed32, miss], dtype=np.int32)
         fp = np.array([self.lam, self.alpha, float(self.min_leaf)], dtype=np.float32)
         if self._masks is None or self._masks[0] != dev:
             u8 = lambda m: None if m is None else m.to(device=dev, dtype=torch.uint8).contiguous()
@@ -327,7 +342,8 @@ class HistTreeBuilder:
         else:
             if _native.host().hm_split_find_cpu(*args) != 0:
                 raise RuntimeError("hm_split_find_cpu: invalid arguments")
-        return gain, feat, bins, left, tot
+        dleft = (bins >> 16) & 1                  # bit 16: the missing rows go left
+        return gain, feat, bins & 0xFFFF, left, tot, dleft
 
     @staticmethod
     def _partition_gpu(act_rows, node_of_row, nb: int, lut, n_keys: int):
@@ -426,7 +442,7 @@ class HistTreeBuilder:
                 lefts.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 rights.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 break
-            best_gain, bf, bb, left_all, tot = self._split_find(H, base)
+            best_gain, bf, bb, left_all, tot, bdl = self._split_find(H, base)
             vals.append(self._leaf_values(tot))
             ok = (best_gain > max(1e-12, self.min_gain)) & torch.isfinite(best_gain) & \
                 (self._weight(tot) >= self.min_split)
@@ -441,6 +457,7 @@ class HistTreeBuilder:
             thr = torch.where(bb < edges.shape[1], edges[bf.long(), bb.clamp(max=edges.shape[1] - 1).long()],
                               torch.full_like(best_gain, math.inf))
             bflag = bf if cat_dev is None else bf | (cat_dev[bf.long()].to(torch.int32) * CAT_FLAG)
+            bflag = bflag | (bdl * DLEFT_FLAG)
             feats.append(torch.where(ok, bflag, torch.full_like(bf, -1)))
             thrs.append(torch.where(ok, thr, torch.full_like(thr, math.inf)))
             lefts.append(lc)
@@ -455,7 +472,8 @@ class HistTreeBuilder:
             lc_all = torch.cat([lc_all, lc])
             rc_all = torch.cat([rc_all, rc])
             p = _native.ptr
-            args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all))
+            args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all),
+                    (q.B - 1) if self.missing else -1)
             if dev.type == "cuda":
                 _native.check(_native.hip().hm_route_rows(*args, _native.stream_of(dev)), "hm_route_rows")
             else:
@@ -501,7 +519,9 @@ class HistTreeBuilder:
         tree = Tree(n_out=n_out)
         cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
         tree.cat = cflag if any(cflag) else []
-        tree.feature = [int(f) & ~CAT_FLAG if f >= 0 else int(f) for f in F]
+        dflag = [1 if (f >= 0 and int(f) & DLEFT_FLAG) else 0 for f in F]
+        tree.dleft = dflag if any(dflag) else []
+        tree.feature = [int(f) & ~(CAT_FLAG | DLEFT_FLAG) if f >= 0 else int(f) for f in F]
         tree.threshold = [float(t) for t in T]
         tree.left = [int(x) for x in Lc]
         tree.right = [int(x) for x in Rc]
@@ -957,8 +977,8 @@ _native.register_host("hm_tree_predict_cpu", [_P, _I64, C.c_int] + [_P] * 7 + [C
 _native.register_hip("hm_quantize", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P, _P])
 _native.register_host("hm_quantize_cpu", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_absmax_cols", [_P, _I64, C.c_int, _P, _P])
-_native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [_P])
-_native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5)
+_native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int, _P])
+_native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int])
 _native.register_hip("hm_split_find", [_P] * 10 + [_P])
 _native.register_host("hm_split_find_cpu", [_P] * 10)
 _native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P])

@@ -121,7 +121,12 @@ class XGBoostTrainer(Learner):
                 self.base_margin = [math.log(bs / (1 - bs))]
             else:
                 self.base_margin = [bs]
-        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer)
+        # NaN = missing: the last bin is reserved for it and every split learns where missing
+        # rows go (XGBoost's sparsity-aware default direction; tree JSON field "m")
+        has_nan = bool(torch.isnan(X).any().item())
+        if self.mixer is not None and self.mixer.world > 1:
+            has_nan = self.mixer.all_reduce_scalar(float(has_nan), "max") > 0
+        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer, missing=has_nan)
         F = torch.tensor(self.base_margin, device=dev).repeat(n, 1)
         g = torch.Generator(device=dev).manual_seed(self.seed)
         gcpu = torch.Generator().manual_seed(self.seed)

@@ -298,7 +298,7 @@ def _split_ref(b, H, cm):
                                          ("gbt", 3, True), ("xgb", 2, False)])
 def test_split_find_matches_tensor_formulation(crit, NS, cat):
     b, H, cm = _split_case(crit, NS, cat)
-    gain, feat, bins, left, tot = b._split_find(H, 0)
+    gain, feat, bins, left, tot, _ = b._split_find(H, 0)
     bg, bi, rtot = _split_ref(b, H, cm)
     torch.testing.assert_close(tot, rtot, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gain, bg, rtol=1e-4, atol=1e-5)
@@ -308,8 +308,8 @@ def test_split_find_matches_tensor_formulation(crit, NS, cat):
 def test_split_find_mtry_draw():
     b, H, _ = _split_case("gini", 3)
     b.mtry = 2
-    _, feat, _, _, _ = b._split_find(H, 0)
-    _, feat2, _, _, _ = b._split_find(H, 0)
+    _, feat, _, _, _, _ = b._split_find(H, 0)
+    _, feat2, _, _, _, _ = b._split_find(H, 0)
     assert torch.equal(feat, feat2)           # the draw is a pure function of (seed, node)
     draws = {tuple(b._split_find(H, base)[1].tolist()) for base in range(0, 400, 40)}
     assert len(draws) > 1                     # ... and differs between nodes
@@ -369,7 +369,7 @@ def _int_split_case(crit, NS, cat=False, seed=0):
 @pytest.mark.parametrize("crit,cat", [("gini", False), ("entropy", True)])
 def test_split_find_many_classes_matches_tensor_formulation(crit, cat):
     b, H, cm = _int_split_case(crit, 11, cat)
-    gain, feat, bins, left, tot = b._split_find(H, 0)
+    gain, feat, bins, left, tot, _ = b._split_find(H, 0)
     bg, bi, rtot = _split_ref(b, H, cm)
     torch.testing.assert_close(tot, rtot)
     torch.testing.assert_close(gain, bg, rtol=1e-4, atol=1e-3)

@@ -97,3 +97,55 @@ def test_binary_gpu_matches_cpu(higgs):
         m = XGBoostTrainer("-num_round 20 -max_depth 6", device=dev).fit(X, y)
         aucs[dev] = roc_auc_score(yt.numpy(), m.predict_proba(Xt)[:, 0])
     assert abs(aucs["cpu"] - aucs["cuda"]) < 0.005, aucs
+
+
+def _nan_data(n, seed):
+    """HIGGS-shaped rows where feature 0 is missing for 40% of the positives and 5% of the
+    negatives (informative missingness), feature 3 missing at random."""
+    X, y = higgs_like(n, seed=seed)
+    X = X.clone()
+    g = torch.Generator().manual_seed(seed + 1)
+    r = torch.rand(n, generator=g)
+    X[(y > 0) & (r < 0.4), 0] = float("nan")
+    X[(y <= 0) & (r < 0.05), 0] = float("nan")
+    X[torch.rand(n, generator=g) < 0.2, 3] = float("nan")
+    return X, y
+
+
+def test_missing_values_learn_default_direction():
+    """NaN = missing: splits learn where missing rows go (XGBoost's default direction) — the
+    model matches scikit-learn's NaN-aware histogram GBM, the tree JSON carries the learned
+    directions, and the Python traversal agrees with the batched predict kernel."""
+    from hivemall_amd.models.trees import Tree, predict_forest
+
+    X, y = _nan_data(30000, 0)
+    Xt, yt = _nan_data(6000, 9)
+    m = XGBoostTrainer("-objective binary:logistic -num_round 40 -eta 0.3 -max_depth 6 -lambda 1",
+                       device="cpu").fit(X, y)
+    auc = roc_auc_score(yt.numpy(), m.predict_proba(Xt)[:, 0])
+    ref = HistGradientBoostingClassifier(max_iter=40, learning_rate=0.3, max_depth=6, l2_regularization=1.0,
+                                         early_stopping=False, max_leaf_nodes=None, min_samples_leaf=1)
+    ref.fit(X.numpy(), y.numpy())
+    auc_ref = roc_auc_score(yt.numpy(), ref.predict_proba(Xt.numpy())[:, 1])
+    assert auc > auc_ref - 0.01, (auc, auc_ref)
+    trees = [t for rt in m.trees for t in rt]
+    assert any(any(t.dleft) for t in trees)                       # some splits send NaN left
+    t0 = next(t for t in trees if any(t.dleft))
+    assert Tree.deserialize(t0.serialize()).dleft == t0.dleft
+    rows = Xt[:300]
+    kern = predict_forest([t0], rows)[:, 0].numpy()
+    py = np.array([t0.predict_one([float(v) for v in r])[0] for r in rows])
+    np.testing.assert_allclose(kern, py, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_missing_values_gpu_matches_cpu():
+    X, y = _nan_data(20000, 3)
+    Xt, yt = _nan_data(4000, 4)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        m = XGBoostTrainer("-num_round 15 -max_depth 5", device=dev).fit(X, y)
+        res[dev] = (roc_auc_score(yt.numpy(), m.predict_proba(Xt)[:, 0]),
+                    [t.dleft for rt in m.trees for t in rt][:3])
+    assert abs(res["cpu"][0] - res["cuda"][0]) < 0.005, res
+    assert res["cpu"][1][0] == res["cuda"][1][0]                  # same first tree directions
