@@ -107,6 +107,10 @@ BPR_OPTS = [
     opt("seed", None, -1, int, "Seed"),
     opt("samples_per_epoch", None, 0, int, "[engine] device-sampled triples per epoch (0 = #positives)"),
     opt("grid", None, 0, int, "[engine] kernel grid override"),
+    flag("shard_model", None, "[engine] row-shard P, Q, Bi over the ranks (model parallel: each "
+         "GPU holds 1/world of the tables; batches pull/push the rows they touch)"),
+    opt("shard_batch", None, 1 << 20, int, "[engine] triples per pull/compute/push step with "
+        "-shard_model"),
 ] + MIX_OPTS
 _BPR_LOSS = {"lnlogistic": 0, "logistic": 1, "sigmoid": 2}
 
@@ -339,12 +343,28 @@ class BPRMF(_MFBase):
         self.t = 0
         self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
         self.grid = int(c["grid"])
+        self.sharded = None        # {"P", "Q", "Bi"} ShardedTables with -shard_model
 
     def init_state(self, n_users, n_items):
         self.n_users, self.n_items = int(n_users), int(n_items)
         g = torch.Generator().manual_seed(self.seed)
         c = self.cl
         dev = self.device
+        if c["shard_model"]:
+            from ..parallel.sharded import ShardedTable
+
+            ctx = self.mixer.ctx if self.mixer is not None else None
+            # the same initial values as the unsharded model (generated once, each rank keeps its rows)
+            P0 = _init_factors(self.n_users, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g)
+            Q0 = _init_factors(self.n_items, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g)
+            self.sharded = dict(
+                P=ShardedTable(self.n_users, self.kp, ctx, device=dev, init=lambda gid: P0[gid.cpu()]),
+                Q=ShardedTable(self.n_items, self.kp, ctx, device=dev, init=lambda gid: Q0[gid.cpu()]),
+                Bi=ShardedTable(self.n_items, 1, ctx, device=dev))
+            self.state = None
+            self.seen_u = torch.zeros(self.n_users, dtype=torch.bool, device=dev)
+            self.seen_i = torch.zeros(self.n_items, dtype=torch.bool, device=dev)
+            return
         self.state = dict(
             P=_init_factors(self.n_users, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g).to(dev),
             Q=_init_factors(self.n_items, self.k, self.kp, c["init"], c["maxval"], c["min_init_stddev"], g).to(dev),
@@ -383,13 +403,74 @@ class BPRMF(_MFBase):
         self.t += n
         return float(loss.item())
 
+    def _step_sharded(self, tu, ti, tj) -> float:
+        """-shard_model: pull the rows the triples touch from their owner ranks, run the same
+        kernel on the compact tables, push the changes back (parallel/sharded.py)."""
+        sh = self.sharded
+        B = max(1, int(self.cl["shard_batch"]))
+        n = tu.numel()
+        steps = sh["P"].steps_agreed((n + B - 1) // B)
+        total = 0.0
+        full_u, full_i = self.n_users, self.n_items
+        try:
+            for s in range(steps):
+                cu, ci, cj = tu[s * B:(s + 1) * B], ti[s * B:(s + 1) * B], tj[s * B:(s + 1) * B]
+                U = torch.unique(cu.long())
+                I = torch.unique(torch.cat([ci, cj]).long())
+                P0, Q0, B0 = sh["P"].pull(U), sh["Q"].pull(I), sh["Bi"].pull(I)
+                self.state = dict(P=P0.clone(), Q=Q0.clone(), Bi=B0[:, 0].clone().contiguous())
+                if cu.numel():
+                    self.n_users, self.n_items = max(1, U.numel()), max(1, I.numel())
+                    lu = torch.searchsorted(U, cu.long()).to(torch.int32)
+                    li = torch.searchsorted(I, ci.long()).to(torch.int32)
+                    lj = torch.searchsorted(I, cj.long()).to(torch.int32)
+                    total += self.step(lu.contiguous(), li.contiguous(), lj.contiguous())
+                    self.n_users, self.n_items = full_u, full_i
+                sh["P"].push_add(U, self.state["P"] - P0)
+                sh["Q"].push_add(I, self.state["Q"] - Q0)
+                sh["Bi"].push_add(I, (self.state["Bi"] - B0[:, 0])[:, None])
+        finally:
+            self.n_users, self.n_items = full_u, full_i
+            self.state = None
+        return total
+
+    def full_state(self) -> dict:
+        """The model tables (all-gathered on every rank with -shard_model)."""
+        if self.sharded is None:
+            return self.state
+        return dict(P=self.sharded["P"].full(), Q=self.sharded["Q"].full(),
+                    Bi=self.sharded["Bi"].full()[:, 0].contiguous())
+
     def fit(self, users, pos_items, neg_items) -> "BPRMF":
         dev = self.device
         tu = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev)
         ti = torch.as_tensor(np.asarray(pos_items, dtype=np.int32)).to(dev)
         tj = torch.as_tensor(np.asarray(neg_items, dtype=np.int32)).to(dev)
-        if self.state is None:
-            self.init_state(int(tu.max().item()) + 1, int(max(ti.max().item(), tj.max().item())) + 1)
+        if self.state is None and self.sharded is None:
+            nu = int(tu.max().item()) + 1 if tu.numel() else 1
+            ni = int(max(ti.max().item(), tj.max().item())) + 1 if ti.numel() else 1
+            if self._dp():        # every rank sizes the (sharded or mixed) tables alike
+                nu = int(self.mixer.all_reduce_scalar(float(nu), "max"))
+                ni = int(self.mixer.all_reduce_scalar(float(ni), "max"))
+            self.init_state(nu, ni)
+        if self.sharded is not None:
+            self.seen_u[tu.long()] = True
+            self.seen_i[ti.long()] = True
+            self.seen_i[tj.long()] = True
+            for ep in range(int(self.cl["iters"])):
+                el = self._step_sharded(tu, ti, tj)
+                if self._dp():
+                    el = self.mixer.all_reduce_scalar(el, "sum")
+                self._epoch_end(el)
+                self.cv.incr_loss(el)
+                if self.cv.is_converged():
+                    break
+            if self._dp():
+                f = [self.seen_u.to(torch.float32), self.seen_i.to(torch.float32)]
+                self.mixer.all_reduce_sum(f)
+                self.seen_u, self.seen_i = f[0] > 0, f[1] > 0
+            self.state = self.full_state()
+            return self
         self.seen_u[tu.long()] = True
         self.seen_i[ti.long()] = True
         self.seen_i[tj.long()] = True
@@ -417,6 +498,10 @@ class BPRMF(_MFBase):
 
     def fit_implicit(self, users, items, n_users=None, n_items=None, epochs=None) -> "BPRMF":
         """Train from positive (user, item) pairs; negatives are sampled on the device."""
+        if self.cl["shard_model"]:
+            raise UDFArgumentException("train_bprmf: -shard_model trains on explicit (user, pos, neg) "
+                                       "triples (bpr_sampling); device negative sampling needs the "
+                                       "whole item table on every GPU")
         dev = self.device
         u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev) if not torch.is_tensor(users) else users.to(dev)
         i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev) if not torch.is_tensor(items) else items.to(dev)
