@@ -94,10 +94,14 @@ def test_bpr_shard_model_single_process_equals_unsharded():
 
 @pytest.mark.gpu
 def test_bpr_shard_model_gpu_single_process():
+    """Device tables through pull/compute/push.  -grid 1: on this 300-item catalogue wider
+    Hogwild grids stall the factors on the near-zero init whether sharded or not (AUC 0.50 at
+    the default grid 9 vs 1.00 at grid 1 for the plain learner too: benchmarks/probes/
+    bpr_shard_probe.py, profiles/bpr_shard_probe_r2.log; docs/perf_notes.md MF staleness)."""
     from hivemall_amd.models.mf import BPRMF
 
     u, i, j = _triples(n=40000)
-    a = BPRMF("-factors 8 -iters 5 -eta0 0.05 -disable_cv -seed 5 -shard_model -shard_batch 8192",
+    a = BPRMF("-factors 8 -iters 5 -eta0 0.05 -disable_cv -seed 5 -shard_model -shard_batch 8192 -grid 1",
               device="cuda").fit(u, i, j)
     st = a.state
     assert _auc(st["P"].cpu().numpy(), st["Q"].cpu().numpy(), st["Bi"].cpu().numpy()) > 0.85
