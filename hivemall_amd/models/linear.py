@@ -134,8 +134,15 @@ def encode_rows(rows, encoder: FeatureEncoder | None, train: bool) -> tuple[CSR,
     return encoder.encode(rows, add_new=train and encoder.mode == "dict"), encoder
 
 
+def _arrow(x) -> bool:
+    from ..io.ingest import is_arrow_like
+
+    return is_arrow_like(x)
+
+
 class OnlineLinearLearner(Learner):
     SQL_DP = "shard"
+    ARROW_INPUT = True      # Arrow list<string> rows with integer names are parsed on the device
     NAME = "train_linear"
     ALGO = "general"
     TASK = "binary"           # binary | regression | multiclass
@@ -243,7 +250,37 @@ class OnlineLinearLearner(Learner):
             return out
         return a.astype(np.float32)
 
+    def _prepare_device(self, features, y) -> SparseRows | None:
+        """Integer-named string features ("123:0.5") parsed on the GPU (io/ingest.py
+        hm_feat_parse) — None when the rows are not strings or hold non-integer names (the
+        host encoder then dictionary-encodes them)."""
+        from ..io import ingest
+        from .fm import _string_rows
+
+        if not _string_rows(features):
+            return None
+        try:
+            ip, idx, val, _ = ingest.csr_device(features, "int", device=self.device)
+        except UDFArgumentException:
+            return None
+        if idx.numel() and (int(idx.min().item()) < 0 or int(idx.max().item()) >= 2 ** 31 - 1):
+            return None
+        self.encoder = FeatureEncoder("int")
+        self.encoder.string_names = True
+        yt = None if y is None else torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)).to(self.device)
+        vv = None if (val.numel() and bool((val == 1.0).all().item())) else val
+        return SparseRows(ip, idx.to(torch.int32), vv, yt)
+
     def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
+        if (self.device.type == "cuda" and self._warm is None and not isinstance(features, CSR)
+                and (self.encoder is None or (self.encoder.mode == "int" and
+                                              getattr(self.encoder, "string_names", False)))):
+            y = None if labels is None else self._labels_to_float(labels)
+            rows = self._prepare_device(features, y)
+            if rows is not None:
+                return rows
+        if not isinstance(features, (list, CSR)) and _arrow(features):
+            features = features.to_pylist() if hasattr(features, "to_pylist") else features.tolist()
         if self.encoder is None and self._warm is not None and not isinstance(features, CSR):
             feats = self._warm["feature"].tolist()
             if any(isinstance(f, str) and not f.lstrip("-").isdigit() for f in feats):

@@ -143,3 +143,29 @@ def test_train_ffm_sql_udtf_ingests_on_device():
         os.environ.pop("HM_INGEST_HOST")
     for x, z in ((ba.idx, bb.idx), (ba.fld, bb.fld), (ba.val, bb.val), (ba.y, bb.y)):
         assert torch.equal(x.cpu(), z.cpu())
+
+
+@pytest.mark.gpu
+def test_linear_learner_ingests_integer_features_on_device():
+    """train_classifier over "idx:value" strings: the GPU path parses them on the device and
+    trains the same model as host-parsed rows; non-integer names fall back to the host
+    dictionary encoder."""
+    from hivemall_amd.models.linear import TrainClassifier
+
+    rnd = random.Random(7)
+    rows = [[f"{rnd.randint(1, 500)}:{rnd.choice(['0.5', '1', '2.25'])}" for _ in range(12)] + ["0:1.0"]
+            for _ in range(3000)]
+    y = [rnd.randint(0, 1) for _ in range(3000)]
+    a = TrainClassifier("-loss logloss -replicas 4", device="cuda")
+    ra = a.prepare(rows, y)
+    assert ingest.LAST_STATS.chunks >= 1 and ingest.LAST_STATS.host_fallback_chunks == 0
+    b = TrainClassifier("-loss logloss -replicas 4", device="cpu")
+    rb = b.prepare(rows, y)
+    assert torch.equal(ra.indptr.cpu(), rb.indptr) and torch.equal(ra.idx.cpu(), rb.idx)
+    assert torch.equal(ra.val.cpu(), rb.val) and torch.equal(ra.y.cpu(), rb.y)
+    a.fit(rows=ra)
+    tab = a.model_table()
+    assert tab["feature"].map(type).eq(str).all()          # string names stay strings
+    c = TrainClassifier("-loss logloss", device="cuda")
+    rc = c.prepare([["a:1", "b:2"], ["c"]], [1, 0])          # dictionary names: host encoder
+    assert c.encoder.mode == "dict" and rc.n == 2
