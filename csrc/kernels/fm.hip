@@ -222,10 +222,162 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
     }
 }
 
+// Pipelined variant (default): the same per-row math and Hogwild update as fm_kernel, with the
+// row's dependent load chain taken off the critical path.  A wave's next row (row + nw) has its
+// CSR bounds loaded one iteration ahead and its indices/values at the top of the current
+// iteration (read-only data, so nothing goes stale): on entry to a row only the V/w gathers are
+// left to wait for — one global round trip instead of three (indptr -> idx -> V).  V is NOT
+// prefetched across rows: the wave's own update of the current row may touch the next row's
+// features.  Reductions are DPP wave sums (~8 instructions against ~36 for the shuffle
+// butterfly; EXEC is full in the forward pass).
+template <int KP, bool BF16>
+__global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t* __restrict__ indptr,
+                                                      const int32_t* __restrict__ idx,
+                                                      const float* __restrict__ val,
+                                                      const float* __restrict__ y, int64_t n_rows,
+                                                      int64_t t0, float* __restrict__ w,
+                                                      void* __restrict__ V, float* __restrict__ w0,
+                                                      float* __restrict__ pred, float* __restrict__ loss) {
+    const int lane = hm::lane_id();
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    if (gw >= n_rows) return;                                  // wave-uniform
+    // pipeline registers: bounds of the current row, first-chunk (index, value) of it
+    int64_t s = indptr[gw], e = indptr[gw + 1];
+    int ci = -1;
+    float cx = 0.f;
+    if (lane < e - s) {
+        ci = idx[s + lane];
+        cx = val ? val[s + lane] : 1.f;
+    }
+    int64_t ns = 0, ne = 0;                                   // bounds of row + nw
+    if (gw + nw < n_rows) { ns = indptr[gw + nw]; ne = indptr[gw + nw + 1]; }
+    // the global-bias shards are read one row ahead too: the atomics of the other waves keep
+    // those lines out of L2, so a same-row read was a memory round trip on the critical path
+    // (one row of extra staleness on a parameter every wave of the chip updates anyway)
+    float w0part = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
+    float yy = y ? y[gw] : 0.f;
+    for (int64_t row = gw; row < n_rows; row += nw) {
+        const int nnz = (int)(e - s);
+        int i = (ci >= 0 && ci < P.dims) ? ci : -1;
+        float x = i >= 0 ? cx : 0.f;
+        // ---- gathers of this row (the only loads the forward waits for) ----
+        VRow<KP, BF16> vr;
+        float wi = 0.f;
+        if (i >= 0) {
+            vr.load(V, i);
+            wi = w[i];
+        } else {
+#pragma unroll
+            for (int f = 0; f < KP; ++f) vr.v[f] = 0.f;
+        }
+        // ---- prefetch: next row's indices/values/label/bias shards, the row after's bounds ----
+        const int64_t nrow = row + nw;
+        int pi = -1;
+        float px = 0.f, pw0 = 0.f, py = 0.f;
+        int64_t ns2 = 0, ne2 = 0;
+        if (nrow < n_rows) {
+            pw0 = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
+            py = y ? y[nrow] : 0.f;
+            if (lane < ne - ns) {
+                pi = idx[ns + lane];
+                px = val ? val[ns + lane] : 1.f;
+            }
+            if (nrow + nw < n_rows) { ns2 = indptr[nrow + nw]; ne2 = indptr[nrow + nw + 1]; }
+        }
+        // ---- forward ----
+        float S[KP];
+        float lin = wi * x, sq = 0.f;
+#pragma unroll
+        for (int f = 0; f < KP; ++f) {
+            const float vx = vr.v[f] * x;
+            S[f] = vx;
+            sq += vx * vx;
+        }
+        for (int base = 64; base < nnz; base += 64) {             // rows wider than one wave
+            const int j = base + lane;
+            int i2 = -1;
+            float x2 = 0.f;
+            if (j < nnz) {
+                i2 = idx[s + j];
+                x2 = val ? val[s + j] : 1.f;
+                if (i2 < 0 || i2 >= P.dims) i2 = -1;
+            }
+            if (i2 >= 0) {
+                VRow<KP, BF16> t;
+                t.load(V, i2);
+                lin += w[i2] * x2;
+#pragma unroll
+                for (int f = 0; f < KP; ++f) {
+                    const float vx = t.v[f] * x2;
+                    S[f] += vx;
+                    sq += vx * vx;
+                }
+            }
+        }
+        lin = hm::wave_sum_uniform(lin);
+        sq = hm::wave_sum_uniform(sq);
+        float pair = 0.f;
+#pragma unroll
+        for (int f = 0; f < KP; ++f) {
+            S[f] = hm::wave_sum_uniform(S[f]);
+            pair += S[f] * S[f];
+        }
+        float p = lin + 0.5f * (pair - sq);
+        const float w0v = P.use_w0 ? hm::wave_sum_uniform(w0part) : 0.f;
+        p += w0v;
+        float d;
+        if (P.classification) {
+            const float z = yy * p;
+            d = -yy / (1.f + __expf(z));
+            if (lane == 0) {
+                if (pred) pred[row] = p;
+                if (loss) loss[row] = hm::log1pexp(-z);
+            }
+        } else {
+            const float pc = fminf(fmaxf(p, P.min_target), P.max_target);
+            d = pc - yy;
+            if (lane == 0) {
+                if (pred) pred[row] = pc;
+                if (loss) loss[row] = 0.5f * d * d;
+            }
+        }
+        if (P.train) {
+            const float eta = fm_eta(P, (float)(t0 + row + 1));
+            const uint32_t rbase = P.seed ^ (uint32_t)(t0 + row) * 0x9E3779B9u;
+            auto upd = [&](VRow<KP, BF16>& t, int ii, float xx, float ww) {
+                w[ii] = ww - eta * (d * xx + 2.f * P.lambda_w * ww);
+#pragma unroll
+                for (int f = 0; f < KP; ++f) {
+                    const float g = d * xx * (S[f] - t.v[f] * xx) + 2.f * P.lambda_v * t.v[f];
+                    t.v[f] = f < P.k ? t.v[f] - eta * g : 0.f;
+                }
+                t.store(V, ii, rbase);
+            };
+            if (i >= 0) upd(vr, i, x, wi);
+            for (int base = 64; base < nnz; base += 64) {
+                const int j = base + lane;
+                if (j >= nnz) continue;
+                const int i2 = idx[s + j];
+                if (i2 < 0 || i2 >= P.dims) continue;
+                const float x2 = val ? val[s + j] : 1.f;
+                VRow<KP, BF16> t;
+                t.load(V, i2);
+                upd(t, i2, x2, w[i2]);
+            }
+            if (P.use_w0 && lane == 0)
+                atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, -eta * (d + 2.f * P.lambda0 * w0v));
+        }
+        // rotate the pipeline
+        s = ns; e = ne; ci = pi; cx = px; w0part = pw0; yy = py;
+        ns = ns2; ne = ne2;
+    }
+}
+
 template <int KP, bool BF16>
 int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const float* val,
            const float* y, int64_t n, int64_t t0, float* w, void* V, float* w0, float* pred,
-           float* loss, int grid, hipStream_t st) {
+           float* loss, int grid, int variant, hipStream_t st) {
     // Default: 256 blocks x 4 waves.  With the global bias behind ONE atomic address every
     // grid topped out near 40 M rows/s (64 blocks was best; profiles/fm_sweep_r1.log); with 64
     // line-padded shards (profiles/fm_grid_probe_r1.log, 2M rows, 2^24 features, k=8 bf16):
@@ -238,14 +390,19 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
     if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
-                       val, y, n, t0, w, V, w0, pred, loss);
+    if (variant == 1)
+        hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
+                           val, y, n, t0, w, V, w0, pred, loss);
+    else
+        hipLaunchKernelGGL((fm_pipe_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
+                           val, y, n, t0, w, V, w0, pred, loss);
     HM_LAUNCH_RET();
 }
 
 }  // namespace
 
-// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards
+// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant
+//     (variant 0 = fm_pipe_kernel, 1 = fm_kernel)
 // hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
                       const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
@@ -257,14 +414,15 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     const int bf16 = ip[7], grid = ip[8];
     P.seed = (uint32_t)ip[9];
     P.w0_shards = ip[10];
+    const int variant = ip[11];
     if (P.w0_shards < 1 || P.w0_shards > 64) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
     if (n_rows <= 0) return 0;
 #define HM_FM_CASE(K)                                                                            \
     case K:                                                                                      \
-        return bf16 ? launch<K, true>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, stream) \
-                    : launch<K, false>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, stream);
+        return bf16 ? launch<K, true>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, stream) \
+                    : launch<K, false>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, stream);
     switch (KP) {
         HM_FM_CASE(4)
         HM_FM_CASE(8)

@@ -5,6 +5,8 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import torch
 
@@ -49,7 +51,8 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
             assert t.numel() >= n
     bf16 = V.dtype == torch.bfloat16
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
-                   int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32)], dtype=np.int32)
+                   int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
+                   int(os.environ.get("HM_FM_VARIANT", "0"))], dtype=np.int32)
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,
                    h.min_target, h.max_target], dtype=np.float32)
