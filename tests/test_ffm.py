@@ -209,3 +209,31 @@ def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
         p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
     assert abs(res["cpu"] - res["cuda"]) < 0.016, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [4, 5])
+def test_ffm_pipe_polling_variants_match_at_grid1(variant):
+    """The polled pipelined kernels (LDS_EMPTY marks instead of vmcnt(0) waits, shared slots and
+    linear terms handed over in LDS) at grid 1 — where the only concurrency is the kernel's own
+    lookahead — give the vmcnt kernel's held-out logloss (measured 0.444252 / 0.444294 vs
+    0.444253, benchmarks/probes/ffm_sink_probe.py)."""
+    from hivemall_amd.ops import ffm as ffm_op
+
+    idx, y = criteo_like(20000, hash_bits=16, seed=5)
+    eidx, ey = criteo_like(5000, hash_bits=16, seed=99)
+    res = {}
+    old = ffm_op._VARIANT
+    try:
+        for v in (3, variant):
+            ffm_op._VARIANT = v
+            t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 16 -seed 1 -bf16_state",
+                           device="cuda")
+            t.grid = 1
+            t.fit(batch=FFMBatch(idx, None, None, y).to("cuda"))
+            ffm_op._VARIANT = 3
+            p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to("cuda")).cpu()
+            res[v] = torch.nn.functional.binary_cross_entropy_with_logits(p, (ey > 0).float()).item()
+    finally:
+        ffm_op._VARIANT = old
+    assert np.isfinite(res[variant]) and abs(res[variant] - res[3]) < 1e-3, res
