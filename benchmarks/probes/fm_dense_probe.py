@@ -6,10 +6,9 @@ loss.  Two engines:
 
 * ``rowwise``: ``train_fm``'s gfx950 kernel (``csrc/kernels/fm.hip``) on CSR rows with 28
   non-zeros each — Hivemall's per-row SGD, every row of every wave touching the SAME 28 V rows;
-* ``minibatch``: B rows per step as bf16 GEMMs (torch.matmul -> hipBLASLt, MFMA):
-  XV = X V, p = w0 + X w + 0.5 * sum((XV)^2 - X^2 V^2), g = dloss/dp,
-  dV = X^T (g * XV) - V * (X^2)^T g, dw = X^T g — AdaGrad on the mean gradient; the step is
-  captured once in a HIP graph and replayed per batch (one launch per step on the host).
+* ``minibatch``: ``train_fm -engine minibatch`` (models/fm_dense.py) — B rows per step in two
+  fused launches (``csrc/kernels/fm_dense.hip``), AdaGrad on the mean gradient, whole epochs
+  replayed from HIP graphs.
 
 Reports rows/s of the timed second epoch and held-out logloss for each engine.
     python benchmarks/probes/fm_dense_probe.py [--rows N] [--batches 1024,8192,65536]
@@ -53,67 +52,40 @@ def rowwise(X, y, Xe, ye, epochs):
     return out
 
 
-def minibatch(X, y, Xe, ye, epochs, B, k=8, lr=0.05, eps=1e-8, graph=True):
+def minibatch(X, y, Xe, ye, epochs, B, k=8):
+    """``train_fm -engine minibatch`` (models/fm_dense.py) end to end, plus the engine's own
+    per-epoch time (epochs after the first: the HIP graphs are captured in epoch 1)."""
+    from hivemall_amd.models.fm import FMTrainer
+    from hivemall_amd.models.fm_dense import DenseMinibatchFM, densify
+    from hivemall_amd.models.linear import SparseRows
+
     n, d = X.shape
     dev = X.device
-    g = torch.Generator(device="cpu").manual_seed(3)
-    V = (torch.randn(d, k, generator=g) * 0.01).to(dev)
-    w = torch.zeros(d, device=dev)
-    w0 = torch.zeros(1, device=dev)
-    GV, Gw, Gw0 = torch.zeros_like(V), torch.zeros_like(w), torch.zeros_like(w0)
-    nb = n // B
-    Xb = X[: nb * B].to(torch.bfloat16).reshape(nb, B, d)
-    yb = y[: nb * B].reshape(nb, B)
-    sX = torch.empty(B, d, dtype=torch.bfloat16, device=dev)
-    sy = torch.empty(B, device=dev)
-
-    def step():
-        x = sX
-        Vb = V.to(torch.bfloat16)
-        XV = (x @ Vb).float()                                     # [B, k]   MFMA
-        x2 = x.float().square()
-        p = w0 + x.float() @ w + 0.5 * (XV.square().sum(1) - x2 @ V.square().sum(1))
-        gr = (torch.sigmoid(p) - sy) / B                          # d mean-logloss / dp
-        dV = (x.t() @ (gr[:, None] * XV).to(torch.bfloat16)).float() - V * (x2.t() @ gr)[:, None]
-        dw = x.float().t() @ gr
-        dw0 = gr.sum().reshape(1)
-        for P, G, D in ((V, GV, dV), (w, Gw, dw), (w0, Gw0, dw0)):
-            G.add_(D.square())
-            P.sub_(lr * D / (G.sqrt() + eps))
-
-    sX.copy_(Xb[0])
-    sy.copy_(yb[0])
-    if graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):                    # warm the kernels before capture
-            for _ in range(2):
-                step()
-        torch.cuda.current_stream().wait_stream(s)
-        for P in (V, w, w0, GV, Gw, Gw0):
-            P.zero_()
-        V.copy_((torch.randn(d, k, generator=torch.Generator().manual_seed(3)) * 0.01).to(dev))
-        gph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gph):
-            step()
-        run = gph.replay
-    else:
-        run = step
-    rps = None
-    for ep in range(epochs):
-        _sync()
-        t0 = time.perf_counter()
-        for b in range(nb):
-            sX.copy_(Xb[b], non_blocking=True)
-            sy.copy_(yb[b], non_blocking=True)
-            run()
-        _sync()
-        rps = round(nb * B / (time.perf_counter() - t0))
-    Xf = Xe.float()
-    XV = Xf @ V
-    p = w0 + Xf @ w + 0.5 * (XV.square().sum(1) - Xf.square() @ V.square().sum(1))
-    return {"rows_per_s": rps, "heldout_logloss": round(Fn.binary_cross_entropy_with_logits(p, ye).item(), 5),
-            "batch": B, "steps_per_epoch": nb}
+    yy = torch.where(y > 0, 1.0, -1.0)
+    Xd = densify(torch.arange(0, n * d + 1, d, dtype=torch.int64, device=dev),
+                 torch.arange(d, dtype=torch.int32, device=dev).repeat(n), X.reshape(-1), d, dev)
+    eng = DenseMinibatchFM(d, k, torch.randn(d, k, generator=torch.Generator().manual_seed(3)) * 0.01, dev, B,
+                           0.05, 0.01, 0.01, 0.01, True, -3.4e38, 3.4e38)
+    eng.epoch(Xd, yy)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(epochs - 1):
+        eng.epoch(Xd, yy)
+    _sync()
+    rps = round(n * (epochs - 1) / (time.perf_counter() - t0))
+    ll_engine = Fn.binary_cross_entropy_with_logits(eng.predict(Xe), ye).item()
+    # the same through the learner API (write-back into the FM state, predicted by the kernel)
+    rows = SparseRows(torch.arange(0, n * d + 1, d, dtype=torch.int64, device=dev),
+                      torch.arange(d, dtype=torch.int32, device=dev).repeat(n), X.reshape(-1).contiguous(), yy)
+    t = FMTrainer(f"-c -factors {k} -num_features {d} -sigma 0.01 -iters {epochs} -disable_cv -fp32 "
+                  f"-engine minibatch -mini_batch {B}", device=dev)
+    t.fit(rows=rows)
+    ne = Xe.shape[0]
+    er = SparseRows(torch.arange(0, ne * d + 1, d, dtype=torch.int64, device=dev),
+                    torch.arange(d, dtype=torch.int32, device=dev).repeat(ne), Xe.reshape(-1).contiguous(), None)
+    ll_api = Fn.binary_cross_entropy_with_logits(t.predict_raw(rows=er), ye).item()
+    return {"rows_per_s": rps, "heldout_logloss": round(ll_engine, 5), "heldout_logloss_train_fm_api": round(ll_api, 5),
+            "batch": B, "steps_per_epoch": n // B}
 
 
 def main():
@@ -129,7 +101,7 @@ def main():
     base = {"probe": "fm_dense", "rows": a.rows, "features": 28, "k": 8, "epochs": a.epochs}
     print(json.dumps({**base, "engine": "rowwise_hogwild_kernel", **rowwise(X, y, Xe, ye, a.epochs)}), flush=True)
     for B in (int(b) for b in a.batches.split(",")):
-        print(json.dumps({**base, "engine": "minibatch_gemm_graph", **minibatch(X, y, Xe, ye, a.epochs, B)}),
+        print(json.dumps({**base, "engine": "train_fm -engine minibatch (fm_dense.hip + HIP graphs)", **minibatch(X, y, Xe, ye, a.epochs, B)}),
               flush=True)
 
 

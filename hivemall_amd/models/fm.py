@@ -78,6 +78,9 @@ FM_OPTS = [
     flag("disable_cv", "disable_cvtest", "Disable convergence check"),
     flag("fp32", None, "[engine] keep V in fp32 on the GPU (default bf16)"),
     opt("batch_size", None, 1 << 20, int, "[engine] rows per kernel launch"),
+    opt("engine", None, "rowwise", str, "[engine] rowwise (per-row Hogwild kernel) | minibatch "
+        "(dense mini-batch GEMMs + AdaGrad; for low-dimensional dense rows, models/fm_dense.py)"),
+    opt("mini_batch", None, 8192, int, "[engine] rows per step of -engine minibatch"),
 ] + MIX_OPTS
 _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2}
 
@@ -196,6 +199,8 @@ class FMTrainer(Learner):
         if rows.y is None:
             raise UDFArgumentException("train_fm: labels are required")
         self._ensure(rows)
+        if str(self.cl["engine"]).lower() == "minibatch":
+            return self._fit_minibatch(rows)
         va = None
         if self.cl["adareg"] and rows.n > int(self.cl["va_threshold"]):
             # hold out the tail as the validation slice for adaptive regularization
@@ -211,6 +216,42 @@ class FMTrainer(Learner):
             if self.cv.is_converged():
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
+        self.mix()
+        return self
+
+    def _fit_minibatch(self, rows: SparseRows) -> "FMTrainer":
+        """-engine minibatch (models/fm_dense.py): rows densified to X [n, dims] fp32 in HBM,
+        mini-batch AdaGrad steps replayed from HIP graphs; the result is written back into the
+        usual state so prediction, model_table and mixing are unchanged."""
+        from .fm_dense import DenseMinibatchFM, densify
+
+        dims = self.dims
+        if dims > 4096 or rows.n * dims > (1 << 31):
+            raise UDFArgumentException(
+                f"train_fm -engine minibatch: {rows.n} x {dims} dense rows do not fit the dense "
+                "engine (dims <= 4096); use the default rowwise engine for sparse rows")
+        if self.cl["adareg"]:
+            log.warning("train_fm -engine minibatch: -adareg is not applied by this engine")
+        X = densify(rows.indptr, rows.idx, rows.val, dims, self.device)
+        y = rows.y.to(self.device, torch.float32)
+        if self.h.classification:
+            y = torch.where(y > 0, 1.0, -1.0)
+        st = self.state
+        eng = DenseMinibatchFM(dims, self.k, st["V"].float(), self.device, int(self.cl["mini_batch"]),
+                               self.h.eta0, self.h.lambda0, self.h.lambda_w, self.h.lambda_v,
+                               self.h.classification, self.h.min_target, self.h.max_target)
+        for ep in range(int(self.cl["iters"])):
+            self.cv.incr_loss(eng.epoch(X, y))
+            if self.cv.is_converged():
+                log.info("train_fm converged at epoch %d", ep + 1)
+                break
+        self.t += rows.n * (ep + 1)
+        st["w"].copy_(eng.w)
+        st["V"][:, : self.k] = eng.V[:, : self.k].to(st["V"].dtype)
+        st["w0"].zero_()
+        st["w0"][0] = eng.w0[0]
+        i = rows.idx.long()
+        self.touched[i[(i >= 0) & (i < self.dims)]] = True
         self.mix()
         return self
 
