@@ -1,6 +1,6 @@
-"""Per-row loss traces of the pipelined FFM kernel, polled (variant 0) vs vmcnt(0) waits
-(variant 3), at grid 1 on bf16 state: the first row where they differ, on Criteo-like rows
-(shared features) and on rows with disjoint features.
+"""Per-row loss traces at grid 1 on bf16 state: the polled pipelined FFM kernel (variant 5) vs
+the round-1 packed kernel (variant 1, no lookahead: the sequential order) — the first row where
+they differ, on Criteo-like rows (shared features) and on rows with disjoint features.
     python benchmarks/probes/ffm_poll_trace.py
 """
 import torch
@@ -31,8 +31,8 @@ def main():
                                         torch.where(torch.rand(4096) < 0.3, 1.0, -1.0))}.items():
         nf = int(idx.max()) + 1
         for lin in (False, True):
-            a, Va = trace(0, idx.cuda(), y.cuda(), nf, lin)
-            b, Vb = trace(3, idx.cuda(), y.cuda(), nf, lin)
+            a, Va = trace(5, idx.cuda(), y.cuda(), nf, lin)
+            b, Vb = trace(1, idx.cuda(), y.cuda(), nf, lin)
             d = (a - b).abs()
             bad = torch.nonzero(d > 1e-6).flatten()
             first = int(bad[0]) if bad.numel() else -1
@@ -40,7 +40,7 @@ def main():
                   f"max|dloss| {d.max().item():.3g}, max|dV| {(Va - Vb).abs().max().item():.3g}", flush=True)
             if first >= 0:
                 r = first
-                print("   loss poll", a[max(0, r - 2): r + 3].tolist(), "\n   loss vmcnt", b[max(0, r - 2): r + 3].tolist())
+                print("   loss poll  ", a[max(0, r - 2): r + 3].tolist(), "\n   loss packed", b[max(0, r - 2): r + 3].tolist())
                 prev = idx[r - 1].tolist() if r else []
                 print("   shared features with the previous row:", len(set(prev) & set(idx[r].tolist())),
                       "with row-2:", len(set(idx[r - 2].tolist()) & set(idx[r].tolist())) if r > 1 else None)

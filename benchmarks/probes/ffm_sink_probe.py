@@ -1,5 +1,6 @@
 """Pipelined FFM kernel variants at fixed grids: polled DMA targets with the next row's slot DMA
-issued early (C, HM_FFM_VARIANT 5) or late (after this row's stores, 4) vs vmcnt(0) waits (3).
+issued early (C, HM_FFM_VARIANT 5) or late (after this row's stores, 4) vs vmcnt(0) waits (the
+default, 0) and the round-1 packed kernel (1, no lookahead).
 Held-out logloss of bf16-state training on one stream, to separate a semantic difference
 (visible at grid 1, where the only concurrency is the kernel's own one-row lookahead) from
 Hogwild staleness (full grid).
@@ -22,7 +23,7 @@ def run(variant, grid, n, bits, opts=""):
                    device="cuda")
     t.grid = grid
     t.fit(batch=FFMBatch(idx, None, None, y).to("cuda"))
-    ffm_op._VARIANT = 3
+    ffm_op._VARIANT = 0
     p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to("cuda")).cpu()
     return torch.nn.functional.binary_cross_entropy_with_logits(p, (ey > 0).float()).item()
 
@@ -30,9 +31,9 @@ def run(variant, grid, n, bits, opts=""):
 def main():
     for grid, n, bits, opts in ((1, 30000, 16, ""), (1, 30000, 16, "-disable_wi"),
                                 (0, 1000000, 20, ""), (0, 1000000, 20, "-disable_wi")):
-        r = {v: round(run(v, grid, n, bits, opts), 6) for v in (5, 3, 4)}
+        r = {v: round(run(v, grid, n, bits, opts), 6) for v in (5, 0, 4, 1)}
         print(json.dumps({"grid": grid, "rows": n, "bits": bits, "opts": opts,
-                          "logloss_poll_early_dma": r[5], "logloss_vmcnt": r[3], "logloss_poll_late_dma": r[4]}),
+                          "logloss_poll_early_dma": r[5], "logloss_vmcnt": r[0], "logloss_poll_late_dma": r[4], "logloss_round1_packed": r[1]}),
               flush=True)
 
 

@@ -905,19 +905,18 @@ __device__ __forceinline__ bool lds_poll4(const void* p, uint32_t empty) {
     return false;
 }
 
-// PM (polling modes, HM_FFM_VARIANT 4 / 5, training only).  Step A's vmcnt(0) also waits for the
-// previous row's ~1,500 slot stores, issued just before it.  With PM every LDS-DMA target is
-// re-marked "empty" (LDS_EMPTY) after it is consumed and the consumer polls its own words until
-// the DMA has overwritten the mark (the wave that issued a DMA polls it; fallback vmcnt(0) past
-// POLL_MAX), so no wave waits on stores.  A slot the next row shares with this one (same feature
-// and field: same address, same thread) and a shared linear term are handed over in LDS by E
-// instead of DMA'd.  PM 1 issues the next row's slot DMA in C (as the vmcnt kernel does), PM 2
-// after this row's stores.  Measured (benchmarks/probes/ffm_sink_probe.py, ffm_poll_trace.py,
-// profiles/ffm_poll_r2.log): at grid 1 all three give the sequential engine's logloss, but at
-// full grid PM 1 runs +14 % rows/s at +1.3e-3 held-out logloss (its gathers are a row older
-// than the vmcnt kernel's — whose DMA, though issued in C, returns data that includes stores
-// made during D/E: grid-1 row losses equal the sequential engine's), and PM 2 matches the vmcnt
-// kernel in both rows/s and logloss.  The default stays the vmcnt kernel.
+// PM (polling modes, HM_FFM_VARIANT 4 / 5, training only; an experiment kept opt-in).  Step A's
+// vmcnt(0) also waits for the previous row's ~1,500 slot stores.  With PM every LDS-DMA target
+// is re-marked "empty" (LDS_EMPTY) after it is consumed and the consumer polls its own words
+// until the DMA has overwritten the mark (the wave that issued a DMA polls it; fallback
+// vmcnt(0) past POLL_MAX), so no wave waits on stores; a slot or linear term the next row
+// shares with this one (same feature and field: same address, same thread) is handed over in
+// LDS by E instead of DMA'd.  PM 1 issues the next row's slot DMA in C, PM 2 after this row's
+// stores.  Measured same-box (profiles/ffm_poll_r2/bench_ab_corrected.log): default 101.1-101.6 M
+// rows/s at held-out 0.4510-0.4512, PM 1 100.3-100.8 M at 0.4516-0.4518, PM 2 98.8-99.3 M at
+// 0.4510-0.4512 — the store wait is not what bounds this kernel.  At grid 1 the handover makes
+// PM 1 / 2 match the sequential order (round-1 packed kernel) where the default is one row stale
+// (benchmarks/probes/ffm_sink_probe.py), but at full grid cross-block staleness dominates.
 template <int NS, int PM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1369,7 +1368,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
              float* pred, float* loss, int grid, int packed, int variant, hipStream_t stream) {
     if (packed) {
         int rc = -1;
-        if (variant == 0 || variant == 2) {
+        if (variant != 1) {
             rc = dispatch_lean<BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
             if (rc != -1) return rc;
         }
@@ -1396,8 +1395,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 // variant (Kp == 4, packed, F <= 45, table < 4 GiB): 0 = auto (bf16: ffm_pipe_kernel with
 // vmcnt(0) waits; fp32: ffm_lean_kernel), 1 = ffm_packed_kernel (round 1), 2 = ffm_lean_kernel,
 // 3 = ffm_pipe_kernel (vmcnt), 4 / 5 = ffm_pipe_kernel polling its DMA targets with the next
-// row's slot DMA issued after / before this row's stores (training only; A/B: 5 is +14 % rows/s
-// at +1.3e-3 held-out logloss, see ffm_pipe_kernel)
+// row's slot DMA issued after / before this row's stores (training only; no faster, see PM above)
 // packed = 1: V and G are the two halves of one [num_features][num_fields][2][Kp] table
 //             (G == V + Kp elements, slot stride 2*Kp); 0: separate [.][.][Kp] tables.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,

@@ -43,7 +43,7 @@ _CALLS = 0  # per-launch counter mixed into the stochastic-rounding seed
 # kernel variant (A/B only), K <= 4 packed: 0 = auto (bf16 state: LDS-DMA pipelined
 # ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the round-1 ffm_packed_kernel, 2 = ffm_lean_kernel,
 # 3 = ffm_pipe_kernel, 4 / 5 = ffm_pipe_kernel polling its DMA targets, next row's gather issued
-# after / before this row's stores (5: +14 % rows/s at +1.3e-3 held-out logloss)
+# after / before this row's stores (measured no faster: profiles/ffm_poll_r2/)
 _VARIANT = int(os.environ.get("HM_FFM_VARIANT", "0"))
 
 
