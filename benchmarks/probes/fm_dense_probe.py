@@ -52,7 +52,7 @@ def rowwise(X, y, Xe, ye, epochs):
     return out
 
 
-def minibatch(X, y, Xe, ye, epochs, B, k=8):
+def minibatch(X, y, Xe, ye, epochs, B, k=8, variant=0, blocks=0, api=True):
     """``train_fm -engine minibatch`` (models/fm_dense.py) end to end, plus the engine's own
     per-epoch time (epochs after the first: the HIP graphs are captured in epoch 1)."""
     from hivemall_amd.models.fm import FMTrainer
@@ -65,7 +65,7 @@ def minibatch(X, y, Xe, ye, epochs, B, k=8):
     Xd = densify(torch.arange(0, n * d + 1, d, dtype=torch.int64, device=dev),
                  torch.arange(d, dtype=torch.int32, device=dev).repeat(n), X.reshape(-1), d, dev)
     eng = DenseMinibatchFM(d, k, torch.randn(d, k, generator=torch.Generator().manual_seed(3)) * 0.01, dev, B,
-                           0.05, 0.01, 0.01, 0.01, True, -3.4e38, 3.4e38)
+                           0.05, 0.01, 0.01, 0.01, True, -3.4e38, 3.4e38, variant=variant, blocks=blocks)
     eng.epoch(Xd, yy)
     _sync()
     t0 = time.perf_counter()
@@ -74,6 +74,9 @@ def minibatch(X, y, Xe, ye, epochs, B, k=8):
     _sync()
     rps = round(n * (epochs - 1) / (time.perf_counter() - t0))
     ll_engine = Fn.binary_cross_entropy_with_logits(eng.predict(Xe), ye).item()
+    if not api:
+        return {"rows_per_s": rps, "heldout_logloss": round(ll_engine, 5), "batch": B, "steps_per_epoch": n // B,
+                "variant": ["mfma", "valu"][variant], "blocks": blocks}
     # the same through the learner API (write-back into the FM state, predicted by the kernel)
     rows = SparseRows(torch.arange(0, n * d + 1, d, dtype=torch.int64, device=dev),
                       torch.arange(d, dtype=torch.int32, device=dev).repeat(n), X.reshape(-1).contiguous(), yy)
@@ -93,12 +96,23 @@ def main():
     ap.add_argument("--rows", type=int, default=4_000_000)
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--batches", default="1024,8192,65536")
+    ap.add_argument("--ab", action="store_true", help="gradient-kernel A/B: MFMA (block sweep) vs VALU")
+    ap.add_argument("--blocks", default="0,256,1024")
     a = ap.parse_args()
     from hivemall_amd.io.synthetic import higgs_like
 
     X, y = higgs_like(a.rows, seed=5, device="cuda")
     Xe, ye = higgs_like(500_000, seed=77, device="cuda")
     base = {"probe": "fm_dense", "rows": a.rows, "features": 28, "k": 8, "epochs": a.epochs}
+    if a.ab:
+        for rep in range(2):
+            for B in (int(b) for b in a.batches.split(",")):
+                print(json.dumps({**base, "engine": "minibatch", **minibatch(X, y, Xe, ye, a.epochs, B, variant=1, api=False)}),
+                      flush=True)
+                for nb in (int(b) for b in a.blocks.split(",")):
+                    print(json.dumps({**base, "engine": "minibatch", **minibatch(X, y, Xe, ye, a.epochs, B, variant=0, blocks=nb,
+                                                                                  api=False)}), flush=True)
+        return
     print(json.dumps({**base, "engine": "rowwise_hogwild_kernel", **rowwise(X, y, Xe, ye, a.epochs)}), flush=True)
     for B in (int(b) for b in a.batches.split(",")):
         print(json.dumps({**base, "engine": "train_fm -engine minibatch (fm_dense.hip + HIP graphs)", **minibatch(X, y, Xe, ye, a.epochs, B)}),

@@ -33,6 +33,8 @@ struct MFParams {
     uint32_t seed;
     int max_tries;             // negative-sampling rejection tries
     int coherent;              // 1: factor/bias/state loads bypass L1 (hm::ld_coherent)
+    int atomic;                // MF: 0 = read-modify-write stores, 1 = atomic delta adds on users
+                               // and items, 2 = atomic adds on items only (the skewed side)
 };
 
 // Shared-model load: L1-bypassing unless disabled for an A/B (HM_MF_PLAIN_LOADS=1).
@@ -94,13 +96,45 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
         const float t = (float)(t0 + r + 1);
         if (!P.adagrad) {
             const float eta = eta_t(P, t);
+            const float dp = eta * (e * qi - P.lambda_u * pu), dq = eta * (e * pu - P.lambda_i * qi);
+            const float dbu = eta * (e - P.lambda_b * bu), dbi = eta * (e - P.lambda_b * bi);
+            if (P.atomic) {
+                // Hogwild as analysed (Niu et al.): component-wise atomic increments, so
+                // concurrent ratings of one popular item/user all land (reads stay stale)
+                if (fa) {
+                    if (P.atomic == 1) atomicAdd(Pu + ou, dp);
+                    else Pu[ou] = pu + dp;
+                    atomicAdd(Qi + oi, dq);
+                }
+                if (P.use_bias && f == 0) {
+                    if (P.atomic == 1) atomicAdd(Bu + u, dbu);
+                    else Bu[u] = bu + dbu;
+                    atomicAdd(Bi + i, dbi);
+                }
+            } else {
+                if (fa) {
+                    Pu[ou] = pu + dp;
+                    Qi[oi] = qi + dq;
+                }
+                if (P.use_bias && f == 0) {
+                    Bu[u] = bu + dbu;
+                    Bi[i] = bi + dbi;
+                }
+            }
+        } else if (P.atomic) {
             if (fa) {
-                Pu[ou] = pu + eta * (e * qi - P.lambda_u * pu);
-                Qi[oi] = qi + eta * (e * pu - P.lambda_i * qi);
+                const float gp = e * qi - P.lambda_u * pu, gq = e * pu - P.lambda_i * qi;
+                const float Gp = atomicAdd(GPu + ou, gp * gp) + gp * gp;
+                const float Gq = atomicAdd(GQi + oi, gq * gq) + gq * gq;
+                atomicAdd(Pu + ou, P.eta0 * gp * rsqrtf(P.eps + Gp));
+                atomicAdd(Qi + oi, P.eta0 * gq * rsqrtf(P.eps + Gq));
             }
             if (P.use_bias && f == 0) {
-                Bu[u] = bu + eta * (e - P.lambda_b * bu);
-                Bi[i] = bi + eta * (e - P.lambda_b * bi);
+                const float gbu = e - P.lambda_b * bu, gbi = e - P.lambda_b * bi;
+                const float Gu = atomicAdd(GBu + u, gbu * gbu) + gbu * gbu;
+                const float Gi = atomicAdd(GBi + i, gbi * gbi) + gbi * gbi;
+                atomicAdd(Bu + u, P.eta0 * gbu * rsqrtf(P.eps + Gu));
+                atomicAdd(Bi + i, P.eta0 * gbi * rsqrtf(P.eps + Gi));
             }
         } else {
             if (fa) {
@@ -222,6 +256,7 @@ MFParams unpack(const int32_t* ip, const float* hp) {
     P.use_bias = ip[5]; P.update_mean = ip[6]; P.eta_kind = ip[7]; P.loss = ip[8];
     P.seed = (uint32_t)ip[9]; P.max_tries = ip[10] > 0 ? ip[10] : 16;
     P.coherent = ip[12] == 0;  // ip[12] = 1: plain (L1-cached) loads, A/B only
+    P.atomic = ip[13];         // MF: atomic delta updates
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda_u = hp[3];
     P.lambda_i = hp[4]; P.lambda_j = hp[5]; P.lambda_b = hp[6]; P.eps = hp[7];
     return P;
@@ -243,7 +278,7 @@ int grid_for(int64_t n, int per) {
 }  // namespace
 
 // ip: k, kp, n_users, n_items, adagrad, use_bias, update_mean, eta_kind, loss, seed, max_tries,
-//     grid, plain_loads
+//     grid, plain_loads, atomic
 // hp: eta0, power_t, total_steps, lambda_u, lambda_i, lambda_j, lambda_b, eps
 HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
                       const int32_t* items, const float* ratings, int64_t n, int64_t t0, float* Pu,

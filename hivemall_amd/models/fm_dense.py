@@ -12,8 +12,10 @@ B rows computes
     XV = X V,  p = w0 + X w + 0.5 sum_f ((XV)^2 - X^2 V^2)_f,  g = dloss/dp,
     dV = X^T (g * XV) - V * (X^2)^T g,  dw = X^T g,  dw0 = sum g
 and an AdaGrad update of the mean gradient (L2 terms lambda0 / lambda_w / lambda).  On the GPU
-(d <= 64, padded k <= 32) a step is two launches of ``csrc/kernels/fm_dense.hip`` (row tiles in
-LDS, per-workgroup partial gradients, a parameter-parallel AdaGrad kernel); elsewhere it is the
+(d <= 64, padded k <= 32) a step is two launches of ``csrc/kernels/fm_dense.hip``: a gradient
+kernel whose two GEMM-shaped products (X V and (g X)^T [XV | 1]) run on f32 MFMA
+(v_mfma_f32_16x16x4_f32: exact f32) with the partial gradient held in accumulator registers over
+the workgroup's row tiles, then a parameter-parallel AdaGrad kernel; elsewhere it is the
 same math as torch ops (the GEMM formulation — on the GPU hipBLASLt's MFMA kernels — measured
 9-56 M rows/s, launch- and skinny-GEMM-bound).  A whole epoch (up to 256 steps per graph) is
 captured once as HIP graphs and replayed, so the host issues one launch per 256 steps.
@@ -30,12 +32,14 @@ from .. import _native
 GRAPH_STEPS = 256
 _P = _native.c_p
 _native.register_hip("hm_fmd_step", [_P] * 13)     # ..., loss_sum, stream
+_native.register_hip("hm_fmd_max_blocks", [], restype=__import__("ctypes").c_int64)
 
 
 class DenseMinibatchFM:
     def __init__(self, dims: int, k: int, V0: torch.Tensor, device, batch: int, lr: float,
                  lambda0: float, lambda_w: float, lambda_v: float, classification: bool,
-                 min_target: float, max_target: float, eps: float = 1e-8):
+                 min_target: float, max_target: float, eps: float = 1e-8, variant: int = 0,
+                 blocks: int = 0):
         dev = torch.device(device)
         self.dims, self.k, self.B, self.dev = int(dims), int(k), int(batch), dev
         self.KP = int(V0.shape[1])             # padded factors (columns >= k stay zero)
@@ -56,7 +60,11 @@ class DenseMinibatchFM:
         self.kernel = dev.type == "cuda" and self.dims <= 64 and self.KP <= 32
         if self.kernel:
             self._hp = np.array([self.lr, self.eps, self.l0, self.lw, self.lv, self.lo, self.hi], dtype=np.float32)
-            self._partial = torch.empty(min(128, (self.B + 63) // 64) * (self.dims * self.KP + self.dims + 2),
+            # variant 0: the f32-MFMA gradient kernel, 1: the VALU kernel; blocks: workgroups per
+            # step (0 = the kernel's default); partial rows for up to hm_fmd_max_blocks() workgroups
+            self.variant, self.blocks = int(variant), int(blocks)
+            nblk = min(max(128, int(_native.hip().hm_fmd_max_blocks())), (self.B + 63) // 64)
+            self._partial = torch.empty(nblk * (self.dims * self.KP + self.dims + 2),
                                         dtype=torch.float32, device=dev)
             self._ips: dict = {}
 
@@ -73,7 +81,8 @@ class DenseMinibatchFM:
         if self.kernel and b <= self.B:
             ip = self._ips.get(b)
             if ip is None:      # kept alive: a captured graph bakes the pointer values in
-                ip = self._ips[b] = np.array([b, self.dims, self.KP, self.k, int(self.cls)], dtype=np.int64)
+                ip = self._ips[b] = np.array([b, self.dims, self.KP, self.k, int(self.cls), self.variant,
+                                              self.blocks], dtype=np.int64)
             p = _native.ptr
             rc = _native.hip().hm_fmd_step(ip.ctypes.data, self._hp.ctypes.data, p(x), p(y), p(self.V), p(self.w),
                                            p(self.w0), p(self.GV), p(self.Gw), p(self.Gw0), p(self._partial),

@@ -171,13 +171,17 @@ class _MFBase(Learner):
             raise UDFArgumentException(f"{self.NAME}: unknown -eta {eta}")
         return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
-                         self._grid(), int(os.environ.get("HM_MF_PLAIN_LOADS", "0") == "1")],
+                         self._grid(), int(os.environ.get("HM_MF_PLAIN_LOADS", "0") == "1"),
+                         int(os.environ.get("HM_MF_ATOMIC", "1"))],
                         dtype=np.int32)
 
     # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
-    # keeps 256: on a small catalogue, concurrent stale updates slow the escape from the
-    # near-zero factor init (300 items: 20-epoch RMSE 0.14 at grid 1, 1.40 at grid 3, 2.24 at
-    # grid 9; profiles/mf_staleness_probe23_r1.log, docs/perf_notes.md); -grid overrides.
+    # updates are atomic delta adds (HM_MF_ATOMIC=1, default): with them the held-out RMSE
+    # curve equals the sequential engine's at every grid (fixture grid 1..36: 0.1438-0.1439;
+    # ML-20M shape 0.3229 vs sequential 0.3217 after 12 epochs), while read-modify-write
+    # stores lost concurrent updates of popular rows and never left the bias-only level
+    # (profiles/mf_atomic_r2/).  A wider grid no longer hurts quality but also does not add
+    # throughput (~350 M ratings/s at grid 106 or 848), so the cap stays; -grid overrides.
     ROWS_PER_BLOCK = 256
 
     def _grid(self) -> int:

@@ -172,3 +172,59 @@ def test_fm_minibatch_engine_gpu_graphs_match_cpu():
     # near-zero gradients show up at ~1e-3 after 120 steps
     np.testing.assert_allclose(tg.state["V"].cpu().numpy(), tc.state["V"].numpy(), rtol=1e-2, atol=3e-3)
     assert abs(llg - llc) < 1e-3 and llg < 0.62, (llg, llc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("d,KP,k,n,blocks,cls", [
+    (28, 8, 8, 4096, 0, True),        # HIGGS shape, 64 tiles
+    (28, 8, 8, 64 * 40 + 17, 4, True),  # tail tile, 10+ tiles per workgroup (prefetch loop)
+    (5, 8, 3, 300, 0, False),          # padded factors, regression clip, d < 8
+    (40, 16, 16, 1000, 3, True),       # two output column blocks (KP + 2 > 16)
+    (64, 32, 30, 777, 0, False),       # d = 64: the bias row in a fifth row block; 3 column blocks
+])
+def test_fm_minibatch_kernel_gradient_matches_fp32_reference(variant, d, KP, k, n, blocks, cls, device="cuda"):
+    """One hm_fmd_step (variant 0: f32-MFMA gradient kernel, 1: VALU kernel) against the
+    float64 autograd gradient of the mean FM loss + L2.  lr = eps = 1e6 turns AdaGrad's first
+    step into P -= D (to ~|D| 1e-6), so the parameter change IS the kernel's gradient."""
+    from hivemall_amd.models.fm_dense import DenseMinibatchFM
+
+    g = torch.Generator().manual_seed(d * 131 + n)
+    x = torch.randn(n, d, generator=g)
+    y = torch.where(torch.rand(n, generator=g) < 0.4, 1.0, -1.0) if cls else torch.randn(n, generator=g) * 2
+    V0 = torch.zeros(d, KP)
+    V0[:, :k] = torch.randn(d, k, generator=g) * 0.2
+    lo, hi = (-3.4e38, 3.4e38) if cls else (-1.5, 1.5)
+    e = DenseMinibatchFM(d, k, V0, device, n, 1e6, 0.01, 0.02, 0.03, cls, lo, hi, eps=1e6,
+                         variant=variant, blocks=blocks)
+    w_init = torch.randn(d, generator=g) * 0.1
+    e.w.copy_(w_init)
+    e.w0.fill_(0.05)
+    e.step(x.to(device), y.to(device))
+    if device == "cuda":
+        torch.cuda.synchronize()
+    V = V0.double().clone().requires_grad_()
+    w = w_init.double().clone().requires_grad_()
+    w0 = torch.full((1,), 0.05, dtype=torch.float64, requires_grad=True)
+    xd = x.double()
+    XV = xd @ V
+    p = w0 + xd @ w + 0.5 * (XV.square().sum(1) - (xd * xd) @ V.square().sum(1))
+    if cls:
+        data = torch.nn.functional.softplus(-y.double() * p)
+    else:
+        # Hivemall clips the prediction and takes (clip(p) - y) as dloss/dp (straight-through)
+        data = 0.5 * (p + (p.clamp(lo, hi) - p).detach() - y.double()).square()
+    loss = data.mean() + 0.5 * (0.03 * V.square().sum() + 0.02 * w.square().sum() + 0.01 * w0.square().sum())
+    loss.backward()
+    gV = V.grad.clone()
+    gV[:, k:] = 0                                          # padded columns are never updated
+    for got, want, init in ((e.V, gV, V0), (e.w, w.grad, w_init), (e.w0, w0.grad, torch.tensor([0.05]))):
+        D = init.double() - got.double().cpu()
+        np.testing.assert_allclose(D.numpy(), want.numpy(), rtol=2e-4, atol=2e-6)
+    assert abs(e.loss_sum.item() - data.sum().item()) < 1e-4 * n
+
+
+@pytest.mark.parametrize("d,KP,k,n,cls", [(28, 8, 8, 500, True), (5, 8, 3, 300, False)])
+def test_fm_minibatch_gradient_reference_cpu(d, KP, k, n, cls):
+    """The same gradient check on the CPU path (torch ops) — validates the check itself."""
+    test_fm_minibatch_kernel_gradient_matches_fp32_reference(0, d, KP, k, n, 0, cls, device="cpu")

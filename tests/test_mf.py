@@ -112,6 +112,23 @@ def test_mf_gpu_quality():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cls,opts", [(MatrixFactorization, "-eta0 0.01"), (MatrixFactorizationAdaGrad, "-eta0 0.1")])
+def test_mf_gpu_wide_grid_learns_factors(cls, opts):
+    """Hogwild at -grid 9 / 36 (up to 576 ratings in flight on a 300-item catalogue): with the
+    atomic delta updates the factors are learned as sequentially (plain read-modify-write
+    stores lost most concurrent updates and stayed at the bias-only RMSE 2.25;
+    profiles/mf_atomic_r2/)."""
+    u, i, r = _ratings()
+    base = cls(f"-factors 10 -iters 20 -disable_cv -update_mean {opts}", device="cpu").fit(u[:35000], i[:35000], r[:35000])
+    ref = float(np.sqrt(((base.predict(u[35000:], i[35000:]) - r[35000:]) ** 2).mean()))
+    for grid in (9, 36):
+        m = cls(f"-factors 10 -iters 20 -disable_cv -update_mean -grid {grid} {opts}", device="cuda").fit(
+            u[:35000], i[:35000], r[:35000])
+        rmse = float(np.sqrt(((m.predict(u[35000:], i[35000:]) - r[35000:]) ** 2).mean()))
+        assert rmse < ref * 1.1 + 0.02, (grid, rmse, ref)
+
+
+@pytest.mark.gpu
 def test_bpr_gpu_explicit_triples_match_cpu():
     n = 200
     u, i, j = np.arange(n), np.arange(n), np.arange(n, 2 * n)
