@@ -917,8 +917,10 @@ __device__ __forceinline__ bool lds_poll4(const void* p, uint32_t empty) {
 // 0.4510-0.4512 — the store wait is not what bounds this kernel.  At grid 1 the handover makes
 // PM 1 / 2 match the sequential order (round-1 packed kernel) where the default is one row stale
 // (benchmarks/probes/ffm_sink_probe.py), but at full grid cross-block staleness dominates.
-template <int NS, int PM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_kernel(
+// BF = false: the same pipeline over fp32 packed slots (32 B: V float4 | G float4; two 16-B DMAs
+// per slot; LDS 77.6 KB at NS = 6 -> 2 blocks/CU); PM = 0 only; opt-in (HM_FFM_VARIANT=3).
+template <int NS, int PM, bool BF = true>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2))) void ffm_pipe_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
@@ -926,8 +928,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 {
     constexpr bool POLL = PM != 0;   // PM 1: next row's slot DMA in C; 2: after this row's stores (F)
     constexpr bool LATE = PM == 2;
-    __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256];   // slot DMA landing zone
-    __shared__ __attribute__((aligned(16))) uint2 s_t[NS * 256];     // transposed V image
+    static_assert(BF || PM == 0, "fp32 state: vmcnt waits only");
+    constexpr uint32_t SLOT_B = BF ? 16u : 32u;                        // bytes per packed slot
+    using Img = typename std::conditional<BF, uint2, float4>::type;   // V in the transposed image
+    __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256 * (BF ? 1 : 2)];   // slot DMA landing zone
+    __shared__ __attribute__((aligned(16))) Img s_t[NS * 256];        // transposed V image
     // F <= 45 (F*F <= 2048): per-field arrays of 48; total LDS 40,736 B at NS = 6 -> 4 blocks/CU
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
@@ -998,7 +1003,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
         const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
         const bool live = ok && SA(j) != SB(j);
-        const uint32_t o = ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * 16u;   // branch-free
+        const uint32_t o = ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * SLOT_B;   // branch-free
         const float x = __int_as_float(ma.z) * __int_as_float(mb.z);
         off = ok ? o : 0u;
         xab = live ? x : 0.f;
@@ -1011,8 +1016,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             uint32_t off;
             float xab;
             slot(bf, j, off, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + off),
-                                             (lds_ptr_t)(s_raw + j * 256 + wave * 64), 16, 0, 0);
+            if constexpr (BF) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + off),
+                                                 (lds_ptr_t)(s_raw + j * 256 + wave * 64), 16, 0, 0);
+            } else {   // V half, then G half: rows 2j and 2j + 1 of the landing zone
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + off),
+                                                 (lds_ptr_t)(s_raw + (2 * j) * 256 + wave * 64), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + off + 16u),
+                                                 (lds_ptr_t)(s_raw + (2 * j + 1) * 256 + wave * 64), 16, 0, 0);
+            }
         }
     };
     // wave W_LIN, lanes < F with a valid feature: DMA of w, z, n of the row in buffer bf
@@ -1070,7 +1082,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         bar_raw();
         // ---- B: raw -> registers, V -> transposed image; meta(row + G) -> s_m[nxt] ----
         uint4 q[NS];
-        if constexpr (POLL) {
+        float4 qv[NS], qg[NS];   // fp32 state
+        if constexpr (!BF) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const uint4 a = s_raw[(2 * j) * 256 + tid], b = s_raw[(2 * j + 1) * 256 + tid];
+                qv[j] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+                qg[j] = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
+            }
+        } else if constexpr (POLL) {
             // this thread's own slot DMAs (issued by its wave): poll until every word has replaced
             // its mark; past POLL_MAX wait for the DMA itself
             for (int it = 0;; ++it) {
@@ -1090,7 +1110,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 #pragma unroll
             for (int j = 0; j < NS; ++j) q[j] = s_raw[j * 256 + tid];
         }
-        if constexpr (POLL) {
+        if constexpr (!BF) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = qv[j];
+        } else if constexpr (POLL) {
 #pragma unroll
             for (int j = 0; j < NS; ++j) lds_write8(&s_t[SB(j) * F + SA(j)], make_uint2(q[j].x, q[j].y));
         } else {
@@ -1148,8 +1171,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int s = tid + j * 256;
-            const uint2 pv = s_t[s < FF ? s : 0];
-            const float d = dot2_bf16(q[j].x, pv.x, dot2_bf16(q[j].y, pv.y, 0.f));
+            float d;
+            if constexpr (BF) {
+                const uint2 pv = s_t[s < FF ? s : 0];
+                d = dot2_bf16(q[j].x, pv.x, dot2_bf16(q[j].y, pv.y, 0.f));
+            } else {
+                const float4 pv = s_t[s < FF ? s : 0];
+                d = qv[j].x * pv.x + qv[j].y * pv.y + qv[j].z * pv.z + qv[j].w * pv.w;
+            }
             part += d * xab[j];
         }
         part *= 0.5f * scale * scale;
@@ -1174,10 +1203,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             for (int j = 0; j < NS; ++j) {
                 const int s = tid + j * 256;
                 const f2 coef = {ks * xab[j], ks * xab[j]};
-                const uint2 pv = s_t[s < FF ? s : 0];
-                f2 o0 = bf2_to_f2(q[j].x), o1 = bf2_to_f2(q[j].y);
-                f2 g0 = bf2_to_f2(q[j].z), g1 = bf2_to_f2(q[j].w);
-                const f2 p0 = bf2_to_f2(pv.x), p1 = bf2_to_f2(pv.y);
+                f2 o0, o1, g0, g1, p0, p1;
+                if constexpr (BF) {
+                    const uint2 pv = s_t[s < FF ? s : 0];
+                    o0 = bf2_to_f2(q[j].x); o1 = bf2_to_f2(q[j].y);
+                    g0 = bf2_to_f2(q[j].z); g1 = bf2_to_f2(q[j].w);
+                    p0 = bf2_to_f2(pv.x);   p1 = bf2_to_f2(pv.y);
+                } else {
+                    const float4 pv = s_t[s < FF ? s : 0];
+                    o0 = f2{qv[j].x, qv[j].y}; o1 = f2{qv[j].z, qv[j].w};
+                    g0 = f2{qg[j].x, qg[j].y}; g1 = f2{qg[j].z, qg[j].w};
+                    p0 = f2{pv.x, pv.y};       p1 = f2{pv.z, pv.w};
+                }
                 // diagonal slots: coef = 0 and lambda = 0 -> d = 0, V and G unchanged, and the
                 // stochastic rounding of a value already in bf16 is exact
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
@@ -1190,6 +1227,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 const f2 r1 = {__builtin_amdgcn_rsqf(t1.x), __builtin_amdgcn_rsqf(t1.y)};
                 o0 = o0 + meta * d0 * r0;
                 o1 = o1 + meta * d1 * r1;
+                if constexpr (!BF) {
+                    if (wr >> j & 1u) {
+                        *reinterpret_cast<float4*>(vg + off[j]) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                        *reinterpret_cast<float4*>(vg + off[j] + 16u) = make_float4(g0.x, g0.y, g1.x, g1.y);
+                    }
+                    continue;
+                }
                 // this thread's row hash, re-keyed per slot: each 16-bit window stays uniform
                 const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
                 const uint4 st = make_uint4(pack_sr_hi(o0, h, rotl32(h, 16)),
@@ -1201,8 +1245,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             }
             if (mi >= 0) {
                 // the feature block's pad slots (never read): zeros, completing its last line
-                for (int f = P.num_fields; f < (int)nfld; ++f)
-                    *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * 16u) = make_uint4(0u, 0u, 0u, 0u);
+                for (int f = P.num_fields; f < (int)nfld; ++f) {
+                    *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * SLOT_B) = make_uint4(0u, 0u, 0u, 0u);
+                    if (!BF) *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * SLOT_B + 16u) = make_uint4(0u, 0u, 0u, 0u);
+                }
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
                     float lz, ln;
                     if (POLL) {
@@ -1284,6 +1330,22 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
             else if (need <= 6) { HM_PIPE(6); }
             else { HM_PIPE(8); }
 #undef HM_PIPE
+            HM_LAUNCH_RET();
+        }
+    } else {
+        // fp32 state: the same pipeline over 32-B slots, opt-in (variant 3).  Measured same-box
+        // (profiles/ffm_r2/fp32_pipe_ab.log): 52.5 M rows/s vs the lean kernel's 51.2 M (+2.6 %)
+        // — both move ~4.9 TB/s of slot traffic, the rate the bf16 pipeline reaches too — while
+        // its extra row of staleness costs held-out logloss at small row counts (500 K rows:
+        // +0.019 vs sequential, lean +0.010), so the lean kernel stays the fp32 default.
+        if (variant == 3) {
+#define HM_PIPE32(NSV) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, 0, false>), dim3(blocks), dim3(256), 0, stream, P, idx, \
+                                          fld, val, y, VG, w, wz, wn, bias, pred, loss)
+            if (need <= 2) { HM_PIPE32(2); }
+            else if (need <= 4) { HM_PIPE32(4); }
+            else if (need <= 6) { HM_PIPE32(6); }
+            else { HM_PIPE32(8); }
+#undef HM_PIPE32
             HM_LAUNCH_RET();
         }
     }
@@ -1394,7 +1456,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride
 // variant (Kp == 4, packed, F <= 45, table < 4 GiB): 0 = auto (bf16: ffm_pipe_kernel with
 // vmcnt(0) waits; fp32: ffm_lean_kernel), 1 = ffm_packed_kernel (round 1), 2 = ffm_lean_kernel,
-// 3 = ffm_pipe_kernel (vmcnt), 4 / 5 = ffm_pipe_kernel polling its DMA targets with the next
+// 3 = ffm_pipe_kernel (vmcnt; bf16 or fp32 state), 4 / 5 = ffm_pipe_kernel polling its DMA targets with the next
 // row's slot DMA issued after / before this row's stores (training only; no faster, see PM above)
 // packed = 1: V and G are the two halves of one [num_features][num_fields][2][Kp] table
 //             (G == V + Kp elements, slot stride 2*Kp); 0: separate [.][.][Kp] tables.

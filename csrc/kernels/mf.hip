@@ -35,6 +35,7 @@ struct MFParams {
     int coherent;              // 1: factor/bias/state loads bypass L1 (hm::ld_coherent)
     int atomic;                // MF: 0 = read-modify-write stores, 1 = atomic delta adds on users
                                // and items, 2 = atomic adds on items only (the skewed side)
+    int bstride;               // MF: element stride of Bu / Bi / GBu / GBi (16: one 64-B line each)
 };
 
 // Shared-model load: L1-bypassing unless disabled for an A/B (HM_MF_PLAIN_LOADS=1).
@@ -83,7 +84,8 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
         if (fa) { pu = ldm(P, Pu + ou); qi = ldm(P, Qi + oi); }
         float dot = group_sum<G>(pu * qi);
         float bu = 0.f, bi = 0.f;
-        if (ok && P.use_bias) { bu = ldm(P, Bu + u); bi = ldm(P, Bi + i); }
+        const size_t bu_o = (size_t)(ok ? u : 0) * P.bstride, bi_o = (size_t)(ok ? i : 0) * P.bstride;
+        if (ok && P.use_bias) { bu = ldm(P, Bu + bu_o); bi = ldm(P, Bi + bi_o); }
         const float m = ldm(P, mu);
         const float rhat = m + bu + bi + dot;
         const float rr = act ? ratings[r] : 0.f;
@@ -107,9 +109,9 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
                     atomicAdd(Qi + oi, dq);
                 }
                 if (P.use_bias && f == 0) {
-                    if (P.atomic == 1) atomicAdd(Bu + u, dbu);
-                    else Bu[u] = bu + dbu;
-                    atomicAdd(Bi + i, dbi);
+                    if (P.atomic == 1) atomicAdd(Bu + bu_o, dbu);
+                    else Bu[bu_o] = bu + dbu;
+                    atomicAdd(Bi + bi_o, dbi);
                 }
             } else {
                 if (fa) {
@@ -117,8 +119,8 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
                     Qi[oi] = qi + dq;
                 }
                 if (P.use_bias && f == 0) {
-                    Bu[u] = bu + dbu;
-                    Bi[i] = bi + dbi;
+                    Bu[bu_o] = bu + dbu;
+                    Bi[bi_o] = bi + dbi;
                 }
             }
         } else if (P.atomic) {
@@ -131,10 +133,10 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
             }
             if (P.use_bias && f == 0) {
                 const float gbu = e - P.lambda_b * bu, gbi = e - P.lambda_b * bi;
-                const float Gu = atomicAdd(GBu + u, gbu * gbu) + gbu * gbu;
-                const float Gi = atomicAdd(GBi + i, gbi * gbi) + gbi * gbi;
-                atomicAdd(Bu + u, P.eta0 * gbu * rsqrtf(P.eps + Gu));
-                atomicAdd(Bi + i, P.eta0 * gbi * rsqrtf(P.eps + Gi));
+                const float Gu = atomicAdd(GBu + bu_o, gbu * gbu) + gbu * gbu;
+                const float Gi = atomicAdd(GBi + bi_o, gbi * gbi) + gbi * gbi;
+                atomicAdd(Bu + bu_o, P.eta0 * gbu * rsqrtf(P.eps + Gu));
+                atomicAdd(Bi + bi_o, P.eta0 * gbi * rsqrtf(P.eps + Gi));
             }
         } else {
             if (fa) {
@@ -147,11 +149,11 @@ __global__ __launch_bounds__(256) void mf_kernel(MFParams P, const int32_t* __re
             }
             if (P.use_bias && f == 0) {
                 const float gbu = e - P.lambda_b * bu, gbi = e - P.lambda_b * bi;
-                const float Gu = ldm(P, GBu + u) + gbu * gbu, Gi = ldm(P, GBi + i) + gbi * gbi;
-                GBu[u] = Gu;
-                GBi[i] = Gi;
-                Bu[u] = bu + P.eta0 * gbu * rsqrtf(P.eps + Gu);
-                Bi[i] = bi + P.eta0 * gbi * rsqrtf(P.eps + Gi);
+                const float Gu = ldm(P, GBu + bu_o) + gbu * gbu, Gi = ldm(P, GBi + bi_o) + gbi * gbi;
+                GBu[bu_o] = Gu;
+                GBi[bi_o] = Gi;
+                Bu[bu_o] = bu + P.eta0 * gbu * rsqrtf(P.eps + Gu);
+                Bi[bi_o] = bi + P.eta0 * gbi * rsqrtf(P.eps + Gi);
             }
         }
     }
@@ -257,6 +259,7 @@ MFParams unpack(const int32_t* ip, const float* hp) {
     P.seed = (uint32_t)ip[9]; P.max_tries = ip[10] > 0 ? ip[10] : 16;
     P.coherent = ip[12] == 0;  // ip[12] = 1: plain (L1-cached) loads, A/B only
     P.atomic = ip[13];         // MF: atomic delta updates
+    P.bstride = ip[14] > 0 ? ip[14] : 1;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda_u = hp[3];
     P.lambda_i = hp[4]; P.lambda_j = hp[5]; P.lambda_b = hp[6]; P.eps = hp[7];
     return P;
@@ -278,7 +281,7 @@ int grid_for(int64_t n, int per) {
 }  // namespace
 
 // ip: k, kp, n_users, n_items, adagrad, use_bias, update_mean, eta_kind, loss, seed, max_tries,
-//     grid, plain_loads, atomic
+//     grid, plain_loads, atomic, bias_stride
 // hp: eta0, power_t, total_steps, lambda_u, lambda_i, lambda_j, lambda_b, eps
 HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
                       const int32_t* items, const float* ratings, int64_t n, int64_t t0, float* Pu,

@@ -172,17 +172,19 @@ class _MFBase(Learner):
         return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
                          self._grid(), int(os.environ.get("HM_MF_PLAIN_LOADS", "0") == "1"),
-                         int(os.environ.get("HM_MF_ATOMIC", "1"))],
+                         int(os.environ.get("HM_MF_ATOMIC", "1")), 0],
                         dtype=np.int32)
 
     # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
     # updates are atomic delta adds (HM_MF_ATOMIC=1, default): with them the held-out RMSE
     # curve equals the sequential engine's at every grid (fixture grid 1..36: 0.1438-0.1439;
-    # ML-20M shape 0.3229 vs sequential 0.3217 after 12 epochs), while read-modify-write
+    # ML-20M shape 0.3228 vs sequential 0.3217 after 12 epochs), while read-modify-write
     # stores lost concurrent updates of popular rows and never left the bias-only level
-    # (profiles/mf_atomic_r2/).  A wider grid no longer hurts quality but also does not add
-    # throughput (~350 M ratings/s at grid 106 or 848), so the cap stays; -grid overrides.
+    # (profiles/mf_atomic_r2/).  So the grid is sized for throughput, as for BPR: 32 rows per
+    # block (ML-20M: 852 blocks; 794 M ratings/s at 106 blocks, 847 M at 3,392).  With
+    # HM_MF_ATOMIC=0 (A/B only) the old cap of 256 rows per block applies.
     ROWS_PER_BLOCK = 256
+    ROWS_PER_BLOCK_ATOMIC = 32
 
     def _grid(self) -> int:
         """Hogwild concurrency cap: keep the number of ratings in flight well below the number
@@ -192,7 +194,10 @@ class _MFBase(Learner):
         g = int(self.cl["grid"])
         if g > 0:
             return g
-        return int(max(1, min(4096, min(self.n_users, self.n_items) // self.ROWS_PER_BLOCK)))
+        rows = self.ROWS_PER_BLOCK
+        if self.ROWS_PER_BLOCK_ATOMIC and os.environ.get("HM_MF_ATOMIC", "1") != "0":
+            rows = self.ROWS_PER_BLOCK_ATOMIC
+        return int(max(1, min(4096, min(self.n_users, self.n_items) // rows)))
 
 
 class MatrixFactorization(_MFBase):
@@ -233,16 +238,44 @@ class MatrixFactorization(_MFBase):
         lam = float(c["lambda"])
         return np.array([self._eta0(), c["power_t"], c["t"], lam, lam, lam, lam, c["eps"]], dtype=np.float32)
 
+    # Atomic bias updates on the GPU go to line-padded copies (one 64-B line per user / item):
+    # in the packed arrays the 16 most popular items share one line, and its same-line atomics
+    # bounded the whole kernel (ML-20M shape: 372 M ratings/s with biases, 890 M without;
+    # profiles/mf_atomic_r2/contention.log).  Copied in and out around each training launch.
+    BIAS_PAD = 16
+
+    def _padded_bias(self, names):
+        pads = getattr(self, "_bias_pads", None)
+        if pads is None:
+            pads = self._bias_pads = {}
+        out = []
+        for nm in names:
+            t = self.state[nm]
+            b = pads.get(nm)
+            if b is None or b.shape[0] != t.shape[0]:
+                b = pads[nm] = torch.zeros(t.shape[0], self.BIAS_PAD, dtype=t.dtype, device=t.device)
+            b[:, 0].copy_(t)
+            out.append(b)
+        return out
+
     def _step(self, u, i, r, train=True, pred=None, loss=None):
         st = self.state
         p = _native.ptr
         ip, hp = self._ip(), self._hp()
         n = u.numel()
+        names = ["Bu", "Bi"] + (["GBu", "GBi"] if self.adagrad else [])
+        pad = u.is_cuda and train and self.use_bias and int(ip[13]) != 0
+        bias = dict(zip(names, self._padded_bias(names))) if pad else {nm: st.get(nm) for nm in names}
+        if pad:
+            ip[14] = self.BIAS_PAD
         args = [ip.ctypes.data, hp.ctypes.data, p(u), p(i), p(r), C.c_int64(n), C.c_int64(self.t),
-                p(st["P"]), p(st["Q"]), p(st["Bu"]), p(st["Bi"]), p(st["mu"]), p(st.get("GP")),
-                p(st.get("GQ")), p(st.get("GBu")), p(st.get("GBi")), int(train), p(pred), p(loss)]
+                p(st["P"]), p(st["Q"]), p(bias["Bu"]), p(bias["Bi"]), p(st["mu"]), p(st.get("GP")),
+                p(st.get("GQ")), p(bias.get("GBu")), p(bias.get("GBi")), int(train), p(pred), p(loss)]
         if u.is_cuda:
             _native.check(_native.hip().hm_mf_step(*args, _native.stream_of(u.device)), "hm_mf_step")
+            if pad:
+                for nm in names:
+                    st[nm].copy_(bias[nm][:, 0])
         else:
             _native.host().hm_mf_step_cpu(*args)
         if train:
@@ -329,6 +362,7 @@ class BPRMF(_MFBase):
     # sweep on MI355X (profiles/bpr_grid_r1.log): grid 106 -> 852 blocks = 170M -> 966M
     # triples/s at sampled AUC 0.7103 -> 0.7101 (sequential CPU engine 0.7105).
     ROWS_PER_BLOCK = 32
+    ROWS_PER_BLOCK_ATOMIC = None   # BPR updates are plain stores (AUC-neutral at every grid)
     NAME = "train_bprmf"
     OPTIONS = BPR_OPTS
 
