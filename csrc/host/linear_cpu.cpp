@@ -43,6 +43,7 @@ void train_replica(const Params& P, int r, int R, int dims, int L, int64_t n_row
         const float yy = y[row];
         rs[RS_T] += 1.f;
         const float t = rs[RS_T];
+        const StepK sk = step_consts(P, t);
         if (!mc) {
             float p = 0.f, var = 0.f, sq = 0.f;
             for (int64_t k = s; k < e; ++k) {
@@ -72,7 +73,7 @@ void train_replica(const Params& P, int r, int R, int dims, int L, int64_t n_row
                     const float inv = 1.f / (float)in_batch;
                     for (int i : tlist) {
                         F4 st = ld4(M + (size_t)i * 4);
-                        optimizer_update(P, st, gacc[i] * inv, t, rs[RS_EVE_D]);
+                        optimizer_update(P, st, gacc[i] * inv, sk, rs[RS_EVE_D]);
                         st4(M + (size_t)i * 4, st);
                         gacc[i] = 0.f;
                         gmark[i] = 0;
@@ -88,7 +89,7 @@ void train_replica(const Params& P, int r, int R, int dims, int L, int64_t n_row
                 if (i < 0 || i >= dims) continue;
                 const float x = val ? val[k] : 1.f;
                 F4 st = ld4(M + (size_t)i * 4);
-                feature_update(P, c, st, x, t, rs[RS_EVE_D]);
+                feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
                 st4(M + (size_t)i * 4, st);
             }
         } else {
@@ -144,7 +145,9 @@ HM_API int hm_linear_train_cpu(const Params* P, const int32_t* ip, int64_t n_row
                                float* RS, double* loss_out) {
     const int R = ip[0], dims = ip[1], L = ip[2], mini_batch = ip[3];
     if (R <= 0 || dims <= 0 || L <= 0) return 1;
-#pragma omp parallel for schedule(dynamic, 1)
+    // one replica (Hivemall's single mapper): no parallel region — waking the OpenMP team for
+    // one worker cost more than the a9a epoch itself
+#pragma omp parallel for schedule(dynamic, 1) if (R > 1)
     for (int r = 0; r < R; ++r)
         train_replica(*P, r, R, dims, L, n_rows, mini_batch, indptr, idx, val, y, order, S, touched,
                       RS, loss_out);

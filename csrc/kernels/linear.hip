@@ -78,6 +78,7 @@ __global__ __launch_bounds__(64) void linear_train_kernel(
         const float yy = y[row];
         rs[RS_T] += 1.f;
         const float t = rs[RS_T];
+        const StepK sk = step_consts(P, t);
         // ---- cached first chunk ----
         int ci = -1;
         float cx = 0.f;
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(64) void linear_train_kernel(
                         const int i = TL[k];
                         F4 st = ld4(M + i);
                         float2 a = GA[i];
-                        optimizer_update(P, st, a.x * inv, t, rs[RS_EVE_D]);
+                        optimizer_update(P, st, a.x * inv, sk, rs[RS_EVE_D]);
                         st4(M + i, st);
                         GA[i] = make_float2(0.f, 0.f);
                     }
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(64) void linear_train_kernel(
             }
             if (!c.update) continue;
             if (ci >= 0) {
-                feature_update(P, c, cst, cx, t, rs[RS_EVE_D]);
+                feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
                 st4(M + ci, cst);
             }
             for (int64_t k = s + 64 + lane; k < e; k += 64) {
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(64) void linear_train_kernel(
                 const float x = val ? val[k] : 1.f;
                 if (i < 0 || i >= dims) continue;
                 F4 st = ld4(M + i);
-                feature_update(P, c, st, x, t, rs[RS_EVE_D]);
+                feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
                 st4(M + i, st);
             }
         } else {
@@ -362,6 +363,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
         const float yy = y[row];
         const float t = (float)(t0 + q + 1);
         rs[RS_T] = t;
+        const StepK sk = step_consts(P, t);
         int ci = -1;
         float cx = 0.f;
         if (s + lane < e) {
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             touched[ci] = 1;
             if (c.update) {
                 if (RELOAD) cst = ld4m<NT>(S + ci);
-                feature_update(P, c, cst, cx, t, rs[RS_EVE_D]);
+                feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
                 st4(S + ci, cst);
             }
         }
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             touched[i] = 1;
             if (!c.update) continue;
             F4 st = ld4m<NT>(S + i);
-            feature_update(P, c, st, x, t, rs[RS_EVE_D]);
+            feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
             st4(S + i, st);
         }
     }

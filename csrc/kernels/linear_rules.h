@@ -150,6 +150,26 @@ HM_HD float eta_at(const Params& P, float t) {
     }
 }
 
+// Row-invariant step constants: the eta schedule and Adam-family bias corrections depend only on
+// the step t, so each row computes them once (powf per feature update dominated the CPU engine:
+// a9a AdaGrad 0.92 -> see docs/perf_notes.md) instead of once per feature.
+struct StepK {
+    float t, eta;
+    float c1, c2, c1n, cp1, cp2;   // 1 - beta^t, 1 - beta2^t, 1 - beta1^(t+1), 1 - beta^(t-1) (Adam family)
+};
+HM_HD StepK step_consts(const Params& P, float t) {
+    StepK k;
+    k.t = t;
+    k.eta = eta_at(P, t);
+    const bool adam = P.opt == O_ADAM || P.opt == O_EVE || P.opt == O_ADAM_HD || P.opt == O_NADAM;
+    k.c1 = adam ? 1.f - powf(P.beta1, t) : 0.f;
+    k.c2 = adam ? 1.f - powf(P.beta2, t) : 0.f;
+    k.c1n = P.opt == O_NADAM ? 1.f - powf(P.beta1, t + 1.f) : 0.f;
+    k.cp1 = P.opt == O_ADAM_HD ? 1.f - powf(P.beta1, t - 1.f) : 0.f;
+    k.cp2 = P.opt == O_ADAM_HD ? 1.f - powf(P.beta2, t - 1.f) : 0.f;
+    return k;
+}
+
 // ---------------------------------------------------------------- regularisers
 HM_HD float regularize(const Params& P, float w, float g) {
     switch (P.reg) {
@@ -162,10 +182,11 @@ HM_HD float regularize(const Params& P, float w, float g) {
 
 // ---------------------------------------------------------------- optimizers
 // g is dloss * x_i (before regularisation); t >= 1 is the replica step counter.
-HM_HD void optimizer_update(const Params& P, F4& s, float g, float t, float eve_d) {
+HM_HD void optimizer_update(const Params& P, F4& s, float g, const StepK& k, float eve_d) {
     const int o = (P.reg == R_RDA && P.opt == O_ADAGRAD) ? O_ADAGRAD_RDA : P.opt;
     if (o != O_ADAGRAD_RDA) g = regularize(P, s.w, g);
-    const float eta = eta_at(P, t);
+    const float eta = k.eta;
+    const float t = k.t;
     switch (o) {
         case O_SGD: s.w -= eta * g; break;
         case O_MOMENTUM: {
@@ -210,7 +231,7 @@ HM_HD void optimizer_update(const Params& P, F4& s, float g, float t, float eve_
             const float m_prev = s.s1, v_prev = s.s2;
             s.s1 = P.beta1 * s.s1 + (1.f - P.beta1) * g;
             s.s2 = P.beta2 * s.s2 + (1.f - P.beta2) * g * g;
-            const float c1 = 1.f - powf(P.beta1, t), c2 = 1.f - powf(P.beta2, t);
+            const float c1 = k.c1, c2 = k.c2;
             float vhat = s.s2;
             if (o == O_ADAM && P.amsgrad) { s.s3 = fmaxf(s.s3, s.s2); vhat = s.s3; }
             float lr = eta * P.alpha * sqrtf(c2) / c1;
@@ -218,7 +239,7 @@ HM_HD void optimizer_update(const Params& P, F4& s, float g, float t, float eve_
             if (o == O_ADAM_HD) {
                 // per-coordinate hypergradient descent on the step size (s3 = alpha_i)
                 if (s.s3 == 0.f) s.s3 = P.alpha;
-                const float cp1 = 1.f - powf(P.beta1, t - 1.f), cp2 = 1.f - powf(P.beta2, t - 1.f);
+                const float cp1 = k.cp1, cp2 = k.cp2;
                 const float u_prev = (t > 1.f && cp1 > 0.f)
                                          ? (m_prev / cp1) / (sqrtf(v_prev / (cp2 > 0.f ? cp2 : 1.f)) + P.eps)
                                          : 0.f;
@@ -231,8 +252,8 @@ HM_HD void optimizer_update(const Params& P, F4& s, float g, float t, float eve_
         case O_NADAM: {
             s.s1 = P.beta1 * s.s1 + (1.f - P.beta1) * g;
             s.s2 = P.beta2 * s.s2 + (1.f - P.beta2) * g * g;
-            const float c1 = 1.f - powf(P.beta1, t), c1n = 1.f - powf(P.beta1, t + 1.f);
-            const float c2 = 1.f - powf(P.beta2, t);
+            const float c1 = k.c1, c1n = k.c1n;
+            const float c2 = k.c2;
             const float mhat = P.beta1 * s.s1 / c1n + (1.f - P.beta1) * g / c1;
             const float vhat = s.s2 / c2;
             s.w -= eta * P.alpha * mhat / (sqrtf(vhat) + P.eps);
@@ -429,7 +450,8 @@ HM_HD RowCoef row_rule(const Params& P, float p, float y, float var, float sq, f
 }
 
 // Per-feature update of a binary/regression rule.  x: feature value, t: step.
-HM_HD void feature_update(const Params& P, const RowCoef& c, F4& s, float x, float t, float eve_d) {
+HM_HD void feature_update(const Params& P, const RowCoef& c, F4& s, float x, const StepK& k, float eve_d) {
+    const float t = k.t;
     switch (P.algo) {
         case A_PERCEPTRON: case A_PA: case A_PA1: case A_PA2:
         case A_PA1_REGR: case A_PA2_REGR: case A_PA1A_REGR: case A_PA2A_REGR:
@@ -457,7 +479,7 @@ HM_HD void feature_update(const Params& P, const RowCoef& c, F4& s, float x, flo
             break;
         }
         case A_LOGRESS: {
-            s.w -= eta_at(P, t) * c.dloss * x;
+            s.w -= k.eta * c.dloss * x;
             break;
         }
         case A_ADAGRAD_REGR: {
@@ -475,7 +497,7 @@ HM_HD void feature_update(const Params& P, const RowCoef& c, F4& s, float x, flo
             break;
         }
         case A_GENERAL:
-            optimizer_update(P, s, c.dloss * x, t, eve_d);
+            optimizer_update(P, s, c.dloss * x, k, eve_d);
             break;
     }
 }

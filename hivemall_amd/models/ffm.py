@@ -34,6 +34,7 @@ from ..io.ingest import is_arrow_like as ingest_is_arrow
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
 from .base import COMMON_ITER_OPTS, ConversionState, Learner, log, parse_labels_binary
+from ..utils.reduce import tmax
 
 
 @dataclass
@@ -170,9 +171,9 @@ class FFMTrainer(Learner):
                                                   hash_ints=self.cl["feature_hashing"] > 0,
                                                   device=self.device)[:3]
             if self.num_features is None:
-                self.num_features = int(idx.max().item()) + 1 if idx.numel() else 1
+                self.num_features = int(tmax(idx)) + 1 if idx.numel() else 1
             if self.num_fields is None:
-                self.num_fields = int(fld.max().item()) + 1 if fld.numel() else 1
+                self.num_fields = int(tmax(fld)) + 1 if fld.numel() else 1
             yt = None if y is None else torch.from_numpy(y).to(self.device)
             return FFMBatch(idx, fld, val, yt)
         if ingest_is_arrow(features):

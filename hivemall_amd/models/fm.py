@@ -30,6 +30,7 @@ from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import MIX_OPTS, ConversionState, Learner, log, parse_labels_binary
 from .linear import SparseRows, encode_rows
+from ..utils.reduce import tmax
 
 
 def _is_arrow(x) -> bool:
@@ -162,7 +163,7 @@ class FMTrainer(Learner):
         if self.state is None:
             dims = self.dims
             if dims is None:
-                dims = int(rows.idx.max().item()) + 1 if rows.idx.numel() else 1
+                dims = int(tmax(rows.idx)) + 1 if rows.idx.numel() else 1
                 if self.encoder is not None and self.encoder.mode == "dict":
                     dims = max(dims, self.encoder.vocab_size())
             self.init_state(dims)

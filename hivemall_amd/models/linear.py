@@ -31,6 +31,7 @@ from ..ops import linear as LO
 from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import ConversionState, Learner, log
+from ..utils.reduce import tmax, tmin
 
 # ------------------------------------------------------------------ option specs
 _MIX_INERT = ("mixing is a collective between the job's ranks over RCCL (-mix_interval), "
@@ -263,7 +264,7 @@ class OnlineLinearLearner(Learner):
             ip, idx, val, _ = ingest.csr_device(features, "int", device=self.device)
         except UDFArgumentException:
             return None
-        if idx.numel() and (int(idx.min().item()) < 0 or int(idx.max().item()) >= 2 ** 31 - 1):
+        if idx.numel() and (int(tmin(idx)) < 0 or int(tmax(idx)) >= 2 ** 31 - 1):
             return None
         self.encoder = FeatureEncoder("int")
         self.encoder.string_names = True
@@ -304,7 +305,7 @@ class OnlineLinearLearner(Learner):
             return
         dims = int(self.cl["dims"])
         if dims <= 0:
-            dims = int(rows.idx.max().item()) + 1 if rows.idx.numel() else 1
+            dims = int(tmax(rows.idx)) + 1 if rows.idx.numel() else 1
             if self.encoder is not None and self.encoder.mode == "dict":
                 if self._dp():
                     raise UDFArgumentException(
@@ -359,7 +360,7 @@ class OnlineLinearLearner(Learner):
         if rows.y is None:
             raise UDFArgumentException(f"{self.NAME}: labels are required")
         self._ensure_state(rows)
-        if rows.idx.numel() and int(rows.idx.max().item()) >= self.state.dims:
+        if rows.idx.numel() and int(tmax(rows.idx)) >= self.state.dims:
             log.warning("%s: feature index >= dims (%d) ignored", self.NAME, self.state.dims)
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         iters = int(self.cl["iters"])

@@ -31,6 +31,7 @@ from ..ops import topk_mips
 from ..registry import udf
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import MIX_OPTS, ConversionState, Learner, log
+from ..utils.reduce import tmax
 
 _ETAS = {"fixed": 0, "simple": 1, "inverse": 2, "inv": 2, "bolddriver": 0, "bold_driver": 0}
 _BOLD = ("bolddriver", "bold_driver")
@@ -286,7 +287,7 @@ class MatrixFactorization(_MFBase):
         u, i, r = _dev(users, torch.int32, dev), _dev(items, torch.int32, dev), \
             _dev(ratings, torch.float32, dev)
         if self.state is None:
-            self.init_state(int(u.max().item()) + 1, int(i.max().item()) + 1)
+            self.init_state(int(tmax(u)) + 1, int(tmax(i)) + 1)
             if self.cl["update_mean"]:
                 self.state["mu"].fill_(float(r.mean().item()))
         self.seen_u[u.long()] = True
@@ -485,8 +486,8 @@ class BPRMF(_MFBase):
         ti = torch.as_tensor(np.asarray(pos_items, dtype=np.int32)).to(dev)
         tj = torch.as_tensor(np.asarray(neg_items, dtype=np.int32)).to(dev)
         if self.state is None and self.sharded is None:
-            nu = int(tu.max().item()) + 1 if tu.numel() else 1
-            ni = int(max(ti.max().item(), tj.max().item())) + 1 if ti.numel() else 1
+            nu = int(tmax(tu)) + 1 if tu.numel() else 1
+            ni = int(max(tmax(ti), tmax(tj))) + 1 if ti.numel() else 1
             if self._dp():        # every rank sizes the (sharded or mixed) tables alike
                 nu = int(self.mixer.all_reduce_scalar(float(nu), "max"))
                 ni = int(self.mixer.all_reduce_scalar(float(ni), "max"))
@@ -544,7 +545,7 @@ class BPRMF(_MFBase):
         u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev) if not torch.is_tensor(users) else users.to(dev)
         i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev) if not torch.is_tensor(items) else items.to(dev)
         if self.state is None:
-            self.init_state(n_users or int(u.max().item()) + 1, n_items or int(i.max().item()) + 1)
+            self.init_state(n_users or int(tmax(u)) + 1, n_items or int(tmax(i)) + 1)
         csr = self.build_csr(u, i, self.n_users)
         self.seen_u[u.long()] = True
         self.seen_i.fill_(True)
