@@ -161,8 +161,28 @@ __global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ b
     }
 }
 
-// out[s] = max_r |stats[r, s]| (out zeroed by the caller): non-negative floats order like their
-// bit patterns, so a block max finishes with one integer atomicMax per column.
+// Column |max| finish: every wave's maxima -> LDS -> one integer atomicMax per column per BLOCK
+// (non-negative floats order like their bit patterns).  Per-wave atomics on the same 3 words
+// serialised: 8,192 of them cost ~0.28 ms per 11M-row tree (profiles/gbt_r2/).
+template <int NS>
+__device__ __forceinline__ void block_absmax_flush(float (&m)[NS], float* __restrict__ out) {
+    __shared__ float s_m[4][NS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        float v = m[s];
+        for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+        if (lane == 0) s_m[w][s] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+        const int s = threadIdx.x;
+        const float v = fmaxf(fmaxf(s_m[0][s], s_m[1][s]), fmaxf(s_m[2][s], s_m[3][s]));
+        atomicMax(reinterpret_cast<int*>(out) + s, __float_as_int(v));
+    }
+}
+
+// out[s] = max_r |stats[r, s]| (out zeroed by the caller)
 template <int NS>
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ stats, int64_t n,
                                                      float* __restrict__ out) {
@@ -174,11 +194,43 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
 #pragma unroll
         for (int s = 0; s < NS; ++s) m[s] = fmaxf(m[s], fabsf(stats[r * NS + s]));
     }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        float v = m[s];
-        for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-        if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int*>(out) + s, __float_as_int(v));
+    block_absmax_flush<NS>(m, out);
+}
+
+// Binary logistic GBT, one fused pass per tree (models/trees.py GradientTreeBoostingClassifier):
+// p = sigmoid(F[r]), residual R = y - p, hessian |R| (1 - |R|), count 1, all times the row's
+// subsample mask (NULL = every row), written as stats[r] = {R, H, c}, plus the columns' |max|
+// for the histogram's fixed-point scale (smax zeroed by the caller).  Replaces ~8 tensor passes
+// over n rows (sigmoid, sub, abs, stack, mask multiply, absmax).
+__global__ __launch_bounds__(256) void gbt_stats_kernel(const float* __restrict__ F, const float* __restrict__ y,
+                                                        const uint8_t* __restrict__ mask, int64_t n,
+                                                        float* __restrict__ stats, float* __restrict__ smax) {
+    float m[3] = {0.f, 0.f, 0.f};
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const float p = 1.f / (1.f + __expf(-F[r]));
+        const float w = (mask == nullptr || mask[r]) ? 1.f : 0.f;
+        const float R = y[r] - p;
+        const float aR = fabsf(R);
+        const float st0 = R * w, st1 = aR * (1.f - aR) * w;
+        stats[r * 3 + 0] = st0;
+        stats[r * 3 + 1] = st1;
+        stats[r * 3 + 2] = w;
+        m[0] = fmaxf(m[0], fabsf(st0));
+        m[1] = fmaxf(m[1], st1);
+        m[2] = fmaxf(m[2], w);
+    }
+    block_absmax_flush<3>(m, smax);
+}
+
+// F[r * ldf + k] += scale * vals[leaf[r] * ldv] for every routed row (leaf >= 0).
+__global__ __launch_bounds__(256) void gbt_apply_kernel(float* __restrict__ F, int ldf, int k,
+                                                        const float* __restrict__ vals, int ldv,
+                                                        const int32_t* __restrict__ leaf, int64_t n, float scale) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const int l = leaf[r];
+        if (l >= 0) F[r * ldf + k] += scale * vals[(int64_t)l * ldv];
     }
 }
 
@@ -753,7 +805,7 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
 HM_API int hm_absmax_cols(const float* stats, int64_t n, int NS, float* out, hipStream_t stream) {
     if (n <= 0) return 0;
     int64_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 1024) blocks = 1024;
 #define HM_A(K) \
     case K: hipLaunchKernelGGL((absmax_kernel<K>), dim3((int)blocks), dim3(256), 0, stream, stats, n, out); break;
     switch (NS) {
@@ -865,5 +917,27 @@ HM_API int hm_hist_sibling(const float* H, const float* Hs, const int64_t* li, c
     if (bx > 64) bx = 64;
     hipLaunchKernelGGL(hist_sibling_kernel, dim3((unsigned)bx, (unsigned)n_split), dim3(256), 0, stream,
                        H, Hs, li, small_right, per, n_split, Hn);
+    HM_LAUNCH_RET();
+}
+
+// Fused binary-logistic GBT statistics (see gbt_stats_kernel): F, y [n] fp32, mask [n] uint8
+// or NULL; stats [n, 3] fp32 out; smax [3] zeroed by the caller.
+HM_API int hm_gbt_stats(const float* F, const float* y, const uint8_t* mask, int64_t n, float* stats,
+                        float* smax, hipStream_t stream) {
+    if (n <= 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(gbt_stats_kernel, dim3((int)blocks), dim3(256), 0, stream, F, y, mask, n, stats, smax);
+    HM_LAUNCH_RET();
+}
+
+// F[r * ldf + k] += scale * vals[leaf[r] * ldv] for leaf[r] >= 0.
+HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, const int32_t* leaf, int64_t n,
+                        float scale, hipStream_t stream) {
+    if (n <= 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(gbt_apply_kernel, dim3((int)blocks), dim3(256), 0, stream, F, ldf, k, vals, ldv, leaf, n,
+                       scale);
     HM_LAUNCH_RET();
 }

@@ -396,24 +396,29 @@ class HistTreeBuilder:
             self.mixer.all_reduce_sum([hist])
         return hist
 
-    def build(self, stats: torch.Tensor, active: torch.Tensor | None = None) -> Tree:
+    def build(self, stats: torch.Tensor, active: torch.Tensor | None = None, smax: torch.Tensor | None = None,
+              act_rows: torch.Tensor | None = None) -> Tree:
         """Grow one tree level by level.  stats: f32 [n, NS] per-row statistics.
 
         Every level: split search on the device over the level's histograms; one host sync
         (the number of splits); rows routed by the bins; the next level histograms only the
         smaller child of each split (sibling = parent - child).  After the call
-        ``self.leaf_of_row`` holds the leaf node id of every row (-1: inactive)."""
+        ``self.leaf_of_row`` holds the leaf node id of every row (-1: inactive).  ``smax`` (the
+        columns' |max|) and ``act_rows`` (int32 ids of the rows with non-zero stats) may be
+        passed in when the caller already has them (the fused GBT statistics kernel)."""
         q = self.q
         dev = stats.device
         n, NS = stats.shape
         d, B = q.d, q.B
         stats = stats.contiguous()
         node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
-        act = (stats != 0).any(1)
         if active is not None:
             node_of_row[~active] = -1
-            act &= active
-        act_rows = torch.nonzero(act).flatten().to(torch.int32)
+        if act_rows is None:
+            act = (stats != 0).any(1)
+            if active is not None:
+                act &= active
+            act_rows = torch.nonzero(act).flatten().to(torch.int32)
         edges = q.edges.to(dev)
         cat_dev = None if self.cat is None else self.cat.to(dev)
         n_out = NS if self.criterion in ("gini", "entropy") else 1
@@ -421,7 +426,9 @@ class HistTreeBuilder:
         # level 0: the root histogram over every active row
         seg = torch.stack([torch.zeros((), dtype=torch.int64, device=dev),
                            torch.full((), act_rows.numel(), dtype=torch.int64, device=dev)])
-        if dev.type == "cuda" and NS <= 8:                # fixed-point range of the LDS sums
+        if smax is not None:
+            smax = smax.contiguous()
+        elif dev.type == "cuda" and NS <= 8:              # fixed-point range of the LDS sums
             smax = torch.zeros(NS, dtype=torch.float32, device=dev)
             _native.check(_native.hip().hm_absmax_cols(_native.ptr(stats), C.c_int64(n), NS, _native.ptr(smax),
                                                         _native.stream_of(dev)), "hm_absmax_cols")
@@ -767,7 +774,43 @@ class GradientTreeBoostingClassifier(Learner):
             F = torch.zeros((n, K), device=self.device)
             Y = torch.nn.functional.one_hot(yi, K).float()
         m_sub = max(1, int(round(n * float(c["subsample"]))))
+        fused = self.device.type == "cuda" and K == 2
+        if fused:
+            # binary logistic on the GPU: one fused statistics pass and one fused leaf update per
+            # tree instead of ~12 tensor passes over the n rows (profiles/gbt_r2/)
+            y1 = Y[:, 0].contiguous()
+            stats_buf = torch.empty((n, 3), dtype=torch.float32, device=self.device)
+            smax = torch.zeros(3, dtype=torch.float32, device=self.device)
+            all_rows = torch.arange(n, dtype=torch.int32, device=self.device)
+            st = _native.stream_of(self.device)
         for it in range(int(c["trees"])):
+            if fused:
+                mask = None
+                if m_sub < n:
+                    sel = torch.randperm(n, generator=g, device=self.device)[:m_sub]
+                    mask = torch.zeros(n, dtype=torch.bool, device=self.device)
+                    mask[sel] = True
+                smax.zero_()
+                _native.check(_native.hip().hm_gbt_stats(
+                    _native.ptr(F), _native.ptr(y1), _native.ptr(mask), C.c_int64(n), _native.ptr(stats_buf),
+                    _native.ptr(smax), st), "hm_gbt_stats")
+                b = HistTreeBuilder(q, "gbt", int(c["max_depth"]), c["min_split"], c["min_samples_leaf"],
+                                    c["mtry"], c["max_leaf_nodes"], seed=self.seed * 7919 + it * K,
+                                    mixer=self.mixer, lam=float(c["lambda"]))
+                tree = b.build(stats_buf, smax=smax, act_rows=all_rows if mask is None else None)
+                self.importance += b.importance
+                vals = b.node_values.float().contiguous()
+                _native.check(_native.hip().hm_gbt_apply(
+                    _native.ptr(F), F.shape[1], 0, _native.ptr(vals), vals.shape[1], _native.ptr(b.leaf_of_row),
+                    C.c_int64(n), C.c_float(eta), st), "hm_gbt_apply")
+                self.iters.append([tree])
+                if mask is None:
+                    self.oob_rates.append(0.0)
+                else:
+                    oob = ~mask
+                    pred = (F[oob, 0] > 0).long()
+                    self.oob_rates.append(float((pred != yi[oob]).float().mean().item()))
+                continue
             P = torch.sigmoid(F) if K == 2 else torch.softmax(F, 1)
             R = Y - P
             H = (R.abs() * (1 - R.abs())) if K == 2 else P * (1 - P)
@@ -985,3 +1028,5 @@ _native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, 
 _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
                                               _P, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
+_native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
+_native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, _P])

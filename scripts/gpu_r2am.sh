@@ -1,0 +1,11 @@
+#!/bin/bash
+# GBDT kernel breakdown (rocprofv3 kernel stats) + wall time per tree
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export HM_NO_AUTOBUILD=1 PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
+timeout -k 10 200 python -u benchmarks/probes/gbt_prof_target.py 20 > gpurun_out/gbt_wall_r2am.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gbt -o run -- \
+  python3 benchmarks/probes/gbt_prof_target.py 20 > gpurun_out/prof_gbt.log 2>&1
+echo done

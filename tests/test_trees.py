@@ -108,6 +108,21 @@ def test_hist_kernel_matches_cpu(higgs):
 
 
 @pytest.mark.gpu
+def test_gbt_gpu_fused_path_subsample_matches_cpu_quality(higgs):
+    """Binary GBT on the GPU runs the fused statistics / leaf-update kernels (hm_gbt_stats /
+    hm_gbt_apply); with row subsampling the masked rows must drop out of the histograms and
+    still get their leaf update.  Quality equals the CPU engine's (same rule, its own sampling)."""
+    X, y, Xt, yt = higgs
+    auc = {}
+    for dev in ("cpu", "cuda"):
+        gb = GradientTreeBoostingClassifier("-trees 20 -eta 0.1 -max_depth 5 -subsample 0.7 -seed 3",
+                                            device=dev).fit(X, y)
+        auc[dev] = roc_auc_score(yt.numpy(), gb.predict_proba(Xt)[:, 1])
+        assert len(gb.oob_rates) == 20 and 0.0 < gb.oob_rates[-1] < 0.5
+    assert abs(auc["cpu"] - auc["cuda"]) < 0.01, auc
+
+
+@pytest.mark.gpu
 def test_rf_gpu_quality(higgs):
     X, y, Xt, yt = higgs
     aucs = {}
