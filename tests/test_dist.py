@@ -1,5 +1,6 @@
 """Multi-process (gloo, world_size=2) tests of the RCCL mixing layer — the MixServerTest
 analogue: N learners, one mixed model."""
+import io
 import json
 import os
 import socket
@@ -22,6 +23,32 @@ def _free_port():
     return p
 
 
+class _TensorBytes(bytes):
+    """A tensor serialised by value (torch.save) inside a queued result."""
+
+
+def _pack(x):
+    if torch.is_tensor(x):
+        buf = io.BytesIO()
+        torch.save(x.detach().cpu().clone(), buf)
+        return _TensorBytes(buf.getvalue())
+    if isinstance(x, dict):
+        return {k: _pack(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_pack(v) for v in x)
+    return x
+
+
+def _unpack(x):
+    if isinstance(x, _TensorBytes):
+        return torch.load(io.BytesIO(bytes(x)), weights_only=True)
+    if isinstance(x, dict):
+        return {k: _unpack(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_unpack(v) for v in x)
+    return x
+
+
 def _worker(rank, world, port, fn_name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -38,7 +65,9 @@ def _worker(rank, world, port, fn_name, q):
             f = getattr(importlib.import_module(mod), fn)
         else:
             f = getattr(T, fn_name)
-        q.put((rank, f(ctx)))
+        # results travel by value: a tensor put on an mp queue is shared through a file
+        # descriptor that dies with this process, racing the parent's get (FileNotFoundError)
+        q.put((rank, _pack(f(ctx))))
     finally:
         D.shutdown()
 
@@ -50,7 +79,7 @@ def run_world(fn_name, world=2):
     ps = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
     for p in ps:
         p.start()
-    out = dict(q.get(timeout=120) for _ in ps)
+    out = {r: _unpack(b) for r, b in (q.get(timeout=120) for _ in ps)}
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
