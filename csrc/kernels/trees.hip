@@ -941,3 +941,127 @@ HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, co
                        scale);
     HM_LAUNCH_RET();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Level finalisation (one launch per level instead of ~40 tensor ops; models/trees.py build):
+// from the split search's per-node results decide which nodes split, number their children,
+// and lay out everything the next level needs — leaf values, node records (flagged feature,
+// threshold, children), the compacted list of splitting nodes, which child is the smaller
+// (histogrammed) one, the partition LUT and the split count (the level's one host read).
+// One 1024-thread block; thread t owns a contiguous chunk of the L nodes, so children are
+// numbered in node order (an exclusive block scan of the per-thread counts), as the
+// cumsum-based host path does.
+struct LevelParams {
+    int L, NS, d, E, crit, n_out, nb, has_cat;
+    float lam, alpha, min_gain, min_split;
+};
+
+__device__ __forceinline__ float node_weight(const float* S, int NS, int crit) {
+    if (crit <= 1) {                         // gini / entropy: sum of class counts
+        float w = 0.f;
+        for (int s = 0; s < NS; ++s) w += S[s];
+        return w;
+    }
+    if (crit == 2 || crit == 4) return S[1];  // variance / xgb
+    return S[2];                              // gbt: count
+}
+
+__global__ __launch_bounds__(1024) void level_finalize_kernel(
+    LevelParams P, const float* __restrict__ gain, const int32_t* __restrict__ feat,
+    const int32_t* __restrict__ bins_raw, const float* __restrict__ left, const float* __restrict__ tot,
+    const float* __restrict__ edges, const uint8_t* __restrict__ cat, float* __restrict__ vals,
+    int32_t* __restrict__ feats_out, float* __restrict__ thrs_out, int32_t* __restrict__ lc_out,
+    int32_t* __restrict__ rc_out, int32_t* __restrict__ sb_out, int32_t* __restrict__ li_out,
+    uint8_t* __restrict__ small_right, int16_t* __restrict__ lut, int32_t* __restrict__ n_split) {
+    __shared__ int s_cnt[1024];
+    const int t = threadIdx.x;
+    const int chunk = (P.L + 1023) / 1024;
+    const int l0 = min(P.L, t * chunk), l1 = min(P.L, l0 + chunk);
+    const float gmin = fmaxf(1e-12f, P.min_gain);
+    auto is_ok = [&](int l) {
+        const float g = gain[l];
+        return g > gmin && isfinite(g) && node_weight(tot + (size_t)l * P.NS, P.NS, P.crit) >= P.min_split;
+    };
+    int cnt = 0;
+    for (int l = l0; l < l1; ++l) cnt += is_ok(l) ? 1 : 0;
+    s_cnt[t] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {      // inclusive Hillis-Steele scan
+        const int v = t >= o ? s_cnt[t - o] : 0;
+        __syncthreads();
+        s_cnt[t] += v;
+        __syncthreads();
+    }
+    int rank = s_cnt[t] - cnt;                 // exclusive prefix
+    if (t == 1023) n_split[0] = s_cnt[1023];
+    for (int l = l0; l < l1; ++l) {
+        const float* S = tot + (size_t)l * P.NS;
+        // leaf value(s) of the node
+        float* v = vals + (size_t)l * P.n_out;
+        if (P.crit <= 1) {
+            const float w = node_weight(S, P.NS, P.crit);
+            for (int s = 0; s < P.NS; ++s) v[s] = w > 0.f ? S[s] / fmaxf(w, 1e-30f) : 1.f / (float)P.NS;
+        } else if (P.crit == 2) {
+            v[0] = S[1] > 0.f ? S[0] / fmaxf(S[1], 1e-30f) : 0.f;
+        } else if (P.crit == 4) {
+            const float den = S[1] + P.lam;
+            v[0] = den > 0.f ? -soft_thr(S[0], P.alpha) / fmaxf(den, 1e-30f) : 0.f;
+        } else {
+            v[0] = fabsf(S[1]) > 1e-12f ? S[0] / S[1] : 0.f;
+        }
+        const int bf = feat[l];
+        const int br = bins_raw[l];
+        const int bb = br & 0xFFFF;
+        sb_out[l] = bb;
+        if (!is_ok(l)) {
+            feats_out[l] = -1;
+            thrs_out[l] = INFINITY;
+            lc_out[l] = -1;
+            rc_out[l] = -1;
+            continue;
+        }
+        const bool fok = bf >= 0 && bf < P.d;
+        int flag = bf;
+        if (P.has_cat && fok && cat[bf]) flag |= HM_TREE_CAT;
+        if ((br >> 16) & 1) flag |= HM_TREE_DLEFT;
+        feats_out[l] = flag;
+        thrs_out[l] = (fok && bb < P.E) ? edges[(size_t)bf * P.E + bb] : INFINITY;
+        const int lc = P.nb + 2 * rank;
+        lc_out[l] = lc;
+        rc_out[l] = lc + 1;
+        li_out[rank] = l;
+        const float* Lf = left + (size_t)l * P.NS;
+        float rgt[8];
+        float wl, wr;
+        if (P.NS <= 8) {
+            for (int s = 0; s < P.NS; ++s) rgt[s] = S[s] - Lf[s];
+            wl = node_weight(Lf, P.NS, P.crit);
+            wr = node_weight(rgt, P.NS, P.crit);
+        } else {                               // many classes: weights are sums of counts
+            wl = 0.f; wr = 0.f;
+            for (int s = 0; s < P.NS; ++s) { wl += Lf[s]; wr += S[s] - Lf[s]; }
+        }
+        const int sr = wr < wl ? 1 : 0;
+        small_right[rank] = (uint8_t)sr;
+        lut[2 * rank + sr] = (int16_t)rank;
+        lut[2 * rank + 1 - sr] = (int16_t)32767;
+        ++rank;
+    }
+}
+
+// ip: L, NS, d, E, crit, n_out, nb, has_cat;  fp: lam, alpha, min_gain, min_split
+HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* gain, const int32_t* feat,
+                             const int32_t* bins_raw, const float* left, const float* tot, const float* edges,
+                             const uint8_t* cat, float* vals, int32_t* feats_out, float* thrs_out, int32_t* lc_out,
+                             int32_t* rc_out, int32_t* sb_out, int32_t* li_out, uint8_t* small_right, int16_t* lut,
+                             int32_t* n_split, hipStream_t stream) {
+    LevelParams P;
+    P.L = ip[0]; P.NS = ip[1]; P.d = ip[2]; P.E = ip[3]; P.crit = ip[4]; P.n_out = ip[5]; P.nb = ip[6];
+    P.has_cat = ip[7];
+    P.lam = fp[0]; P.alpha = fp[1]; P.min_gain = fp[2]; P.min_split = fp[3];
+    if (P.L <= 0 || P.NS <= 0 || (P.crit > 1 && P.NS > 8) || P.E <= 0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream, P, gain, feat, bins_raw, left, tot,
+                       edges, cat, vals, feats_out, thrs_out, lc_out, rc_out, sb_out, li_out, small_right, lut,
+                       n_split);
+    HM_LAUNCH_RET();
+}

@@ -316,7 +316,13 @@ class HistTreeBuilder:
     def _split_find(self, H: torch.Tensor, node_base: int):
         """Best split of every node of the level (csrc hm_split_find: one fused kernel instead
         of ~30 tensor ops over [L, d, B, NS]).  Returns gain [L] (-inf: no valid split), feature
-        and bin (int32), left-child statistics [L, NS] and node totals [L, NS]."""
+        and bin (int32), left-child statistics [L, NS], node totals [L, NS] and the learned
+        missing-value direction."""
+        gain, feat, bins, left, tot = self._split_find_raw(H, node_base)
+        dleft = (bins >> 16) & 1                  # bit 16: the missing rows go left
+        return gain, feat, bins & 0xFFFF, left, tot, dleft
+
+    def _split_find_raw(self, H: torch.Tensor, node_base: int):
         L, d, B, NS = H.shape
         dev = H.device
         H = H.contiguous()
@@ -342,8 +348,31 @@ class HistTreeBuilder:
         else:
             if _native.host().hm_split_find_cpu(*args) != 0:
                 raise RuntimeError("hm_split_find_cpu: invalid arguments")
-        dleft = (bins >> 16) & 1                  # bit 16: the missing rows go left
-        return gain, feat, bins & 0xFFFF, left, tot, dleft
+        return gain, feat, bins, left, tot
+
+    def _level_finalize(self, gain, feat, braw, left, tot, nb: int, edges, n_out: int):
+        """GPU: the level's split decisions and bookkeeping in one kernel (hm_level_finalize);
+        returns (vals, feats, thrs, lc, rc, sb, li, small_right, lut, n_split)."""
+        L, NS = tot.shape
+        dev = tot.device
+        vals = torch.empty((L, n_out), dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        feats, lc, rc, sb, li = (torch.empty(L, **i32) for _ in range(5))
+        thrs = torch.empty(L, dtype=torch.float32, device=dev)
+        sr = torch.empty(L, dtype=torch.uint8, device=dev)
+        lut = torch.empty(2 * L, dtype=torch.int16, device=dev)
+        nsp = torch.empty(1, **i32)
+        cat = self._masks[1]
+        ip = np.array([L, NS, self.q.d, edges.shape[1], self._CRIT[self.criterion], n_out, nb,
+                       int(cat is not None)], dtype=np.int32)
+        fp = np.array([self.lam, self.alpha, self.min_gain, float(self.min_split)], dtype=np.float32)
+        p = _native.ptr
+        _native.check(_native.hip().hm_level_finalize(
+            ip.ctypes.data, fp.ctypes.data, p(gain), p(feat), p(braw), p(left.contiguous()), p(tot.contiguous()),
+            p(edges), p(cat), p(vals), p(feats), p(thrs), p(lc), p(rc), p(sb), p(li), p(sr), p(lut), p(nsp),
+            _native.stream_of(dev)), "hm_level_finalize")
+        n_split = int(nsp.item())                                            # the level's one sync
+        return vals, feats, thrs, lc, rc, sb, li[:n_split], sr[:n_split], lut[:2 * n_split], n_split
 
     @staticmethod
     def _partition_gpu(act_rows, node_of_row, nb: int, lut, n_keys: int):
@@ -419,8 +448,9 @@ class HistTreeBuilder:
             if active is not None:
                 act &= active
             act_rows = torch.nonzero(act).flatten().to(torch.int32)
-        edges = q.edges.to(dev)
+        edges = q.edges.to(device=dev, dtype=torch.float32).contiguous()
         cat_dev = None if self.cat is None else self.cat.to(dev)
+        fused = dev.type == "cuda" and self.max_leaves is None and (NS <= 8 or self.criterion in ("gini", "entropy"))
         n_out = NS if self.criterion in ("gini", "entropy") else 1
         imp = torch.zeros(d, dtype=torch.float64, device=dev)
         # level 0: the root histogram over every active row
@@ -449,6 +479,46 @@ class HistTreeBuilder:
                 lefts.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 rights.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 break
+            if fused:
+                gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
+                nb = base + L
+                (v_l, f_l, t_l, lc, rc, sb_l, li, small_right, lut, n_split) = self._level_finalize(
+                    gain, bf, braw, left_all, tot, nb, edges, n_out)
+                vals.append(v_l)
+                feats.append(f_l)
+                thrs.append(t_l)
+                lefts.append(lc)
+                rights.append(rc)
+                if n_split == 0:
+                    break
+                li = li.long()                      # hm_hist_sibling takes int64 node ids
+                imp.index_add_(0, bf[li].long(), gain[li].double())
+                sf_all = torch.cat([sf_all, f_l])
+                sb_all = torch.cat([sb_all, sb_l])
+                lc_all = torch.cat([lc_all, lc])
+                rc_all = torch.cat([rc_all, rc])
+                p = _native.ptr
+                _native.check(_native.hip().hm_route_rows(
+                    p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all),
+                    (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
+                if n_split <= 8192:
+                    rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, n_split)
+                else:
+                    nr = node_of_row[act_rows.long()] - nb
+                    key = torch.where(nr >= 0, lut[nr.clamp_min(0).long()],
+                                      torch.full_like(nr, 32767, dtype=torch.int16))
+                    skey, order = torch.sort(key, stable=True)
+                    rows = act_rows[order].contiguous()
+                    seg = torch.searchsorted(skey, torch.arange(n_split + 1, device=dev, dtype=torch.int16)).to(torch.int64)
+                Hs = self._hist(rows, seg.contiguous(), n_split, stats, smax)
+                Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
+                _native.check(_native.hip().hm_hist_sibling(
+                    _native.ptr(H), _native.ptr(Hs), _native.ptr(li), _native.ptr(small_right), C.c_int64(d * B * NS),
+                    n_split, _native.ptr(Hn), _native.stream_of(dev)), "hm_hist_sibling")
+                H = Hn
+                base, L = nb, 2 * n_split
+                depth += 1
+                continue
             best_gain, bf, bb, left_all, tot, bdl = self._split_find(H, base)
             vals.append(self._leaf_values(tot))
             ok = (best_gain > max(1e-12, self.min_gain)) & torch.isfinite(best_gain) & \
@@ -1029,4 +1099,5 @@ _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int
                                               _P, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
+_native.register_hip("hm_level_finalize", [_P] * 20)
 _native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, _P])
