@@ -200,19 +200,24 @@ __global__ __launch_bounds__(256) void fmd_mfma_kernel(const float* __restrict__
     const int NBS = (KP + 1) >> 4, CS = (KP + 1) & 15;   // block / column of the -vsq/2 column
 
     // B1 operands (constant over the step): lane holds B1[k = q + 4t][c = 16 nb + c16]
+    // |V_k|^2 from the operands themselves: the 16 lanes of group q hold row k's columns
     float bV[NB][KT], bS[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
         const int k = q + 4 * t;
         float vsq = 0.f;
-        if (k < d)
-            for (int c = 0; c < KP; ++c) vsq += V[k * KP + c] * V[k * KP + c];
-        bS[t] = (k < d && c16 == CS) ? -0.5f * vsq : 0.f;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
             const int c = 16 * nb + c16;
-            bV[nb][t] = k < d ? (c < KP ? V[k * KP + c] : (c == KP ? w[k] : 0.f)) : 0.f;
+            const float v = k < d ? (c < KP ? V[k * KP + c] : (c == KP ? w[k] : 0.f)) : 0.f;
+            bV[nb][t] = v;
+            if (c < KP) vsq += v * v;
         }
+        vsq += __shfl_xor(vsq, 1);
+        vsq += __shfl_xor(vsq, 2);
+        vsq += __shfl_xor(vsq, 4);
+        vsq += __shfl_xor(vsq, 8);
+        bS[t] = (k < d && c16 == CS) ? -0.5f * vsq : 0.f;
     }
     const float w0v = w0[0];
     fmd_f4 acc[MB][NB];
