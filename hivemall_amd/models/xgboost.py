@@ -24,10 +24,13 @@ import json
 import math
 import zlib
 
+import ctypes as C
+
 import numpy as np
 import pandas as pd
 import torch
 
+from .. import _native
 from ..registry import udtf
 from ..utils import base91
 from ..utils.options import UDFArgumentException, opt
@@ -158,7 +161,13 @@ class XGBoostTrainer(Learner):
                                     min_gain=2.0 * float(c["gamma"]), feature_mask=fmask)
                 tree = b.build(stats)
                 tree.value = [None if v is None else [eta * v[0]] for v in tree.value]
-                F[:, k] += eta * b.node_values[b.leaf_of_row.long(), 0]
+                if F.is_cuda:   # fused leaf update (trees.hip gbt_apply_kernel)
+                    vals = b.node_values.float().contiguous()
+                    _native.check(_native.hip().hm_gbt_apply(
+                        _native.ptr(F), F.shape[1], k, _native.ptr(vals), vals.shape[1], _native.ptr(b.leaf_of_row),
+                        C.c_int64(n), C.c_float(eta), _native.stream_of(F.device)), "hm_gbt_apply")
+                else:
+                    F[:, k] += eta * b.node_values[b.leaf_of_row.long(), 0]
                 self.importance += b.importance
                 round_trees.append(tree)
             self.trees.append(round_trees)
