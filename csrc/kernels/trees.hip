@@ -971,8 +971,9 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
     const int32_t* __restrict__ bins_raw, const float* __restrict__ left, const float* __restrict__ tot,
     const float* __restrict__ edges, const uint8_t* __restrict__ cat, float* __restrict__ vals,
     int32_t* __restrict__ feats_out, float* __restrict__ thrs_out, int32_t* __restrict__ lc_out,
-    int32_t* __restrict__ rc_out, int32_t* __restrict__ sb_out, int32_t* __restrict__ li_out,
-    uint8_t* __restrict__ small_right, int16_t* __restrict__ lut, int32_t* __restrict__ n_split) {
+    int32_t* __restrict__ rc_out, int32_t* __restrict__ sb_out, int64_t* __restrict__ li_out,
+    uint8_t* __restrict__ small_right, int16_t* __restrict__ lut, int32_t* __restrict__ n_split,
+    double* __restrict__ imp) {
     __shared__ int s_cnt[1024];
     const int t = threadIdx.x;
     const int chunk = (P.L + 1023) / 1024;
@@ -1030,6 +1031,7 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
         lc_out[l] = lc;
         rc_out[l] = lc + 1;
         li_out[rank] = l;
+        if (fok) atomicAdd(imp + bf, (double)gain[l]);   // split-gain importance
         const float* Lf = left + (size_t)l * P.NS;
         float rgt[8];
         float wl, wr;
@@ -1049,12 +1051,14 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
     }
 }
 
-// ip: L, NS, d, E, crit, n_out, nb, has_cat;  fp: lam, alpha, min_gain, min_split
+// ip: L, NS, d, E, crit, n_out, nb, has_cat;  fp: lam, alpha, min_gain, min_split.  The per-node
+// outputs (vals .. sb_out) are written at [0, L) of the pointers given (the caller offsets them to
+// the level's first node id); li_out / small_right / lut are per split; imp [d] += split gains.
 HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* gain, const int32_t* feat,
                              const int32_t* bins_raw, const float* left, const float* tot, const float* edges,
                              const uint8_t* cat, float* vals, int32_t* feats_out, float* thrs_out, int32_t* lc_out,
-                             int32_t* rc_out, int32_t* sb_out, int32_t* li_out, uint8_t* small_right, int16_t* lut,
-                             int32_t* n_split, hipStream_t stream) {
+                             int32_t* rc_out, int32_t* sb_out, int64_t* li_out, uint8_t* small_right, int16_t* lut,
+                             int32_t* n_split, double* imp, hipStream_t stream) {
     LevelParams P;
     P.L = ip[0]; P.NS = ip[1]; P.d = ip[2]; P.E = ip[3]; P.crit = ip[4]; P.n_out = ip[5]; P.nb = ip[6];
     P.has_cat = ip[7];
@@ -1062,6 +1066,6 @@ HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* ga
     if (P.L <= 0 || P.NS <= 0 || (P.crit > 1 && P.NS > 8) || P.E <= 0) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream, P, gain, feat, bins_raw, left, tot,
                        edges, cat, vals, feats_out, thrs_out, lc_out, rc_out, sb_out, li_out, small_right, lut,
-                       n_split);
+                       n_split, imp);
     HM_LAUNCH_RET();
 }

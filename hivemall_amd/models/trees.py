@@ -229,6 +229,32 @@ def predict_forest(trees: list[Tree], X: torch.Tensor, sum_trees: bool = True,
     return out
 
 
+class _NodeBuf:
+    """Growable device arrays of one tree's nodes (GPU builder): flagged split feature, split
+    bin, children, threshold and leaf values, indexed by node id.  The routing kernel reads them
+    as they stand, so no per-level concatenation is needed."""
+
+    def __init__(self, cap: int, n_out: int, dev):
+        self.n_out, self.dev, self.cap = n_out, dev, 0
+        self.sf = self.sb = self.lc = self.rc = self.thr = self.vals = None
+        self.ensure(cap)
+
+    def ensure(self, need: int) -> None:
+        if need <= self.cap:
+            return
+        cap = max(need, 2 * self.cap)
+        i32 = dict(dtype=torch.int32, device=self.dev)
+        new = dict(sf=torch.empty(cap, **i32), sb=torch.empty(cap, **i32), lc=torch.empty(cap, **i32),
+                   rc=torch.empty(cap, **i32), thr=torch.empty(cap, dtype=torch.float32, device=self.dev),
+                   vals=torch.empty((cap, self.n_out), dtype=torch.float32, device=self.dev))
+        for k, t in new.items():
+            old = getattr(self, k)
+            if old is not None:
+                t[:self.cap] = old
+            setattr(self, k, t)
+        self.cap = cap
+
+
 class HistTreeBuilder:
     """Level-wise histogram tree growth on the device."""
 
@@ -350,29 +376,30 @@ class HistTreeBuilder:
                 raise RuntimeError("hm_split_find_cpu: invalid arguments")
         return gain, feat, bins, left, tot
 
-    def _level_finalize(self, gain, feat, braw, left, tot, nb: int, edges, n_out: int):
-        """GPU: the level's split decisions and bookkeeping in one kernel (hm_level_finalize);
-        returns (vals, feats, thrs, lc, rc, sb, li, small_right, lut, n_split)."""
+    def _level_finalize(self, gain, feat, braw, left, tot, base: int, nb: int, edges, buf: "_NodeBuf", imp):
+        """GPU: the level's split decisions and bookkeeping in one kernel (hm_level_finalize),
+        written straight into the tree's node arrays at [base, base + L); returns
+        (li int64, small_right, lut, n_split) of the splitting nodes."""
         L, NS = tot.shape
         dev = tot.device
-        vals = torch.empty((L, n_out), dtype=torch.float32, device=dev)
-        i32 = dict(dtype=torch.int32, device=dev)
-        feats, lc, rc, sb, li = (torch.empty(L, **i32) for _ in range(5))
-        thrs = torch.empty(L, dtype=torch.float32, device=dev)
+        buf.ensure(base + L)
+        li = torch.empty(L, dtype=torch.int64, device=dev)
         sr = torch.empty(L, dtype=torch.uint8, device=dev)
         lut = torch.empty(2 * L, dtype=torch.int16, device=dev)
-        nsp = torch.empty(1, **i32)
+        nsp = torch.empty(1, dtype=torch.int32, device=dev)
         cat = self._masks[1]
-        ip = np.array([L, NS, self.q.d, edges.shape[1], self._CRIT[self.criterion], n_out, nb,
+        ip = np.array([L, NS, self.q.d, edges.shape[1], self._CRIT[self.criterion], buf.n_out, nb,
                        int(cat is not None)], dtype=np.int32)
         fp = np.array([self.lam, self.alpha, self.min_gain, float(self.min_split)], dtype=np.float32)
         p = _native.ptr
+        o4, ov = 4 * base, 4 * base * buf.n_out          # byte offsets of node `base`
         _native.check(_native.hip().hm_level_finalize(
             ip.ctypes.data, fp.ctypes.data, p(gain), p(feat), p(braw), p(left.contiguous()), p(tot.contiguous()),
-            p(edges), p(cat), p(vals), p(feats), p(thrs), p(lc), p(rc), p(sb), p(li), p(sr), p(lut), p(nsp),
+            p(edges), p(cat), p(buf.vals) + ov, p(buf.sf) + o4, p(buf.thr) + o4, p(buf.lc) + o4,
+            p(buf.rc) + o4, p(buf.sb) + o4, p(li), p(sr), p(lut), p(nsp), p(imp),
             _native.stream_of(dev)), "hm_level_finalize")
         n_split = int(nsp.item())                                            # the level's one sync
-        return vals, feats, thrs, lc, rc, sb, li[:n_split], sr[:n_split], lut[:2 * n_split], n_split
+        return li[:n_split], sr[:n_split], lut[:2 * n_split], n_split
 
     @staticmethod
     def _partition_gpu(act_rows, node_of_row, nb: int, lut, n_keys: int):
@@ -451,6 +478,8 @@ class HistTreeBuilder:
         edges = q.edges.to(device=dev, dtype=torch.float32).contiguous()
         cat_dev = None if self.cat is None else self.cat.to(dev)
         fused = dev.type == "cuda" and self.max_leaves is None and (NS <= 8 or self.criterion in ("gini", "entropy"))
+        n_out_ = NS if self.criterion in ("gini", "entropy") else 1
+        nbuf = _NodeBuf(min(1 << 13, 2 << min(self.max_depth, 30)), n_out_, dev) if fused else None
         n_out = NS if self.criterion in ("gini", "entropy") else 1
         imp = torch.zeros(d, dtype=torch.float64, device=dev)
         # level 0: the root histogram over every active row
@@ -472,6 +501,14 @@ class HistTreeBuilder:
         sb_all, lc_all, rc_all = sf_all.clone(), sf_all.clone(), sf_all.clone()
         depth = 0
         while True:
+            if depth >= self.max_depth and fused:
+                nbuf.ensure(base + L)
+                nbuf.vals[base:base + L] = self._leaf_values(H[:, 0].sum(1))
+                nbuf.sf[base:base + L] = -1
+                nbuf.thr[base:base + L] = math.inf
+                nbuf.lc[base:base + L] = -1
+                nbuf.rc[base:base + L] = -1
+                break
             if depth >= self.max_depth:
                 vals.append(self._leaf_values(H[:, 0].sum(1)))
                 feats.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
@@ -482,24 +519,13 @@ class HistTreeBuilder:
             if fused:
                 gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
                 nb = base + L
-                (v_l, f_l, t_l, lc, rc, sb_l, li, small_right, lut, n_split) = self._level_finalize(
-                    gain, bf, braw, left_all, tot, nb, edges, n_out)
-                vals.append(v_l)
-                feats.append(f_l)
-                thrs.append(t_l)
-                lefts.append(lc)
-                rights.append(rc)
+                li, small_right, lut, n_split = self._level_finalize(gain, bf, braw, left_all, tot, base, nb,
+                                                                     edges, nbuf, imp)
                 if n_split == 0:
                     break
-                li = li.long()                      # hm_hist_sibling takes int64 node ids
-                imp.index_add_(0, bf[li].long(), gain[li].double())
-                sf_all = torch.cat([sf_all, f_l])
-                sb_all = torch.cat([sb_all, sb_l])
-                lc_all = torch.cat([lc_all, lc])
-                rc_all = torch.cat([rc_all, rc])
                 p = _native.ptr
                 _native.check(_native.hip().hm_route_rows(
-                    p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all),
+                    p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
                     (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
                 if n_split <= 8192:
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, n_split)
@@ -587,12 +613,19 @@ class HistTreeBuilder:
             depth += 1
         self.importance = self.importance + imp.cpu().numpy()
         self.leaf_of_row = node_of_row
-        F = torch.cat(feats).cpu().numpy()
-        T = torch.cat(thrs).cpu().numpy()
-        Lc = torch.cat(lefts).cpu().numpy()
-        Rc = torch.cat(rights).cpu().numpy()
-        V = torch.cat(vals).double().cpu().numpy()
-        self.node_values = torch.cat(vals)
+        if fused:
+            t = base + L                                   # nodes written, ids 0 .. t - 1
+            F, Lc, Rc = torch.stack([nbuf.sf[:t], nbuf.lc[:t], nbuf.rc[:t]]).cpu().numpy()
+            T = nbuf.thr[:t].cpu().numpy()
+            self.node_values = nbuf.vals[:t]
+            V = self.node_values.double().cpu().numpy()
+        else:
+            F = torch.cat(feats).cpu().numpy()
+            T = torch.cat(thrs).cpu().numpy()
+            Lc = torch.cat(lefts).cpu().numpy()
+            Rc = torch.cat(rights).cpu().numpy()
+            V = torch.cat(vals).double().cpu().numpy()
+            self.node_values = torch.cat(vals)
         tree = Tree(n_out=n_out)
         cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
         tree.cat = cflag if any(cflag) else []
@@ -704,6 +737,7 @@ class _ForestBase(Learner):
         T = int(c["trees"])
         my = [t for t in range(T) if t % world == rank]
         strat = yi if (self.TASK == "classification" and c["stratified"]) else None
+        pending = []
         for t in my:
             g.manual_seed(self.seed * 1000003 + t)   # tree t's bootstrap does not depend on the rank split
             w = bootstrap_weights(n, float(c["subsample"]), g, self.device, strat)
@@ -716,19 +750,24 @@ class _ForestBase(Learner):
             tree = b.build(stats)
             self.trees.append(tree)
             self.importances.append(b.importance)
-            # out-of-bag error from the leaf every row was routed to while growing
+            # out-of-bag error from the leaf every row was routed to while growing; kept on the
+            # device (full-size masked reductions, no boolean indexing) and read once after the
+            # last tree instead of two host syncs per tree
             oob = w == 0
-            no = int(oob.sum().item())
-            if no:
-                out = b.node_values[b.leaf_of_row[oob].long()]
-                if self.TASK == "classification":
-                    err = int((out.argmax(1) != yi[oob]).sum().item())
-                else:
-                    err = float(((out[:, 0] - yf[oob]) ** 2).sum().item())
+            leaf = b.leaf_of_row.long()
+            out = b.node_values[leaf.clamp_min(0)]
+            oob = oob & (leaf >= 0)
+            if self.TASK == "classification":
+                err = ((out.argmax(1) != yi) & oob).sum()
             else:
-                err = 0
-            self.oob_errors.append(err)
-            self.oob_tests.append(no)
+                err = torch.where(oob, (out[:, 0] - yf) ** 2, torch.zeros_like(yf)).double().sum()
+            pending.append((err, oob.sum()))
+        if pending:
+            errs = torch.stack([e.double() for e, _ in pending]).cpu().tolist()
+            nos = torch.stack([n for _, n in pending]).cpu().tolist()
+            for e, no in zip(errs, nos):
+                self.oob_errors.append(int(e) if self.TASK == "classification" else float(e))
+                self.oob_tests.append(int(no))
         return self
 
     def model_table(self) -> pd.DataFrame:
@@ -1099,5 +1138,5 @@ _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int
                                               _P, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
-_native.register_hip("hm_level_finalize", [_P] * 20)
+_native.register_hip("hm_level_finalize", [_P] * 21)
 _native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, _P])
