@@ -177,16 +177,39 @@ def bench_bprmf(dev="cuda", k=64, epochs=3, opts=""):
             "opts": opts, "grid": m._grid()}
 
 
+def bench_xgboost(dev="cuda", n=11_000_000, rounds=100):
+    """train_xgboost binary:logistic on HIGGS-shaped rows (second-order stats, learned NaN
+    directions), the xgboost4j replacement; quality against scikit-learn in test_xgboost."""
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.xgboost import XGBoostClassifier
+    X, y = higgs_like(n, device=dev)
+    Xt, yt = higgs_like(500000, seed=9, device=dev)
+    XGBoostClassifier("-num_round 2 -max_depth 6", device=dev).fit(X[:100000], y[:100000])
+    xg = XGBoostClassifier(f"-num_round {rounds} -max_depth 6 -eta 0.1", device=dev)
+    _sync(dev)
+    t0 = time.perf_counter()
+    xg.fit(X, y)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    auc = roc_auc_score(yt.cpu().numpy(), xg.predict_proba(Xt)[:, -1])
+    return {"config": f"train_xgboost binary:logistic, HIGGS-shaped {n} x 28, depth 6, {rounds} rounds",
+            "device": dev, "seconds": round(dt, 3), "ms_per_round": round(dt * 1e3 / rounds, 2),
+            "row_rounds_per_s": round(n * rounds / dt), "test_auc": round(float(auc), 4)}
+
+
 ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "linear_hashed": bench_linear_hashed,
        "fm": bench_fm,
-       "gbdt": bench_gbdt, "rf": bench_rf, "bprmf": bench_bprmf}
+       "gbdt": bench_gbdt, "rf": bench_rf, "bprmf": bench_bprmf, "xgboost": bench_xgboost}
 
 SMALL = {"linear_gpu": dict(n=20000), "linear_hashed": dict(n_rows=20000, bits=16), "fm": dict(n_rows=20000, bits=16),
-         "gbdt": dict(n=20000, trees=4), "rf": dict(n=20000, trees=2), "bprmf": dict(k=16, epochs=1)}
+         "gbdt": dict(n=20000, trees=4), "rf": dict(n=20000, trees=2), "bprmf": dict(k=16, epochs=1),
+         "xgboost": dict(n=20000, rounds=3)}
 
 # CPU reference-class points (8-core host): same code paths on the C++/OpenMP engines
 CPU = {"linear_gpu": dict(n=1_000_000), "linear_hashed": dict(n_rows=8 * 262144, bits=24),"fm": dict(n_rows=262144, bits=20),
-       "gbdt": dict(n=1_000_000, trees=10), "rf": dict(n=1_000_000, trees=4), "bprmf": dict(k=64, epochs=1)}
+       "gbdt": dict(n=1_000_000, trees=10), "rf": dict(n=1_000_000, trees=4), "bprmf": dict(k=64, epochs=1),
+       "xgboost": dict(n=1_000_000, rounds=10)}
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
