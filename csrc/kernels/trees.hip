@@ -197,30 +197,42 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ s
     block_absmax_flush<NS>(m, out);
 }
 
-// Binary logistic GBT, one fused pass per tree (models/trees.py GradientTreeBoostingClassifier):
-// p = sigmoid(F[r]), residual R = y - p, hessian |R| (1 - |R|), count 1, all times the row's
-// subsample mask (NULL = every row), written as stats[r] = {R, H, c}, plus the columns' |max|
-// for the histogram's fixed-point scale (smax zeroed by the caller).  Replaces ~8 tensor passes
-// over n rows (sigmoid, sub, abs, stack, mask multiply, absmax).
+// Binary logistic boosting, one fused pass per tree (models/trees.py GBT, models/xgboost.py):
+// p = sigmoid(F[r]) and, times the row's subsample mask (NULL = every row),
+//   XGB = 0: GBT   stats[r] = {R = y - p, |R| (1 - |R|), 1}            (NS = 3)
+//   XGB = 1: xgb   stats[r] = {g = p - y, max(p (1 - p), 1e-16)}       (NS = 2)
+// plus the columns' |max| for the histogram's fixed-point scale (smax zeroed by the caller).
+// Replaces ~8 tensor passes over n rows (sigmoid, sub, abs, clamp, stack, mask multiply, absmax).
+template <int XGB>
 __global__ __launch_bounds__(256) void gbt_stats_kernel(const float* __restrict__ F, const float* __restrict__ y,
                                                         const uint8_t* __restrict__ mask, int64_t n,
                                                         float* __restrict__ stats, float* __restrict__ smax) {
-    float m[3] = {0.f, 0.f, 0.f};
+    constexpr int NS = XGB ? 2 : 3;
+    float m[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) m[s] = 0.f;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         const float p = 1.f / (1.f + __expf(-F[r]));
         const float w = (mask == nullptr || mask[r]) ? 1.f : 0.f;
-        const float R = y[r] - p;
-        const float aR = fabsf(R);
-        const float st0 = R * w, st1 = aR * (1.f - aR) * w;
-        stats[r * 3 + 0] = st0;
-        stats[r * 3 + 1] = st1;
-        stats[r * 3 + 2] = w;
-        m[0] = fmaxf(m[0], fabsf(st0));
-        m[1] = fmaxf(m[1], st1);
-        m[2] = fmaxf(m[2], w);
+        float st[NS];
+        if constexpr (XGB) {
+            st[0] = (p - y[r]) * w;
+            st[1] = fmaxf(p * (1.f - p), 1e-16f) * w;
+        } else {
+            const float R = y[r] - p;
+            const float aR = fabsf(R);
+            st[0] = R * w;
+            st[1] = aR * (1.f - aR) * w;
+            st[2] = w;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            stats[r * NS + s] = st[s];
+            m[s] = fmaxf(m[s], fabsf(st[s]));
+        }
     }
-    block_absmax_flush<3>(m, smax);
+    block_absmax_flush<NS>(m, smax);
 }
 
 // F[r * ldf + k] += scale * vals[leaf[r] * ldv] for every routed row (leaf >= 0).
@@ -927,7 +939,17 @@ HM_API int hm_gbt_stats(const float* F, const float* y, const uint8_t* mask, int
     if (n <= 0) return 0;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(gbt_stats_kernel, dim3((int)blocks), dim3(256), 0, stream, F, y, mask, n, stats, smax);
+    hipLaunchKernelGGL((gbt_stats_kernel<0>), dim3((int)blocks), dim3(256), 0, stream, F, y, mask, n, stats, smax);
+    HM_LAUNCH_RET();
+}
+
+// The XGBoost binary-logistic form: stats [n, 2] = {p - y, max(p (1 - p), 1e-16)} x mask.
+HM_API int hm_xgb_stats(const float* F, const float* y, const uint8_t* mask, int64_t n, float* stats,
+                        float* smax, hipStream_t stream) {
+    if (n <= 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL((gbt_stats_kernel<1>), dim3((int)blocks), dim3(256), 0, stream, F, y, mask, n, stats, smax);
     HM_LAUNCH_RET();
 }
 

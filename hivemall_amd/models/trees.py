@@ -1138,5 +1138,6 @@ _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int
                                               _P, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
+_native.register_hip("hm_xgb_stats", [_P, _P, _P, _I64, _P, _P, _P])
 _native.register_hip("hm_level_finalize", [_P] * 21)
 _native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, _P])

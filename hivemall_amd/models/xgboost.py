@@ -140,9 +140,27 @@ class XGBoostTrainer(Learner):
         if float(c["colsample_bynode"]) < 1.0:
             mtry = max(1, int(round(ncol * float(c["colsample_bynode"]))))
         self.importance = np.zeros(d)
+        # binary logistic on the GPU: the round's (g, h) and |max| in one fused kernel
+        fused = F.is_cuda and self.K == 1 and self.objective in ("binary:logistic", "reg:logistic")
+        if fused:
+            y1 = Y[:, 0].contiguous()
+            stats_buf = torch.empty((n, 2), dtype=torch.float32, device=dev)
+            smax = torch.zeros(2, dtype=torch.float32, device=dev)
+            all_rows = torch.arange(n, dtype=torch.int32, device=dev)
         for it in range(int(c["num_round"])):
-            Gr, Hs = self._grad(F, Y)
-            if m_sub < n:
+            if fused:
+                mask = None
+                if m_sub < n:
+                    sel = torch.randperm(n, generator=g, device=dev)[:m_sub]
+                    mask = torch.zeros(n, dtype=torch.bool, device=dev)
+                    mask[sel] = True
+                smax.zero_()
+                _native.check(_native.hip().hm_xgb_stats(
+                    _native.ptr(F), _native.ptr(y1), _native.ptr(mask), C.c_int64(n), _native.ptr(stats_buf),
+                    _native.ptr(smax), _native.stream_of(dev)), "hm_xgb_stats")
+            else:
+                Gr, Hs = self._grad(F, Y)
+            if not fused and m_sub < n:
                 sel = torch.randperm(n, generator=g, device=dev)[:m_sub]
                 w = torch.zeros(n, device=dev)
                 w[sel] = 1.0
@@ -153,13 +171,16 @@ class XGBoostTrainer(Learner):
                 fmask[torch.randperm(d, generator=gcpu)[:ncol]] = True
             round_trees = []
             for k in range(self.K):
-                stats = torch.stack([Gr[:, k], Hs[:, k]], 1).contiguous()
+                stats = stats_buf if fused else torch.stack([Gr[:, k], Hs[:, k]], 1).contiguous()
                 b = HistTreeBuilder(q, "xgb", int(c["max_depth"]), 2 * float(c["min_child_weight"]),
                                     float(c["min_child_weight"]), mtry, c["max_leaves"],
                                     seed=self.seed * 7919 + it * self.K + k, mixer=self.mixer,
                                     lam=float(c["lambda"]), alpha=float(c["alpha"]),
                                     min_gain=2.0 * float(c["gamma"]), feature_mask=fmask)
-                tree = b.build(stats)
+                if fused:
+                    tree = b.build(stats, smax=smax, act_rows=all_rows if mask is None else None)
+                else:
+                    tree = b.build(stats)
                 tree.value = [None if v is None else [eta * v[0]] for v in tree.value]
                 if F.is_cuda:   # fused leaf update (trees.hip gbt_apply_kernel)
                     vals = b.node_values.float().contiguous()
