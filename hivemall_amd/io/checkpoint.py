@@ -23,6 +23,7 @@ import json
 import os
 import shutil
 import tempfile
+import time
 
 import numpy as np
 import torch
@@ -99,6 +100,7 @@ def save(learner, path: str, model_table: bool = True) -> str:
             "cv": vars(learner.cv) if hasattr(learner, "cv") else None,
             "hyper": dataclasses.asdict(learner.hyper) if dataclasses.is_dataclass(getattr(learner, "hyper", None)) else None,
             "torch_rng": torch.get_rng_state().tolist(),
+            "saved_ns": time.time_ns(),       # orders checkpoints (the .old-* fallback)
         }
         with open(os.path.join(tmp, "meta.json"), "w") as f:
             json.dump(meta, f, default=lambda o: None)
@@ -123,6 +125,10 @@ def save(learner, path: str, model_table: bool = True) -> str:
         _fsync_dir(parent)
         if old is not None:
             shutil.rmtree(old, ignore_errors=True)
+        # a crash between the final rename and this cleanup in an EARLIER save left a stale
+        # .old-* behind: ``path`` is complete now, so none of them is needed any more
+        for stale in glob.glob(glob.escape(path.rstrip("/")) + ".old-*"):
+            shutil.rmtree(stale, ignore_errors=True)
     except BaseException:
         shutil.rmtree(tmp, ignore_errors=True)
         raise
@@ -155,9 +161,19 @@ def load(path: str, device=None, restore_rng: bool = False, **kw):
     """Rebuild a learner from ``save``.  ``restore_rng``: also restore the process-global torch
     CPU RNG to its state at save time (off by default: loading must not reseed the caller)."""
     if not os.path.exists(os.path.join(path, "meta.json")):
-        olds = sorted(glob.glob(path.rstrip("/") + ".old-*"))
-        if olds:                     # a crash between the two renames of save(): take the old one
-            path = olds[-1]
+        # a crash between the two renames of save(): take the newest complete .old-* (by the
+        # save time written into its meta; the mkdtemp suffixes are random, not ordered)
+        best = None
+        for cand in glob.glob(glob.escape(path.rstrip("/")) + ".old-*"):
+            try:
+                with open(os.path.join(cand, "meta.json")) as f:
+                    t = json.load(f).get("saved_ns") or os.path.getmtime(os.path.join(cand, "meta.json"))
+            except (OSError, ValueError):
+                continue
+            if best is None or t > best[0]:
+                best = (t, cand)
+        if best is not None:
+            path = best[1]
     with open(os.path.join(path, "meta.json")) as f:
         meta = json.load(f)
     mod, qual = meta["class"].split(":")

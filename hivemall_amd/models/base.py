@@ -121,6 +121,34 @@ class Learner:
     def _dp(self) -> bool:
         return self.mixer is not None and self.mixer.world > 1
 
+    def agree_max(self, *sizes: int) -> tuple[int, ...]:
+        """The max of each size over the ranks (data-parallel replicas must share one shape:
+        every rank sizes its tables from its own shard's largest id otherwise)."""
+        if not self._dp():
+            return tuple(int(s) for s in sizes)
+        return tuple(int(self.mixer.all_reduce_scalar(float(s), "max")) for s in sizes)
+
+    def dp_sum(self, x: float) -> float:
+        """``x`` summed over the ranks (an epoch loss, a row count); ``x`` itself when not
+        data-parallel."""
+        return self.mixer.all_reduce_scalar(float(x), "sum") if self._dp() else float(x)
+
+    def epoch_converged(self, loss: float, reduced: bool = False) -> bool:
+        """ConversionState step on the job-wide epoch loss: every rank takes the same
+        break decision, so no rank leaves the epoch loop while another still calls the mixing
+        collectives."""
+        self.cv.incr_loss(loss if reduced else self.dp_sum(loss))
+        return self.cv.is_converged()
+
+    def dp_batches(self, n: int, bs: int) -> int:
+        """Launches for ``n`` rows in batches of ``bs``; data-parallel learners that mix every
+        few batches agree on the max over ranks (a rank with fewer rows runs empty batches), so
+        every rank reaches the same number of mix points."""
+        nb = (n + bs - 1) // bs if n > 0 else 0
+        if self._dp() and int(self.cl.get("mix_interval", 0) or 0) > 0:
+            nb = self.agree_max(nb)[0]
+        return nb
+
     def mix_tensors(self, tensors: list, flags: list = ()) -> None:
         """Average this rank's replica with the other ranks' (the ``GROUP BY feature
         avg(weight)`` / MixServer step): a dense bucketed all-reduce, or the

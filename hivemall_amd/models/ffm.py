@@ -187,17 +187,21 @@ class FFMTrainer(Learner):
 
     def _ensure_state(self):
         if self.state is None:
-            self.init_state(self.num_features, self.num_fields)
+            # data-parallel: the replicas of every rank must have one shape (each rank infers
+            # the sizes from its own shard otherwise)
+            self.init_state(*self.agree_max(self.num_features, self.num_fields))
 
     # ------------------------------------------------------------------ training
     def train_batch(self, b: FFMBatch, loss_buf: torch.Tensor | None = None) -> None:
         self._ensure_state()
         bs = int(self.cl["batch_size"])
-        for s in range(0, b.n, bs):
+        for k in range(self.dp_batches(b.n, bs)):
+            s = min(b.n, k * bs)
             sub = b.slice(s, min(b.n, s + bs))
             lb = None if loss_buf is None else loss_buf[s:s + sub.n]
-            ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True, loss=lb,
-                     grid=self.grid)
+            if sub.n:
+                ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True,
+                         loss=lb, grid=self.grid)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:
@@ -229,8 +233,7 @@ class FFMTrainer(Learner):
                 f = lambda t: None if t is None else t.index_select(0, perm).contiguous()
                 eb = FFMBatch(f(b.idx), f(b.fld), f(b.val), f(b.y))
             self.train_batch(eb, loss_buf)
-            self.cv.incr_loss(float(loss_buf.double().sum().item()))
-            if self.cv.is_converged():
+            if self.epoch_converged(float(loss_buf.double().sum().item())):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         if self.mixer is not None:

@@ -165,23 +165,27 @@ class FMTrainer(Learner):
             if dims is None:
                 dims = int(tmax(rows.idx)) + 1 if rows.idx.numel() else 1
                 if self.encoder is not None and self.encoder.mode == "dict":
+                    if self._dp():
+                        raise UDFArgumentException(
+                            "train_fm: data-parallel training needs integer feature indices or "
+                            "-feature_hashing (a per-rank string dictionary gives every rank its own ids)")
                     dims = max(dims, self.encoder.vocab_size())
-            self.init_state(dims)
+            # data-parallel replicas share one shape (each rank's shard has its own max id)
+            self.init_state(self.agree_max(dims)[0])
 
     # ------------------------------------------------------------------ training
     def train_rows(self, rows: SparseRows, loss_buf: torch.Tensor | None = None) -> None:
         self._ensure(rows)
         bs = int(self.cl["batch_size"])
         n = rows.n
-        for s in range(0, n, bs):
+        for k in range(self.dp_batches(n, bs)):
+            s = min(n, k * bs)
             e = min(n, s + bs)
-            ip = rows.indptr[s:e + 1]
-            if s:
-                # CSR slice: rebase is not needed, the kernel reads absolute offsets
-                pass
+            ip = rows.indptr[s:e + 1]   # CSR slice: the kernel reads absolute offsets
             lb = None if loss_buf is None else loss_buf[s:e]
-            fm_step(self.state, ip, rows.idx, rows.val, rows.y[s:e], self.h, self.k, train=True,
-                    t0=self.t, loss=lb, grid=self.grid)
+            if e > s:
+                fm_step(self.state, ip, rows.idx, rows.val, rows.y[s:e], self.h, self.k, train=True,
+                        t0=self.t, loss=lb, grid=self.grid)
             self.t += e - s
             mi = int(self.cl["mix_interval"])
             if mi > 0 and self._dp():
@@ -213,8 +217,7 @@ class FMTrainer(Learner):
             self.train_rows(rows, loss_buf)
             if va is not None:
                 self._adapt_lambda(va)
-            self.cv.incr_loss(float(loss_buf.double().sum().item()))
-            if self.cv.is_converged():
+            if self.epoch_converged(float(loss_buf.double().sum().item())):
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
         self.mix()
@@ -242,8 +245,7 @@ class FMTrainer(Learner):
                                self.h.eta0, self.h.lambda0, self.h.lambda_w, self.h.lambda_v,
                                self.h.classification, self.h.min_target, self.h.max_target)
         for ep in range(int(self.cl["iters"])):
-            self.cv.incr_loss(eng.epoch(X, y))
-            if self.cv.is_converged():
+            if self.epoch_converged(eng.epoch(X, y)):
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
         self.t += rows.n * (ep + 1)

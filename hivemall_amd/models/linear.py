@@ -374,8 +374,7 @@ class OnlineLinearLearner(Learner):
                                      None, mb)
             self.rows_seen += rows.n
             self.mix()
-            self.cv.incr_loss(float(loss.sum().item()))
-            if self.cv.is_converged():
+            if self.epoch_converged(float(loss.sum().item())):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         return self

@@ -287,19 +287,22 @@ class MatrixFactorization(_MFBase):
         u, i, r = _dev(users, torch.int32, dev), _dev(items, torch.int32, dev), \
             _dev(ratings, torch.float32, dev)
         if self.state is None:
-            self.init_state(int(tmax(u)) + 1, int(tmax(i)) + 1)
+            # data-parallel replicas share one shape: the max ids over every rank's shard
+            self.init_state(*self.agree_max(int(tmax(u)) + 1 if u.numel() else 1,
+                                            int(tmax(i)) + 1 if i.numel() else 1))
             if self.cl["update_mean"]:
-                self.state["mu"].fill_(float(r.mean().item()))
+                mu = self.dp_sum(float(r.double().sum().item())) / max(
+                    1.0, self.dp_sum(float(r.numel())))
+                self.state["mu"].fill_(mu)
         self.seen_u[u.long()] = True
         self.seen_i[i.long()] = True
         loss = torch.empty(u.numel(), device=dev)
         for ep in range(int(self.cl["iters"])):
             self._step(u, i, r, loss=loss)
             self._epoch_mix(ep)
-            el = float(loss.double().sum().item())
+            el = self.dp_sum(float(loss.double().sum().item()))
             self._epoch_end(el)
-            self.cv.incr_loss(el)
-            if self.cv.is_converged():
+            if self.epoch_converged(el, reduced=True):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         self.mix()
@@ -497,12 +500,9 @@ class BPRMF(_MFBase):
             self.seen_i[ti.long()] = True
             self.seen_i[tj.long()] = True
             for ep in range(int(self.cl["iters"])):
-                el = self._step_sharded(tu, ti, tj)
-                if self._dp():
-                    el = self.mixer.all_reduce_scalar(el, "sum")
+                el = self.dp_sum(self._step_sharded(tu, ti, tj))
                 self._epoch_end(el)
-                self.cv.incr_loss(el)
-                if self.cv.is_converged():
+                if self.epoch_converged(el, reduced=True):
                     break
             if self._dp():
                 f = [self.seen_u.to(torch.float32), self.seen_i.to(torch.float32)]
@@ -514,11 +514,10 @@ class BPRMF(_MFBase):
         self.seen_i[ti.long()] = True
         self.seen_i[tj.long()] = True
         for ep in range(int(self.cl["iters"])):
-            el = self.step(tu, ti, tj)
+            el = self.dp_sum(self.step(tu, ti, tj))
             self._epoch_end(el)
-            self.cv.incr_loss(el)
             self._epoch_mix(ep)
-            if self.cv.is_converged():
+            if self.epoch_converged(el, reduced=True):
                 break
         self.mix()
         return self
@@ -545,17 +544,16 @@ class BPRMF(_MFBase):
         u = torch.as_tensor(np.asarray(users, dtype=np.int32)).to(dev) if not torch.is_tensor(users) else users.to(dev)
         i = torch.as_tensor(np.asarray(items, dtype=np.int32)).to(dev) if not torch.is_tensor(items) else items.to(dev)
         if self.state is None:
-            self.init_state(n_users or int(tmax(u)) + 1, n_items or int(tmax(i)) + 1)
+            self.init_state(*self.agree_max(n_users or int(tmax(u)) + 1, n_items or int(tmax(i)) + 1))
         csr = self.build_csr(u, i, self.n_users)
         self.seen_u[u.long()] = True
         self.seen_i.fill_(True)
         per = int(self.cl["samples_per_epoch"]) or csr[1].numel()
         for ep in range(int(epochs or self.cl["iters"])):
-            el = self.step(n=per, csr=csr)
+            el = self.dp_sum(self.step(n=per, csr=csr))
             self._epoch_end(el)
-            self.cv.incr_loss(el)
             self._epoch_mix(ep)
-            if self.cv.is_converged():
+            if self.epoch_converged(el, reduced=True):
                 break
         self.mix()
         return self

@@ -694,6 +694,25 @@ def _encode_classes(yl):
     return cls.tolist(), torch.from_numpy(inv.astype(np.int64))
 
 
+def _encode_classes_dp(yl, mixer=None):
+    """:func:`_encode_classes` over the union of every rank's labels: a data-parallel fit
+    (row-sharded boosting) needs one class list on every rank, or K, the statistics width and
+    the label -> index map differ between ranks whose shards lack a class."""
+    if mixer is None or mixer.world <= 1:
+        return _encode_classes(yl)
+    import torch.distributed as dist
+
+    mine = _encode_classes(yl)[0]
+    allc = [None] * mixer.world
+    dist.all_gather_object(allc, mine)
+    cls = sorted(set().union(*allc))
+    if torch.is_tensor(yl):
+        ct = torch.tensor(cls, dtype=yl.dtype, device=yl.device)
+        return cls, torch.searchsorted(ct, yl.reshape(-1).contiguous()).to(torch.int64)
+    a = np.asarray(yl).reshape(-1)
+    return cls, torch.from_numpy(np.searchsorted(np.asarray(cls), a).astype(np.int64))
+
+
 class _ForestBase(Learner):
     SQL_DP = "union"     # trees t with t % world == rank, over all rows
     OPTIONS = TREE_OPTS
@@ -859,7 +878,8 @@ class GradientTreeBoostingClassifier(Learner):
         c = self.cl
         X = features if torch.is_tensor(features) else torch.from_numpy(_to_dense(features))
         X = X.float().to(self.device)
-        self.classes, yi = _encode_classes(labels if torch.is_tensor(labels) else np.asarray(labels))
+        self.classes, yi = _encode_classes_dp(labels if torch.is_tensor(labels) else np.asarray(labels),
+                                              self.mixer)
         yi = yi.to(self.device)
         K = len(self.classes)
         n, d = X.shape

@@ -35,7 +35,7 @@ from ..registry import udtf
 from ..utils import base91
 from ..utils.options import UDFArgumentException, opt
 from .base import Learner
-from .trees import HistTreeBuilder, Tree, _encode_classes, _to_dense, predict_forest, quantize
+from .trees import HistTreeBuilder, Tree, _encode_classes_dp, _to_dense, predict_forest, quantize
 
 XGB_OPTS = [
     opt("objective", None, "binary:logistic", str,
@@ -105,7 +105,7 @@ class XGBoostTrainer(Learner):
         lab = labels if torch.is_tensor(labels) else torch.as_tensor(np.asarray(labels, dtype=np.float64))
         lab = lab.to(dev)
         if self.objective.startswith("multi:"):
-            self.classes, yi = _encode_classes(lab)
+            self.classes, yi = _encode_classes_dp(lab, self.mixer)
             yi = yi.to(dev)
             self.K = int(c["num_class"] or len(self.classes))
             if len(self.classes) > self.K:

@@ -26,7 +26,10 @@ AVERAGE (:meth:`ModelMixer.average`) is a *shard mean*, not a ring all-reduce:
 Tensors are grouped by dtype into one flat, world-padded wire buffer per group (allocated once
 per tensor list), so a model of five tensors costs two collectives per dtype, never a small
 all-reduce per tensor.  Strided views (the V half of the packed FFM V|G table) are packed by one
-strided copy; only the weights travel (AdaGrad/FTRL state stays local, as upstream).
+strided copy.  What travels is the caller's choice: the learners mix the weights and keep the
+AdaGrad accumulators local, as upstream; FFM also mixes the FTRL (z, n) of its linear term,
+because its weight w is a function of (z, n) recomputed at every update (a mixed w alone would be
+overwritten by the next local update).
 
 ARGMIN_KLD = SUM all-reduce over [w/σ, 1/σ] -> w = Σ(w/σ)/Σ(1/σ), σ = 1/Σ(1/σ) (fp32).
 SUM (:meth:`ModelMixer.all_reduce_sum`, histograms / counters) widens bf16/fp16 to fp32.
@@ -34,6 +37,7 @@ SUM (:meth:`ModelMixer.all_reduce_sum`, histograms / counters) widens bf16/fp16 
 from __future__ import annotations
 
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -74,7 +78,10 @@ class _FlatGroup:
     """Same-dtype tensors packed into one flat wire buffer, padded to a multiple of 4*world."""
 
     def __init__(self, tensors: list[torch.Tensor], world: int):
-        self.tensors = tensors
+        # weak references: a cached plan must not keep a discarded model alive in HBM
+        self._refs = [weakref.ref(t) for t in tensors]
+        self.shapes = [tuple(t.shape) for t in tensors]
+        self.busy = False            # an OverlappedMixer collective is in flight on the buffers
         self.dtype = tensors[0].dtype
         dev = tensors[0].device
         self.offs = []
@@ -90,10 +97,23 @@ class _FlatGroup:
         self.mean = torch.empty(self.shard, dtype=self.dtype, device=dev)
         self.out = torch.empty(self.n, dtype=self.dtype, device=dev)
         self.nbytes = self.n * self.send.element_size()
+        self.buf_bytes = 3 * self.nbytes + self.mean.numel() * self.mean.element_size()
+
+    @property
+    def tensors(self) -> list[torch.Tensor]:
+        ts = [r() for r in self._refs]
+        if any(t is None for t in ts):
+            raise RuntimeError("mix plan: a mixed tensor was freed while its plan was in use")
+        return ts
+
+    def matches(self, tensors: list[torch.Tensor]) -> bool:
+        return all(r() is t for r, t in zip(self._refs, tensors))
 
     def seg(self, buf: torch.Tensor, k: int) -> torch.Tensor:
-        t = self.tensors[k]
-        return buf[self.offs[k]:self.offs[k] + t.numel()].view(t.shape)
+        n = 1
+        for d in self.shapes[k]:
+            n *= d
+        return buf[self.offs[k]:self.offs[k] + n].view(self.shapes[k])
 
     def pack(self) -> None:
         for k, t in enumerate(self.tensors):
@@ -131,6 +151,10 @@ class _FlatGroup:
 
 
 class ModelMixer:
+    # cached shard-mean plans: at most this many, holding at most this many buffer bytes
+    MAX_PLANS = 4
+    MAX_PLAN_BYTES = 16 << 30
+
     def __init__(self, ctx: DistContext | None = None, bucket_mb: float = 64.0,
                  small_bytes: int = 4 << 20, wire_dtype: torch.dtype | None = None):
         self.ctx = ctx or context()
@@ -151,18 +175,43 @@ class ModelMixer:
 
     # ---------------------------------------------------------------- shard-mean plan
     def plan(self, tensors: list[torch.Tensor]) -> list[_FlatGroup]:
-        """Flat wire groups for this exact tensor list (cached by identity and shape)."""
+        """Flat wire groups for this exact tensor list (cached by identity and shape).
+
+        The cache holds at most ``MAX_PLANS`` plans and ``MAX_PLAN_BYTES`` of wire buffers (3x
+        the mixed bytes each); the oldest idle plan is evicted first, and a plan whose
+        overlapped collective is still in flight is never evicted.  Plans refer to the model
+        tensors weakly: a freed model's plan is dropped, never matched by a new model that
+        happens to reuse its addresses."""
         key = tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) for t in tensors)
         p = self._plans.get(key)
+        if p is not None and not all(g.matches([t for t in tensors if t.dtype == g.dtype])
+                                     for g in p):
+            del self._plans[key]
+            p = None
         if p is None:
             by_dt: dict = {}
             for t in tensors:
                 by_dt.setdefault(t.dtype, []).append(t)
             p = [_FlatGroup(ts, self.world) for ts in by_dt.values()]
-            if len(self._plans) >= 4:                # one-off lists must not pin buffers
-                self._plans.pop(next(iter(self._plans)))
             self._plans[key] = p
+            self._evict(keep=key)
         return p
+
+    def _plan_bytes(self) -> int:
+        return sum(g.buf_bytes for p in self._plans.values() for g in p)
+
+    def _evict(self, keep) -> None:
+        for k in list(self._plans):
+            if len(self._plans) <= self.MAX_PLANS and self._plan_bytes() <= self.MAX_PLAN_BYTES:
+                break
+            if k != keep and not any(g.busy for g in self._plans[k]):
+                del self._plans[k]
+
+    def release(self) -> None:
+        """Drop every idle cached plan (frees its wire buffers)."""
+        for k in list(self._plans):
+            if not any(g.busy for g in self._plans[k]):
+                del self._plans[k]
 
     def _count(self, groups: list[_FlatGroup], tensors) -> None:
         self.calls += 1
@@ -331,6 +380,7 @@ class OverlappedMixer:
         self.groups = self.m.plan(tensors)
         for g in self.groups:
             g.pack()                                 # the snapshot (exact copy of the replica)
+            g.busy = True
         world = self.m.world
         if tensors[0].is_cuda:
             if self.side is None:
@@ -358,6 +408,7 @@ class OverlappedMixer:
         self.works = []
         for g in self.groups:
             g.merge()
+            g.busy = False
 
 
 class SparseDeltaMixer:

@@ -89,3 +89,31 @@ def test_checkpoint_save_replaces_atomically_and_keeps_rng(tmp_path):
     os.replace(p, p + ".old-x1")
     b = checkpoint.load(p, device="cpu")
     assert torch.equal(b.weights()[0], m.weights()[0])
+
+
+def test_checkpoint_old_fallback_takes_newest_and_save_cleans_stale(tmp_path):
+    """The .old-* fallback is ordered by the save time in meta.json, not by the random mkdtemp
+    suffix, and a successful save() removes .old-* directories left by earlier crashes."""
+    import json
+
+    import torch
+
+    from hivemall_amd.io import checkpoint
+    from hivemall_amd.models.linear import TrainClassifier
+    from hivemall_amd.io.synthetic import a9a_like
+    rows, y = a9a_like(300)
+    m1 = TrainClassifier("-loss logloss -iters 1", device="cpu").fit(rows, y)
+    m2 = TrainClassifier("-loss logloss -iters 3", device="cpu").fit(rows, y)
+    p = str(tmp_path / "ck")
+    checkpoint.save(m1, str(tmp_path / "a"))
+    checkpoint.save(m2, str(tmp_path / "b"))
+    os.replace(tmp_path / "b", p + ".old-aaaa")   # newer save, lexically FIRST suffix
+    os.replace(tmp_path / "a", p + ".old-zzzz")   # older save, lexically last suffix
+    # make the older one really older by its recorded time
+    meta = json.load(open(p + ".old-zzzz/meta.json"))
+    meta["saved_ns"] = 1
+    json.dump(meta, open(p + ".old-zzzz/meta.json", "w"))
+    b = checkpoint.load(p, device="cpu")
+    assert torch.equal(b.weights()[0], m2.weights()[0])
+    checkpoint.save(m1, p)
+    assert sorted(os.listdir(tmp_path)) == ["ck"]
