@@ -8,22 +8,32 @@ N>1 without a launcher: the parent process starts ``torch.distributed.run`` with
 launcher (``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``) every
 rank checks WORLD_SIZE == N and that the process group really holds N ranks, else exits 2.
 
-One process per GPU.  Each rank holds a full FFM model replica in HBM
-(2^20 hashed features x 39 fields x k=4, fp32 V + AdaGrad G + FTRL state, ~1.3 GB) and
-trains on its own shard of synthetic Criteo-shaped rows (weak scaling: per-GPU batch is
-fixed).  A step = one fused ``hm_ffm_step`` launch over ``--batch`` rows per GPU; every
-``--mix-every`` steps the replicas are averaged with a bucketed RCCL all-reduce over xGMI
-(the MixServer replacement) — that mixing cost is inside the timed region.
+One process per GPU.  Each rank holds a full FFM model replica in HBM (2^20 hashed features x
+39 fields x k=4, one AdaGrad accumulator per (feature, field) slot as Hivemall's AdaGradEntry,
+all in line-padded feature blocks [V | G]: bf16 V (stochastic rounding, fp32 math) + fp32 G by
+default, 0.5 GB; ``--state fp32`` = Hivemall's fp32 V, 0.9 GB; FTRL w/z/n of the linear term
+fp32; ``--adagrad element`` = one accumulator per V element, stored like V) and trains on its own shard of synthetic
+Criteo-shaped rows (weak scaling: per-GPU batch is fixed).  A step = one fused ``hm_ffm_step``
+launch over ``--batch`` rows per GPU; every ``--mix-every`` steps the replicas are averaged
+with the shard-mean collective of ``parallel/mix.py`` (all-to-all -> fp32 mean of each rank's
+1/N shard -> all-gather, over RCCL/xGMI: the MixServer replacement), stale-by-one and
+overlapped with the next steps' compute; that mixing cost is inside the timed region.
 
 Timing: W untimed warmup steps, then barrier + synchronize, K timed steps, synchronize +
-barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the
-mixed model on held-out rows and the planted model's logloss (the Bayes floor).
+barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the mixed
+model on held-out rows and the planted model's logloss (the Bayes floor).
+
+On the GPU the same schedule then runs a second time with fp32 V|G state (the reference's
+precision) in the same process, on the same rows: ``value_fp32_state`` / ``logloss_heldout_fp32``
+(``--fp32-run 0`` skips it).  ``wall_s`` breaks the process's wall time down (data generation,
+setup, warmup, timed region, evaluation, the fp32 run).  ``HM_METRICS=<path>`` appends one JSON
+line per timed step (device ms from per-step events read after the timed region, rows/s, mean
+training loss, mixes and wire bytes) — the loss buffer is only written when it is set.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -46,11 +56,25 @@ def parse_args(argv=None):
     ap.add_argument("--mix-every", type=int, default=10)
     ap.add_argument("--mix-overlap", type=int, default=1,
                     help="1: stale-by-one mixing overlapped with compute (async MixServer semantics)")
-    ap.add_argument("--resident-batches", type=int, default=8)
+    ap.add_argument("--mix-mode", choices=("mean", "sum", "touched"), default="mean",
+                    help="mean: replicas averaged (Hivemall's MixServer); sum: the consensus moves "
+                         "by the sum of every rank's delta since the last mix")
+    ap.add_argument("--mix-power", type=float, default=1.0,
+                    help="sum mode: the consensus step is mean_r(delta_r) * N**power (1 = the sum)")
+    ap.add_argument("--mix-state", type=int, default=0,
+                    help="1: the AdaGrad accumulators G are mixed too (delta-summed in sum mode)")
+    ap.add_argument("--resident-batches", type=int, default=8,
+                    help="distinct batches per rank kept in HBM and replayed in turn")
     ap.add_argument("--eval-rows", type=int, default=262144)
     ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
     ap.add_argument("--state", choices=("bf16", "fp32"), default="bf16",
-                    help="V / AdaGrad state storage (bf16 = stochastic-rounded, fp32 accumulate)")
+                    help="V / AdaGrad state storage of the headline run (bf16 = stochastic-rounded, "
+                         "fp32 accumulate)")
+    ap.add_argument("--fp32-run", type=int, default=1,
+                    help="GPU, --state bf16: also time the same schedule with fp32 state")
+    ap.add_argument("--adagrad", choices=("slot", "element"), default="slot",
+                    help="AdaGrad accumulator of V: one per (feature, field) slot (Hivemall's "
+                         "AdaGradEntry; fp32) or one per V element (stored like V)")
     ap.add_argument("--layout", choices=("packed", "split"), default="packed",
                     help="V/G state layout: packed V|G slots (one 16-B access per slot) or split tables")
     ap.add_argument("--reload", type=int, default=-1,
@@ -110,47 +134,47 @@ def check_world(args, ctx) -> None:
         sys.exit(2)
 
 
-def main(argv=None):
-    args = parse_args(argv)
-    rc = self_launch(args, argv)
-    if rc is not None:
-        sys.exit(rc)
-    from hivemall_amd.parallel.dist import init_distributed
-    from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
+def run_schedule(args, ctx, idx, y, state: str, data, metrics=None) -> dict:
+    """One full FFM schedule (fresh model, warmup, timed region, final mix, held-out logloss).
+
+    ``state``: "bf16" or "fp32" V|G storage.  Returns the timing / quality record."""
     from hivemall_amd.models.ffm import FFMTrainer
     from hivemall_amd.ops.ffm import ffm_step
-    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
 
-    ctx = init_distributed(device=args.device)
     dev = ctx.device
     world, rank = ctx.world_size, ctx.rank
-    check_world(args, ctx)
-    F = 39
+    F = idx.shape[1]
     NF = 1 << args.hash_bits
     B = args.batch
     nres = max(1, args.resident_batches)
-
-    # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
-    gdev = torch.device("cpu") if args.gen_device == "cpu" else dev
-    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=gdev)
-    idx, y = idx.to(dev), y.to(dev)
+    wall = {}
+    t_setup = time.perf_counter()
     opts = (f"-classification -factors {args.factors} -feature_hashing {args.hash_bits} "
             f"-num_fields {F} -seed 31 -batch_size {B}" +
-            (" -bf16_state" if args.state == "bf16" and dev.type == "cuda" else "") +
-            (" -split_state" if args.layout == "split" else ""))
+            (" -bf16_state" if state == "bf16" and dev.type == "cuda" else "") +
+            (" -split_state" if args.layout == "split" else "") +
+            (" -elementwise_adagrad" if args.adagrad == "element" else ""))
     tr = FFMTrainer(opts, device=dev)
     tr.init_state(NF, F)
     st, hyper = tr.state, tr.hyper
     hyper.reload = None if args.reload < 0 else bool(args.reload)
     mixer = ModelMixer(ctx)
+    # mixed: V (weights) and the FTRL (z, n) the linear weight w is computed from, w, w0;
+    # AdaGrad's G stays local (parallel/mix.py)
     mix_tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
-    grid = args.grid
-
-    overlap = OverlappedMixer(mixer) if args.mix_overlap else None
+    if args.mix_state:
+        mix_tensors.append(st["G"])
+    overlap = OverlappedMixer(mixer, args.mix_mode, args.mix_power) if args.mix_overlap else None
+    loss_buf = torch.empty(B, dtype=torch.float32, device=dev) if metrics is not None else None
+    step_loss = []
 
     def step(i):
         s = (i % nres) * B
-        ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True, grid=grid)
+        ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True, grid=args.grid,
+                 loss=loss_buf)
+        if loss_buf is not None:
+            step_loss.append(loss_buf.mean())          # device scalar, read after timing
         if world > 1 and (i + 1) % args.mix_every == 0:
             if overlap is not None:
                 overlap.start(mix_tensors)   # finishes the previous mix, launches this one
@@ -161,31 +185,57 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    sync()
+    wall["setup"] = time.perf_counter() - t_setup
+    t = time.perf_counter()
     for i in range(args.warmup):
         step(i)
     sync()
     ctx.barrier()
     sync()
+    wall["warmup"] = time.perf_counter() - t
     calls0 = mixer.calls
+    wire0 = mixer.wire_bytes
+    step_loss.clear()
+    ev = []
+    timed_steps = range(args.warmup, args.warmup + args.steps)
+    use_ev = metrics is not None and dev.type == "cuda"
     t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
+    for i in timed_steps:
+        if use_ev:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append(e)
         step(i)
     if overlap is not None:
         overlap.finish()   # the last in-flight mix is applied inside the timed region
+    if use_ev:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.append(e)
     sync()
     ctx.barrier()
     t1 = time.perf_counter()
+    wall["timed"] = t1 - t0
     mixes_timed = mixer.calls - calls0
-    elapsed = t1 - t0
-    elapsed = mixer.all_reduce_scalar(elapsed, "max")
-    ms_per_step = 1000.0 * elapsed / max(1, args.steps)
-    rows_total = float(B) * world * args.steps
-    rows_per_s = rows_total / elapsed
+    wire_timed = mixer.wire_bytes - wire0
+    elapsed = mixer.all_reduce_scalar(t1 - t0, "max")
+    if metrics is not None:
+        for k, i in enumerate(timed_steps):
+            ms = ev[k].elapsed_time(ev[k + 1]) if use_ev else 1e3 * elapsed / args.steps
+            mixed = world > 1 and (i + 1) % args.mix_every == 0
+            metrics.log(event="step", state=state, step=i, device_ms=round(ms, 4),
+                        rows_per_s=round(B / (ms * 1e-3), 1) if ms > 0 else None,
+                        loss=round(float(step_loss[k].item()), 6), mix=mixed,
+                        wire_bytes=(wire_timed // max(1, mixes_timed)) if mixed else 0)
+    out = {"elapsed_s": elapsed, "ms_per_step": 1000.0 * elapsed / max(1, args.steps),
+           "rows_per_s": float(B) * world * args.steps / elapsed, "mixes_timed": mixes_timed,
+           "mixed_bytes": int(sum(t.numel() * t.element_size() for t in mix_tensors))}
     if os.environ.get("HM_TRACE"):
         # host + device timeline of a few extra steps (outside the timed region)
         from hivemall_amd.prof import host_trace
 
-        with host_trace(os.environ["HM_TRACE"], name="bench_ffm", rank=ctx.rank):
+        with host_trace(os.environ["HM_TRACE"], name=f"bench_ffm_{state}", rank=rank):
             for i in range(3):
                 step(args.warmup + args.steps + i)
             if overlap is not None:
@@ -193,35 +243,91 @@ def main(argv=None):
             sync()
 
     # ---- mix cost on its own (synchronous, outside the timed region); leaves the model mixed ----
-    probe = mixer.probe(mix_tensors, args.mix_probe) if world > 1 else {}
+    out["probe"] = mixer.probe(mix_tensors, args.mix_probe) if world > 1 else {}
     # ---- quality: final mix, then held-out logloss vs the planted-model floor ----
+    t = time.perf_counter()
     if world > 1:
         mixer.average(mix_tensors)
-    ll = floor = None
+    out["ll"] = None
+    if rank == 0:
+        eidx, ey, elogit = data["eval"]
+        pred = torch.empty(eidx.shape[0], dtype=torch.float32, device=dev)
+        for s in range(0, eidx.shape[0], B):
+            e = min(eidx.shape[0], s + B)
+            ffm_step(st, eidx[s:e], None, None, None, hyper, train=False, pred=pred[s:e])
+        yy = (ey > 0).float()
+        out["ll"] = torch.nn.functional.binary_cross_entropy_with_logits(pred, yy).item()
+        out["floor"] = torch.nn.functional.binary_cross_entropy_with_logits(elogit, yy).item()
+    sync()
+    wall["eval"] = time.perf_counter() - t
+    out["wall"] = wall
+    mixer.release()
+    del tr, st
+    return out
+
+
+def main(argv=None):
+    t_start = time.perf_counter()
+    args = parse_args(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    from hivemall_amd.parallel.dist import init_distributed
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.prof import MetricsWriter
+
+    ctx = init_distributed(device=args.device)
+    dev = ctx.device
+    world, rank = ctx.world_size, ctx.rank
+    check_world(args, ctx)
+    F = 39
+    B = args.batch
+    nres = max(1, args.resident_batches)
+    metrics = MetricsWriter(rank=rank) if os.environ.get("HM_METRICS") else None
+
+    # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
+    t = time.perf_counter()
+    gdev = torch.device("cpu") if args.gen_device == "cpu" else dev
+    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=gdev)
+    idx, y = idx.to(dev), y.to(dev)
+    data = {"eval": None}
     if rank == 0:
         eidx, ey, elogit = criteo_like(args.eval_rows, args.hash_bits, seed=999_999, device=gdev,
                                        return_logit=True)
-        eidx, ey, elogit = eidx.to(dev), ey.to(dev), elogit.to(dev)
-        pred = torch.empty(args.eval_rows, dtype=torch.float32, device=dev)
-        for s in range(0, args.eval_rows, B):
-            e = min(args.eval_rows, s + B)
-            ffm_step(st, eidx[s:e], None, None, None, hyper, train=False, pred=pred[s:e])
-        yy = (ey > 0).float()
-        ll = torch.nn.functional.binary_cross_entropy_with_logits(pred, yy).item()
-        floor = torch.nn.functional.binary_cross_entropy_with_logits(elogit, yy).item()
+        data["eval"] = (eidx.to(dev), ey.to(dev), elogit.to(dev))
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_gen = time.perf_counter() - t
+
+    state = args.state if dev.type == "cuda" else "fp32"
+    main_run = run_schedule(args, ctx, idx, y, state, data, metrics)
+    fp32_run = None
+    if dev.type == "cuda" and state == "bf16" and args.fp32_run:
+        fp32_run = run_schedule(args, ctx, idx, y, "fp32", data, metrics)
+
+    wall = {"gen": round(t_gen, 3)}
+    for k, v in main_run["wall"].items():
+        wall[k] = round(v, 3)
+    if fp32_run is not None:
+        wall["fp32_run"] = round(sum(fp32_run["wall"].values()), 3)
+    wall["total"] = round(time.perf_counter() - t_start, 3)
+    if metrics is not None:
+        metrics.log(event="summary", wall_s=wall, rows_per_s=main_run["rows_per_s"],
+                    rows_per_s_fp32=fp32_run["rows_per_s"] if fp32_run else None)
     if rank == 0:
+        ll, floor = main_run["ll"], main_run.get("floor")
         out = {
             "metric": BASELINE_METRIC,
-            "value": round(rows_per_s, 1),
+            "value": round(main_run["rows_per_s"], 1),
             "unit": "rows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(main_run["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if (args.state == "bf16" and dev.type == "cuda") else "fp32",
+            "dtype": "bf16" if state == "bf16" else "fp32",
             "data": "synthetic (Criteo-shaped: 39 fields, Kaggle-DAC cardinalities, power-law "
                     "values, planted FM logit), random-init weights",
             "config": {
@@ -232,20 +338,29 @@ def main(argv=None):
                 "nnz_per_row": F,
                 "parallelism": f"dp{world}",
                 "mix_every": args.mix_every,
+                "state": (f"{state} V, " + ("fp32 AdaGrad accumulator per (feature, field) slot"
+                                            if args.adagrad == "slot" else f"{state} AdaGrad G per element") +
+                          " (fp32 math" + (", stochastic rounding)" if state == "bf16" else ")")),
                 "state_layout": args.layout if dev.type == "cuda" else "split",
                 "reload": (args.layout == "split") if args.reload < 0 else bool(args.reload),
-                "mixed_bytes_per_mix": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
-                "mixes_in_timed_region": mixes_timed,
-                "mix_overlapped": bool(overlap is not None),
+                "mixed_bytes_per_mix": main_run["mixed_bytes"],
+                "mixes_in_timed_region": main_run["mixes_timed"],
+                "mix_overlapped": bool(args.mix_overlap),
+                "resident_batches": nres,
             },
             "rccl_world": world if ctx.backend == "nccl" else None,
             "dist_backend": ctx.backend,
             "world": world,
-            **probe,
+            **main_run["probe"],
             "logloss_heldout": round(ll, 5) if ll is not None else None,
             "logloss_planted_floor": round(floor, 5) if floor is not None else None,
             "rows_trained_per_rank": B * (args.steps + args.warmup),
+            "wall_s": wall,
         }
+        if fp32_run is not None:
+            out["value_fp32_state"] = round(fp32_run["rows_per_s"], 1)
+            out["ms_per_step_fp32_state"] = round(fp32_run["ms_per_step"], 4)
+            out["logloss_heldout_fp32"] = round(fp32_run["ll"], 5)
         print(json.dumps(out), flush=True)
     from hivemall_amd.parallel.dist import shutdown
     shutdown()

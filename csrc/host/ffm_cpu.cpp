@@ -42,6 +42,12 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
     // slots between consecutive features (>= NFLD: the GPU's packed table pads each feature
     // block to whole 128-B lines)
     const size_t FS = ip[16] > 0 ? (size_t)ip[16] : (size_t)NFLD;
+    // AdaGrad accumulator: 1 = ONE per (feature, field) slot, G[i * GS + f] (Hivemall's
+    // AdaGradEntry: a single sum of squared gradients per entry, shared by the k factors);
+    // 0 = one per element, laid out like V
+    const int slot_g = ip[17];
+    const size_t GS = ip[18] > 0 ? (size_t)ip[18] : FS;   // slot-G: floats between features
+    if (slot_g && Kp > 64) return 22;
     std::vector<int> ri(F), rf(F);
     std::vector<float> rx(F);
     std::vector<float> snap((size_t)F * F * Kp);
@@ -102,9 +108,23 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
                 if (a == b || ri[a] < 0 || ri[b] < 0) continue;
                 const float coef = ks * rx[a] * rx[b];
                 float* pv = V + ((size_t)ri[a] * FS + rf[b]) * ss;
-                float* pg = G + ((size_t)ri[a] * FS + rf[b]) * ss;
                 const float* own = &snap[((size_t)a * F + b) * Kp];
                 const float* par = &snap[((size_t)b * F + a) * Kp];
+                if (slot_g) {
+                    // G += sum_f g_f^2 (fp32, factor order), then every factor steps with it
+                    float* pg = G + (size_t)ri[a] * GS + rf[b];
+                    float gs = *pg;
+                    float gk[64];
+                    for (int k = 0; k < Kp; ++k) {
+                        gk[k] = coef * par[k] + lv * own[k];
+                        gs += gk[k] * gk[k];
+                    }
+                    *pg = gs;
+                    const float r = 1.f / std::sqrt(gs + eps);
+                    for (int k = 0; k < Kp; ++k) pv[k] = own[k] - eta0 * gk[k] * r;
+                    continue;
+                }
+                float* pg = G + ((size_t)ri[a] * FS + rf[b]) * ss;
                 for (int k = 0; k < Kp; ++k) {
                     const float g = coef * par[k] + lv * own[k];
                     pg[k] += g * g;

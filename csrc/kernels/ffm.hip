@@ -47,6 +47,9 @@ struct FFMParams {
     int train;             // 0: predict only
     int use_linear, use_bias, norm;
     int reload;
+    int gstride;           // per-slot G: floats between consecutive features of G
+    int vpad;              // per-slot G block layout: V slots per feature block (0: separate tables)
+    int tail16;            // per-slot G block layout: zero 16-B chunks after each G region
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
                            // table pads each feature block to whole 128-B lines)
@@ -237,8 +240,9 @@ __device__ __forceinline__ void linear_updates(const FFMParams& P, float kappa, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Generic kernel: any K, either layout (slot stride P.sstride), LDS staging when it fits.
-template <int KC, bool STAGE, bool BF>
+// Generic kernel: any K, either per-element layout (slot stride P.sstride) or per-slot G
+// (SG: one fp32 accumulator per slot at G[i * P.gstride + f]), LDS staging when it fits.
+template <int KC, bool STAGE, bool BF, bool SG>
 __global__ __launch_bounds__(256) void ffm_row_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y,
@@ -266,6 +270,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     const size_t nfld = (size_t)P.fstride;
     const size_t ss = (size_t)P.sstride;
     auto slot_off = [&](int i, int f) -> size_t { return ((size_t)i * nfld + (size_t)f) * ss; };
+    float* Gs = reinterpret_cast<float*>(G);
 
     for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
@@ -330,8 +335,10 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 const float coef = ks * s_x[a] * s_x[b];
                 const size_t ov = slot_off(ia, s_fld[b]);
                 float4 own[KC], par[KC], gg[KC];
+                if (!SG) {
 #pragma unroll
-                for (int c = 0; c < KC; ++c) gg[c] = ld_chunk<BF>(G, ov + 4 * c);
+                    for (int c = 0; c < KC; ++c) gg[c] = ld_chunk<BF>(G, ov + 4 * c);
+                }
                 if (STAGE) {
 #pragma unroll
                     for (int c = 0; c < KC; ++c) {
@@ -343,21 +350,46 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
 #pragma unroll
                     for (int c = 0; c < KC; ++c) { own[c] = ld_chunk<BF>(V, ov + 4 * c); par[c] = ld_chunk<BF>(V, op + 4 * c); }
                 }
+                float4 g[KC];
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-                    float4 g;
-                    g.x = coef * par[c].x + P.lambda_v * own[c].x;
-                    g.y = coef * par[c].y + P.lambda_v * own[c].y;
-                    g.z = coef * par[c].z + P.lambda_v * own[c].z;
-                    g.w = coef * par[c].w + P.lambda_v * own[c].w;
-                    gg[c].x += g.x * g.x; gg[c].y += g.y * g.y; gg[c].z += g.z * g.z; gg[c].w += g.w * g.w;
-                    own[c].x -= P.eta0 * g.x * rsqrtf(gg[c].x + P.eps);
-                    own[c].y -= P.eta0 * g.y * rsqrtf(gg[c].y + P.eps);
-                    own[c].z -= P.eta0 * g.z * rsqrtf(gg[c].z + P.eps);
-                    own[c].w -= P.eta0 * g.w * rsqrtf(gg[c].w + P.eps);
-                    const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
-                    st_chunk<BF>(V, ov + 4 * c, own[c], rnd);
-                    st_chunk<BF>(G, ov + 4 * c, gg[c], rnd ^ 0xA5A5A5A5u);
+                    g[c].x = coef * par[c].x + P.lambda_v * own[c].x;
+                    g[c].y = coef * par[c].y + P.lambda_v * own[c].y;
+                    g[c].z = coef * par[c].z + P.lambda_v * own[c].z;
+                    g[c].w = coef * par[c].w + P.lambda_v * own[c].w;
+                }
+                if constexpr (SG) {
+                    // one accumulator per slot: G += sum of the k squared gradients (factor
+                    // order), then every factor steps with 1 / sqrt(G + eps)
+                    float* pg = Gs + (size_t)ia * P.gstride + s_fld[b];
+                    float gs = *pg;
+#pragma unroll
+                    for (int c = 0; c < KC; ++c)
+                        gs = (((gs + g[c].x * g[c].x) + g[c].y * g[c].y) + g[c].z * g[c].z) + g[c].w * g[c].w;
+                    *pg = gs;
+                    const float r = rsqrtf(gs + P.eps);
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) {
+                        own[c].x -= P.eta0 * g[c].x * r;
+                        own[c].y -= P.eta0 * g[c].y * r;
+                        own[c].z -= P.eta0 * g[c].z * r;
+                        own[c].w -= P.eta0 * g[c].w * r;
+                        const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
+                        st_chunk<BF>(V, ov + 4 * c, own[c], rnd);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < KC; ++c) {
+                        gg[c].x += g[c].x * g[c].x; gg[c].y += g[c].y * g[c].y;
+                        gg[c].z += g[c].z * g[c].z; gg[c].w += g[c].w * g[c].w;
+                        own[c].x -= P.eta0 * g[c].x * rsqrtf(gg[c].x + P.eps);
+                        own[c].y -= P.eta0 * g[c].y * rsqrtf(gg[c].y + P.eps);
+                        own[c].z -= P.eta0 * g[c].z * rsqrtf(gg[c].z + P.eps);
+                        own[c].w -= P.eta0 * g[c].w * rsqrtf(gg[c].w + P.eps);
+                        const uint32_t rnd = BF ? hash3(rrow, (uint32_t)s, (uint32_t)c) : 0u;
+                        st_chunk<BF>(V, ov + 4 * c, own[c], rnd);
+                        st_chunk<BF>(G, ov + 4 * c, gg[c], rnd ^ 0xA5A5A5A5u);
+                    }
                 }
             }
             linear_updates(P, kappa, scale, s_idx, s_x, w, wz, wn, bias);
@@ -366,207 +398,6 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Packed-layout kernel (K <= 8, F*F <= 2048): each thread owns NS = ceil(F*F / 256) slots,
-// decodes their (a, b) once per launch, and moves a slot's V and G with the same 16-B
-// accesses.  RELOAD = false keeps the gathered raw V/G words in registers until the update
-// (two memory instructions per slot in total: gather, store); RELOAD = true re-reads the packed
-// slot right before the update (an L2 hit: the gather brought the line in a few microseconds
-// earlier), as short a Hogwild read-modify-write window as the split kernel's.
-template <int KC, bool BF>
-struct SlotIO {
-    using SV = typename std::conditional<BF, uint2, float4>::type;
-    // slot index -> raw V and G chunks (Kp = 4*KC elements per half)
-    __device__ static __forceinline__ void load(const void* VG, uint32_t slot, SV (&v)[KC], SV (&g)[KC]) {
-        if constexpr (BF) {
-            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(VG) + (size_t)slot * (8 * KC));
-            uint2 u[2 * KC];
-#pragma unroll
-            for (int c = 0; c < KC; ++c) {
-                const uint4 q = p[c];
-                u[2 * c] = make_uint2(q.x, q.y);
-                u[2 * c + 1] = make_uint2(q.z, q.w);
-            }
-#pragma unroll
-            for (int c = 0; c < KC; ++c) { v[c] = u[c]; g[c] = u[KC + c]; }
-        } else {
-            const float4* p = reinterpret_cast<const float4*>(VG) + (size_t)slot * (2 * KC);
-#pragma unroll
-            for (int c = 0; c < KC; ++c) { v[c] = p[c]; g[c] = p[KC + c]; }
-        }
-    }
-    __device__ static __forceinline__ void store(void* VG, uint32_t slot, const float4 (&v)[KC],
-                                                 const float4 (&g)[KC], uint32_t rnd0) {
-        if constexpr (BF) {
-            uint2 u[2 * KC];
-#pragma unroll
-            for (int c = 0; c < KC; ++c) {
-                const uint32_t r1 = hash3(rnd0, (uint32_t)c, 0x51u);
-                const uint32_t r2 = r1 * 0x9E3779B1u + 0x632BE5ABu;
-                const uint32_t r3 = r2 * 0x85EBCA77u + 0x27D4EB2Fu;
-                const uint32_t r4 = r3 * 0xC2B2AE3Du + 0x165667B1u;
-                u[c] = make_uint2(hm::pack_bf16x2_sr(v[c].x, r1, v[c].y, r1 >> 16),
-                                  hm::pack_bf16x2_sr(v[c].z, r2, v[c].w, r2 >> 16));
-                u[KC + c] = make_uint2(hm::pack_bf16x2_sr(g[c].x, r3, g[c].y, r3 >> 16),
-                                       hm::pack_bf16x2_sr(g[c].z, r4, g[c].w, r4 >> 16));
-            }
-            uint4* p = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(VG) + (size_t)slot * (8 * KC));
-#pragma unroll
-            for (int c = 0; c < KC; ++c)
-                p[c] = make_uint4(u[2 * c].x, u[2 * c].y, u[2 * c + 1].x, u[2 * c + 1].y);
-        } else {
-            float4* p = reinterpret_cast<float4*>(VG) + (size_t)slot * (2 * KC);
-#pragma unroll
-            for (int c = 0; c < KC; ++c) { p[c] = v[c]; p[KC + c] = g[c]; }
-        }
-    }
-};
-
-// bf16 K=4 (the bench shape) is register-allocated for 4 waves/SIMD (<= 128 VGPRs); the other
-// shapes keep the compiler's choice.
-template <int KC, bool BF, int NS, bool RELOAD>
-__global__ __launch_bounds__(256, (BF && KC == 1 && NS <= 6) ? 4 : 1) void ffm_packed_kernel(
-    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
-    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
-    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
-    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
-{
-    using IO = SlotIO<KC, BF>;
-    using SV = typename IO::SV;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int F = P.F;
-    const int FF = F * F;
-    SV* s_v = reinterpret_cast<SV*>(smem);                                      // FF*KC
-    int* s_idx = reinterpret_cast<int*>(smem + (size_t)FF * KC * sizeof(SV));   // F
-    int* s_fld = s_idx + F;
-    float* s_x = reinterpret_cast<float*>(s_fld + F);
-    float* s_red = s_x + F;
-    const int tid = threadIdx.x;
-    const uint32_t nfld = (uint32_t)P.fstride;
-
-    // slot -> (a, b) is row-invariant: decoded once as a | b << 16 (-1 past the end)
-    int ab[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        const int s = tid + j * 256;
-        ab[j] = s < FF ? ((s / F) | ((s % F) << 16)) : -1;
-    }
-
-    // (Prefetching the next row's metadata during the gather was measured 15 % slower: the three
-    // extra VGPRs cross the 128-register line, 4 -> 3 waves/SIMD; profiles/ffm_layout_ab_r1.log.)
-    for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
-        // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
-        const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);
-
-        // ---- 2. gather own packed slots: V -> LDS image (+ registers), G -> registers; the
-        //         linear weight is fetched alongside, so the forward waits on no further global
-        //         round trip ----
-        float lw = 0.f;
-        if (P.use_linear && tid < F && s_idx[tid] >= 0) lw = w[s_idx[tid]];
-        SV ov[NS][KC], og[NS][KC];
-        uint32_t slot[NS];
-        uint32_t live = 0u;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            slot[j] = 0u;
-            if (ab[j] >= 0) {
-                const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
-                const int ia = s_idx[a];
-                SV v[KC], g[KC];
-                if (a != b && ia >= 0 && s_idx[b] >= 0) {
-                    slot[j] = (uint32_t)ia * nfld + (uint32_t)s_fld[b];
-                    IO::load(VG, slot[j], v, g);
-                    live |= 1u << j;
-                } else {
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) { v[c] = SV{}; g[c] = SV{}; }
-                }
-#pragma unroll
-                for (int c = 0; c < KC; ++c) {
-                    s_v[(a * F + b) * KC + c] = v[c];
-                    if (!RELOAD) { ov[j][c] = v[c]; og[j][c] = g[c]; }
-                }
-            }
-        }
-        __syncthreads();
-
-        // ---- 3. forward: pairs a < b ----
-        float part = 0.f;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            if (!(live >> j & 1u)) continue;
-            const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
-            if (a >= b) continue;
-            float d = 0.f;
-#pragma unroll
-            for (int c = 0; c < KC; ++c) {
-                const float4 u = to_f4<BF>(RELOAD ? s_v[(a * F + b) * KC + c] : ov[j][c]);
-                const float4 v = to_f4<BF>(s_v[(b * F + a) * KC + c]);
-                d += u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w;
-            }
-            part += d * s_x[a] * s_x[b];
-        }
-        part *= scale * scale;
-        if (P.use_linear && tid < F) part += lw * s_x[tid] * scale;   // lw = 0 for padding
-        float p = hm::block_sum(part, s_red);
-        if (P.use_bias) p += bias_w0(P, bias);
-
-        // ---- 4. loss ----
-        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
-
-        // ---- 5. AdaGrad(V) update on the packed slots (Hogwild) ----
-        if (P.train) {
-            float lz = 0.f, ln = 0.f;     // FTRL state of the linear term: in flight during the V updates
-            if (P.use_linear && tid < F && s_idx[tid] >= 0) { lz = wz[s_idx[tid]]; ln = wn[s_idx[tid]]; }
-            const float ks = kappa * scale * scale;
-            const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                if (!(live >> j & 1u)) continue;
-                const int a = ab[j] & 0xFFFF, b = ab[j] >> 16;
-                const float coef = ks * s_x[a] * s_x[b];
-                SV rv[KC], rg[KC];
-                if (RELOAD) {
-                    IO::load(VG, slot[j], rv, rg);
-                } else {
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) { rv[c] = ov[j][c]; rg[c] = og[j][c]; }
-                }
-                float4 own[KC], gg[KC];
-#pragma unroll
-                for (int c = 0; c < KC; ++c) {
-                    own[c] = to_f4<BF>(rv[c]);
-                    gg[c] = to_f4<BF>(rg[c]);
-                    const float4 par = to_f4<BF>(s_v[(b * F + a) * KC + c]);
-                    float4 g;
-                    g.x = coef * par.x + P.lambda_v * own[c].x;
-                    g.y = coef * par.y + P.lambda_v * own[c].y;
-                    g.z = coef * par.z + P.lambda_v * own[c].z;
-                    g.w = coef * par.w + P.lambda_v * own[c].w;
-                    gg[c].x += g.x * g.x; gg[c].y += g.y * g.y; gg[c].z += g.z * g.z; gg[c].w += g.w * g.w;
-                    own[c].x -= P.eta0 * g.x * rsqrtf(gg[c].x + P.eps);
-                    own[c].y -= P.eta0 * g.y * rsqrtf(gg[c].y + P.eps);
-                    own[c].z -= P.eta0 * g.z * rsqrtf(gg[c].z + P.eps);
-                    own[c].w -= P.eta0 * g.w * rsqrtf(gg[c].w + P.eps);
-                }
-                IO::store(VG, slot[j], own, gg, BF ? hash3(rrow, (uint32_t)(a * F + b), 0x3u) : 0u);
-            }
-            if (P.use_linear && tid < F) {
-                const int i = s_idx[tid];
-                if (i >= 0) {   // FTRL-proximal on the prefetched (w, z, n)
-                    const float g = kappa * s_x[tid] * scale;
-                    const float n1 = ln + g * g;
-                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[i] = z1;
-                    wn[i] = n1;
-                    w[i] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
-                }
-            }
-            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
-        }
-        __syncthreads();  // LDS reuse by the next row
-    }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Lean packed kernel (K <= 4, packed V|G slots): the shipped kernel for the headline shape.
@@ -787,9 +618,11 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
     }
 }
 
+
 // ---------------------------------------------------------------------------------------------
-// Pipelined kernel (bf16 packed V|G, K <= 4): the next row's 1,482 slot gathers fly into LDS by
-// LDS-DMA (global_load_lds_dwordx4: no VGPR destination) while the current row computes.
+// Pipelined kernel (packed per-element V|G, K <= 4; bf16 or fp32 state): the next row's 1,482
+// slot gathers fly into LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR destination) while the
+// current row computes.
 //
 // The lean kernel above still waits on two dependent global round trips per row (row metadata,
 // then the slot gather) with nothing else to do: per CU only ~4 rows' gathers are ever in flight,
@@ -807,128 +640,27 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
 // so each block keeps one row's 24 KB gather in flight behind its compute (4 blocks/CU: ~96 KB
 // in flight per CU).  Staleness: row r+G's slots are read before row r's updates land — the
 // same one-row Hogwild window the other ~1,000 rows in flight already impose.
+// Polling the DMA targets instead of vmcnt(0) (so no wave waits on the previous row's stores),
+// with an LDS hand-over of slots shared by consecutive rows, was measured no faster (101.1-101.6 M
+// rows/s default vs 98.8-100.8 M polled, profiles/ffm_poll_r2/bench_ab_corrected.log) and removed.
+// BF = false: the same pipeline over fp32 packed slots (32 B: V float4 | G float4; two 16-B DMAs
+// per slot; LDS 77.6 KB at NS = 6 -> 2 blocks/CU; opt-in HM_FFM_VARIANT=3).
 __device__ __forceinline__ void bar_raw() {
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes are done
     __builtin_amdgcn_s_barrier();
     __asm__ __volatile__("" ::: "memory");
 }
 
-// LDS reads of LDS-DMA targets hidden from hipcc's waitcnt pass (inline asm): the pass cannot
-// tell that a counted vmcnt(N) already retired the DMA and would put a vmcnt(0) — the previous
-// row's stores included — in front of every such read.  lds_read4 waits for its own result.
-typedef __attribute__((address_space(3))) const void* lds_cptr_t;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(lds_cptr_t)p;
-}
-// NS 16-B reads (stride 256 x 16 B: one address register, immediate offsets) and their wait in
-// ONE statement: with the wait in a separate asm the register allocator is free to copy the
-// destinations (v_mov) before the data has arrived
-template <int NS>
-__device__ __forceinline__ void lds_read16xN(uint4 (&q)[NS], const uint4* base) {
-    const uint32_t a = lds_addr(base);
-    if constexpr (NS == 2) {
-        __asm__ __volatile__("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:4096\n\ts_waitcnt lgkmcnt(0)"
-                             : "=&v"(q[0]), "=&v"(q[1]) : "v"(a) : "memory");
-    } else if constexpr (NS == 4) {
-        __asm__ __volatile__("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:4096\n\t"
-                             "ds_read_b128 %2, %4 offset:8192\n\tds_read_b128 %3, %4 offset:12288\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]) : "v"(a) : "memory");
-    } else if constexpr (NS == 6) {
-        __asm__ __volatile__("ds_read_b128 %0, %6\n\tds_read_b128 %1, %6 offset:4096\n\t"
-                             "ds_read_b128 %2, %6 offset:8192\n\tds_read_b128 %3, %6 offset:12288\n\t"
-                             "ds_read_b128 %4, %6 offset:16384\n\tds_read_b128 %5, %6 offset:20480\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5])
-                             : "v"(a) : "memory");
-    } else {
-        static_assert(NS == 8, "NS in {2, 4, 6, 8}");
-        __asm__ __volatile__("ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:4096\n\t"
-                             "ds_read_b128 %2, %8 offset:8192\n\tds_read_b128 %3, %8 offset:12288\n\t"
-                             "ds_read_b128 %4, %8 offset:16384\n\tds_read_b128 %5, %8 offset:20480\n\t"
-                             "ds_read_b128 %6, %8 offset:24576\n\tds_read_b128 %7, %8 offset:28672\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
-                               "=&v"(q[6]), "=&v"(q[7])
-                             : "v"(a) : "memory");
-    }
-}
-// the NS slots of this thread (stride 4096 B) set to the LDS_EMPTY mark (defined below)
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-template <int NS>
-__device__ __forceinline__ void lds_mark16xN(const uint4* base, uint32_t m) {
-    const uint32_t a = lds_addr(base);
-    const u32x4_t mm = {m, m, m, m};
-    static_assert(NS == 2 || NS == 4 || NS == 6 || NS == 8, "NS in {2, 4, 6, 8}");
-    __asm__ __volatile__("ds_write_b128 %0, %1\n\tds_write_b128 %0, %1 offset:4096" : : "v"(a), "v"(mm) : "memory");
-    if constexpr (NS >= 4)
-        __asm__ __volatile__("ds_write_b128 %0, %1 offset:8192\n\tds_write_b128 %0, %1 offset:12288" : : "v"(a), "v"(mm) : "memory");
-    if constexpr (NS >= 6)
-        __asm__ __volatile__("ds_write_b128 %0, %1 offset:16384\n\tds_write_b128 %0, %1 offset:20480" : : "v"(a), "v"(mm) : "memory");
-    if constexpr (NS >= 8)
-        __asm__ __volatile__("ds_write_b128 %0, %1 offset:24576\n\tds_write_b128 %0, %1 offset:28672" : : "v"(a), "v"(mm) : "memory");
-}
-__device__ __forceinline__ void lds_write16(void* p, u32x4_t v) {
-    __asm__ __volatile__("ds_write_b128 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_write8(void* p, uint2 v) {
-    const uint64_t x = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    __asm__ __volatile__("ds_write_b64 %0, %1" : : "v"(lds_addr(p)), "v"(x) : "memory");
-}
-__device__ __forceinline__ int lds_read4(const void* p) {
-    int v;
-    __asm__ __volatile__("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-    return v;
-}
-__device__ __forceinline__ void lds_write4(void* p, uint32_t v) {
-    __asm__ __volatile__("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
-}
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* glb_ptr_t;
 
-// "not landed yet" marks of the polled LDS-DMA targets.  A slot word is a pair of bf16 V or G
-// values: 0xFFFF is a NaN with a full payload that no arithmetic produces (canonical NaNs are
-// 0x7FC0 / 0xFFC0), so 0xFFFFFFFF never is a slot word; the same pattern is the float NaN that
-// marks w / z / n and val; idx and fld use INT_MIN + 1.  A genuine word equal to its mark only
-// costs the poll's bound, after which the wave falls back to vmcnt(0): results never depend on it.
-constexpr uint32_t LDS_EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t LDS_EMPTY_I = 0x80000001u;
-constexpr int POLL_MAX = 8192;
-
-__device__ __forceinline__ bool slot_landed(uint4 v) {
-    return v.x != LDS_EMPTY && v.y != LDS_EMPTY && v.z != LDS_EMPTY && v.w != LDS_EMPTY;
-}
-// wait until this lane's LDS-DMA word at p has replaced its mark (bounded; false = not seen)
-__device__ __forceinline__ bool lds_poll4(const void* p, uint32_t empty) {
-    for (int it = 0; it < POLL_MAX; ++it) {
-        if ((uint32_t)lds_read4(p) != empty) return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-// PM (polling modes, HM_FFM_VARIANT 4 / 5, training only; an experiment kept opt-in).  Step A's
-// vmcnt(0) also waits for the previous row's ~1,500 slot stores.  With PM every LDS-DMA target
-// is re-marked "empty" (LDS_EMPTY) after it is consumed and the consumer polls its own words
-// until the DMA has overwritten the mark (the wave that issued a DMA polls it; fallback
-// vmcnt(0) past POLL_MAX), so no wave waits on stores; a slot or linear term the next row
-// shares with this one (same feature and field: same address, same thread) is handed over in
-// LDS by E instead of DMA'd.  PM 1 issues the next row's slot DMA in C, PM 2 after this row's
-// stores.  Measured same-box (profiles/ffm_poll_r2/bench_ab_corrected.log): default 101.1-101.6 M
-// rows/s at held-out 0.4510-0.4512, PM 1 100.3-100.8 M at 0.4516-0.4518, PM 2 98.8-99.3 M at
-// 0.4510-0.4512 — the store wait is not what bounds this kernel.  At grid 1 the handover makes
-// PM 1 / 2 match the sequential order (round-1 packed kernel) where the default is one row stale
-// (benchmarks/probes/ffm_sink_probe.py), but at full grid cross-block staleness dominates.
-// BF = false: the same pipeline over fp32 packed slots (32 B: V float4 | G float4; two 16-B DMAs
-// per slot; LDS 77.6 KB at NS = 6 -> 2 blocks/CU); PM = 0 only; opt-in (HM_FFM_VARIANT=3).
-template <int NS, int PM, bool BF = true>
+template <int NS, bool BF = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2))) void ffm_pipe_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
-    constexpr bool POLL = PM != 0;   // PM 1: next row's slot DMA in C; 2: after this row's stores (F)
-    constexpr bool LATE = PM == 2;
-    static_assert(BF || PM == 0, "fp32 state: vmcnt waits only");
     constexpr uint32_t SLOT_B = BF ? 16u : 32u;                        // bytes per packed slot
     using Img = typename std::conditional<BF, uint2, float4>::type;   // V in the transposed image
     __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256 * (BF ? 1 : 2)];   // slot DMA landing zone
@@ -947,8 +679,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
     const uint32_t nfld = (uint32_t)P.fstride;
     const int G = gridDim.x;
     char* vg = reinterpret_cast<char*>(VG);
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    typedef const __attribute__((address_space(1))) void* glb_ptr_t;
 
     // row-invariant slot decode, packed a | b << 8 (one register per slot; F <= 45)
     int ab[NS];
@@ -960,11 +690,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 #define SA(j) (ab[j] & 0xFF)
 #define SB(j) (ab[j] >> 8)
     const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
-    if (wave == W_LIN && lane < 48) {
-        const float e = POLL ? __uint_as_float(LDS_EMPTY) : 0.f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { s_lin[0][k][lane] = e; s_lin[1][k][lane] = e; }
-    }
 
     // wave W_DMA, lanes < F: DMA of one row's raw meta into s_mr[bf] (no registers held)
     auto dma_meta = [&](int bf, int row) {
@@ -980,14 +705,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
         if (wave == W_META) {
             float sq = 0.f;
             if (lane < F) {
-                int ri = POLL ? lds_read4(&s_mr[bf][0][lane]) : s_mr[bf][0][lane];
-                int rf = fld ? (POLL ? lds_read4(&s_mr[bf][1][lane]) : s_mr[bf][1][lane]) : lane;
-                float rx = val ? __int_as_float(POLL ? lds_read4(&s_mr[bf][2][lane]) : s_mr[bf][2][lane]) : 1.f;
-                if (POLL) {   // consumed: mark empty for the DMA after next
-                    lds_write4(&s_mr[bf][0][lane], LDS_EMPTY_I);
-                    lds_write4(&s_mr[bf][1][lane], LDS_EMPTY_I);
-                    lds_write4(&s_mr[bf][2][lane], LDS_EMPTY);
-                }
+                int ri = s_mr[bf][0][lane];
+                int rf = fld ? s_mr[bf][1][lane] : lane;
+                float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
                 if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
                 s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
                 sq = rx * rx;
@@ -1029,12 +749,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
     };
     // wave W_LIN, lanes < F with a valid feature: DMA of w, z, n of the row in buffer bf
     // (issued after this wave's FTRL stores: same-wave order keeps a shared feature's update exact)
-    auto dma_lin = [&](int bf, bool handover) {
+    auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
-            // POLL (issued before the current row's FTRL stores): a feature the current row has in
-            // the same field is handed over by E instead (not in the prologue: no current row)
-            if (i >= 0 && !(POLL && handover && i == s_m[bf ^ 1][lane].x)) {
+            if (i >= 0) {
                 __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
                     __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
@@ -1053,32 +771,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
     publish_meta(0);
     bar_raw();
     dma_slots(0);
-    dma_lin(0, false);
+    dma_lin(0);
     dma_meta(1, row + G);
 
-    for (int cur = 0, first = 1; row < P.B; row += G, cur ^= 1, first = 0) {
+    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
 
         // ---- A: every DMA of this wave has landed (slots + lin of this row, meta of the
         //      next), then every wave's ----
-        if (!POLL || first) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
-        } else {
-            // the DMA'd meta of row + G (wave W_DMA) and linear state of row (wave W_LIN)
-            if (wave == W_DMA && more && lane < F) {
-                bool ok = lds_poll4(&s_mr[nxt][0][lane], LDS_EMPTY_I);
-                if (fld) ok = ok && lds_poll4(&s_mr[nxt][1][lane], LDS_EMPTY_I);
-                if (val) ok = ok && lds_poll4(&s_mr[nxt][2][lane], LDS_EMPTY);
-                if (!ok) __builtin_amdgcn_s_waitcnt(0x0F70);
-            }
-            if (wave == W_LIN && P.use_linear && lane < F && s_m[cur][lane].x >= 0) {
-                bool ok = lds_poll4(&s_lin[cur][0][lane], LDS_EMPTY);
-                ok = ok && lds_poll4(&s_lin[cur][1][lane], LDS_EMPTY);
-                ok = ok && lds_poll4(&s_lin[cur][2][lane], LDS_EMPTY);
-                if (!ok) __builtin_amdgcn_s_waitcnt(0x0F70);
-            }
-        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
         bar_raw();
         // ---- B: raw -> registers, V -> transposed image; meta(row + G) -> s_m[nxt] ----
         uint4 q[NS];
@@ -1090,39 +792,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                 qv[j] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
                 qg[j] = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
             }
-        } else if constexpr (POLL) {
-            // this thread's own slot DMAs (issued by its wave): poll until every word has replaced
-            // its mark; past POLL_MAX wait for the DMA itself
-            for (int it = 0;; ++it) {
-                if (it == POLL_MAX) __builtin_amdgcn_s_waitcnt(0x0F70);
-                lds_read16xN<NS>(q, &s_raw[tid]);
-                bool ok = first || it == POLL_MAX;
-                if (!ok) {
-                    ok = true;
 #pragma unroll
-                    for (int j = 0; j < NS; ++j) ok = ok && slot_landed(q[j]);
-                }
-                if (ok) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            lds_mark16xN<NS>(&s_raw[tid], LDS_EMPTY);
+            for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = qv[j];
         } else {
 #pragma unroll
             for (int j = 0; j < NS; ++j) q[j] = s_raw[j * 256 + tid];
-        }
-        if constexpr (!BF) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = qv[j];
-        } else if constexpr (POLL) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) lds_write8(&s_t[SB(j) * F + SA(j)], make_uint2(q[j].x, q[j].y));
-        } else {
 #pragma unroll
             for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = make_uint2(q[j].x, q[j].y);
         }
         uint32_t off[NS];
         float xab[NS];
-        uint32_t live = 0u, wr = 0u, ho = 0u;
+        uint32_t live = 0u, wr = 0u;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const uint32_t k = slot(cur, j, off[j], xab[j]);
@@ -1133,26 +813,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
         bar_raw();
         // ---- C: next row's slot DMA, then the raw meta of the row after it ----
         if (more) {
-            if constexpr (POLL) {
-                // a slot the next row shares with this one (same feature, same field: same
-                // address, same thread) is not DMA'd; E hands it the updated value instead
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    uint32_t o2;
-                    float x2;
-                    slot(nxt, j, o2, x2);
-                    if ((wr >> j & 1u) && o2 == off[j]) {
-                        ho |= 1u << j;
-                    } else if (!LATE) {
-                        __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + o2),
-                                                         (lds_ptr_t)(s_raw + j * 256 + wave * 64), 16, 0, 0);
-                    }
-                }
-            } else {
-                dma_slots(nxt);
-            }
+            dma_slots(nxt);
             dma_meta(cur, row + 2 * G);    // s_mr[cur] was consumed at this row's B
-            if (POLL) dma_lin(nxt, true);        // before this row's stores (see POLL above)
         }
         const float scale = s_red[4 + cur];
         int mi = -1;
@@ -1161,10 +823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
             const int4 m = s_m[cur][lane];
             mi = m.x;
             mx = __int_as_float(m.z);
-            if (POLL)
-                lw = (mi < 0 || !P.use_linear) ? 0.f : __int_as_float(lds_read4(&s_lin[cur][0][lane]));
-            else
-                lw = s_lin[cur][0][lane];
+            lw = s_lin[cur][0][lane];
         }
         // ---- D: forward ----
         float part = 0.f;
@@ -1241,7 +900,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                                             pack_sr_hi(g0, rotl32(h, 4), rotl32(h, 20)),
                                             pack_sr_hi(g1, rotl32(h, 12), rotl32(h, 28)));
                 if (wr >> j & 1u) *reinterpret_cast<uint4*>(vg + off[j]) = st;
-                if (POLL && (ho >> j & 1u)) lds_write16(&s_raw[j * 256 + tid], u32x4_t{st.x, st.y, st.z, st.w});
             }
             if (mi >= 0) {
                 // the feature block's pad slots (never read): zeros, completing its last line
@@ -1250,59 +908,291 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                     if (!BF) *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * SLOT_B + 16u) = make_uint4(0u, 0u, 0u, 0u);
                 }
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                    float lz, ln;
-                    if (POLL) {
-                        lz = __int_as_float(lds_read4(&s_lin[cur][1][lane]));
-                        ln = __int_as_float(lds_read4(&s_lin[cur][2][lane]));
-                    } else {
-                        lz = s_lin[cur][1][lane];
-                        ln = s_lin[cur][2][lane];
-                    }
+                    const float lz = s_lin[cur][1][lane];
+                    const float ln = s_lin[cur][2][lane];
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    const float w1 = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                     wz[mi] = z1;
                     wn[mi] = n1;
-                    w[mi] = w1;
-                    if (POLL && more && s_m[nxt][lane].x == mi) {
-                        // the next row's DMA skipped this lane (same feature): hand it the result
-                        lds_write4(&s_lin[nxt][0][lane], __float_as_uint(w1));
-                        lds_write4(&s_lin[nxt][1][lane], __float_as_uint(z1));
-                        lds_write4(&s_lin[nxt][2][lane], __float_as_uint(n1));
-                    }
+                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
-        if (POLL && wave == W_LIN && lane < F) {   // s_lin[cur] consumed: mark empty
-            lds_write4(&s_lin[cur][0][lane], LDS_EMPTY);
-            lds_write4(&s_lin[cur][1][lane], LDS_EMPTY);
-            lds_write4(&s_lin[cur][2][lane], LDS_EMPTY);
-        }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
-        if (!POLL && more) dma_lin(nxt, false);
-        if (LATE && more) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                if (!(ho >> j & 1u)) {
-                    uint32_t o2;
-                    float x2;
-                    slot(nxt, j, o2, x2);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(vg + o2),
-                                                     (lds_ptr_t)(s_raw + j * 256 + wave * 64), 16, 0, 0);
-                }
-            }
-        }
+        if (more) dma_lin(nxt);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
 #undef SA
 #undef SB
 }
 
-int default_blocks(int B, int grid);
 
-// Lean dispatch (Kp == 4, packed, table < 4 GiB, F*F <= 2048); -1 when the shape needs another kernel.
+// ---------------------------------------------------------------------------------------------
+// Per-slot-AdaGrad pipelined kernel (the GPU default; K <= 4, F <= 45): one fp32 accumulator per
+// (feature, field) slot, as Hivemall's AdaGradEntry keeps one sum of squared gradients per FFM
+// entry, shared by the k factors (docs/compat.md "FFM AdaGrad").  V is fp32
+// (Hivemall's precision) or bf16 with stochastic rounding (VBF).
+//
+// Table (ops/ffm.py slot_block_layout): per feature one line-padded block
+//   [ V: FS slots x VSB bytes | G: FS x fp32 | zero tail ]     fp32 V: 640 + 160 (+96) = 896 B
+//                                                              bf16 V: 320 + 160 (+32) = 512 B
+// so a row moves 39 blocks: 35 KB read + 35 KB written with fp32 V (the per-element fp32 V|G
+// layout moves 50 + 50 KB), 20 + 20 KB with bf16 V (per-element bf16: 25 + 25 KB).  The FFM row
+// loop is bound by this scattered gather + write-back (profiles/ffm_r2/roofline_probe_e.log), so
+// bytes per row set the rate.
+//
+// Pipeline: the next row's V and G are loaded into REGISTERS (5 VGPRs per fp32 slot, 3 per bf16
+// slot) right after the current row's image is published, so their latency hides behind the
+// current row's forward pass and update; no LDS landing zone is needed, only the transposed V
+// image of the current row (partner reads) and two metadata buffers:
+//   top  cur V/G := the prefetched registers (the waitcnt lands here); own V -> T[b*F + a];
+//        publish meta(r+G) (held in registers since the previous iteration) and its L2 scale;
+//        barrier
+//   C    prefetch V/G of r+G (offsets from meta(r+G)); load the raw meta of r+2G (registers)
+//   D    forward(r) from registers + T, block sum (barrier)
+//   E    AdaGrad(V) with the slot accumulator, FTRL(w); stores; then the linear state of r+G
+//        is loaded (after E's FTRL stores: a feature shared by consecutive rows of the block is
+//        updated in sequence, same lane, same address); barrier (T reuse)
+template <int NS, bool VBF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3))) void ffm_sg_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
+    float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    constexpr uint32_t VSB = VBF ? 8u : 16u;                          // V bytes per slot
+    using Img = typename std::conditional<VBF, uint2, float4>::type;
+    __shared__ __attribute__((aligned(16))) Img s_t[NS * 256];       // transposed V image
+    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];         // meta {i, f, x} of 2 rows
+    __shared__ float s_red[8];                                       // [0..3] sums, [4+b] scale
+    const int F = P.F;
+    const int FF = F * F;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr int W_META = 1, W_LIN = 2;
+    const uint32_t vfs = (uint32_t)P.fstride * VSB;                  // V bytes between features
+    const uint32_t gfs = (uint32_t)P.gstride * 4u;                   // G bytes between features
+    const int G = gridDim.x;
+    char* vb = reinterpret_cast<char*>(Vt);
+    char* gb = reinterpret_cast<char*>(Gt);
+
+    int ab[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
+    }
+#define SA(j) (ab[j] & 0xFF)
+#define SB(j) (ab[j] >> 8)
+    const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
+
+    // raw meta of one row -> registers (wave W_META, lanes < F)
+    int rmi = -1, rmf = 0;
+    float rmx = 0.f;
+    auto load_meta = [&](int row) {
+        if (wave == W_META && lane < F && row < P.B) {
+            const size_t o = (size_t)row * F + lane;
+            rmi = idx[o];
+            rmf = fld ? fld[o] : lane;
+            rmx = val ? val[o] : 1.f;
+        }
+    };
+    // validated meta -> s_m[bf] + the row's L2-norm scale (wave W_META)
+    auto publish_meta = [&](int bf) {
+        if (wave == W_META) {
+            float sq = 0.f;
+            if (lane < F) {
+                int i = rmi, f = rmf;
+                float x = rmx;
+                if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; f = 0; }
+                s_m[bf][lane] = make_int4(i, f, __float_as_int(x), 0);
+                sq = x * x;
+            }
+            const float tot = hm::wave_sum_uniform(sq);
+            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+        }
+    };
+    // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal
+    // (written back unchanged: whole lines), 0 = dead
+    auto slot = [&](int bf, int j, uint32_t& ov, uint32_t& og, float& xab) -> uint32_t {
+        const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
+        const bool live = ok && SA(j) != SB(j);
+        const uint32_t i = ok ? (uint32_t)ma.x : 0u, f = ok ? (uint32_t)mb.y : 0u;
+        ov = i * vfs + f * VSB;
+        og = i * gfs + f * 4u;
+        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+        return live ? 1u : (ok ? 2u : 0u);
+    };
+    Img nv[NS];
+    float ng[NS];
+    auto prefetch = [&](int bf) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t ov, og;
+            float xab;
+            slot(bf, j, ov, og, xab);
+            nv[j] = *reinterpret_cast<const Img*>(vb + ov);
+            ng[j] = *reinterpret_cast<const float*>(gb + og);
+        }
+    };
+    // linear state (w, z, n) of this lane's feature in the row of s_m[bf] (wave W_LIN)
+    float lw = 0.f, lz = 0.f, ln = 0.f;
+    auto load_lin = [&](int bf) {
+        if (P.use_linear && wave == W_LIN && lane < F) {
+            const int i = s_m[bf][lane].x;
+            if (i >= 0) {
+                lw = w[i];
+                if (P.train) { lz = wz[i]; ln = wn[i]; }
+            } else {
+                lw = lz = ln = 0.f;
+            }
+        }
+    };
+
+    int row = blockIdx.x;
+    if (row >= P.B) return;
+    // ---- prologue: meta(row) -> s_m[0]; prefetch its slots and linear state; meta(row + G) ----
+    load_meta(row);
+    publish_meta(0);
+    bar_raw();
+    prefetch(0);
+    load_lin(0);
+    load_meta(row + G);
+
+    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
+        const int nxt = cur ^ 1;
+        const bool more = row + G < P.B;
+        // ---- top: the prefetched slots become the current row's; own V -> transposed image ----
+        Img cv[NS];
+        float cg[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) { cv[j] = nv[j]; cg[j] = ng[j]; }
+#pragma unroll
+        for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = cv[j];
+        if (more) publish_meta(nxt);
+        bar_raw();
+        // ---- C: prefetch the next row; raw meta of the row after it ----
+        if (more) {
+            prefetch(nxt);
+            load_meta(row + 2 * G);
+        }
+        const float scale = s_red[4 + cur];
+        int mi = -1;
+        float mx = 0.f;
+        if (wave == W_LIN && lane < F) {
+            const int4 m = s_m[cur][lane];
+            mi = m.x;
+            mx = __int_as_float(m.z);
+        }
+        // ---- D: forward ----
+        uint32_t live = 0u, wr = 0u;
+        float xab[NS];
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t ov, og;
+            const uint32_t k = slot(cur, j, ov, og, xab[j]);
+            live |= (k & 1u) << j;
+            wr |= (uint32_t)(k != 0u) << j;
+            const int s = tid + j * 256;
+            const Img pv = s_t[s < FF ? s : 0];
+            float d;
+            if constexpr (VBF) d = dot2_bf16(cv[j].x, pv.x, dot2_bf16(cv[j].y, pv.y, 0.f));
+            else d = cv[j].x * pv.x + cv[j].y * pv.y + cv[j].z * pv.z + cv[j].w * pv.w;
+            part += d * xab[j];
+        }
+        part *= 0.5f * scale * scale;
+        part += lw * mx * scale;
+        part = hm::wave_sum_uniform(part);
+        if (lane == 0) s_red[wave] = part;
+        bar_raw();
+        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        if (P.use_bias) p += bias_w0(P, bias);
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- E: updates ----
+        if (P.train) {
+            const float ks = kappa * scale * scale;
+            uint32_t hrow = (P.seed ^ ((uint32_t)row * 0x85EBCA77u)) + tid_h;
+            hrow ^= hrow >> 16;
+            hrow *= 0x7FEB352Du;
+            hrow ^= hrow >> 15;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (!(wr >> j & 1u)) continue;
+                uint32_t ov, og;
+                float xj;
+                slot(cur, j, ov, og, xj);
+                const int s = tid + j * 256;
+                const Img pv = s_t[s];
+                const float c = ks * xab[j];
+                // diagonal slots: c = 0 and lambda = 0 -> zero gradient, V and G unchanged (the
+                // stochastic rounding of a value already in bf16 is exact)
+                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
+                f2 o0, o1, p0, p1;
+                if constexpr (VBF) {
+                    o0 = bf2_to_f2(cv[j].x); o1 = bf2_to_f2(cv[j].y);
+                    p0 = bf2_to_f2(pv.x);    p1 = bf2_to_f2(pv.y);
+                } else {
+                    o0 = f2{cv[j].x, cv[j].y}; o1 = f2{cv[j].z, cv[j].w};
+                    p0 = f2{pv.x, pv.y};       p1 = f2{pv.z, pv.w};
+                }
+                const f2 cc = {c, c}, ll = {lj, lj};
+                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
+                // G += g0^2 + g1^2 + g2^2 + g3^2 (factor order, as the CPU engine)
+                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
+                const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
+                const f2 rr = {r, r};
+                o0 = o0 + rr * d0;
+                o1 = o1 + rr * d1;
+                if constexpr (VBF) {
+                    const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
+                    *reinterpret_cast<uint2*>(vb + ov) = make_uint2(pack_sr_hi(o0, h, rotl32(h, 16)),
+                                                                    pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)));
+                } else {
+                    *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                }
+                *reinterpret_cast<float*>(gb + og) = gs;
+            }
+            if (mi >= 0) {
+                // the feature block's pad slots and tail (never read): zeros, completing its lines
+                char* vblk = vb + (uint32_t)mi * vfs;
+                char* gblk = gb + (uint32_t)mi * gfs;
+                for (int f = P.num_fields; f < P.vpad; ++f) {
+                    if constexpr (VBF) *reinterpret_cast<uint2*>(vblk + f * VSB) = make_uint2(0u, 0u);
+                    else *reinterpret_cast<uint4*>(vblk + f * VSB) = make_uint4(0u, 0u, 0u, 0u);
+                    *reinterpret_cast<float*>(gblk + f * 4) = 0.f;
+                }
+                for (int t = 0; t < P.tail16; ++t)
+                    *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * t) = make_uint4(0u, 0u, 0u, 0u);
+                if (P.use_linear) {   // FTRL-proximal on the prefetched (w, z, n)
+                    const float g = kappa * mx * scale;
+                    const float n1 = ln + g * g;
+                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                    wz[mi] = z1;
+                    wn[mi] = n1;
+                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                }
+            }
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
+        }
+        // linear state of the next row, after this row's FTRL stores (same lane, same field)
+        if (more) load_lin(nxt);
+        bar_raw();   // T and s_m[cur] are rewritten by the next iterations
+    }
+#undef SA
+#undef SB
+}
+
+
+int default_blocks(int B, int grid) {
+    return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
+}
+
+// Per-element pipelined / lean dispatch (Kp == 4, packed, table < 4 GiB, F*F <= 2048); -1 when
+// the shape needs the generic kernel.
 template <bool BF>
 int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
@@ -1315,39 +1205,19 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-    if constexpr (BF) {
-        if (variant == 0 || variant >= 3) {   // LDS-DMA pipelined kernel (static LDS)
-            const int pm = !P.train ? 0 : variant == 5 ? 1 : variant == 4 ? 2 : 0;
-#define HM_PIPE(NSV)                                                                                     \
-    if (pm == 1) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, 1>), dim3(blocks), dim3(256), 0, stream, P, idx, fld, \
-                                    val, y, VG, w, wz, wn, bias, pred, loss);                               \
-    else if (pm == 2) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, 2>), dim3(blocks), dim3(256), 0, stream, P, idx, \
-                                         fld, val, y, VG, w, wz, wn, bias, pred, loss);                     \
-    else hipLaunchKernelGGL((ffm_pipe_kernel<NSV, 0>), dim3(blocks), dim3(256), 0, stream, P, idx, fld,     \
-                            val, y, VG, w, wz, wn, bias, pred, loss)
-            if (need <= 2) { HM_PIPE(2); }
-            else if (need <= 4) { HM_PIPE(4); }
-            else if (need <= 6) { HM_PIPE(6); }
-            else { HM_PIPE(8); }
+    // bf16: the LDS-DMA pipeline unless variant 2; fp32: the lean kernel unless variant 3
+    // (measured same-box, profiles/ffm_r2/fp32_pipe_ab.log: 52.5 M rows/s vs 51.2 M (+2.6 %),
+    // while the pipeline's extra row of staleness cost held-out logloss at 500 K rows: +0.019 vs
+    // sequential, lean +0.010)
+    if ((BF && variant != 2) || (!BF && variant == 3)) {
+#define HM_PIPE(NSV) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, BF>), dim3(blocks), dim3(256), 0, stream, P, idx, \
+                                        fld, val, y, VG, w, wz, wn, bias, pred, loss)
+        if (need <= 2) { HM_PIPE(2); }
+        else if (need <= 4) { HM_PIPE(4); }
+        else if (need <= 6) { HM_PIPE(6); }
+        else { HM_PIPE(8); }
 #undef HM_PIPE
-            HM_LAUNCH_RET();
-        }
-    } else {
-        // fp32 state: the same pipeline over 32-B slots, opt-in (variant 3).  Measured same-box
-        // (profiles/ffm_r2/fp32_pipe_ab.log): 52.5 M rows/s vs the lean kernel's 51.2 M (+2.6 %)
-        // — both move ~4.9 TB/s of slot traffic, the rate the bf16 pipeline reaches too — while
-        // its extra row of staleness costs held-out logloss at small row counts (500 K rows:
-        // +0.019 vs sequential, lean +0.010), so the lean kernel stays the fp32 default.
-        if (variant == 3) {
-#define HM_PIPE32(NSV) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, 0, false>), dim3(blocks), dim3(256), 0, stream, P, idx, \
-                                          fld, val, y, VG, w, wz, wn, bias, pred, loss)
-            if (need <= 2) { HM_PIPE32(2); }
-            else if (need <= 4) { HM_PIPE32(4); }
-            else if (need <= 6) { HM_PIPE32(6); }
-            else { HM_PIPE32(8); }
-#undef HM_PIPE32
-            HM_LAUNCH_RET();
-        }
+        HM_LAUNCH_RET();
     }
 #define HM_LEAN(NSV)                                                                                \
     hipLaunchKernelGGL((ffm_lean_kernel<BF, NSV>), dim3(blocks), dim3(256), sh, stream, P, idx, fld, \
@@ -1360,52 +1230,29 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
-int default_blocks(int B, int grid) {
-    return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
-}
-
-// Occupancy: the NS loops are fully unrolled so every owned slot's load is in flight at once;
-// that costs 110-127 VGPRs (4 waves/SIMD).  Capping the registers for 6 waves/SIMD spilled
-// (124-192 B/lane of scratch) and ran 22-44 % slower (profiles/ffm_layout_ab_r1.log); a cap for
-// 5 waves/SIMD still spills (36-104 B/lane).
-template <int KC, bool BF, int NS, bool RELOAD>
-int launch_packed_w(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-                    const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
-                    float* pred, float* loss, int blocks, size_t shmem, hipStream_t stream) {
-    hipLaunchKernelGGL((ffm_packed_kernel<KC, BF, NS, RELOAD>), dim3(blocks), dim3(256), shmem, stream,
-                       P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss);
-    HM_LAUNCH_RET();
-}
-
-template <int KC, bool BF, int NS>
-int launch_packed(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
-                  float* pred, float* loss, int blocks, size_t shmem, hipStream_t stream) {
-    if (P.reload)
-        return launch_packed_w<KC, BF, NS, true>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, shmem, stream);
-    return launch_packed_w<KC, BF, NS, false>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, shmem, stream);
-}
-
-// Packed dispatch; returns -1 when the shape needs the generic kernel instead.
-template <int KC, bool BF>
-int dispatch_packed(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-                    const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
-                    float* pred, float* loss, int grid, hipStream_t stream) {
-    const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
-    const size_t stage = (size_t)P.F * P.F * KC * (BF ? 8 : 16);
-    if (stage + meta > 64 * 1024) return -1;
+// Per-slot-G pipelined dispatch (Kp == 4, F <= 45, block layout, table < 4 GiB); -1 otherwise.
+template <bool BF>
+int dispatch_sg(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
+                float* pred, float* loss, int grid, hipStream_t stream) {
+    if (P.Kp != 4 || P.F > 45 || P.vpad <= 0) return -1;
+    const size_t vsb = BF ? 8 : 16;
+    if ((size_t)P.num_features * (size_t)P.fstride * vsb >= ((size_t)1 << 32)) return -1;
+    if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-    const size_t sh = stage + meta;
-    if (need <= 2) return launch_packed<KC, BF, 2>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
-    if (need <= 4) return launch_packed<KC, BF, 4>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
-    if (need <= 6) return launch_packed<KC, BF, 6>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
-    if (need <= 8) return launch_packed<KC, BF, 8>(P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss, blocks, sh, stream);
-    return -1;
+#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF>), dim3(blocks), dim3(256), 0, stream, P, idx, fld, \
+                                      val, y, V, G, w, wz, wn, bias, pred, loss)
+    if (need <= 2) { HM_SG(2); }
+    else if (need <= 4) { HM_SG(4); }
+    else if (need <= 6) { HM_SG(6); }
+    else { HM_SG(8); }
+#undef HM_SG
+    HM_LAUNCH_RET();
 }
 
-template <int KC, bool BF>
+template <int KC, bool BF, bool SG>
 int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
                float* pred, float* loss, int grid, hipStream_t stream) {
@@ -1415,51 +1262,64 @@ int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
     if (use_stage) {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF>), dim3(blocks), dim3(256), stage + meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, true, BF, SG>), dim3(blocks), dim3(256), stage + meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     } else {
-        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF>), dim3(blocks), dim3(256), meta, stream,
+        hipLaunchKernelGGL((ffm_row_kernel<KC, false, BF, SG>), dim3(blocks), dim3(256), meta, stream,
                            P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
     }
     HM_LAUNCH_RET();
 }
 
+template <bool BF, bool SG>
+int launch_generic(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                   const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
+                   float* pred, float* loss, int grid, hipStream_t stream) {
+    switch (P.Kp / 4) {
+        case 1: return launch_ffm<1, BF, SG>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 2: return launch_ffm<2, BF, SG>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 3: return launch_ffm<3, BF, SG>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 4: return launch_ffm<4, BF, SG>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        case 8: return launch_ffm<8, BF, SG>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
 template <bool BF>
 int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
-             float* pred, float* loss, int grid, int packed, int variant, hipStream_t stream) {
-    if (packed) {
-        int rc = -1;
+             float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream) {
+    if (slot_g) {
         if (variant != 1) {
-            rc = dispatch_lean<BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
+            const int rc = dispatch_sg<BF>(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
+                                           bias, pred, loss, grid, stream);
             if (rc != -1) return rc;
         }
-        if (P.Kp == 4) rc = dispatch_packed<1, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
-        else if (P.Kp == 8) rc = dispatch_packed<2, BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+        return launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+    }
+    if (packed && variant != 1) {
+        const int rc = dispatch_lean<BF>(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
         if (rc != -1) return rc;
         // other shapes: the generic kernel handles the packed strides too (G = V + Kp)
     }
-    switch (P.Kp / 4) {
-        case 1: return launch_ffm<1, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 2: return launch_ffm<2, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 3: return launch_ffm<3, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 4: return launch_ffm<4, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        case 8: return launch_ffm<8, BF>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
-        default: return (int)hipErrorInvalidValue;
-    }
+    return launch_generic<BF, false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
 }
 
 }  // namespace
 
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
-//                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride
-// variant (Kp == 4, packed, F <= 45, table < 4 GiB): 0 = auto (bf16: ffm_pipe_kernel with
-// vmcnt(0) waits; fp32: ffm_lean_kernel), 1 = ffm_packed_kernel (round 1), 2 = ffm_lean_kernel,
-// 3 = ffm_pipe_kernel (vmcnt; bf16 or fp32 state), 4 / 5 = ffm_pipe_kernel polling its DMA targets with the next
-// row's slot DMA issued after / before this row's stores (training only; no faster, see PM above)
-// packed = 1: V and G are the two halves of one [num_features][num_fields][2][Kp] table
-//             (G == V + Kp elements, slot stride 2*Kp); 0: separate [.][.][Kp] tables.
+//                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
+//                     slot_g, gstride, vpad, tail16
+// slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f]; with the
+//             block layout (G = V + vpad * slot bytes, vpad > 0) the pipelined ffm_sg_kernel runs
+//             (K <= 4, F <= 45), else the generic kernel.  tail16 = zero 16-B chunks after each
+//             feature's G region (line completion).
+// slot_g = 0 (per-element G shaped like V): packed = 1: V and G are the two halves of one
+//             [num_features][fstride][2][Kp] table (G == V + Kp elements, slot stride 2*Kp); 0:
+//             separate [.][.][Kp] tables.
+// variant: 0 = auto (per-slot: ffm_sg_kernel; per-element bf16: ffm_pipe_kernel, fp32:
+// ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel, 3 = ffm_pipe_kernel.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -1475,11 +1335,24 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     const int variant = ip[15];
     P.sstride = packed ? 2 * P.Kp : P.Kp;
     P.fstride = ip[16] > 0 ? ip[16] : P.num_fields;
+    const int slot_g = ip[17];
+    P.gstride = ip[18];
+    P.vpad = ip[19];
+    P.tail16 = ip[20];
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
-    if (packed) {
+    if (slot_g) {
+        if (packed || P.gstride < P.num_fields || P.tail16 < 0) return (int)hipErrorInvalidValue;
+        if (P.vpad > 0) {
+            // block layout: G right after the V region of the same feature block
+            const size_t es = bf16 ? 2 : 4;
+            if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.vpad * P.Kp * es ||
+                (size_t)P.fstride * P.Kp * es != (size_t)P.gstride * 4 || P.vpad < P.num_fields)
+                return (int)hipErrorInvalidValue;
+        }
+    } else if (packed) {
         // G must be the second half of every packed slot
         const size_t es = bf16 ? 2 : 4;
         if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.Kp * es)
@@ -1487,6 +1360,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
         // 32-bit slot indices in the packed kernel
         if ((size_t)P.num_features * (size_t)P.fstride >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
     }
-    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, variant, stream)
-                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, variant, stream);
+    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream)
+                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream);
 }

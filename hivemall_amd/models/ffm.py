@@ -82,6 +82,8 @@ class FFMTrainer(Learner):
         flag("no_norm", "disable_norm", "Disable instance-wise L2 normalization"),
         flag("bf16_state", None, "[engine] keep V and the AdaGrad state in bf16 on the GPU "
                                  "(stochastic rounding); halves the HBM traffic"),
+        flag("elementwise_adagrad", None, "[engine] one AdaGrad accumulator per V element "
+                                          "instead of one per (feature, field) slot"),
         flag("split_state", None, "[engine] separate V and G tables on the GPU instead of the "
                                   "packed V|G slot layout (A/B)"),
         opt("feature_hashing", None, -1, int, "Hash feature indices into 2^bits"),
@@ -130,7 +132,8 @@ class FFMTrainer(Learner):
         sdt = torch.bfloat16 if (self.cl["bf16_state"] and dev.type == "cuda") else torch.float32
         # packed V|G slots on the GPU (csrc/kernels/ffm.hip); split tables on the CPU engine
         V, G = new_state_tables(self.num_features, self.num_fields, self.kp, sdt, dev,
-                                packed=dev.type == "cuda" and not self.cl["split_state"])
+                                packed=dev.type == "cuda" and not self.cl["split_state"],
+                                slot_g=not self.cl["elementwise_adagrad"])
         if self.cl["init_v"] == "gaussian":
             init = lambda n: torch.randn(n, generator=g) * self.cl["sigma"]
         else:
@@ -303,16 +306,36 @@ class FFMTrainer(Learner):
         self.touched = torch.ones(nf, dtype=torch.bool, device=self.device)
 
     def pack_state(self) -> None:
-        """Move split V/G tables into the packed GPU layout (after a load)."""
+        """Bring loaded V/G tables into this trainer's layout: the AdaGrad accumulator form
+        (per slot: a per-element G is summed over the factors — the per-slot accumulator IS the
+        sum of the squared gradients of the slot's k factors; per element: a per-slot G is
+        spread evenly) and, on the GPU, the packed / block layout."""
         st = self.state
-        if (st is None or self.device.type != "cuda" or self.cl["split_state"]
-                or is_packed(st["V"], st["G"])):
+        if st is None:
             return
-        NF, NFLD, kp = st["V"].shape
-        V, G = new_state_tables(NF, NFLD, kp, st["V"].dtype, st["V"].device, packed=True)
-        V.copy_(st["V"])
-        G.copy_(st["G"])
-        st["V"], st["G"] = V, G
+        slot_g = not self.cl["elementwise_adagrad"]
+        V, G = st["V"], st["G"]
+        if slot_g and G.dim() == 3:
+            G = G.to(torch.float32).sum(-1)
+        elif not slot_g and G.dim() == 2:
+            G = (G / self.kp).unsqueeze(-1).expand(*G.shape, self.kp).to(V.dtype)
+        packed = self.device.type == "cuda" and not self.cl["split_state"]
+        if slot_g and G is st["G"] and (not packed or _is_block(V, G)):
+            return
+        if not slot_g and G is st["G"] and (not packed or is_packed(V, G)):
+            return
+        NF, NFLD, kp = V.shape
+        V2, G2 = new_state_tables(NF, NFLD, kp, V.dtype, V.device, packed=packed, slot_g=slot_g)
+        V2.copy_(V)
+        G2.copy_(G)
+        st["V"], st["G"] = V2, G2
+
+
+def _is_block(V: torch.Tensor, G: torch.Tensor) -> bool:
+    """Per-slot G laid out in V's feature blocks (ops.ffm.slot_block_layout)."""
+    es = V.element_size()
+    return (G.dim() == 2 and V.is_cuda and 0 < G.data_ptr() - V.data_ptr() < V.stride(0) * es
+            and G.stride(0) * 4 == V.stride(0) * es)
 
 
 def train_ffm(features, labels, options: str | None = None, device=None, **kw) -> pd.DataFrame:

@@ -75,10 +75,40 @@ def padded_fields(num_fields: int, kp: int, dtype) -> int:
     return (num_fields + per_line - 1) // per_line * per_line
 
 
+def slot_block_layout(num_fields: int, kp: int, dtype) -> tuple[int, int, int]:
+    """Per-slot-G block layout of one feature (GPU): ``[V: FS x Kp (dtype) | G: FS x fp32]``
+    padded to whole 128-B lines.  Returns (FS, block bytes, G byte offset); FS is the field
+    count padded so the V region is whole lines (fp32 k=4: 40 slots = 640 B, G 160 B, block
+    896 B = 7 lines; bf16: 320 B + 160 B -> 512 B = 4 lines)."""
+    es = torch.empty(0, dtype=dtype).element_size()
+    vsb = kp * es
+    per_line = max(1, 128 // vsb) if 128 % vsb == 0 else 1
+    fs = (num_fields + per_line - 1) // per_line * per_line
+    goff = fs * vsb
+    bs = (goff + fs * 4 + 127) // 128 * 128
+    return fs, bs, goff
+
+
 def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
-                     packed: bool) -> tuple[torch.Tensor, torch.Tensor]:
-    """Zeroed (V, G): views of one packed [NF, FS, 2, Kp] table (FS = line-padded field count),
-    or two split tables."""
+                     packed: bool, slot_g: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    """Zeroed (V, G).
+
+    ``slot_g`` (one AdaGrad accumulator per (feature, field) slot, G is [NF, NFLD] fp32):
+    ``packed`` -> views of one byte table whose feature blocks hold V then G
+    (:func:`slot_block_layout`); else a contiguous V [NF, NFLD, Kp] and G [NF, NFLD].
+    Per-element G (G shaped like V): views of one packed [NF, FS, 2, Kp] table (FS =
+    line-padded field count), or two split tables."""
+    if slot_g:
+        if packed:
+            fs, bs, goff = slot_block_layout(num_fields, kp, dtype)
+            es = torch.empty(0, dtype=dtype).element_size()
+            buf = torch.zeros((num_features, bs), dtype=torch.uint8, device=device)
+            V = buf[:, :goff].view(dtype).view(num_features, fs, kp)[:, :num_fields]
+            G = buf[:, goff:goff + fs * 4].view(torch.float32)[:, :num_fields]
+            assert V.stride(0) * es == bs and G.stride(0) * 4 == bs
+            return V, G
+        return (torch.zeros((num_features, num_fields, kp), dtype=dtype, device=device),
+                torch.zeros((num_features, num_fields), dtype=torch.float32, device=device))
     if packed:
         fs = padded_fields(num_fields, kp, dtype)
         VG = torch.zeros((num_features, fs, 2, kp), dtype=dtype, device=device)
@@ -118,11 +148,31 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
         assert loss.shape[0] >= B
     G = state["G"]
     bf16 = V.dtype == torch.bfloat16
-    assert G.dtype == V.dtype, "V and G must share the storage dtype"
-    packed = is_packed(V, G)
-    if not packed:
-        assert V.is_contiguous() and G.is_contiguous(), \
-            "FFM state: two contiguous V/G tables or the halves of one packed table"
+    slot_g = G.dim() == 2
+    gstride = 0
+    block = (0, 0)
+    if slot_g:
+        # one fp32 AdaGrad accumulator per (feature, field) slot: G [NF, NFLD]
+        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) == 1, \
+            "per-slot G: fp32 [num_features, num_fields] with unit field stride"
+        assert V.stride(2) == 1 and V.stride(1) == Kp, "V: [NF, FS, Kp] slots"
+        packed = False
+        gstride = G.stride(0)
+        # block layout (slot_block_layout): G right after the V region of each feature block
+        es = V.element_size()
+        d = G.data_ptr() - V.data_ptr()
+        bs = V.stride(0) * es
+        if V.is_cuda and 0 < d < bs and d % (Kp * es) == 0 and G.stride(0) * 4 == bs:
+            vpad = d // (Kp * es)
+            tail = bs - d - vpad * 4
+            if tail >= 0 and tail % 16 == 0:
+                block = (vpad, tail // 16)
+    else:
+        assert G.dtype == V.dtype, "V and G must share the storage dtype"
+        packed = is_packed(V, G)
+        if not packed:
+            assert V.is_contiguous() and G.is_contiguous(), \
+                "FFM state: two contiguous V/G tables or the halves of one packed table"
     assert not bf16 or V.is_cuda, "bf16 FFM state is a device-only layout"
     global _CALLS
     _CALLS += 1
@@ -130,7 +180,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    int(hyper.use_bias), int(hyper.norm), int(grid),
                    int((not packed) if hyper.reload is None else hyper.reload), int(bf16),
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed), _VARIANT,
-                   field_stride(V)],
+                   field_stride(V), int(slot_g), gstride, block[0], block[1]],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr

@@ -82,6 +82,7 @@ class _FlatGroup:
         self._refs = [weakref.ref(t) for t in tensors]
         self.shapes = [tuple(t.shape) for t in tensors]
         self.busy = False            # an OverlappedMixer collective is in flight on the buffers
+        self.base: torch.Tensor | None = None   # fp32 consensus of the last mix (delta-sum mode)
         self.dtype = tensors[0].dtype
         dev = tensors[0].device
         self.offs = []
@@ -123,9 +124,34 @@ class _FlatGroup:
         for k, t in enumerate(self.tensors):
             t.copy_(self.seg(self.out, k))
 
-    def shard_mean(self, world: int) -> None:
-        """mean = fp32 sum over ranks of recv[r] / world, rounded once to the wire dtype."""
+    def pack_delta(self) -> None:
+        """send <- x - base (the local progress since the last consensus), in the wire dtype."""
+        for k, t in enumerate(self.tensors):
+            d = self.seg(self.send, k)
+            d.copy_(t.to(torch.float32) - self.seg(self.base, k))
+
+    def merge_delta(self) -> None:
+        """Delta merge: ``out`` holds the consensus step m (per element), so
+        base <- base + m (rounded to the storage dtype, identically on every rank) and x keeps
+        its progress since the snapshot: x <- x + m - delta_local."""
+        for k, t in enumerate(self.tensors):
+            m = self.seg(self.out, k).to(torch.float32)
+            b = self.seg(self.base, k)
+            b.add_(m)
+            if t.dtype != torch.float32:
+                b.copy_(b.to(t.dtype))               # exactly representable: untouched x == base
+            t.copy_(t.to(torch.float32) + (m - self.seg(self.send, k).to(torch.float32)))
+
+    def shard_mean(self, world: int, changers: bool = False) -> None:
+        """mean = fp32 sum over ranks of recv[r] / world, rounded once to the wire dtype.
+        ``changers``: divide by the number of ranks whose value is non-zero instead (the mean of
+        the deltas of the ranks that updated the element; 0 where none did)."""
         code = _dtype_code(self.dtype)
+        if changers:
+            r = self.recv.view(world, self.shard).to(torch.float32)
+            cnt = (r != 0).sum(0).clamp_min_(1).to(torch.float32)
+            self.mean.copy_(r.sum(0) / cnt)
+            return
         if self.recv.is_cuda and code is not None:
             rc = _native.hip().hm_mix_shard_mean(self.recv.data_ptr(), world, self.shard, code,
                                                  self.mean.data_ptr(),
@@ -363,11 +389,16 @@ class OverlappedMixer:
     sum is still exact fp32 (the shard mean).  Buffers: 3x the mixed bytes, allocated once.
     """
 
-    def __init__(self, mixer: ModelMixer):
+    def __init__(self, mixer: ModelMixer, mode: str = "mean", power: float = 1.0):
+        if mode not in ("mean", "sum", "touched"):
+            raise ValueError("OverlappedMixer mode: mean | sum | touched")
         self.m = mixer
+        self.mode = mode
+        self.power = power           # sum mode: consensus step = mean_r(delta_r) * world**power
         self.groups: list[_FlatGroup] | None = None
         self.works: list = []
         self.side = None
+        self._sum_now = False        # the in-flight mix is a delta-sum one
 
     def pending(self) -> bool:
         return bool(self.works)
@@ -378,8 +409,13 @@ class OverlappedMixer:
         if self.works:
             self.finish()
         self.groups = self.m.plan(tensors)
+        # delta-sum mode needs a consensus to measure deltas from: the first mix is a mean
+        self._sum_now = self.mode != "mean" and all(g.base is not None for g in self.groups)
         for g in self.groups:
-            g.pack()                                 # the snapshot (exact copy of the replica)
+            if self._sum_now:
+                g.pack_delta()                       # this rank's progress since the consensus
+            else:
+                g.pack()                             # the snapshot (exact copy of the replica)
             g.busy = True
         world = self.m.world
         if tensors[0].is_cuda:
@@ -389,16 +425,25 @@ class OverlappedMixer:
             with torch.cuda.stream(self.side):
                 for g in self.groups:
                     self.m._a2a(g, async_op=True).wait()    # side stream waits, host does not
-                    g.shard_mean(world)
+                    self._reduce(g, world)
                     self.works.append(self.m._gather(g, async_op=True))
         else:
             # gloo: the shard mean needs the all-to-all's data on the host, so the first half
             # runs synchronously; the all-gather stays in flight behind the caller's compute
             for g in self.groups:
                 self.m._a2a(g)
-                g.shard_mean(world)
+                self._reduce(g, world)
                 self.works.append(self.m._gather(g, async_op=True))
         self.m._count(self.groups, tensors)
+
+    def _reduce(self, g: _FlatGroup, world: int) -> None:
+        if not self._sum_now:
+            g.shard_mean(world)
+        elif self.mode == "touched":
+            g.shard_mean(world, changers=True)
+        else:
+            g.shard_mean(world)
+            g.mean.mul_(float(world) ** self.power)
 
     def finish(self) -> None:
         if not self.works:
@@ -407,7 +452,12 @@ class OverlappedMixer:
             w.wait()
         self.works = []
         for g in self.groups:
-            g.merge()
+            if self._sum_now:
+                g.merge_delta()
+            else:
+                g.merge()
+                if self.mode != "mean":              # the first consensus: deltas start here
+                    g.base = g.out.to(torch.float32, copy=True)
             g.busy = False
 
 

@@ -1,4 +1,7 @@
-"""Pure numpy per-row FFM oracle (restates the pinned train_ffm semantics, docs/compat.md)."""
+"""Pure numpy per-row FFM oracle (restates the pinned train_ffm semantics, docs/compat.md).
+
+G of shape [NF, NFLD] = one AdaGrad accumulator per (feature, field) slot (the default);
+[NF, NFLD, Kp] = one per V element (-elementwise_adagrad)."""
 import math
 
 import numpy as np
@@ -50,7 +53,12 @@ def ffm_train_rows(state, idx, y, hp, fld=None, val=None, train=True, cls=True, 
                     continue
                 coef = kappa * sc * sc * xx[a] * xx[b]
                 g = coef * snap[(b, a)] + hp["lambda_v"] * snap[(a, b)]
-                G[ii[a], ff[b]] += g * g
+                if G.ndim == 2:
+                    # one accumulator per (feature, field) slot: the squared gradients of its
+                    # k factors are added, then every factor steps with the new total
+                    G[ii[a], ff[b]] += float((g * g).sum())
+                else:
+                    G[ii[a], ff[b]] += g * g
                 V[ii[a], ff[b]] = snap[(a, b)] - hp["eta0"] * g / np.sqrt(G[ii[a], ff[b]] + hp["eps"])
         if use_lin:
             for a in range(F):
