@@ -8,6 +8,8 @@
   bprmf      : BPR-MF on MovieLens-20M-shaped implicit feedback (device negative sampling)
 
     python benchmarks/bench_configs.py [names...]      # one JSON line per config
+    python benchmarks/bench_configs.py --gpus N [gbdt|xgboost|rf|bprmf|bprmf_shard ...]
+                                                       # N ranks (one per GPU), rank 0 prints
 Synthetic data of the named shapes (no datasets offline), random-init weights.
 """
 import json
@@ -198,6 +200,160 @@ def bench_xgboost(dev="cuda", n=11_000_000, rounds=100):
             "row_rounds_per_s": round(n * rounds / dt), "test_auc": round(float(auc), 4)}
 
 
+# ------------------------------------------------------------------ N-GPU (one process per GPU)
+# BASELINE.json:10-11: RF / GBDT on HIGGS-shaped dense rows and BPR-MF on MovieLens-20M-shaped
+# implicit feedback on 8 x MI355X.  ``--gpus N`` starts N ranks (bench.py's self-launch); the
+# dataset is fixed (strong scaling): boosting shards the 11 M rows (rows r, r + N, ...) and
+# all-reduces the per-level histograms; RF keeps all rows on every rank and splits the trees;
+# BPR shards the interactions and mixes the factor tables every epoch (-mix_interval 1), or
+# row-shards the tables over the ranks (-shard_model, explicit triples).  Rank 0 prints the
+# JSON; time = max over ranks.
+
+def _ctx():
+    from hivemall_amd.parallel.dist import init_distributed
+    from hivemall_amd.parallel.mix import ModelMixer
+    ctx = init_distributed()
+    return ctx, ModelMixer(ctx)
+
+
+def _timed(ctx, mixer, fn):
+    dev = ctx.device
+    _sync(dev)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    out = fn()
+    _sync(dev)
+    ctx.barrier()
+    return out, mixer.all_reduce_scalar(time.perf_counter() - t0, "max")
+
+
+def _dist_fields(ctx):
+    return {"world": ctx.world_size, "rccl_world": ctx.world_size if ctx.backend == "nccl" else None,
+            "dist_backend": ctx.backend, "scaling": "strong"}
+
+
+def bench_gbdt_dp(n=11_000_000, trees=100, depth=8, xgb=False):
+    """Row-sharded boosting: rank r holds rows r, r + N, ... of the 11 M; histograms all-reduced."""
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import GradientTreeBoostingClassifier
+    from hivemall_amd.models.xgboost import XGBoostClassifier
+    ctx, mixer = _ctx()
+    dev = ctx.device
+    X, y = higgs_like(n, device=dev)
+    me = slice(ctx.rank, None, ctx.world_size)
+    X, y = X[me].contiguous(), y[me].contiguous()
+    kw = dict(device=dev, mixer=mixer, rank=ctx.rank)
+    if xgb:
+        XGBoostClassifier("-num_round 2 -max_depth 6", **kw).fit(X[:100000], y[:100000])
+        m, dt = _timed(ctx, mixer, lambda: XGBoostClassifier(
+            f"-num_round {trees} -max_depth {depth} -eta 0.1", **kw).fit(X, y))
+    else:
+        GradientTreeBoostingClassifier("-trees 2 -max_depth 8", **kw).fit(X[:100000], y[:100000].long())
+        m, dt = _timed(ctx, mixer, lambda: GradientTreeBoostingClassifier(
+            f"-trees {trees} -eta 0.1 -max_depth {depth} -subsample 1.0", **kw).fit(X, y.long()))
+    Xt, yt = higgs_like(500000, seed=9, device=dev)
+    auc = roc_auc_score(yt.cpu().numpy(), m.predict_proba(Xt)[:, -1])
+    name = "train_xgboost binary:logistic" if xgb else "GBT classifier"
+    return {"config": f"{name}, HIGGS-shaped {n} x 28 rows sharded over {ctx.world_size} ranks, depth {depth}, "
+                      f"{trees} trees, per-level histogram all-reduce", "device": str(dev), "seconds": round(dt, 3),
+            "ms_per_tree": round(dt * 1e3 / trees, 2), "row_trees_per_s": round(n * trees / dt),
+            "test_auc": round(float(auc), 4), **_dist_fields(ctx)}
+
+
+def bench_rf_dp(n=11_000_000, trees=48, depth=12):
+    """RandomForest: every rank all rows, trees t with t % N == rank; the union is the forest."""
+    from sklearn.metrics import roc_auc_score
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import RandomForestClassifier
+    ctx, mixer = _ctx()
+    dev = ctx.device
+    X, y = higgs_like(n, device=dev)
+    kw = dict(device=dev, mixer=mixer, rank=ctx.rank)
+    RandomForestClassifier("-trees 2 -max_depth 12", device=dev).fit(X[:100000], y[:100000].long())
+    m, dt = _timed(ctx, mixer, lambda: RandomForestClassifier(f"-trees {trees} -max_depth {depth}", **kw).fit(X, y.long()))
+    # the forest is the union of the ranks' trees (SQL: the UDTF tables are concatenated)
+    import torch.distributed as tdist
+    if ctx.world_size > 1:
+        parts = [None] * ctx.world_size
+        tdist.all_gather_object(parts, [t.to_json() for t in m.trees])
+        from hivemall_amd.models.trees import Tree
+        m.trees = [Tree.from_json(j) for part in parts for j in part]
+    Xt, yt = higgs_like(500000, seed=9, device=dev)
+    auc = roc_auc_score(yt.cpu().numpy(), m.predict_proba(Xt)[:, 1])
+    return {"config": f"RandomForest classifier, HIGGS-shaped {n} x 28, depth {depth}, {trees} trees split over "
+                      f"{ctx.world_size} ranks", "device": str(dev), "seconds": round(dt, 3),
+            "ms_per_tree": round(dt * 1e3 / trees, 2), "row_trees_per_s": round(n * trees / dt),
+            "test_auc": round(float(auc), 4), "trees_in_forest": len(m.trees), **_dist_fields(ctx)}
+
+
+def bench_bprmf_dp(k=64, epochs=3, shard_model=False, n_ratings=20000263, n_users=138493, n_items=27278):
+    """BPR-MF: interactions sharded over the ranks; factor tables mixed every epoch, or
+    row-sharded over the ranks (-shard_model: explicit triples, uniform negatives)."""
+    from hivemall_amd.io.synthetic import movielens_like
+    from hivemall_amd.models.mf import BPRMF, auc_implicit
+    ctx, mixer = _ctx()
+    dev = ctx.device
+    us, its = movielens_like(n_ratings, n_users, n_items, device=dev, k=16)
+    n = us.numel()
+    ntest = min(200000, n // 10)
+    tu, ti = us[:-ntest], its[:-ntest]
+    me = slice(ctx.rank, None, ctx.world_size)
+    tu, ti = tu[me].contiguous(), ti[me].contiguous()
+    kw = dict(device=dev, mixer=mixer, rank=ctx.rank)
+    if shard_model:
+        g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
+        tj = torch.randint(0, n_items, (tu.numel(),), generator=g, device=dev, dtype=torch.int32)
+        opts = f"-factors {k} -iters {epochs} -eta0 0.05 -shard_model -disable_cv"
+        m, dt = _timed(ctx, mixer, lambda: BPRMF(opts, **kw).fit(tu, ti, tj))
+    else:
+        opts = f"-factors {k} -iters 1 -eta0 0.05 -mix_interval 1 -disable_cv"
+        BPRMF(opts, **kw).fit_implicit(tu[:100000], ti[:100000], n_users, n_items, epochs=1)
+        m, dt = _timed(ctx, mixer, lambda: BPRMF(opts, **kw).fit_implicit(tu, ti, n_users, n_items, epochs=epochs))
+    auc = auc_implicit(m, us[-ntest:].cpu().numpy(), its[-ntest:].cpu().numpy())
+    return {"config": f"BPR-MF k={k}, MovieLens-20M-shaped ({n} interactions, {n_users} users, {n_items} items) "
+                      f"sharded over {ctx.world_size} ranks, "
+                      + ("row-sharded tables (-shard_model), explicit triples" if shard_model else
+                         "device negative sampling, tables mixed every epoch"),
+            "device": str(dev), "triples_per_s": round((n - ntest) * epochs / dt), "seconds": round(dt, 3),
+            "sampled_auc": round(auc, 4), **_dist_fields(ctx)}
+
+
+DIST = {"gbdt": bench_gbdt_dp, "xgboost": lambda **kw: bench_gbdt_dp(xgb=True, **{"depth": 6, **kw}),
+        "rf": bench_rf_dp, "bprmf": bench_bprmf_dp,
+        "bprmf_shard": lambda **kw: bench_bprmf_dp(shard_model=True, **kw)}
+_BPR_SMALL = dict(k=8, epochs=2, n_ratings=60000, n_users=3000, n_items=1500)
+DIST_SMALL = {"gbdt": dict(n=20000, trees=3, depth=4), "xgboost": dict(n=20000, trees=3, depth=4),
+              "rf": dict(n=20000, trees=4, depth=6), "bprmf": _BPR_SMALL, "bprmf_shard": _BPR_SMALL}
+
+
+def main_dist(names, gpus, small):
+    """--gpus N: the N-rank entry point (BASELINE configs 4 and 5)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    if gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # start the ranks as a child process, before this process touches the GPU
+        import subprocess
+        from bench import _free_port
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.run(cmd, env=env).returncode)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        print(f"[bench_configs] --gpus {gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    from hivemall_amd.parallel.dist import shutdown
+    for name in names or ["gbdt", "rf", "bprmf"]:
+        kw = dict(DIST_SMALL.get(name, {})) if small else {}
+        res = DIST[name](**kw)
+        res["bench"] = name
+        res["n_gpus"] = gpus
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps(res), flush=True)
+    shutdown()
+
+
 ALL = {"classifier": bench_classifier, "linear_gpu": bench_linear_gpu, "linear_hashed": bench_linear_hashed,
        "fm": bench_fm,
        "gbdt": bench_gbdt, "rf": bench_rf, "bprmf": bench_bprmf, "xgboost": bench_xgboost}
@@ -212,6 +368,11 @@ CPU = {"linear_gpu": dict(n=1_000_000), "linear_hashed": dict(n_rows=8 * 262144,
        "xgboost": dict(n=1_000_000, rounds=10)}
 
 if __name__ == "__main__":
+    if "--gpus" in sys.argv:
+        i = sys.argv.index("--gpus")
+        main_dist([a for a in sys.argv[1:] if not a.startswith("--") and a != sys.argv[i + 1]],
+                  int(sys.argv[i + 1]), "--small" in sys.argv)
+        sys.exit(0)
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     small = "--small" in sys.argv  # CPU smoke of the harness itself (tiny shapes)
     cpu = "--cpu" in sys.argv      # reference-class CPU measurement

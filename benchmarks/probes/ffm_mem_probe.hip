@@ -11,6 +11,7 @@
 //   mode 4: the aligned layout of mode 3, live slots only (partial lines)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace {
 
@@ -62,6 +63,55 @@ __global__ __launch_bounds__(256) void probe_kernel(const int32_t* __restrict__ 
     }
 }
 
+// mode 5 / 6: the per-slot-AdaGrad block layout of ffm_sg_kernel, fp32 V (5) / bf16 V (6):
+// per feature a 896-B (512-B) block [V: 40 slots | G: 40 x fp32 | zero tail]; each live slot
+// gathers its V (16 / 8 B) and G (4 B) and writes both back; the diagonal, pad and tail are
+// written too (whole lines), as the kernel does.
+template <int NS, bool VBF>
+__global__ __launch_bounds__(256) void probe_sg_kernel(const int32_t* __restrict__ idx, int B, int F,
+                                                       char* __restrict__ tab, float* __restrict__ out) {
+    constexpr uint32_t VSB = VBF ? 8u : 16u, BS = VBF ? 512u : 896u, GOFF = 40u * VSB;
+    __shared__ int s_i[64];
+    const int tid = threadIdx.x;
+    const int FF = F * F;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    using Img = typename std::conditional<VBF, u2v, f4v>::type;
+    for (int row = blockIdx.x; row < B; row += gridDim.x) {
+        if (tid < F) s_i[tid] = idx[(size_t)row * F + tid];
+        __syncthreads();
+        Img v[NS];
+        float g[NS];
+        uint32_t ov[NS], og[NS];
+        bool ok[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int s = tid + j * 256;
+            const int a = s < FF ? s / F : 0, b = s < FF ? s % F : 0;
+            ok[j] = s < FF;
+            const uint32_t i = (uint32_t)s_i[a];
+            ov[j] = i * BS + (uint32_t)b * VSB;
+            og[j] = i * BS + GOFF + (uint32_t)b * 4u;
+            v[j] = *reinterpret_cast<const Img*>(tab + ov[j]);
+            g[j] = *reinterpret_cast<const float*>(tab + og[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            if (!ok[j]) continue;
+            v[j].x += 1;
+            *reinterpret_cast<Img*>(tab + ov[j]) = v[j];
+            *reinterpret_cast<float*>(tab + og[j]) = g[j] + 1.f;
+        }
+        if (tid < F) {
+            char* blk = tab + (uint32_t)s_i[tid] * BS;
+            *reinterpret_cast<Img*>(blk + 39u * VSB) = Img{};
+            *reinterpret_cast<float*>(blk + GOFF + 39u * 4u) = 0.f;
+            for (uint32_t t = GOFF + 160u; t < BS; t += 16u) *reinterpret_cast<uint4*>(blk + t) = make_uint4(0u, 0u, 0u, 0u);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 extern "C" int hm_probe_ffm_mem(const int32_t* idx, int B, int F, int nfld, void* vg, float* out, int mode,
@@ -74,6 +124,8 @@ extern "C" int hm_probe_ffm_mem(const int32_t* idx, int B, int F, int nfld, void
     else if (mode == 1) L(1, 39);
     else if (mode == 2) L(2, 39);
     else if (mode == 3) L(3, 40);
+    else if (mode == 5) hipLaunchKernelGGL((probe_sg_kernel<6, false>), dim3(blocks), dim3(256), 0, stream, idx, B, F, (char*)vg, out);
+    else if (mode == 6) hipLaunchKernelGGL((probe_sg_kernel<6, true>), dim3(blocks), dim3(256), 0, stream, idx, B, F, (char*)vg, out);
     else L(1, 40);
 #undef L
     return (int)hipGetLastError();

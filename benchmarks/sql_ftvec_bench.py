@@ -1,0 +1,60 @@
+"""HiveQL feature engineering + training on Criteo-shaped string rows:
+
+    SELECT train_classifier(add_bias(feature_hashing(features)), label, '-loss logloss -opt adagrad')
+
+Times the feature-engineering expressions alone (SELECT add_bias(feature_hashing(features)))
+and the whole training statement, on an Arrow-backed table (list<string> column, as a Parquet
+or Arrow source arrives) and on a table of Python lists.
+
+    python benchmarks/sql_ftvec_bench.py [rows] [device]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def table(n, arrow=True):
+    from hivemall_amd.io.synthetic import criteo_like
+    idx, y = criteo_like(n, 20, seed=1)
+    idx = idx.numpy()
+    # Criteo-shaped raw feature names "<field>#<value>" (categorical, hashed by the query)
+    names = np.char.add(np.char.add(np.arange(39).astype(str)[None, :].repeat(n, 0), "#"), idx.astype(str))
+    flat = pa.array(names.reshape(-1).astype(object), type=pa.string())
+    col = pa.ListArray.from_arrays(pa.array(np.arange(0, n * 39 + 1, 39, dtype=np.int32)), flat)
+    feats = pd.Series(pd.arrays.ArrowExtensionArray(col)) if arrow else pd.Series(col.to_pylist(), dtype=object)
+    return pd.DataFrame({"features": feats, "label": (y.numpy() > 0).astype(np.int32)})
+
+
+def main():
+    from hivemall_amd.sql import Session
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    dev = sys.argv[2] if len(sys.argv) > 2 else "cpu"
+    for arrow in (True, False):
+        t = time.perf_counter()
+        df = table(n, arrow)
+        gen = time.perf_counter() - t
+        s = Session(device=dev)
+        s.register("criteo", df)
+        t = time.perf_counter()
+        fe = s.sql("SELECT add_bias(feature_hashing(features)) AS f FROM criteo")
+        t_fe = time.perf_counter() - t
+        t = time.perf_counter()
+        m = s.sql("SELECT train_classifier(add_bias(feature_hashing(features)), label, "
+                  "'-loss logloss -opt adagrad') AS (feature, weight) FROM criteo")
+        t_all = time.perf_counter() - t
+        print(json.dumps({"rows": n, "device": dev, "table": "arrow list<string>" if arrow else "python lists",
+                          "gen_s": round(gen, 2), "feature_eng_s": round(t_fe, 3),
+                          "feature_eng_rows_per_s": round(n / t_fe), "train_stmt_s": round(t_all, 3),
+                          "train_stmt_rows_per_s": round(n / t_all), "model_rows": len(m),
+                          "first": fe["f"].iloc[0][:3]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

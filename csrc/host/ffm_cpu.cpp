@@ -47,6 +47,7 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
     // 0 = one per element, laid out like V
     const int slot_g = ip[17];
     const size_t GS = ip[18] > 0 ? (size_t)ip[18] : FS;   // slot-G: floats between features
+    const size_t GF = ip[21] > 0 ? (size_t)ip[21] : 1;    // slot-G: floats between fields
     if (slot_g && Kp > 64) return 22;
     std::vector<int> ri(F), rf(F);
     std::vector<float> rx(F);
@@ -112,7 +113,7 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
                 const float* par = &snap[((size_t)b * F + a) * Kp];
                 if (slot_g) {
                     // G += sum_f g_f^2 (fp32, factor order), then every factor steps with it
-                    float* pg = G + (size_t)ri[a] * GS + rf[b];
+                    float* pg = G + (size_t)ri[a] * GS + (size_t)rf[b] * GF;
                     float gs = *pg;
                     float gk[64];
                     for (int k = 0; k < Kp; ++k) {

@@ -8,6 +8,7 @@
 //   Python layer never loops over individual features.
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -112,6 +113,88 @@ HM_API void hm_mhash_batch(const uint8_t* buf, const int64_t* off, int64_t n, ui
 }
 
 // ---------------------------------------------------------------- dictionary
+// feature_hashing over packed feature strings (ftvec/functions.py feature_hashing, vectorised):
+// "name" -> "h", "name:v" -> "h:v", "field:index:v" -> "h:v" with h = mhash(name) (the name is
+// everything before the LAST of at most two ':' separators, as the per-row UDF's _split).  The
+// value text is copied verbatim.  out needs off[n] + 11 * n bytes; out_off gets n + 1 offsets;
+// returns the bytes written.  Two passes (lengths, then a parallel fill) keep it O(bytes).
+// decimal text of a signed 32-bit int (no locale, no format parsing); returns the length
+inline int fmt_i32(int32_t v, char* o) {
+    char t[12];
+    uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+    int n = 0;
+    do { t[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    int k = 0;
+    if (v < 0) o[k++] = '-';
+    while (n) o[k++] = t[--n];
+    return k;
+}
+
+HM_API int64_t hm_feature_hash_strs(const uint8_t* buf, const int64_t* off, int64_t n,
+                                    int32_t num_features, uint32_t seed, uint8_t* out,
+                                    int64_t* out_off) {
+    std::vector<int32_t> h(n);
+    std::vector<int32_t> namelen(n);
+    std::vector<int64_t> len(n + 1);
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* p = buf + off[i];
+        const int L = (int)(off[i + 1] - off[i]);
+        int c1 = -1, c2 = -1;
+        for (int k = 0; k < L; ++k)
+            if (p[k] == ':') {
+                if (c1 < 0) c1 = k;
+                else { c2 = k; break; }
+            }
+        const int nl = c2 >= 0 ? c2 : (c1 >= 0 ? c1 : L);
+        namelen[i] = c1 >= 0 ? nl : -1;                      // -1: no value part
+        h[i] = mhash_reduce(murmur3_x86_32(p, nl, seed), num_features);
+        char tmp[16];
+        const int hd = fmt_i32(h[i], tmp);
+        len[i] = hd + (c1 >= 0 ? 1 + (L - nl - 1) : 0);
+    }
+    out_off[0] = 0;
+    for (int64_t i = 0; i < n; ++i) out_off[i + 1] = out_off[i] + len[i];
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t* o = out + out_off[i];
+        const int hd = fmt_i32(h[i], reinterpret_cast<char*>(o));
+        if (namelen[i] >= 0) {
+            o[hd] = ':';
+            const int nl = namelen[i];
+            const int L = (int)(off[i + 1] - off[i]);
+            std::memcpy(o + hd + 1, buf + off[i] + nl + 1, L - nl - 1);
+        }
+    }
+    return out_off[n];
+}
+
+// list<string> rows with one constant string appended to every valid row (add_bias): new string
+// buffer + string offsets + row offsets in one pass.  valid may be null (every row valid);
+// out needs off[row_off[n]] + n * clen bytes, out_off row_off[n] + n + 1, out_row n + 1.
+HM_API int64_t hm_list_append_str(const uint8_t* buf, const int64_t* off, const int64_t* row_off,
+                                  const uint8_t* valid, int64_t n, const uint8_t* cstr, int32_t clen,
+                                  uint8_t* out, int64_t* out_off, int64_t* out_row) {
+    int64_t s = 0, b = 0;
+    out_off[0] = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        out_row[r] = s;
+        const int64_t a0 = row_off[r], a1 = row_off[r + 1];
+        const int64_t nb = off[a1] - off[a0];
+        std::memcpy(out + b, buf + off[a0], (size_t)nb);
+        for (int64_t k = a0; k < a1; ++k) out_off[s + (k - a0) + 1] = b + (off[k + 1] - off[a0]);
+        s += a1 - a0;
+        b += nb;
+        if (!valid || valid[r]) {
+            std::memcpy(out + b, cstr, (size_t)clen);
+            b += clen;
+            out_off[++s] = b;
+        }
+    }
+    out_row[n] = s;
+    return b;
+}
+
 HM_API void* hm_dict_new() { return new Dict(); }
 HM_API void hm_dict_free(void* d) { delete static_cast<Dict*>(d); }
 HM_API int64_t hm_dict_size(void* d) { return (int64_t)static_cast<Dict*>(d)->keys.size(); }

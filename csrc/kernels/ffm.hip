@@ -50,6 +50,8 @@ struct FFMParams {
     int gstride;           // per-slot G: floats between consecutive features of G
     int vpad;              // per-slot G block layout: V slots per feature block (0: separate tables)
     int tail16;            // per-slot G block layout: zero 16-B chunks after each G region
+    int gfstride;          // per-slot G: floats between consecutive fields (1, or 4 in 16-B slots)
+    int sg_threads;        // ffm_sg_kernel block size (256 default; 512 for A/B)
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
                            // table pads each feature block to whole 128-B lines)
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 if constexpr (SG) {
                     // one accumulator per slot: G += sum of the k squared gradients (factor
                     // order), then every factor steps with 1 / sqrt(G + eps)
-                    float* pg = Gs + (size_t)ia * P.gstride + s_fld[b];
+                    float* pg = Gs + (size_t)ia * P.gstride + (size_t)s_fld[b] * P.gfstride;
                     float gs = *pg;
 #pragma unroll
                     for (int c = 0; c < KC; ++c)
@@ -654,13 +656,18 @@ __device__ __forceinline__ void bar_raw() {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* glb_ptr_t;
 
-template <int NS, bool BF = true>
+// SG (bf16 only): per-slot AdaGrad in 16-B slots {V bf16 x 4 | G fp32 | 0}: the per-slot
+// accumulator in fp32 at the byte size and access pattern of the per-element bf16 slots (one
+// 16-B DMA and one 16-B store per slot; the block layout of ffm_sg_kernel needs an 8-B and a
+// 4-B access per slot, measured 79.5 M rows/s against this layout's rate).
+template <int NS, bool BF = true, bool SG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2))) void ffm_pipe_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
+    static_assert(BF || !SG, "per-slot 16-B slots hold bf16 V");
     constexpr uint32_t SLOT_B = BF ? 16u : 32u;                        // bytes per packed slot
     using Img = typename std::conditional<BF, uint2, float4>::type;   // V in the transposed image
     __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256 * (BF ? 1 : 2)];   // slot DMA landing zone
@@ -879,6 +886,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
                 const f2 lamj = {lj, lj};
                 const f2 d0 = coef * p0 + lamj * o0, d1 = coef * p1 + lamj * o1;
+                if constexpr (SG) {
+                    // one fp32 accumulator per slot (word 2): G += sum of the 4 squared gradients
+                    const float gs = (((__uint_as_float(q[j].z) + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
+                    const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
+                    const f2 rr = {r, r};
+                    o0 = o0 + rr * d0;
+                    o1 = o1 + rr * d1;
+                    const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
+                    const uint4 st = make_uint4(pack_sr_hi(o0, h, rotl32(h, 16)),
+                                                pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
+                                                __float_as_uint(gs), 0u);
+                    if (wr >> j & 1u) *reinterpret_cast<uint4*>(vg + off[j]) = st;
+                    continue;
+                }
                 g0 = g0 + d0 * d0;
                 g1 = g1 + d1 * d1;
                 const f2 t0 = g0 + eps, t1 = g1 + eps;
@@ -955,18 +976,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 //   E    AdaGrad(V) with the slot accumulator, FTRL(w); stores; then the linear state of r+G
 //        is loaded (after E's FTRL stores: a feature shared by consecutive rows of the block is
 //        updated in sequence, same lane, same address); barrier (T reuse)
-template <int NS, bool VBF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3))) void ffm_sg_kernel(
+// TH threads per block (256 or 512): with 512 a thread owns half the slots, so the prefetch
+// registers halve and 8 waves/SIMD fit; the block is the same one row (same LDS image), so a
+// CU holds more rows in flight at the same LDS per row.
+template <int NS, bool VBF, int TH = 256>
+__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(TH == 512 ? 6 : 4))) void ffm_sg_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
     float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
     constexpr uint32_t VSB = VBF ? 8u : 16u;                          // V bytes per slot
-    using Img = typename std::conditional<VBF, uint2, float4>::type;
-    __shared__ __attribute__((aligned(16))) Img s_t[NS * 256];       // transposed V image
+    // native ext_vector types: HIP's float4 struct kept the prefetch array in scratch memory
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    using Img = typename std::conditional<VBF, u2v, f4v>::type;
+    __shared__ __attribute__((aligned(16))) Img s_t[NS * TH];       // transposed V image
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];         // meta {i, f, x} of 2 rows
-    __shared__ float s_red[8];                                       // [0..3] sums, [4+b] scale
+    constexpr int NW = TH / 64;
+    __shared__ float s_red[NW + 2];                                  // [0..NW) sums, [NW+b] scale
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -980,7 +1008,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
     int ab[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-        const int s = tid + j * 256;
+        const int s = tid + j * TH;
         ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
     }
 #define SA(j) (ab[j] & 0xFF)
@@ -1010,14 +1038,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
                 sq = x * x;
             }
             const float tot = hm::wave_sum_uniform(sq);
-            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+            if (lane == 0) s_red[NW + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
         }
     };
     // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal
     // (written back unchanged: whole lines), 0 = dead
     auto slot = [&](int bf, int j, uint32_t& ov, uint32_t& og, float& xab) -> uint32_t {
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
-        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * TH < FF;
         const bool live = ok && SA(j) != SB(j);
         const uint32_t i = ok ? (uint32_t)ma.x : 0u, f = ok ? (uint32_t)mb.y : 0u;
         ov = i * vfs + f * VSB;
@@ -1025,18 +1053,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
+    // the prefetch registers (a macro, not a lambda: an array captured by reference stayed in
+    // scratch memory for the float4 case)
     Img nv[NS];
     float ng[NS];
-    auto prefetch = [&](int bf) {
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            uint32_t ov, og;
-            float xab;
-            slot(bf, j, ov, og, xab);
-            nv[j] = *reinterpret_cast<const Img*>(vb + ov);
-            ng[j] = *reinterpret_cast<const float*>(gb + og);
-        }
-    };
+#define SG_PREFETCH(bf)                                                  \
+    _Pragma("unroll") for (int j = 0; j < NS; ++j) {                     \
+        uint32_t ov_, og_;                                               \
+        float xab_;                                                      \
+        slot(bf, j, ov_, og_, xab_);                                     \
+        nv[j] = *reinterpret_cast<const Img*>(vb + ov_);                 \
+        ng[j] = *reinterpret_cast<const float*>(gb + og_);               \
+    }
     // linear state (w, z, n) of this lane's feature in the row of s_m[bf] (wave W_LIN)
     float lw = 0.f, lz = 0.f, ln = 0.f;
     auto load_lin = [&](int bf) {
@@ -1057,28 +1085,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
     load_meta(row);
     publish_meta(0);
     bar_raw();
-    prefetch(0);
+    SG_PREFETCH(0);
     load_lin(0);
     load_meta(row + G);
 
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
-        // ---- top: the prefetched slots become the current row's; own V -> transposed image ----
-        Img cv[NS];
+        // ---- top: the prefetched slots become the current row's; own V -> transposed image
+        //      (the forward and the update read it back from there: no registers held for V
+        //      across the row, so the next row's prefetch fits beside it at higher occupancy) ----
         float cg[NS];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) { cv[j] = nv[j]; cg[j] = ng[j]; }
-#pragma unroll
-        for (int j = 0; j < NS; ++j) s_t[SB(j) * F + SA(j)] = cv[j];
+        for (int j = 0; j < NS; ++j) {
+            // slots past F*F decode to (0, 0): they must not overwrite that diagonal slot's V,
+            // which is read back from the image (its update writes it to memory)
+            if (tid + j * TH < FF) s_t[SB(j) * F + SA(j)] = nv[j];
+            cg[j] = ng[j];
+        }
         if (more) publish_meta(nxt);
         bar_raw();
         // ---- C: prefetch the next row; raw meta of the row after it ----
         if (more) {
-            prefetch(nxt);
+            SG_PREFETCH(nxt);
             load_meta(row + 2 * G);
         }
-        const float scale = s_red[4 + cur];
+        const float scale = s_red[NW + cur];
         int mi = -1;
         float mx = 0.f;
         if (wave == W_LIN && lane < F) {
@@ -1096,11 +1128,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            const int s = tid + j * 256;
+            const int s = tid + j * TH;
             const Img pv = s_t[s < FF ? s : 0];
+            const Img cv = s_t[SB(j) * F + SA(j)];
             float d;
-            if constexpr (VBF) d = dot2_bf16(cv[j].x, pv.x, dot2_bf16(cv[j].y, pv.y, 0.f));
-            else d = cv[j].x * pv.x + cv[j].y * pv.y + cv[j].z * pv.z + cv[j].w * pv.w;
+            if constexpr (VBF) d = dot2_bf16(cv.x, pv.x, dot2_bf16(cv.y, pv.y, 0.f));
+            else d = cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w;
             part += d * xab[j];
         }
         part *= 0.5f * scale * scale;
@@ -1108,7 +1141,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
         part = hm::wave_sum_uniform(part);
         if (lane == 0) s_red[wave] = part;
         bar_raw();
-        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        float p = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) p += s_red[k];
         if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
@@ -1125,19 +1160,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
                 uint32_t ov, og;
                 float xj;
                 slot(cur, j, ov, og, xj);
-                const int s = tid + j * 256;
+                const int s = tid + j * TH;
                 const Img pv = s_t[s];
+                const Img cv = s_t[SB(j) * F + SA(j)];
                 const float c = ks * xab[j];
                 // diagonal slots: c = 0 and lambda = 0 -> zero gradient, V and G unchanged (the
                 // stochastic rounding of a value already in bf16 is exact)
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
                 f2 o0, o1, p0, p1;
                 if constexpr (VBF) {
-                    o0 = bf2_to_f2(cv[j].x); o1 = bf2_to_f2(cv[j].y);
-                    p0 = bf2_to_f2(pv.x);    p1 = bf2_to_f2(pv.y);
+                    o0 = bf2_to_f2(cv.x); o1 = bf2_to_f2(cv.y);
+                    p0 = bf2_to_f2(pv.x); p1 = bf2_to_f2(pv.y);
                 } else {
-                    o0 = f2{cv[j].x, cv[j].y}; o1 = f2{cv[j].z, cv[j].w};
-                    p0 = f2{pv.x, pv.y};       p1 = f2{pv.z, pv.w};
+                    o0 = f2{cv.x, cv.y}; o1 = f2{cv.z, cv.w};
+                    p0 = f2{pv.x, pv.y}; p1 = f2{pv.z, pv.w};
                 }
                 const f2 cc = {c, c}, ll = {lj, lj};
                 const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
@@ -1149,10 +1185,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
                 o1 = o1 + rr * d1;
                 if constexpr (VBF) {
                     const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
-                    *reinterpret_cast<uint2*>(vb + ov) = make_uint2(pack_sr_hi(o0, h, rotl32(h, 16)),
-                                                                    pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)));
+                    *reinterpret_cast<u2v*>(vb + ov) = u2v{pack_sr_hi(o0, h, rotl32(h, 16)),
+                                                          pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24))};
                 } else {
-                    *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                    *reinterpret_cast<f4v*>(vb + ov) = f4v{o0.x, o0.y, o1.x, o1.y};
                 }
                 *reinterpret_cast<float*>(gb + og) = gs;
             }
@@ -1161,8 +1197,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
                 char* vblk = vb + (uint32_t)mi * vfs;
                 char* gblk = gb + (uint32_t)mi * gfs;
                 for (int f = P.num_fields; f < P.vpad; ++f) {
-                    if constexpr (VBF) *reinterpret_cast<uint2*>(vblk + f * VSB) = make_uint2(0u, 0u);
-                    else *reinterpret_cast<uint4*>(vblk + f * VSB) = make_uint4(0u, 0u, 0u, 0u);
+                    *reinterpret_cast<Img*>(vblk + f * VSB) = Img{};
                     *reinterpret_cast<float*>(gblk + f * 4) = 0.f;
                 }
                 for (int t = 0; t < P.tail16; ++t)
@@ -1183,6 +1218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VBF ? 4 : 3
         bar_raw();   // T and s_m[cur] are rewritten by the next iterations
     }
 #undef SA
+#undef SG_PREFETCH
 #undef SB
 }
 
@@ -1230,6 +1266,25 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
+// Per-slot-G in 16-B bf16 slots {V | G | 0} (Kp == 4, F <= 45, table < 4 GiB); -1 otherwise.
+int dispatch_sg16(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                  float* pred, float* loss, int grid, hipStream_t stream) {
+    if (P.Kp != 4 || P.F > 45) return -1;
+    if ((size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32)) return -1;
+    const int need = (P.F * P.F + 255) / 256;
+    const int blocks = default_blocks(P.B, grid);
+    if (blocks <= 0) return 0;
+#define HM_PIPE(NSV) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, true, true>), dim3(blocks), dim3(256), 0, stream, P, \
+                                        idx, fld, val, y, VG, w, wz, wn, bias, pred, loss)
+    if (need <= 2) { HM_PIPE(2); }
+    else if (need <= 4) { HM_PIPE(4); }
+    else if (need <= 6) { HM_PIPE(6); }
+    else { HM_PIPE(8); }
+#undef HM_PIPE
+    HM_LAUNCH_RET();
+}
+
 // Per-slot-G pipelined dispatch (Kp == 4, F <= 45, block layout, table < 4 GiB); -1 otherwise.
 template <bool BF>
 int dispatch_sg(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
@@ -1242,12 +1297,25 @@ int dispatch_sg(const FFMParams& P, const int32_t* idx, const int32_t* fld, cons
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF>), dim3(blocks), dim3(256), 0, stream, P, idx, fld, \
-                                      val, y, V, G, w, wz, wn, bias, pred, loss)
-    if (need <= 2) { HM_SG(2); }
-    else if (need <= 4) { HM_SG(4); }
-    else if (need <= 6) { HM_SG(6); }
-    else { HM_SG(8); }
+    // 256 threads at 4 waves/SIMD (128 VGPRs, no spill: 4 rows in flight per CU); 512 threads
+    // (half the slots per thread; 3 blocks per CU) is variant 4 (A/B)
+    if (P.sg_threads == 256) {
+#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF, 256>), dim3(blocks), dim3(256), 0, stream, P, idx, \
+                                      fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+        if (need <= 2) { HM_SG(2); }
+        else if (need <= 4) { HM_SG(4); }
+        else if (need <= 6) { HM_SG(6); }
+        else { HM_SG(8); }
+#undef HM_SG
+        HM_LAUNCH_RET();
+    }
+    const int need2 = (P.F * P.F + 511) / 512;
+#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF, 512>), dim3(blocks), dim3(512), 0, stream, P, idx, \
+                                      fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+    if (need2 <= 1) { HM_SG(1); }
+    else if (need2 <= 2) { HM_SG(2); }
+    else if (need2 <= 3) { HM_SG(3); }
+    else { HM_SG(4); }
 #undef HM_SG
     HM_LAUNCH_RET();
 }
@@ -1290,7 +1358,12 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
              float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream) {
     if (slot_g) {
-        if (variant != 1) {
+        if (variant != 1 && BF && P.gfstride == 4 && P.vpad == 0 &&
+            reinterpret_cast<char*>(G) == reinterpret_cast<char*>(V) + 8) {
+            const int rc = dispatch_sg16(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+            if (rc != -1) return rc;
+        }
+        if (variant != 1 && P.gfstride == 1) {
             const int rc = dispatch_sg<BF>(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
                                            bias, pred, loss, grid, stream);
             if (rc != -1) return rc;
@@ -1310,8 +1383,9 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
-//                     slot_g, gstride, vpad, tail16
-// slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f]; with the
+//                     slot_g, gstride, vpad, tail16, gfstride
+// slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f * gfstride];
+//             bf16 V in 16-B slots {V | G | 0} (G = V + 8 B, gfstride 4): ffm_pipe_kernel<SG>; with the
 //             block layout (G = V + vpad * slot bytes, vpad > 0) the pipelined ffm_sg_kernel runs
 //             (K <= 4, F <= 45), else the generic kernel.  tail16 = zero 16-B chunks after each
 //             feature's G region (line completion).
@@ -1319,7 +1393,8 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             [num_features][fstride][2][Kp] table (G == V + Kp elements, slot stride 2*Kp); 0:
 //             separate [.][.][Kp] tables.
 // variant: 0 = auto (per-slot: ffm_sg_kernel; per-element bf16: ffm_pipe_kernel, fp32:
-// ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel, 3 = ffm_pipe_kernel.
+// ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel, 3 = ffm_pipe_kernel,
+// 4 = ffm_sg_kernel with 512-thread blocks (default 256).
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -1339,6 +1414,9 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.gstride = ip[18];
     P.vpad = ip[19];
     P.tail16 = ip[20];
+    P.gfstride = ip[21] > 0 ? ip[21] : 1;
+    P.sg_threads = variant == 4 ? 512 : 256;
+    if (slot_g && P.gfstride == 4) P.sstride = 2 * P.Kp;   // 16-B {V | G | 0} slots (bf16, Kp 4)
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
@@ -1349,7 +1427,8 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
             // block layout: G right after the V region of the same feature block
             const size_t es = bf16 ? 2 : 4;
             if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.vpad * P.Kp * es ||
-                (size_t)P.fstride * P.Kp * es != (size_t)P.gstride * 4 || P.vpad < P.num_fields)
+                (size_t)P.fstride * P.Kp * es != (size_t)P.gstride * 4 || P.vpad < P.num_fields ||
+                P.gfstride != 1)
                 return (int)hipErrorInvalidValue;
         }
     } else if (packed) {

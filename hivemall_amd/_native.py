@@ -112,6 +112,8 @@ _HOST_SIGS: dict[str, tuple] = {
     "hm_murmur3": (c_u32, [c_p, c_int, c_u32]),
     "hm_murmur3_batch": (None, [c_p, c_p, c_i64, c_u32, c_p]),
     "hm_mhash_batch": (None, [c_p, c_p, c_i64, c_u32, c_i32, c_p]),
+    "hm_feature_hash_strs": (c_i64, [c_p, c_p, c_i64, c_i32, c_u32, c_p, c_p]),
+    "hm_list_append_str": (c_i64, [c_p, c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_p, c_p]),
     "hm_dict_new": (c_p, []),
     "hm_dict_free": (None, [c_p]),
     "hm_dict_size": (c_i64, [c_p]),

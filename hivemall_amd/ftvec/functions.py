@@ -39,16 +39,117 @@ def _fmt(v: float) -> str:
     return repr(v) if v != int(v) or abs(v) > 1e15 else f"{v:.1f}"
 
 
+# ------------------------------------------------------------------ vectorised column paths
+# The SQL executor hands vectorised UDFs whole columns.  A column of feature lists becomes one
+# Arrow list<string> array (zero-copy when the table is Arrow-backed) whose flat string buffer
+# is processed by the native host library in one call; the result is an Arrow-backed Series, so
+# a learner downstream parses it from the buffers again without any Python object per feature.
+
+def _list_column(col):
+    """Arrow list<string> array of a Series of feature lists, or None (mixed / non-string
+    content: the per-row path handles it)."""
+    import pandas as pd
+    import pyarrow as pa
+
+    if not isinstance(col, pd.Series):
+        return None
+    if isinstance(col.dtype, pd.ArrowDtype):
+        a = col.array._pa_array
+        a = a.combine_chunks() if isinstance(a, pa.ChunkedArray) else a
+        if (pa.types.is_list(a.type) or pa.types.is_large_list(a.type)) and \
+                (pa.types.is_string(a.type.value_type) or pa.types.is_large_string(a.type.value_type)):
+            return a
+        return None
+    vals = col.to_numpy(dtype=object)
+    for r in vals[:64]:
+        if r is not None and not (isinstance(r, (list, tuple, np.ndarray)) and all(isinstance(v, str) for v in r)):
+            return None
+    try:
+        return pa.array([None if r is None else list(r) for r in vals], type=pa.list_(pa.string()))
+    except (pa.ArrowInvalid, pa.ArrowTypeError):
+        return None
+
+
+def _arrow_series(arr, index):
+    import pandas as pd
+
+    return pd.Series(pd.arrays.ArrowExtensionArray(arr), index=index)
+
+
+def _hash_list_column(arr, num_features: int):
+    """feature_hashing over every string of a list<string> array (hm_feature_hash_strs)."""
+    import pyarrow as pa
+
+    from .. import _native
+    from ..io.ingest import arrow_buffers
+
+    data, so, lo = arrow_buffers(arr)
+    n = len(so) - 1
+    out = np.empty(max(1, int(so[-1]) + 11 * n), dtype=np.uint8)
+    oo = np.empty(n + 1, dtype=np.int64)
+    if n:
+        d = data if len(data) else np.zeros(1, np.uint8)
+        tot = _native.host().hm_feature_hash_strs(d.ctypes.data, np.ascontiguousarray(so).ctypes.data, n,
+                                                  int(num_features), DEFAULT_SEED, out.ctypes.data,
+                                                  oo.ctypes.data)
+    else:
+        oo[0], tot = 0, 0
+    vals = pa.LargeStringArray.from_buffers(n, pa.py_buffer(oo), pa.py_buffer(out[:max(1, tot)]))
+    return pa.LargeListArray.from_arrays(pa.array(lo, pa.int64()), vals.cast(pa.string()),
+                                         mask=arr.is_null())
+
+
+def _append_const(arr, const: str):
+    """list<string> rows with ``const`` appended to every non-null row (nulls stay null):
+    one native pass over the string buffer (hm_list_append_str)."""
+    import pyarrow as pa
+
+    from .. import _native
+    from ..io.ingest import arrow_buffers
+
+    data, so, lo = arrow_buffers(arr)
+    n = len(arr)
+    valid = None
+    if arr.null_count:
+        valid = np.ascontiguousarray(~np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool),
+                                     dtype=np.uint8)
+    c = np.frombuffer(const.encode("utf-8"), dtype=np.uint8)
+    nrows_valid = n if valid is None else int(valid.sum())
+    out = np.empty(max(1, len(data) + len(c) * n), dtype=np.uint8)
+    oo = np.empty(int(lo[-1]) + nrows_valid + 1, dtype=np.int64)
+    orow = np.empty(n + 1, dtype=np.int64)
+    d = data if len(data) else np.zeros(1, np.uint8)
+    so = np.ascontiguousarray(so, dtype=np.int64)
+    lo = np.ascontiguousarray(lo, dtype=np.int64)
+    tot = _native.host().hm_list_append_str(d.ctypes.data, so.ctypes.data, lo.ctypes.data,
+                                            None if valid is None else valid.ctypes.data, n, c.ctypes.data,
+                                            len(c), out.ctypes.data, oo.ctypes.data, orow.ctypes.data)
+    vals = pa.LargeStringArray.from_buffers(len(oo) - 1, pa.py_buffer(oo), pa.py_buffer(out[:max(1, tot)]))
+    return pa.LargeListArray.from_arrays(pa.array(orow, pa.int64()), vals.cast(pa.string()),
+                                         mask=arr.is_null())
+
+
 # ------------------------------------------------------------------ basic
-@udf("add_bias")
-def add_bias(features):
-    """Append the bias feature ``0:1.0`` (index 0 is reserved for the bias)."""
+def _add_bias1(features):
     if features is None:
         return None
     fs = list(features)
     if fs and isinstance(fs[0], (int, np.integer)):
         return fs + [0]
     return fs + ["0:1.0"]
+
+
+@udf("add_bias", vectorized=True)
+def add_bias(features):
+    """Append the bias feature ``0:1.0`` (index 0 is reserved for the bias)."""
+    import pandas as pd
+
+    if isinstance(features, pd.Series):
+        arr = _list_column(features)
+        if arr is None:
+            return _rowwise(_add_bias1, features)
+        return _arrow_series(_append_const(arr, "0:1.0"), features.index)
+    return _add_bias1(features)
 
 
 @udf("add_feature_index")
@@ -163,9 +264,26 @@ def sort_by_feature(m):
 
 
 # ------------------------------------------------------------------ hashing
-@udf("mhash")
+@udf("mhash", vectorized=True)
 def mhash(word, num_features: int = 1 << 24):
     """MurmurHash3 x86_32 (seed 0x9747b28c) of the UTF-8 word, mod num_features, 1-based."""
+    import pandas as pd
+
+    from ..utils.hashing import mhash_batch
+
+    if isinstance(word, pd.Series):
+        nf = int(num_features.iloc[0]) if isinstance(num_features, pd.Series) else int(num_features)
+        if isinstance(num_features, pd.Series) and num_features.nunique(dropna=False) > 1:
+            return pd.Series([None if w is None else _mhash(str(w), int(k))
+                              for w, k in zip(word.tolist(), num_features.tolist())], index=word.index,
+                             dtype=object)
+        ok = word.notna().to_numpy()
+        h = mhash_batch([str(w) for w in word[ok].tolist()], nf) if ok.any() else np.zeros(0, np.int64)
+        if ok.all():
+            return pd.Series(np.asarray(h, dtype=np.int64), index=word.index)
+        out = np.full(len(word), None, dtype=object)
+        out[ok] = [int(x) for x in h]
+        return pd.Series(out, index=word.index, dtype=object)
     if word is None:
         return None
     return _mhash(str(word), int(num_features))
@@ -176,12 +294,9 @@ _FH_OPTS = Options([opt("num_features", "features", 1 << 24, int, "Number of has
                    "feature_hashing")
 
 
-@udf("feature_hashing")
-def feature_hashing(features, options: str | None = None):
-    """Hash feature names (keeping values): ``"name:v"`` -> ``"mhash(name):v"``."""
+def _feature_hashing1(features, n):
     if features is None:
         return None
-    n = _FH_OPTS.parse(options)["num_features"]
 
     def one(f):
         name, v = _split(f)
@@ -190,6 +305,26 @@ def feature_hashing(features, options: str | None = None):
     if isinstance(features, (list, tuple, np.ndarray)):
         return [one(f) for f in features if f is not None]
     return one(features)
+
+
+@udf("feature_hashing", vectorized=True)
+def feature_hashing(features, options=None):
+    """Hash feature names (keeping values): ``"name:v"`` -> ``"mhash(name):v"``.
+
+    Column form (SQL): the option string is parsed once and the whole column is hashed in one
+    native call over its Arrow string buffer (hm_feature_hash_strs) — bit-identical to the
+    per-row form."""
+    import pandas as pd
+
+    if isinstance(options, pd.Series):
+        options = options.iloc[0] if len(options) else None
+    n = _FH_OPTS.parse(options)["num_features"]
+    if isinstance(features, pd.Series):
+        arr = _list_column(features)
+        if arr is None:
+            return _rowwise(lambda f: _feature_hashing1(f, n), features)
+        return _arrow_series(_hash_list_column(arr, n), features.index)
+    return _feature_hashing1(features, n)
 
 
 @udf("sha1")

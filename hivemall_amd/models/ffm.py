@@ -30,7 +30,6 @@ import pandas as pd
 import torch
 
 from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
-from ..io.ingest import is_arrow_like as ingest_is_arrow
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
 from .base import COMMON_ITER_OPTS, ConversionState, Learner, log, parse_labels_binary
@@ -179,8 +178,7 @@ class FFMTrainer(Learner):
                 self.num_fields = int(tmax(fld)) + 1 if fld.numel() else 1
             yt = None if y is None else torch.from_numpy(y).to(self.device)
             return FFMBatch(idx, fld, val, yt)
-        if ingest_is_arrow(features):
-            features = features.to_pylist() if hasattr(features, "to_pylist") else list(features)
+        # (an Arrow list<string> column is parsed from its buffers by parse_ffm_rows)
         csr = parse_ffm_rows(features, nf, nfld, hash_ints=self.cl["feature_hashing"] > 0)
         if self.num_features is None:
             self.num_features = int(csr.idx.max()) + 1 if csr.nnz else 1
@@ -332,10 +330,14 @@ class FFMTrainer(Learner):
 
 
 def _is_block(V: torch.Tensor, G: torch.Tensor) -> bool:
-    """Per-slot G laid out in V's feature blocks (ops.ffm.slot_block_layout)."""
+    """Per-slot G in a GPU layout: V's feature blocks (ops.ffm.slot_block_layout) or the 16-B
+    bf16 slots {V | G | 0}."""
     es = V.element_size()
-    return (G.dim() == 2 and V.is_cuda and 0 < G.data_ptr() - V.data_ptr() < V.stride(0) * es
-            and G.stride(0) * 4 == V.stride(0) * es)
+    if G.dim() != 2 or not V.is_cuda:
+        return False
+    if G.stride(1) == 4:
+        return G.data_ptr() - V.data_ptr() == 8 and V.dtype == torch.bfloat16
+    return 0 < G.data_ptr() - V.data_ptr() < V.stride(0) * es and G.stride(0) * 4 == V.stride(0) * es
 
 
 def train_ffm(features, labels, options: str | None = None, device=None, **kw) -> pd.DataFrame:

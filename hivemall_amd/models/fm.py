@@ -29,7 +29,7 @@ W0_STRIDE = 32      # floats between shards: one 128-B line each
 from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
 from .base import MIX_OPTS, ConversionState, Learner, log, parse_labels_binary
-from .linear import SparseRows, encode_rows
+from .linear import SparseRows, _arrow_string_lists, encode_rows
 from ..utils.reduce import tmax
 
 
@@ -154,7 +154,7 @@ class FMTrainer(Learner):
                                                 device=self.device, seed=self.encoder.seed)
             yt = None if y is None else torch.from_numpy(y).to(self.device)
             return SparseRows(ip, idx.to(torch.int32), val, yt)
-        if not isinstance(features, (list, CSR)) and _is_arrow(features):
+        if not isinstance(features, (list, CSR)) and _is_arrow(features) and not _arrow_string_lists(features):
             features = features.to_pylist()
         csr, self.encoder = encode_rows(features, self.encoder, train)
         return SparseRows.from_csr(csr, y, self.device)

@@ -125,8 +125,11 @@ def encode_rows(rows, encoder: FeatureEncoder | None, train: bool) -> tuple[CSR,
     if encoder is None:
         enc = FeatureEncoder("int")
         # string features that are integer literals keep the string type in the model table
-        first = next((r[0] for r in rows if r is not None and len(r)), None)
-        enc.string_names = isinstance(first, str)
+        if _arrow(rows):
+            enc.string_names = True
+        else:
+            first = next((r[0] for r in rows if r is not None and len(r)), None)
+            enc.string_names = isinstance(first, str)
         try:
             return enc.encode(rows), enc
         except UDFArgumentException:
@@ -139,6 +142,17 @@ def _arrow(x) -> bool:
     from ..io.ingest import is_arrow_like
 
     return is_arrow_like(x)
+
+
+def _arrow_string_lists(x) -> bool:
+    """An Arrow list<string> column (parsed from its buffers by FeatureEncoder.encode)."""
+    from ..io.ingest import to_arrow_lists
+
+    try:
+        to_arrow_lists(x)
+        return True
+    except (TypeError, ValueError):
+        return False
 
 
 class OnlineLinearLearner(Learner):
@@ -280,7 +294,7 @@ class OnlineLinearLearner(Learner):
             rows = self._prepare_device(features, y)
             if rows is not None:
                 return rows
-        if not isinstance(features, (list, CSR)) and _arrow(features):
+        if not isinstance(features, (list, CSR)) and _arrow(features) and not _arrow_string_lists(features):
             features = features.to_pylist() if hasattr(features, "to_pylist") else features.tolist()
         if self.encoder is None and self._warm is not None and not isinstance(features, CSR):
             feats = self._warm["feature"].tolist()

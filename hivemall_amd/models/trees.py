@@ -883,7 +883,10 @@ class GradientTreeBoostingClassifier(Learner):
         yi = yi.to(self.device)
         K = len(self.classes)
         n, d = X.shape
+        # ``edges=`` (engine kwarg): fixed bin edges, e.g. shared by a data-parallel job and its
+        # single-process reference
         q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer,
+                     edges=self.kw.get("edges"),
                      categorical=parse_attrs(c["attrs"], d))
         self.importance = np.zeros(d)
         g = torch.Generator(device=self.device).manual_seed(self.seed)

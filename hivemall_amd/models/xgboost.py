@@ -129,7 +129,8 @@ class XGBoostTrainer(Learner):
         has_nan = bool(torch.isnan(X).any().item())
         if self.mixer is not None and self.mixer.world > 1:
             has_nan = self.mixer.all_reduce_scalar(float(has_nan), "max") > 0
-        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer, missing=has_nan)
+        q = quantize(X, min(256, int(c["num_bins"])), seed=self.seed, mixer=self.mixer, missing=has_nan,
+                     edges=self.kw.get("edges"))
         F = torch.tensor(self.base_margin, device=dev).repeat(n, 1)
         g = torch.Generator(device=dev).manual_seed(self.seed)
         gcpu = torch.Generator().manual_seed(self.seed)

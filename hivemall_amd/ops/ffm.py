@@ -99,6 +99,13 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
     Per-element G (G shaped like V): views of one packed [NF, FS, 2, Kp] table (FS =
     line-padded field count), or two split tables."""
     if slot_g:
+        if packed and dtype == torch.bfloat16 and kp == 4:
+            # 16-B slots {V bf16 x 4 | G fp32 | 0}: one 16-B access per slot (ffm_pipe_kernel SG)
+            fs = padded_fields(num_fields, kp, dtype)
+            buf = torch.zeros((num_features, fs, 16), dtype=torch.uint8, device=device)
+            V = buf.view(torch.bfloat16)[:, :num_fields, :4]
+            G = buf.view(torch.float32)[:, :num_fields, 2]
+            return V, G
         if packed:
             fs, bs, goff = slot_block_layout(num_fields, kp, dtype)
             es = torch.empty(0, dtype=dtype).element_size()
@@ -153,16 +160,17 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     block = (0, 0)
     if slot_g:
         # one fp32 AdaGrad accumulator per (feature, field) slot: G [NF, NFLD]
-        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) == 1, \
-            "per-slot G: fp32 [num_features, num_fields] with unit field stride"
-        assert V.stride(2) == 1 and V.stride(1) == Kp, "V: [NF, FS, Kp] slots"
+        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) in (1, 4), \
+            "per-slot G: fp32 [num_features, num_fields], field stride 1 (or 4: 16-B bf16 slots)"
+        assert V.stride(2) == 1 and (V.stride(1) == Kp or (G.stride(1) == 4 and V.stride(1) == 2 * Kp)), \
+            "V: [NF, FS, Kp] slots (or the V half of 16-B {V | G | 0} slots)"
         packed = False
         gstride = G.stride(0)
         # block layout (slot_block_layout): G right after the V region of each feature block
         es = V.element_size()
         d = G.data_ptr() - V.data_ptr()
         bs = V.stride(0) * es
-        if V.is_cuda and 0 < d < bs and d % (Kp * es) == 0 and G.stride(0) * 4 == bs:
+        if V.is_cuda and G.stride(1) == 1 and 0 < d < bs and d % (Kp * es) == 0 and G.stride(0) * 4 == bs:
             vpad = d // (Kp * es)
             tail = bs - d - vpad * 4
             if tail >= 0 and tail % 16 == 0:
@@ -180,7 +188,8 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    int(hyper.use_bias), int(hyper.norm), int(grid),
                    int((not packed) if hyper.reload is None else hyper.reload), int(bf16),
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed), _VARIANT,
-                   field_stride(V), int(slot_g), gstride, block[0], block[1]],
+                   field_stride(V), int(slot_g), gstride, block[0], block[1],
+                   G.stride(1) if slot_g else 0],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr

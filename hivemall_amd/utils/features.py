@@ -133,7 +133,37 @@ class FeatureEncoder:
         return [b[off[i]:off[i + 1]].decode("utf-8") for i in range(n)]
 
     # ---------------------------------------------------------------- encode
+    def _encode_packed(self, b: np.ndarray, off: np.ndarray, indptr: np.ndarray, add_new: bool,
+                       shown) -> CSR:
+        nnz = int(indptr[-1])
+        idx = np.empty(nnz, dtype=np.int64)
+        val = np.empty(nnz, dtype=np.float32)
+        mode = {"int": 0, "dict": 1, "hash": 2, "auto": 3}[self.mode]
+        d = self._d() if mode in (1, 3) else None
+        base = self.int_base if self.int_base is not None else self.num_features
+        bad = _native.host().hm_parse_features(b.ctypes.data, off.ctypes.data, nnz, mode, d,
+                                               1 if add_new else 0, self.num_features, self.seed,
+                                               int(base), idx.ctypes.data, val.ctypes.data)
+        if bad >= 0:
+            raise UDFArgumentException(f"malformed feature: '{shown(bad)}'")
+        if mode in (1, 3) and self.vocab_size() > 0:
+            self.saw_strings = True
+        return CSR(indptr, idx, val)
+
     def encode(self, rows: Sequence, add_new: bool = True) -> CSR:
+        from ..io.ingest import arrow_buffers, is_arrow_like, to_arrow_lists
+
+        if is_arrow_like(rows):
+            # Arrow list<string> column: parsed straight from its buffers (no Python object per
+            # feature; a SQL feature_hashing / add_bias result arrives this way)
+            data, so, lo = arrow_buffers(to_arrow_lists(rows))
+            indptr = np.ascontiguousarray(lo, dtype=np.int64)
+            if int(indptr[-1]) == 0:
+                return CSR(indptr, np.zeros(0, np.int64), np.zeros(0, np.float32))
+            b = np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)
+            so = np.ascontiguousarray(so, dtype=np.int64)
+            return self._encode_packed(b, so, indptr, add_new,
+                                       lambda k: bytes(b[so[k]:so[k + 1]]).decode("utf-8", "replace"))
         rows = [([] if r is None else r) for r in rows]
         lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=len(rows))
         indptr = np.zeros(len(rows) + 1, dtype=np.int64)
@@ -147,19 +177,7 @@ class FeatureEncoder:
         flat = [str(x) for r in rows for x in r]
         buf, off = pack_strings(flat)
         b = np.frombuffer(buf, dtype=np.uint8) if buf else np.zeros(1, np.uint8)
-        idx = np.empty(nnz, dtype=np.int64)
-        val = np.empty(nnz, dtype=np.float32)
-        mode = {"int": 0, "dict": 1, "hash": 2, "auto": 3}[self.mode]
-        d = self._d() if mode in (1, 3) else None
-        base = self.int_base if self.int_base is not None else self.num_features
-        bad = _native.host().hm_parse_features(b.ctypes.data, off.ctypes.data, nnz, mode, d,
-                                               1 if add_new else 0, self.num_features, self.seed,
-                                               int(base), idx.ctypes.data, val.ctypes.data)
-        if bad >= 0:
-            raise UDFArgumentException(f"malformed feature: '{flat[bad]}'")
-        if mode in (1, 3) and self.vocab_size() > 0:
-            self.saw_strings = True
-        return CSR(indptr, idx, val)
+        return self._encode_packed(b, off, indptr, add_new, lambda k: flat[k])
 
     def decode(self, ids: np.ndarray) -> list:
         """Map indices back to feature names (ints stay ints)."""
@@ -180,21 +198,43 @@ class FeatureEncoder:
         return out
 
 
+class _LazyStrings:
+    """``flat[k]`` of a packed string buffer (error messages only)."""
+
+    def __init__(self, b, off):
+        self.b, self.off = b, off
+
+    def __getitem__(self, k):
+        return bytes(self.b[self.off[k]:self.off[k + 1]]).decode("utf-8", "replace")
+
+
 def parse_ffm_rows(rows: Sequence, num_features: int, num_fields: int, hash_ints: bool = False,
                    seed: int = DEFAULT_SEED) -> CSR:
-    """Parse rows of ``field:index[:value]`` strings (FFM input)."""
-    rows = [([] if r is None else r) for r in rows]
-    lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=len(rows))
-    indptr = np.zeros(len(rows) + 1, dtype=np.int64)
-    np.cumsum(lens, out=indptr[1:])
+    """Parse rows of ``field:index[:value]`` strings (FFM input; Python lists or an Arrow
+    list<string> column, the latter straight from its buffers)."""
+    from ..io.ingest import arrow_buffers, is_arrow_like, to_arrow_lists
+
+    if is_arrow_like(rows):
+        data, off, lo = arrow_buffers(to_arrow_lists(rows))
+        indptr = np.ascontiguousarray(lo, dtype=np.int64)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        b = np.ascontiguousarray(data) if len(data) else np.zeros(1, np.uint8)
+        flat = _LazyStrings(b, off)
+    else:
+        rows = [([] if r is None else r) for r in rows]
+        lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=len(rows))
+        indptr = np.zeros(len(rows) + 1, dtype=np.int64)
+        np.cumsum(lens, out=indptr[1:])
+        flat = None
     nnz = int(indptr[-1])
     fld = np.empty(nnz, dtype=np.int32)
     idx = np.empty(nnz, dtype=np.int32)
     val = np.empty(nnz, dtype=np.float32)
     if nnz:
-        flat = [str(x) for r in rows for x in r]
-        buf, off = pack_strings(flat)
-        b = np.frombuffer(buf, dtype=np.uint8) if buf else np.zeros(1, np.uint8)
+        if flat is None:
+            flat = [str(x) for r in rows for x in r]
+            buf, off = pack_strings(flat)
+            b = np.frombuffer(buf, dtype=np.uint8) if buf else np.zeros(1, np.uint8)
         bad = _native.host().hm_parse_ffm_features(b.ctypes.data, off.ctypes.data, nnz,
                                                    int(num_features), int(num_fields),
                                                    1 if hash_ints else 0, seed, fld.ctypes.data,

@@ -288,3 +288,58 @@ def test_fm_mf_bpr_data_parallel_replicas_identical():
     out = run_world("_fm_mf_bpr_dp")
     for mode in ("dense", " -mix_sparse"):
         assert out[0][mode] == pytest.approx(out[1][mode], rel=1e-5, abs=1e-5)
+
+
+def _gbt_union_equal(ctx):
+    """World-2 row-sharded boosting with fixed bin edges vs ONE process on the union of the
+    shards: histograms are additive, so the trees must be the same up to float summation order."""
+    import numpy as np
+
+    from hivemall_amd.io.synthetic import higgs_like
+    from hivemall_amd.models.trees import GradientTreeBoostingClassifier, quantize
+    from hivemall_amd.models.xgboost import XGBoostTrainer
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    X, y = higgs_like(6000, seed=40)
+    edges = quantize(X, 64).edges
+    mine = slice(ctx.rank, None, ctx.world_size)
+    opts = "-trees 4 -max_depth 4 -subsample 1.0 -seed 5 -num_bins 64"
+    xopts = "-num_round 4 -max_depth 4 -num_bins 64"
+    dp = GradientTreeBoostingClassifier(opts, device="cpu", mixer=ModelMixer(ctx), rank=ctx.rank,
+                                        edges=edges).fit(X[mine], y[mine].long())
+    xdp = XGBoostTrainer(xopts, device="cpu", mixer=ModelMixer(ctx), rank=ctx.rank, edges=edges).fit(X[mine], y[mine])
+    one = GradientTreeBoostingClassifier(opts, device="cpu", edges=edges).fit(X, y.long())
+    xone = XGBoostTrainer(xopts, device="cpu", edges=edges).fit(X, y)
+    Xt, _ = higgs_like(2000, seed=41)
+    feats = lambda m: [t.feature for it in m.iters for t in it]
+    xfeats = lambda m: [t.feature for rt in m.trees for t in rt]
+    return {"feat_dp": feats(dp), "feat_one": feats(one), "p_dp": dp.predict_proba(Xt), "p_one": one.predict_proba(Xt),
+            "xfeat_dp": xfeats(xdp), "xfeat_one": xfeats(xone),
+            "xp_dp": xdp.margin(Xt).cpu().numpy(), "xp_one": xone.margin(Xt).cpu().numpy()}
+
+
+def test_boosting_data_parallel_equals_single_process_on_union():
+    import numpy as np
+
+    out = run_world("_gbt_union_equal")
+    for r in (0, 1):
+        o = out[r]
+        assert o["feat_dp"] == o["feat_one"] and o["xfeat_dp"] == o["xfeat_one"]
+        np.testing.assert_allclose(o["p_dp"], o["p_one"], atol=1e-5)
+        np.testing.assert_allclose(o["xp_dp"], o["xp_one"], atol=1e-4)
+
+
+def test_bench_configs_n_gpu_entry_point_cpu_world2():
+    """benchmarks/bench_configs.py --gpus 2 (BASELINE configs 4 and 5): self-launches 2 ranks
+    (gloo here) and rank 0 prints one JSON line per config with the world fields."""
+    cmd = [sys.executable, os.path.join(ROOT, "benchmarks", "bench_configs.py"), "--gpus", "2", "--small",
+           "gbdt", "rf", "bprmf"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [d["bench"] for d in recs] == ["gbdt", "rf", "bprmf"]
+    for d in recs:
+        assert d["world"] == 2 and d["n_gpus"] == 2 and d["dist_backend"] == "gloo"
+    assert recs[1]["trees_in_forest"] == 4
+    assert 0.6 < recs[0]["test_auc"] and 0.6 < recs[2]["sampled_auc"]
