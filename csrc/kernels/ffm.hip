@@ -51,7 +51,7 @@ struct FFMParams {
     int vpad;              // per-slot G block layout: V slots per feature block (0: separate tables)
     int tail16;            // per-slot G block layout: zero 16-B chunks after each G region
     int gfstride;          // per-slot G: floats between consecutive fields (1, or 4 in 16-B slots)
-    int sg_threads;        // ffm_sg_kernel block size (256 default; 512 for A/B)
+    int sg_threads;        // ffm_sg_kernel block size 256 / 512; 0 = fp32 V: ffm_pipe_sg32_kernel
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
                            // table pads each feature block to whole 128-B lines)
@@ -922,12 +922,245 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                                             pack_sr_hi(g1, rotl32(h, 12), rotl32(h, 28)));
                 if (wr >> j & 1u) *reinterpret_cast<uint4*>(vg + off[j]) = st;
             }
-            if (mi >= 0) {
-                // the feature block's pad slots (never read): zeros, completing its last line
-                for (int f = P.num_fields; f < (int)nfld; ++f) {
-                    *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * SLOT_B) = make_uint4(0u, 0u, 0u, 0u);
-                    if (!BF) *reinterpret_cast<uint4*>(vg + ((uint32_t)mi * nfld + (uint32_t)f) * SLOT_B + 16u) = make_uint4(0u, 0u, 0u, 0u);
+            // the feature blocks' pad slots (never read): zeros, completing their last lines;
+            // written by wave 0 (wave W_LIN has the FTRL updates: one wave doing both was the
+            // last to reach the barrier, cf. ffm_pipe_sg32_kernel)
+            if (wave == 0 && lane < F) {
+                const int pi = s_m[cur][lane].x;
+                if (pi >= 0) {
+                    for (int f = P.num_fields; f < (int)nfld; ++f) {
+                        *reinterpret_cast<uint4*>(vg + ((uint32_t)pi * nfld + (uint32_t)f) * SLOT_B) = make_uint4(0u, 0u, 0u, 0u);
+                        if (!BF) *reinterpret_cast<uint4*>(vg + ((uint32_t)pi * nfld + (uint32_t)f) * SLOT_B + 16u) = make_uint4(0u, 0u, 0u, 0u);
+                    }
                 }
+            }
+            if (mi >= 0) {
+                if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
+                    const float lz = s_lin[cur][1][lane];
+                    const float ln = s_lin[cur][2][lane];
+                    const float g = kappa * mx * scale;
+                    const float n1 = ln + g * g;
+                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                    wz[mi] = z1;
+                    wn[mi] = n1;
+                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                }
+            }
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
+        }
+        // ---- F: linear state of the next row (after this row's FTRL stores) ----
+        if (more) dma_lin(nxt);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
+#undef SA
+#undef SB
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout of
+// ffm_sg_kernel ([V: FS x 16 B | G: FS x fp32 | zero tail] per feature, 896 B): the schedule of
+// ffm_pipe_kernel (A..F above) with two DMAs per slot (V 16 B, G 4 B) into separate landing
+// zones.  The register-prefetch ffm_sg_kernel reached 66-68 M rows/s (70 % of this layout's
+// access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log); here no VGPR holds the
+// next row and the LDS image is the only staging (55 KB per block -> 2 blocks/CU).
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffm_pipe_sg32_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
+    float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * 256];    // V DMA landing zone
+    __shared__ __attribute__((aligned(16))) float s_rg[NS * 256];     // G DMA landing zone
+    __shared__ __attribute__((aligned(16))) float4 s_t[NS * 256];     // transposed V image
+    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
+    __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
+    __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
+    __shared__ float s_red[8];                                        // [0..3] sums, [4+b] scale
+    const int F = P.F;
+    const int FF = F * F;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
+    const uint32_t vfs = (uint32_t)P.fstride * 16u;                  // V bytes between features
+    const uint32_t gfs = (uint32_t)P.gstride * 4u;                   // G bytes between features
+    const int G = gridDim.x;
+    char* vb = reinterpret_cast<char*>(Vt);
+    char* gb = reinterpret_cast<char*>(Gt);
+
+    int ab[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
+    }
+#define SA(j) (ab[j] & 0xFF)
+#define SB(j) (ab[j] >> 8)
+
+    auto dma_meta = [&](int bf, int row) {
+        if (wave == W_DMA && lane < F && row < P.B) {
+            const size_t o = (size_t)row * F + lane;
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(idx + o), (lds_ptr_t)&s_mr[bf][0][0], 4, 0, 0);
+            if (fld) __builtin_amdgcn_global_load_lds((glb_ptr_t)(fld + o), (lds_ptr_t)&s_mr[bf][1][0], 4, 0, 0);
+            if (val) __builtin_amdgcn_global_load_lds((glb_ptr_t)(val + o), (lds_ptr_t)&s_mr[bf][2][0], 4, 0, 0);
+        }
+    };
+    auto publish_meta = [&](int bf) {
+        if (wave == W_META) {
+            float sq = 0.f;
+            if (lane < F) {
+                int ri = s_mr[bf][0][lane];
+                int rf = fld ? s_mr[bf][1][lane] : lane;
+                float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
+                if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
+                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
+                sq = rx * rx;
+            }
+            const float tot = hm::wave_sum_uniform(sq);
+            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+        }
+    };
+    // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal, 0 = dead
+    auto slot = [&](int bf, int j, uint32_t& ov, uint32_t& og, float& xab) -> uint32_t {
+        const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
+        const bool live = ok && SA(j) != SB(j);
+        const uint32_t i = ok ? (uint32_t)ma.x : 0u, f = ok ? (uint32_t)mb.y : 0u;
+        ov = i * vfs + f * 16u;
+        og = i * gfs + f * 4u;
+        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+        return live ? 1u : (ok ? 2u : 0u);
+    };
+    auto dma_slots = [&](int bf) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t ov, og;
+            float xab;
+            slot(bf, j, ov, og, xab);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * 256 + wave * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * 256 + wave * 64), 4, 0, 0);
+        }
+    };
+    auto dma_lin = [&](int bf) {
+        if (P.use_linear && wave == W_LIN && lane < F) {
+            const int i = s_m[bf][lane].x;
+            if (i >= 0) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                if (P.train) {
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                }
+            }
+        }
+    };
+
+    int row = blockIdx.x;
+    if (row >= P.B) return;
+    dma_meta(0, row);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    bar_raw();
+    publish_meta(0);
+    bar_raw();
+    dma_slots(0);
+    dma_lin(0);
+    dma_meta(1, row + G);
+
+    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
+        const int nxt = cur ^ 1;
+        const bool more = row + G < P.B;
+        // ---- A: this wave's DMAs have landed, then every wave's ----
+        __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
+        bar_raw();
+        // ---- B: landing zone -> registers (G) and the transposed image (V); meta(row + G) ----
+        float cg[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            cg[j] = s_rg[j * 256 + tid];
+            if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = s_rv[j * 256 + tid];
+        }
+        if (more) publish_meta(nxt);
+        bar_raw();
+        // ---- C: next row's slot DMA (the landing zones are free: read in B), its meta after ----
+        if (more) {
+            dma_slots(nxt);
+            dma_meta(cur, row + 2 * G);
+        }
+        const float scale = s_red[4 + cur];
+        int mi = -1;
+        float mx = 0.f, lw = 0.f;
+        if (wave == W_LIN && lane < F) {
+            const int4 m = s_m[cur][lane];
+            mi = m.x;
+            mx = __int_as_float(m.z);
+            lw = s_lin[cur][0][lane];
+        }
+        // ---- D: forward ----
+        uint32_t live = 0u, wr = 0u;
+        float xab[NS];
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t ov, og;
+            const uint32_t k = slot(cur, j, ov, og, xab[j]);
+            live |= (k & 1u) << j;
+            wr |= (uint32_t)(k != 0u) << j;
+            const int s = tid + j * 256;
+            const float4 pv = s_t[s < FF ? s : 0];
+            const float4 cv = s_t[SB(j) * F + SA(j)];
+            part += (cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w) * xab[j];
+        }
+        part *= 0.5f * scale * scale;
+        part += lw * mx * scale;
+        part = hm::wave_sum_uniform(part);
+        if (lane == 0) s_red[wave] = part;
+        bar_raw();
+        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        if (P.use_bias) p += bias_w0(P, bias);
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- E: updates ----
+        if (P.train) {
+            const float ks = kappa * scale * scale;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (!(wr >> j & 1u)) continue;
+                uint32_t ov, og;
+                float xj;
+                slot(cur, j, ov, og, xj);
+                const int s = tid + j * 256;
+                const float4 pv = s_t[s];
+                const float4 cv = s_t[SB(j) * F + SA(j)];
+                const float c = ks * xab[j];
+                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
+                const f2 cc = {c, c}, ll = {lj, lj};
+                f2 o0 = f2{cv.x, cv.y}, o1 = f2{cv.z, cv.w};
+                const f2 p0 = f2{pv.x, pv.y}, p1 = f2{pv.z, pv.w};
+                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
+                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
+                const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
+                const f2 rr = {r, r};
+                o0 = o0 + rr * d0;
+                o1 = o1 + rr * d1;
+                *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                *reinterpret_cast<float*>(gb + og) = gs;
+            }
+            // the row's features' pad slots and block tails (never read): zeros, so every line a
+            // row touches is written whole; spread over all threads (one wave doing them all
+            // was the last to reach the barrier)
+            {
+                const int npad = P.vpad - P.num_fields;
+                const int per = 2 * npad + P.tail16;
+                for (int q = tid; q < F * per; q += 256) {
+                    const int a = q / per, kk = q - a * per;
+                    const int i = s_m[cur][a].x;
+                    if (i < 0) continue;
+                    char* vblk = vb + (uint32_t)i * vfs;
+                    char* gblk = gb + (uint32_t)i * gfs;
+                    if (kk < npad) *reinterpret_cast<uint4*>(vblk + (P.num_fields + kk) * 16) = make_uint4(0u, 0u, 0u, 0u);
+                    else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
+                    else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
+            if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
                     const float lz = s_lin[cur][1][lane];
                     const float ln = s_lin[cur][2][lane];
@@ -1192,16 +1425,23 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(TH == 512 ? 
                 }
                 *reinterpret_cast<float*>(gb + og) = gs;
             }
-            if (mi >= 0) {
-                // the feature block's pad slots and tail (never read): zeros, completing its lines
-                char* vblk = vb + (uint32_t)mi * vfs;
-                char* gblk = gb + (uint32_t)mi * gfs;
-                for (int f = P.num_fields; f < P.vpad; ++f) {
-                    *reinterpret_cast<Img*>(vblk + f * VSB) = Img{};
-                    *reinterpret_cast<float*>(gblk + f * 4) = 0.f;
+            // the row's features' pad slots and block tails (never read): zeros, completing their
+            // lines; spread over all threads (one wave doing them was the last at the barrier)
+            {
+                const int npad = P.vpad - P.num_fields;
+                const int per = 2 * npad + P.tail16;
+                for (int q = tid; q < F * per; q += TH) {
+                    const int a = q / per, kk = q - a * per;
+                    const int i = s_m[cur][a].x;
+                    if (i < 0) continue;
+                    char* vblk = vb + (uint32_t)i * vfs;
+                    char* gblk = gb + (uint32_t)i * gfs;
+                    if (kk < npad) *reinterpret_cast<Img*>(vblk + (P.num_fields + kk) * VSB) = Img{};
+                    else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
+                    else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
                 }
-                for (int t = 0; t < P.tail16; ++t)
-                    *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * t) = make_uint4(0u, 0u, 0u, 0u);
+            }
+            if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the prefetched (w, z, n)
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
@@ -1297,9 +1537,20 @@ int dispatch_sg(const FFMParams& P, const int32_t* idx, const int32_t* fld, cons
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
+    if (!BF && P.sg_threads == 0) {
+        // fp32 V: the LDS-DMA pipeline (variant 5 selects the register-prefetch kernel below)
+#define HM_P32(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
+                                       fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+        if (need <= 2) { HM_P32(2); }
+        else if (need <= 4) { HM_P32(4); }
+        else if (need <= 6) { HM_P32(6); }
+        else { HM_P32(8); }
+#undef HM_P32
+        HM_LAUNCH_RET();
+    }
     // 256 threads at 4 waves/SIMD (128 VGPRs, no spill: 4 rows in flight per CU); 512 threads
     // (half the slots per thread; 3 blocks per CU) is variant 4 (A/B)
-    if (P.sg_threads == 256) {
+    if (P.sg_threads != 512) {
 #define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF, 256>), dim3(blocks), dim3(256), 0, stream, P, idx, \
                                       fld, val, y, V, G, w, wz, wn, bias, pred, loss)
         if (need <= 2) { HM_SG(2); }
@@ -1394,7 +1645,8 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             separate [.][.][Kp] tables.
 // variant: 0 = auto (per-slot: ffm_sg_kernel; per-element bf16: ffm_pipe_kernel, fp32:
 // ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel, 3 = ffm_pipe_kernel,
-// 4 = ffm_sg_kernel with 512-thread blocks (default 256).
+// 4 = ffm_sg_kernel with 512-thread blocks, 5 = ffm_sg_kernel (256) for fp32 V (default there:
+// ffm_pipe_sg32_kernel).
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -1415,7 +1667,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.vpad = ip[19];
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
-    P.sg_threads = variant == 4 ? 512 : 256;
+    P.sg_threads = variant == 4 ? 512 : (variant == 5 ? 256 : 0);   // 0: fp32 LDS-DMA pipeline
     if (slot_g && P.gfstride == 4) P.sstride = 2 * P.Kp;   // 16-B {V | G | 0} slots (bf16, Kp 4)
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
