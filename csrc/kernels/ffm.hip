@@ -1182,6 +1182,227 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #undef SB
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined kernel for per-slot AdaGrad with bf16 V in 12-B slots {V bf16 x 4 | G fp32}:
+// 40 slots per feature = 480 B + a 32-B zero tail = one 512-B block (4 lines; the 16-B
+// {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
+// per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
+// footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
+    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
+    float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
+    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
+{
+    // 12-B slot landing zone: global_load_lds_dwordx3 lands each lane at a 16-B stride
+    // (measured: benchmarks/lds_dma12_probe.py, profiles/ffm_r3/lds_dma12_probe.log)
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[NS * 256 * 4];
+    __shared__ __attribute__((aligned(16))) uint2 s_t[NS * 256];            // transposed V image
+    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];
+    __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];
+    __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];
+    __shared__ float s_red[8];
+    const int F = P.F;
+    const int FF = F * F;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
+    const uint32_t bs = (uint32_t)P.gstride * 4u;                    // block bytes per feature
+    const int G = gridDim.x;
+    char* vb = reinterpret_cast<char*>(Vt);
+    typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+
+    int ab[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int s = tid + j * 256;
+        ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
+    }
+#define SA(j) (ab[j] & 0xFF)
+#define SB(j) (ab[j] >> 8)
+    const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
+
+    auto dma_meta = [&](int bf, int row) {
+        if (wave == W_DMA && lane < F && row < P.B) {
+            const size_t o = (size_t)row * F + lane;
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(idx + o), (lds_ptr_t)&s_mr[bf][0][0], 4, 0, 0);
+            if (fld) __builtin_amdgcn_global_load_lds((glb_ptr_t)(fld + o), (lds_ptr_t)&s_mr[bf][1][0], 4, 0, 0);
+            if (val) __builtin_amdgcn_global_load_lds((glb_ptr_t)(val + o), (lds_ptr_t)&s_mr[bf][2][0], 4, 0, 0);
+        }
+    };
+    auto publish_meta = [&](int bf) {
+        if (wave == W_META) {
+            float sq = 0.f;
+            if (lane < F) {
+                int ri = s_mr[bf][0][lane];
+                int rf = fld ? s_mr[bf][1][lane] : lane;
+                float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
+                if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
+                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
+                sq = rx * rx;
+            }
+            const float tot = hm::wave_sum_uniform(sq);
+            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+        }
+    };
+    auto slot = [&](int bf, int j, uint32_t& off, float& xab) -> uint32_t {
+        const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
+        const bool live = ok && SA(j) != SB(j);
+        off = ok ? (uint32_t)ma.x * bs + (uint32_t)mb.y * 12u : 0u;
+        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
+        return live ? 1u : (ok ? 2u : 0u);
+    };
+    auto dma_slots = [&](int bf) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t off;
+            float xab;
+            slot(bf, j, off, xab);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + off), (lds_ptr_t)(s_raw + (j * 256 + wave * 64) * 4),
+                                             12, 0, 0);
+        }
+    };
+    auto dma_lin = [&](int bf) {
+        if (P.use_linear && wave == W_LIN && lane < F) {
+            const int i = s_m[bf][lane].x;
+            if (i >= 0) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                if (P.train) {
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                }
+            }
+        }
+    };
+
+    int row = blockIdx.x;
+    if (row >= P.B) return;
+    dma_meta(0, row);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    bar_raw();
+    publish_meta(0);
+    bar_raw();
+    dma_slots(0);
+    dma_lin(0);
+    dma_meta(1, row + G);
+
+    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
+        const int nxt = cur ^ 1;
+        const bool more = row + G < P.B;
+        __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
+        bar_raw();
+        // ---- B: landing zone -> G registers + transposed V image ----
+        float cg[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const uint32_t* q = s_raw + (j * 256 + tid) * 4;
+            cg[j] = __uint_as_float(q[2]);
+            if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = make_uint2(q[0], q[1]);
+        }
+        if (more) publish_meta(nxt);
+        bar_raw();
+        if (more) {
+            dma_slots(nxt);
+            dma_meta(cur, row + 2 * G);
+        }
+        const float scale = s_red[4 + cur];
+        int mi = -1;
+        float mx = 0.f, lw = 0.f;
+        if (wave == W_LIN && lane < F) {
+            const int4 m = s_m[cur][lane];
+            mi = m.x;
+            mx = __int_as_float(m.z);
+            lw = s_lin[cur][0][lane];
+        }
+        // ---- D: forward ----
+        uint32_t live = 0u, wr = 0u;
+        float xab[NS];
+        float part = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            uint32_t off;
+            const uint32_t k = slot(cur, j, off, xab[j]);
+            live |= (k & 1u) << j;
+            wr |= (uint32_t)(k != 0u) << j;
+            const int s = tid + j * 256;
+            const uint2 pv = s_t[s < FF ? s : 0];
+            const uint2 cv = s_t[SB(j) * F + SA(j)];
+            part += dot2_bf16(cv.x, pv.x, dot2_bf16(cv.y, pv.y, 0.f)) * xab[j];
+        }
+        part *= 0.5f * scale * scale;
+        part += lw * mx * scale;
+        part = hm::wave_sum_uniform(part);
+        if (lane == 0) s_red[wave] = part;
+        bar_raw();
+        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        if (P.use_bias) p += bias_w0(P, bias);
+        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
+
+        // ---- E: updates ----
+        if (P.train) {
+            const float ks = kappa * scale * scale;
+            uint32_t hrow = (P.seed ^ ((uint32_t)row * 0x85EBCA77u)) + tid_h;
+            hrow ^= hrow >> 16;
+            hrow *= 0x7FEB352Du;
+            hrow ^= hrow >> 15;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                if (!(wr >> j & 1u)) continue;
+                uint32_t off;
+                float xj;
+                slot(cur, j, off, xj);
+                const int s = tid + j * 256;
+                const uint2 pv = s_t[s];
+                const uint2 cv = s_t[SB(j) * F + SA(j)];
+                const float c = ks * xab[j];
+                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
+                const f2 cc = {c, c}, ll = {lj, lj};
+                f2 o0 = bf2_to_f2(cv.x), o1 = bf2_to_f2(cv.y);
+                const f2 p0 = bf2_to_f2(pv.x), p1 = bf2_to_f2(pv.y);
+                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
+                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
+                const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
+                const f2 rr = {r, r};
+                o0 = o0 + rr * d0;
+                o1 = o1 + rr * d1;
+                const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
+                *reinterpret_cast<u3v*>(vb + off) = u3v{pack_sr_hi(o0, h, rotl32(h, 16)),
+                                                        pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
+                                                        __float_as_uint(gs)};
+            }
+            // pad slots + block tails of the row's features, spread over all threads
+            {
+                const int npad = P.vpad - P.num_fields;
+                const int per = npad + P.tail16;
+                for (int q = tid; q < F * per; q += 256) {
+                    const int a = q / per, kk = q - a * per;
+                    const int i = s_m[cur][a].x;
+                    if (i < 0) continue;
+                    char* blk = vb + (uint32_t)i * bs;
+                    if (kk < npad) *reinterpret_cast<u3v*>(blk + (P.num_fields + kk) * 12) = u3v{0u, 0u, 0u};
+                    else *reinterpret_cast<uint4*>(blk + P.vpad * 12 + 16 * (kk - npad)) = make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
+            if (mi >= 0 && P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
+                const float lz = s_lin[cur][1][lane];
+                const float ln = s_lin[cur][2][lane];
+                const float g = kappa * mx * scale;
+                const float n1 = ln + g * g;
+                const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                wz[mi] = z1;
+                wn[mi] = n1;
+                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+            }
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
+        }
+        if (more) dma_lin(nxt);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#undef SA
+#undef SB
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // Per-slot-AdaGrad pipelined kernel (the GPU default; K <= 4, F <= 45): one fp32 accumulator per
@@ -1506,6 +1727,25 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
+// Per-slot-G in 12-B bf16 slots {V | G}, 512-B feature blocks (Kp == 4, F <= 45, table < 4 GiB).
+int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+                  float* pred, float* loss, int grid, hipStream_t stream) {
+    if (P.Kp != 4 || P.F > 45) return -1;
+    if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
+    const int need = (P.F * P.F + 255) / 256;
+    const int blocks = default_blocks(P.B, grid);
+    if (blocks <= 0) return 0;
+#define HM_P12(NSV) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
+                                       fld, val, y, VG, w, wz, wn, bias, pred, loss)
+    if (need <= 2) { HM_P12(2); }
+    else if (need <= 4) { HM_P12(4); }
+    else if (need <= 6) { HM_P12(6); }
+    else { HM_P12(8); }
+#undef HM_P12
+    HM_LAUNCH_RET();
+}
+
 // Per-slot-G in 16-B bf16 slots {V | G | 0} (Kp == 4, F <= 45, table < 4 GiB); -1 otherwise.
 int dispatch_sg16(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
@@ -1609,6 +1849,12 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
              float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream) {
     if (slot_g) {
+        if (P.gfstride == 3) {
+            // 12-B {V | G} slots: only the pipelined kernel knows this layout
+            if (!BF) return (int)hipErrorInvalidValue;
+            const int rc = dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+            return rc == -1 ? (int)hipErrorInvalidValue : rc;
+        }
         if (variant != 1 && BF && P.gfstride == 4 && P.vpad == 0 &&
             reinterpret_cast<char*>(G) == reinterpret_cast<char*>(V) + 8) {
             const int rc = dispatch_sg16(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
@@ -1675,7 +1921,12 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
     if (slot_g) {
         if (packed || P.gstride < P.num_fields || P.tail16 < 0) return (int)hipErrorInvalidValue;
-        if (P.vpad > 0) {
+        if (P.gfstride == 3) {
+            // 12-B {V | G} slots: G = V + 8 B, vpad slots of 12 B then a zero tail per block
+            if (!bf16 || P.Kp != 4 || reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + 8 ||
+                P.vpad < P.num_fields || (size_t)P.vpad * 12 + (size_t)P.tail16 * 16 != (size_t)P.gstride * 4)
+                return (int)hipErrorInvalidValue;
+        } else if (P.vpad > 0) {
             // block layout: G right after the V region of the same feature block
             const size_t es = bf16 ? 2 : 4;
             if (reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + (size_t)P.vpad * P.Kp * es ||

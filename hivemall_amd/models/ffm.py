@@ -335,7 +335,7 @@ def _is_block(V: torch.Tensor, G: torch.Tensor) -> bool:
     es = V.element_size()
     if G.dim() != 2 or not V.is_cuda:
         return False
-    if G.stride(1) == 4:
+    if G.stride(1) in (3, 4):
         return G.data_ptr() - V.data_ptr() == 8 and V.dtype == torch.bfloat16
     return 0 < G.data_ptr() - V.data_ptr() < V.stride(0) * es and G.stride(0) * 4 == V.stride(0) * es
 

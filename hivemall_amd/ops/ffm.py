@@ -89,6 +89,14 @@ def slot_block_layout(num_fields: int, kp: int, dtype) -> tuple[int, int, int]:
     return fs, bs, goff
 
 
+def slot12_layout(num_fields: int) -> tuple[int, int]:
+    """12-B slot layout of bf16 V with per-slot G (GPU, k <= 4): per feature FS slots
+    {V bf16 x 4 | G fp32} then a zero tail, the block padded to whole 128-B lines (39 fields:
+    40 x 12 = 480 B + 32 -> 512 B = 4 lines).  Returns (FS, block bytes)."""
+    fs = (num_fields + 3) // 4 * 4            # FS * 12 is a multiple of 16: the tail is 16-B chunks
+    return fs, (fs * 12 + 127) // 128 * 128
+
+
 def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
                      packed: bool, slot_g: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """Zeroed (V, G).
@@ -99,7 +107,16 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
     Per-element G (G shaped like V): views of one packed [NF, FS, 2, Kp] table (FS =
     line-padded field count), or two split tables."""
     if slot_g:
-        if packed and dtype == torch.bfloat16 and kp == 4:
+        lay = os.environ.get("HM_FFM_BF16_LAYOUT", "slot12")
+        if packed and dtype == torch.bfloat16 and kp == 4 and lay == "slot12":
+            # 12-B slots {V bf16 x 4 | G fp32} in 512-B blocks (ffm_pipe_sg12_kernel)
+            fs, bs = slot12_layout(num_fields)
+            buf = torch.zeros((num_features, bs), dtype=torch.uint8, device=device)
+            sl = buf[:, :fs * 12]
+            V = sl.view(torch.bfloat16).view(num_features, fs, 6)[:, :num_fields, :4]
+            G = sl.view(torch.float32).view(num_features, fs, 3)[:, :num_fields, 2]
+            return V, G
+        if packed and dtype == torch.bfloat16 and kp == 4 and lay == "slot16":
             # 16-B slots {V bf16 x 4 | G fp32 | 0}: one 16-B access per slot (ffm_pipe_kernel SG)
             fs = padded_fields(num_fields, kp, dtype)
             buf = torch.zeros((num_features, fs, 16), dtype=torch.uint8, device=device)
@@ -160,17 +177,21 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     block = (0, 0)
     if slot_g:
         # one fp32 AdaGrad accumulator per (feature, field) slot: G [NF, NFLD]
-        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) in (1, 4), \
-            "per-slot G: fp32 [num_features, num_fields], field stride 1 (or 4: 16-B bf16 slots)"
-        assert V.stride(2) == 1 and (V.stride(1) == Kp or (G.stride(1) == 4 and V.stride(1) == 2 * Kp)), \
-            "V: [NF, FS, Kp] slots (or the V half of 16-B {V | G | 0} slots)"
+        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) in (1, 3, 4), \
+            "per-slot G: fp32 [num_features, num_fields], field stride 1 (or 3 / 4: 12-B / 16-B bf16 slots)"
+        assert V.stride(2) == 1 and (V.stride(1) == Kp or (G.stride(1) in (3, 4) and V.stride(1) == 2 * G.stride(1))), \
+            "V: [NF, FS, Kp] slots (or the V part of 12-B / 16-B {V | G} slots)"
         packed = False
         gstride = G.stride(0)
         # block layout (slot_block_layout): G right after the V region of each feature block
         es = V.element_size()
         d = G.data_ptr() - V.data_ptr()
         bs = V.stride(0) * es
-        if V.is_cuda and G.stride(1) == 1 and 0 < d < bs and d % (Kp * es) == 0 and G.stride(0) * 4 == bs:
+        if G.stride(1) == 3:
+            fs, bs12 = slot12_layout(NFLD)
+            assert V.is_cuda and bf16 and d == 8 and G.stride(0) * 4 == bs12, "12-B slot layout"
+            block = (fs, (bs12 - fs * 12) // 16)
+        elif V.is_cuda and G.stride(1) == 1 and 0 < d < bs and d % (Kp * es) == 0 and G.stride(0) * 4 == bs:
             vpad = d // (Kp * es)
             tail = bs - d - vpad * 4
             if tail >= 0 and tail % 16 == 0:
