@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import hashlib
 import math
-import random
 from collections import Counter, defaultdict
 from typing import Iterable, Sequence
 
@@ -420,12 +419,19 @@ def amplify(xtimes, *cols):
 
 
 class RandAmplifier:
-    """``rand_amplify(xtimes, num_buffers, *cols)``: rows are amplified and emitted in a
-    shuffled order through a reservoir of ``num_buffers`` rows (seeded)."""
+    """``rand_amplify(xtimes, num_buffers, *cols [, '-seed N'])``: rows are amplified and
+    emitted in a shuffled order through a reservoir of ``num_buffers`` rows (upstream
+    ftvec/amplify/RandomAmplifierUDTF.java + utils/collections/RandomizedAmplifier.java).
+    ``run`` is a generator: it holds at most ``num_buffers`` rows, never the whole input.
+    Draws come from ``java.util.Random`` (``JavaRandom``) seeded with ``seed``."""
 
     def __init__(self, xtimes: int, num_buffers: int, seed: int = 43):
+        from ..utils.prng import JavaRandom
+
         self.x, self.nb = int(xtimes), int(num_buffers)
-        self.rng = random.Random(seed)
+        if self.x < 1 or self.nb < 1:
+            raise ValueError("rand_amplify: xtimes and num_buffers must be >= 1")
+        self.rng = JavaRandom(seed)
 
     def run(self, rows: Iterable[tuple]):
         buf = []
@@ -434,21 +440,40 @@ class RandAmplifier:
                 if len(buf) < self.nb:
                     buf.append(r)
                 else:
-                    i = self.rng.randrange(len(buf))
+                    i = self.rng.next_int(len(buf))
                     yield buf[i]
                     buf[i] = r
-        self.rng.shuffle(buf)
+        for i in range(len(buf) - 1, 0, -1):          # Fisher-Yates drain of the reservoir
+            j = self.rng.next_int(i + 1)
+            buf[i], buf[j] = buf[j], buf[i]
         yield from buf
+
+
+_AMPLIFY_OPTS = Options([opt("seed", None, 43, int, "Seed of the reservoir draws")], "rand_amplify")
 
 
 @udtf("rand_amplify", per_row=False)
 def rand_amplify(xtimes, num_buffers, *cols):
+    """Whole-input form: ``cols`` are columns (a trailing ``'-seed N'`` string is the
+    options); the output frame is built from the streamed rows chunk by chunk."""
     x = xtimes[0] if isinstance(xtimes, (list, tuple)) else xtimes
     nb = num_buffers[0] if isinstance(num_buffers, (list, tuple)) else num_buffers
+    seed = 43
+    if cols and isinstance(cols[-1], str):
+        seed = _AMPLIFY_OPTS.parse(cols[-1])["seed"]
+        cols = cols[:-1]
     import pandas as pd
-    rows = list(zip(*cols))
-    out = list(RandAmplifier(x, nb).run(rows))
-    return pd.DataFrame(out, columns=[f"c{i}" for i in range(len(cols))])
+    names = [f"c{i}" for i in range(len(cols))]
+    it = RandAmplifier(x, nb, seed).run(zip(*cols))
+    chunks, chunk = [], []
+    for r in it:
+        chunk.append(r)
+        if len(chunk) == 65536:
+            chunks.append(pd.DataFrame(chunk, columns=names))
+            chunk = []
+    if chunk or not chunks:
+        chunks.append(pd.DataFrame(chunk, columns=names))
+    return chunks[0] if len(chunks) == 1 else pd.concat(chunks, ignore_index=True)
 
 
 # ------------------------------------------------------------------ conversion
@@ -619,13 +644,18 @@ def bpr_sampling(user, pos_items, max_item_id=None, options=None):
     pos = set(int(p) for p in pos_items)
     if len(pos) > mx:
         return
-    rng = random.Random((cl["seed"] * 1000003) ^ hash(user))
+    # the per-user stream is seeded from a stable hash of str(user) (MurmurHash3), never
+    # Python's salted hash(): the same -seed replays the same triples in every process
+    from ..utils.hashing import murmurhash3
+    from ..utils.prng import JavaRandom
+
+    rng = JavaRandom((int(cl["seed"]) * 1000003) ^ (murmurhash3(str(user)) & 0xFFFFFFFF))
     n = max(1, int(round(len(pos) * cl["sampling_rate"])))
     plist = sorted(pos)
     for k in range(n):
-        p = plist[k % len(plist)] if k < len(plist) else rng.choice(plist)
+        p = plist[k % len(plist)] if k < len(plist) else plist[rng.next_int(len(plist))]
         while True:
-            j = rng.randint(0, mx)
+            j = rng.next_int(mx + 1)
             if j not in pos:
                 break
         yield (user, p, j)

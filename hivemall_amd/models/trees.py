@@ -661,27 +661,25 @@ TREE_OPTS = [
 
 
 def _to_dense(features, d=None) -> np.ndarray:
-    """Dense feature rows (arrays of numbers) or sparse 'i:v' strings -> float32 matrix."""
+    """Training rows -> float32 matrix, assembled the way upstream's RandomForest / GBT UDTFs
+    buffer them (``MatrixBuilder.nextRow`` then ``buildMatrix``; utils/matrix.py): dense rows of
+    numbers, sparse ``"i:v"`` strings or int index arrays.  Dense float rows take the fast path
+    straight into an array."""
     rows = list(features)
-    if rows and isinstance(rows[0], (list, tuple, np.ndarray)) and len(rows[0]) and \
-            isinstance(list(rows[0])[0], str):
-        mx = 0
-        parsed = []
-        for r in rows:
-            pr = []
-            for f in r:
-                k, _, v = str(f).partition(":")
-                pr.append((int(k), float(v) if v else 1.0))
-                mx = max(mx, int(k))
-            parsed.append(pr)
-        d = d or mx + 1
-        X = np.zeros((len(rows), d), dtype=np.float32)
-        for i, pr in enumerate(parsed):
-            for k, v in pr:
-                if k < d:
-                    X[i, k] = v
-        return X
-    return np.asarray([list(r) for r in rows], dtype=np.float32)
+    if not rows:
+        return np.zeros((0, d or 0), dtype=np.float32)
+    first = next((r for r in rows if r is not None and len(r)), None)
+    if first is not None and not isinstance(list(first)[0], str) and \
+            all(r is not None and len(r) == len(first) for r in rows):
+        return np.asarray([list(r) for r in rows], dtype=np.float32)
+    from ..utils.matrix import MatrixBuilder
+
+    mb = MatrixBuilder("csr", n_cols=d)
+    for r in rows:
+        if d is not None and r is not None and len(r) and isinstance(list(r)[0], str):
+            r = [f for f in r if int(str(f).partition(":")[0]) < d]   # features past d are dropped
+        mb.next_row(r)
+    return mb.build().to_dense().astype(np.float32)
 
 
 def _encode_classes(yl):

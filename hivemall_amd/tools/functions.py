@@ -18,6 +18,7 @@ import numpy as np
 
 from ..registry import udaf, udf, udtf
 from ..utils import base91 as _b91
+from ..utils.collections import BoundedPriorityQueue
 
 
 def _arr(x):
@@ -292,15 +293,39 @@ def to_ordered_list(values, keys=None, options=None):
         reverse = "-reverse" in toks
         if "-k" in toks:
             k = int(toks[toks.index("-k") + 1])
-            if k < 0:
-                reverse, k = not reverse, -k
-            else:
-                reverse = not reverse if "-reverse" not in toks else reverse
+            # -k N: the N largest keys, largest first; -k -N: the N smallest, smallest first;
+            # -reverse flips the order in both cases
+            reverse = (k > 0) != reverse
+            k = abs(k)
     ks = list(values) if keys is None else list(keys)
-    order = sorted(range(len(ks)), key=lambda i: ks[i], reverse=reverse)
     if k is not None:
-        order = order[:k]
+        if k == 0:
+            return []
+        # top-k through a bounded heap (upstream keeps a BoundedPriorityQueue per group,
+        # tools/list/UDAFToOrderedList.java): O(n log k), ties in arrival order
+        q = BoundedPriorityQueue(k, key=(lambda i: ks[i]) if reverse else (lambda i: _Desc(ks[i])))
+        for i in range(len(ks)):
+            q.offer(i)
+        return [values[i] for i in q.sorted()]
+    order = sorted(range(len(ks)), key=lambda i: ks[i], reverse=reverse)
     return [values[i] for i in order]
+
+
+class _Desc:
+    """Inverts the ordering of a key, so a max-heap keeps the k smallest."""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def __lt__(self, o):
+        return o.v < self.v
+
+    def __gt__(self, o):
+        return self.v < o.v
+
+    def __eq__(self, o):
+        return self.v == o.v
 
 
 @udf("to_bits")

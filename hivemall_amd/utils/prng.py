@@ -6,9 +6,9 @@ SmileRandom,CommonsMathRandom}.java).
   (multiplier 0x5DEECE66D, addend 0xB, seed scrambled with the multiplier), ``nextInt``,
   bounded ``nextInt(n)`` with Java's rejection rule in 32-bit arithmetic, ``nextLong``,
   ``nextDouble`` (26 + 27 bits), ``nextFloat`` and the polar-method ``nextGaussian`` with its
-  cached second value.  Scripts that pass ``-seed`` to a Hivemall function which draws from
-  ``java.util.Random`` (``rand_amplify``, ``bpr_sampling``, the learners' weight init) can thus
-  replay the same stream on the host.
+  cached second value.  ``rand_amplify`` (reservoir draws) and ``bpr_sampling`` (per-user
+  negative draws) take their streams from it, so a ``-seed`` replays the same rows in every
+  process.  The learners' weight init draws on the device (below), not from this class.
 * ``SmileRandom`` / ``CommonsMathRandom`` are Mersenne-Twister generators upstream; here both
   wrap numpy's MT19937 seeded with the same integer (stream parity with Smile / commons-math
   is unpinned: their seeding routines differ from numpy's).

@@ -1,4 +1,4 @@
-"""Host collections (C11), HalfFloat codec (C14), int matrices and vectors (C16)."""
+"""Host collections (C11), HalfFloat codec (C14)."""
 import numpy as np
 import pytest
 from hypothesis import given, settings, strategies as st
@@ -6,8 +6,6 @@ from hypothesis import given, settings, strategies as st
 from hivemall_amd.utils.collections import (BoundedPriorityQueue, Int2FloatOpenHashTable,
                                             Int2LongOpenHashTable, float_to_half_bits,
                                             half_bits_to_float, is_representable_as_half)
-from hivemall_amd.utils.intmatrix import (ColumnMajorDenseIntMatrix2d, ColumnMajorIntMatrix,
-                                          DenseVector, DoKIntMatrix, SparseVector)
 
 
 def test_bounded_priority_queue_keeps_top():
@@ -69,42 +67,6 @@ def test_half_float_codec():
     assert (np.abs(tr) <= np.abs(r)).all()
     assert np.array_equal(float_to_half_bits(back[:7], "truncate"), h[:7])
     assert is_representable_as_half(65504.0) and not is_representable_as_half(70000.0)
-
-
-def test_int_matrices_agree():
-    d = DoKIntMatrix()
-    rng = np.random.default_rng(1)
-    for i, j in rng.integers(0, 6, size=(40, 2)):
-        d.incr(i, j)
-    dense = d.to_dense()
-    assert dense.sum() == 40
-    cm = d.to_column_major()
-    cd = ColumnMajorDenseIntMatrix2d.from_dense(dense)
-    for i in range(d.n_rows):
-        for j in range(d.n_cols):
-            assert d.get(i, j) == cm.get(i, j) == cd.get(i, j) == dense[i, j]
-    for j in range(d.n_cols):
-        ref = [(int(i), int(dense[i, j])) for i in np.flatnonzero(dense[:, j])]
-        assert list(d.each_nonzero_in_column(j)) == ref
-        assert list(cm.each_nonzero_in_column(j)) == ref
-        assert list(cd.each_nonzero_in_column(j)) == ref
-    assert cm.nnz() == d.nnz() == cd.nnz()
-    with pytest.raises(TypeError):
-        cm.set(0, 0, 1)
-    d.set(0, 0, 0)
-    assert d.get(0, 0) == 0
-
-
-def test_vectors():
-    a = DenseVector([1.0, 0.0, 2.0])
-    s = SparseVector()
-    s.set(2, 4.0)
-    s.incr(0, 1.0)
-    assert a.dot(s) == 9.0 and s.size() == 3
-    assert list(s.each()) == [(0, 1.0), (2, 4.0)]
-    assert list(a.each()) == [(0, 1.0), (2, 2.0)]
-    s.set(2, 0.0)
-    assert s.size() == 1
 
 
 def test_function_catalogue_covers_registry():

@@ -165,6 +165,16 @@ def test_tools():
     assert T.sigmoid(0) == 0.5
     assert T.to_ordered_list([3, 1, 2]) == [1, 2, 3]
     assert T.to_ordered_list(["a", "b", "c"], [3, 1, 2], "-k 2") == ["a", "c"]
+    vals, keys = ["a", "b", "c", "d", "e"], [3, 1, 2, 1, 5]
+    assert T.to_ordered_list(vals, keys, "-k -2") == ["b", "d"]          # smallest, ties in order
+    assert T.to_ordered_list(vals, keys, "-k 3 -reverse") == ["b", "d", "c"]
+    assert T.to_ordered_list(vals, keys, "-k 0") == []
+    assert T.to_ordered_list(vals, keys, "-k 9") == ["e", "a", "c", "b", "d"]
+    rng = np.random.default_rng(0)
+    ks = rng.integers(0, 50, 400).tolist()
+    vs = list(range(400))
+    full = sorted(vs, key=lambda i: ks[i], reverse=True)
+    assert T.to_ordered_list(vs, ks, "-k 37") == full[:37]       # bounded heap == stable sort
     assert T.convert_label(0) == -1 and T.convert_label(-1) == 0
     assert [r[0] for r in T.generate_series(1, 3)] == [1, 2, 3]
     assert T.from_json(T.to_json({"a": [1, 2]})) == {"a": [1, 2]}
@@ -195,3 +205,41 @@ def test_mhash_kernel_bit_exact():
         got = mhash_device(words, nf).cpu().numpy()
         ref = murmur3_batch(words) if nf == 0 else mhash_batch(words, nf)
         assert (got == ref).all(), nf
+
+
+def test_bpr_sampling_is_stable_across_hash_seeds():
+    """The per-user stream must not depend on Python's salted ``hash()``: two interpreters
+    with different PYTHONHASHSEED emit identical triples for string and int users."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import hivemall_amd.ftvec.functions as F;"
+            "print([list(F.bpr_sampling(u, [1, 5, 9], 50, '-seed 7 -sampling_rate 2')) "
+            "for u in ('alice', 'bob', 42)])")
+    outs = []
+    for hs in ("1", "12345"):
+        env = dict(os.environ, PYTHONHASHSEED=hs)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout)
+    assert outs[0] == outs[1] and outs[0].count("(") == 18
+    a = list(F.bpr_sampling("alice", [1, 5, 9], 50, "-seed 7"))
+    b = list(F.bpr_sampling("alice", [1, 5, 9], 50, "-seed 8"))
+    assert a != b
+
+
+def test_rand_amplify_seed_and_streaming():
+    amp = F.RandAmplifier(3, 16, seed=5)
+    src = ((i,) for i in range(1000))                  # a generator: never materialised
+    it = amp.run(src)
+    first = [next(it) for _ in range(10)]
+    assert all(r[0] < 20 for r in first)               # reservoir of 16 rows, 3 copies each
+    rest = list(it)
+    assert sorted(r[0] for r in first + rest) == sorted(list(range(1000)) * 3)
+    a = F.rand_amplify(2, 50, list(range(200)), "-seed 1")
+    b = F.rand_amplify(2, 50, list(range(200)), "-seed 1")
+    c = F.rand_amplify(2, 50, list(range(200)), "-seed 2")
+    assert a["c0"].tolist() == b["c0"].tolist() != c["c0"].tolist()
+    assert sorted(a["c0"].tolist()) == sorted(list(range(200)) * 2)
