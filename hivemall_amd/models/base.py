@@ -10,6 +10,7 @@ from __future__ import annotations
 import logging
 import math
 import os
+import time
 from typing import Any
 
 import numpy as np
@@ -133,12 +134,49 @@ class Learner:
         data-parallel."""
         return self.mixer.all_reduce_scalar(float(x), "sum") if self._dp() else float(x)
 
-    def epoch_converged(self, loss: float, reduced: bool = False) -> bool:
+    def epoch_converged(self, loss: float, reduced: bool = False, rows: int | None = None) -> bool:
         """ConversionState step on the job-wide epoch loss: every rank takes the same
         break decision, so no rank leaves the epoch loop while another still calls the mixing
-        collectives."""
-        self.cv.incr_loss(loss if reduced else self.dp_sum(loss))
+        collectives.  With ``HM_METRICS`` set, also appends the epoch's metrics record."""
+        total = loss if reduced else self.dp_sum(loss)
+        self.cv.incr_loss(total)
+        self._log_epoch(total, rows)
         return self.cv.is_converged()
+
+    # ------------------------------------------------------------------ metrics stream
+    @property
+    def metrics(self):
+        """``prof.MetricsWriter`` when ``HM_METRICS=<path>`` is set (SURVEY.md §5.5 per-step
+        JSONL), else None; rank-tagged with the mixer's rank."""
+        if not os.environ.get("HM_METRICS"):
+            return None
+        m = getattr(self, "_metrics", None)
+        if m is None:
+            from ..prof import MetricsWriter
+            m = self._metrics = MetricsWriter(rank=getattr(self.mixer, "rank", self.rank))
+            self._m_t = time.perf_counter()
+            self._m_epoch, self._m_mix_s, self._m_mix_bytes, self._m_mixes = 0, 0.0, 0, 0
+        return m
+
+    def _log_epoch(self, loss: float, rows: int | None) -> None:
+        m = self.metrics
+        if m is None:
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        dt, self._m_t = now - self._m_t, now
+        self._m_epoch += 1
+        rec = dict(learner=self.NAME, epoch=self._m_epoch, loss=float(loss), epoch_s=round(dt, 6),
+                   mixes=self._m_mixes, mix_ms=round(self._m_mix_s * 1e3, 3),
+                   mixed_bytes=self._m_mix_bytes)
+        if rows:
+            rec["rows"] = int(rows)
+            rec["rows_per_s"] = round(rows / max(dt, 1e-9), 1)
+        if self._m_mix_s > 0:
+            rec["mix_GBps"] = round(self._m_mix_bytes / self._m_mix_s / 1e9, 3)
+        m.log(**rec)
+        self._m_mix_s, self._m_mix_bytes, self._m_mixes = 0.0, 0, 0
 
     def dp_batches(self, n: int, bs: int) -> int:
         """Launches for ``n`` rows in batches of ``bs``; data-parallel learners that mix every
@@ -156,6 +194,11 @@ class Learner:
         over ranks so every rank emits the same model table."""
         if not self._dp():
             return
+        timed = self.metrics is not None
+        if timed:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
         if self.cl.get("mix_sparse", False):
             if getattr(self, "_sparse_mixer", None) is None:
                 from ..parallel.mix import SparseDeltaMixer
@@ -168,3 +211,9 @@ class Learner:
             self.mixer.all_reduce_sum(f)
             for m, v in zip(flags, f):
                 m.copy_(v > 0)
+        if timed:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self._m_mix_s += time.perf_counter() - t0
+            self._m_mix_bytes += sum(t.numel() * t.element_size() for t in tensors)
+            self._m_mixes += 1

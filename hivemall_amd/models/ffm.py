@@ -234,7 +234,7 @@ class FFMTrainer(Learner):
                 f = lambda t: None if t is None else t.index_select(0, perm).contiguous()
                 eb = FFMBatch(f(b.idx), f(b.fld), f(b.val), f(b.y))
             self.train_batch(eb, loss_buf)
-            if self.epoch_converged(float(loss_buf.double().sum().item())):
+            if self.epoch_converged(float(loss_buf.double().sum().item()), rows=b.n):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         if self.mixer is not None:

@@ -217,7 +217,7 @@ class FMTrainer(Learner):
             self.train_rows(rows, loss_buf)
             if va is not None:
                 self._adapt_lambda(va)
-            if self.epoch_converged(float(loss_buf.double().sum().item())):
+            if self.epoch_converged(float(loss_buf.double().sum().item()), rows=rows.n):
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
         self.mix()
@@ -245,7 +245,7 @@ class FMTrainer(Learner):
                                self.h.eta0, self.h.lambda0, self.h.lambda_w, self.h.lambda_v,
                                self.h.classification, self.h.min_target, self.h.max_target)
         for ep in range(int(self.cl["iters"])):
-            if self.epoch_converged(eng.epoch(X, y)):
+            if self.epoch_converged(eng.epoch(X, y), rows=X.shape[0]):
                 log.info("train_fm converged at epoch %d", ep + 1)
                 break
         self.t += rows.n * (ep + 1)

@@ -388,7 +388,7 @@ class OnlineLinearLearner(Learner):
                                      None, mb)
             self.rows_seen += rows.n
             self.mix()
-            if self.epoch_converged(float(loss.sum().item())):
+            if self.epoch_converged(float(loss.sum().item()), rows=rows.n):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         return self

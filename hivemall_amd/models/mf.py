@@ -302,7 +302,7 @@ class MatrixFactorization(_MFBase):
             self._epoch_mix(ep)
             el = self.dp_sum(float(loss.double().sum().item()))
             self._epoch_end(el)
-            if self.epoch_converged(el, reduced=True):
+            if self.epoch_converged(el, reduced=True, rows=u.numel()):
                 log.info("%s converged at epoch %d", self.NAME, ep + 1)
                 break
         self.mix()
@@ -502,7 +502,7 @@ class BPRMF(_MFBase):
             for ep in range(int(self.cl["iters"])):
                 el = self.dp_sum(self._step_sharded(tu, ti, tj))
                 self._epoch_end(el)
-                if self.epoch_converged(el, reduced=True):
+                if self.epoch_converged(el, reduced=True, rows=tu.numel()):
                     break
             if self._dp():
                 f = [self.seen_u.to(torch.float32), self.seen_i.to(torch.float32)]
@@ -517,7 +517,7 @@ class BPRMF(_MFBase):
             el = self.dp_sum(self.step(tu, ti, tj))
             self._epoch_end(el)
             self._epoch_mix(ep)
-            if self.epoch_converged(el, reduced=True):
+            if self.epoch_converged(el, reduced=True, rows=tu.numel()):
                 break
         self.mix()
         return self
@@ -553,7 +553,7 @@ class BPRMF(_MFBase):
             el = self.dp_sum(self.step(n=per, csr=csr))
             self._epoch_end(el)
             self._epoch_mix(ep)
-            if self.epoch_converged(el, reduced=True):
+            if self.epoch_converged(el, reduced=True, rows=per):
                 break
         self.mix()
         return self

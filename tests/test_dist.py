@@ -343,3 +343,40 @@ def test_bench_configs_n_gpu_entry_point_cpu_world2():
         assert d["world"] == 2 and d["n_gpus"] == 2 and d["dist_backend"] == "gloo"
     assert recs[1]["trees_in_forest"] == 4
     assert 0.6 < recs[0]["test_auc"] and 0.6 < recs[2]["sampled_auc"]
+
+
+def _metrics_dp(ctx):
+    import tempfile
+
+    import numpy as np
+
+    from hivemall_amd.models.mf import MatrixFactorization
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    path = os.path.join(tempfile.gettempdir(), f"hm_metrics_{os.environ['MASTER_PORT']}.jsonl")
+    os.environ["HM_METRICS"] = path
+    rng = np.random.default_rng(5 + ctx.rank)
+    u, i = rng.integers(0, 50, 400), rng.integers(0, 80, 400)
+    MatrixFactorization("-factors 4 -iters 3 -seed 3 -mix_interval 1", device="cpu",
+                        mixer=ModelMixer(ctx), rank=ctx.rank).fit(u, i, rng.random(400) * 5)
+    return path
+
+
+def test_learner_metrics_stream_world2():
+    """``HM_METRICS=<path>``: every learner epoch appends a rank-tagged record with the job-wide
+    loss, rows/s and the mixes' time and wire bytes."""
+    out = run_world("_metrics_dp")
+    path = out[0]
+    try:
+        recs = [json.loads(l) for l in open(path)]
+    finally:
+        os.remove(path)
+    assert sorted({r["rank"] for r in recs}) == [0, 1]
+    r0 = [r for r in recs if r["rank"] == 0]
+    assert [r["epoch"] for r in r0] == [1, 2, 3]
+    for r in r0:
+        assert r["learner"] == "train_mf_sgd" and r["rows"] == 400 and r["rows_per_s"] > 0
+        assert r["mixes"] == 1 and r["mixed_bytes"] > 50 * 4 * 4 and r["mix_ms"] > 0
+    # the loss is the job-wide sum: both ranks log the same value
+    r1 = [r for r in recs if r["rank"] == 1]
+    assert [r["loss"] for r in r0] == [r["loss"] for r in r1]
