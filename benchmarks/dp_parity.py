@@ -9,7 +9,8 @@ rows of one rank, exactly as in the driver's weak-scaling run.
     python benchmarks/dp_parity.py --worlds 1 2 4 8 --device cpu            # gloo, CPU engine
     HM_DIST_BACKEND=gloo python benchmarks/dp_parity.py --device cuda ...   # N ranks on one GPU
 
-Prints one JSON line per run and a summary line with logloss_N - logloss_1(same rows).
+Prints one JSON line per world: logloss_N, logloss_1 over the same total rows (``delta``) and
+logloss_1 over one rank's share only (``logloss_1_same_steps``).
 """
 from __future__ import annotations
 
@@ -72,11 +73,15 @@ def main(argv=None):
     ap.add_argument("--mix-power", type=float, default=1.0)
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--timeout", type=int, default=1800)
+    ap.add_argument("--same-steps", type=int, default=1,
+                    help="also run one rank for --steps only (its own share of the rows)")
     a = ap.parse_args(argv)
     res = []
     for w in a.worlds:
         rn = run(w, a.steps, a, a.timeout)
         r1 = run(1, a.steps * w, a, a.timeout) if w > 1 else rn
+        # one rank on its own share only (the weak-scaling comparison: what N ranks add)
+        r1s = run(1, a.steps, a, a.timeout) if (w > 1 and a.same_steps) else None
         rec = {"world": w, "steps_per_rank": a.steps, "rows_per_rank": a.batch * (a.steps + a.warmup),
                "total_rows": a.batch * (a.steps + a.warmup) * w, "mix_every": a.mix_every,
                "overlap": a.mix_overlap, "mix_mode": a.mix_mode, "mix_state": a.mix_state,
@@ -85,6 +90,7 @@ def main(argv=None):
                "backend": rn.get("dist_backend"), "device": a.device,
                "logloss_N": rn["logloss_heldout"], "logloss_1_same_rows": r1["logloss_heldout"],
                "delta": round(rn["logloss_heldout"] - r1["logloss_heldout"], 5),
+               "logloss_1_same_steps": r1s["logloss_heldout"] if r1s else None,
                "floor": rn["logloss_planted_floor"], "mixes_timed": rn["config"]["mixes_in_timed_region"]}
         res.append(rec)
         print(json.dumps(rec), flush=True)
