@@ -15,6 +15,7 @@ from .. import _native
 _P = _native.c_p
 _native.register_hip("hm_join_dot", [_P, _P, _P, _P, _native.c_i64, _P, _P, _P])
 _native.register_hip("hm_join_fm", [_P, _P, _P, _P, _P, _P, _native.c_i64, _native.c_int, _P, _P, _P, _P])
+_native.register_hip("hm_join_ffm", [_P] * 10 + [_native.c_i64, _native.c_int, _P, _P])
 
 
 def _dev(a: np.ndarray, dev) -> torch.Tensor:
@@ -69,3 +70,32 @@ def join_fm(tm, x, g, W, V, vmask, n_groups: int, device=None):
     np.add.at(S, g[vm], vv)
     np.add.at(Q, g[vm], vv * vv)
     return lin + 0.5 * (S * S - Q).sum(1)
+
+
+def join_ffm(ti, tj, xi, xj, g, W1, V1, m1, V2, m2, n_groups: int, device=None):
+    """Per group: ffm_predict = Σ <V1[ti], V2[tj]> xi xj over rows with both V rows, plus
+    Σ W1[ti] xi over the other matched rows (NaN W = NULL)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    k = V1.shape[1]
+    if V2.shape[1] != k:
+        raise ValueError("join_ffm: the two model tables disagree on k")
+    if dev.type == "cuda":
+        p = _native.ptr
+        ts = [_dev(a, dev) for a in (ti, tj, xi, xj, g, W1, V1, m1.astype(np.uint8), V2, m2.astype(np.uint8))]
+        out = torch.zeros(n_groups, dtype=torch.float64, device=dev)
+        rc = _native.hip().hm_join_ffm(*[p(t) for t in ts], len(ti), k, p(out), _native.stream_of(dev))
+        _native.check(rc, "hm_join_ffm")
+        return out.cpu().numpy()
+    ok = ti >= 0
+    a = np.where(ok, ti, 0)
+    b = np.where(tj >= 0, tj, 0)
+    both = ok & (tj >= 0) & m1[a].astype(bool) & m2[b].astype(bool)
+    val = np.zeros(len(ti))
+    if both.any():
+        d = np.einsum("ij,ij->i", V1[a[both]].astype(np.float64), V2[b[both]].astype(np.float64))
+        val[both] = d * xi[both].astype(np.float64) * xj[both].astype(np.float64)
+    lin = ok & ~both
+    w = W1[a].astype(np.float64)
+    lw = lin & ~np.isnan(w)
+    val[lw] = w[lw] * xi[lw].astype(np.float64)
+    return np.bincount(g, weights=val, minlength=n_groups)

@@ -65,7 +65,7 @@ def _syntactic_ok(session, s) -> bool:
             and j.on.op == "=" and isinstance(j.on.left, Col) and isinstance(j.on.right, Col)):
         return False
     if isinstance(j.left, Join) or isinstance(j.right, Join):
-        return False
+        return False       # the two-join FFM shape goes through try_fused_ffm
     if s.where is not None or s.having is not None or s.distinct or not s.group_by:
         return False
     if not all(isinstance(g, Col) for g in s.group_by):
@@ -122,6 +122,8 @@ def _key_arrays(lk: pd.Series, rk: pd.Series):
 def try_fused(session, s, ctes):
     """Run ``s`` through the fused operator; returns the result Frame, or None after stashing
     the already-built join inputs for the generic path."""
+    if enabled() and isinstance(s.source, Join) and isinstance(s.source.left, Join):
+        return try_fused_ffm(session, s, ctes)
     if not enabled() or not _syntactic_ok(session, s):
         return None
     from .executor import Frame, _GroupBase
@@ -253,6 +255,210 @@ def try_fused(session, s, ctes):
             x = Lj.series(sp[3]).to_numpy(dtype=np.float32)
             agg_values[id(a)] = pd.Series(join_fm(tmj, x, g32, W, V, vmask, n_groups, dev))
     session.last_plan = "fused_join_predict"
+    out = session._project(s.items, gframe, ctes, agg_values)
+    base = _GroupBase(gframe, agg_values, session)
+    return session._finish(out, base, s, ctes)
+
+
+# ------------------------------------------------------------------ FFM: two model joins
+#   SELECT t.rowid, ffm_predict(m1.Wi, m1.Vi, m2.Vi, t.Xi, t.Xj) FROM (... feature_pairs(
+#     features, '-ffm') ...) t LEFT OUTER JOIN m m1 ON (t.i = m1.i) LEFT OUTER JOIN m m2 ON
+#   (t.j = m2.i) GROUP BY t.rowid
+def _eqjoin(j) -> bool:
+    return (isinstance(j, Join) and j.kind in ("left", "inner") and isinstance(j.on, BinOp)
+            and j.on.op == "=" and isinstance(j.on.left, Col) and isinstance(j.on.right, Col))
+
+
+def _ffm_syntactic_ok(session, s) -> bool:
+    j2 = s.source
+    j1 = j2.left if isinstance(j2, Join) else None
+    if not (_eqjoin(j2) and _eqjoin(j1)) or isinstance(j2.right, Join) \
+            or isinstance(j1.left, Join) or isinstance(j1.right, Join):
+        return False
+    if s.where is not None or s.having is not None or s.distinct or not s.group_by:
+        return False
+    if not all(isinstance(g, Col) for g in s.group_by):
+        return False
+    aggs = _aggs_of(session, s)
+    n_ffm = 0
+    for a in aggs:
+        n = a.name.lower()
+        if a.distinct or a.window is not None:
+            return False
+        if n == "ffm_predict" and len(a.args) == 5 and all(isinstance(x, Col) for x in a.args):
+            n_ffm += 1
+            continue
+        if n == "count" and (a.star or not a.args):
+            continue
+        if n in ("sum", "max", "min", "avg", "mean", "count") and len(a.args) == 1 and isinstance(a.args[0], Col):
+            continue
+        return False
+    return n_ffm >= 1
+
+
+def _which(col: Col, frames):
+    """Index of the one frame that resolves ``col`` (None: unresolvable or ambiguous) and the
+    column position in it."""
+    from .executor import SQLError
+
+    hits = []
+    for fi, fr in enumerate(frames):
+        try:
+            ci = fr.resolve(col.name, col.table)
+        except SQLError:
+            return None, None
+        if ci is not None:
+            hits.append((fi, ci))
+    return hits[0] if len(hits) == 1 else (None, None)
+
+
+def _join_index(lk: pd.Series, rk: pd.Series):
+    """Model row per test row (-1: none; NULL keys never match), or None when the model keys
+    are not unique or not comparable (the generic join decides then)."""
+    keys = _key_arrays(lk, rk)
+    if keys is None:
+        return None
+    lk, rk = keys
+    rnn = rk.notna().to_numpy()
+    rpos = np.nonzero(rnn)[0]
+    ridx = pd.Index(rk[rnn].to_numpy())
+    if not ridx.is_unique:
+        return None
+    tm = ridx.get_indexer(lk.to_numpy())
+    return np.where(lk.notna().to_numpy() & (tm >= 0), rpos[np.maximum(tm, 0)], -1).astype(np.int32)
+
+
+def _v_matrix(col: pd.Series):
+    """list column -> (V f32 [R, k], row mask) or None when the lists disagree on k."""
+    vl = col.tolist()
+    null = [v is None or v is pd.NA or (isinstance(v, float) and np.isnan(v)) for v in vl]
+    if any(not n and not isinstance(v, (list, tuple, np.ndarray)) for v, n in zip(vl, null)):
+        return None
+    ks = {len(v) for v, n in zip(vl, null) if not n}
+    if len(ks) > 1:
+        return None
+    k = ks.pop() if ks else 1
+    vmask = ~np.asarray(null, dtype=bool)
+    V = np.zeros((len(vl), k), dtype=np.float32)
+    if vmask.any():
+        V[vmask] = np.asarray([v for v, m in zip(vl, vmask) if m], dtype=np.float32)
+    return V, vmask
+
+
+def try_fused_ffm(session, s, ctes):
+    """The FFM scoring query as one gather-reduce (``ops.join_predict.join_ffm``): both joins
+    resolve to a model-row index per exploded test row; no joined table is materialised."""
+    if not _ffm_syntactic_ok(session, s):
+        return None
+    from .executor import Frame, _GroupBase
+    from ..ops.join_predict import join_ffm
+
+    j2 = s.source
+    j1 = j2.left
+    T = session._source(j1.left, ctes)
+    M1 = session._source(j1.right, ctes)
+
+    def fallback():
+        session._prebuilt[id(j1)] = (T, M1)
+        return None
+
+    M2 = session._source(j2.right, ctes)
+    frames = (T, M1, M2)
+    # join 1: T x M1; join 2: (T, M1) x M2 with the left key on T
+    a, b = _which(j1.on.left, frames), _which(j1.on.right, frames)
+    if {a[0], b[0]} != {0, 1}:
+        return fallback()
+    t1, m1k = (a[1], b[1]) if a[0] == 0 else (b[1], a[1])
+    a, b = _which(j2.on.left, frames), _which(j2.on.right, frames)
+    if {a[0], b[0]} != {0, 2}:
+        return fallback()
+    t2, m2k = (a[1], b[1]) if a[0] == 0 else (b[1], a[1])
+    gcols = []
+    for gc in s.group_by:
+        w = _which(gc, frames)
+        if w[0] != 0:
+            return fallback()
+        gcols.append(w[1])
+    aggs = _aggs_of(session, s)
+    ids = {id(x) for x in aggs}
+    bare = []
+    for it in s.items:
+        _cols_outside_aggs(it.expr, ids, bare)
+    gset = {(c.name.lower(), (c.table or "").lower()) for c in s.group_by}
+    for c in bare:
+        if (c.name.lower(), (c.table or "").lower()) not in gset and _which(c, frames)[0] != 0:
+            return fallback()
+    specs = []
+    for x in aggs:
+        n = x.name.lower()
+        if n == "ffm_predict":
+            w = [_which(c, frames) for c in x.args]
+            if [f for f, _ in w] != [1, 1, 2, 0, 0]:
+                return fallback()
+            specs.append(("ffm",) + tuple(c for _, c in w))
+        elif n == "count" and (x.star or not x.args):
+            specs.append(("count_star",))
+        else:
+            if _which(x.args[0], frames)[0] != 0:
+                return fallback()
+            specs.append(("test",))
+
+    ti = _join_index(T.series(t1), M1.series(m1k))
+    tj = _join_index(T.series(t2), M2.series(m2k))
+    if ti is None or tj is None:
+        return fallback()
+    ffm_in = {}
+    for sp in specs:
+        if sp[0] != "ffm":
+            continue
+        _, w1c, v1c, v2c, xic, xjc = sp
+        W1 = M1.series(w1c)
+        xi, xj = T.series(xic), T.series(xjc)
+        if not all(pd.api.types.is_numeric_dtype(c) or c.isna().all() for c in (W1, xi, xj)):
+            return fallback()
+        A, B = _v_matrix(M1.series(v1c)), _v_matrix(M2.series(v2c))
+        if A is None or B is None or A[0].shape[1] != B[0].shape[1]:
+            return fallback()
+        xi_a = xi.to_numpy(dtype=np.float32, na_value=np.nan)
+        xj_a = xj.to_numpy(dtype=np.float32, na_value=np.nan)
+        both = (ti >= 0) & (tj >= 0)
+        both &= A[1][np.maximum(ti, 0)] & B[1][np.maximum(tj, 0)]
+        if np.isnan(xi_a[ti >= 0]).any() or np.isnan(xj_a[both]).any():
+            return fallback()          # NULL operands: the generic UDAF defines what they mean
+        ffm_in[id(sp)] = (W1.to_numpy(dtype=np.float32, na_value=np.nan), A, B, xi_a, xj_a)
+
+    # joined row order of the generic path: join 1 (matched in test order, then for LEFT the
+    # unmatched), then join 2 over that order the same way
+    def order_of(tm, kind, base):
+        hit = tm[base] >= 0
+        return np.concatenate([base[hit], base[~hit]]) if kind == "left" else base[hit]
+
+    rows = order_of(ti, j1.kind, np.arange(T.n))
+    rows = order_of(tj, j2.kind, rows)
+    Lj = T.take(rows)
+    if len(gcols) == 1:
+        codes = pd.factorize(Lj.series(gcols[0]), use_na_sentinel=False)[0]
+    else:
+        kdf = pd.DataFrame({f"k{i}": Lj.series(c) for i, c in enumerate(gcols)})
+        codes = kdf.groupby(list(kdf.columns), sort=False, dropna=False).ngroup().to_numpy()
+    codes = codes.astype(np.int64)
+    n_groups = int(codes.max()) + 1 if len(codes) else 0
+    order = np.argsort(codes, kind="stable")
+    bounds = np.searchsorted(codes[order], np.arange(n_groups + 1))
+    first_idx = order[bounds[:-1]] if len(codes) else np.zeros(0, dtype=np.int64)
+    gframe = Lj.take(first_idx)
+    g32 = codes.astype(np.int32)
+    agg_values = {}
+    for x, sp in zip(aggs, specs):
+        if sp[0] == "count_star":
+            agg_values[id(x)] = pd.Series(np.diff(bounds))
+        elif sp[0] == "test":
+            agg_values[id(x)] = session._agg_values(x, Lj, ctes, order, bounds, n_groups, codes)
+        else:
+            W1, (V1, vm1), (V2, vm2), xi_a, xj_a = ffm_in[id(sp)]
+            agg_values[id(x)] = pd.Series(join_ffm(ti[rows], tj[rows], xi_a[rows], xj_a[rows], g32, W1,
+                                                   V1, vm1, V2, vm2, n_groups, session.device))
+    session.last_plan = "fused_ffm_join_predict"
     out = session._project(s.items, gframe, ctes, agg_values)
     base = _GroupBase(gframe, agg_values, session)
     return session._finish(out, base, s, ctes)

@@ -131,3 +131,72 @@ def test_fused_join_predict_gpu_equals_cpu():
         b, pb_ = _run(_tables("cpu", seed=3, n=20000, nf=5000), None, q, fused=True)
         assert pa_ == pb_ == "fused_join_predict"
         _assert_same(a, b)
+
+
+FFM_Q = """
+SELECT t.rowid, sigmoid(ffm_predict(m1.Wi, m1.Vi, m2.Vi, t.Xi, t.Xj)) AS p, max(t.Xi) AS mx,
+       count(*) AS n
+FROM tp t
+LEFT OUTER JOIN ffm_model m1 ON (t.i = m1.i)
+LEFT OUTER JOIN ffm_model m2 ON (t.j = m2.i)
+GROUP BY t.rowid ORDER BY rowid"""
+
+
+def _ffm_tables(device="cpu", n=300, nf=5, seed=1, drop_model_rows=0):
+    """Trains an FFM model on ``n`` rows, explodes them with feature_pairs('-ffm'); optionally
+    drops model rows so some joins miss (the LEFT JOIN NULL paths)."""
+    rng = np.random.default_rng(seed)
+    rows = [[f"{f}:{int(rng.integers(0, 20))}:1" for f in range(nf)] for _ in range(n)]
+    y = (rng.random(n) < 0.4).astype(int)
+    opts = f"-c -factors 3 -num_fields {nf} -feature_hashing 10 -iters 2 -w0"
+    base = Session(device="cpu")
+    base.register("t", pd.DataFrame({"rowid": range(n), "features": rows, "label": y}))
+    model = base.sql(f"SELECT train_ffm(features, label, '{opts}') AS (model_id, i, Wi, Vi) FROM t")
+    if drop_model_rows:
+        model = model.drop(index=rng.choice(len(model), drop_model_rows, replace=False)).reset_index(drop=True)
+    tp = base.sql(f"SELECT rowid, i, j, Xi, Xj FROM t LATERAL VIEW feature_pairs(features, "
+                  f"'-ffm -feature_hashing 10 -num_fields {nf}') x AS i, j, Xi, Xj")
+
+    def make():
+        s = Session(device=device)
+        s.register("ffm_model", model)
+        s.register("tp", tp)
+        return s
+    return make, rows, y, opts
+
+
+@pytest.mark.parametrize("drop", [0, 40])
+def test_fused_ffm_predict_equals_generic(drop):
+    """The two-join FFM scoring query runs as one gather-reduce and returns
+    exactly the generic path's table; with every model row present it is the trainer's
+    prediction."""
+    from hivemall_amd.models.ffm import FFMTrainer
+
+    make, rows, y, opts = _ffm_tables(drop_model_rows=drop)
+    a, plan_a = _run(make, None, FFM_Q, fused=True)
+    b, plan_b = _run(make, None, FFM_Q, fused=False)
+    assert plan_a == "fused_ffm_join_predict" and plan_b is None
+    _assert_same(a, b)
+    if not drop:
+        ref = FFMTrainer(opts, device="cpu").fit(rows, y).predict(rows)
+        np.testing.assert_allclose(a["p"].to_numpy(dtype=float), ref, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_ffm_inner_joins_equal_generic():
+    make, *_ = _ffm_tables(drop_model_rows=25, seed=4)
+    q = FFM_Q.replace("LEFT OUTER JOIN", "JOIN")
+    a, plan_a = _run(make, None, q, fused=True)
+    b, _ = _run(make, None, q, fused=False)
+    assert plan_a == "fused_ffm_join_predict"
+    _assert_same(a, b)
+
+
+@pytest.mark.gpu
+def test_fused_ffm_predict_gpu_equals_cpu():
+    """hm_join_ffm (gfx950, wave-reduced fp64 atomics) against the numpy path."""
+    mk_g, *_ = _ffm_tables("cuda", n=3000, nf=8, drop_model_rows=30)
+    mk_c, *_ = _ffm_tables("cpu", n=3000, nf=8, drop_model_rows=30)
+    a, pa_ = _run(mk_g, None, FFM_Q, fused=True)
+    b, pb_ = _run(mk_c, None, FFM_Q, fused=True)
+    assert pa_ == pb_ == "fused_ffm_join_predict"
+    _assert_same(a, b)
