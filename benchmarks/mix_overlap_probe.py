@@ -62,18 +62,18 @@ def main():
                 g.out.view(a.world, g.shard).copy_(g.mean.expand(a.world, g.shard))   # all_gather
         pending.append(True)
 
-    def mix_finish():
+    def mix_finish(repack=False):
         if pending:
             cur.wait_stream(side)
             for g in groups:
-                g.merge()
+                g.merge(repack)
             pending.clear()
 
     def step(i, mix):
         s = (i % nres) * B
         ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True)
         if mix and (i + 1) % a.mix_every == 0:
-            mix_finish()
+            mix_finish(repack=True)     # OverlappedMixer.start: merge fused with the next pack
             mix_start()
 
     def timed(fn):

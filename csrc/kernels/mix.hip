@@ -69,6 +69,74 @@ __global__ __launch_bounds__(256) void merge_kernel(void* __restrict__ x, const 
     }
 }
 
+// 3-level views: element (i0, i1, c) of x at i0 * s0 + i1 * s1 + c, c < inner (inner % 4 == 0):
+// the V part of the per-slot FFM feature blocks (fp32: [NF][40][4] in 896-B blocks; bf16:
+// [NF][40][4] in 12-B slots of 512-B blocks, so a slot is only 4-B aligned).  ALN: every quad
+// of x is 16-B (fp32) / 8-B (bf16) aligned, so it moves as one vector; else as 32-bit words.
+template <bool BF, bool ALN>
+__device__ __forceinline__ float4 ldx(const void* p, int64_t e) {
+    if constexpr (ALN || !BF) {
+        if constexpr (ALN) return ld4<BF>(p, e);
+        const float* f = reinterpret_cast<const float*>(p) + e;
+        return make_float4(f[0], f[1], f[2], f[3]);
+    } else {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(p) + e);
+        const uint32_t a = w[0], b = w[1];
+        return make_float4(__uint_as_float(a << 16), __uint_as_float(a & 0xFFFF0000u),
+                           __uint_as_float(b << 16), __uint_as_float(b & 0xFFFF0000u));
+    }
+}
+
+template <bool BF, bool ALN>
+__device__ __forceinline__ void stx(void* p, int64_t e, float4 v) {
+    if constexpr (ALN) {
+        st4<BF>(p, e, v);
+    } else if constexpr (!BF) {
+        float* f = reinterpret_cast<float*>(p) + e;
+        f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+    } else {
+        uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(p) + e);
+        w[0] = (uint32_t)hm::f32_to_bf16(v.x) | ((uint32_t)hm::f32_to_bf16(v.y) << 16);
+        w[1] = (uint32_t)hm::f32_to_bf16(v.z) | ((uint32_t)hm::f32_to_bf16(v.w) << 16);
+    }
+}
+
+// MODE 0 (pack):  out[q] = x[view(q)]
+// MODE 1 (merge): x[view(q)] += mean[q] - snap[q]; when out != nullptr also out[q] = the new x
+//                 (merge of the finished mix fused with the snapshot of the next one; out may
+//                 alias snap: each quad is read before it is written by the same thread)
+template <int MODE, bool BF, bool ALN>
+__global__ __launch_bounds__(256) void view3_kernel(void* __restrict__ x, const void* __restrict__ mean,
+                                                    const void* snap, void* out, int64_t n0, int d1,
+                                                    int inner, int64_t s0, int64_t s1) {
+    const int qps = inner >> 2;
+    const int64_t per0 = (int64_t)d1 * qps;
+    const int64_t nq = n0 * per0;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+        const int64_t i0 = q / per0;
+        const int64_t rem = q - i0 * per0;
+        const int64_t i1 = rem / qps;
+        const int c = (int)(rem - i1 * qps) * 4;
+        const int64_t xe = i0 * s0 + i1 * s1 + c, qe = 4 * q;
+        float4 a = ldx<BF, ALN>(x, xe);
+        if constexpr (MODE == 1) {
+            const float4 m = ld4<BF>(mean, qe), sn = ld4<BF>(snap, qe);
+            a = make_float4(a.x + (m.x - sn.x), a.y + (m.y - sn.y), a.z + (m.z - sn.z), a.w + (m.w - sn.w));
+            if constexpr (BF) {
+                // round once here, so x and the next snapshot hold the same bits
+                a = make_float4(__uint_as_float((uint32_t)hm::f32_to_bf16(a.x) << 16),
+                                __uint_as_float((uint32_t)hm::f32_to_bf16(a.y) << 16),
+                                __uint_as_float((uint32_t)hm::f32_to_bf16(a.z) << 16),
+                                __uint_as_float((uint32_t)hm::f32_to_bf16(a.w) << 16));
+            }
+            stx<BF, ALN>(x, xe, a);
+            if (out != nullptr) st4<BF>(out, qe, a);
+        } else {
+            st4<BF>(out, qe, a);
+        }
+    }
+}
+
 int grid_for(int64_t quads) {
     const int64_t b = (quads + 255) / 256;
     return (int)(b < 256 * 16 ? (b > 0 ? b : 1) : 256 * 16);
@@ -105,4 +173,40 @@ HM_API int hm_mix_merge(void* x, const void* mean, const void* snap, int64_t row
     else
         return (int)hipErrorInvalidValue;
     HM_LAUNCH_RET();
+}
+
+namespace {
+template <int MODE>
+int launch_view3(void* x, const void* mean, const void* snap, void* out, int64_t n0, int d1, int inner,
+                 int64_t s0, int64_t s1, int dtype, hipStream_t stream) {
+    if (n0 < 0 || d1 <= 0 || inner <= 0 || (inner & 3) || s1 < inner || s0 < (int64_t)(d1 - 1) * s1 + inner)
+        return (int)hipErrorInvalidValue;
+    if (n0 == 0) return 0;
+    const int64_t nq = n0 * d1 * (inner >> 2);
+    const bool aln = (s0 % 4 == 0) && (s1 % 4 == 0) &&
+                     ((uintptr_t)x % (dtype == 1 ? 8 : 16) == 0);
+#define HM_V3(BF, ALN) hipLaunchKernelGGL((view3_kernel<MODE, BF, ALN>), dim3(grid_for(nq)), dim3(256), 0, stream, \
+                                           x, mean, snap, out, n0, d1, inner, s0, s1)
+    if (dtype == 1) {
+        if (aln) HM_V3(true, true); else HM_V3(true, false);
+    } else if (dtype == 0) {
+        if (aln) HM_V3(false, true); else HM_V3(false, false);
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+#undef HM_V3
+    HM_LAUNCH_RET();
+}
+}  // namespace
+
+// x: [n0][d1][inner] view with strides (s0, s1, 1) elements; out: contiguous n0*d1*inner.
+HM_API int hm_mix_pack3(const void* x, void* out, int64_t n0, int d1, int inner, int64_t s0, int64_t s1,
+                        int dtype, hipStream_t stream) {
+    return launch_view3<0>(const_cast<void*>(x), nullptr, nullptr, out, n0, d1, inner, s0, s1, dtype, stream);
+}
+
+// x += mean - snap over the view; out (nullable, may alias snap) <- the merged x.
+HM_API int hm_mix_merge3(void* x, const void* mean, const void* snap, void* out, int64_t n0, int d1, int inner,
+                         int64_t s0, int64_t s1, int dtype, hipStream_t stream) {
+    return launch_view3<1>(x, mean, snap, out, n0, d1, inner, s0, s1, dtype, stream);
 }

@@ -47,6 +47,11 @@ from .dist import DistContext, context
 
 _native.register_hip("hm_mix_shard_mean", [_native.c_p, _native.c_int, _native.c_i64,
                                            _native.c_int, _native.c_p, _native.c_p])
+_native.register_hip("hm_mix_pack3", [_native.c_p, _native.c_p, _native.c_i64, _native.c_int, _native.c_int,
+                                      _native.c_i64, _native.c_i64, _native.c_int, _native.c_p])
+_native.register_hip("hm_mix_merge3", [_native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_i64,
+                                       _native.c_int, _native.c_int, _native.c_i64, _native.c_i64, _native.c_int,
+                                       _native.c_p])
 _native.register_hip("hm_mix_merge", [_native.c_p, _native.c_p, _native.c_p, _native.c_i64,
                                       _native.c_int, _native.c_i64, _native.c_int, _native.c_p])
 
@@ -74,6 +79,21 @@ def _row_view(t: torch.Tensor):
     return rows, inner, rs
 
 
+def _view3(t: torch.Tensor):
+    """(n0, d1, inner, s0, s1) when ``t`` is an [n0][d1][inner] view with strides (s0, s1, 1)
+    and inner % 4 == 0 (contiguous tensors, row views, and the V part of the per-slot FFM
+    feature blocks), else None."""
+    if t.is_contiguous():
+        return (t.numel() // 4, 1, 4, 4, 4) if t.numel() % 4 == 0 else None
+    if t.stride(-1) != 1 or t.shape[-1] % 4:
+        return None
+    if t.dim() == 2:
+        return (t.shape[0], 1, t.shape[1], t.stride(0), t.shape[1])
+    if t.dim() == 3:
+        return (t.shape[0], t.shape[1], t.shape[2], t.stride(0), t.stride(1))
+    return None
+
+
 class _FlatGroup:
     """Same-dtype tensors packed into one flat wire buffer, padded to a multiple of 4*world."""
 
@@ -82,6 +102,7 @@ class _FlatGroup:
         self._refs = [weakref.ref(t) for t in tensors]
         self.shapes = [tuple(t.shape) for t in tensors]
         self.busy = False            # an OverlappedMixer collective is in flight on the buffers
+        self.prepacked = False       # send already holds the current snapshot (fused merge)
         self.base: torch.Tensor | None = None   # fp32 consensus of the last mix (delta-sum mode)
         self.dtype = tensors[0].dtype
         dev = tensors[0].device
@@ -117,8 +138,19 @@ class _FlatGroup:
         return buf[self.offs[k]:self.offs[k] + n].view(self.shapes[k])
 
     def pack(self) -> None:
+        if self.prepacked:           # the previous merge already wrote this snapshot
+            self.prepacked = False
+            return
+        code = _dtype_code(self.dtype)
         for k, t in enumerate(self.tensors):
-            self.seg(self.send, k).copy_(t)
+            d = self.seg(self.send, k)
+            v3 = _view3(t) if t.is_cuda and code is not None else None
+            if v3 is not None:
+                rc = _native.hip().hm_mix_pack3(t.data_ptr(), d.data_ptr(), *v3, code,
+                                                _native.stream_of(t.device))
+                _native.check(rc, "hm_mix_pack3")
+            else:
+                d.copy_(t)
 
     def unpack(self) -> None:
         for k, t in enumerate(self.tensors):
@@ -161,11 +193,22 @@ class _FlatGroup:
             s = self.recv.view(world, self.shard).sum(0, dtype=torch.float32)
             self.mean.copy_(s.mul_(1.0 / world))
 
-    def merge(self) -> None:
-        """t <- t + (mean - snapshot), fp32 math, one rounding (overlapped mixing)."""
+    def merge(self, repack: bool = False) -> None:
+        """t <- t + (mean - snapshot), fp32 math, one rounding (overlapped mixing).
+        ``repack``: also write the merged t into the snapshot buffer, in the same pass — the
+        next mix's pack (its ``pack()`` is then skipped)."""
         code = _dtype_code(self.dtype)
+        fused = repack and all(t.is_cuda and code is not None and _view3(t) is not None
+                               for t in self.tensors)
         for k, t in enumerate(self.tensors):
             m, s = self.seg(self.out, k), self.seg(self.send, k)
+            v3 = _view3(t) if t.is_cuda and code is not None else None
+            if v3 is not None:
+                rc = _native.hip().hm_mix_merge3(t.data_ptr(), m.data_ptr(), s.data_ptr(),
+                                                 s.data_ptr() if fused else None, *v3, code,
+                                                 _native.stream_of(t.device))
+                _native.check(rc, "hm_mix_merge3")
+                continue
             rv = _row_view(t) if t.is_cuda else None
             if rv is not None and code is not None and t.data_ptr() % 16 == 0:
                 rows, inner, rs = rv
@@ -174,6 +217,7 @@ class _FlatGroup:
                 _native.check(rc, "hm_mix_merge")
             else:
                 t.copy_(t.to(torch.float32) + (m.to(torch.float32) - s.to(torch.float32)))
+        self.prepacked = fused
 
 
 class ModelMixer:
@@ -406,9 +450,11 @@ class OverlappedMixer:
     def start(self, tensors: list[torch.Tensor]) -> None:
         if not self.m._active():
             return
+        groups = self.m.plan(tensors)
         if self.works:
-            self.finish()
-        self.groups = self.m.plan(tensors)
+            # mean mode, same tensors: the merge also writes the next snapshot (one pass less)
+            self.finish(repack=self.mode == "mean" and groups is self.groups)
+        self.groups = groups
         # delta-sum mode needs a consensus to measure deltas from: the first mix is a mean
         self._sum_now = self.mode != "mean" and all(g.base is not None for g in self.groups)
         for g in self.groups:
@@ -445,7 +491,7 @@ class OverlappedMixer:
             g.shard_mean(world)
             g.mean.mul_(float(world) ** self.power)
 
-    def finish(self) -> None:
+    def finish(self, repack: bool = False) -> None:
         if not self.works:
             return
         for w in self.works:
@@ -455,7 +501,7 @@ class OverlappedMixer:
             if self._sum_now:
                 g.merge_delta()
             else:
-                g.merge()
+                g.merge(repack)
                 if self.mode != "mean":              # the first consensus: deltas start here
                     g.base = g.out.to(torch.float32, copy=True)
             g.busy = False

@@ -107,3 +107,60 @@ def test_mix_kernels_match_torch():
         torch.cuda.synchronize()
         assert torch.equal(V, ref)
         assert torch.equal(VG[:, :, 1], G0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["slot12_bf16", "block_fp32", "contiguous_bf16"])
+def test_mix_view3_pack_merge_match_torch(layout):
+    """hm_mix_pack3 / hm_mix_merge3 over the V part of the per-slot FFM feature blocks (12-B
+    bf16 slots: 4-B aligned quads; fp32 896-B blocks) against torch; the fused merge+pack
+    leaves the snapshot bit-identical to the merged replica, and the G words are untouched."""
+    from hivemall_amd import _native
+    from hivemall_amd.parallel.mix import _FlatGroup, _view3
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    nf, S = 1000, 40
+    if layout == "slot12_bf16":
+        dt, code = torch.bfloat16, 1
+        blk = torch.randn(nf, 256, generator=g).to(dt).to(dev)          # 512-B blocks
+        V = blk[:, :S * 6].view(nf, S, 6)[:, :, :4]                      # 12-B slots, V = 8 B
+        other = lambda: blk[:, :S * 6].view(nf, S, 6)[:, :, 4:].clone()  # noqa: E731  (G words)
+    elif layout == "block_fp32":
+        dt, code = torch.float32, 0
+        blk = torch.randn(nf, 224, generator=g).to(dev)                 # 896-B blocks
+        V = blk[:, :S * 4].view(nf, S, 4)
+        other = lambda: blk[:, S * 4:].clone()                           # noqa: E731
+    else:
+        dt, code = torch.bfloat16, 1
+        V = torch.randn(nf, S, 4, generator=g).to(dt).to(dev)
+        other = lambda: torch.zeros(1)                                   # noqa: E731
+    v3 = _view3(V)
+    assert v3 is not None
+    st = _native.stream_of(dev)
+    out = torch.empty(V.numel(), dtype=dt, device=dev)
+    assert _native.hip().hm_mix_pack3(V.data_ptr(), out.data_ptr(), *v3, code, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(V.shape), V.contiguous())
+    keep = other()
+    m = torch.randn(V.shape, generator=g).to(dt).to(dev)
+    snap = V.contiguous().clone()
+    snap.view(-1)[::3] += 0.5
+    ref = (V.float() + (m.float() - snap.float())).to(dt)
+    assert _native.hip().hm_mix_merge3(V.data_ptr(), m.data_ptr(), snap.data_ptr(), snap.data_ptr(),
+                                       *v3, code, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(V, ref)
+    assert torch.equal(snap.view(V.shape), V)                            # fused next snapshot
+    assert torch.equal(other(), keep)
+    # the _FlatGroup path (pack -> merge(repack) -> pack is skipped)
+    fg = _FlatGroup([V], 8)
+    fg.pack()
+    assert torch.equal(fg.seg(fg.send, 0), V)
+    fg.out.copy_(fg.send)
+    fg.seg(fg.out, 0).add_(1.0)
+    before = V.float().clone()
+    fg.merge(repack=True)
+    assert fg.prepacked and torch.equal(V, (before + 1.0).to(dt))
+    fg.pack()
+    assert not fg.prepacked and torch.equal(fg.seg(fg.send, 0), V)
