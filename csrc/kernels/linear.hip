@@ -339,15 +339,48 @@ __device__ __forceinline__ F4 ld4m(const float4* p) {
     }
 }
 
-template <bool RELOAD, bool NT>
+// HOT: the hottest features (hot_slot[i] >= 0, at most HM_HOT_MAX, chosen by the host from the
+// pass's feature counts) are not read-modify-written per row: each block sums their gradients
+// (sum g, sum g^2, count) in LDS over a chunk of CH rows per wave, then applies them with one
+// returning float atomic on G and one on w per touched hot feature (AdaGrad / SGD of the general
+// learner, no or L2 regularisation).  No update of a hot feature is lost, and the atomics on its
+// address drop by 4*CH x.  Cold features keep the Hogwild read-modify-write.
+constexpr int HM_HOT_MAX = 4096;
+
+__device__ __forceinline__ void hot_flush(const Params& P, float4* __restrict__ s, float4 a, const StepK& k) {
+    float gs = a.x, g2 = a.y;
+    if (P.reg == R_L2) {
+        const float w = __builtin_nontemporal_load(&s->x);
+        const float lw = P.lambda * w;
+        g2 += 2.f * lw * gs + a.z * lw * lw;
+        gs += a.z * lw;
+    }
+    if (P.opt == O_ADAGRAD) {
+        const float gn = atomicAdd(&s->y, g2) + g2;
+        atomicAdd(&s->x, -k.eta * gs / (sqrtf(gn) + P.eps));
+    } else {
+        atomicAdd(&s->x, -k.eta * gs);
+    }
+}
+
+__device__ __forceinline__ void hot_add(float4* acc, float g) {
+    atomicAdd(&acc->x, g);
+    atomicAdd(&acc->y, g * g);
+    atomicAdd(&acc->z, 1.f);
+}
+
+template <bool RELOAD, bool NT, bool HOT>
 __global__ __launch_bounds__(256) void linear_shared_kernel(
     Params P, int64_t n_rows, int dims, int64_t t0, int W, int R, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
     const int32_t* __restrict__ order, float4* __restrict__ S0, uint8_t* __restrict__ touched0,
-    float* __restrict__ RSW, double* __restrict__ loss_out) {
+    float* __restrict__ RSW, double* __restrict__ loss_out, const int32_t* __restrict__ hot_slot,
+    const int32_t* __restrict__ hot_feat, int H, int CH) {
+    __shared__ float4 s_acc[HOT ? HM_HOT_MAX : 1];
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= W) return;                          // wave-uniform: the whole wave leaves
+    const bool active = g < W;
+    if (!HOT && !active) return;                 // wave-uniform: the whole wave leaves
     // replica: XCD x = block % 8 owns replicas x, x + 8, ...; R = 1 or a multiple of 8
     const int b = blockIdx.x;
     const int rep = R == 1 ? 0 : ((b >> 3) % (R >> 3)) * 8 + (b & 7);
@@ -355,60 +388,96 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     uint8_t* __restrict__ touched = touched0 + (size_t)rep * dims;
     float rs[HM_REP_SCALARS];
 #pragma unroll
-    for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = RSW[(size_t)g * HM_REP_SCALARS + k];
+    for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = active ? RSW[(size_t)g * HM_REP_SCALARS + k] : 0.f;
+    if constexpr (HOT) {
+        for (int h = threadIdx.x; h < H; h += 256) s_acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+    }
     double loss_acc = 0.0;
-    for (int64_t q = g; q < n_rows; q += W) {
-        const int64_t row = order ? (int64_t)order[q] : q;
-        const int64_t s = indptr[row], e = indptr[row + 1];
-        const float yy = y[row];
-        const float t = (float)(t0 + q + 1);
-        rs[RS_T] = t;
-        const StepK sk = step_consts(P, t);
-        int ci = -1;
-        float cx = 0.f;
-        if (s + lane < e) {
-            ci = idx[s + lane];
-            cx = val ? val[s + lane] : 1.f;
-            if (ci < 0 || ci >= dims) ci = -1;
-        }
-        F4 cst = {0.f, 0.f, 0.f, 0.f};
-        float p = 0.f, sq = 0.f;
-        if (ci >= 0) {
-            cst = ld4m<NT>(S + ci);
-            p = cst.w * cx;
-            sq = cx * cx;
-        }
-        for (int64_t k = s + 64 + lane; k < e; k += 64) {      // rows wider than a wave
-            const int i = idx[k];
-            const float x = val ? val[k] : 1.f;
-            if (i < 0 || i >= dims) continue;
-            p += ld4m<NT>(S + i).w * x;
-            sq += x * x;
-        }
-        p = hm::wave_sum(p);
-        sq = hm::wave_sum(sq);
-        const RowCoef c = row_rule(P, p, yy, 0.f, sq, rs);
-        loss_acc += c.loss;
-        if (ci >= 0) {
-            touched[ci] = 1;
-            if (c.update) {
-                if (RELOAD) cst = ld4m<NT>(S + ci);
-                feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
-                st4(S + ci, cst);
+    const int ch = HOT ? CH : 1;
+    const int64_t span = (int64_t)W * ch;
+    const int64_t nchunks = (n_rows + span - 1) / span;
+    for (int64_t ck = 0; ck < nchunks; ++ck) {
+        for (int j = 0; j < ch && active; ++j) {
+            const int64_t q = ck * span + (int64_t)j * W + g;
+            if (q >= n_rows) break;
+            const int64_t row = order ? (int64_t)order[q] : q;
+            const int64_t s = indptr[row], e = indptr[row + 1];
+            const float yy = y[row];
+            const float t = (float)(t0 + q + 1);
+            rs[RS_T] = t;
+            const StepK sk = step_consts(P, t);
+            int ci = -1, hs = -1;
+            float cx = 0.f;
+            if (s + lane < e) {
+                ci = idx[s + lane];
+                cx = val ? val[s + lane] : 1.f;
+                if (ci < 0 || ci >= dims) ci = -1;
+                if (HOT && ci >= 0) hs = hot_slot[ci];
+            }
+            F4 cst = {0.f, 0.f, 0.f, 0.f};
+            float p = 0.f, sq = 0.f;
+            if (ci >= 0) {
+                cst = ld4m<NT>(S + ci);
+                p = cst.w * cx;
+                sq = cx * cx;
+            }
+            for (int64_t k = s + 64 + lane; k < e; k += 64) {      // rows wider than a wave
+                const int i = idx[k];
+                const float x = val ? val[k] : 1.f;
+                if (i < 0 || i >= dims) continue;
+                p += ld4m<NT>(S + i).w * x;
+                sq += x * x;
+            }
+            p = hm::wave_sum(p);
+            sq = hm::wave_sum(sq);
+            const RowCoef c = row_rule(P, p, yy, 0.f, sq, rs);
+            loss_acc += c.loss;
+            if (ci >= 0) {
+                touched[ci] = 1;
+                if (c.update) {
+                    if (HOT && hs >= 0) {
+                        hot_add(&s_acc[hs], c.dloss * cx);
+                    } else {
+                        if (RELOAD) cst = ld4m<NT>(S + ci);
+                        feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
+                        st4(S + ci, cst);
+                    }
+                }
+            }
+            for (int64_t k = s + 64 + lane; k < e; k += 64) {
+                const int i = idx[k];
+                const float x = val ? val[k] : 1.f;
+                if (i < 0 || i >= dims) continue;
+                touched[i] = 1;
+                if (!c.update) continue;
+                if (HOT) {
+                    const int h = hot_slot[i];
+                    if (h >= 0) {
+                        hot_add(&s_acc[h], c.dloss * x);
+                        continue;
+                    }
+                }
+                F4 st = ld4m<NT>(S + i);
+                feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
+                st4(S + i, st);
             }
         }
-        for (int64_t k = s + 64 + lane; k < e; k += 64) {
-            const int i = idx[k];
-            const float x = val ? val[k] : 1.f;
-            if (i < 0 || i >= dims) continue;
-            touched[i] = 1;
-            if (!c.update) continue;
-            F4 st = ld4m<NT>(S + i);
-            feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
-            st4(S + i, st);
+        if constexpr (HOT) {
+            // every wave of the block has finished its CH rows of this chunk
+            __syncthreads();
+            const int64_t tend = t0 + min(n_rows, (ck + 1) * span);
+            const StepK sk = step_consts(P, (float)tend);
+            for (int h = threadIdx.x; h < H; h += 256) {
+                const float4 a = s_acc[h];
+                if (a.z == 0.f) continue;
+                s_acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                hot_flush(P, S + hot_feat[h], a, sk);
+            }
+            __syncthreads();
         }
     }
-    if (lane == 0) {
+    if (active && lane == 0) {
 #pragma unroll
         for (int k = 0; k < HM_REP_SCALARS; ++k) RSW[(size_t)g * HM_REP_SCALARS + k] = rs[k];
         loss_out[g] = loss_acc;
@@ -482,18 +551,31 @@ HM_API int hm_linear_predict(const float* w, int dims, int L, const int64_t* ind
 HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int64_t t0, int W, int R,
                                   int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,
-                                  float* RSW, double* loss_out, hipStream_t stream) {
+                                  float* RSW, double* loss_out, const int32_t* hot_slot, const int32_t* hot_feat,
+                                  int H, int CH, hipStream_t stream) {
     if (n_rows <= 0) return 0;
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
-#define HM_SHARED_LAUNCH(RL, NTT)                                                                      \
-    hipLaunchKernelGGL((linear_shared_kernel<RL, NTT>), dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows, \
+    const bool hot = H > 0;
+    if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 ||
+                P->algo != A_GENERAL || (P->opt != O_SGD && P->opt != O_ADAGRAD) ||
+                (P->reg != R_NO && P->reg != R_L2)))
+        return (int)hipErrorInvalidValue;
+#define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
+    hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows, \
                        dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
-                       RSW, loss_out)
-    if (reload && nt) HM_SHARED_LAUNCH(true, true);
-    else if (reload) HM_SHARED_LAUNCH(true, false);
-    else if (nt) HM_SHARED_LAUNCH(false, true);
-    else HM_SHARED_LAUNCH(false, false);
+                       RSW, loss_out, hot_slot, hot_feat, H, CH)
+    if (hot) {
+        if (reload && nt) HM_SHARED_LAUNCH(true, true, true);
+        else if (reload) HM_SHARED_LAUNCH(true, false, true);
+        else if (nt) HM_SHARED_LAUNCH(false, true, true);
+        else HM_SHARED_LAUNCH(false, false, true);
+    } else {
+        if (reload && nt) HM_SHARED_LAUNCH(true, true, false);
+        else if (reload) HM_SHARED_LAUNCH(true, false, false);
+        else if (nt) HM_SHARED_LAUNCH(false, true, false);
+        else HM_SHARED_LAUNCH(false, false, false);
+    }
 #undef HM_SHARED_LAUNCH
     HM_LAUNCH_RET();
 }

@@ -624,6 +624,25 @@ def feature_pairs(features, options=None):
             yield (ha, hb, xa, xb)
 
 
+def _feature_pairs_batch(features, options=None):
+    """Column-at-once ``feature_pairs(features, '-ffm ...')`` for LATERAL VIEW (a constant option
+    string); None -> the per-row path."""
+    if options is not None:
+        ops = set(map(str, options))
+        if len(ops) != 1:
+            return None
+        options = ops.pop()
+    cl = _FP_OPTS.parse(options)
+    if not cl["ffm"]:
+        return None
+    from ..models.ffm_keys import ffm_pair_columns
+    rows_idx, cols = ffm_pair_columns(features, cl)
+    return rows_idx, [cols["i"], cols["j"], cols["xi"], cols["xj"]]
+
+
+feature_pairs.batch = _feature_pairs_batch
+
+
 # ------------------------------------------------------------------ ranking / sampling
 _BPR_OPTS = Options([opt("sampling_rate", None, 1.0, float, "Sampling rate"),
                      flag("with_replacement", None, "Sample with replacement"),

@@ -46,6 +46,60 @@ def ffm_pair_rows(features, cl):
                    float(val[a]), float(val[b]))
 
 
+def ffm_pair_columns(rows: list, cl):
+    """``ffm_pair_rows`` for a whole column at once (the LATERAL VIEW batch path): returns
+    (source row of every output row, {i, j, xi, xj} arrays), rows in the per-row order.  NULL
+    feature lists produce no rows.  ``j`` / ``xj`` are NaN where the per-row path yields NULL
+    (the float64 column pandas builds from those rows)."""
+    nf = (1 << cl["feature_hashing"]) if cl["feature_hashing"] > 0 else (1 << 24)
+    F = int(cl["num_fields"])
+    keep = np.asarray([r is not None for r in rows], dtype=bool)
+    src = np.nonzero(keep)[0]
+    csr = parse_ffm_rows([list(rows[r]) for r in src], nf, F, hash_ints=cl["feature_hashing"] > 0)
+    indptr = np.asarray(csr.indptr, dtype=np.int64)
+    idx = np.asarray(csr.idx, dtype=np.int64)
+    fld = np.asarray(csr.fld, dtype=np.int64)
+    val = np.asarray(csr.val, dtype=np.float32).astype(np.float64)
+    lens = np.diff(indptr)
+    n = len(src)
+    if not cl.has("no_norm") or not cl["no_norm"]:
+        row_of = np.repeat(np.arange(n), lens)
+        norm = np.sqrt(np.bincount(row_of, weights=val * val, minlength=n))
+        norm[norm == 0] = 1.0
+        val = val / norm[row_of]
+    nb = 0 if cl["no_bias"] else 1
+    cnt = nb + lens + lens * (lens - 1) // 2
+    start = np.zeros(n, dtype=np.int64)
+    np.cumsum(cnt[:-1], out=start[1:])
+    total = int(cnt.sum())
+    I = np.empty(total, dtype=np.int64)
+    J = np.full(total, np.nan)
+    XI = np.empty(total, dtype=np.float64)
+    XJ = np.full(total, np.nan)
+    if nb:
+        I[start] = -1
+        XI[start] = 1.0
+    for L in np.unique(lens):
+        L = int(L)
+        if L == 0:
+            continue
+        rs = np.nonzero(lens == L)[0]
+        base = start[rs] + nb
+        fi = indptr[rs][:, None] + np.arange(L)
+        ii, vv, ff = idx[fi], val[fi], fld[fi]
+        pos = base[:, None] + np.arange(L)
+        I[pos] = ii
+        XI[pos] = vv
+        a, b = np.triu_indices(L, 1)
+        if len(a):
+            pos = base[:, None] + L + np.arange(len(a))
+            I[pos] = nf + ii[:, a] * F + ff[:, b]
+            J[pos] = nf + ii[:, b] * F + ff[:, a]
+            XI[pos] = vv[:, a]
+            XJ[pos] = vv[:, b]
+    return np.repeat(src, cnt), {"i": I, "j": J, "xi": XI, "xj": XJ}
+
+
 @udaf("ffm_predict")
 def ffm_predict(Wi, Vi, Vj, Xi, Xj):
     """Σ Wi·Xi over linear/bias rows + Σ <Vi, Vj>·Xi·Xj over pair rows (raw score)."""

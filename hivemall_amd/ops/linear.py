@@ -10,6 +10,7 @@ State layout (``LinearState``):
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -170,6 +171,40 @@ def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, r
     return st
 
 
+HOT_MAX = 4096          # csrc/kernels/linear.hip HM_HOT_MAX (64 KB of LDS accumulators)
+
+
+def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
+    """The features the shared-table kernel pre-aggregates per block instead of updating them
+    Hogwild (csrc/kernels/linear.hip, HOT): the at most ``HOT_MAX`` most frequent features of
+    the pass that more than one in-flight row is expected to hit (count >= n_rows / W), for the
+    rules whose update is a function of the summed gradients (general learner, SGD / AdaGrad,
+    no or L2 regularisation).  Returns (hot_slot i32 [dims], hot_feat i32 [H]) or None.
+    Cached per index tensor (epochs reuse it).  ``HM_LINEAR_HOT=0`` disables."""
+    if os.environ.get("HM_LINEAR_HOT", "1") == "0":
+        return None
+    if not (P.algo == ALGOS["general"] and P.opt in (OPTIMIZERS["sgd"], OPTIMIZERS["adagrad"])
+            and P.reg in (REGS["no"], REGS["l2"]) and P.n_labels == 1):
+        return None
+    key = (idx.data_ptr(), idx.numel(), st.dims, n_rows)
+    hit = st.meta.get("hot")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    W = st.RS.shape[0]
+    ids = idx.long()
+    ids = ids[(ids >= 0) & (ids < st.dims)]
+    cnt = torch.bincount(ids, minlength=st.dims)
+    vals, feats = torch.topk(cnt, min(HOT_MAX, st.dims))
+    feats = feats[vals >= max(2, n_rows // max(1, W))].to(torch.int32)
+    res = None
+    if feats.numel():
+        slot = torch.full((st.dims,), -1, dtype=torch.int32, device=idx.device)
+        slot[feats.long()] = torch.arange(feats.numel(), dtype=torch.int32, device=idx.device)
+        res = (slot, feats.contiguous())
+    st.meta["hot"] = (key, res)
+    return res
+
+
 def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.Tensor,
                       val: torch.Tensor | None, y: torch.Tensor, t0: int,
                       order: torch.Tensor | None = None) -> torch.Tensor:
@@ -186,11 +221,15 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     W = st.RS.shape[0]
     loss = torch.zeros(W, dtype=torch.float64, device=dev)
     p = _native.ptr
+    hot = hot_features(st, P, idx, n) if W > 1 else None
+    hs, hf, H = (hot[0], hot[1], hot[1].numel()) if hot is not None else (None, None, 0)
+    ch = int(os.environ.get("HM_LINEAR_HOT_CH", "16"))
     rc = _native.hip().hm_linear_train_shared(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
                                               st.R, int(st.meta.get("reload", False)),
                                               int(st.meta.get("nt", True)),
                                               p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
-                                              p(st.touched), p(st.RS), p(loss), _native.stream_of(dev))
+                                              p(st.touched), p(st.RS), p(loss), p(hs), p(hf), H, ch,
+                                              _native.stream_of(dev))
     _native.check(rc, "hm_linear_train_shared")
     return loss
 
@@ -274,7 +313,8 @@ _P = _native.c_p
 _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
-                                              C.c_int, C.c_int] + [_P] * 9 + [_P])
+                                              C.c_int, C.c_int] + [_P] * 9 + [_P, _P, C.c_int, C.c_int]
+                     + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
 _native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])

@@ -13,6 +13,7 @@ from __future__ import annotations
 import fnmatch
 import itertools
 import math
+import os
 import re
 from dataclasses import dataclass
 
@@ -557,6 +558,18 @@ class Session:
             fast = self._explode_lists(src, lv, args[0])
             if fast is not None:
                 return fast
+        batch = getattr(impl, "batch", None)
+        if per_row and batch is not None and not lv.outer and os.environ.get("HM_SQL_BATCH_UDTF", "1") != "0":
+            # column-at-once form of a per-row UDTF (e.g. feature_pairs '-ffm'): same rows, same
+            # order, no Python generator per input row
+            res = batch(*args)
+            if res is not None:
+                rows_idx, cols = res
+                names = lv.col_aliases or list(default_cols or [f"col{i}" for i in range(len(cols))])
+                if len(names) == len(cols):
+                    new = Frame(pd.DataFrame({f"c{i}": c for i, c in enumerate(cols)}),
+                                [(lv.table_alias, n) for n in names])
+                    return Frame.concat_cols(src.take(np.asarray(rows_idx, dtype=np.int64)), new)
         rows_idx, out_rows = [], []
         if per_row:
             for r in range(src.n):

@@ -141,3 +141,27 @@ def test_amplify_and_rand_amplify(sess):
     assert len(r) == 9000
     r = sess.sql("SELECT rand_amplify(2, 100, rowid, label) AS (rowid, label) FROM train")
     assert len(r) == 6000 and sorted(r["rowid"].tolist()) == sorted(list(range(3000)) * 2)
+
+
+@pytest.mark.parametrize("opt", ["-ffm -feature_hashing 10 -num_fields 7", "-ffm -feature_hashing 10 -num_fields 7 -no_bias"])
+def test_feature_pairs_batch_path_equals_per_row(opt, monkeypatch):
+    """LATERAL VIEW feature_pairs('-ffm'): the column-at-once path (models/ffm_keys.
+    ffm_pair_columns) returns the per-row generator's table exactly — rows, order, dtypes,
+    NULLs — including NULL rows, empty rows, named features and explicit values."""
+    rng = np.random.default_rng(3)
+    rows = []
+    for _ in range(400):
+        nf = int(rng.integers(0, 7))
+        rows.append([f"{f}:{int(rng.integers(0, 30))}" + (f":{rng.uniform(0.1, 3):.3f}" if rng.random() < 0.5 else "")
+                     for f in range(nf)])
+    rows[3] = None
+    rows[5] = ["2:abc:1.5", "0:xyz"]
+    df = pd.DataFrame({"rowid": range(400), "features": rows})
+    q = f"SELECT rowid, i, j, Xi, Xj FROM t LATERAL VIEW feature_pairs(features, '{opt}') x AS i, j, Xi, Xj"
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HM_SQL_BATCH_UDTF", mode)
+        s = Session(device="cpu")
+        s.register("t", df)
+        out.append(s.sql(q))
+    pd.testing.assert_frame_equal(out[0], out[1])
