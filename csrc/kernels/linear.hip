@@ -343,12 +343,23 @@ __device__ __forceinline__ F4 ld4m(const float4* p) {
 // pass's feature counts) are not read-modify-written per row: each block sums their gradients
 // (sum g, sum g^2, count) in LDS over a chunk of CH rows per wave, then applies them with one
 // returning float atomic on G and one on w per touched hot feature (AdaGrad / SGD of the general
-// learner, no or L2 regularisation).  No update of a hot feature is lost, and the atomics on its
+// learner, no or L2 regularisation; AdaGrad-RDA: atomics on its two sums, w recomputed).  No update of a hot feature is lost, and the atomics on its
 // address drop by 4*CH x.  Cold features keep the Hogwild read-modify-write.
 constexpr int HM_HOT_MAX = 4096;
 
 __device__ __forceinline__ void hot_flush(const Params& P, float4* __restrict__ s, float4 a, const StepK& k) {
     float gs = a.x, g2 = a.y;
+    if (P.reg == R_RDA) {
+        // AdaGrad-RDA (optimizer_update O_ADAGRAD_RDA): w is a function of the running sums
+        // u = sum g and G = sum g^2 and of t, so the sums are added atomically and w rewritten
+        // from the totals this flush observed
+        const float u = atomicAdd(&s->y, gs) + gs;
+        const float G = atomicAdd(&s->z, g2) + g2;
+        const float sign = u > 0.f ? 1.f : -1.f;
+        const float mean = sign * u / k.t - P.lambda;
+        s->x = mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
+        return;
+    }
     if (P.reg == R_L2) {
         const float w = __builtin_nontemporal_load(&s->x);
         const float lw = P.lambda * w;
@@ -559,7 +570,7 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
     const bool hot = H > 0;
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 ||
                 P->algo != A_GENERAL || (P->opt != O_SGD && P->opt != O_ADAGRAD) ||
-                (P->reg != R_NO && P->reg != R_L2)))
+                (P->reg != R_NO && P->reg != R_L2 && !(P->reg == R_RDA && P->opt == O_ADAGRAD))))
         return (int)hipErrorInvalidValue;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows, \

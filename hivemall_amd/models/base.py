@@ -65,6 +65,14 @@ class ConversionState:
         return converged
 
 
+# per-epoch checkpoint / resume of a learner's epoch loop
+CKPT_OPTS = [
+    opt("checkpoint", "checkpoint_dir", None, str,
+        "[engine] directory for per-epoch checkpoints; a rerun of the same query resumes after "
+        "the newest epoch every rank completed (parallel.elastic.ResumableLoop)"),
+    opt("checkpoint_every", None, 1, int, "[engine] epochs between checkpoints"),
+]
+
 COMMON_ITER_OPTS = [
     opt("iters", "iterations", 1, int, "The maximum number of iterations (epochs)", aliases=("iter",)),
     opt("cv_rate", "convergence_rate", 0.005, float, "Threshold to determine convergence"),
@@ -74,10 +82,10 @@ COMMON_ITER_OPTS = [
     opt("mix_interval", None, 0, int, "[engine] RCCL model-mix every N batches (0 = at end only)"),
     flag("mix_sparse", None, "[engine] mix only the rows touched since the last mix: all-gather "
          "of (index, delta) instead of a dense all-reduce (parallel.mix.SparseDeltaMixer)"),
-]
+] + CKPT_OPTS
 
-# data-parallel mixing options of the learners that do not take COMMON_ITER_OPTS
-MIX_OPTS = [COMMON_ITER_OPTS[-2], COMMON_ITER_OPTS[-1]]
+# data-parallel mixing (+ checkpoint) options of the learners that do not take COMMON_ITER_OPTS
+MIX_OPTS = [COMMON_ITER_OPTS[-4], COMMON_ITER_OPTS[-3]] + CKPT_OPTS
 
 
 def parse_labels_binary(y) -> np.ndarray:
@@ -142,6 +150,37 @@ class Learner:
         self.cv.incr_loss(total)
         self._log_epoch(total, rows)
         return self.cv.is_converged()
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def epochs(self, n: int):
+        """The epoch indices of a training loop.  With ``-checkpoint <dir>`` the learner's whole
+        state is saved after every ``-checkpoint_every`` epochs (per rank, atomically), and a
+        rerun resumes after the newest epoch that every rank completed — the same rows and
+        options replay bit-identically on the deterministic engines.  ``HM_FAULT=rank:epoch``
+        injects a crash before that epoch (parallel.elastic)."""
+        try:
+            ckpt = self.cl.get("checkpoint")
+        except KeyError:
+            ckpt = None
+        if not ckpt:
+            yield from range(n)
+            return
+        from ..parallel.elastic import ResumableLoop, maybe_inject_fault
+
+        loop = ResumableLoop(self, ckpt, every=int(self.cl.get("checkpoint_every") or 1),
+                             ctx=getattr(self.mixer, "ctx", None))
+        start = loop.resume(self.device)
+        if start > 0:
+            keep = {"mixer": self.mixer, "rank": self.rank, "kw": self.kw}
+            self.__dict__.update(loop.learner.__dict__)
+            self.__dict__.update(keep)
+            loop.learner = self
+            log.info("%s: resumed from %s after epoch %d", self.NAME, ckpt, start - 1)
+        for ep in range(start, n):
+            maybe_inject_fault(loop.rank, ep)
+            yield ep
+            if (ep + 1) % loop.every == 0 or ep + 1 == n:
+                loop.save(ep)
 
     # ------------------------------------------------------------------ metrics stream
     @property

@@ -225,11 +225,12 @@ class FFMTrainer(Learner):
         self._ensure_state()
         loss_buf = torch.empty(b.n, dtype=torch.float32, device=self.device)
         iters = int(self.cl["iters"])
-        g = torch.Generator(device="cpu").manual_seed(self.seed)
-        for ep in range(iters):
+        for ep in self.epochs(iters):
             if ep == 0:
                 eb = b
             else:  # per-epoch device-side shuffle (replaces rand_amplify / spill replay)
+                # seeded per epoch, so a resumed run draws the same order as an uninterrupted one
+                g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + ep)
                 perm = torch.randperm(b.n, generator=g).to(self.device)
                 f = lambda t: None if t is None else t.index_select(0, perm).contiguous()
                 eb = FFMBatch(f(b.idx), f(b.fld), f(b.val), f(b.y))

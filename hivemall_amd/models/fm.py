@@ -213,7 +213,7 @@ class FMTrainer(Learner):
             va = _slice_rows(rows, rows.n - nva, rows.n)
             rows = _slice_rows(rows, 0, rows.n - nva)
         loss_buf = torch.empty(rows.n, dtype=torch.float32, device=self.device)
-        for ep in range(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"])):
             self.train_rows(rows, loss_buf)
             if va is not None:
                 self._adapt_lambda(va)

@@ -30,7 +30,7 @@ import torch
 from ..ops import linear as LO
 from ..utils.features import CSR, FeatureEncoder
 from ..utils.options import UDFArgumentException, flag, opt
-from .base import ConversionState, Learner, log
+from .base import CKPT_OPTS, ConversionState, Learner, log
 from ..utils.reduce import tmax, tmin
 
 # ------------------------------------------------------------------ option specs
@@ -64,7 +64,7 @@ LEARNER_BASE_OPTS = [
         "after every pass"),
     opt("shared_waves", None, 512, int,
         "[engine] shared engine: rows in flight (more = faster, staler hot features)"),
-]
+] + CKPT_OPTS
 
 GENERAL_OPTS = [
     opt("loss", "loss_function", None, str, "Loss function"),
@@ -379,7 +379,7 @@ class OnlineLinearLearner(Learner):
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         iters = int(self.cl["iters"])
         shared = self.state.meta.get("shared", False)
-        for ep in range(iters):
+        for ep in self.epochs(iters):
             if shared:
                 loss = LO.train_pass_shared(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
                                             self.rows_seen)

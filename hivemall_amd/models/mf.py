@@ -297,7 +297,7 @@ class MatrixFactorization(_MFBase):
         self.seen_u[u.long()] = True
         self.seen_i[i.long()] = True
         loss = torch.empty(u.numel(), device=dev)
-        for ep in range(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"])):
             self._step(u, i, r, loss=loss)
             self._epoch_mix(ep)
             el = self.dp_sum(float(loss.double().sum().item()))
@@ -513,7 +513,7 @@ class BPRMF(_MFBase):
         self.seen_u[tu.long()] = True
         self.seen_i[ti.long()] = True
         self.seen_i[tj.long()] = True
-        for ep in range(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"])):
             el = self.dp_sum(self.step(tu, ti, tj))
             self._epoch_end(el)
             self._epoch_mix(ep)

@@ -179,12 +179,14 @@ def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     Hogwild (csrc/kernels/linear.hip, HOT): the at most ``HOT_MAX`` most frequent features of
     the pass that more than one in-flight row is expected to hit (count >= n_rows / W), for the
     rules whose update is a function of the summed gradients (general learner, SGD / AdaGrad,
-    no or L2 regularisation).  Returns (hot_slot i32 [dims], hot_feat i32 [H]) or None.
+    no or L2 regularisation, AdaGrad-RDA).  Returns (hot_slot i32 [dims], hot_feat i32 [H]) or None.
     Cached per index tensor (epochs reuse it).  ``HM_LINEAR_HOT=0`` disables."""
     if os.environ.get("HM_LINEAR_HOT", "1") == "0":
         return None
     if not (P.algo == ALGOS["general"] and P.opt in (OPTIMIZERS["sgd"], OPTIMIZERS["adagrad"])
-            and P.reg in (REGS["no"], REGS["l2"]) and P.n_labels == 1):
+            and (P.reg in (REGS["no"], REGS["l2"])
+                 or (P.reg == REGS["rda"] and P.opt == OPTIMIZERS["adagrad"]))
+            and P.n_labels == 1):
         return None
     key = (idx.data_ptr(), idx.numel(), st.dims, n_rows)
     hit = st.meta.get("hot")
