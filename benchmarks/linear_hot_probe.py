@@ -39,7 +39,7 @@ def main():
                       "rows_per_s": round(N * EPOCHS / (time.perf_counter() - t0)),
                       "heldout_logloss": round(seq, 5)}), flush=True)
     tr, te = tr_c.to("cuda"), te_c.to("cuda")
-    grid = [(0, 512, 16)] + [(1, W, ch) for W in (512, 2048) for ch in (4, 16, 64)]
+    grid = [(0, 512, 16), (0, 512, 16)] + [(1, W, ch) for W, ch in ((512, 64), (1024, 16), (1024, 32), (2048, 8), (2048, 16), (4096, 4), (4096, 8))]
     for hot, W, ch in grid:
         os.environ["HM_LINEAR_HOT"] = str(hot)
         os.environ["HM_LINEAR_HOT_CH"] = str(ch)

@@ -345,39 +345,62 @@ __device__ __forceinline__ F4 ld4m(const float4* p) {
 // returning float atomic on G and one on w per touched hot feature (AdaGrad / SGD of the general
 // learner, no or L2 regularisation; AdaGrad-RDA: atomics on its two sums, w recomputed).  No update of a hot feature is lost, and the atomics on its
 // address drop by 4*CH x.  Cold features keep the Hogwild read-modify-write.
-constexpr int HM_HOT_MAX = 4096;
+constexpr int HM_HOT_MAX = 8192;          // <= 96 KB of LDS accumulators
 
-__device__ __forceinline__ void hot_flush(const Params& P, float4* __restrict__ s, float4 a, const StepK& k) {
-    float gs = a.x, g2 = a.y;
+// Flush of up to 4 hot features per thread: all returning atomics are issued before any result
+// is used, so their round trips overlap instead of running back to back.
+constexpr int HM_HOT_U = 4;
+
+__device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__ S, float (&gs)[HM_HOT_U],
+                                           float (&g2)[HM_HOT_U], const float (&cnt)[HM_HOT_U],
+                                           const int (&f)[HM_HOT_U], const StepK& k) {
+    float r1[HM_HOT_U], r2[HM_HOT_U];
+    if (P.reg == R_L2) {
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u) {
+            if (f[u] < 0) continue;
+            const float lw = P.lambda * __builtin_nontemporal_load(&S[f[u]].x);
+            g2[u] += 2.f * lw * gs[u] + cnt[u] * lw * lw;
+            gs[u] += cnt[u] * lw;
+        }
+    }
     if (P.reg == R_RDA) {
         // AdaGrad-RDA (optimizer_update O_ADAGRAD_RDA): w is a function of the running sums
         // u = sum g and G = sum g^2 and of t, so the sums are added atomically and w rewritten
         // from the totals this flush observed
-        const float u = atomicAdd(&s->y, gs) + gs;
-        const float G = atomicAdd(&s->z, g2) + g2;
-        const float sign = u > 0.f ? 1.f : -1.f;
-        const float mean = sign * u / k.t - P.lambda;
-        s->x = mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
-        return;
-    }
-    if (P.reg == R_L2) {
-        const float w = __builtin_nontemporal_load(&s->x);
-        const float lw = P.lambda * w;
-        g2 += 2.f * lw * gs + a.z * lw * lw;
-        gs += a.z * lw;
-    }
-    if (P.opt == O_ADAGRAD) {
-        const float gn = atomicAdd(&s->y, g2) + g2;
-        atomicAdd(&s->x, -k.eta * gs / (sqrtf(gn) + P.eps));
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u) {
+            if (f[u] < 0) continue;
+            r1[u] = atomicAdd(&S[f[u]].y, gs[u]);
+            r2[u] = atomicAdd(&S[f[u]].z, g2[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u) {
+            if (f[u] < 0) continue;
+            const float uu = r1[u] + gs[u], G = r2[u] + g2[u];
+            const float sign = uu > 0.f ? 1.f : -1.f;
+            const float mean = sign * uu / k.t - P.lambda;
+            S[f[u]].x = mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
+        }
+    } else if (P.opt == O_ADAGRAD) {
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u)
+            if (f[u] >= 0) r2[u] = atomicAdd(&S[f[u]].y, g2[u]);
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u)
+            if (f[u] >= 0) atomicAdd(&S[f[u]].x, -k.eta * gs[u] / (sqrtf(r2[u] + g2[u]) + P.eps));
     } else {
-        atomicAdd(&s->x, -k.eta * gs);
+#pragma unroll
+        for (int u = 0; u < HM_HOT_U; ++u)
+            if (f[u] >= 0) atomicAdd(&S[f[u]].x, -k.eta * gs[u]);
     }
 }
 
-__device__ __forceinline__ void hot_add(float4* acc, float g) {
-    atomicAdd(&acc->x, g);
-    atomicAdd(&acc->y, g * g);
-    atomicAdd(&acc->z, 1.f);
+// LDS accumulators, structure of arrays: sum g [H] | sum g^2 [H] | count [H] (count: L2 only)
+__device__ __forceinline__ void hot_add(float* acc, int H, bool cnt, int h, float g) {
+    atomicAdd(acc + h, g);
+    atomicAdd(acc + H + h, g * g);
+    if (cnt) atomicAdd(acc + 2 * H + h, 1.f);
 }
 
 template <bool RELOAD, bool NT, bool HOT>
@@ -387,7 +410,8 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     const int32_t* __restrict__ order, float4* __restrict__ S0, uint8_t* __restrict__ touched0,
     float* __restrict__ RSW, double* __restrict__ loss_out, const int32_t* __restrict__ hot_slot,
     const int32_t* __restrict__ hot_feat, int H, int CH) {
-    __shared__ float4 s_acc[HOT ? HM_HOT_MAX : 1];
+    extern __shared__ float s_acc[];             // HOT: H x (2 or 3) floats, see hot_add
+    const bool hcnt = HOT && P.reg == R_L2;
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool active = g < W;
@@ -401,7 +425,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
 #pragma unroll
     for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = active ? RSW[(size_t)g * HM_REP_SCALARS + k] : 0.f;
     if constexpr (HOT) {
-        for (int h = threadIdx.x; h < H; h += 256) s_acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int h = threadIdx.x; h < (hcnt ? 3 : 2) * H; h += 256) s_acc[h] = 0.f;
         __syncthreads();
     }
     double loss_acc = 0.0;
@@ -448,7 +472,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                 touched[ci] = 1;
                 if (c.update) {
                     if (HOT && hs >= 0) {
-                        hot_add(&s_acc[hs], c.dloss * cx);
+                        hot_add(s_acc, H, hcnt, hs, c.dloss * cx);
                     } else {
                         if (RELOAD) cst = ld4m<NT>(S + ci);
                         feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
@@ -465,7 +489,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                 if (HOT) {
                     const int h = hot_slot[i];
                     if (h >= 0) {
-                        hot_add(&s_acc[h], c.dloss * x);
+                        hot_add(s_acc, H, hcnt, h, c.dloss * x);
                         continue;
                     }
                 }
@@ -479,11 +503,24 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             __syncthreads();
             const int64_t tend = t0 + min(n_rows, (ck + 1) * span);
             const StepK sk = step_consts(P, (float)tend);
-            for (int h = threadIdx.x; h < H; h += 256) {
-                const float4 a = s_acc[h];
-                if (a.z == 0.f) continue;
-                s_acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-                hot_flush(P, S + hot_feat[h], a, sk);
+            for (int h0 = threadIdx.x; h0 < H; h0 += 256 * HM_HOT_U) {
+                float gs[HM_HOT_U], g2[HM_HOT_U], cnt[HM_HOT_U];
+                int f[HM_HOT_U];
+#pragma unroll
+                for (int u = 0; u < HM_HOT_U; ++u) {
+                    const int h = h0 + u * 256;
+                    gs[u] = h < H ? s_acc[h] : 0.f;
+                    g2[u] = h < H ? s_acc[H + h] : 0.f;
+                    cnt[u] = hcnt && h < H ? s_acc[2 * H + h] : 0.f;
+                    // a hot feature whose rows all had a zero gradient needs no update either
+                    f[u] = g2[u] != 0.f ? hot_feat[h] : -1;
+                    if (f[u] >= 0) {
+                        s_acc[h] = 0.f;
+                        s_acc[H + h] = 0.f;
+                        if (hcnt) s_acc[2 * H + h] = 0.f;
+                    }
+                }
+                hot_flush4(P, S, gs, g2, cnt, f, sk);
             }
             __syncthreads();
         }
@@ -568,12 +605,13 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
     const bool hot = H > 0;
+    const size_t lds = hot ? (size_t)H * (P->reg == R_L2 ? 3 : 2) * sizeof(float) : 0;
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 ||
                 P->algo != A_GENERAL || (P->opt != O_SGD && P->opt != O_ADAGRAD) ||
                 (P->reg != R_NO && P->reg != R_L2 && !(P->reg == R_RDA && P->opt == O_ADAGRAD))))
         return (int)hipErrorInvalidValue;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
-    hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), 0, stream, *P, n_rows, \
+    hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \
                        dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
                        RSW, loss_out, hot_slot, hot_feat, H, CH)
     if (hot) {

@@ -193,11 +193,16 @@ def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     if hit is not None and hit[0] == key:
         return hit[1]
     W = st.RS.shape[0]
-    ids = idx.long()
+    # counts from a strided sample of the indices (a prime stride: coprime with any row width
+    # it does not divide, so every field is sampled): the hot set only needs the frequent features, and a full bincount of
+    # a large pass costs as much as a training epoch
+    want = idx.numel() // (1 << 22)
+    stride = next((q for q in (1, 17, 31, 61, 127, 251, 509, 1021) if q >= want), 2039)
+    ids = idx[::stride].long()
     ids = ids[(ids >= 0) & (ids < st.dims)]
     cnt = torch.bincount(ids, minlength=st.dims)
     vals, feats = torch.topk(cnt, min(HOT_MAX, st.dims))
-    feats = feats[vals >= max(2, n_rows // max(1, W))].to(torch.int32)
+    feats = feats[vals * stride >= max(2, n_rows // max(1, W))].to(torch.int32)
     res = None
     if feats.numel():
         slot = torch.full((st.dims,), -1, dtype=torch.int32, device=idx.device)
