@@ -305,3 +305,70 @@ HM_API int64_t hm_parse_ffm_features(const uint8_t* buf, const int64_t* off, int
     }
     return -1;
 }
+
+// ---------------------------------------------------------------- int64 open-addressing probe
+// Bulk probe of utils/collections._OpenHashTable (power-of-two table of int64 keys, INT64_MIN =
+// empty, splitmix64 slot, linear probing): out[i] = slot of keys[i] (-1 when absent and not
+// inserting).  insert != 0: absent keys claim the first empty slot of their probe sequence, in
+// input order (sequential; returns the number inserted); lookups run in parallel.
+static inline uint64_t oht_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+HM_API int64_t hm_oht_probe(int64_t* table, int64_t cap, const int64_t* keys, int64_t n, int64_t* out,
+                            int insert) {
+    const int64_t empty = INT64_MIN;
+    const uint64_t mask = (uint64_t)cap - 1;
+    if (insert) {
+        int64_t added = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t k = keys[i];
+            uint64_t h = oht_mix64((uint64_t)k) & mask;
+            while (table[h] != k && table[h] != empty) h = (h + 1) & mask;
+            if (table[h] == empty) {
+                table[h] = k;
+                ++added;
+            }
+            out[i] = (int64_t)h;
+        }
+        return added;
+    }
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t k = keys[i];
+        uint64_t h = oht_mix64((uint64_t)k) & mask;
+        int64_t r = -1;
+        for (;;) {
+            const int64_t t = table[h];
+            if (t == k) { r = (int64_t)h; break; }
+            if (t == empty) break;
+            h = (h + 1) & mask;
+        }
+        out[i] = r;
+    }
+    return 0;
+}
+
+// Lookup straight to values for int64-valued tables (Int2LongOpenHashTable.get_many): out[i] =
+// vals[slot of keys[i]], or dflt when absent.
+HM_API void hm_oht_get_i64(const int64_t* table, const int64_t* vals, int64_t cap, const int64_t* keys,
+                           int64_t n, int64_t dflt, int64_t* out) {
+    const int64_t empty = INT64_MIN;
+    const uint64_t mask = (uint64_t)cap - 1;
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t k = keys[i];
+        uint64_t h = oht_mix64((uint64_t)k) & mask;
+        int64_t r = dflt;
+        for (;;) {
+            const int64_t t = table[h];
+            if (t == k) { r = vals[h]; break; }
+            if (t == empty) break;
+            h = (h + 1) & mask;
+        }
+        out[i] = r;
+    }
+}

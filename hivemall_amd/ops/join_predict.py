@@ -86,16 +86,9 @@ def join_ffm(ti, tj, xi, xj, g, W1, V1, m1, V2, m2, n_groups: int, device=None):
         rc = _native.hip().hm_join_ffm(*[p(t) for t in ts], len(ti), k, p(out), _native.stream_of(dev))
         _native.check(rc, "hm_join_ffm")
         return out.cpu().numpy()
-    ok = ti >= 0
-    a = np.where(ok, ti, 0)
-    b = np.where(tj >= 0, tj, 0)
-    both = ok & (tj >= 0) & m1[a].astype(bool) & m2[b].astype(bool)
-    val = np.zeros(len(ti))
-    if both.any():
-        d = np.einsum("ij,ij->i", V1[a[both]].astype(np.float64), V2[b[both]].astype(np.float64))
-        val[both] = d * xi[both].astype(np.float64) * xj[both].astype(np.float64)
-    lin = ok & ~both
-    w = W1[a].astype(np.float64)
-    lw = lin & ~np.isnan(w)
-    val[lw] = w[lw] * xi[lw].astype(np.float64)
+    c = lambda a, dt: np.ascontiguousarray(a, dtype=dt)   # noqa: E731
+    ts = (c(ti, np.int32), c(tj, np.int32), c(xi, np.float32), c(xj, np.float32), c(W1, np.float32),
+          c(V1, np.float32), c(m1, np.uint8), c(V2, np.float32), c(m2, np.uint8))
+    val = np.empty(len(ti), dtype=np.float64)
+    _native.host().hm_join_ffm_rows_cpu(*[t.ctypes.data for t in ts], len(ti), k, val.ctypes.data)
     return np.bincount(g, weights=val, minlength=n_groups)

@@ -312,9 +312,39 @@ def _which(col: Col, frames):
     return hits[0] if len(hits) == 1 else (None, None)
 
 
+def _int_keys(s: pd.Series):
+    """int64 keys of an all-integral, NULL-free numeric column (else None)."""
+    if not pd.api.types.is_numeric_dtype(s) or pd.api.types.is_bool_dtype(s):
+        return None
+    a = s.to_numpy()
+    if a.dtype.kind in "iu":
+        return a.astype(np.int64, copy=False)
+    if a.dtype.kind == "f" and not np.isnan(a).any() and np.all(a == np.round(a)) \
+            and (a.size == 0 or np.abs(a).max() < 2.0 ** 53):
+        return a.astype(np.int64)
+    return None
+
+
 def _join_index(lk: pd.Series, rk: pd.Series):
     """Model row per test row (-1: none; NULL keys never match), or None when the model keys
-    are not unique or not comparable (the generic join decides then)."""
+    are not unique or not comparable (the generic join decides then).  Integer keys (the
+    feature / V(feature, field) keys of the linear, FM and FFM model tables) resolve through
+    the native open-addressing table (utils.collections.Int2LongOpenHashTable); NULL test keys
+    (NaN) are mapped to a key no model row holds."""
+    from ..utils.collections import Int2LongOpenHashTable
+
+    rki = _int_keys(rk)
+    if rki is not None and rki.size and not (rki == np.iinfo(np.int64).min).any():
+        lnull = lk.isna().to_numpy()
+        lki = _int_keys(lk.fillna(0)) if pd.api.types.is_numeric_dtype(lk) else None
+        if lki is not None:
+            tab = Int2LongOpenHashTable(rki.size)
+            if len(np.unique(rki)) != rki.size:
+                return None
+            tab.put_many(rki, np.arange(rki.size, dtype=np.int64))
+            tm = tab.get_many(lki, default=-1)
+            tm[lnull] = -1
+            return tm.astype(np.int32)
     keys = _key_arrays(lk, rk)
     if keys is None:
         return None

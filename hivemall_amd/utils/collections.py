@@ -125,9 +125,26 @@ class _OpenHashTable:
         return self.size
 
     def _probe(self, keys: np.ndarray, insert: bool) -> np.ndarray:
-        """Vectorised linear probing: every round resolves the keys whose slot holds them (or
-        is empty), the rest advance one slot.  Duplicate new keys in one batch are inserted
-        once (the first claims the slot, the others then find it)."""
+        """Slot of every key (-1: absent).  The native bulk probe (csrc/host/hashing.cpp
+        ``hm_oht_probe``: sequential inserts, OpenMP lookups) when the host library is loaded,
+        else vectorised numpy rounds: each resolves the keys whose slot holds them (or is
+        empty), the rest advance one slot."""
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        try:
+            from .. import _native
+            lib = _native.host()
+        except Exception:   # noqa: BLE001 - no host library: the numpy rounds below
+            lib = None
+        if lib is not None and keys.size:
+            out = np.empty(keys.size, dtype=np.int64)
+            self.size += int(lib.hm_oht_probe(self.keys.ctypes.data, self.keys.size, keys.ctypes.data,
+                                              keys.size, out.ctypes.data, int(insert)))
+            return out
+        return self._probe_np(keys, insert)
+
+    def _probe_np(self, keys: np.ndarray, insert: bool) -> np.ndarray:
+        """Duplicate new keys in one batch are inserted once (the first claimant claims the
+        slot, the others then find it)."""
         mask = self.keys.size - 1
         pos = (_mix64(keys) & np.uint64(mask)).astype(np.int64)
         out = np.full(keys.size, -1, dtype=np.int64)
@@ -191,8 +208,24 @@ class Int2FloatOpenHashTable(_OpenHashTable):
 
 class Int2LongOpenHashTable(_OpenHashTable):
     """Key -> int64 offset (upstream FFM model store: V(feature, field) key -> HeapBuffer
-    offset)."""
+    offset).  Resolves the SQL fused join-predict's integer keys to model rows
+    (sql/fused.py ``_join_index``)."""
     VALUE_DTYPE = np.int64
+
+    def get_many(self, keys, default=None) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        d = self.default_value if default is None else default
+        try:
+            from .. import _native
+            lib = _native.host()
+        except Exception:   # noqa: BLE001 - no host library: the generic path
+            lib = None
+        if lib is None or not keys.size:
+            return super().get_many(keys, default)
+        out = np.empty(keys.size, dtype=np.int64)
+        lib.hm_oht_get_i64(self.keys.ctypes.data, self.vals.ctypes.data, self.keys.size, keys.ctypes.data,
+                           keys.size, int(d), out.ctypes.data)
+        return out
 
 
 class Long2DoubleOpenHashTable(_OpenHashTable):
