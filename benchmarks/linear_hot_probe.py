@@ -39,10 +39,12 @@ def main():
                       "rows_per_s": round(N * EPOCHS / (time.perf_counter() - t0)),
                       "heldout_logloss": round(seq, 5)}), flush=True)
     tr, te = tr_c.to("cuda"), te_c.to("cuda")
-    grid = [(0, 512, 16), (0, 512, 16)] + [(1, W, ch) for W, ch in ((512, 64), (1024, 16), (1024, 32), (2048, 8), (2048, 16), (4096, 4), (4096, 8))]
-    for hot, W, ch in grid:
+    grid = [(0, 512, 16, 16, 4), (0, 512, 16, 16, 4)] + [(1, W, ch, mn, ev) for W, ch, mn, ev in ((1024, 16, 16, 4), (1024, 16, 16, 8), (1024, 16, 32, 8), (1024, 32, 32, 4), (1024, 32, 32, 8), (2048, 16, 16, 8), (2048, 16, 32, 16))]
+    for hot, W, ch, mn, ev in grid:
         os.environ["HM_LINEAR_HOT"] = str(hot)
         os.environ["HM_LINEAR_HOT_CH"] = str(ch)
+        os.environ["HM_LINEAR_HOT_MIN"] = str(mn)
+        os.environ["HM_LINEAR_HOT_EVERY"] = str(ev)
         m = L.TrainClassifier(opts + " -engine shared", device="cuda")
         m._ensure_state(tr)
         m.state = LO.new_shared_state(1 << BITS, "cuda", N, waves=W)
@@ -58,7 +60,7 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ll = heldout(m, te)
-        print(json.dumps({"hot": hot, "waves": W, "chunk_rows_per_wave": ch,
+        print(json.dumps({"hot": hot, "waves": W, "chunk_rows_per_wave": ch, "min_rows": mn, "every": ev,
                           "hot_features": 0 if hs is None else int(hs[1].numel()),
                           "hot_select_ms": round(1e3 * t_hot, 2), "rows_per_s": round(N * EPOCHS / dt),
                           "heldout_logloss": round(ll, 5), "delta_vs_seq": round(ll - seq, 5)}), flush=True)

@@ -347,6 +347,7 @@ __device__ __forceinline__ F4 ld4m(const float4* p) {
 // address drop by 4*CH x.  Cold features keep the Hogwild read-modify-write.
 constexpr int HM_HOT_MAX = 8192;          // <= 96 KB of LDS accumulators
 
+
 // Flush of up to 4 hot features per thread: all returning atomics are issued before any result
 // is used, so their round trips overlap instead of running back to back.
 constexpr int HM_HOT_U = 4;
@@ -354,7 +355,8 @@ constexpr int HM_HOT_U = 4;
 __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__ S, float (&gs)[HM_HOT_U],
                                            float (&g2)[HM_HOT_U], const float (&cnt)[HM_HOT_U],
                                            const int (&f)[HM_HOT_U], const StepK& k) {
-    float r1[HM_HOT_U], r2[HM_HOT_U];
+    // only non-returning atomics: they retire at L2 without the issuing wave waiting, so blocks
+    // that flush the same hot address at once no longer queue behind each other's round trips
     if (P.reg == R_L2) {
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u) {
@@ -365,30 +367,25 @@ __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__
         }
     }
     if (P.reg == R_RDA) {
-        // AdaGrad-RDA (optimizer_update O_ADAGRAD_RDA): w is a function of the running sums
-        // u = sum g and G = sum g^2 and of t, so the sums are added atomically and w rewritten
-        // from the totals this flush observed
+        // AdaGrad-RDA: only the running sums u = sum g, G = sum g^2 are stored; a hot
+        // feature's w is recomputed from them where it is read (rda_w) and once after the pass
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u) {
             if (f[u] < 0) continue;
-            r1[u] = atomicAdd(&S[f[u]].y, gs[u]);
-            r2[u] = atomicAdd(&S[f[u]].z, g2[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < HM_HOT_U; ++u) {
-            if (f[u] < 0) continue;
-            const float uu = r1[u] + gs[u], G = r2[u] + g2[u];
-            const float sign = uu > 0.f ? 1.f : -1.f;
-            const float mean = sign * uu / k.t - P.lambda;
-            S[f[u]].x = mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
+            atomicAdd(&S[f[u]].y, gs[u]);
+            atomicAdd(&S[f[u]].z, g2[u]);
         }
     } else if (P.opt == O_ADAGRAD) {
+        float G0[HM_HOT_U];
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u)
-            if (f[u] >= 0) r2[u] = atomicAdd(&S[f[u]].y, g2[u]);
+            G0[u] = f[u] >= 0 ? __builtin_nontemporal_load(&S[f[u]].y) : 0.f;
 #pragma unroll
-        for (int u = 0; u < HM_HOT_U; ++u)
-            if (f[u] >= 0) atomicAdd(&S[f[u]].x, -k.eta * gs[u] / (sqrtf(r2[u] + g2[u]) + P.eps));
+        for (int u = 0; u < HM_HOT_U; ++u) {
+            if (f[u] < 0) continue;
+            atomicAdd(&S[f[u]].y, g2[u]);
+            atomicAdd(&S[f[u]].x, -k.eta * gs[u] / (sqrtf(G0[u] + g2[u]) + P.eps));
+        }
     } else {
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u)
@@ -396,11 +393,27 @@ __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__
     }
 }
 
-// LDS accumulators, structure of arrays: sum g [H] | sum g^2 [H] | count [H] (count: L2 only)
-__device__ __forceinline__ void hot_add(float* acc, int H, bool cnt, int h, float g) {
+// AdaGrad-RDA weight from its sums at step t (optimizer_update O_ADAGRAD_RDA)
+__device__ __forceinline__ float rda_w(const Params& P, float u, float G, const StepK& k) {
+    if (G <= 0.f) return 0.f;
+    const float sign = u > 0.f ? 1.f : -1.f;
+    const float mean = sign * u / k.t - P.lambda;
+    return mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
+}
+
+// Block barrier over the LDS accumulators only: waits for this wave's LDS operations, not for
+// its outstanding global atomics (a __syncthreads fence would drain those too)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// LDS accumulators, structure of arrays: sum g [H] | sum g^2 [H] | rows [H]
+__device__ __forceinline__ void hot_add(float* acc, int H, int h, float g) {
     atomicAdd(acc + h, g);
     atomicAdd(acc + H + h, g * g);
-    if (cnt) atomicAdd(acc + 2 * H + h, 1.f);
+    atomicAdd(acc + 2 * H + h, 1.f);
 }
 
 template <bool RELOAD, bool NT, bool HOT>
@@ -409,9 +422,8 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
     const int32_t* __restrict__ order, float4* __restrict__ S0, uint8_t* __restrict__ touched0,
     float* __restrict__ RSW, double* __restrict__ loss_out, const int32_t* __restrict__ hot_slot,
-    const int32_t* __restrict__ hot_feat, int H, int CH) {
-    extern __shared__ float s_acc[];             // HOT: H x (2 or 3) floats, see hot_add
-    const bool hcnt = HOT && P.reg == R_L2;
+    const int32_t* __restrict__ hot_feat, int H, int CH, int min_rows, int every) {
+    extern __shared__ float s_acc[];             // HOT: 3 x H floats, see hot_add
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool active = g < W;
@@ -425,8 +437,8 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
 #pragma unroll
     for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = active ? RSW[(size_t)g * HM_REP_SCALARS + k] : 0.f;
     if constexpr (HOT) {
-        for (int h = threadIdx.x; h < (hcnt ? 3 : 2) * H; h += 256) s_acc[h] = 0.f;
-        __syncthreads();
+        for (int h = threadIdx.x; h < 3 * H; h += 256) s_acc[h] = 0.f;
+        lds_barrier();
     }
     double loss_acc = 0.0;
     const int ch = HOT ? CH : 1;
@@ -452,16 +464,18 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             }
             F4 cst = {0.f, 0.f, 0.f, 0.f};
             float p = 0.f, sq = 0.f;
+            const bool hrda = HOT && P.reg == R_RDA;
             if (ci >= 0) {
                 cst = ld4m<NT>(S + ci);
-                p = cst.w * cx;
+                p = (hrda && hs >= 0 ? rda_w(P, cst.s1, cst.s2, sk) : cst.w) * cx;
                 sq = cx * cx;
             }
             for (int64_t k = s + 64 + lane; k < e; k += 64) {      // rows wider than a wave
                 const int i = idx[k];
                 const float x = val ? val[k] : 1.f;
                 if (i < 0 || i >= dims) continue;
-                p += ld4m<NT>(S + i).w * x;
+                const F4 st = ld4m<NT>(S + i);
+                p += (hrda && hot_slot[i] >= 0 ? rda_w(P, st.s1, st.s2, sk) : st.w) * x;
                 sq += x * x;
             }
             p = hm::wave_sum(p);
@@ -472,7 +486,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                 touched[ci] = 1;
                 if (c.update) {
                     if (HOT && hs >= 0) {
-                        hot_add(s_acc, H, hcnt, hs, c.dloss * cx);
+                        hot_add(s_acc, H, hs, c.dloss * cx);
                     } else {
                         if (RELOAD) cst = ld4m<NT>(S + ci);
                         feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
@@ -489,7 +503,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                 if (HOT) {
                     const int h = hot_slot[i];
                     if (h >= 0) {
-                        hot_add(s_acc, H, hcnt, h, c.dloss * x);
+                        hot_add(s_acc, H, h, c.dloss * x);
                         continue;
                     }
                 }
@@ -500,9 +514,14 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
         }
         if constexpr (HOT) {
             // every wave of the block has finished its CH rows of this chunk
-            __syncthreads();
+            lds_barrier();
             const int64_t tend = t0 + min(n_rows, (ck + 1) * span);
             const StepK sk = step_consts(P, (float)tend);
+            // an entry is applied once it holds min_rows rows of this block (the hottest
+            // features: every chunk), else every `every` chunks — staggered over the blocks, so
+            // they do not all hit the same addresses in the same chunk — and at the end of the
+            // pass: the global atomics on hot addresses bound the kernel
+            const bool all = ((ck + blockIdx.x) % every) == every - 1 || ck == nchunks - 1;
             for (int h0 = threadIdx.x; h0 < H; h0 += 256 * HM_HOT_U) {
                 float gs[HM_HOT_U], g2[HM_HOT_U], cnt[HM_HOT_U];
                 int f[HM_HOT_U];
@@ -511,24 +530,37 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                     const int h = h0 + u * 256;
                     gs[u] = h < H ? s_acc[h] : 0.f;
                     g2[u] = h < H ? s_acc[H + h] : 0.f;
-                    cnt[u] = hcnt && h < H ? s_acc[2 * H + h] : 0.f;
+                    cnt[u] = h < H ? s_acc[2 * H + h] : 0.f;
                     // a hot feature whose rows all had a zero gradient needs no update either
-                    f[u] = g2[u] != 0.f ? hot_feat[h] : -1;
+                    f[u] = g2[u] != 0.f && (all || cnt[u] >= (float)min_rows) ? hot_feat[h] : -1;
                     if (f[u] >= 0) {
                         s_acc[h] = 0.f;
                         s_acc[H + h] = 0.f;
-                        if (hcnt) s_acc[2 * H + h] = 0.f;
+                        s_acc[2 * H + h] = 0.f;
                     }
                 }
                 hot_flush4(P, S, gs, g2, cnt, f, sk);
             }
-            __syncthreads();
+            lds_barrier();
         }
     }
     if (active && lane == 0) {
 #pragma unroll
         for (int k = 0; k < HM_REP_SCALARS; ++k) RSW[(size_t)g * HM_REP_SCALARS + k] = rs[k];
         loss_out[g] = loss_acc;
+    }
+}
+
+// After a HOT AdaGrad-RDA pass: the stored w of every hot feature from its sums at the pass's
+// last step (the value the next reader, prediction or export, must see).
+__global__ __launch_bounds__(256) void hot_rda_finalize_kernel(Params P, float4* __restrict__ S0, int dims, int R,
+                                                               const int32_t* __restrict__ hot_feat, int H,
+                                                               float t) {
+    const StepK k = step_consts(P, t);
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < (int64_t)H * R; q += (int64_t)gridDim.x * 256) {
+        const int r = (int)(q / H), h = (int)(q - (int64_t)r * H);
+        float4* s = S0 + (size_t)r * dims + hot_feat[h];
+        s->x = rda_w(P, s->y, s->z, k);
     }
 }
 
@@ -600,25 +632,30 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
                                   int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,
                                   float* RSW, double* loss_out, const int32_t* hot_slot, const int32_t* hot_feat,
-                                  int H, int CH, hipStream_t stream) {
+                                  int H, int CH, int min_rows, int every, hipStream_t stream) {
     if (n_rows <= 0) return 0;
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
     const bool hot = H > 0;
-    const size_t lds = hot ? (size_t)H * (P->reg == R_L2 ? 3 : 2) * sizeof(float) : 0;
-    if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 ||
+    const size_t lds = hot ? (size_t)H * 3 * sizeof(float) : 0;
+    if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 || min_rows <= 0 || every <= 0 ||
                 P->algo != A_GENERAL || (P->opt != O_SGD && P->opt != O_ADAGRAD) ||
                 (P->reg != R_NO && P->reg != R_L2 && !(P->reg == R_RDA && P->opt == O_ADAGRAD))))
         return (int)hipErrorInvalidValue;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \
                        dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
-                       RSW, loss_out, hot_slot, hot_feat, H, CH)
+                       RSW, loss_out, hot_slot, hot_feat, H, CH, min_rows, every)
     if (hot) {
         if (reload && nt) HM_SHARED_LAUNCH(true, true, true);
         else if (reload) HM_SHARED_LAUNCH(true, false, true);
         else if (nt) HM_SHARED_LAUNCH(false, true, true);
         else HM_SHARED_LAUNCH(false, false, true);
+        if (P->reg == R_RDA) {
+            const int64_t tot = (int64_t)H * R;
+            hipLaunchKernelGGL(hot_rda_finalize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *P,
+                               reinterpret_cast<float4*>(S), dims, R, hot_feat, H, (float)(t0 + n_rows));
+        }
     } else {
         if (reload && nt) HM_SHARED_LAUNCH(true, true, false);
         else if (reload) HM_SHARED_LAUNCH(true, false, false);

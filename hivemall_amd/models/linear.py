@@ -62,8 +62,9 @@ LEARNER_BASE_OPTS = [
     opt("shared_replicas", None, 1, int,
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
-    opt("shared_waves", None, 512, int,
-        "[engine] shared engine: rows in flight (more = faster, staler hot features)"),
+    opt("shared_waves", None, 0, int,
+        "[engine] shared engine: rows in flight (0 = auto: 1024 when the hot features are "
+        "pre-aggregated per block (SGD / AdaGrad / AdaGrad-RDA general learners), else 512)"),
 ] + CKPT_OPTS
 
 GENERAL_OPTS = [
@@ -340,7 +341,8 @@ class OnlineLinearLearner(Learner):
             try:
                 self.state = LO.new_shared_state(
                     dims, self.device, rows.n, replicas=int(self.cl["shared_replicas"]),
-                    waves=LO.shared_waves(rows.n, max(1, int(self.cl["shared_waves"]))))
+                    waves=LO.shared_waves(rows.n, int(self.cl["shared_waves"])
+                                          or (1024 if LO.hot_rule(self.P) else 512)))
             except ValueError as e:
                 raise UDFArgumentException(f"{self.NAME}: {e}") from None
             if self._warm is not None:

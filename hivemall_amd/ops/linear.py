@@ -171,7 +171,23 @@ def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, r
     return st
 
 
-HOT_MAX = 4096          # csrc/kernels/linear.hip HM_HOT_MAX (64 KB of LDS accumulators)
+HOT_MAX = 4096          # <= csrc/kernels/linear.hip HM_HOT_MAX; 48 KB of LDS accumulators
+# hot-feature flush schedule (csrc/kernels/linear.hip HOT): rows per wave per chunk, rows an
+# accumulator must hold to be applied before the periodic flush, chunks between periodic flushes
+# (profiles/linear_hot_r3/: 2 M Criteo-shaped rows, 2^24 dims, AdaGrad-RDA logistic)
+HOT_CHUNK, HOT_MIN_ROWS, HOT_EVERY = 32, 32, 8
+
+
+def hot_rule(P: LinParams) -> bool:
+    """Rules whose per-feature update is a function of the summed gradients, so the hot features
+    can be pre-aggregated (general learner: SGD, AdaGrad with no / L2 regularisation, and
+    AdaGrad-RDA).  ``HM_LINEAR_HOT=0`` disables the pre-aggregation."""
+    if os.environ.get("HM_LINEAR_HOT", "1") == "0":
+        return False
+    return (P.algo == ALGOS["general"] and P.opt in (OPTIMIZERS["sgd"], OPTIMIZERS["adagrad"])
+            and (P.reg in (REGS["no"], REGS["l2"])
+                 or (P.reg == REGS["rda"] and P.opt == OPTIMIZERS["adagrad"]))
+            and P.n_labels == 1)
 
 
 def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
@@ -181,12 +197,7 @@ def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     rules whose update is a function of the summed gradients (general learner, SGD / AdaGrad,
     no or L2 regularisation, AdaGrad-RDA).  Returns (hot_slot i32 [dims], hot_feat i32 [H]) or None.
     Cached per index tensor (epochs reuse it).  ``HM_LINEAR_HOT=0`` disables."""
-    if os.environ.get("HM_LINEAR_HOT", "1") == "0":
-        return None
-    if not (P.algo == ALGOS["general"] and P.opt in (OPTIMIZERS["sgd"], OPTIMIZERS["adagrad"])
-            and (P.reg in (REGS["no"], REGS["l2"])
-                 or (P.reg == REGS["rda"] and P.opt == OPTIMIZERS["adagrad"]))
-            and P.n_labels == 1):
+    if not hot_rule(P):
         return None
     key = (idx.data_ptr(), idx.numel(), st.dims, n_rows)
     hit = st.meta.get("hot")
@@ -230,12 +241,14 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     p = _native.ptr
     hot = hot_features(st, P, idx, n) if W > 1 else None
     hs, hf, H = (hot[0], hot[1], hot[1].numel()) if hot is not None else (None, None, 0)
-    ch = int(os.environ.get("HM_LINEAR_HOT_CH", "16"))
+    ch = int(os.environ.get("HM_LINEAR_HOT_CH", HOT_CHUNK))
+    hmin = int(os.environ.get("HM_LINEAR_HOT_MIN", HOT_MIN_ROWS))
+    hevery = int(os.environ.get("HM_LINEAR_HOT_EVERY", HOT_EVERY))
     rc = _native.hip().hm_linear_train_shared(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
                                               st.R, int(st.meta.get("reload", False)),
                                               int(st.meta.get("nt", True)),
                                               p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
-                                              p(st.touched), p(st.RS), p(loss), p(hs), p(hf), H, ch,
+                                              p(st.touched), p(st.RS), p(loss), p(hs), p(hf), H, ch, hmin, hevery,
                                               _native.stream_of(dev))
     _native.check(rc, "hm_linear_train_shared")
     return loss
@@ -320,7 +333,7 @@ _P = _native.c_p
 _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
-                                              C.c_int, C.c_int] + [_P] * 9 + [_P, _P, C.c_int, C.c_int]
+                                              C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 4
                      + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])

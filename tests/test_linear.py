@@ -232,19 +232,24 @@ def test_gpu_shared_engine_one_wave_is_sequential(name, opts, reload):
 
 
 @pytest.mark.gpu
-def test_gpu_shared_engine_hashed_2p24_logloss_parity():
+@pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6",
+                                  "-opt sgd -reg no -eta fixed -eta0 0.05"])
+def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
     """Hivemall's default -dims 2^24 (hashed Criteo-shaped rows, 39 nnz): auto picks the shared
-    table; Hogwild with 512 rows in flight lands within 0.03 held-out logloss of the sequential
-    CPU engine after one epoch (measured 0.02 at 2M rows: profiles/linear_shared_r2o_nt.log)."""
+    table, 1,024 rows in flight, with the hot features' gradients summed per block in LDS and
+    applied by atomics (csrc/kernels/linear.hip HOT), so no hot update is lost.  Held-out logloss
+    after one epoch within 5e-3 of the sequential CPU engine (plain Hogwild: 0.018 at 2 M rows;
+    pre-aggregated: -7e-4, profiles/linear_hot_r3/)."""
     rows = _criteo_rows(200000, 24, seed=5)
     test = _criteo_rows(50000, 24, seed=99)
     yy = (test.y > 0).float()
     res = {}
     for dev in ("cpu", "cuda"):
-        m = L.TrainClassifier("-loss logloss -opt adagrad -dims 16777216", device=dev)
+        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216", device=dev)
         m.fit(rows=rows.to(dev))
         if dev == "cuda":
-            assert m.state.meta.get("shared") and m.state.RS.shape[0] == 512
+            assert m.state.meta.get("shared") and m.state.RS.shape[0] == 1024
+            assert m.state.meta["hot"][1] is not None and m.state.meta["hot"][1][1].numel() > 100
         s = m.decision_function(rows=test.to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
-    assert abs(res["cpu"] - res["cuda"]) < 0.03, res
+    assert abs(res["cpu"] - res["cuda"]) < 5e-3, res
