@@ -342,8 +342,9 @@ __device__ __forceinline__ F4 ld4m(const float4* p) {
 // HOT: the hottest features (hot_slot[i] >= 0, at most HM_HOT_MAX, chosen by the host from the
 // pass's feature counts) are not read-modify-written per row: each block sums their gradients
 // (sum g, sum g^2, count) in LDS over a chunk of CH rows per wave, then applies them with one
-// returning float atomic on G and one on w per touched hot feature (AdaGrad / SGD of the general
-// learner, no or L2 regularisation; AdaGrad-RDA: atomics on its two sums, w recomputed).  No update of a hot feature is lost, and the atomics on its
+// float atomic on G and one on w per touched hot feature (AdaGrad of the general learner, no or L2
+// regularisation; AdaGrad-RDA: atomics on its two sums, w recomputed).  Plain SGD would apply
+// a block's summed gradient at full rate and diverge, so it stays Hogwild.  No update of a hot feature is lost, and the atomics on its
 // address drop by 4*CH x.  Cold features keep the Hogwild read-modify-write.
 constexpr int HM_HOT_MAX = 8192;          // <= 96 KB of LDS accumulators
 
@@ -386,10 +387,6 @@ __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__
             atomicAdd(&S[f[u]].y, g2[u]);
             atomicAdd(&S[f[u]].x, -k.eta * gs[u] / (sqrtf(G0[u] + g2[u]) + P.eps));
         }
-    } else {
-#pragma unroll
-        for (int u = 0; u < HM_HOT_U; ++u)
-            if (f[u] >= 0) atomicAdd(&S[f[u]].x, -k.eta * gs[u]);
     }
 }
 
@@ -639,8 +636,8 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
     const bool hot = H > 0;
     const size_t lds = hot ? (size_t)H * 3 * sizeof(float) : 0;
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 || min_rows <= 0 || every <= 0 ||
-                P->algo != A_GENERAL || (P->opt != O_SGD && P->opt != O_ADAGRAD) ||
-                (P->reg != R_NO && P->reg != R_L2 && !(P->reg == R_RDA && P->opt == O_ADAGRAD))))
+                P->algo != A_GENERAL || P->opt != O_ADAGRAD ||
+                (P->reg != R_NO && P->reg != R_L2 && P->reg != R_RDA)))
         return (int)hipErrorInvalidValue;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \

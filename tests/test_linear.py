@@ -232,8 +232,7 @@ def test_gpu_shared_engine_one_wave_is_sequential(name, opts, reload):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6",
-                                  "-opt sgd -reg no -eta fixed -eta0 0.05"])
+@pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6"])
 def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
     """Hivemall's default -dims 2^24 (hashed Criteo-shaped rows, 39 nnz): auto picks the shared
     table, 1,024 rows in flight, with the hot features' gradients summed per block in LDS and
