@@ -8,7 +8,7 @@ export HM_NO_AUTOBUILD=1
 STEPS="${STEPS:-tests smoke bench prof configs}"
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 600 python -m pytest tests -m gpu -x -q 2>&1 | tee gpurun_out/pytest_gpu.log ;;
+    tests) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread 2>&1 | tee gpurun_out/pytest_gpu.log ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log ;;
     bench) timeout -k 10 300 python bench.py ${BENCH_ARGS:-} 2>&1 | tee gpurun_out/bench.log ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
