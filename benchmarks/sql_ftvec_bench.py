@@ -6,7 +6,7 @@ Times the feature-engineering expressions alone (SELECT add_bias(feature_hashing
 and the whole training statement, on an Arrow-backed table (list<string> column, as a Parquet
 or Arrow source arrives) and on a table of Python lists.
 
-    python benchmarks/sql_ftvec_bench.py [rows] [device]
+    python benchmarks/sql_ftvec_bench.py [rows] [device] [arrow|lists|both]
 """
 import json
 import os
@@ -36,7 +36,8 @@ def main():
     from hivemall_amd.sql import Session
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     dev = sys.argv[2] if len(sys.argv) > 2 else "cpu"
-    for arrow in (True, False):
+    which = sys.argv[3] if len(sys.argv) > 3 else "both"
+    for arrow in {"arrow": (True,), "lists": (False,)}.get(which, (True, False)):
         t = time.perf_counter()
         df = table(n, arrow)
         gen = time.perf_counter() - t

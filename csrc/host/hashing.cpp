@@ -67,6 +67,36 @@ bool parse_int(const char* p, int n, int64_t* out) {
 
 bool parse_float(const char* p, int n, float* out) {
     if (n <= 0 || n > 63) return false;
+    {
+        // exact fast path: [+-]digits[.digits] with <= 15 significant digits is m / 10^f with
+        // m < 2^53 and f <= 15, both exact in double, so the one IEEE division is the correctly
+        // rounded value strtod returns; anything else (exponents, inf/nan, spaces) -> strtod
+        static const double P10[16] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10,
+                                       1e11, 1e12, 1e13, 1e14, 1e15};
+        int i = 0;
+        bool neg = false;
+        if (p[0] == '-' || p[0] == '+') { neg = p[0] == '-'; i = 1; }
+        uint64_t m = 0;
+        int nd = 0, fd = -1;
+        bool ok = i < n;
+        for (; i < n && ok; ++i) {
+            const char c = p[i];
+            if (c >= '0' && c <= '9') {
+                m = m * 10 + (uint64_t)(c - '0');
+                ++nd;
+                if (fd >= 0) ++fd;
+            } else if (c == '.' && fd < 0) {
+                fd = 0;
+            } else {
+                ok = false;
+            }
+        }
+        if (ok && nd > 0 && nd <= 15) {
+            const double d = fd > 0 ? (double)m / P10[fd] : (double)m;
+            *out = (float)(neg ? -d : d);
+            return true;
+        }
+    }
     char tmp[64];
     std::memcpy(tmp, p, n);
     tmp[n] = 0;
@@ -130,40 +160,75 @@ inline int fmt_i32(int32_t v, char* o) {
     return k;
 }
 
+// name length of a feature string (before the last of at most two ':'), -1 in *has_val when
+// there is no value part
+inline int feature_name_len(const uint8_t* p, int L, bool* has_val) {
+    const void* a = std::memchr(p, ':', (size_t)L);
+    if (!a) { *has_val = false; return L; }
+    *has_val = true;
+    const int c1 = (int)((const uint8_t*)a - p);
+    const void* b = std::memchr(p + c1 + 1, ':', (size_t)(L - c1 - 1));
+    return b ? (int)((const uint8_t*)b - p) : c1;
+}
+
+inline int dec_digits(uint32_t u) {
+    int d = 1;
+    while (u >= 10) { u /= 10; ++d; }
+    return d;
+}
+
+// Exclusive prefix sum in place over out[1..n] (out[0] = 0 on return), parallel in blocks.
+void prefix_sum_inplace(int64_t* out, int64_t n) {
+    out[0] = 0;
+    if (n < (1 << 20)) {
+        for (int64_t i = 0; i < n; ++i) out[i + 1] += out[i];
+        return;
+    }
+    constexpr int NB = 64;
+    int64_t part[NB + 1] = {0};
+#pragma omp parallel for schedule(static)
+    for (int b = 0; b < NB; ++b) {
+        const int64_t s = n * b / NB + 1, e = n * (b + 1) / NB + 1;
+        int64_t acc = 0;
+        for (int64_t i = s; i < e; ++i) { acc += out[i]; out[i] = acc; }
+        part[b + 1] = acc;
+    }
+    for (int b = 0; b < NB; ++b) part[b + 1] += part[b];
+#pragma omp parallel for schedule(static)
+    for (int b = 1; b < NB; ++b) {
+        const int64_t s = n * b / NB + 1, e = n * (b + 1) / NB + 1;
+        for (int64_t i = s; i < e; ++i) out[i] += part[b];
+    }
+}
+
 HM_API int64_t hm_feature_hash_strs(const uint8_t* buf, const int64_t* off, int64_t n,
                                     int32_t num_features, uint32_t seed, uint8_t* out,
                                     int64_t* out_off) {
-    std::vector<int32_t> h(n);
-    std::vector<int32_t> namelen(n);
-    std::vector<int64_t> len(n + 1);
+    // pass 1: output length of each string into out_off[i + 1]; pass 2 re-hashes and writes.
+    // Hashing a ~10-B name twice is cheaper than first-touching three n-sized temporaries
+    // (the page faults of those cost more than the whole parallel pass).
 #pragma omp parallel for schedule(static) if (n > 65536)
     for (int64_t i = 0; i < n; ++i) {
         const uint8_t* p = buf + off[i];
         const int L = (int)(off[i + 1] - off[i]);
-        int c1 = -1, c2 = -1;
-        for (int k = 0; k < L; ++k)
-            if (p[k] == ':') {
-                if (c1 < 0) c1 = k;
-                else { c2 = k; break; }
-            }
-        const int nl = c2 >= 0 ? c2 : (c1 >= 0 ? c1 : L);
-        namelen[i] = c1 >= 0 ? nl : -1;                      // -1: no value part
-        h[i] = mhash_reduce(murmur3_x86_32(p, nl, seed), num_features);
-        char tmp[16];
-        const int hd = fmt_i32(h[i], tmp);
-        len[i] = hd + (c1 >= 0 ? 1 + (L - nl - 1) : 0);
+        bool hv;
+        const int nl = feature_name_len(p, L, &hv);
+        const int32_t h = mhash_reduce(murmur3_x86_32(p, nl, seed), num_features);   // >= 1
+        out_off[i + 1] = dec_digits((uint32_t)h) + (hv ? L - nl : 0);
     }
-    out_off[0] = 0;
-    for (int64_t i = 0; i < n; ++i) out_off[i + 1] = out_off[i] + len[i];
+    prefix_sum_inplace(out_off, n);
 #pragma omp parallel for schedule(static) if (n > 65536)
     for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* p = buf + off[i];
+        const int L = (int)(off[i + 1] - off[i]);
+        bool hv;
+        const int nl = feature_name_len(p, L, &hv);
         uint8_t* o = out + out_off[i];
-        const int hd = fmt_i32(h[i], reinterpret_cast<char*>(o));
-        if (namelen[i] >= 0) {
+        const int hd = fmt_i32(mhash_reduce(murmur3_x86_32(p, nl, seed), num_features),
+                               reinterpret_cast<char*>(o));
+        if (hv) {
             o[hd] = ':';
-            const int nl = namelen[i];
-            const int L = (int)(off[i + 1] - off[i]);
-            std::memcpy(o + hd + 1, buf + off[i] + nl + 1, L - nl - 1);
+            std::memcpy(o + hd + 1, p + nl + 1, L - nl - 1);
         }
     }
     return out_off[n];
@@ -230,6 +295,33 @@ HM_API int64_t hm_parse_features(const uint8_t* buf, const int64_t* off, int64_t
                                  void* dict, int add_new, int32_t num_features, uint32_t seed,
                                  int64_t int_base, int64_t* idx_out, float* val_out) {
     Dict* D = static_cast<Dict*>(dict);
+    if (mode == 0 || mode == 2) {
+        // no dictionary: every feature parses on its own -> parallel; the first malformed
+        // feature (lowest index) is reported as in the sequential loop
+        int64_t bad = n;
+#pragma omp parallel for schedule(static) reduction(min : bad) if (n > 65536)
+        for (int64_t i = 0; i < n; ++i) {
+            const char* s = (const char*)buf + off[i];
+            const int len = (int)(off[i + 1] - off[i]);
+            const char* colon = (const char*)std::memchr(s, ':', (size_t)len);
+            int nlen = len;
+            float v = 1.f;
+            if (colon) {
+                nlen = (int)(colon - s);
+                if (!parse_float(colon + 1, len - nlen - 1, &v)) { bad = i < bad ? i : bad; continue; }
+            }
+            if (nlen <= 0) { bad = i < bad ? i : bad; continue; }
+            int64_t id;
+            if (mode == 0) {
+                if (!parse_int(s, nlen, &id)) { bad = i < bad ? i : bad; continue; }
+            } else {
+                id = mhash_reduce(murmur3_x86_32((const uint8_t*)s, nlen, seed), num_features);
+            }
+            idx_out[i] = id;
+            val_out[i] = v;
+        }
+        return bad < n ? bad : -1;
+    }
     for (int64_t i = 0; i < n; ++i) {
         const char* s = (const char*)buf + off[i];
         const int len = (int)(off[i + 1] - off[i]);

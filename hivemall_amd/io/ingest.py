@@ -103,9 +103,10 @@ def arrow_buffers(arr):
     array, rebased to start at 0 (slices honoured, zero-copy views where possible)."""
     import pyarrow as pa
 
-    lo = np.asarray(arr.offsets, dtype=np.int64)
+    lo = np.array(arr.offsets, dtype=np.int64)
     vals = arr.values.slice(int(lo[0]), int(lo[-1] - lo[0]))
-    lo = lo - lo[0]
+    if lo[0]:
+        lo -= lo[0]
     bufs = vals.buffers()
     odt = np.int64 if pa.types.is_large_string(vals.type) else np.int32
     so = np.frombuffer(bufs[1], dtype=odt)[vals.offset:vals.offset + len(vals) + 1].astype(np.int64) \
@@ -113,7 +114,8 @@ def arrow_buffers(arr):
     buf = bufs[2]
     data = np.frombuffer(buf, dtype=np.uint8) if buf is not None else np.zeros(0, np.uint8)
     data = data[int(so[0]):int(so[-1])] if len(so) else data[:0]
-    so = so - (so[0] if len(so) else 0)
+    if len(so) and so[0]:
+        so -= so[0]        # so is already a fresh int64 copy
     return data, so, lo
 
 

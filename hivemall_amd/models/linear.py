@@ -111,8 +111,12 @@ class SparseRows:
 
     @staticmethod
     def from_csr(csr: CSR, y=None, device="cpu") -> "SparseRows":
-        val = None if csr.nnz and np.all(csr.val == 1.0) else torch.from_numpy(csr.val.astype(np.float32))
-        idx = np.where((csr.idx >= 0) & (csr.idx < 2 ** 31 - 1), csr.idx, -1).astype(np.int32)
+        v = np.asarray(csr.val, dtype=np.float32)
+        val = None if csr.nnz and v.min() == 1.0 == v.max() else torch.from_numpy(v.copy())
+        idx = np.asarray(csr.idx)
+        if idx.size and (idx.min() < 0 or idx.max() >= 2 ** 31 - 1):
+            idx = np.where((idx >= 0) & (idx < 2 ** 31 - 1), idx, -1)
+        idx = idx.astype(np.int32)
         yy = None if y is None else torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32))
         return SparseRows(torch.from_numpy(csr.indptr.astype(np.int64)), torch.from_numpy(idx),
                           val, yy).to(device)
@@ -422,8 +426,8 @@ class OnlineLinearLearner(Learner):
         if self.encoder is not None and self.encoder.mode == "dict":
             return self.encoder.decode(ids)
         if self.encoder is not None and getattr(self.encoder, "string_names", False):
-            return [str(int(i)) for i in ids]
-        return [int(i) for i in ids]
+            return list(map(str, ids.tolist()))
+        return ids.tolist()
 
     def model_table(self) -> pd.DataFrame:
         w, cov = self.weights()
