@@ -50,8 +50,7 @@ struct FFMParams {
     int gstride;           // per-slot G: floats between consecutive features of G
     int vpad;              // per-slot G block layout: V slots per feature block (0: separate tables)
     int tail16;            // per-slot G block layout: zero 16-B chunks after each G region
-    int gfstride;          // per-slot G: floats between consecutive fields (1, or 4 in 16-B slots)
-    int sg_threads;        // ffm_sg_kernel block size 256 / 512; 0 = fp32 V: ffm_pipe_sg32_kernel
+    int gfstride;          // per-slot G: floats between consecutive fields (1, or 3 in 12-B slots)
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
                            // table pads each feature block to whole 128-B lines)
@@ -656,18 +655,14 @@ __device__ __forceinline__ void bar_raw() {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* glb_ptr_t;
 
-// SG (bf16 only): per-slot AdaGrad in 16-B slots {V bf16 x 4 | G fp32 | 0}: the per-slot
-// accumulator in fp32 at the byte size and access pattern of the per-element bf16 slots (one
-// 16-B DMA and one 16-B store per slot; the block layout of ffm_sg_kernel needs an 8-B and a
-// 4-B access per slot, measured 79.5 M rows/s against this layout's rate).
-template <int NS, bool BF = true, bool SG = false>
+
+template <int NS, bool BF = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2))) void ffm_pipe_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ VG,
     float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
-    static_assert(BF || !SG, "per-slot 16-B slots hold bf16 V");
     constexpr uint32_t SLOT_B = BF ? 16u : 32u;                        // bytes per packed slot
     using Img = typename std::conditional<BF, uint2, float4>::type;   // V in the transposed image
     __shared__ __attribute__((aligned(16))) uint4 s_raw[NS * 256 * (BF ? 1 : 2)];   // slot DMA landing zone
@@ -886,20 +881,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
                 const f2 lamj = {lj, lj};
                 const f2 d0 = coef * p0 + lamj * o0, d1 = coef * p1 + lamj * o1;
-                if constexpr (SG) {
-                    // one fp32 accumulator per slot (word 2): G += sum of the 4 squared gradients
-                    const float gs = (((__uint_as_float(q[j].z) + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
-                    const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
-                    const f2 rr = {r, r};
-                    o0 = o0 + rr * d0;
-                    o1 = o1 + rr * d1;
-                    const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
-                    const uint4 st = make_uint4(pack_sr_hi(o0, h, rotl32(h, 16)),
-                                                pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
-                                                __float_as_uint(gs), 0u);
-                    if (wr >> j & 1u) *reinterpret_cast<uint4*>(vg + off[j]) = st;
-                    continue;
-                }
                 g0 = g0 + d0 * d0;
                 g1 = g1 + d1 * d1;
                 const f2 t0 = g0 + eps, t1 = g1 + eps;
@@ -957,12 +938,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 }
 
 // ---------------------------------------------------------------------------------------------
-// LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout of
-// ffm_sg_kernel ([V: FS x 16 B | G: FS x fp32 | zero tail] per feature, 896 B): the schedule of
+// LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout
+// ([V: FS x 16 B | G: FS x fp32 | zero tail] per feature, 896 B): the schedule of
 // ffm_pipe_kernel (A..F above) with two DMAs per slot (V 16 B, G 4 B) into separate landing
-// zones.  The register-prefetch ffm_sg_kernel reached 66-68 M rows/s (70 % of this layout's
-// access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log); here no VGPR holds the
-// next row and the LDS image is the only staging (55 KB per block -> 2 blocks/CU).
+// zones.  A register-prefetch variant of this layout reached 66-68 M rows/s (70 % of the
+// access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
+// removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
+// block -> 2 blocks/CU).
 template <int NS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1404,286 +1386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Per-slot-AdaGrad pipelined kernel (the GPU default; K <= 4, F <= 45): one fp32 accumulator per
-// (feature, field) slot, as Hivemall's AdaGradEntry keeps one sum of squared gradients per FFM
-// entry, shared by the k factors (docs/compat.md "FFM AdaGrad").  V is fp32
-// (Hivemall's precision) or bf16 with stochastic rounding (VBF).
-//
-// Table (ops/ffm.py slot_block_layout): per feature one line-padded block
-//   [ V: FS slots x VSB bytes | G: FS x fp32 | zero tail ]     fp32 V: 640 + 160 (+96) = 896 B
-//                                                              bf16 V: 320 + 160 (+32) = 512 B
-// so a row moves 39 blocks: 35 KB read + 35 KB written with fp32 V (the per-element fp32 V|G
-// layout moves 50 + 50 KB), 20 + 20 KB with bf16 V (per-element bf16: 25 + 25 KB).  The FFM row
-// loop is bound by this scattered gather + write-back (profiles/ffm_r2/roofline_probe_e.log), so
-// bytes per row set the rate.
-//
-// Pipeline: the next row's V and G are loaded into REGISTERS (5 VGPRs per fp32 slot, 3 per bf16
-// slot) right after the current row's image is published, so their latency hides behind the
-// current row's forward pass and update; no LDS landing zone is needed, only the transposed V
-// image of the current row (partner reads) and two metadata buffers:
-//   top  cur V/G := the prefetched registers (the waitcnt lands here); own V -> T[b*F + a];
-//        publish meta(r+G) (held in registers since the previous iteration) and its L2 scale;
-//        barrier
-//   C    prefetch V/G of r+G (offsets from meta(r+G)); load the raw meta of r+2G (registers)
-//   D    forward(r) from registers + T, block sum (barrier)
-//   E    AdaGrad(V) with the slot accumulator, FTRL(w); stores; then the linear state of r+G
-//        is loaded (after E's FTRL stores: a feature shared by consecutive rows of the block is
-//        updated in sequence, same lane, same address); barrier (T reuse)
-// TH threads per block (256 or 512): with 512 a thread owns half the slots, so the prefetch
-// registers halve and 8 waves/SIMD fit; the block is the same one row (same LDS image), so a
-// CU holds more rows in flight at the same LDS per row.
-template <int NS, bool VBF, int TH = 256>
-__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(TH == 512 ? 6 : 4))) void ffm_sg_kernel(
-    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
-    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
-    float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
-    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
-{
-    constexpr uint32_t VSB = VBF ? 8u : 16u;                          // V bytes per slot
-    // native ext_vector types: HIP's float4 struct kept the prefetch array in scratch memory
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-    using Img = typename std::conditional<VBF, u2v, f4v>::type;
-    __shared__ __attribute__((aligned(16))) Img s_t[NS * TH];       // transposed V image
-    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];         // meta {i, f, x} of 2 rows
-    constexpr int NW = TH / 64;
-    __shared__ float s_red[NW + 2];                                  // [0..NW) sums, [NW+b] scale
-    const int F = P.F;
-    const int FF = F * F;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    constexpr int W_META = 1, W_LIN = 2;
-    const uint32_t vfs = (uint32_t)P.fstride * VSB;                  // V bytes between features
-    const uint32_t gfs = (uint32_t)P.gstride * 4u;                   // G bytes between features
-    const int G = gridDim.x;
-    char* vb = reinterpret_cast<char*>(Vt);
-    char* gb = reinterpret_cast<char*>(Gt);
-
-    int ab[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        const int s = tid + j * TH;
-        ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
-    }
-#define SA(j) (ab[j] & 0xFF)
-#define SB(j) (ab[j] >> 8)
-    const uint32_t tid_h = (uint32_t)tid * 0x9E3779B1u;
-
-    // raw meta of one row -> registers (wave W_META, lanes < F)
-    int rmi = -1, rmf = 0;
-    float rmx = 0.f;
-    auto load_meta = [&](int row) {
-        if (wave == W_META && lane < F && row < P.B) {
-            const size_t o = (size_t)row * F + lane;
-            rmi = idx[o];
-            rmf = fld ? fld[o] : lane;
-            rmx = val ? val[o] : 1.f;
-        }
-    };
-    // validated meta -> s_m[bf] + the row's L2-norm scale (wave W_META)
-    auto publish_meta = [&](int bf) {
-        if (wave == W_META) {
-            float sq = 0.f;
-            if (lane < F) {
-                int i = rmi, f = rmf;
-                float x = rmx;
-                if (i < 0 || i >= P.num_features || f < 0 || f >= P.num_fields) { i = -1; x = 0.f; f = 0; }
-                s_m[bf][lane] = make_int4(i, f, __float_as_int(x), 0);
-                sq = x * x;
-            }
-            const float tot = hm::wave_sum_uniform(sq);
-            if (lane == 0) s_red[NW + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
-        }
-    };
-    // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal
-    // (written back unchanged: whole lines), 0 = dead
-    auto slot = [&](int bf, int j, uint32_t& ov, uint32_t& og, float& xab) -> uint32_t {
-        const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
-        const bool ok = (ma.x | mb.x) >= 0 && tid + j * TH < FF;
-        const bool live = ok && SA(j) != SB(j);
-        const uint32_t i = ok ? (uint32_t)ma.x : 0u, f = ok ? (uint32_t)mb.y : 0u;
-        ov = i * vfs + f * VSB;
-        og = i * gfs + f * 4u;
-        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
-        return live ? 1u : (ok ? 2u : 0u);
-    };
-    // the prefetch registers (a macro, not a lambda: an array captured by reference stayed in
-    // scratch memory for the float4 case)
-    Img nv[NS];
-    float ng[NS];
-#define SG_PREFETCH(bf)                                                  \
-    _Pragma("unroll") for (int j = 0; j < NS; ++j) {                     \
-        uint32_t ov_, og_;                                               \
-        float xab_;                                                      \
-        slot(bf, j, ov_, og_, xab_);                                     \
-        nv[j] = *reinterpret_cast<const Img*>(vb + ov_);                 \
-        ng[j] = *reinterpret_cast<const float*>(gb + og_);               \
-    }
-    // linear state (w, z, n) of this lane's feature in the row of s_m[bf] (wave W_LIN)
-    float lw = 0.f, lz = 0.f, ln = 0.f;
-    auto load_lin = [&](int bf) {
-        if (P.use_linear && wave == W_LIN && lane < F) {
-            const int i = s_m[bf][lane].x;
-            if (i >= 0) {
-                lw = w[i];
-                if (P.train) { lz = wz[i]; ln = wn[i]; }
-            } else {
-                lw = lz = ln = 0.f;
-            }
-        }
-    };
-
-    int row = blockIdx.x;
-    if (row >= P.B) return;
-    // ---- prologue: meta(row) -> s_m[0]; prefetch its slots and linear state; meta(row + G) ----
-    load_meta(row);
-    publish_meta(0);
-    bar_raw();
-    SG_PREFETCH(0);
-    load_lin(0);
-    load_meta(row + G);
-
-    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
-        const int nxt = cur ^ 1;
-        const bool more = row + G < P.B;
-        // ---- top: the prefetched slots become the current row's; own V -> transposed image
-        //      (the forward and the update read it back from there: no registers held for V
-        //      across the row, so the next row's prefetch fits beside it at higher occupancy) ----
-        float cg[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            // slots past F*F decode to (0, 0): they must not overwrite that diagonal slot's V,
-            // which is read back from the image (its update writes it to memory)
-            if (tid + j * TH < FF) s_t[SB(j) * F + SA(j)] = nv[j];
-            cg[j] = ng[j];
-        }
-        if (more) publish_meta(nxt);
-        bar_raw();
-        // ---- C: prefetch the next row; raw meta of the row after it ----
-        if (more) {
-            SG_PREFETCH(nxt);
-            load_meta(row + 2 * G);
-        }
-        const float scale = s_red[NW + cur];
-        int mi = -1;
-        float mx = 0.f;
-        if (wave == W_LIN && lane < F) {
-            const int4 m = s_m[cur][lane];
-            mi = m.x;
-            mx = __int_as_float(m.z);
-        }
-        // ---- D: forward ----
-        uint32_t live = 0u, wr = 0u;
-        float xab[NS];
-        float part = 0.f;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            uint32_t ov, og;
-            const uint32_t k = slot(cur, j, ov, og, xab[j]);
-            live |= (k & 1u) << j;
-            wr |= (uint32_t)(k != 0u) << j;
-            const int s = tid + j * TH;
-            const Img pv = s_t[s < FF ? s : 0];
-            const Img cv = s_t[SB(j) * F + SA(j)];
-            float d;
-            if constexpr (VBF) d = dot2_bf16(cv.x, pv.x, dot2_bf16(cv.y, pv.y, 0.f));
-            else d = cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w;
-            part += d * xab[j];
-        }
-        part *= 0.5f * scale * scale;
-        part += lw * mx * scale;
-        part = hm::wave_sum_uniform(part);
-        if (lane == 0) s_red[wave] = part;
-        bar_raw();
-        float p = 0.f;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) p += s_red[k];
-        if (P.use_bias) p += bias_w0(P, bias);
-        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
-
-        // ---- E: updates ----
-        if (P.train) {
-            const float ks = kappa * scale * scale;
-            uint32_t hrow = (P.seed ^ ((uint32_t)row * 0x85EBCA77u)) + tid_h;
-            hrow ^= hrow >> 16;
-            hrow *= 0x7FEB352Du;
-            hrow ^= hrow >> 15;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                if (!(wr >> j & 1u)) continue;
-                uint32_t ov, og;
-                float xj;
-                slot(cur, j, ov, og, xj);
-                const int s = tid + j * TH;
-                const Img pv = s_t[s];
-                const Img cv = s_t[SB(j) * F + SA(j)];
-                const float c = ks * xab[j];
-                // diagonal slots: c = 0 and lambda = 0 -> zero gradient, V and G unchanged (the
-                // stochastic rounding of a value already in bf16 is exact)
-                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;
-                f2 o0, o1, p0, p1;
-                if constexpr (VBF) {
-                    o0 = bf2_to_f2(cv.x); o1 = bf2_to_f2(cv.y);
-                    p0 = bf2_to_f2(pv.x); p1 = bf2_to_f2(pv.y);
-                } else {
-                    o0 = f2{cv.x, cv.y}; o1 = f2{cv.z, cv.w};
-                    p0 = f2{pv.x, pv.y}; p1 = f2{pv.z, pv.w};
-                }
-                const f2 cc = {c, c}, ll = {lj, lj};
-                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
-                // G += g0^2 + g1^2 + g2^2 + g3^2 (factor order, as the CPU engine)
-                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
-                const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
-                const f2 rr = {r, r};
-                o0 = o0 + rr * d0;
-                o1 = o1 + rr * d1;
-                if constexpr (VBF) {
-                    const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
-                    *reinterpret_cast<u2v*>(vb + ov) = u2v{pack_sr_hi(o0, h, rotl32(h, 16)),
-                                                          pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24))};
-                } else {
-                    *reinterpret_cast<f4v*>(vb + ov) = f4v{o0.x, o0.y, o1.x, o1.y};
-                }
-                *reinterpret_cast<float*>(gb + og) = gs;
-            }
-            // the row's features' pad slots and block tails (never read): zeros, completing their
-            // lines; spread over all threads (one wave doing them was the last at the barrier)
-            {
-                const int npad = P.vpad - P.num_fields;
-                const int per = 2 * npad + P.tail16;
-                for (int q = tid; q < F * per; q += TH) {
-                    const int a = q / per, kk = q - a * per;
-                    const int i = s_m[cur][a].x;
-                    if (i < 0) continue;
-                    char* vblk = vb + (uint32_t)i * vfs;
-                    char* gblk = gb + (uint32_t)i * gfs;
-                    if (kk < npad) *reinterpret_cast<Img*>(vblk + (P.num_fields + kk) * VSB) = Img{};
-                    else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
-                    else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
-                }
-            }
-            if (mi >= 0) {
-                if (P.use_linear) {   // FTRL-proximal on the prefetched (w, z, n)
-                    const float g = kappa * mx * scale;
-                    const float n1 = ln + g * g;
-                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[mi] = z1;
-                    wn[mi] = n1;
-                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
-                }
-            }
-            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
-        }
-        // linear state of the next row, after this row's FTRL stores (same lane, same field)
-        if (more) load_lin(nxt);
-        bar_raw();   // T and s_m[cur] are rewritten by the next iterations
-    }
-#undef SA
-#undef SG_PREFETCH
-#undef SB
-}
-
-
+// 8,192 blocks (8 per CU, 4 resident at a time) unless the batch is smaller or a grid is given
 int default_blocks(int B, int grid) {
     return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
 }
@@ -1746,68 +1449,25 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
-// Per-slot-G in 16-B bf16 slots {V | G | 0} (Kp == 4, F <= 45, table < 4 GiB); -1 otherwise.
-int dispatch_sg16(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-                  const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
+// Per-slot-G fp32 pipelined dispatch (Kp == 4, F <= 45, block layout, tables < 4 GiB): the
+// LDS-DMA ffm_pipe_sg32_kernel; -1 otherwise (bf16 V in this layout: the generic kernel; the
+// bf16 default is the 12-B slot layout of dispatch_sg12).
+int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
+                  const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
                   float* pred, float* loss, int grid, hipStream_t stream) {
-    if (P.Kp != 4 || P.F > 45) return -1;
-    if ((size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32)) return -1;
-    const int need = (P.F * P.F + 255) / 256;
-    const int blocks = default_blocks(P.B, grid);
-    if (blocks <= 0) return 0;
-#define HM_PIPE(NSV) hipLaunchKernelGGL((ffm_pipe_kernel<NSV, true, true>), dim3(blocks), dim3(256), 0, stream, P, \
-                                        idx, fld, val, y, VG, w, wz, wn, bias, pred, loss)
-    if (need <= 2) { HM_PIPE(2); }
-    else if (need <= 4) { HM_PIPE(4); }
-    else if (need <= 6) { HM_PIPE(6); }
-    else { HM_PIPE(8); }
-#undef HM_PIPE
-    HM_LAUNCH_RET();
-}
-
-// Per-slot-G pipelined dispatch (Kp == 4, F <= 45, block layout, table < 4 GiB); -1 otherwise.
-template <bool BF>
-int dispatch_sg(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
-                const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
-                float* pred, float* loss, int grid, hipStream_t stream) {
     if (P.Kp != 4 || P.F > 45 || P.vpad <= 0) return -1;
-    const size_t vsb = BF ? 8 : 16;
-    if ((size_t)P.num_features * (size_t)P.fstride * vsb >= ((size_t)1 << 32)) return -1;
+    if ((size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32)) return -1;
     if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-    if (!BF && P.sg_threads == 0) {
-        // fp32 V: the LDS-DMA pipeline (variant 5 selects the register-prefetch kernel below)
 #define HM_P32(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
                                        fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (need <= 2) { HM_P32(2); }
-        else if (need <= 4) { HM_P32(4); }
-        else if (need <= 6) { HM_P32(6); }
-        else { HM_P32(8); }
+    if (need <= 2) { HM_P32(2); }
+    else if (need <= 4) { HM_P32(4); }
+    else if (need <= 6) { HM_P32(6); }
+    else { HM_P32(8); }
 #undef HM_P32
-        HM_LAUNCH_RET();
-    }
-    // 256 threads at 4 waves/SIMD (128 VGPRs, no spill: 4 rows in flight per CU); 512 threads
-    // (half the slots per thread; 3 blocks per CU) is variant 4 (A/B)
-    if (P.sg_threads != 512) {
-#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF, 256>), dim3(blocks), dim3(256), 0, stream, P, idx, \
-                                      fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (need <= 2) { HM_SG(2); }
-        else if (need <= 4) { HM_SG(4); }
-        else if (need <= 6) { HM_SG(6); }
-        else { HM_SG(8); }
-#undef HM_SG
-        HM_LAUNCH_RET();
-    }
-    const int need2 = (P.F * P.F + 511) / 512;
-#define HM_SG(NSV) hipLaunchKernelGGL((ffm_sg_kernel<NSV, BF, 512>), dim3(blocks), dim3(512), 0, stream, P, idx, \
-                                      fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-    if (need2 <= 1) { HM_SG(1); }
-    else if (need2 <= 2) { HM_SG(2); }
-    else if (need2 <= 3) { HM_SG(3); }
-    else { HM_SG(4); }
-#undef HM_SG
     HM_LAUNCH_RET();
 }
 
@@ -1855,14 +1515,9 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
             const int rc = dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
             return rc == -1 ? (int)hipErrorInvalidValue : rc;
         }
-        if (variant != 1 && BF && P.gfstride == 4 && P.vpad == 0 &&
-            reinterpret_cast<char*>(G) == reinterpret_cast<char*>(V) + 8) {
-            const int rc = dispatch_sg16(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
-            if (rc != -1) return rc;
-        }
-        if (variant != 1 && P.gfstride == 1) {
-            const int rc = dispatch_sg<BF>(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
-                                           bias, pred, loss, grid, stream);
+        if (variant != 1 && !BF && P.gfstride == 1) {
+            const int rc = dispatch_sg32(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
+                                         bias, pred, loss, grid, stream);
             if (rc != -1) return rc;
         }
         return launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
@@ -1882,17 +1537,16 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
 //                     slot_g, gstride, vpad, tail16, gfstride
 // slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f * gfstride];
-//             bf16 V in 16-B slots {V | G | 0} (G = V + 8 B, gfstride 4): ffm_pipe_kernel<SG>; with the
-//             block layout (G = V + vpad * slot bytes, vpad > 0) the pipelined ffm_sg_kernel runs
-//             (K <= 4, F <= 45), else the generic kernel.  tail16 = zero 16-B chunks after each
+//             bf16 V in 12-B slots {V | G} (G = V + 8 B, gfstride 3): ffm_pipe_sg12_kernel; fp32 V
+//             in the block layout (G = V + vpad * 16 B, vpad > 0): ffm_pipe_sg32_kernel (K <= 4,
+//             F <= 45); anything else the generic kernel.  tail16 = zero 16-B chunks after each
 //             feature's G region (line completion).
 // slot_g = 0 (per-element G shaped like V): packed = 1: V and G are the two halves of one
 //             [num_features][fstride][2][Kp] table (G == V + Kp elements, slot stride 2*Kp); 0:
 //             separate [.][.][Kp] tables.
-// variant: 0 = auto (per-slot: ffm_sg_kernel; per-element bf16: ffm_pipe_kernel, fp32:
-// ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel, 3 = ffm_pipe_kernel,
-// 4 = ffm_sg_kernel with 512-thread blocks, 5 = ffm_sg_kernel (256) for fp32 V (default there:
-// ffm_pipe_sg32_kernel).
+// variant (A/B): 0 = auto (per-slot: the sg12 / sg32 pipelines; per-element bf16:
+// ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel
+// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
@@ -1913,8 +1567,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.vpad = ip[19];
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
-    P.sg_threads = variant == 4 ? 512 : (variant == 5 ? 256 : 0);   // 0: fp32 LDS-DMA pipeline
-    if (slot_g && P.gfstride == 4) P.sstride = 2 * P.Kp;   // 16-B {V | G | 0} slots (bf16, Kp 4)
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];

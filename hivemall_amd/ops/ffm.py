@@ -40,10 +40,10 @@ class FFMHyper:
 
 
 _CALLS = 0  # per-launch counter mixed into the stochastic-rounding seed
-# kernel variant (A/B only), K <= 4 packed: 0 = auto (bf16 state: LDS-DMA pipelined
-# ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the round-1 ffm_packed_kernel, 2 = ffm_lean_kernel,
-# 3 = ffm_pipe_kernel, 4 / 5 = ffm_pipe_kernel polling its DMA targets, next row's gather issued
-# after / before this row's stores (measured no faster: profiles/ffm_poll_r2/)
+# kernel variant (A/B only; csrc/kernels/ffm.hip hm_ffm_step): 0 = auto (per-slot G: the
+# sg12 / sg32 LDS-DMA pipelines; per-element G, K <= 4 packed: bf16 ffm_pipe_kernel, fp32
+# ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel for bf16,
+# 3 = ffm_pipe_kernel for fp32
 _VARIANT = int(os.environ.get("HM_FFM_VARIANT", "0"))
 
 
@@ -107,21 +107,13 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
     Per-element G (G shaped like V): views of one packed [NF, FS, 2, Kp] table (FS =
     line-padded field count), or two split tables."""
     if slot_g:
-        lay = os.environ.get("HM_FFM_BF16_LAYOUT", "slot12")
-        if packed and dtype == torch.bfloat16 and kp == 4 and lay == "slot12":
+        if packed and dtype == torch.bfloat16 and kp == 4:
             # 12-B slots {V bf16 x 4 | G fp32} in 512-B blocks (ffm_pipe_sg12_kernel)
             fs, bs = slot12_layout(num_fields)
             buf = torch.zeros((num_features, bs), dtype=torch.uint8, device=device)
             sl = buf[:, :fs * 12]
             V = sl.view(torch.bfloat16).view(num_features, fs, 6)[:, :num_fields, :4]
             G = sl.view(torch.float32).view(num_features, fs, 3)[:, :num_fields, 2]
-            return V, G
-        if packed and dtype == torch.bfloat16 and kp == 4 and lay == "slot16":
-            # 16-B slots {V bf16 x 4 | G fp32 | 0}: one 16-B access per slot (ffm_pipe_kernel SG)
-            fs = padded_fields(num_fields, kp, dtype)
-            buf = torch.zeros((num_features, fs, 16), dtype=torch.uint8, device=device)
-            V = buf.view(torch.bfloat16)[:, :num_fields, :4]
-            G = buf.view(torch.float32)[:, :num_fields, 2]
             return V, G
         if packed:
             fs, bs, goff = slot_block_layout(num_fields, kp, dtype)
@@ -177,10 +169,10 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     block = (0, 0)
     if slot_g:
         # one fp32 AdaGrad accumulator per (feature, field) slot: G [NF, NFLD]
-        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) in (1, 3, 4), \
-            "per-slot G: fp32 [num_features, num_fields], field stride 1 (or 3 / 4: 12-B / 16-B bf16 slots)"
-        assert V.stride(2) == 1 and (V.stride(1) == Kp or (G.stride(1) in (3, 4) and V.stride(1) == 2 * G.stride(1))), \
-            "V: [NF, FS, Kp] slots (or the V part of 12-B / 16-B {V | G} slots)"
+        assert G.dtype == torch.float32 and G.shape == V.shape[:2] and G.stride(1) in (1, 3), \
+            "per-slot G: fp32 [num_features, num_fields], field stride 1 (or 3: 12-B bf16 slots)"
+        assert V.stride(2) == 1 and (V.stride(1) == Kp or (G.stride(1) == 3 and V.stride(1) == 6)), \
+            "V: [NF, FS, Kp] slots (or the V part of 12-B {V | G} slots)"
         packed = False
         gstride = G.stride(0)
         # block layout (slot_block_layout): G right after the V region of each feature block

@@ -156,7 +156,7 @@ def test_train_ffm_udtf_strings():
                                              ("packed", False, 8)])
 def test_ffm_gpu_matches_cpu_engine(layout, reload, k, adagrad):
     """HIP kernels vs the sequential C++ engine: identical on rows with disjoint features (no
-    Hogwild interaction).  Per-slot AdaGrad (default): the pipelined ffm_sg_kernel on the
+    Hogwild interaction).  Per-slot AdaGrad (default): the pipelined sg12 / sg32 kernels on the
     feature-block layout (k = 4), the generic kernel for k = 8 and for split tables; per-element
     (-elementwise_adagrad): the packed-slot and split-table kernels, with and without reload."""
     torch.manual_seed(0)
