@@ -28,6 +28,10 @@ __global__ __launch_bounds__(256) void probe(float* out, int spread) {
         if (MODE == 0) atomicAdd(&sf[a], v);                          // ds_add_f32
         else if (MODE == 1) atomicAdd(&su[a], (uint32_t)(s & 0xff));  // ds_add_u32
         else if (MODE == 2) sf[a] += v;                               // plain RMW (racy: throughput bound only)
+        else if (MODE == 3) {                                          // ds_add_u64: two packed sums per op
+            const int a2 = spread == 0 ? threadIdx.x : ((s >> 8) % spread) + (it % 24) * 256;
+            atomicAdd(reinterpret_cast<unsigned long long*>(su) + a2, (unsigned long long)(s & 0xff) << 32 | 3ull);
+        }
     }
     __syncthreads();
     float acc = 0.f;
@@ -47,14 +51,15 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[] = {"ds_add_f32", "ds_add_u32", "ld/st RMW"};
-    for (int mode = 0; mode < 3; ++mode) {
+    const char* names[] = {"ds_add_f32", "ds_add_u32", "ld/st RMW", "ds_add_u64"};
+    for (int mode = 0; mode < 4; ++mode) {
         for (int spread : {0, 256, 64}) {
             for (int rep = 0; rep < 2; ++rep) {
                 hipEventRecord(a);
                 if (mode == 0) hipLaunchKernelGGL(probe<0>, blocks, 256, 0, 0, out, spread);
                 if (mode == 1) hipLaunchKernelGGL(probe<1>, blocks, 256, 0, 0, out, spread);
                 if (mode == 2) hipLaunchKernelGGL(probe<2>, blocks, 256, 0, 0, out, spread);
+                if (mode == 3) hipLaunchKernelGGL(probe<3>, blocks, 256, 0, 0, out, spread);
                 hipEventRecord(b);
                 hipEventSynchronize(b);
                 float ms;
