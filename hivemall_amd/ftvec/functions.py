@@ -454,8 +454,11 @@ _AMPLIFY_OPTS = Options([opt("seed", None, 43, int, "Seed of the reservoir draws
 
 @udtf("rand_amplify", per_row=False)
 def rand_amplify(xtimes, num_buffers, *cols):
-    """Whole-input form: ``cols`` are columns (a trailing ``'-seed N'`` string is the
-    options); the output frame is built from the streamed rows chunk by chunk."""
+    """Emit every row xtimes, shuffled through num_buffers buffers (multi-epoch emulation);
+    a trailing ``'-seed N'`` option string seeds the shuffle.
+
+    Whole-input form: ``cols`` are columns; the output frame is built from the streamed rows
+    chunk by chunk."""
     x = xtimes[0] if isinstance(xtimes, (list, tuple)) else xtimes
     nb = num_buffers[0] if isinstance(num_buffers, (list, tuple)) else num_buffers
     seed = 43

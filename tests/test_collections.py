@@ -79,3 +79,18 @@ def test_function_catalogue_covers_registry():
     for name in registry.names():
         assert f"| `{name}`" in text
     assert "(see hivemall" not in text
+
+
+def test_checked_in_catalogue_and_ddl_are_current():
+    """docs/funcs.md and resources/ddl/define-all.hive are regenerated whenever a function or its
+    description changes (``python -m hivemall_amd.ddl --funcs docs/funcs.md``;
+    ``python -m hivemall_amd.ddl resources/ddl``)."""
+    import os
+
+    from hivemall_amd.ddl import define_all, function_catalogue
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "docs", "funcs.md")) as f:
+        assert f.read() == function_catalogue()
+    with open(os.path.join(root, "resources", "ddl", "define-all.hive")) as f:
+        assert f.read() == define_all()
