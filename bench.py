@@ -127,7 +127,9 @@ def check_world(args, ctx) -> None:
         bad.append(f"WORLD_SIZE={env_world}")
     if pg_world != args.gpus or ctx.world_size != args.gpus:
         bad.append(f"process group world={pg_world}")
-    if ctx.device.type == "cuda" and torch.cuda.device_count() < args.gpus:
+    # HM_DIST_BACKEND=gloo is the multi-rank rehearsal on fewer cards (ranks share a GPU; the
+    # JSON then reports dist_backend "gloo" and rccl_world null)
+    if ctx.device.type == "cuda" and torch.cuda.device_count() < args.gpus and ctx.backend != "gloo":
         bad.append(f"only {torch.cuda.device_count()} visible GPUs")
     if bad:
         print(f"[bench] --gpus {args.gpus} but " + ", ".join(bad), file=sys.stderr, flush=True)
