@@ -6,6 +6,8 @@
 //   num_features (default 2^24), fixes up negatives and returns a value starting from 1.
 // * Feature strings "name:value" / "name" / "field:index:value" are parsed here so the
 //   Python layer never loops over individual features.
+#include <charconv>
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -463,4 +465,73 @@ HM_API void hm_oht_get_i64(const int64_t* table, const int64_t* vals, int64_t ca
         }
         out[i] = r;
     }
+}
+
+// ---------------------------------------------------------------- add_feature_index
+// Text of a feature value as ftvec/functions.py _fmt writes it: integral |v| <= 1e15 as "%.1f",
+// anything else as Python's repr(float) — the shortest round-trip digits (std::to_chars, as
+// Python's dtoa), in fixed notation when the decimal exponent is in [-4, 16), else "d.ddde+XX".
+// Returns the length written to o (o needs 32 bytes); v must be finite.
+int fmt_py_float(double v, char* o) {
+    if (v == std::trunc(v) && std::fabs(v) <= 1e15) {
+        char t[40];                                       // snprintf's NUL must not land in o
+        const int n = std::snprintf(t, sizeof(t), "%.1f", v);
+        std::memcpy(o, t, (size_t)n);
+        return n;
+    }
+    char sci[32];
+    auto r = std::to_chars(sci, sci + sizeof(sci), v, std::chars_format::scientific);
+    const int sl = (int)(r.ptr - sci);
+    const char* e = (const char*)std::memchr(sci, 'e', (size_t)sl);
+    int ex = 0;                                           // value = d.ddd x 10^ex
+    for (const char* q = e + 2; q < sci + sl; ++q) ex = ex * 10 + (*q - '0');
+    if (e[1] == '-') ex = -ex;
+    if (ex < -4 || ex >= 16) {
+        std::memcpy(o, sci, (size_t)sl);
+        return sl;
+    }
+    auto f = std::to_chars(o, o + 32, v, std::chars_format::fixed);
+    int n = (int)(f.ptr - o);
+    if (!std::memchr(o, '.', (size_t)n)) { o[n++] = '.'; o[n++] = '0'; }
+    return n;
+}
+
+// add_feature_index over a list<double> column: row r's values vals[row_off[r] .. row_off[r+1])
+// -> strings "<position + 1>:<value>", null values (valid[k] == 0) skipped with their position
+// kept.  Two calls: out == nullptr returns the total bytes and fills out_off's lengths; then the
+// bytes.  out_off has row_off[n] + 1 entries (strings of skipped values are empty and dropped by
+// the caller through keep); returns -2 - k when value k is not finite (the per-row path raises).
+HM_API int64_t hm_format_feature_index(const double* vals, const uint8_t* valid,
+                                       const int64_t* row_off, int64_t n_rows, uint8_t* out,
+                                       int64_t* out_off) {
+    const int64_t nv = row_off[n_rows] - row_off[0];
+    int64_t bad = nv;
+    if (!out) {
+#pragma omp parallel for schedule(static) reduction(min : bad) if (n_rows > 4096)
+        for (int64_t r = 0; r < n_rows; ++r) {
+            char tmp[48];
+            for (int64_t k = row_off[r]; k < row_off[r + 1]; ++k) {
+                const int64_t q = k - row_off[0];
+                if (valid && !valid[q]) { out_off[q + 1] = 0; continue; }
+                if (!std::isfinite(vals[q])) { bad = q < bad ? q : bad; out_off[q + 1] = 0; continue; }
+                const int pos = (int)(k - row_off[r]) + 1;
+                out_off[q + 1] = dec_digits((uint32_t)pos) + 1 + fmt_py_float(vals[q], tmp);
+            }
+        }
+        if (bad < nv) return -2 - bad;
+        prefix_sum_inplace(out_off, nv);
+        return out_off[nv];
+    }
+#pragma omp parallel for schedule(static) if (n_rows > 4096)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        for (int64_t k = row_off[r]; k < row_off[r + 1]; ++k) {
+            const int64_t q = k - row_off[0];
+            if (out_off[q + 1] == out_off[q]) continue;
+            char* o = reinterpret_cast<char*>(out + out_off[q]);
+            const int hd = fmt_i32((int32_t)(k - row_off[r]) + 1, o);
+            o[hd] = ':';
+            fmt_py_float(vals[q], o + hd + 1);
+        }
+    }
+    return out_off[nv];
 }

@@ -151,12 +151,82 @@ def add_bias(features):
     return _add_bias1(features)
 
 
-@udf("add_feature_index")
-def add_feature_index(values):
-    """[v1, v2, ...] -> ["1:v1", "2:v2", ...]"""
+def _add_feature_index1(values):
     if values is None:
         return None
     return [f"{i + 1}:{_fmt(v)}" for i, v in enumerate(values) if v is not None]
+
+
+def _numeric_list_column(col):
+    """Arrow list<double> array of a Series of numeric lists, or None (strings, bools, mixed
+    content: the per-row path handles those)."""
+    import pandas as pd
+    import pyarrow as pa
+
+    if isinstance(col.dtype, pd.ArrowDtype):
+        a = col.array._pa_array
+        a = a.combine_chunks() if isinstance(a, pa.ChunkedArray) else a
+        if not (pa.types.is_list(a.type) or pa.types.is_large_list(a.type)):
+            return None
+        vt = a.type.value_type
+        if not (pa.types.is_integer(vt) or pa.types.is_floating(vt)):
+            return None
+        return a.cast(pa.large_list(pa.float64()))
+    vals = col.to_numpy(dtype=object)
+    for r in vals[:64]:
+        if r is not None and not (isinstance(r, (list, tuple, np.ndarray)) and all(
+                v is None or (isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool))
+                for v in r)):
+            return None
+    try:
+        return pa.array([None if r is None else list(r) for r in vals], type=pa.large_list(pa.float64()))
+    except (pa.ArrowInvalid, pa.ArrowTypeError, OverflowError):
+        return None
+
+
+@udf("add_feature_index", vectorized=True)
+def add_feature_index(values):
+    """[v1, v2, ...] -> ["1:v1", "2:v2", ...]"""
+    import pandas as pd
+
+    if not isinstance(values, pd.Series):
+        return _add_feature_index1(values)
+    arr = _numeric_list_column(values)
+    if arr is None:
+        return _rowwise(_add_feature_index1, values)
+    import pyarrow as pa
+
+    from .. import _native
+
+    n = len(arr)
+    lo = np.array(arr.offsets, dtype=np.int64)
+    flat = arr.values.slice(int(lo[0]), int(lo[-1] - lo[0]))
+    v = np.ascontiguousarray(flat.to_numpy(zero_copy_only=False), dtype=np.float64)
+    valid = None
+    if flat.null_count:
+        valid = np.ascontiguousarray(flat.is_valid().to_numpy(zero_copy_only=False), dtype=np.uint8)
+        v = np.where(valid.astype(bool), v, 0.0)
+    nv = len(v)
+    oo = np.empty(nv + 1, dtype=np.int64)
+    lib = _native.host()
+    vp = (v if nv else np.zeros(1)).ctypes.data
+    tot = lib.hm_format_feature_index(vp, None if valid is None else valid.ctypes.data, lo.ctypes.data, n,
+                                      None, oo.ctypes.data)
+    if tot < -1:                       # a non-finite value: the per-row path raises as before
+        return _rowwise(_add_feature_index1, values)
+    out = np.empty(max(1, int(tot)), dtype=np.uint8)
+    lib.hm_format_feature_index(vp, None if valid is None else valid.ctypes.data, lo.ctypes.data, n,
+                                out.ctypes.data, oo.ctypes.data)
+    strs = pa.LargeStringArray.from_buffers(nv, pa.py_buffer(oo), pa.py_buffer(out))
+    if valid is not None:              # null values are skipped, their positions kept
+        keep = pa.array(valid.astype(bool))
+        strs = strs.filter(keep)
+        cnt = np.concatenate([[0], np.cumsum(valid, dtype=np.int64)])
+        lo = cnt[lo - lo[0]]
+    else:
+        lo = lo - lo[0]
+    res = pa.LargeListArray.from_arrays(pa.array(lo, pa.int64()), strs.cast(pa.string()), mask=arr.is_null())
+    return _arrow_series(res, values.index)
 
 
 _FV_RE = r"^([^:]*:[^:]*|[^:]*):(.*)$"     # _split: value after the 2nd ':' when there is one

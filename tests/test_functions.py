@@ -243,3 +243,32 @@ def test_rand_amplify_seed_and_streaming():
     c = F.rand_amplify(2, 50, list(range(200)), "-seed 2")
     assert a["c0"].tolist() == b["c0"].tolist() != c["c0"].tolist()
     assert sorted(a["c0"].tolist()) == sorted(list(range(200)) * 2)
+
+
+def test_add_feature_index_vectorised_matches_rowwise():
+    """The column path (hm_format_feature_index: Python repr digits via std::to_chars) gives the
+    per-row strings exactly, nulls skipped with their positions kept; non-finite values fall
+    back to the per-row path and raise as before."""
+    import numpy as np
+    import pandas as pd
+    import pytest
+
+    from hivemall_amd.ftvec import functions as F
+
+    rng = np.random.default_rng(3)
+    rows = []
+    for _ in range(3000):
+        row = []
+        for _ in range(int(rng.integers(0, 8))):
+            t = int(rng.integers(0, 7))
+            row.append([int(rng.integers(-10**6, 10**6)), float(rng.standard_normal()),
+                        float(rng.standard_normal() * 10.0 ** rng.integers(-12, 20)), None,
+                        float(10.0 ** rng.integers(14, 18)) * float(rng.choice([1, -1, 2.5])), -0.0,
+                        float(np.float32(rng.random()))][t])
+        rows.append(row if rng.random() > 0.05 else None)
+    got = F.add_feature_index(pd.Series(rows, dtype=object)).tolist()
+    norm = lambda a: None if a is None or a is pd.NA else list(a)
+    assert [norm(a) for a in got] == [F._add_feature_index1(r) for r in rows]
+    assert F.add_feature_index([1, 2.5, None, 1e-7]) == ["1:1.0", "2:2.5", "4:1e-07"]
+    with pytest.raises((ValueError, OverflowError)):
+        F.add_feature_index(pd.Series([[1.0, float("nan")]], dtype=object))
