@@ -535,3 +535,89 @@ HM_API int64_t hm_format_feature_index(const double* vals, const uint8_t* valid,
     }
     return out_off[nv];
 }
+
+// ---------------------------------------------------------------- l1 / l2_normalize
+// Python float() of a value text, for the plain forms only ([+-]digits[.digits][e[+-]digits]):
+// strtod of those is the correctly rounded double, as float() is; anything else (spaces,
+// underscores, inf / nan words, hex) returns false and the caller takes the per-row path.
+bool parse_plain_double(const char* p, int n, double* out) {
+    if (n <= 0 || n > 63) return false;
+    for (int i = 0; i < n; ++i) {
+        const char c = p[i];
+        if (!((c >= '0' && c <= '9') || c == '.' || c == '-' || c == '+' || c == 'e' || c == 'E')) return false;
+    }
+    char tmp[64];
+    std::memcpy(tmp, p, (size_t)n);
+    tmp[n] = 0;
+    char* end = nullptr;
+    *out = std::strtod(tmp, &end);
+    return end == tmp + n;
+}
+
+// ftvec/functions.py _normalize over a list<string> column: per row, every "name:value" is
+// split as _split does, the values' L1 (p = 1) or L2 (p = 2) norm is summed left to right in
+// double, and each feature becomes "name:" + repr(value / norm); a row whose norm is 0 is
+// copied verbatim.  Two calls as hm_format_feature_index (out == nullptr: lengths + total).
+// Returns -2 - k when string k needs the per-row path (unparsable / non-finite).
+HM_API int64_t hm_normalize_features(const uint8_t* buf, const int64_t* off, const int64_t* row_off,
+                                     int64_t n_rows, int p, uint8_t* out, int64_t* out_off,
+                                     double* norm) {
+    const int64_t ns = row_off[n_rows] - row_off[0];
+    auto split = [&](int64_t q, int* nl, double* v) -> bool {
+        const char* s = (const char*)buf + off[q];
+        const int L = (int)(off[q + 1] - off[q]);
+        bool hv;
+        *nl = feature_name_len((const uint8_t*)s, L, &hv);
+        if (!hv) { *v = 1.0; return true; }
+        return parse_plain_double(s + *nl + 1, L - *nl - 1, v);
+    };
+    if (!out) {
+        int64_t bad = ns;
+#pragma omp parallel for schedule(static) reduction(min : bad) if (n_rows > 4096)
+        for (int64_t r = 0; r < n_rows; ++r) {
+            double acc = 0.0;
+            bool ok = true;
+            for (int64_t k = row_off[r]; k < row_off[r + 1]; ++k) {
+                const int64_t q = k - row_off[0];
+                int nl;
+                double v;
+                if (!split(q, &nl, &v) || !std::isfinite(v)) { bad = q < bad ? q : bad; ok = false; break; }
+                acc += p == 1 ? std::fabs(v) : v * v;
+            }
+            const double nr = p == 1 ? acc : std::sqrt(acc);
+            norm[r] = nr;
+            char tmp[48];
+            for (int64_t k = row_off[r]; k < row_off[r + 1]; ++k) {
+                const int64_t q = k - row_off[0];
+                const int L = (int)(off[q + 1] - off[q]);
+                if (!ok || nr == 0.0) { out_off[q + 1] = L; continue; }
+                int nl;
+                double v;
+                split(q, &nl, &v);
+                const double x = v / nr;
+                if (!std::isfinite(x)) { bad = q < bad ? q : bad; out_off[q + 1] = L; continue; }
+                out_off[q + 1] = nl + 1 + fmt_py_float(x, tmp);
+            }
+        }
+        if (bad < ns) return -2 - bad;
+        prefix_sum_inplace(out_off, ns);
+        return out_off[ns];
+    }
+#pragma omp parallel for schedule(static) if (n_rows > 4096)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const double nr = norm[r];
+        for (int64_t k = row_off[r]; k < row_off[r + 1]; ++k) {
+            const int64_t q = k - row_off[0];
+            char* o = reinterpret_cast<char*>(out + out_off[q]);
+            const char* s = (const char*)buf + off[q];
+            if (nr == 0.0) { std::memcpy(o, s, (size_t)(off[q + 1] - off[q])); continue; }
+            int nl;
+            double v;
+            split(q, &nl, &v);
+            std::memcpy(o, s, (size_t)nl);
+            o[nl] = ':';
+            fmt_py_float(v / nr, o + nl + 1);
+        }
+    }
+    return out_off[ns];
+}

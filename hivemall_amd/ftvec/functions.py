@@ -470,13 +470,56 @@ def _normalize(features, p):
     return [f"{n}:{_fmt(v / norm)}" for n, v in parsed]
 
 
-@udf("l1_normalize")
+def _normalize_column(col, p: int):
+    """l1 / l2_normalize over a whole list<string> column (hm_normalize_features: the per-row
+    rule, bit-identical); None when the column needs the per-row path."""
+    import pyarrow as pa
+
+    from .. import _native
+    from ..io.ingest import arrow_buffers
+
+    arr = _list_column(col)
+    if arr is None:
+        return None
+    data, so, lo = arrow_buffers(arr)
+    n = len(lo) - 1
+    ns = len(so) - 1
+    d = data if len(data) else np.zeros(1, np.uint8)
+    so = np.ascontiguousarray(so, dtype=np.int64)
+    lo = np.ascontiguousarray(lo, dtype=np.int64)
+    oo = np.empty(ns + 1, dtype=np.int64)
+    norm = np.empty(max(1, n), dtype=np.float64)
+    lib = _native.host()
+    tot = lib.hm_normalize_features(d.ctypes.data, so.ctypes.data, lo.ctypes.data, n, p, None,
+                                    oo.ctypes.data, norm.ctypes.data)
+    if tot < -1:
+        return None
+    out = np.empty(max(1, int(tot)), dtype=np.uint8)
+    lib.hm_normalize_features(d.ctypes.data, so.ctypes.data, lo.ctypes.data, n, p, out.ctypes.data,
+                              oo.ctypes.data, norm.ctypes.data)
+    strs = pa.LargeStringArray.from_buffers(ns, pa.py_buffer(oo), pa.py_buffer(out))
+    res = pa.LargeListArray.from_arrays(pa.array(lo, pa.int64()), strs.cast(pa.string()),
+                                        mask=arr.is_null())
+    return _arrow_series(res, col.index)
+
+
+@udf("l1_normalize", vectorized=True)
 def l1_normalize(features):
+    import pandas as pd
+
+    if isinstance(features, pd.Series):
+        r = _normalize_column(features, 1)
+        return r if r is not None else _rowwise(lambda f: _normalize(f, 1), features)
     return _normalize(features, 1)
 
 
-@udf("l2_normalize", "normalize")
+@udf("l2_normalize", "normalize", vectorized=True)
 def l2_normalize(features):
+    import pandas as pd
+
+    if isinstance(features, pd.Series):
+        r = _normalize_column(features, 2)
+        return r if r is not None else _rowwise(lambda f: _normalize(f, 2), features)
     return _normalize(features, 2)
 
 

@@ -272,3 +272,31 @@ def test_add_feature_index_vectorised_matches_rowwise():
     assert F.add_feature_index([1, 2.5, None, 1e-7]) == ["1:1.0", "2:2.5", "4:1e-07"]
     with pytest.raises((ValueError, OverflowError)):
         F.add_feature_index(pd.Series([[1.0, float("nan")]], dtype=object))
+
+
+def test_normalize_vectorised_matches_rowwise():
+    """l1 / l2_normalize over a column (hm_normalize_features) equal the per-row rule bit for
+    bit: bare names, "name:v" and "field:index:v" forms, zero-norm rows, null rows."""
+    import numpy as np
+    import pandas as pd
+
+    from hivemall_amd.ftvec import functions as F
+
+    rng = np.random.default_rng(7)
+
+    def val():
+        return [str(int(rng.integers(-50, 50))), repr(float(rng.standard_normal())), f"{rng.random():.3e}",
+                "0", repr(float(rng.standard_normal() * 1e12)), f"{rng.random():.4f}"][int(rng.integers(0, 6))]
+    rows = []
+    for _ in range(2000):
+        row = []
+        for j in range(int(rng.integers(0, 10))):
+            t = int(rng.integers(0, 4))
+            row.append([f"f{j}", f"f{j}:{val()}", f"{j}:{int(rng.integers(0, 99))}:{val()}", f"{j}:0"][t])
+        rows.append(row if rng.random() > 0.03 else None)
+    col = pd.Series(rows, dtype=object)
+    norm = lambda a: None if a is None or a is pd.NA else list(a)
+    for fn, p in ((F.l1_normalize, 1), (F.l2_normalize, 2)):
+        assert [norm(a) for a in fn(col).tolist()] == [F._normalize(r, p) for r in rows]
+    # a value the plain parser does not take (spaces) sends the column down the per-row path
+    assert F.l2_normalize(pd.Series([["a: 3", "b:4"]], dtype=object)).tolist() == [["a:0.6", "b:0.8"]]
