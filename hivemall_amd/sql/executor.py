@@ -5,7 +5,10 @@ A :class:`Session` holds named tables (pandas DataFrames), ``SET`` variables, ma
 function registry.  Statements: SELECT (joins, LATERAL VIEW, GROUP BY/HAVING, window
 functions, ORDER/SORT/CLUSTER BY, LIMIT, UNION ALL, CTEs, subqueries), CREATE TABLE [AS],
 CREATE VIEW, INSERT OVERWRITE/INTO, DROP, CREATE TEMPORARY FUNCTION/MACRO, SET, ADD JAR /
-SOURCE (accepted), SHOW FUNCTIONS, DESCRIBE FUNCTION.  Learner UDTFs (``train_*``) execute on
+SOURCE (accepted), SHOW FUNCTIONS, DESCRIBE FUNCTION; files come in through ``CREATE [EXTERNAL]
+TABLE ... [ROW FORMAT DELIMITED ...] [STORED AS ...] LOCATION '...'`` and ``LOAD DATA [LOCAL]
+INPATH`` and go out through ``INSERT OVERWRITE [LOCAL] DIRECTORY`` (io/tables.py: Hive text,
+parquet, libsvm, jsonl).  Learner UDTFs (``train_*``) execute on
 the session's device (``SET hivemall.device=cuda``) through the gfx950 kernels.
 """
 from __future__ import annotations
@@ -24,8 +27,9 @@ from .. import registry
 from . import builtins as B
 from .lexer import split_statements
 from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacro, CreateTable,
-                     DescribeFunction, Drop, Expr, Field, Func, Index, InList, Insert, IsNull, Join,
-                     LateralView, Like, Lit, NoOp, Query, Select, SelectItem, SetStmt,
+                     DescribeFunction, Drop, Expr, Field, Func, Index, InList, Insert,
+                     InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query,
+                     Select, SelectItem, SetStmt,
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, UnOp, Union, parse)
 
 
@@ -237,6 +241,7 @@ class Session:
             elif distributed:
                 raise SQLError("Session(distributed=True) needs an initialised process group")
         self.tables: dict[str, pd.DataFrame] = {}
+        self.table_meta: dict[str, dict] = {}    # declared columns / types / ROW FORMAT of CREATE TABLE
         self.views: dict[str, Query] = {}
         self.vars: dict[str, str] = {}
         self.macros: dict[str, tuple] = {}
@@ -307,8 +312,18 @@ class Session:
             if ast.view:
                 self.views[name] = ast.query
                 return None
-            if ast.query is None:
+            if ast.query is None and ast.storage.get("location"):
+                # CREATE [EXTERNAL] TABLE ... LOCATION '<file or directory>' (io/tables.py)
+                from ..io.tables import read_table
+
+                st = ast.storage
+                self.tables[name] = read_table(st["location"], st.get("stored_as"), ast.columns or None,
+                                               ast.types or None, st.get("field_delim"),
+                                               st.get("collection_delim")).reset_index(drop=True)
+                self.table_meta[name] = dict(columns=ast.columns, types=ast.types, storage=dict(st))
+            elif ast.query is None:
                 self.tables[name] = pd.DataFrame({c: pd.Series(dtype=object) for c in ast.columns})
+                self.table_meta[name] = dict(columns=ast.columns, types=ast.types, storage=dict(ast.storage))
             else:
                 self.tables[name] = self.run_query(ast.query).to_df()
             return None
@@ -327,6 +342,29 @@ class Session:
                 self.tables[name] = df.reset_index(drop=True)
             else:
                 self.tables[name] = pd.concat([self.tables[name], df], ignore_index=True)
+            return None
+        if isinstance(ast, LoadData):
+            # LOAD DATA [LOCAL] INPATH '<path>' [OVERWRITE] INTO TABLE t: the file is read with
+            # t's declared columns, types and ROW FORMAT
+            from ..io.tables import read_table
+
+            name = ast.table.lower()
+            meta = self.table_meta.get(name, {})
+            st = meta.get("storage", {})
+            cols = meta.get("columns") or (list(self.tables[name].columns) if name in self.tables else None)
+            df = read_table(ast.path, st.get("stored_as"), cols or None, meta.get("types") or None,
+                            st.get("field_delim"), st.get("collection_delim"))
+            if ast.overwrite or name not in self.tables or len(self.tables[name]) == 0:
+                self.tables[name] = df.reset_index(drop=True)
+            else:
+                self.tables[name] = pd.concat([self.tables[name], df], ignore_index=True)
+            return None
+        if isinstance(ast, InsertDirectory):
+            from ..io.tables import write_table
+
+            st = ast.storage
+            write_table(self.run_query(ast.query).to_df(), ast.path, st.get("stored_as"),
+                        st.get("field_delim"), st.get("collection_delim"))
             return None
         if isinstance(ast, Drop):
             n = ast.name.lower()

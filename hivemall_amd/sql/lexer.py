@@ -55,6 +55,16 @@ def _unescape(s: str) -> str:
     while i < len(body):
         c = body[i]
         if c == "\\" and i + 1 < len(body):
+            m = re.match(r"[0-7]{1,3}", body[i + 1:i + 4])
+            if m:                                   # Hive's octal escapes: '\001', '\t' = '\011'
+                out.append(chr(int(m.group(0), 8)))
+                i += 1 + len(m.group(0))
+                continue
+            m = re.match(r"u[0-9a-fA-F]{4}", body[i + 1:i + 6])
+            if m:
+                out.append(chr(int(m.group(0)[1:], 16)))
+                i += 6
+                continue
             out.append(_ESC.get(body[i + 1], body[i + 1]))
             i += 2
         else:

@@ -195,6 +195,22 @@ class CreateTable:
     columns: list = field(default_factory=list)
     if_not_exists: bool = False
     view: bool = False
+    types: list = field(default_factory=list)     # declared Hive types, parallel to columns
+    storage: dict = field(default_factory=dict)   # location / stored_as / field_delim / collection_delim
+
+
+@dataclass
+class LoadData:
+    path: str
+    table: str
+    overwrite: bool = False
+
+
+@dataclass
+class InsertDirectory:
+    path: str
+    query: Query
+    storage: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -321,6 +337,8 @@ class Parser:
             q = self.drop()
         elif t.is_kw("set"):
             q = self.set_stmt()
+        elif t.kind == "ident" and t.val.lower() == "load":
+            q = self.load_data()
         elif t.is_kw("add", "source", "use", "reload") or (t.kind == "ident" and t.val.lower() in ("delete", "list")):
             q = NoOp(self.sql)
             self.i = len(self.toks) - 1
@@ -418,18 +436,66 @@ class Parser:
                     self.error("unterminated column list")
             if cur:
                 cols.append(cur)
-            cols = [c[0] for c in cols if c]
+            cols = [c for c in cols if c]
+            types = ["".join(c[1:c.index("comment")] if "comment" in c else c[1:]) for c in cols]
+            cols = [c[0] for c in cols]
+        else:
+            types = []
         query = None
-        # skip STORED AS <fmt>, ROW FORMAT ..., LOCATION '...', TBLPROPERTIES (...), COMMENT '...'
+        # ROW FORMAT DELIMITED ..., STORED AS <fmt>, LOCATION '...' are kept (io/tables.py reads
+        # the location); TBLPROPERTIES (...), COMMENT '...', PARTITIONED BY (...) are skipped
+        storage = self.storage_clause(stop_at_query=True)
+        if self.accept_kw("as") or self.t.is_kw("select", "with"):
+            query = self.query()
+        return CreateTable(name, query, cols, ine, view, types, storage)
+
+    def storage_clause(self, stop_at_query: bool) -> dict:
+        st: dict = {}
         while self.t.kind != "eof" and not self.t.is_op(";"):
-            if self.t.is_kw("select", "with"):
+            if stop_at_query and self.t.is_kw("select", "with"):
                 break
             if self.t.is_kw("as") and (self.peek().is_kw("select", "with") or self.peek().is_op("(")):
                 break
+            if not stop_at_query and self.t.is_kw("select", "with"):
+                break
+            v = self.t.val.lower() if self.t.kind in ("kw", "ident") else None
+            if v == "terminated" and self.peek().is_kw("by") and self.peek(2).kind == "str":
+                prev = self.toks[self.i - 1].val.lower() if self.i else ""
+                self.next(); self.next()
+                key = {"fields": "field_delim", "items": "collection_delim", "keys": "map_key_delim",
+                       "lines": "line_delim"}.get(prev)
+                d = self.next().val
+                if key:
+                    st[key] = d
+                continue
+            if v == "stored" and self.peek().is_kw("as"):
+                self.next(); self.next()
+                st["stored_as"] = self.next().val.lower()
+                continue
+            if v == "location" and self.peek().kind == "str":
+                self.next()
+                st["location"] = self.next().val
+                continue
             self.next()
-        if self.accept_kw("as") or self.t.is_kw("select", "with"):
-            query = self.query()
-        return CreateTable(name, query, cols, ine, view)
+        return st
+
+    def load_data(self):
+        self.next()                                   # LOAD
+        if not (self.t.kind == "ident" and self.t.val.lower() == "data"):
+            self.error("expected LOAD DATA")
+        self.next()
+        if self.t.kind == "ident" and self.t.val.lower() == "local":
+            self.next()
+        if not (self.t.kind == "ident" and self.t.val.lower() == "inpath"):
+            self.error("expected INPATH")
+        self.next()
+        if self.t.kind != "str":
+            self.error("expected a path string")
+        path = self.next().val
+        overwrite = self.accept_kw("overwrite")
+        self.expect_kw("into")
+        self.expect_kw("table")
+        return LoadData(path, self.qualified_name(), overwrite)
 
     def insert(self):
         self.expect_kw("insert")
@@ -439,6 +505,17 @@ class Parser:
         else:
             self.expect_kw("into")
             overwrite = False
+        if self.t.kind == "ident" and self.t.val.lower() in ("local", "directory"):
+            if self.t.val.lower() == "local":
+                self.next()
+            if not (self.t.kind == "ident" and self.t.val.lower() == "directory"):
+                self.error("expected DIRECTORY")
+            self.next()
+            if self.t.kind != "str":
+                self.error("expected a directory path string")
+            path = self.next().val
+            storage = self.storage_clause(stop_at_query=False)
+            return InsertDirectory(path, self.query(), storage)
         self.accept_kw("table")
         name = self.qualified_name()
         if self.accept_kw("partition"):

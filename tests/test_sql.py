@@ -165,3 +165,60 @@ def test_feature_pairs_batch_path_equals_per_row(opt, monkeypatch):
         s.register("t", df)
         out.append(s.sql(q))
     pd.testing.assert_frame_equal(out[0], out[1])
+
+
+def test_file_backed_tables_and_cli(tmp_path):
+    """CREATE EXTERNAL TABLE ... LOCATION (libsvm, delimited text with arrays, parquet), LOAD
+    DATA INPATH, INSERT OVERWRITE LOCAL DIRECTORY and the `python -m hivemall_amd.sql` runner
+    (io/tables.py)."""
+    import pandas as pd
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    from hivemall_amd.sql import Session
+    from hivemall_amd.sql.__main__ import main as cli
+
+    (tmp_path / "a9a.libsvm").write_text("1 3:1 5:0.5 7:1\n-1 2:1 5:1\n\n1 1:0.25 3:1 9:1\n")
+    (tmp_path / "t.tsv").write_text("1\tapple,banana\t0.5\n0\tcherry\t\\N\n")
+    pq.write_table(pa.table({"rowid": [1, 2], "features": [["1:0.5", "2:1"], ["3:1"]]}),
+                   tmp_path / "test.parquet")
+    s = Session(device="cpu")
+    s.sql(f"""
+        CREATE EXTERNAL TABLE a9a (label double, features array<string>) STORED AS libsvm
+          LOCATION '{tmp_path}/a9a.libsvm';
+        CREATE TABLE t (id int, tags array<string>, w double)
+          ROW FORMAT DELIMITED FIELDS TERMINATED BY '\\t' COLLECTION ITEMS TERMINATED BY ','
+          STORED AS TEXTFILE;
+        LOAD DATA LOCAL INPATH '{tmp_path}/t.tsv' OVERWRITE INTO TABLE t;
+        CREATE EXTERNAL TABLE test (rowid bigint, features array<string>) STORED AS PARQUET
+          LOCATION '{tmp_path}/test.parquet';
+    """)
+    a9a = s.table("a9a")
+    assert a9a["label"].tolist() == [1.0, -1.0, 1.0]
+    assert [list(f) for f in a9a["features"]] == [["3:1", "5:0.5", "7:1"], ["2:1", "5:1"], ["1:0.25", "3:1", "9:1"]]
+    t = s.table("t")
+    assert t["id"].tolist() == [1, 0] and [list(x) for x in t["tags"]] == [["apple", "banana"], ["cherry"]]
+    assert t["w"].iloc[0] == 0.5 and pd.isna(t["w"].iloc[1])
+    assert isinstance(s.table("test")["features"].dtype, pd.ArrowDtype)
+    m = s.sql("SELECT train_classifier(add_bias(features), label, '-loss logloss') AS (feature, weight) FROM a9a")
+    assert sorted(m["feature"].tolist()) == ["0", "1", "2", "3", "5", "7", "9"]
+    # INSERT OVERWRITE DIRECTORY writes Hive text; reading it back with the same declaration
+    s.sql(f"INSERT OVERWRITE LOCAL DIRECTORY '{tmp_path}/out' ROW FORMAT DELIMITED FIELDS TERMINATED BY '\\t' "
+          "COLLECTION ITEMS TERMINATED BY ',' SELECT id, tags, w FROM t")
+    assert (tmp_path / "out" / "000000_0").read_text() == "1\tapple,banana\t0.5\n0\tcherry\t\\N\n"
+    s.sql(f"CREATE EXTERNAL TABLE t2 (id int, tags array<string>, w double) ROW FORMAT DELIMITED "
+          f"FIELDS TERMINATED BY '\\t' COLLECTION ITEMS TERMINATED BY ',' LOCATION '{tmp_path}/out'")
+    t2 = s.table("t2")
+    assert t2["id"].tolist() == t["id"].tolist() and [list(x) for x in t2["tags"]] == [list(x) for x in t["tags"]]
+    # the command-line runner: a registered file, a script with ${hivevar:...}, --out
+    (tmp_path / "q.sql").write_text("SELECT label, size(features) AS n FROM ${hivevar:tab} WHERE label > 0;")
+    assert cli(["-f", str(tmp_path / "q.sql"), "--device", "cpu", "--hivevar", "tab=x",
+                "--table", f"x={tmp_path}/a9a.libsvm", "--out", str(tmp_path / "r.tsv")]) == 0
+    assert (tmp_path / "r.tsv").read_text() == "1.0\t3\n1.0\t3\n"
+
+
+def test_lexer_octal_and_unicode_escapes():
+    from hivemall_amd.sql.lexer import tokenize
+
+    vals = [t.val for t in tokenize(r"select '\001', '\t', '\u0002', 'a\nb', '\0'") if t.kind == "str"]
+    assert vals == ["\x01", "\t", "\x02", "a\nb", "\x00"]
