@@ -116,6 +116,7 @@ _HOST_SIGS: dict[str, tuple] = {
     "hm_list_append_str": (c_i64, [c_p, c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_p, c_p]),
     "hm_format_feature_index": (c_i64, [c_p, c_p, c_p, c_i64, c_p, c_p]),
     "hm_normalize_features": (c_i64, [c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p]),
+    "hm_sigmoid_f64": (None, [c_p, c_i64, c_p]),
     "hm_oht_probe": (c_i64, [c_p, c_i64, c_p, c_i64, c_p, c_int]),
     "hm_oht_get_i64": (None, [c_p, c_p, c_i64, c_p, c_i64, c_i64, c_p]),
     "hm_join_ffm_rows_cpu": (None, [c_p] * 9 + [c_i64, c_int, c_p]),

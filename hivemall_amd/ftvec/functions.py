@@ -432,29 +432,88 @@ def prefixed_hash_values(values, prefix: str, use_index_as_prefix: bool = False)
 
 
 # ------------------------------------------------------------------ scaling
-@udf("rescale")
-def rescale(value, mn, mx):
-    """Min-max scaling to [0, 1]; also accepts a ``name:value`` feature string."""
+def _rescale1(value, mn, mx):
     if value is None:
         return None
     if isinstance(value, str):
         name, v = _split(value)
-        return f"{name}:{_fmt(rescale(v, mn, mx))}"
+        return f"{name}:{_fmt(_rescale1(v, mn, mx))}"
     mn, mx = float(mn), float(mx)
     if mx == mn:
         return 0.5
     return min(1.0, max(0.0, (float(value) - mn) / (mx - mn)))
 
 
-@udf("zscore")
-def zscore(value, mean, stddev):
+def _zscore1(value, mean, stddev):
     if value is None:
         return None
     if isinstance(value, str):
         name, v = _split(value)
-        return f"{name}:{_fmt(zscore(v, mean, stddev))}"
+        return f"{name}:{_fmt(_zscore1(v, mean, stddev))}"
     sd = float(stddev)
     return (float(value) - float(mean)) / sd if sd != 0 else 0.0
+
+
+def _num_cols(*args):
+    """float64 arrays of numeric Series / scalars (one length), or None for the per-row path."""
+    import pandas as pd
+
+    from ..tools.functions import _numeric_values
+
+    out = []
+    for a in args:
+        if isinstance(a, pd.Series):
+            v = _numeric_values(a)
+            if v is None:
+                return None
+            out.append(v)
+        elif isinstance(a, (int, float, np.integer, np.floating)) and not isinstance(a, bool):
+            out.append(np.float64(a))
+        else:
+            return None
+    return out
+
+
+def _scalar_or_rows(fn, args, index):
+    import pandas as pd
+
+    cols = [a.tolist() if isinstance(a, pd.Series) else None for a in args]
+    n = len(index)
+    rows = [fn(*[c[i] if c is not None else a for c, a in zip(cols, args)]) for i in range(n)]
+    return pd.Series(rows, index=index, dtype=object).infer_objects()
+
+
+@udf("rescale", vectorized=True)
+def rescale(value, mn, mx):
+    """Min-max scaling to [0, 1]; also accepts a ``name:value`` feature string."""
+    import pandas as pd
+
+    if not isinstance(value, pd.Series):
+        return _rescale1(value, mn, mx)
+    c = _num_cols(value, mn, mx)
+    if c is None:
+        return _scalar_or_rows(_rescale1, (value, mn, mx), value.index)
+    v, lo, hi = c
+    with np.errstate(divide="ignore", invalid="ignore"):
+        x = (v - lo) / (hi - lo)
+    y = np.where(x > 0.0, x, 0.0)                  # Python max(0.0, x): x only when x > 0.0
+    z = np.where(y < 1.0, y, 1.0)                  # min(1.0, y)
+    return pd.Series(np.where(hi == lo, 0.5, z), index=value.index)
+
+
+@udf("zscore", vectorized=True)
+def zscore(value, mean, stddev):
+    import pandas as pd
+
+    if not isinstance(value, pd.Series):
+        return _zscore1(value, mean, stddev)
+    c = _num_cols(value, mean, stddev)
+    if c is None:
+        return _scalar_or_rows(_zscore1, (value, mean, stddev), value.index)
+    v, m, sd = c
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = (v - m) / sd
+    return pd.Series(np.where(sd != 0, r, 0.0), index=value.index)
 
 
 def _normalize(features, p):

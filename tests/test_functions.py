@@ -300,3 +300,30 @@ def test_normalize_vectorised_matches_rowwise():
         assert [norm(a) for a in fn(col).tolist()] == [F._normalize(r, p) for r in rows]
     # a value the plain parser does not take (spaces) sends the column down the per-row path
     assert F.l2_normalize(pd.Series([["a: 3", "b:4"]], dtype=object)).tolist() == [["a:0.6", "b:0.8"]]
+
+
+def test_vectorised_math_udfs_match_rowwise():
+    """sigmoid (native, libm exp) / rescale / zscore over numeric columns equal the per-row
+    Python bit for bit, with per-row semantics for constants, equal bounds, zero stddev, +-inf."""
+    import numpy as np
+    import pandas as pd
+
+    from hivemall_amd.ftvec import functions as F
+    from hivemall_amd.tools import functions as T
+
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.standard_normal(20000) * 30, [0.0, -0.0, 700, -700, 745, -745, np.inf, -np.inf]])
+    got = T.sigmoid(pd.Series(x)).to_numpy()
+    want = np.array([T._sigmoid1(v) for v in x])
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    lo = pd.Series(rng.standard_normal(len(x)))
+    hi = lo + pd.Series(rng.random(len(x)))
+    hi[:10] = lo[:10]
+    xs = pd.Series(x)
+    for fn, f1, args in ((F.rescale, F._rescale1, (xs, lo, hi)), (F.rescale, F._rescale1, (xs, -3.0, 5.0)),
+                         (F.zscore, F._zscore1, (xs, lo, hi)), (F.zscore, F._zscore1, (xs, 0.5, 0.0))):
+        g = fn(*args).to_numpy()
+        cols = [a.tolist() if isinstance(a, pd.Series) else [a] * len(xs) for a in args]
+        w = np.array([f1(*r) for r in zip(*cols)], dtype=float)
+        assert np.array_equal(g, w, equal_nan=True), fn.__name__
+    assert F.rescale(pd.Series(["a:3", "b:7"]), 0, 10).tolist() == ["a:0.3", "b:0.7"]
