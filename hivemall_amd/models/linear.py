@@ -403,6 +403,11 @@ class OnlineLinearLearner(Learner):
         """Mix replicas (and ranks): average, or argmin-KLD for covariance learners."""
         st = self.state
         kld = self.covar
+        if st.R == 1 and not kld and st.device.type == "cpu" and not self._dp():
+            # one replica, plain average: num / den = w * 1 / 1 = w exactly, so the mix is the
+            # identity; skip its three passes over the (2^24-dim) table
+            self._w, self._cov = st.S[0, ..., 0].clone(), None
+            return
         num, den, cnt = LO.mix_reduce(st, kld)
         if self.mixer is not None and self.mixer.world > 1:
             self.mixer.all_reduce_sum([num, den, cnt])
