@@ -33,6 +33,10 @@ from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacr
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, UnOp, Union, parse)
 
 
+# UDFs that see NULL arguments themselves (everything else: NULL first argument -> NULL)
+_NULL_AWARE_UDFS = frozenset({"assert", "raise_error", "sessionize", "rowid", "rownum", "taskid"})
+
+
 class SQLError(Exception):
     pass
 
@@ -1165,8 +1169,14 @@ class Session:
                 return _ser(res if not isinstance(res, list) else pd.Series(res, dtype=object), n)
             cols = [_ser(a, n).tolist() if isinstance(a, pd.Series) else None for a in args]
             out = []
+            # Hivemall's UDFs return NULL for a NULL principal (first) argument: such rows yield
+            # NULL without calling the function (assert / raise_error / sessionize see NULLs)
+            null_rule = bool(args) and name not in _NULL_AWARE_UDFS
             for r in range(n):
                 row = [c[r] if c is not None else a for c, a in zip(cols, args)]
+                if null_rule and row[0] is None:
+                    out.append(None)
+                    continue
                 out.append(fd.impl(*row))
             return pd.Series(out, dtype=object).infer_objects() if out else pd.Series([], dtype=object)
         if fd is not None and fd.kind == registry.UDTF:

@@ -222,3 +222,18 @@ def test_lexer_octal_and_unicode_escapes():
 
     vals = [t.val for t in tokenize(r"select '\001', '\t', '\u0002', 'a\nb', '\0'") if t.kind == "str"]
     assert vals == ["\x01", "\t", "\x02", "a\nb", "\x00"]
+
+
+def test_udf_null_first_argument_yields_null():
+    """Hivemall's NULL rule: a per-row UDF whose principal (first) argument is NULL returns
+    NULL instead of raising (lat2tiley, popcnt, distance2similarity, ... on NULL rows)."""
+    import pandas as pd
+
+    from hivemall_amd.sql import Session
+
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"a": [1.5, None], "b": [[1, 2], None]}, dtype=object))
+    r = s.sql("SELECT popcnt(b) AS p, lat2tiley(a, 3) AS y, vectorize_features(array('x'), a) AS v FROM t")
+    assert pd.isna(r["p"].iloc[1]) and pd.isna(r["y"].iloc[1]) and r["p"].iloc[0] == 2
+    r2 = s.sql("SELECT distance2similarity(a) AS d FROM t")
+    assert pd.isna(r2["d"].iloc[1]) and r2["d"].iloc[0] > 0
