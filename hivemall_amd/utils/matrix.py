@@ -21,12 +21,14 @@ summed, as upstream's builders do.
 """
 from __future__ import annotations
 
+from abc import ABC, abstractmethod
+
 from typing import Iterable, Sequence
 
 import numpy as np
 
 
-class Matrix:
+class Matrix(ABC):
     """Common read interface (upstream ``hivemall.math.matrix.Matrix``)."""
 
     n_rows: int
@@ -36,24 +38,30 @@ class Matrix:
     def shape(self) -> tuple[int, int]:
         return (self.n_rows, self.n_cols)
 
+    @abstractmethod
     def nnz(self) -> int:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def get(self, i: int, j: int, default: float = 0.0) -> float:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def row(self, i: int) -> tuple[np.ndarray, np.ndarray]:
         """(column indices, values) of the non-zeros of row ``i``."""
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def to_dense(self) -> np.ndarray:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def matvec(self, x: np.ndarray) -> np.ndarray:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def to_csr(self) -> "CSRMatrix":
-        raise NotImplementedError
+        ...
 
     def to_torch(self, device=None, dtype=None):
         """Dense tensor (dense layouts) or ``torch.sparse_csr_tensor`` (sparse layouts)."""

@@ -18,6 +18,8 @@ Device code does not draw from these: the GPU kernels use counter-based hashes o
 """
 from __future__ import annotations
 
+from abc import ABC, abstractmethod
+
 import math
 
 import numpy as np
@@ -37,20 +39,24 @@ def _i64(x: int) -> int:
     return x - (1 << 64) if x >= (1 << 63) else x
 
 
-class PRNG:
+class PRNG(ABC):
     """Interface of upstream ``hivemall.math.random.PRNG``."""
 
+    @abstractmethod
     def next_int(self, bound: int | None = None) -> int:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def next_long(self) -> int:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def next_double(self) -> float:
-        raise NotImplementedError
+        ...
 
+    @abstractmethod
     def next_gaussian(self) -> float:
-        raise NotImplementedError
+        ...
 
     # Java-style aliases
     def nextInt(self, bound: int | None = None) -> int:  # noqa: N802
