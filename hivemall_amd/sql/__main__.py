@@ -3,6 +3,8 @@
     python -m hivemall_amd.sql -f train.sql [--device cuda] [--table a9a=a9a.libsvm]
         [--hivevar k=v ...] [--out model.parquet] [--show 20]
     python -m hivemall_amd.sql -e "SELECT hivemall_version()"
+    python -m hivemall_amd.sql < script.sql          # statements from stdin; a terminal gets
+                                                      # an interactive ``hivemall>`` prompt
 
 Scripts run statement by statement in one :class:`Session`: ``CREATE TABLE ... LOCATION``,
 ``LOAD DATA`` and ``INSERT OVERWRITE DIRECTORY`` move files in and out (io/tables.py);
@@ -30,8 +32,6 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default=None, help="write the last result (parquet / tsv / csv / jsonl)")
     ap.add_argument("--show", type=int, default=20, help="rows of the last result to print")
     a = ap.parse_args(argv)
-    if not a.file and not a.execute:
-        ap.error("nothing to run: give -f SCRIPT and/or -e SQL")
 
     rank = 0
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -52,22 +52,56 @@ def main(argv=None) -> int:
         if ":" in path and not os.path.exists(path):
             path, _, fmt = path.rpartition(":")
         s.register(name.strip(), read_table(path, fmt))
+
+    def show(df):
+        import pandas as pd
+
+        with pd.option_context("display.max_columns", 50, "display.width", 160):
+            print(df.head(a.show).to_string(index=False))
+            if len(df) > a.show:
+                print(f"... ({len(df)} rows)")
+
     out = None
     for path in a.file:
         out = s.run_script(path)
     for text in a.execute:
         out = s.sql(text)
+    if not a.file and not a.execute:
+        if sys.stdin.isatty():
+            return _repl(s, show)
+        out = s.sql(sys.stdin.read())
     if rank == 0 and out is not None:
         if a.out:
             print(f"wrote {len(out)} rows to {write_table(out, a.out)}")
         else:
-            import pandas as pd
-
-            with pd.option_context("display.max_columns", 50, "display.width", 160):
-                print(out.head(a.show).to_string(index=False))
-                if len(out) > a.show:
-                    print(f"... ({len(out)} rows)")
+            show(out)
     return 0
+
+
+def _repl(session, show) -> int:
+    """``hivemall>`` prompt: statements end at ``;``; errors are printed, not fatal."""
+    from .lexer import split_statements
+
+    buf = ""
+    while True:
+        try:
+            line = input("hivemall> " if not buf.strip() else "    ...> ")
+        except EOFError:
+            print()
+            return 0
+        if not buf.strip() and line.strip().lower() in ("quit", "exit", "quit;", "exit;"):
+            return 0
+        buf += line + "\n"
+        if not line.rstrip().endswith(";"):
+            continue
+        for stmt in split_statements(buf):
+            try:
+                r = session.sql(stmt)
+                if r is not None:
+                    show(r)
+            except Exception as e:          # the session stays usable after a bad statement
+                print(f"FAILED: {type(e).__name__}: {e}")
+        buf = ""
 
 
 if __name__ == "__main__":

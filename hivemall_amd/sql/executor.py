@@ -29,8 +29,37 @@ from .lexer import split_statements
 from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacro, CreateTable,
                      DescribeFunction, Drop, Expr, Field, Func, Index, InList, Insert,
                      InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query,
-                     Select, SelectItem, SetStmt,
+                     Select, SelectItem, SetStmt, ShowTables, DescribeTable,
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, UnOp, Union, parse)
+
+
+def _hive_type(col: pd.Series) -> str:
+    """Hive type name of a table column (DESCRIBE)."""
+    dt = col.dtype
+    if isinstance(dt, pd.ArrowDtype):
+        import pyarrow as pa
+
+        t = dt.pyarrow_dtype
+        if pa.types.is_list(t) or pa.types.is_large_list(t):
+            inner = t.value_type
+            return "array<" + ("string" if pa.types.is_string(inner) or pa.types.is_large_string(inner)
+                               else "double" if pa.types.is_floating(inner) else
+                               "bigint" if pa.types.is_integer(inner) else str(inner)) + ">"
+        return "string" if pa.types.is_string(t) or pa.types.is_large_string(t) else str(t)
+    if pd.api.types.is_bool_dtype(dt):
+        return "boolean"
+    if pd.api.types.is_integer_dtype(dt):
+        return "bigint" if dt.itemsize >= 8 else "int"
+    if pd.api.types.is_float_dtype(dt):
+        return "double" if dt.itemsize >= 8 else "float"
+    first = next((v for v in col if v is not None and not (isinstance(v, float) and v != v)), None)
+    if isinstance(first, (list, tuple, np.ndarray)):
+        inner = next((x for x in first if x is not None), None)
+        return "array<" + ("string" if isinstance(inner, str) else "double" if isinstance(inner, float)
+                           else "bigint" if isinstance(inner, (int, np.integer)) else "string") + ">"
+    if isinstance(first, dict):
+        return "map<string,double>"
+    return "string"
 
 
 # UDFs that see NULL arguments themselves (everything else: NULL first argument -> NULL)
@@ -403,6 +432,22 @@ class Session:
                 pat = ast.pattern.replace("*", ".*")
                 names = [n for n in names if re.fullmatch(pat, n)]
             return pd.DataFrame({"tab_name": sorted(set(names))})
+        if isinstance(ast, ShowTables):
+            names = sorted(set(self.tables) | set(self.views))
+            if ast.pattern:
+                pat = ast.pattern.replace("*", ".*")
+                names = [n for n in names if re.fullmatch(pat, n)]
+            return pd.DataFrame({"tab_name": names})
+        if isinstance(ast, DescribeTable):
+            n = ast.name.lower()
+            meta = self.table_meta.get(n, {})
+            if n in self.views:
+                df = self.run_query(self.views[n]).to_df().head(0)
+            else:
+                df = self.table(ast.name)
+            declared = dict(zip(meta.get("columns") or [], meta.get("types") or []))
+            return pd.DataFrame({"col_name": list(df.columns),
+                                 "data_type": [declared.get(c) or _hive_type(df[c]) for c in df.columns]})
         if isinstance(ast, DescribeFunction):
             fd = registry.lookup(ast.name)
             if fd is None:

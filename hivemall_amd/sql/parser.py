@@ -261,6 +261,16 @@ class DescribeFunction:
     name: str
 
 
+@dataclass
+class ShowTables:
+    pattern: str | None
+
+
+@dataclass
+class DescribeTable:
+    name: str
+
+
 # ------------------------------------------------------------------ parser
 class Parser:
     def __init__(self, sql: str):
@@ -344,19 +354,28 @@ class Parser:
             self.i = len(self.toks) - 1
         elif t.is_kw("show"):
             self.next()
-            self.expect_kw("functions")
+            tables = self.t.kind == "ident" and self.t.val.lower() == "tables"
+            if tables:
+                self.next()
+            else:
+                self.expect_kw("functions")
             pat = None
             if self.t.kind == "str":
                 pat = self.next().val
             elif self.accept_kw("like"):
                 pat = self.next().val
-            q = ShowFunctions(pat)
+            q = ShowTables(pat) if tables else ShowFunctions(pat)
         elif t.is_kw("describe"):
             self.next()
-            self.expect_kw("function")
-            if self.t.kind == "ident" and self.t.val.lower() == "extended":
-                self.next()
-            q = DescribeFunction(self.ident())
+            if self.accept_kw("function"):
+                if self.t.kind == "ident" and self.t.val.lower() == "extended":
+                    self.next()
+                q = DescribeFunction(self.ident())
+            else:
+                self.accept_kw("table")
+                if self.t.kind == "ident" and self.t.val.lower() in ("extended", "formatted"):
+                    self.next()
+                q = DescribeTable(self.qualified_name())
         elif t.is_kw("explain"):
             self.next()
             return ("explain", self.statement())

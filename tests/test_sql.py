@@ -237,3 +237,24 @@ def test_udf_null_first_argument_yields_null():
     assert pd.isna(r["p"].iloc[1]) and pd.isna(r["y"].iloc[1]) and r["p"].iloc[0] == 2
     r2 = s.sql("SELECT distance2similarity(a) AS d FROM t")
     assert pd.isna(r2["d"].iloc[1]) and r2["d"].iloc[0] > 0
+
+
+def test_show_tables_describe_and_stdin_runner(monkeypatch, capsys):
+    import io
+
+    import pandas as pd
+
+    from hivemall_amd.sql import Session
+    from hivemall_amd.sql.__main__ import main as cli
+
+    s = Session(device="cpu")
+    s.register("train", pd.DataFrame({"rowid": [1, 2], "features": [["a:1"], ["b:2"]], "label": [1.0, 0.0]}))
+    s.sql("CREATE TABLE t2 (k string, v array<double>); CREATE VIEW v AS SELECT rowid FROM train")
+    assert s.sql("SHOW TABLES")["tab_name"].tolist() == ["t2", "train", "v"]
+    assert s.sql("SHOW TABLES 'tr*'")["tab_name"].tolist() == ["train"]
+    d = s.sql("DESCRIBE train")
+    assert d["data_type"].tolist() == ["bigint", "array<string>", "double"]
+    assert s.sql("DESCRIBE t2")["data_type"].tolist() == ["string", "array<double>"]
+    monkeypatch.setattr("sys.stdin", io.StringIO("SELECT 40 + 2 AS answer;"))
+    assert cli(["--device", "cpu"]) == 0
+    assert "42" in capsys.readouterr().out
