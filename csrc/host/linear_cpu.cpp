@@ -37,9 +37,21 @@ void train_replica(const Params& P, int r, int R, int dims, int L, int64_t n_row
         gmark.assign(dims, 0);
     }
     int in_batch = 0;
+    // Rows are sequential (row q+1 reads what row q wrote), but the state lines a later row needs
+    // can be requested early: at Hivemall's 2^24 hashed dims the 256-MB table misses every
+    // cache, and touching row q+PF's lines now overlaps their misses with row q's math.  A pure
+    // hint: the arithmetic and its order are unchanged.
+    constexpr int64_t PF = 2;
     for (int64_t q = r0; q < r1; ++q) {
         const int64_t row = order ? (int64_t)order[q] : q;
         const int64_t s = indptr[row], e = indptr[row + 1];
+        if (!mc && q + PF < r1) {
+            const int64_t pr = order ? (int64_t)order[q + PF] : q + PF;
+            for (int64_t k = indptr[pr], ke = indptr[pr + 1]; k < ke; ++k) {
+                const uint32_t i = (uint32_t)idx[k];
+                if (i < (uint32_t)dims) __builtin_prefetch(M + (size_t)i * 4, 1, 3);
+            }
+        }
         const float yy = y[row];
         rs[RS_T] += 1.f;
         const float t = rs[RS_T];

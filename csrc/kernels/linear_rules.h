@@ -25,7 +25,7 @@
 #include <hip/hip_runtime.h>
 #define HM_HD __host__ __device__ __forceinline__
 #else
-#define HM_HD static inline
+#define HM_HD static inline __attribute__((always_inline))   // as on the device: the per-feature rules must inline into the row loop
 #endif
 
 namespace hm_lin {
