@@ -27,13 +27,15 @@ inline float ftrl_update(float* z, float* n, float w, float g, float alpha, floa
 
 inline float log1pexp(float x) { return x > 0.f ? x + std::log1p(std::exp(-x)) : std::log1p(std::exp(x)); }
 
-}  // namespace
-
-HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
-                           const int32_t* fld, const float* val, const float* y, float* V,
-                           float* G, float* w, float* wz, float* wn, float* bias, float* pred,
-                           float* loss) {
-    const int B = ip[0], F = ip[1], NF = ip[2], NFLD = ip[3], Kp = ip[4];
+template <int KP>
+int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
+                 const int32_t* fld, const float* val, const float* y, float* V,
+                 float* G, float* w, float* wz, float* wn, float* bias, float* pred,
+                 float* loss) {
+    // KP > 0: the factor count as a compile-time constant (k = 4 / 8: the slot copies and the
+    // k-loops unroll, no memcpy call per slot); KP = 0: any Kp.  Same operations in the same
+    // order either way, so the results are identical.
+    const int B = ip[0], F = ip[1], NF = ip[2], NFLD = ip[3], Kp = KP > 0 ? KP : ip[4];
     const int cls = ip[5], train = ip[6], use_lin = ip[7], use_bias = ip[8], norm = ip[9];
     const float eta0 = hp[0], eps = hp[1], lv = hp[2], alpha = hp[3], beta = hp[4];
     const float l1 = hp[5], l2 = hp[6], tmin = hp[7], tmax = hp[8];
@@ -70,10 +72,12 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
         for (int a = 0; a < F; ++a)
             for (int b = 0; b < F; ++b) {
                 float* dst = &snap[((size_t)a * F + b) * Kp];
-                if (a != b && ri[a] >= 0 && ri[b] >= 0)
-                    std::memcpy(dst, V + ((size_t)ri[a] * FS + rf[b]) * ss, sizeof(float) * Kp);
-                else
-                    std::memset(dst, 0, sizeof(float) * Kp);
+                if (a != b && ri[a] >= 0 && ri[b] >= 0) {
+                    const float* src = V + ((size_t)ri[a] * FS + rf[b]) * ss;
+                    for (int k = 0; k < Kp; ++k) dst[k] = src[k];
+                } else {
+                    for (int k = 0; k < Kp; ++k) dst[k] = 0.f;
+                }
             }
         double p = 0.0;
         for (int a = 0; a < F; ++a)
@@ -141,4 +145,17 @@ HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* id
         if (use_bias) bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, alpha, beta, 0.f, 0.f);
     }
     return 0;
+}
+
+}  // namespace
+
+HM_API int hm_ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
+                           const int32_t* fld, const float* val, const float* y, float* V,
+                           float* G, float* w, float* wz, float* wn, float* bias, float* pred,
+                           float* loss) {
+    switch (ip[4]) {
+        case 4: return ffm_step_cpu<4>(ip, hp, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
+        case 8: return ffm_step_cpu<8>(ip, hp, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
+        default: return ffm_step_cpu<0>(ip, hp, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss);
+    }
 }
