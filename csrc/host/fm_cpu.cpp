@@ -22,8 +22,17 @@ HM_API int hm_fm_step_cpu(const int32_t* ip, const float* hp, int64_t n_rows, in
     const float eta0 = hp[0], power_t = hp[1], total = hp[2], l0 = hp[3], lw = hp[4], lv = hp[5];
     const float mn = hp[6], mx = hp[7];
     std::vector<float> S(KP);
+    constexpr int64_t PF = 2;      // rows ahead whose w / V lines are requested (a hint only)
     for (int64_t row = 0; row < n_rows; ++row) {
         const int64_t s = indptr[row], e = indptr[row + 1];
+        if (row + PF < n_rows)
+            for (int64_t q = indptr[row + PF]; q < indptr[row + PF + 1]; ++q) {
+                const uint32_t i = (uint32_t)idx[q];
+                if (i < (uint32_t)dims) {
+                    __builtin_prefetch(w + i, 1, 3);
+                    __builtin_prefetch(V + (size_t)i * KP, 1, 3);
+                }
+            }
         std::fill(S.begin(), S.end(), 0.f);
         float lin = 0.f, sq = 0.f;
         for (int64_t q = s; q < e; ++q) {
