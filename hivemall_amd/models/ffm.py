@@ -30,6 +30,7 @@ import pandas as pd
 import torch
 
 from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
+from ..ops.touched import mark_touched
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
 from .base import COMMON_ITER_OPTS, ConversionState, Learner, log, parse_labels_binary
@@ -212,9 +213,7 @@ class FFMTrainer(Learner):
         self._mark_touched(b)
 
     def _mark_touched(self, b: FFMBatch) -> None:
-        i = b.idx.reshape(-1).long()
-        i = i[(i >= 0) & (i < self.num_features)]
-        self.touched[i] = True
+        mark_touched(self.touched, b.idx, self.num_features)
 
     def mix(self) -> None:
         self.mix_tensors([self.state["V"], self.state["wz"], self.state["wn"], self.state["w"],

@@ -21,6 +21,7 @@ import pandas as pd
 import torch
 
 from ..ops.fm import FMHyper, fm_step
+from ..ops.touched import mark_touched
 
 # global-bias shards on the GPU (see ops/fm.py): one same-address atomic per row capped train_fm
 # at ~40 M rows/s on MI355X whatever the grid (profiles/fm_grid_probe_r1.log)
@@ -192,8 +193,7 @@ class FMTrainer(Learner):
                 self._nbatches = getattr(self, "_nbatches", 0) + 1
                 if self._nbatches % mi == 0:
                     self.mix()
-        i = rows.idx.long()
-        self.touched[i[(i >= 0) & (i < self.dims)]] = True
+        mark_touched(self.touched, rows.idx, self.dims)
 
     def mix(self) -> None:
         """Replica averaging over the ranks (w, V, w0; the SGD state has no optimizer slots)."""
@@ -253,8 +253,7 @@ class FMTrainer(Learner):
         st["V"][:, : self.k] = eng.V[:, : self.k].to(st["V"].dtype)
         st["w0"].zero_()
         st["w0"][0] = eng.w0[0]
-        i = rows.idx.long()
-        self.touched[i[(i >= 0) & (i < self.dims)]] = True
+        mark_touched(self.touched, rows.idx, self.dims)
         self.mix()
         return self
 

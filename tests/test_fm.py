@@ -228,3 +228,29 @@ def test_fm_minibatch_kernel_gradient_matches_fp32_reference(variant, d, KP, k, 
 def test_fm_minibatch_gradient_reference_cpu(d, KP, k, n, cls):
     """The same gradient check on the CPU path (torch ops) — validates the check itself."""
     test_fm_minibatch_kernel_gradient_matches_fp32_reference(0, d, KP, k, n, 0, cls, device="cpu")
+
+
+@pytest.mark.gpu
+def test_mark_touched_kernel_matches_torch():
+    """hm_mark_touched (csrc/kernels/util.hip) sets exactly the flags a torch scatter sets:
+    valid ids only, unaligned tails, duplicates, ids out of range ignored."""
+    from hivemall_amd.ops.touched import mark_touched
+
+    g = torch.Generator().manual_seed(3)
+    for n, dims in ((1, 10), (7, 5), (1 << 20, 1 << 16), ((1 << 20) + 3, 1000)):
+        idx = torch.randint(-5, dims + 5, (n,), generator=g, dtype=torch.int32)
+        want = torch.zeros(dims, dtype=torch.bool)
+        i = idx.long()
+        want[i[(i >= 0) & (i < dims)]] = True
+        got = torch.zeros(dims, dtype=torch.bool, device="cuda")
+        mark_touched(got, idx.cuda(), dims)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), want), (n, dims)
+        # an unaligned view (offset 1 element) goes through the scalar path
+        if n > 8:
+            got2 = torch.zeros(dims, dtype=torch.bool, device="cuda")
+            mark_touched(got2, idx.cuda()[1:], dims)
+            w2 = torch.zeros(dims, dtype=torch.bool)
+            j = idx[1:].long()
+            w2[j[(j >= 0) & (j < dims)]] = True
+            assert torch.equal(got2.cpu(), w2)
