@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import fnmatch
 import itertools
+import logging
 import math
 import os
 import re
@@ -31,6 +32,46 @@ from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacr
                      InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query,
                      Select, SelectItem, SetStmt, ShowTables, DescribeTable,
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, UnOp, Union, parse)
+
+
+# Hivemall classes whose function name is not the snake_case of the class name
+_HIVEMALL_CLASSES = {
+    "GeneralClassifierUDTF": "train_classifier", "GeneralRegressorUDTF": "train_regressor",
+    "GeneralRegressionUDTF": "train_regressor", "FactorizationMachineUDTF": "train_fm",
+    "FieldAwareFactorizationMachineUDTF": "train_ffm", "FMPredictGenericUDAF": "fm_predict",
+    "FFMPredictGenericUDAF": "ffm_predict", "FFMPredictUDF": "ffm_predict",
+    "RandomForestClassifierUDTF": "train_randomforest_classifier",
+    "RandomForestRegressionUDTF": "train_randomforest_regressor",
+    "GradientTreeBoostingClassifierUDTF": "train_gradient_tree_boosting_classifier",
+    "TreePredictUDF": "tree_predict", "RandomForestEnsembleUDAF": "rf_ensemble",
+    "MurmurHash3UDF": "mhash", "LogressUDTF": "logress", "AdaGradRDAUDTF": "train_adagrad_rda",
+    "PerceptronUDTF": "train_perceptron", "PassiveAggressiveUDTF": "train_pa",
+    "AROWClassifierUDTF": "train_arow", "ConfidenceWeightedUDTF": "train_cw",
+    "BPRMatrixFactorizationUDTF": "train_bprmf", "MatrixFactorizationSGDUDTF": "train_mf_sgd",
+    "MatrixFactorizationAdaGradUDTF": "train_mf_adagrad", "LDAUDTF": "train_lda",
+    "PLSAUDTF": "train_plsa", "SigmoidGenericUDF": "sigmoid", "AUCUDAF": "auc",
+    "LogarithmicLossUDAF": "logloss", "L2NormalizationUDF": "l2_normalize",
+    "L1NormalizationUDF": "l1_normalize", "XGBoostClassifierUDTF": "train_xgboost_classifier",
+    "XGBoostRegressionUDTF": "train_xgboost_regr", "XGBoostTrainUDTF": "train_xgboost",
+}
+
+
+def _resolve_function_class(cls: str) -> str | None:
+    """Registry name behind a CREATE TEMPORARY FUNCTION class: one of this engine's own
+    implementations (define-all.hive names them), or a Hivemall class by its simple name."""
+    for name in registry.names():
+        impl = registry.REGISTRY[name].impl
+        if f"{getattr(impl, '__module__', '')}.{getattr(impl, '__qualname__', '')}" == cls:
+            return name
+    simple = cls.rsplit(".", 1)[-1]
+    if simple in _HIVEMALL_CLASSES and registry.lookup(_HIVEMALL_CLASSES[simple]) is not None:
+        return _HIVEMALL_CLASSES[simple]
+    base = re.sub(r"(Generic)?(UDTF|UDAF|UDF)$", "", simple)
+    snake = re.sub(r"(?<=[a-z0-9])(?=[A-Z])|(?<=[A-Z])(?=[A-Z][a-z])", "_", base).lower()
+    for cand in (snake, "train_" + snake):
+        if registry.lookup(cand) is not None:
+            return cand
+    return None
 
 
 def _hive_type(col: pd.Series) -> str:
@@ -64,6 +105,9 @@ def _hive_type(col: pd.Series) -> str:
 
 # UDFs that see NULL arguments themselves (everything else: NULL first argument -> NULL)
 _NULL_AWARE_UDFS = frozenset({"assert", "raise_error", "sessionize", "rowid", "rownum", "taskid"})
+
+
+log = logging.getLogger("hivemall_amd.sql")
 
 
 class SQLError(Exception):
@@ -279,11 +323,21 @@ class Session:
         self.vars: dict[str, str] = {}
         self.macros: dict[str, tuple] = {}
         self.functions_declared: dict[str, str] = {}
+        self.function_aliases: dict[str, str] = {}   # CREATE TEMPORARY FUNCTION alias -> registry name
         if device is not None:
             self.vars["hivemall.device"] = str(device)
         registry.load_all()
 
     # -- public API
+    def _lookup(self, name: str):
+        """Registry entry of a function name, through CREATE TEMPORARY FUNCTION aliases."""
+        fd = registry.lookup(name)
+        if fd is None:
+            target = self.function_aliases.get(name.lower())
+            if target is not None:
+                fd = registry.lookup(target)
+        return fd
+
     def register(self, name: str, df: pd.DataFrame) -> None:
         self.tables[name.lower()] = df.reset_index(drop=True)
 
@@ -327,7 +381,7 @@ class Session:
         n = name.lower()
         if n in self.macros:
             return False
-        fd = registry.lookup(n)
+        fd = self._lookup(n)
         if fd is not None:
             return fd.kind == registry.UDAF
         return n in B.AGGREGATE
@@ -412,7 +466,17 @@ class Session:
                 self.macros.pop(n, None)
             return None
         if isinstance(ast, CreateFunction):
-            self.functions_declared[ast.name.lower()] = ast.class_name
+            n = ast.name.lower()
+            self.functions_declared[n] = ast.class_name
+            if registry.lookup(n) is None:
+                target = _resolve_function_class(ast.class_name)
+                if target is None:
+                    # as Hive with the class missing from the classpath, except that the script
+                    # goes on (a define-all.hive may name functions the script never calls)
+                    log.warning("CREATE TEMPORARY FUNCTION %s: no implementation of '%s'; calls "
+                                "to %s will fail", ast.name, ast.class_name, ast.name)
+                else:
+                    self.function_aliases[n] = target
             return None
         if isinstance(ast, CreateMacro):
             self.macros[ast.name.lower()] = (ast.params, ast.body)
@@ -449,7 +513,7 @@ class Session:
             return pd.DataFrame({"col_name": list(df.columns),
                                  "data_type": [declared.get(c) or _hive_type(df[c]) for c in df.columns]})
         if isinstance(ast, DescribeFunction):
-            fd = registry.lookup(ast.name)
+            fd = self._lookup(ast.name)
             if fd is None:
                 return pd.DataFrame({"tab_name": [f"Function '{ast.name}' does not exist."]})
             return pd.DataFrame({"tab_name": [f"{fd.name} ({fd.kind}): {fd.doc or ''}"]})
@@ -630,7 +694,7 @@ class Session:
 
     # -- lateral view
     def _table_fn(self, name: str):
-        fd = registry.lookup(name)
+        fd = self._lookup(name)
         if fd is not None and fd.kind == registry.UDTF:
             return fd.impl, fd.per_row, fd.cols
         if name in B.TABLE:
@@ -719,7 +783,7 @@ class Session:
         # UDTF in the select list
         if len(s.items) == 1 and isinstance(s.items[0].expr, Func) and s.items[0].expr.window is None:
             fname = s.items[0].expr.name
-            fd = registry.lookup(fname)
+            fd = self._lookup(fname)
             if (fd is not None and fd.kind == registry.UDTF) or fname in B.TABLE:
                 out = self._select_udtf(s.items[0], src, ctes)
                 return self._finish(out, out, s, ctes)
@@ -901,7 +965,7 @@ class Session:
         if name == "count" and (a.star or not a.args):
             return pd.Series(np.diff(bounds))
         arg_vals = [_ser(self.eval(x, src, ctes), src.n) for x in a.args]
-        fd = registry.lookup(name)
+        fd = self._lookup(name)
         if fd is None and name in B.PANDAS_AGG and len(arg_vals) == 1 and not a.distinct:
             s = arg_vals[0]
             numeric = pd.api.types.is_numeric_dtype(s) or name == "count"
@@ -976,7 +1040,7 @@ class Session:
                 for r, i in enumerate(grp):
                     out[i] = r * k // len(grp) + 1
             else:
-                impl = registry.lookup(name)
+                impl = self._lookup(name)
                 impl = impl.impl if impl is not None else B.AGGREGATE.get(name)
                 if impl is None:
                     raise SQLError(f"unknown window function {name}")
@@ -1195,7 +1259,7 @@ class Session:
             params, body = self.macros[name]
             sub = {p.lower(): a for p, a in zip(params, f.args)}
             return self.eval(_subst_macro(body, sub), fr, ctes, vals)
-        fd = registry.lookup(name)
+        fd = self._lookup(name)
         if fd is not None and fd.kind == registry.UDAF or (fd is None and name in B.AGGREGATE):
             if isinstance(fr, _GroupBase):
                 return fr.agg(f, ctes)

@@ -258,3 +258,28 @@ def test_show_tables_describe_and_stdin_runner(monkeypatch, capsys):
     monkeypatch.setattr("sys.stdin", io.StringIO("SELECT 40 + 2 AS answer;"))
     assert cli(["--device", "cpu"]) == 0
     assert "42" in capsys.readouterr().out
+
+
+def test_create_temporary_function_aliases():
+    """CREATE TEMPORARY FUNCTION name AS '<class>' makes `name` callable: a Hivemall class (by its
+    simple name) or one of this engine's implementations (as define-all.hive names them)."""
+    import pandas as pd
+
+    from hivemall_amd.sql import Session
+
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"f": [["a:1", "b:2"]], "y": [1]}))
+    s.sql("CREATE TEMPORARY FUNCTION my_hash AS 'hivemall.ftvec.hashing.FeatureHashingUDF';"
+          "CREATE TEMPORARY FUNCTION my_train AS 'hivemall.classifier.GeneralClassifierUDTF';"
+          "CREATE TEMPORARY FUNCTION sig AS 'hivemall_amd.tools.functions.sigmoid';"
+          "CREATE TEMPORARY FUNCTION nope AS 'com.example.Missing'")
+    r = s.sql("SELECT my_hash(f) AS h, sig(0) AS p FROM t")
+    assert list(r["h"].iloc[0]) == list(s.sql("SELECT feature_hashing(f) AS h FROM t")["h"].iloc[0])
+    assert r["p"].iloc[0] == 0.5
+    m = s.sql("SELECT my_train(add_bias(f), y) AS (feature, weight) FROM t")
+    assert sorted(m["feature"]) == ["0", "a", "b"]
+    import pytest
+
+    from hivemall_amd.sql import SQLError
+    with pytest.raises(SQLError):
+        s.sql("SELECT nope(1) FROM t")
