@@ -226,8 +226,12 @@ class ModelMixer:
     MAX_PLAN_BYTES = 16 << 30
 
     def __init__(self, ctx: DistContext | None = None, bucket_mb: float = 64.0,
-                 small_bytes: int = 4 << 20, wire_dtype: torch.dtype | None = None):
+                 small_bytes: int = 4 << 20, wire_dtype: torch.dtype | None = None,
+                 min_world: int = 2):
         self.ctx = ctx or context()
+        # min_world = 1: run the collectives even in a one-rank process group (the RCCL smoke
+        # test drives the real all_to_all / all_gather / all_reduce calls on one GPU)
+        self.min_world = int(min_world)
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.small_bytes = small_bytes
         self.wire_dtype = wire_dtype
@@ -241,7 +245,9 @@ class ModelMixer:
         return self.ctx.world_size
 
     def _active(self) -> bool:
-        return self.ctx.is_dist and self.world > 1
+        if self.world > 1:
+            return self.ctx.is_dist
+        return self.min_world <= 1 and dist.is_available() and dist.is_initialized()
 
     # ---------------------------------------------------------------- shard-mean plan
     def plan(self, tensors: list[torch.Tensor]) -> list[_FlatGroup]:

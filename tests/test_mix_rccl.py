@@ -1,0 +1,67 @@
+"""The mixing collectives through RCCL itself.  The pool gives one GPU per box and RCCL refuses
+two ranks on one card, so this drives the real RCCL calls (all_to_all_single,
+all_gather_into_tensor, all_reduce) in a ONE-rank nccl process group, on the FFM bench's own
+state layout (bf16 V in 12-B slots + fp32 FTRL state): a one-replica mean is the identity, so
+every mix must leave the model bit-exact, and the overlapped mix must keep the progress made
+while its collectives were in flight."""
+import os
+import socket
+
+import pytest
+import torch
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_shard_mean_collectives_through_rccl_one_rank():
+    import torch.distributed as dist
+
+    from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.parallel.dist import DistContext
+    from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
+
+    assert not dist.is_initialized()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        ctx = DistContext(0, 1, 0, dev, "nccl")
+        tr = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 14 -bf16_state -seed 3",
+                        device=dev)
+        tr.init_state(1 << 14, 39)
+        st = tr.state
+        g = torch.Generator(device="cuda").manual_seed(0)
+        st["V"].copy_(torch.randn(st["V"].shape, generator=g, device=dev).to(torch.bfloat16))
+        for k in ("wz", "wn", "w"):
+            st[k].copy_(torch.randn(st[k].shape, generator=g, device=dev))
+        tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+        ref = [t.clone() for t in tensors]
+        m = ModelMixer(ctx, min_world=1)
+        m.average(tensors)                                   # all_to_all + shard mean + all_gather
+        torch.cuda.synchronize()
+        for t, r in zip(tensors, ref):
+            assert torch.equal(t, r)
+        ov = OverlappedMixer(m)
+        ov.start(tensors)                                    # collectives on the side stream
+        st["w"].add_(1.0)                                    # progress while they are in flight
+        st["V"].add_(torch.ones_like(st["V"]))
+        ov.start(tensors)                                    # finishes mix 1 (fused merge + repack)
+        ov.finish()
+        torch.cuda.synchronize()
+        assert torch.equal(st["w"], ref[3] + 1.0)
+        assert torch.equal(st["V"], (ref[0].float() + 1.0).to(torch.bfloat16))
+        x = torch.arange(10, dtype=torch.float32, device=dev)
+        m.all_reduce_sum([x])
+        assert torch.equal(x, torch.arange(10, dtype=torch.float32, device=dev))
+        assert m.all_reduce_scalar(2.5, "max") == 2.5
+        pr = m.probe(tensors, reps=2)
+        assert pr["mix_ms"] > 0 and pr["mix_payload_bytes"] > 0
+    finally:
+        dist.destroy_process_group()
