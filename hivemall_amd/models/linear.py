@@ -64,7 +64,7 @@ LEARNER_BASE_OPTS = [
         "after every pass"),
     opt("shared_waves", None, 0, int,
         "[engine] shared engine: rows in flight (0 = auto: 1024 when the hot features are "
-        "pre-aggregated per block (SGD / AdaGrad / AdaGrad-RDA general learners), else 512)"),
+        "pre-aggregated per block (AdaGrad / AdaGrad-RDA general learners), else 512)"),
 ] + CKPT_OPTS
 
 GENERAL_OPTS = [
@@ -427,10 +427,16 @@ class OnlineLinearLearner(Learner):
             t = f > 0
         return torch.nonzero(t).flatten().cpu().numpy()
 
-    def _feature_names(self, ids: np.ndarray) -> list:
+    def _feature_names(self, ids: np.ndarray, arrow: bool = False):
         if self.encoder is not None and self.encoder.mode == "dict":
             return self.encoder.decode(ids)
         if self.encoder is not None and getattr(self.encoder, "string_names", False):
+            if arrow:
+                # integer-named string features (a feature_hashing result): an Arrow string
+                # column, formatted in C++ (2.9 M names: 0.2 s, 1.2 s as Python str objects)
+                import pyarrow as pa
+
+                return pd.arrays.ArrowExtensionArray(pa.array(np.asarray(ids, dtype=np.int64)).cast(pa.string()))
             return list(map(str, ids.tolist()))
         return ids.tolist()
 
@@ -438,7 +444,7 @@ class OnlineLinearLearner(Learner):
         w, cov = self.weights()
         ids = self.touched_features()
         W = w[:, ids].cpu().numpy()
-        names = self._feature_names(ids)
+        names = self._feature_names(ids, arrow=self.TASK != "multiclass")
         C = cov[:, ids].cpu().numpy() if (cov is not None and self.covar) else None
         if self.TASK == "multiclass":
             L = len(self.labels)
