@@ -147,12 +147,18 @@ def read_table(path: str, fmt: str | None = None, columns=None, types=None,
     return _read_text(path, columns, types, field_delim, collection_delim)
 
 
-def _text_cell(v, cd: str) -> str:
+def _text_scalar(v) -> str:
     if v is None or v is pd.NA or (isinstance(v, float) and np.isnan(v)):
         return "\\N"
-    if isinstance(v, (list, tuple, np.ndarray)):
-        return cd.join("\\N" if x is None else str(x) for x in v)
+    if isinstance(v, (bool, np.bool_)):
+        return "true" if v else "false"           # Hive's boolean text
     return str(v)
+
+
+def _text_cell(v, cd: str) -> str:
+    if isinstance(v, (list, tuple, np.ndarray)):
+        return cd.join(_text_scalar(x) for x in v)
+    return _text_scalar(v)
 
 
 def write_table(df: pd.DataFrame, path: str, fmt: str | None = None, field_delim: str | None = None,
