@@ -1386,9 +1386,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 }
 
 
-// 8,192 blocks (8 per CU, 4 resident at a time) unless the batch is smaller or a grid is given
-int default_blocks(int B, int grid) {
-    return grid > 0 ? grid : (B < 256 * 8 * 4 ? B : 256 * 8 * 4);
+// 8,192 blocks (8 per CU, 4 resident at a time) unless the batch is smaller or a grid is given.
+// The bf16 12-B-slot kernel takes 32,768 (8 rows per block at the bench batch): finer blocks even
+// out the end of the launch, +1.5 % rows/s same-box (profiles/ffm_r3/grid_sweep_*.log; the fp32
+// kernel is flat to slightly slower there, logloss unchanged for both).
+int default_blocks(int B, int grid, int cap = 256 * 8 * 4) {
+    return grid > 0 ? grid : (B < cap ? B : cap);
 }
 
 // Per-element pipelined / lean dispatch (Kp == 4, packed, table < 4 GiB, F*F <= 2048); -1 when
@@ -1437,7 +1440,7 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     if (P.Kp != 4 || P.F > 45) return -1;
     if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
     const int need = (P.F * P.F + 255) / 256;
-    const int blocks = default_blocks(P.B, grid);
+    const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
     if (blocks <= 0) return 0;
 #define HM_P12(NSV) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
                                        fld, val, y, VG, w, wz, wn, bias, pred, loss)
