@@ -296,5 +296,5 @@ precision_at = udaf("precision_at", "precision")(_rank_udaf(precision_at_one))
 recall_at = udaf("recall_at", "recall")(_rank_udaf(recall_at_one))
 hitrate = udaf("hitrate")(_rank_udaf(hitrate_one))
 mrr = udaf("mrr")(_rank_udaf(mrr_one))
-average_precision = udaf("average_precision", "map")(_rank_udaf(average_precision_one))
+average_precision = udaf("average_precision")(_rank_udaf(average_precision_one))
 ndcg = udaf("ndcg")(_rank_udaf(ndcg_one))

@@ -195,6 +195,72 @@ def _get_json_object(s, path):
     return rowwise(f)(s, path)
 
 
+# ------------------------------------------------------------------ date / time
+# Hive's date functions on 'yyyy-MM-dd[ HH:mm:ss]' strings and Unix seconds.  Times are in UTC
+# (Hive uses the session's time zone; a fixed zone keeps query results reproducible).
+_JFMT = [("yyyy", "%Y"), ("yy", "%y"), ("MMMM", "%B"), ("MMM", "%b"), ("MM", "%m"), ("dd", "%d"),
+         ("HH", "%H"), ("hh", "%I"), ("mm", "%M"), ("ss", "%S"), ("EEEE", "%A"), ("EEE", "%a"),
+         ("a", "%p"), ("D", "%j")]
+_JFMT_RE = re.compile("|".join(re.escape(j) for j, _ in _JFMT))
+
+
+def _strftime_fmt(java_fmt: str) -> str:
+    """A Java SimpleDateFormat pattern (the subset Hive scripts use) as a strftime format."""
+    table = dict(_JFMT)
+    return _JFMT_RE.sub(lambda m: table[m.group(0)], str(java_fmt).replace("%", "%%"))
+
+
+def _ts(v):
+    if isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
+        return pd.Timestamp(int(v), unit="s")
+    return pd.Timestamp(str(v))
+
+
+def _date_col(fn):
+    def apply(*cols):
+        def f(*vals):
+            try:
+                return fn(*vals)
+            except (ValueError, TypeError, OverflowError):
+                return None                      # Hive: unparsable date -> NULL
+        return rowwise(f)(*cols)
+    return apply
+
+
+def _from_unixtime(s, fmt=None):
+    if fmt is None:
+        return _date_col(lambda v: pd.Timestamp(int(v), unit="s").strftime("%Y-%m-%d %H:%M:%S"))(s)
+    return _date_col(lambda v, f: pd.Timestamp(int(v), unit="s").strftime(_strftime_fmt(f)))(s, fmt)
+
+
+def _unix_timestamp(s=None, fmt=None):
+    if s is None:
+        return pd.Series([int(pd.Timestamp.now(tz="UTC").timestamp())])
+    if fmt is None:
+        return _date_col(lambda v: int(_ts(v).timestamp()))(s)
+    return _date_col(lambda v, f: int(pd.Timestamp(pd.to_datetime(str(v), format=_strftime_fmt(f))).timestamp()))(s, fmt)
+
+
+def _date_shift(sign):
+    return _date_col(lambda d, n: (_ts(d).normalize() + pd.Timedelta(days=sign * int(n))).strftime("%Y-%m-%d"))
+
+
+SCALAR_DATE = {
+    "from_unixtime": _from_unixtime, "unix_timestamp": _unix_timestamp,
+    "to_date": _date_col(lambda v: _ts(v).strftime("%Y-%m-%d")),
+    "datediff": _date_col(lambda a, b: int((_ts(a).normalize() - _ts(b).normalize()).days)),
+    "date_add": _date_shift(1), "date_sub": _date_shift(-1),
+    "year": _date_col(lambda v: _ts(v).year), "month": _date_col(lambda v: _ts(v).month),
+    "day": _date_col(lambda v: _ts(v).day), "dayofmonth": _date_col(lambda v: _ts(v).day),
+    "hour": _date_col(lambda v: _ts(v).hour), "minute": _date_col(lambda v: _ts(v).minute),
+    "second": _date_col(lambda v: _ts(v).second),
+    "weekofyear": _date_col(lambda v: int(_ts(v).isocalendar()[1])),
+    "date_format": _date_col(lambda v, f: _ts(v).strftime(_strftime_fmt(f))),
+    "current_date": lambda: pd.Series([pd.Timestamp.now(tz="UTC").strftime("%Y-%m-%d")]),
+    "current_timestamp": lambda: pd.Series([pd.Timestamp.now(tz="UTC").strftime("%Y-%m-%d %H:%M:%S")]),
+}
+
+
 SCALAR = {
     "abs": _vec_math(np.abs), "exp": _vec_math(np.exp), "ln": _vec_math(np.log),
     "log10": _vec_math(np.log10), "log2": _vec_math(np.log2), "sqrt": _vec_math(np.sqrt),
@@ -222,9 +288,7 @@ SCALAR = {
     "pmod": rowwise(lambda a, b: a % b), "isnull": lambda a: pd.Series([is_null(v) for v in a.tolist()]),
     "isnotnull": lambda a: pd.Series([not is_null(v) for v in a.tolist()]),
     "nullif": rowwise(lambda a, b: None if a == b else a, null_prop=False),
-    "unix_timestamp": lambda *a: pd.Series([int(pd.Timestamp.now().timestamp())] * (len(a[0]) if a else 1)),
-    "current_timestamp": lambda *a: pd.Series([str(pd.Timestamp.now())]),
-    "to_date": rowwise(lambda a: str(a)[:10]), "format_number": rowwise(lambda a, d: f"{float(a):,.{int(d)}f}"),
+    "format_number": rowwise(lambda a, d: f"{float(a):,.{int(d)}f}"),
     "ascii": rowwise(lambda a: ord(str(a)[0]) if str(a) else 0),
     "repeat": rowwise(lambda a, n: str(a) * int(n)), "reverse": rowwise(lambda a: str(a)[::-1] if isinstance(a, str) else list(a)[::-1]),
     "space": rowwise(lambda n: " " * int(n)),
@@ -232,6 +296,7 @@ SCALAR = {
     "rpad": rowwise(lambda a, n, p: str(a).ljust(int(n), str(p))[: int(n)]),
     "e": lambda *a: pd.Series([math.e]), "pi": lambda *a: pd.Series([math.pi]),
     "collect_array": None,
+    **SCALAR_DATE,
 }
 
 

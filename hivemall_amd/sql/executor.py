@@ -1291,8 +1291,10 @@ class Session:
         if fd is not None and fd.kind == registry.UDTF:
             raise SQLError(f"UDTF {name} must be the only expression in SELECT or used in LATERAL VIEW")
         if name in B.SCALAR and B.SCALAR[name] is not None:
-            res = B.SCALAR[name](*[_ser(a, n) for a in args]) if args else B.SCALAR[name]()
-            return _ser(res, n)
+            if not args:                # array(), current_date(), pi(): one value for every row
+                res = B.SCALAR[name]()
+                return _ser(res.iloc[0] if isinstance(res, pd.Series) and len(res) == 1 else res, n)
+            return _ser(B.SCALAR[name](*[_ser(a, n) for a in args]), n)
         if name == "sigmoid":
             x = pd.to_numeric(_ser(args[0], n), errors="coerce").to_numpy(dtype=np.float64)
             return pd.Series(1.0 / (1.0 + np.exp(-x)))

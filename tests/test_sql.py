@@ -283,3 +283,22 @@ def test_create_temporary_function_aliases():
     from hivemall_amd.sql import SQLError
     with pytest.raises(SQLError):
         s.sql("SELECT nope(1) FROM t")
+
+
+def test_hive_date_functions_and_constructors():
+    """Hive's date built-ins (UTC), zero-argument constructors broadcast to every row, and
+    ``map(...)[key]`` (Hive's map constructor, not a metric alias)."""
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"rowid": [1, 2], "d": ["2020-01-02 10:11:12", "bad"]}))
+    r = s.sql("SELECT from_unixtime(0) a, from_unixtime(86400, 'yyyy/MM/dd') b, "
+              "unix_timestamp('1970-01-01 00:00:01') c, unix_timestamp('01/02/1970', 'MM/dd/yyyy') e, "
+              "to_date(d) f, datediff('2020-01-03', '2020-01-01') g, date_add('2020-02-28', 2) h, "
+              "date_sub('2020-03-01', 1) i, year(d) y, hour(d) hh, date_format(d, 'yyyy-MM') m FROM t")
+    row = r.iloc[0].to_dict()
+    assert row == {"a": "1970-01-01 00:00:00", "b": "1970/01/02", "c": 1, "e": 86400, "f": "2020-01-02",
+                   "g": 2, "h": "2020-03-01", "i": "2020-02-29", "y": 2020, "hh": 10, "m": "2020-01"}
+    assert r["f"].iloc[1] is None and r["y"].iloc[1] is None        # unparsable -> NULL
+    r = s.sql("SELECT map('a', 1)['a'] a, size(array()) z FROM t")
+    assert r["a"].tolist() == [1, 1] and r["z"].tolist() == [0, 0]
+    r = s.sql("SELECT rowid, f FROM t LATERAL VIEW OUTER explode(array()) e AS f")
+    assert r["rowid"].tolist() == [1, 2] and r["f"].isna().all()
