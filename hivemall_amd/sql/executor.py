@@ -19,7 +19,7 @@ import logging
 import math
 import os
 import re
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 
 import numpy as np
 import pandas as pd
@@ -29,9 +29,9 @@ from . import builtins as B
 from .lexer import split_statements
 from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacro, CreateTable,
                      DescribeFunction, Drop, Expr, Field, Func, Index, InList, Insert,
-                     InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query,
+                     InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query, RenameTable,
                      Select, SelectItem, SetStmt, ShowTables, DescribeTable,
-                     ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, UnOp, Union, parse)
+                     ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, Truncate, UnOp, Union, parse)
 
 
 # Hivemall classes whose function name is not the snake_case of the class name
@@ -174,6 +174,27 @@ def _ser(v, n: int) -> pd.Series:
     if isinstance(v, (list, tuple, dict)):
         return pd.Series([v] * n, dtype=object)
     return pd.Series([v] * n, dtype=object if isinstance(v, str) or v is None else None)
+
+
+def _has_star_arg(e) -> bool:
+    return isinstance(e, Func) and any(isinstance(a, Star) or _has_star_arg(a) for a in e.args)
+
+
+def _expand_star_args(e, src: "Frame"):
+    """``f(x, *)`` -> ``f(x, c1, c2, ...)`` over the source's visible columns (``t.*``: those of
+    table alias ``t``), in order, as Hive passes them."""
+    if not isinstance(e, Func):
+        return e
+    args = []
+    for a in e.args:
+        if isinstance(a, Star):
+            cols = [(q, n) for q, n in src.cols if n != "__dummy__" and (a.table is None or q == a.table)]
+            if not cols:
+                raise SQLError(f"{a.table or ''}.* matches no column")
+            args.extend(Col(n, q) for q, n in cols)
+        else:
+            args.append(_expand_star_args(a, src))
+    return replace(e, args=args)
 
 
 def _hashable(v):
@@ -398,7 +419,9 @@ class Session:
                 return None
             if ast.view:
                 self.views[name] = ast.query
+                self.tables.pop(name, None)
                 return None
+            self.views.pop(name, None)
             if ast.query is None and ast.storage.get("location"):
                 # CREATE [EXTERNAL] TABLE ... LOCATION '<file or directory>' (io/tables.py)
                 from ..io.tables import read_table
@@ -489,6 +512,25 @@ class Session:
             self.vars[ast.key] = ast.value
             return None
         if isinstance(ast, NoOp):
+            return None
+        if isinstance(ast, Truncate):
+            n = ast.table.lower()
+            if n not in self.tables:
+                raise SQLError(f"Table not found: {ast.table}")
+            self.tables[n] = self.tables[n].iloc[:0].reset_index(drop=True)
+            return None
+        if isinstance(ast, RenameTable):
+            o, n = ast.old.lower(), ast.new.lower()
+            if n in self.tables or n in self.views:
+                raise SQLError(f"Table already exists: {ast.new}")
+            if o in self.tables:
+                self.tables[n] = self.tables.pop(o)
+                if o in self.table_meta:
+                    self.table_meta[n] = self.table_meta.pop(o)
+            elif o in self.views:
+                self.views[n] = self.views.pop(o)
+            else:
+                raise SQLError(f"Table not found: {ast.old}")
             return None
         if isinstance(ast, ShowFunctions):
             names = registry.names() + sorted(set(B.SCALAR) | set(B.AGGREGATE) | set(B.TABLE))
@@ -778,6 +820,8 @@ class Session:
             if fused is not None:
                 return fused
         src = self._source(s.source, ctes)
+        if any(_has_star_arg(it.expr) for it in s.items):
+            s = replace(s, items=[replace(it, expr=_expand_star_args(it.expr, src)) for it in s.items])
         if s.where is not None:
             src = src.take(np.nonzero(_truthy(_ser(self.eval(s.where, src, ctes), src.n)))[0])
         # UDTF in the select list

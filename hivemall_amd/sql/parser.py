@@ -252,6 +252,17 @@ class NoOp:
 
 
 @dataclass
+class Truncate:
+    table: str
+
+
+@dataclass
+class RenameTable:
+    old: str
+    new: str
+
+
+@dataclass
 class ShowFunctions:
     pattern: str | None
 
@@ -349,6 +360,17 @@ class Parser:
             q = self.set_stmt()
         elif t.kind == "ident" and t.val.lower() == "load":
             q = self.load_data()
+        elif t.kind == "ident" and t.val.lower() == "truncate":
+            self.next()
+            self.accept_kw("table")
+            q = Truncate(self.qualified_name())
+            if self.accept_kw("partition"):
+                self.error("TRUNCATE ... PARTITION is not supported (tables are unpartitioned)")
+        elif t.kind == "ident" and t.val.lower() == "alter":
+            q = self.alter()
+        elif t.kind == "ident" and t.val.lower() in ("analyze", "msck"):
+            q = NoOp(self.sql)                     # statistics / partition repair: nothing to do
+            self.i = len(self.toks) - 1
         elif t.is_kw("add", "source", "use", "reload") or (t.kind == "ident" and t.val.lower() in ("delete", "list")):
             q = NoOp(self.sql)
             self.i = len(self.toks) - 1
@@ -398,8 +420,31 @@ class Parser:
             return SetStmt(k.strip(), v.strip())
         return SetStmt(rest.strip(), None)
 
+    def alter(self):
+        """ALTER TABLE a RENAME TO b; other ALTER TABLE forms (properties, SerDe, partitions,
+        file format) describe storage that has no counterpart here and are accepted as no-ops."""
+        self.next()
+        if self.t.is_kw("table", "view"):
+            self.next()
+            name = self.qualified_name()
+            if self.t.kind == "ident" and self.t.val.lower() == "rename":
+                self.next()
+                if not (self.t.kind == "ident" and self.t.val.lower() == "to"):
+                    self.error("expected RENAME TO")
+                self.next()
+                return RenameTable(name, self.qualified_name())
+        q = NoOp(self.sql)
+        self.i = len(self.toks) - 1
+        return q
+
     def create(self):
         self.expect_kw("create")
+        if self.t.is_kw("or") and self.peek().kind == "ident" and self.peek().val.lower() == "replace":
+            self.next(); self.next()           # CREATE OR REPLACE VIEW: a CREATE replaces anyway
+        if self.t.kind == "ident" and self.t.val.lower() in ("database", "schema"):
+            q = NoOp(self.sql)                 # one namespace: databases are accepted and ignored
+            self.i = len(self.toks) - 1
+            return q
         temporary = self.accept_kw("temporary")
         self.accept_kw("external")
         if self.accept_kw("function"):
@@ -983,6 +1028,18 @@ class Parser:
             parts.append(self.next().val)
         return "".join(parts).lower()
 
+    def _arg(self) -> Expr:
+        """A call argument; ``*`` / ``t.*`` stand for every column of the source (Hive's
+        ``amplify(3, *)``), expanded by the executor."""
+        if self.t.is_op("*"):
+            self.next()
+            return Star()
+        if self.is_ident() and self.peek().is_op(".") and self.peek(2).is_op("*"):
+            tname = self.ident()
+            self.next(); self.next()
+            return Star(tname)
+        return self.expr()
+
     def _call(self, name: str) -> Func:
         self.expect_op("(")
         distinct = self.accept_kw("distinct")
@@ -992,9 +1049,9 @@ class Parser:
             self.next()
             star = True
         elif not self.t.is_op(")"):
-            args.append(self.expr())
+            args.append(self._arg())
             while self.accept_op(","):
-                args.append(self.expr())
+                args.append(self._arg())
         self.expect_op(")")
         f = Func(name.lower(), args, distinct, star)
         if self.accept_kw("over"):

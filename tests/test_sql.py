@@ -302,3 +302,26 @@ def test_hive_date_functions_and_constructors():
     assert r["a"].tolist() == [1, 1] and r["z"].tolist() == [0, 0]
     r = s.sql("SELECT rowid, f FROM t LATERAL VIEW OUTER explode(array()) e AS f")
     assert r["rowid"].tolist() == [1, 2] and r["f"].isna().all()
+
+
+def test_star_arguments_and_table_ddl():
+    """The a9a tutorial's statements: ``amplify(3, *)``, CREATE OR REPLACE VIEW, TRUNCATE,
+    ALTER TABLE ... RENAME TO, and the storage-only statements accepted as no-ops."""
+    s = Session(device="cpu")
+    s.register("train", pd.DataFrame({"rowid": [1, 2], "features": [["a:1"], ["b:2"]], "label": [1, 0]}))
+    s.sql("CREATE TABLE x3 AS SELECT amplify(3, *) AS (rowid, features, label) FROM train")
+    r = s.sql("SELECT rowid, count(*) c FROM x3 GROUP BY rowid ORDER BY rowid")
+    assert r["c"].tolist() == [3, 3]
+    r = s.sql("SELECT concat_ws('|', t.*) j FROM (SELECT cast(rowid AS string) a, 'z' b FROM train) t")
+    assert r["j"].tolist() == ["1|z", "2|z"]
+    s.sql("CREATE OR REPLACE VIEW v AS SELECT rowid FROM train WHERE label = 1")
+    s.sql("CREATE OR REPLACE VIEW v AS SELECT rowid FROM train")
+    assert len(s.sql("SELECT * FROM v")) == 2
+    s.sql("ALTER TABLE x3 RENAME TO x3b")
+    s.sql("TRUNCATE TABLE x3b")
+    assert len(s.sql("SELECT * FROM x3b")) == 0 and list(s.table("x3b").columns) == ["rowid", "features", "label"]
+    with pytest.raises(Exception):
+        s.sql("SELECT * FROM x3")
+    for q in ("CREATE DATABASE IF NOT EXISTS d", "ANALYZE TABLE x3b COMPUTE STATISTICS",
+              "ALTER TABLE x3b SET TBLPROPERTIES ('a'='b')", "MSCK REPAIR TABLE x3b"):
+        assert s.sql(q) is None
