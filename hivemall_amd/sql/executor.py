@@ -176,6 +176,34 @@ def _ser(v, n: int) -> pd.Series:
     return pd.Series([v] * n, dtype=object if isinstance(v, str) or v is None else None)
 
 
+def _peer_bounds(okey: list):
+    """First / last index of each row's peer group (equal ORDER BY keys) in a sorted partition."""
+    m = len(okey)
+    lo, hi = [0] * m, [0] * m
+    start = 0
+    for r in range(1, m + 1):
+        if r == m or okey[r] != okey[start]:
+            for q in range(start, r):
+                lo[q], hi[q] = start, r - 1
+            start = r
+    return lo, hi
+
+
+def _frame_rows(frame, r: int, m: int, peers, pos) -> tuple[int, int]:
+    """Inclusive row range [a, b] of row r's window frame in a sorted partition of m rows.
+    ROWS counts rows; RANGE takes whole peer groups (CURRENT ROW) or, with an offset, the
+    rows whose ORDER BY value lies within it (``pos``: the key in sort direction)."""
+    unit, lo, hi = frame
+    if unit == "rows":
+        return (0 if lo is None else max(0, r + lo)), (m - 1 if hi is None else min(m - 1, r + hi))
+    if pos is None:
+        return (0 if lo is None else peers[0][r]), (m - 1 if hi is None else peers[1][r])
+    x = pos[r]
+    a = 0 if lo is None else next((q for q in range(m) if pos[q] >= x + lo), m)
+    b = m - 1 if hi is None else max((q for q in range(m) if pos[q] <= x + hi), default=-1)
+    return a, b
+
+
 def _has_star_arg(e) -> bool:
     return isinstance(e, Func) and any(isinstance(a, Star) or _has_star_arg(a) for a in e.args)
 
@@ -1083,20 +1111,35 @@ class Session:
                 k = int(args[0][0])
                 for r, i in enumerate(grp):
                     out[i] = r * k // len(grp) + 1
+            elif name in ("percent_rank", "cume_dist"):
+                m = len(grp)
+                lo_, hi_ = _peer_bounds(okey)
+                for r, i in enumerate(grp):
+                    out[i] = (lo_[r] / (m - 1) if m > 1 else 0.0) if name == "percent_rank" else (hi_[r] + 1) / m
             else:
                 impl = self._lookup(name)
                 impl = impl.impl if impl is not None else B.AGGREGATE.get(name)
                 if impl is None:
                     raise SQLError(f"unknown window function {name}")
-                if w.order and name in ("sum", "count", "avg", "min", "max"):
-                    for r, i in enumerate(grp):
-                        sub = [[a[j] for j in grp[: r + 1]] for a in args]
-                        out[i] = impl(*sub) if sub else r + 1
-                else:
+                m = len(grp)
+                frame = w.frame or (("range", None, 0) if w.order else ("rows", None, None))
+                if frame[1] is None and frame[2] is None:      # the whole partition: one value
                     sub = [[a[j] for j in grp] for a in args]
-                    v = impl(*sub) if sub else len(grp)
+                    v = impl(*sub) if sub else m
                     for i in grp:
                         out[i] = v
+                    continue
+                pos = None
+                if frame[0] == "range" and any(b not in (None, 0) for b in frame[1:]):
+                    if len(okeys) != 1:
+                        raise SQLError("RANGE with an offset needs exactly one ORDER BY key")
+                    sign = 1.0 if okeys[0][1] else -1.0
+                    pos = [sign * float(okeys[0][0][i]) for i in grp]
+                peers = _peer_bounds(okey)
+                for r, i in enumerate(grp):
+                    a_, b_ = _frame_rows(frame, r, m, peers, pos)
+                    sub = [[a[grp[q]] for q in range(a_, b_ + 1)] for a in args]
+                    out[i] = impl(*sub) if sub else max(0, b_ - a_ + 1)
         return pd.Series(out, dtype=object)
 
     # -- expressions

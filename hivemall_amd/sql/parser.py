@@ -50,6 +50,10 @@ class Func(Expr):
 class Window:
     partition: list
     order: list          # [(expr, asc)]
+    # (unit "rows" | "range", start, end); offsets relative to the current row: None =
+    # unbounded, 0 = current row, -n = n preceding, +n = n following.  None = Hive's default
+    # (RANGE UNBOUNDED PRECEDING .. CURRENT ROW with ORDER BY, the whole partition without).
+    frame: tuple | None = None
 
 
 @dataclass
@@ -1028,6 +1032,23 @@ class Parser:
             parts.append(self.next().val)
         return "".join(parts).lower()
 
+    def _frame_bound(self):
+        if self.accept_kw("unbounded"):
+            if not self.t.is_kw("preceding", "following"):
+                self.error("expected PRECEDING or FOLLOWING")
+            self.next()
+            return None
+        if self.accept_kw("current"):
+            self.expect_kw("row")
+            return 0
+        if self.t.kind != "num":
+            self.error("expected a window frame bound")
+        n = int(self.next().val)
+        if self.accept_kw("preceding"):
+            return -n
+        self.expect_kw("following")
+        return n
+
     def _arg(self) -> Expr:
         """A call argument; ``*`` / ``t.*`` stand for every column of the source (Hive's
         ``amplify(3, *)``), expanded by the executor."""
@@ -1066,11 +1087,17 @@ class Parser:
                 self.next()
                 self.expect_kw("by")
                 order = self.order_list()
+            frame = None
             if self.t.is_kw("rows", "range"):
-                while not self.t.is_op(")"):
-                    self.next()
+                unit = self.next().val
+                if self.accept_kw("between"):
+                    lo = self._frame_bound()
+                    self.expect_kw("and")
+                    frame = (unit, lo, self._frame_bound())
+                else:
+                    frame = (unit, self._frame_bound(), 0)
             self.expect_op(")")
-            f.window = Window(part, order)
+            f.window = Window(part, order, frame)
         return f
 
 

@@ -325,3 +325,22 @@ def test_star_arguments_and_table_ddl():
     for q in ("CREATE DATABASE IF NOT EXISTS d", "ANALYZE TABLE x3b COMPUTE STATISTICS",
               "ALTER TABLE x3b SET TBLPROPERTIES ('a'='b')", "MSCK REPAIR TABLE x3b"):
         assert s.sql(q) is None
+
+
+def test_window_frames_follow_hive_defaults():
+    """ORDER BY without a frame = RANGE UNBOUNDED PRECEDING .. CURRENT ROW (peers included),
+    no ORDER BY = whole partition, explicit ROWS / RANGE frames, percent_rank / cume_dist."""
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"g": ["a", "a", "a", "b", "b"], "x": [1, 2, 3, 4, 5], "y": [3, 1, 2, 1, 1]}))
+    r = s.sql("SELECT sum(x) OVER (PARTITION BY g ORDER BY x) cs, sum(x) OVER (PARTITION BY g) ts, "
+              "sum(x) OVER (ORDER BY y) rs, "
+              "avg(x) OVER (PARTITION BY g ORDER BY x ROWS BETWEEN 1 PRECEDING AND 1 FOLLOWING) ma, "
+              "last_value(x) OVER (PARTITION BY g ORDER BY x) l, "
+              "count(*) OVER (ORDER BY y RANGE BETWEEN 1 PRECEDING AND CURRENT ROW) rc, "
+              "sum(x) OVER (ORDER BY x ROWS 1 PRECEDING) r1, "
+              "percent_rank() OVER (ORDER BY y) p, cume_dist() OVER (ORDER BY y) c FROM t")
+    assert r["cs"].tolist() == [1, 3, 6, 4, 9] and r["ts"].tolist() == [6, 6, 6, 9, 9]
+    assert r["rs"].tolist() == [15, 11, 14, 11, 11]
+    assert r["ma"].tolist() == [1.5, 2.0, 2.5, 4.5, 4.5] and r["l"].tolist() == [1, 2, 3, 4, 5]
+    assert r["rc"].tolist() == [2, 3, 4, 3, 3] and r["r1"].tolist() == [1, 3, 5, 7, 9]
+    assert r["p"].tolist() == [1.0, 0.0, 0.75, 0.0, 0.0] and r["c"].tolist() == [1.0, 0.6, 0.8, 0.6, 0.6]
