@@ -28,7 +28,7 @@ from .. import registry
 from . import builtins as B
 from .lexer import split_statements
 from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacro, CreateTable,
-                     DescribeFunction, Drop, Expr, Field, Func, Index, InList, Insert,
+                     DescribeFunction, Drop, Exists, Expr, Field, Func, Index, InList, Insert,
                      InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query, RenameTable,
                      Select, SelectItem, SetStmt, ShowTables, DescribeTable,
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, Truncate, UnOp, Union, parse)
@@ -652,7 +652,42 @@ class Session:
         if isinstance(e, (Lit,)):
             return True
         ch = _children(e)
-        return all(self._refs_only(c, fr) for c in ch) if ch else not isinstance(e, SubqueryExpr)
+        return all(self._refs_only(c, fr) for c in ch) if ch else not isinstance(e, (SubqueryExpr, Exists))
+
+    def _exists(self, e: Exists, fr: Frame, ctes, vals) -> pd.Series:
+        """[NOT] EXISTS (subquery).  Uncorrelated: one run.  Correlated through equality
+        conjuncts ``inner_expr = outer_expr`` in the subquery's WHERE (Hive's supported form): a
+        semi-join — the subquery runs once without them, projecting the inner keys, and each
+        outer row looks its key tuple up."""
+        body = e.query.body
+        if not isinstance(body, Select) or body.source is None:
+            return _ser(self.run_query(e.query, ctes).n > 0, fr.n)
+        qctes = dict(ctes)
+        for name, q in e.query.ctes:
+            qctes[name.lower()] = self.run_query(q, qctes)
+        inner = self._source(body.source, qctes)
+        keep, ikeys, okeys = [], [], []
+        for c in (self._split_conj(body.where) if body.where is not None else []):
+            if self._refs_only(c, inner):
+                keep.append(c)
+            elif isinstance(c, BinOp) and c.op == "=" and self._refs_only(c.left, inner) and self._refs_only(c.right, fr):
+                ikeys.append(c.left); okeys.append(c.right)
+            elif isinstance(c, BinOp) and c.op == "=" and self._refs_only(c.right, inner) and self._refs_only(c.left, fr):
+                ikeys.append(c.right); okeys.append(c.left)
+            else:
+                raise SQLError("EXISTS subquery: outer references only in equality conjuncts are supported")
+        if not ikeys:
+            return _ser(self.run_query(e.query, ctes).n > 0, fr.n)
+        where = None
+        for c in keep:
+            where = c if where is None else BinOp("and", where, c)
+        sel = replace(body, items=[SelectItem(k) for k in ikeys], where=where, order_by=[], limit=None,
+                      distinct=False)
+        sub = self.run_select(sel, qctes)
+        pool = set(zip(*[[_hashable(x) for x in sub.series(i).tolist()] for i in range(len(ikeys))]))
+        outer = [_ser(self.eval(k, fr, ctes, vals), fr.n).tolist() for k in okeys]
+        return pd.Series([not any(B.is_null(x) for x in t) and tuple(_hashable(x) for x in t) in pool
+                          for t in zip(*outer)], dtype=object)
 
     def _join(self, j: Join, ctes) -> Frame:
         if id(j) in self._prebuilt:
@@ -1202,6 +1237,8 @@ class Session:
         if isinstance(e, Cast):
             v = _ser(self.eval(e.expr, fr, ctes, vals), fr.n)
             return pd.Series([_cast_value(x, e.type) for x in v.tolist()], dtype=object).infer_objects()
+        if isinstance(e, Exists):
+            return self._exists(e, fr, ctes, vals)
         if isinstance(e, InList):
             v = _ser(self.eval(e.expr, fr, ctes, vals), fr.n).tolist()
             if len(e.items) == 1 and isinstance(e.items[0], SubqueryExpr):

@@ -124,6 +124,11 @@ class Field(Expr):
 
 
 @dataclass
+class Exists(Expr):
+    query: "Query"
+
+
+@dataclass
 class SubqueryExpr(Expr):
     query: "Query"
 
@@ -973,6 +978,12 @@ class Parser:
             e = self.expr()
             self.expect_op(")")
             return e
+        if t.is_kw("exists") and self.peek().is_op("("):
+            self.next()
+            self.next()
+            q = self.query()
+            self.expect_op(")")
+            return Exists(q)
         if t.is_kw("case"):
             self.next()
             base = None

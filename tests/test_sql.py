@@ -344,3 +344,17 @@ def test_window_frames_follow_hive_defaults():
     assert r["ma"].tolist() == [1.5, 2.0, 2.5, 4.5, 4.5] and r["l"].tolist() == [1, 2, 3, 4, 5]
     assert r["rc"].tolist() == [2, 3, 4, 3, 3] and r["r1"].tolist() == [1, 3, 5, 7, 9]
     assert r["p"].tolist() == [1.0, 0.0, 0.75, 0.0, 0.0] and r["c"].tolist() == [1.0, 0.6, 0.8, 0.6, 0.6]
+
+
+def test_exists_subqueries():
+    """[NOT] EXISTS: uncorrelated, and correlated through equality conjuncts (a semi-join)."""
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"g": ["a", "a", "b", "c"], "x": [1, 2, 3, 4]}))
+    s.register("u", pd.DataFrame({"g": ["a", "c", "c"], "y": [10, 5, 50]}))
+    q = "SELECT x FROM t WHERE {} ORDER BY x"
+    assert s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE u.g = t.g)"))["x"].tolist() == [1, 2, 4]
+    assert s.sql(q.format("NOT EXISTS (SELECT 1 FROM u WHERE u.g = t.g AND u.y > 20)"))["x"].tolist() == [1, 2, 3]
+    assert s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE y > 40)"))["x"].tolist() == [1, 2, 3, 4]
+    assert len(s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE y > 400)"))) == 0
+    with pytest.raises(Exception):
+        s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE u.y > t.x)"))
