@@ -204,6 +204,23 @@ def _frame_rows(frame, r: int, m: int, peers, pos) -> tuple[int, int]:
     return a, b
 
 
+def _null_out(e, targets: list):
+    """``e`` with every sub-expression equal to one of ``targets`` replaced by NULL."""
+    if any(e == t for t in targets):
+        return Lit(None)
+    if isinstance(e, Expr) and hasattr(e, "__dataclass_fields__"):
+        ch = {}
+        for f, v in vars(e).items():
+            if isinstance(v, Expr):
+                ch[f] = _null_out(v, targets)
+            elif isinstance(v, list):
+                ch[f] = [_null_out(x, targets) if isinstance(x, Expr) else
+                         (tuple(_null_out(y, targets) if isinstance(y, Expr) else y for y in x)
+                          if isinstance(x, tuple) else x) for x in v]
+        return replace(e, **ch) if ch else e
+    return e
+
+
 def _has_star_arg(e) -> bool:
     return isinstance(e, Func) and any(isinstance(a, Star) or _has_star_arg(a) for a in e.args)
 
@@ -876,6 +893,8 @@ class Session:
 
     # -- select
     def run_select(self, s: Select, ctes) -> Frame:
+        if s.grouping_sets is not None:
+            return self._grouping_sets(s, ctes)
         if isinstance(s.source, Join) and s.group_by:
             from .fused import try_fused
 
@@ -902,6 +921,29 @@ class Session:
             out = self._project(s.items, src, ctes, {})
             base = src
         return self._finish(out, base, s, ctes)
+
+    def _grouping_sets(self, s: Select, ctes) -> Frame:
+        """GROUPING SETS / ROLLUP / CUBE: one aggregation per key subset, the keys left out of a
+        set read as NULL in its rows, the results appended in set order (Hive's UNION ALL
+        semantics); ORDER BY / LIMIT apply to the whole."""
+        frames = []
+        for keep in s.grouping_sets:
+            dropped = [k for i, k in enumerate(s.group_by) if i not in keep]
+            sub = replace(s, grouping_sets=None, group_by=[s.group_by[i] for i in keep], order_by=[],
+                          limit=None, distinct=False,
+                          items=[replace(it, expr=_null_out(it.expr, dropped)) for it in s.items],
+                          having=None if s.having is None else _null_out(s.having, dropped))
+            if not sub.group_by and not any(_contains_agg(it.expr, self) for it in sub.items):
+                sub = replace(sub, items=sub.items + [SelectItem(Func("count", [], False, True), "__gs__")])
+                fr = self.run_select(sub, ctes)
+                fr = Frame(fr.df.iloc[:, :-1], fr.cols[:-1])
+            else:
+                fr = self.run_select(sub, ctes)
+            frames.append(fr)
+        names = [n for _, n in frames[0].cols]
+        df = pd.concat([f.to_df().set_axis(names, axis=1) for f in frames], ignore_index=True)
+        out = Frame.from_df(df)
+        return self._finish(out, out, replace(s, grouping_sets=None), ctes)
 
     def _finish(self, out: Frame, base: Frame, s: Select, ctes) -> Frame:
         if s.distinct:

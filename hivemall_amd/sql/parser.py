@@ -176,6 +176,7 @@ class Select:
     source: Any = None
     where: Expr | None = None
     group_by: list = field(default_factory=list)
+    grouping_sets: list | None = None      # [[index into group_by, ...], ...] (ROLLUP / CUBE / SETS)
     having: Expr | None = None
     order_by: list = field(default_factory=list)      # [(expr, asc)]
     cluster_by: list = field(default_factory=list)
@@ -687,6 +688,7 @@ class Parser:
             s.group_by = [self.expr()]
             while self.accept_op(","):
                 s.group_by.append(self.expr())
+            s.grouping_sets = self._grouping_sets(s.group_by)
         if self.accept_kw("having"):
             s.having = self.expr()
         while self.t.is_kw("order", "sort", "cluster", "distribute"):
@@ -1042,6 +1044,47 @@ class Parser:
                 parts.append(self.next().val)
             parts.append(self.next().val)
         return "".join(parts).lower()
+
+    def _grouping_sets(self, keys: list):
+        """``WITH ROLLUP`` / ``WITH CUBE`` / ``GROUPING SETS ((a, b), a, ())`` after a GROUP BY
+        list: the key subsets to aggregate over, as index lists into ``keys``."""
+        n = len(keys)
+        if self.t.is_kw("with") and self.peek().kind == "ident" and self.peek().val.lower() in ("rollup", "cube"):
+            self.next()
+            kind = self.next().val.lower()
+            if kind == "rollup":
+                return [list(range(k)) for k in range(n, -1, -1)]
+            return [[i for i in range(n) if m >> (n - 1 - i) & 1] for m in range((1 << n) - 1, -1, -1)]
+        if not (self.t.kind == "ident" and self.t.val.lower() == "grouping"):
+            return None
+        self.next()
+        if not (self.t.kind == "ident" and self.t.val.lower() == "sets"):
+            self.error("expected GROUPING SETS")
+        self.next()
+        self.expect_op("(")
+
+        def key_index(e):
+            for i, k in enumerate(keys):
+                if k == e:
+                    return i
+            self.error("a grouping set may only name GROUP BY expressions")
+
+        sets = []
+        while True:
+            if self.accept_op("("):
+                cur = []
+                if not self.t.is_op(")"):
+                    cur.append(key_index(self.expr()))
+                    while self.accept_op(","):
+                        cur.append(key_index(self.expr()))
+                self.expect_op(")")
+            else:
+                cur = [key_index(self.expr())]
+            sets.append(sorted(set(cur)))
+            if not self.accept_op(","):
+                break
+        self.expect_op(")")
+        return sets
 
     def _frame_bound(self):
         if self.accept_kw("unbounded"):

@@ -358,3 +358,14 @@ def test_exists_subqueries():
     assert len(s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE y > 400)"))) == 0
     with pytest.raises(Exception):
         s.sql(q.format("EXISTS (SELECT 1 FROM u WHERE u.y > t.x)"))
+
+
+def test_rollup_cube_grouping_sets():
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"g": ["a", "a", "b", "b"], "h": ["x", "y", "x", "x"], "v": [1, 2, 3, 4]}))
+    r = s.sql("SELECT g, h, sum(v) s FROM t GROUP BY g, h WITH ROLLUP")
+    assert r["s"].tolist() == [1, 2, 7, 3, 7, 10] and r["h"].isna().tolist()[3:] == [True] * 3
+    r = s.sql("SELECT g, h, count(*) c FROM t GROUP BY g, h WITH CUBE")
+    assert len(r) == 8 and r["c"].iloc[-1] == 4 and r["c"].sum() == 16
+    r = s.sql("SELECT g, sum(v) s FROM t GROUP BY g, h GROUPING SETS ((g, h), g, ()) ORDER BY s DESC LIMIT 2")
+    assert r["s"].tolist() == [10, 7] and pd.isna(r["g"].iloc[0])
