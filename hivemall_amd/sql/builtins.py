@@ -137,11 +137,47 @@ def _rand(seed=None, n=None):
     return pd.Series(rng.random(n))
 
 
+def _i32(h: int) -> int:
+    h &= 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def hive_hash_code(v) -> int:
+    """Hive's per-type hash code (``ObjectInspectorUtils.hashCode``): int -> itself, bigint ->
+    ``(int)(v ^ v >>> 32)``, double -> ``Double.hashCode``, string -> the 31-polynomial over its
+    UTF-8 bytes (signed), boolean -> 1/0, NULL -> 0, arrays -> 31-polynomial of the elements.
+    Deterministic across processes (no salted Python hash)."""
+    if v is None:
+        return 0
+    if isinstance(v, (bool, np.bool_)):
+        return 1 if v else 0
+    if isinstance(v, (int, np.integer)):
+        v = int(v)
+        if -(1 << 31) <= v < (1 << 31):
+            return v
+        u = v & 0xFFFFFFFFFFFFFFFF
+        return _i32(u ^ (u >> 32))
+    if isinstance(v, (float, np.floating)):
+        import struct
+
+        u = struct.unpack(">q", struct.pack(">d", float(v)))[0] & 0xFFFFFFFFFFFFFFFF
+        return _i32(u ^ (u >> 32))
+    if isinstance(v, (list, tuple, np.ndarray)):
+        h = 0
+        for x in v:
+            h = _i32(31 * h + hive_hash_code(x))
+        return h
+    h = 0
+    for b in str(v).encode("utf-8"):
+        h = _i32(31 * h + (b - 256 if b > 127 else b))
+    return h
+
+
 def _hash(*cols):
     def f(*vals):
         h = 0
         for v in vals:
-            h = (h * 31 + (hash(str(v)) & 0x7FFFFFFF)) & 0x7FFFFFFF
+            h = _i32(31 * h + hive_hash_code(None if is_null(v) else v))
         return h
     return rowwise(f, null_prop=False)(*cols)
 

@@ -642,17 +642,39 @@ class Session:
             n = src.name.lower()
             alias = src.alias or src.name.split(".")[-1]
             if n in ctes:
-                return Frame.from_df(ctes[n], alias)
-            if n in self.views:
-                return self.run_query(self.views[n], ctes).requalify(alias)
-            return Frame.from_df(self.table(n), alias)
+                fr = Frame.from_df(ctes[n], alias)
+            elif n in self.views:
+                fr = self.run_query(self.views[n], ctes).requalify(alias)
+            else:
+                fr = Frame.from_df(self.table(n), alias)
+            return self._sample(fr, src.sample, ctes) if src.sample else fr
         if isinstance(src, SubqueryRef):
-            return self.run_query(src.query, ctes).requalify(src.alias)
+            fr = self.run_query(src.query, ctes).requalify(src.alias)
+            return self._sample(fr, src.sample, ctes) if src.sample else fr
         if isinstance(src, Join):
             return self._join(src, ctes)
         if isinstance(src, LateralView):
             return self._lateral(src, ctes)
         raise SQLError(f"bad FROM item {src}")
+
+    def _sample(self, fr: Frame, spec: tuple, ctes) -> Frame:
+        """TABLESAMPLE.  BUCKET x OUT OF y ON expr keeps the rows whose Hive hash of expr is
+        x - 1 mod y (``ON rand()`` a seeded random split; no ON: by row position, as for a
+        table without buckets).  n PERCENT / n ROWS keep a prefix (Hive samples whole input
+        splits, so its rows are a prefix of each split too)."""
+        kind = spec[0]
+        if kind == "rows":
+            return fr.take(np.arange(min(spec[1], fr.n)))
+        if kind == "percent":
+            return fr.take(np.arange(min(fr.n, int(math.ceil(fr.n * spec[1] / 100.0)))))
+        _, x, y, on = spec
+        if on is None:
+            h = np.arange(fr.n, dtype=np.int64)
+        else:
+            h = np.array([B.hive_hash_code(None if B.is_null(v) else v)
+                          for v in _ser(self.eval(on, fr, ctes), fr.n).tolist()], dtype=np.int64)
+            h = h & 0x7FFFFFFF
+        return fr.take(np.nonzero(h % y == x - 1)[0])
 
     # -- joins
     def _split_conj(self, e):

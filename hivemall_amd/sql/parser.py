@@ -145,12 +145,14 @@ class SelectItem:
 class TableRef:
     name: str
     alias: str | None = None
+    sample: tuple | None = None     # TABLESAMPLE: ("bucket", x, y, expr|None) | ("percent", p) | ("rows", n)
 
 
 @dataclass
 class SubqueryRef:
     query: "Query"
     alias: str | None = None
+    sample: tuple | None = None
 
 
 @dataclass
@@ -819,15 +821,17 @@ class Parser:
             if self.t.is_kw("select", "with") or self.t.is_op("("):
                 q = self.query()
                 self.expect_op(")")
+                sample = self._tablesample()
                 alias = None
                 self.accept_kw("as")
                 if self.is_ident():
                     alias = self.ident()
-                return SubqueryRef(q, alias)
+                return SubqueryRef(q, alias, sample)
             f = self.from_clause()
             self.expect_op(")")
             return f
         name = self.qualified_name()
+        sample = self._tablesample()
         alias = None
         if self.accept_kw("as"):
             alias = self.ident()
@@ -835,7 +839,40 @@ class Parser:
                                                   "join", "where", "group", "order", "on", "limit",
                                                   "sort", "cluster", "distribute", "having", "union"):
             alias = self.ident()
-        return TableRef(name, alias)
+        return TableRef(name, alias, sample)
+
+    def _tablesample(self):
+        """TABLESAMPLE (BUCKET x OUT OF y [ON expr]) | (n PERCENT) | (n ROWS)."""
+        if not (self.t.kind == "ident" and self.t.val.lower() == "tablesample"):
+            return None
+        self.next()
+        self.expect_op("(")
+        if self.t.kind == "ident" and self.t.val.lower() == "bucket":
+            self.next()
+            x = int(self.next().val)
+            if not (self.t.kind == "ident" and self.t.val.lower() == "out"):
+                self.error("expected OUT OF")
+            self.next()
+            if not self.accept_kw("of"):
+                if not (self.t.kind == "ident" and self.t.val.lower() == "of"):
+                    self.error("expected OUT OF")
+                self.next()
+            y = int(self.next().val)
+            if not 1 <= x <= y:
+                self.error("TABLESAMPLE bucket must be in 1..y")
+            on = self.expr() if self.accept_kw("on") else None
+            self.expect_op(")")
+            return ("bucket", x, y, on)
+        if self.t.kind != "num":
+            self.error("expected BUCKET, n PERCENT or n ROWS")
+        v = self.next().val
+        unit = self.next().val.lower()
+        self.expect_op(")")
+        if unit == "percent":
+            return ("percent", float(v))
+        if unit == "rows":
+            return ("rows", int(v))
+        self.error("expected PERCENT or ROWS")
 
     # -- expressions (precedence climbing)
     def expr(self) -> Expr:

@@ -369,3 +369,17 @@ def test_rollup_cube_grouping_sets():
     assert len(r) == 8 and r["c"].iloc[-1] == 4 and r["c"].sum() == 16
     r = s.sql("SELECT g, sum(v) s FROM t GROUP BY g, h GROUPING SETS ((g, h), g, ()) ORDER BY s DESC LIMIT 2")
     assert r["s"].tolist() == [10, 7] and pd.isna(r["g"].iloc[0])
+
+
+def test_tablesample_and_hive_hash():
+    """TABLESAMPLE(BUCKET x OUT OF y ON e | n PERCENT | n ROWS) and Hive's deterministic
+    hash() (Java hash codes: ints themselves, strings the 31-polynomial of their bytes)."""
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"id": range(10), "k": list("abcdeabcde")}))
+    assert s.sql("SELECT id FROM t TABLESAMPLE(BUCKET 1 OUT OF 2 ON id) s")["id"].tolist() == [0, 2, 4, 6, 8]
+    assert s.sql("SELECT id FROM t TABLESAMPLE(30 PERCENT)")["id"].tolist() == [0, 1, 2]
+    assert s.sql("SELECT id FROM t TABLESAMPLE(2 ROWS) x")["id"].tolist() == [0, 1]
+    parts = [set(s.sql(f"SELECT id FROM t TABLESAMPLE(BUCKET {b} OUT OF 3 ON k)")["id"]) for b in (1, 2, 3)]
+    assert set().union(*parts) == set(range(10)) and sum(map(len, parts)) == 10
+    r = s.sql("SELECT hash('hello') a, hash(1, 'a') b, hash(cast(1.5 AS double)) c FROM t LIMIT 1")
+    assert r.iloc[0].tolist() == [99162322, 128, 1073217536]
