@@ -297,6 +297,174 @@ SCALAR_DATE = {
 }
 
 
+# ------------------------------------------------------------------ more Hive string / math UDFs
+def _conv(v, fb, tb):
+    """conv(num, from_base, to_base): base conversion of an integer string (Hive: negative
+    to_base = signed output; invalid digits end the number)."""
+    digits = "0123456789abcdefghijklmnopqrstuvwxyz"
+    fb, tb = int(fb), int(tb)
+    txt = str(v).strip().lower()
+    neg = txt.startswith("-")
+    n = 0
+    for ch in txt[1:] if neg else txt:
+        d = digits.find(ch)
+        if d < 0 or d >= abs(fb):
+            break
+        n = n * abs(fb) + d
+    if neg:
+        n = -n
+    if tb > 0 and n < 0:
+        n &= 0xFFFFFFFFFFFFFFFF                 # Hive prints the unsigned 64-bit pattern
+    if n == 0:
+        return "0"
+    out, m = [], abs(n)
+    while m:
+        out.append(digits[m % abs(tb)])
+        m //= abs(tb)
+    return ("-" if n < 0 else "") + "".join(reversed(out)).upper()
+
+
+def _soundex(v):
+    s = "".join(c for c in str(v).upper() if c.isalpha())
+    if not s:
+        return ""
+    codes = {**dict.fromkeys("BFPV", "1"), **dict.fromkeys("CGJKQSXZ", "2"), **dict.fromkeys("DT", "3"),
+             "L": "4", **dict.fromkeys("MN", "5"), "R": "6"}
+    out, prev = s[0], codes.get(s[0], "")
+    for c in s[1:]:
+        d = codes.get(c, "")
+        if d and d != prev:
+            out += d
+        if c not in "HW":
+            prev = d
+    return (out + "000")[:4]
+
+
+def _levenshtein(a, b):
+    a, b = str(a), str(b)
+    prev = list(range(len(b) + 1))
+    for i, ca in enumerate(a, 1):
+        cur = [i]
+        for j, cb in enumerate(b, 1):
+            cur.append(min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (ca != cb)))
+        prev = cur
+    return prev[-1]
+
+
+def _parse_url(url, part, key=None):
+    from urllib.parse import parse_qs, urlsplit
+
+    u = urlsplit(str(url))
+    p = str(part).upper()
+    if p == "QUERY" and key is not None:
+        vals = parse_qs(u.query, keep_blank_values=True).get(str(key))
+        return vals[0] if vals else None
+    return {"HOST": u.hostname, "PATH": u.path, "QUERY": u.query or None, "REF": u.fragment or None,
+            "PROTOCOL": u.scheme or None, "FILE": (u.path + ("?" + u.query if u.query else "")) or None,
+            "AUTHORITY": u.netloc or None, "USERINFO": (u.netloc.rpartition("@")[0] or None)}.get(p)
+
+
+def _add_months(d, n):
+    t = _ts(d)
+    m = t.month - 1 + int(n)
+    y, m = t.year + m // 12, m % 12 + 1
+    last = pd.Timestamp(year=y, month=m, day=1).days_in_month
+    day = last if t.day == t.days_in_month else min(t.day, last)
+    return pd.Timestamp(year=y, month=m, day=day).strftime("%Y-%m-%d")
+
+
+def _months_between(a, b):
+    ta, tb = _ts(a), _ts(b)
+    if ta.day == tb.day or (ta.day == ta.days_in_month and tb.day == tb.days_in_month):
+        return float((ta.year - tb.year) * 12 + ta.month - tb.month)
+    secs = lambda t: (t.day - 1) * 86400 + t.hour * 3600 + t.minute * 60 + t.second
+    return round((ta.year - tb.year) * 12 + ta.month - tb.month + (secs(ta) - secs(tb)) / (31 * 86400.0), 8)
+
+
+_DOW = {"MO": 0, "TU": 1, "WE": 2, "TH": 3, "FR": 4, "SA": 5, "SU": 6}
+
+
+def _next_day(d, dow):
+    t = _ts(d).normalize()
+    w = _DOW[str(dow).strip().upper()[:2]]
+    return (t + pd.Timedelta(days=(w - t.dayofweek - 1) % 7 + 1)).strftime("%Y-%m-%d")
+
+
+def _trunc_date(d, fmt):
+    t = _ts(d)
+    f = str(fmt).upper()
+    if f in ("MONTH", "MON", "MM"):
+        return t.replace(day=1).strftime("%Y-%m-%d")
+    if f in ("YEAR", "YYYY", "YY"):
+        return t.replace(month=1, day=1).strftime("%Y-%m-%d")
+    if f in ("QUARTER", "Q"):
+        return t.replace(month=3 * ((t.month - 1) // 3) + 1, day=1).strftime("%Y-%m-%d")
+    return None
+
+
+def _bround(s, d=None):
+    dd = 0 if d is None else int(d.iloc[0])
+    return pd.Series(np.round(_num(s).to_numpy(dtype=np.float64), dd))      # numpy rounds half-even
+
+
+def _translate(v, frm, to):
+    frm, to = str(frm), str(to)
+    table = {}
+    for i, c in enumerate(frm):
+        if c not in table:
+            table[c] = to[i] if i < len(to) else None
+    return "".join(table.get(c, c) or "" for c in str(v))
+
+
+def _printf(fmt, *vals):
+    return str(fmt) % tuple(vals)            # Java's %s / %d / %f / %x / %e behave the same
+
+
+def _sentences(v, *_):
+    out = []
+    for sent in re.split(r"(?<=[.!?])\s+", str(v).strip()):
+        words = re.findall(r"[\w']+", sent)
+        if words:
+            out.append(words)
+    return out
+
+
+SCALAR_MORE = {
+    "conv": rowwise(_conv), "bin": rowwise(lambda a: format(int(a) & 0xFFFFFFFFFFFFFFFF if int(a) < 0 else int(a), "b")),
+    "hex": rowwise(lambda a: (format(int(a) & 0xFFFFFFFFFFFFFFFF, "X") if isinstance(a, (int, np.integer))
+                              else str(a).encode().hex().upper())),
+    "unhex": rowwise(lambda a: bytes.fromhex(str(a)).decode("utf-8", "replace")),
+    "base64": rowwise(lambda a: __import__("base64").b64encode(a if isinstance(a, bytes) else str(a).encode()).decode()),
+    "unbase64": rowwise(lambda a: __import__("base64").b64decode(str(a)).decode("utf-8", "replace")),
+    "decode": rowwise(lambda a, cs: (a if isinstance(a, bytes) else str(a).encode()).decode(str(cs))),
+    "encode": rowwise(lambda a, cs: str(a).encode(str(cs))),
+    "translate": rowwise(_translate), "initcap": rowwise(lambda a: " ".join(w.capitalize() for w in str(a).split(" "))),
+    "levenshtein": rowwise(_levenshtein), "soundex": rowwise(_soundex),
+    "str_to_map": rowwise(lambda a, d1=",", d2=":": {k: v for k, _, v in (p.partition(str(d2)) for p in str(a).split(str(d1)))}),
+    "find_in_set": rowwise(lambda a, lst: (str(lst).split(",").index(str(a)) + 1) if "," not in str(a) and str(a) in str(lst).split(",") else 0),
+    "locate": rowwise(lambda sub, a, pos=1: str(a).find(str(sub), int(pos) - 1) + 1),
+    "field": rowwise(lambda a, *xs: next((i + 1 for i, x in enumerate(xs) if x == a), 0), null_prop=False),
+    "elt": rowwise(lambda n, *xs: xs[int(n) - 1] if 1 <= int(n) <= len(xs) else None),
+    "char_length": rowwise(lambda a: len(str(a))), "character_length": rowwise(lambda a: len(str(a))),
+    "octet_length": rowwise(lambda a: len(str(a).encode("utf-8"))),
+    "parse_url": rowwise(_parse_url), "sentences": rowwise(_sentences),
+    "printf": rowwise(_printf), "sha2": rowwise(lambda a, bits: hashlib.new(f"sha{int(bits) if int(bits) != 0 else 256}", str(a).encode()).hexdigest()),
+    "crc32": rowwise(lambda a: __import__("zlib").crc32(str(a).encode())),
+    "factorial": rowwise(lambda a: math.factorial(int(a)) if 0 <= int(a) <= 20 else None),
+    "bround": _bround, "cbrt": _vec_math(np.cbrt), "degrees": _vec_math(np.degrees),
+    "radians": _vec_math(np.radians), "asin": _vec_math(np.arcsin), "acos": _vec_math(np.arccos),
+    "shiftleft": rowwise(lambda a, n: _i32(int(a) << int(n))), "shiftright": rowwise(lambda a, n: int(a) >> int(n)),
+    "positive": rowwise(lambda a: a), "negative": rowwise(lambda a: -a), "mod": rowwise(lambda a, b: math.fmod(a, b) if isinstance(a, float) or isinstance(b, float) else int(math.fmod(a, b))),
+    "quarter": _date_col(lambda v: (_ts(v).month - 1) // 3 + 1),
+    "last_day": _date_col(lambda v: _ts(v).replace(day=_ts(v).days_in_month).strftime("%Y-%m-%d")),
+    "add_months": _date_col(_add_months), "months_between": _date_col(_months_between),
+    "next_day": _date_col(_next_day), "trunc": _date_col(_trunc_date),
+    "current_user": lambda: pd.Series([__import__("getpass").getuser()]),
+    "current_database": lambda: pd.Series(["default"]),
+    "uuid": lambda: pd.Series([str(__import__("uuid").uuid4())]),
+}
+
+
 SCALAR = {
     "abs": _vec_math(np.abs), "exp": _vec_math(np.exp), "ln": _vec_math(np.log),
     "log10": _vec_math(np.log10), "log2": _vec_math(np.log2), "sqrt": _vec_math(np.sqrt),
@@ -333,12 +501,46 @@ SCALAR = {
     "e": lambda *a: pd.Series([math.e]), "pi": lambda *a: pd.Series([math.pi]),
     "collect_array": None,
     **SCALAR_DATE,
+    **SCALAR_MORE,
 }
 
 
 # ------------------------------------------------------------------ aggregates
 def _vals(c):
     return [v for v in c if not is_null(v)]
+
+
+def _pairs(a, b):
+    """The (a, b) pairs with neither side NULL, as float arrays (Hive's bivariate aggregates)."""
+    keep = [(x, y) for x, y in zip(a, b) if not is_null(x) and not is_null(y)]
+    if not keep:
+        return None
+    arr = np.asarray(keep, dtype=np.float64)
+    return arr[:, 0], arr[:, 1]
+
+
+def _covar(a, b, ddof):
+    p = _pairs(a, b)
+    if p is None or len(p[0]) <= ddof:
+        return None
+    return float(np.cov(p[0], p[1], ddof=ddof)[0, 1]) if len(p[0]) > 1 else 0.0
+
+
+def _histogram_numeric(c, nb):
+    """histogram_numeric(col, b): b (x, y) bin centres and heights, built as Hive does — one
+    bin per value, the two closest bins merged until b remain (Ben-Haim & Tom-Tov)."""
+    b = int(nb[0]) if isinstance(nb, (list, tuple, pd.Series)) else int(nb)
+    bins: list = []
+    for v in sorted(float(x) for x in _vals(c)):
+        if bins and bins[-1][0] == v:
+            bins[-1][1] += 1.0
+        else:
+            bins.append([v, 1.0])
+    while len(bins) > b:
+        i = min(range(len(bins) - 1), key=lambda k: bins[k + 1][0] - bins[k][0])
+        (x1, y1), (x2, y2) = bins[i], bins[i + 1]
+        bins[i:i + 2] = [[(x1 * y1 + x2 * y2) / (y1 + y2), y1 + y2]]
+    return [{"x": x, "y": y} for x, y in bins]
 
 
 def _percentile(c, p):
@@ -371,6 +573,12 @@ AGGREGATE = {
     "first": lambda c: c[0] if len(c) else None, "first_value": lambda c: c[0] if len(c) else None,
     "last": lambda c: c[-1] if len(c) else None, "last_value": lambda c: c[-1] if len(c) else None,
     "corr": lambda a, b: float(np.corrcoef(np.asarray(a, float), np.asarray(b, float))[0, 1]),
+    "covar_pop": lambda a, b: _covar(a, b, 0), "covar_samp": lambda a, b: _covar(a, b, 1),
+    "regr_slope": lambda y, x: (lambda p: None if p is None or p[1].var() == 0 else
+                                float(np.cov(p[0], p[1], ddof=0)[0, 1] / p[1].var()))(_pairs(y, x)),
+    "regr_intercept": lambda y, x: (lambda p: None if p is None or p[1].var() == 0 else
+                                    float(p[0].mean() - np.cov(p[0], p[1], ddof=0)[0, 1] / p[1].var() * p[1].mean()))(_pairs(y, x)),
+    "histogram_numeric": lambda c, nb: _histogram_numeric(c, nb),
 }
 
 # fast pandas paths for the common numeric aggregates
@@ -418,7 +626,21 @@ def json_tuple(js, *keys):
     yield tuple(None if d.get(k) is None else str(d.get(k)) for k in keys)
 
 
+def parse_url_tuple(url, *parts):
+    if is_null(url):
+        yield tuple(None for _ in parts)
+        return
+    out = []
+    for p in parts:
+        p = str(p)
+        if p.upper().startswith("QUERY:"):
+            out.append(_parse_url(url, "QUERY", p.split(":", 1)[1]))
+        else:
+            out.append(_parse_url(url, p))
+    yield tuple(out)
+
+
 TABLE = {"explode": explode, "posexplode": posexplode, "inline": inline, "stack": stack,
-         "json_tuple": json_tuple}
+         "json_tuple": json_tuple, "parse_url_tuple": parse_url_tuple}
 TABLE_COLS = {"explode": ("col",), "posexplode": ("pos", "val"), "inline": None, "stack": None,
-              "json_tuple": None}
+              "json_tuple": None, "parse_url_tuple": None}

@@ -383,3 +383,23 @@ def test_tablesample_and_hive_hash():
     assert set().union(*parts) == set(range(10)) and sum(map(len, parts)) == 10
     r = s.sql("SELECT hash('hello') a, hash(1, 'a') b, hash(cast(1.5 AS double)) c FROM t LIMIT 1")
     assert r.iloc[0].tolist() == [99162322, 128, 1073217536]
+
+
+def test_more_hive_builtins():
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"x": [1.0, 2.0, 3.0, 10.0], "y": [2.0, 4.1, 6.0, 20.5], "d": ["2020-01-31"] * 4}))
+    r = s.sql("SELECT conv('ff', 16, 10) a, conv('-1', 10, 16) b, hex('ab') c, unbase64(base64('hi')) e, "
+              "translate('hello', 'el', 'ip') f, levenshtein('kitten', 'sitting') g, soundex('Robert') h, "
+              "find_in_set('b', 'a,b,c') i, str_to_map('a:1,b:2')['b'] j, "
+              "parse_url('http://h.com/p?q=1&r=2', 'QUERY', 'r') k, printf('%s-%03d', 'x', 7) l, "
+              "crc32('abc') m, add_months(d, 1) n, last_day('2020-02-10') o, next_day('2020-01-01', 'MO') p, "
+              "trunc('2020-05-17', 'MM') q FROM t LIMIT 1").iloc[0].to_dict()
+    assert r == {"a": "255", "b": "FFFFFFFFFFFFFFFF", "c": "6162", "e": "hi", "f": "hippo", "g": 3, "h": "R163",
+                 "i": 2, "j": "2", "k": "2", "l": "x-007", "m": 891568578, "n": "2020-02-29", "o": "2020-02-29",
+                 "p": "2020-01-06", "q": "2020-05-01"}
+    r = s.sql("SELECT covar_pop(x, y) a, covar_samp(x, y) b, histogram_numeric(x, 2) h FROM t").iloc[0]
+    assert abs(r["a"] - 25.7) < 1e-9 and abs(r["b"] - 34.2666666667) < 1e-6
+    assert r["h"] == [{"x": 2.0, "y": 3.0}, {"x": 10.0, "y": 1.0}]
+    r = s.sql("SELECT p.host, p.path FROM t LATERAL VIEW parse_url_tuple('http://h.com/p?q=1', 'HOST', 'PATH') p "
+              "AS host, path LIMIT 1")
+    assert r.iloc[0].tolist() == ["h.com", "/p"]
