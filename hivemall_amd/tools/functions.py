@@ -569,7 +569,8 @@ class _Ctx:
     job_id = "hivemall_amd"
     conf: dict = {}
     distcache: dict = {}
-    row = 0
+    row = 0          # rowid()'s sequence
+    rownum = 0       # rownum()'s sequence (a separate UDF instance in Hive, so its own counter)
 
 
 CONTEXT = _Ctx()
@@ -584,8 +585,10 @@ def rowid():
 
 @udf("rownum")
 def rownum():
-    CONTEXT.row += 1
-    return (CONTEXT.task_id << 40) + CONTEXT.row
+    """Hivemall's ``sprintf("%d%04d", sequence, taskid)`` as a long: unique per task while the
+    task id stays below 10,000."""
+    CONTEXT.rownum += 1
+    return int(f"{CONTEXT.rownum}{CONTEXT.task_id:04d}")
 
 
 @udf("taskid")

@@ -403,3 +403,16 @@ def test_more_hive_builtins():
     r = s.sql("SELECT p.host, p.path FROM t LATERAL VIEW parse_url_tuple('http://h.com/p?q=1', 'HOST', 'PATH') p "
               "AS host, path LIMIT 1")
     assert r.iloc[0].tolist() == ["h.com", "/p"]
+
+
+def test_rowid_and_rownum_sequences():
+    """rowid() and rownum() keep separate sequences (separate UDF instances in Hive);
+    rownum() = sequence followed by the 4-digit task id."""
+    from hivemall_amd.tools.functions import CONTEXT
+
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"x": [1, 2, 3]}))
+    r0, n0 = CONTEXT.row, CONTEXT.rownum
+    r = s.sql("SELECT rowid() a, rownum() b FROM t")
+    assert r["a"].tolist() == [f"{CONTEXT.task_id}-{r0 + i}" for i in (1, 2, 3)]
+    assert r["b"].tolist() == [int(f"{n0 + i}{CONTEXT.task_id:04d}") for i in (1, 2, 3)]
