@@ -29,7 +29,7 @@ from . import builtins as B
 from .lexer import split_statements
 from .parser import (Between, BinOp, Case, Cast, Col, CreateFunction, CreateMacro, CreateTable,
                      DescribeFunction, Drop, Exists, Expr, Field, Func, Index, InList, Insert,
-                     InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, NoOp, Query, RenameTable,
+                     InsertDirectory, IsNull, Join, LateralView, Like, Lit, LoadData, MultiInsert, NoOp, Query, RenameTable,
                      Select, SelectItem, SetStmt, ShowTables, DescribeTable,
                      ShowFunctions, Star, SubqueryExpr, SubqueryRef, TableRef, Truncate, UnOp, Union, parse)
 
@@ -557,6 +557,10 @@ class Session:
             self.vars[ast.key] = ast.value
             return None
         if isinstance(ast, NoOp):
+            return None
+        if isinstance(ast, MultiInsert):
+            for ins in ast.inserts:
+                self._exec(ins)
             return None
         if isinstance(ast, Truncate):
             n = ast.table.lower()

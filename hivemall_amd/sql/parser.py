@@ -264,6 +264,11 @@ class NoOp:
 
 
 @dataclass
+class MultiInsert:
+    inserts: list       # Insert / InsertDirectory statements sharing one FROM source
+
+
+@dataclass
 class Truncate:
     table: str
 
@@ -366,6 +371,8 @@ class Parser:
             q = self.create()
         elif t.is_kw("insert"):
             q = self.insert()
+        elif t.is_kw("from"):
+            q = self.from_first()
         elif t.is_kw("drop"):
             q = self.drop()
         elif t.is_kw("set"):
@@ -572,6 +579,32 @@ class Parser:
         self.expect_kw("into")
         self.expect_kw("table")
         return LoadData(path, self.qualified_name(), overwrite)
+
+    def from_first(self):
+        """Hive's FROM-first forms: ``FROM src SELECT ...`` and the multi-insert
+        ``FROM src INSERT OVERWRITE TABLE a SELECT ... INSERT INTO TABLE b SELECT ...``."""
+        self.expect_kw("from")
+        src = self.from_clause()
+
+        def bind(q):
+            body = q.body
+            if not isinstance(body, Select):
+                self.error("FROM ... INSERT: each branch must be a single SELECT")
+            if body.source is not None:
+                self.error("FROM ... INSERT: a branch may not have its own FROM")
+            body.source = src
+            return q
+
+        if self.t.is_kw("select"):
+            return bind(Query(self.select(), []))
+        inserts = []
+        while self.t.is_kw("insert"):
+            ins = self.insert()
+            bind(ins.query)
+            inserts.append(ins)
+        if not inserts:
+            self.error("expected INSERT or SELECT after FROM")
+        return inserts[0] if len(inserts) == 1 else MultiInsert(inserts)
 
     def insert(self):
         self.expect_kw("insert")
@@ -837,7 +870,8 @@ class Parser:
             alias = self.ident()
         elif self.is_ident() and not self.t.is_kw("lateral", "left", "right", "full", "cross", "inner",
                                                   "join", "where", "group", "order", "on", "limit",
-                                                  "sort", "cluster", "distribute", "having", "union"):
+                                                  "sort", "cluster", "distribute", "having", "union",
+                                                  "insert", "select"):
             alias = self.ident()
         return TableRef(name, alias, sample)
 

@@ -416,3 +416,15 @@ def test_rowid_and_rownum_sequences():
     r = s.sql("SELECT rowid() a, rownum() b FROM t")
     assert r["a"].tolist() == [f"{CONTEXT.task_id}-{r0 + i}" for i in (1, 2, 3)]
     assert r["b"].tolist() == [int(f"{n0 + i}{CONTEXT.task_id:04d}") for i in (1, 2, 3)]
+
+
+def test_from_first_multi_insert():
+    """Hive's ``FROM src INSERT ... SELECT ... INSERT ... SELECT ...`` and ``FROM src SELECT``."""
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"x": [1, 2, 3, 4], "g": ["a", "b", "a", "b"]}))
+    s.sql("CREATE TABLE big (x int)")
+    s.sql("FROM t INSERT OVERWRITE TABLE small SELECT x WHERE x < 3 "
+          "INSERT INTO TABLE big SELECT x WHERE x >= 3 INSERT OVERWRITE TABLE agg SELECT g, sum(x) s GROUP BY g")
+    assert s.table("small")["x"].tolist() == [1, 2] and s.table("big")["x"].tolist() == [3, 4]
+    assert sorted(s.table("agg").itertuples(index=False, name=None)) == [("a", 4), ("b", 6)]
+    assert s.sql("FROM t SELECT max(x) m")["m"].tolist() == [4]
