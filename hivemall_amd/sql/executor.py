@@ -176,6 +176,31 @@ def _ser(v, n: int) -> pd.Series:
     return pd.Series([v] * n, dtype=object if isinstance(v, str) or v is None else None)
 
 
+def _running_agg(name: str, vals, m: int) -> list:
+    """Prefix sum / count / avg / min / max over a sorted partition, NULLs skipped."""
+    out, cnt, acc = [], 0, None
+    for r in range(m):
+        v = None if vals is None else vals[r]
+        if vals is None or not B.is_null(v):
+            cnt += 1
+            if vals is not None:
+                if acc is None:
+                    acc = v
+                elif name in ("sum", "avg"):
+                    acc = acc + v
+                elif name == "min":
+                    acc = min(acc, v)
+                elif name == "max":
+                    acc = max(acc, v)
+        if name == "count":
+            out.append(cnt)
+        elif name == "avg":
+            out.append(None if acc is None else float(acc) / cnt)
+        else:
+            out.append(acc)
+    return out
+
+
 def _peer_bounds(okey: list):
     """First / last index of each row's peer group (equal ORDER BY keys) in a sorted partition."""
     m = len(okey)
@@ -1239,6 +1264,13 @@ class Session:
                     sign = 1.0 if okeys[0][1] else -1.0
                     pos = [sign * float(okeys[0][0][i]) for i in grp]
                 peers = _peer_bounds(okey)
+                if frame[1] is None and frame[2] == 0 and pos is None and \
+                        name in ("sum", "count", "avg", "min", "max") and len(args) <= 1 and not f.distinct:
+                    # running aggregate (the default frame): one pass instead of a slice per row
+                    run = _running_agg(name, [args[0][j] for j in grp] if args else None, m)
+                    for r, i in enumerate(grp):
+                        out[i] = run[r if frame[0] == "rows" else peers[1][r]]
+                    continue
                 for r, i in enumerate(grp):
                     a_, b_ = _frame_rows(frame, r, m, peers, pos)
                     sub = [[a[grp[q]] for q in range(a_, b_ + 1)] for a in args]
