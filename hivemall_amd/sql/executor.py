@@ -1443,7 +1443,7 @@ class Session:
                 elif op == "%":
                     r = np.where(y == 0, np.nan, np.fmod(x, np.where(y == 0, 1, y)))
                 else:
-                    r = np.where(y == 0, np.nan, np.floor(x / np.where(y == 0, 1, y)))
+                    r = np.where(y == 0, np.nan, np.trunc(x / np.where(y == 0, 1, y)))   # Java: toward 0
             ints = (pd.api.types.is_integer_dtype(A) and pd.api.types.is_integer_dtype(Bs)
                     and op in ("+", "-", "*", "%", "div"))
             res = pd.Series(r)

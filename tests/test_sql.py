@@ -428,3 +428,9 @@ def test_from_first_multi_insert():
     assert s.table("small")["x"].tolist() == [1, 2] and s.table("big")["x"].tolist() == [3, 4]
     assert sorted(s.table("agg").itertuples(index=False, name=None)) == [("a", 4), ("b", 6)]
     assert s.sql("FROM t SELECT max(x) m")["m"].tolist() == [4]
+
+
+def test_integer_div_and_mod_truncate_toward_zero():
+    s = Session(device="cpu")
+    r = s.sql("SELECT -7 div 2 a, 7 div 2 b, -7 % 3 c, 7 % -3 d").iloc[0].tolist()
+    assert r == [-3, 3, -1, 1]
