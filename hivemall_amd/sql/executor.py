@@ -492,6 +492,13 @@ class Session:
                 self.tables.pop(name, None)
                 return None
             self.views.pop(name, None)
+            if ast.like:
+                src = ast.like.lower()
+                base = self.run_query(self.views[src]).to_df() if src in self.views else self.table(src)
+                self.tables[name] = base.iloc[:0].reset_index(drop=True)
+                if src in self.table_meta:
+                    self.table_meta[name] = dict(self.table_meta[src])
+                return None
             if ast.query is None and ast.storage.get("location"):
                 # CREATE [EXTERNAL] TABLE ... LOCATION '<file or directory>' (io/tables.py)
                 from ..io.tables import read_table

@@ -209,6 +209,7 @@ class CreateTable:
     view: bool = False
     types: list = field(default_factory=list)     # declared Hive types, parallel to columns
     storage: dict = field(default_factory=dict)   # location / stored_as / field_delim / collection_delim
+    like: str | None = None                       # CREATE TABLE t LIKE src
 
 
 @dataclass
@@ -497,6 +498,10 @@ class Parser:
             self.expect_kw("exists")
             ine = True
         name = self.qualified_name()
+        if self.accept_kw("like"):
+            src = self.qualified_name()
+            self.storage_clause(stop_at_query=False)
+            return CreateTable(name, None, [], ine, view, [], {}, like=src)
         cols = []
         if self.t.is_op("("):
             self.next()

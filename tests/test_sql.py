@@ -434,3 +434,12 @@ def test_integer_div_and_mod_truncate_toward_zero():
     s = Session(device="cpu")
     r = s.sql("SELECT -7 div 2 a, 7 div 2 b, -7 % 3 c, 7 % -3 d").iloc[0].tolist()
     assert r == [-3, 3, -1, 1]
+
+
+def test_create_table_like():
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"x": [1, 2], "f": [["a"], ["b"]]}))
+    s.sql("CREATE TABLE u LIKE t")
+    assert list(s.table("u").columns) == ["x", "f"] and len(s.table("u")) == 0
+    s.sql("INSERT INTO TABLE u SELECT * FROM t WHERE x = 2")
+    assert s.table("u")["x"].tolist() == [2]
