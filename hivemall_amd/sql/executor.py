@@ -667,7 +667,7 @@ class Session:
             if body.order_by:
                 fr = self._order(fr, fr, body.order_by, ctes)
             if body.limit is not None:
-                fr = fr.take(np.arange(min(body.limit, fr.n)))
+                fr = fr.take(np.arange(min(body.offset, fr.n), min(body.offset + body.limit, fr.n)))
             return fr
         return self.run_select(body, ctes)
 
@@ -1011,7 +1011,7 @@ class Session:
         if s.order_by:
             out = self._order(out, base if base.n == out.n else out, s.order_by, ctes)
         if s.limit is not None:
-            out = out.take(np.arange(min(s.limit, out.n)))
+            out = out.take(np.arange(min(s.offset, out.n), min(s.offset + s.limit, out.n)))
         return out
 
     def _distinct_index(self, fr: Frame):

@@ -184,6 +184,7 @@ class Select:
     cluster_by: list = field(default_factory=list)
     distinct: bool = False
     limit: int | None = None
+    offset: int = 0                 # LIMIT offset, n
 
 
 @dataclass
@@ -192,6 +193,7 @@ class Union:
     all: bool = True
     order_by: list = field(default_factory=list)
     limit: int | None = None
+    offset: int = 0                 # LIMIT offset, n
 
 
 @dataclass
@@ -694,12 +696,19 @@ class Parser:
         if len(parts) == 1:
             return first
         u = Union(parts, all_)
+        last = parts[-1]
+        if isinstance(last, Select) and (last.order_by or last.limit is not None):
+            # a trailing ORDER BY / LIMIT belongs to the whole UNION (Hive), not its last branch
+            u.order_by, u.limit, u.offset = last.order_by, last.limit, last.offset
+            last.order_by, last.limit, last.offset = [], None, 0
         if self.t.is_kw("order", "sort"):
             self.next()
             self.expect_kw("by")
             u.order_by = self.order_list()
         if self.accept_kw("limit"):
             u.limit = int(self.next().val)
+            if self.accept_op(","):
+                u.offset, u.limit = u.limit, int(self.next().val)
         return u
 
     def select_or_paren(self):
@@ -747,6 +756,8 @@ class Parser:
                     self.expr()
         if self.accept_kw("limit"):
             s.limit = int(self.next().val)
+            if self.accept_op(","):
+                s.offset, s.limit = s.limit, int(self.next().val)
         return s
 
     def order_list(self):

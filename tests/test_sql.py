@@ -443,3 +443,11 @@ def test_create_table_like():
     assert list(s.table("u").columns) == ["x", "f"] and len(s.table("u")) == 0
     s.sql("INSERT INTO TABLE u SELECT * FROM t WHERE x = 2")
     assert s.table("u")["x"].tolist() == [2]
+
+
+def test_limit_with_offset():
+    s = Session(device="cpu")
+    s.register("t", pd.DataFrame({"x": range(10)}))
+    assert s.sql("SELECT x FROM t ORDER BY x LIMIT 3, 2")["x"].tolist() == [3, 4]
+    assert s.sql("SELECT x FROM t ORDER BY x LIMIT 2")["x"].tolist() == [0, 1]
+    assert s.sql("SELECT x FROM t UNION ALL SELECT x FROM t ORDER BY x LIMIT 1, 2")["x"].tolist() == [0, 1]
