@@ -10,10 +10,12 @@ rank checks WORLD_SIZE == N and that the process group really holds N ranks, els
 
 One process per GPU.  Each rank holds a full FFM model replica in HBM (2^20 hashed features x
 39 fields x k=4, one AdaGrad accumulator per (feature, field) slot as Hivemall's AdaGradEntry,
-all in line-padded feature blocks [V | G]: bf16 V (stochastic rounding, fp32 math) + fp32 G by
-default, 0.5 GB; ``--state fp32`` = Hivemall's fp32 V, 0.9 GB; FTRL w/z/n of the linear term
-fp32; ``--adagrad element`` = one accumulator per V element, stored like V) and trains on its own shard of synthetic
-Criteo-shaped rows (weak scaling: per-GPU batch is fixed).  A step = one fused ``hm_ffm_step``
+in line-padded feature blocks [V | G]: fp32 V + fp32 G by default = Hivemall's precision, 0.9 GB;
+``--state bf16`` = bf16 V (stochastic rounding, fp32 math) in 12-B {V | G} slots, 0.5 GB; FTRL
+w/z/n of the linear term fp32; ``--adagrad element`` = one accumulator per V element, stored like
+V) and trains on its own shard of synthetic Criteo-for-FFM rows (``--data criteo_ffm``: explicit
+field ids and values, log-scaled counts on the 13 integer fields; weak scaling: per-GPU batch
+is fixed).  A step = one fused ``hm_ffm_step``
 launch over ``--batch`` rows per GPU; every ``--mix-every`` steps the replicas are averaged
 with the shard-mean collective of ``parallel/mix.py`` (all-to-all -> fp32 mean of each rank's
 1/N shard -> all-gather, over RCCL/xGMI: the MixServer replacement), stale-by-one and
@@ -23,10 +25,10 @@ Timing: W untimed warmup steps, then barrier + synchronize, K timed steps, synch
 barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the mixed
 model on held-out rows and the planted model's logloss (the Bayes floor).
 
-On the GPU the same schedule then runs a second time with fp32 V|G state (the reference's
-precision) in the same process, on the same rows: ``value_fp32_state`` / ``logloss_heldout_fp32``
-(``--fp32-run 0`` skips it).  ``wall_s`` breaks the process's wall time down (data generation,
-setup, warmup, timed region, evaluation, the fp32 run).  ``HM_METRICS=<path>`` appends one JSON
+On the GPU the same schedule then runs a second time with the other state precision in the
+same process, on the same rows: ``value_bf16_state`` / ``logloss_heldout_bf16`` (``--alt-run 0``
+skips it).  ``wall_s`` breaks the process's wall time down (data generation,
+setup, warmup, timed region, evaluation, the other-precision run).  ``HM_METRICS=<path>`` appends one JSON
 line per timed step (device ms from per-step events read after the timed region, rows/s, mean
 training loss, mixes and wire bytes) — the loss buffer is only written when it is set.
 """
@@ -67,11 +69,15 @@ def parse_args(argv=None):
                     help="distinct batches per rank kept in HBM and replayed in turn")
     ap.add_argument("--eval-rows", type=int, default=262144)
     ap.add_argument("--grid", type=int, default=0, help="kernel grid override (0 = auto)")
-    ap.add_argument("--state", choices=("bf16", "fp32"), default="bf16",
-                    help="V / AdaGrad state storage of the headline run (bf16 = stochastic-rounded, "
-                         "fp32 accumulate)")
-    ap.add_argument("--fp32-run", type=int, default=1,
-                    help="GPU, --state bf16: also time the same schedule with fp32 state")
+    ap.add_argument("--state", choices=("bf16", "fp32"), default="fp32",
+                    help="V storage of the headline run: fp32 = Hivemall's precision (the "
+                         "reported value); bf16 = stochastic-rounded storage, fp32 math")
+    ap.add_argument("--alt-run", type=int, default=1,
+                    help="GPU: also time the same schedule with the other state precision "
+                         "(value_bf16_state / value_fp32_state)")
+    ap.add_argument("--data", choices=("criteo_ffm", "criteo_like"), default="criteo_ffm",
+                    help="criteo_ffm: explicit field ids + log-scaled count values on the 13 "
+                         "integer fields; criteo_like: implicit fields, every value 1.0 (rounds 1-3)")
     ap.add_argument("--adagrad", choices=("slot", "element"), default="slot",
                     help="AdaGrad accumulator of V: one per (feature, field) slot (Hivemall's "
                          "AdaGradEntry; fp32) or one per V element (stored like V)")
@@ -136,7 +142,7 @@ def check_world(args, ctx) -> None:
         sys.exit(2)
 
 
-def run_schedule(args, ctx, idx, y, state: str, data, metrics=None) -> dict:
+def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) -> dict:
     """One full FFM schedule (fresh model, warmup, timed region, final mix, held-out logloss).
 
     ``state``: "bf16" or "fp32" V|G storage.  Returns the timing / quality record."""
@@ -173,8 +179,9 @@ def run_schedule(args, ctx, idx, y, state: str, data, metrics=None) -> dict:
 
     def step(i):
         s = (i % nres) * B
-        ffm_step(st, idx[s:s + B], None, None, y[s:s + B], hyper, train=True, grid=args.grid,
-                 loss=loss_buf)
+        ffm_step(st, idx[s:s + B], None if fld is None else fld[s:s + B],
+                 None if val is None else val[s:s + B], y[s:s + B], hyper, train=True,
+                 grid=args.grid, loss=loss_buf)
         if loss_buf is not None:
             step_loss.append(loss_buf.mean())          # device scalar, read after timing
         if world > 1 and (i + 1) % args.mix_every == 0:
@@ -252,11 +259,12 @@ def run_schedule(args, ctx, idx, y, state: str, data, metrics=None) -> dict:
         mixer.average(mix_tensors)
     out["ll"] = None
     if rank == 0:
-        eidx, ey, elogit = data["eval"]
+        eidx, efld, evl, ey, elogit = data["eval"]
         pred = torch.empty(eidx.shape[0], dtype=torch.float32, device=dev)
         for s in range(0, eidx.shape[0], B):
             e = min(eidx.shape[0], s + B)
-            ffm_step(st, eidx[s:e], None, None, None, hyper, train=False, pred=pred[s:e])
+            ffm_step(st, eidx[s:e], None if efld is None else efld[s:e],
+                     None if evl is None else evl[s:e], None, hyper, train=False, pred=pred[s:e])
         yy = (ey > 0).float()
         out["ll"] = torch.nn.functional.binary_cross_entropy_with_logits(pred, yy).item()
         out["floor"] = torch.nn.functional.binary_cross_entropy_with_logits(elogit, yy).item()
@@ -275,7 +283,7 @@ def main(argv=None):
     if rc is not None:
         sys.exit(rc)
     from hivemall_amd.parallel.dist import init_distributed
-    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.io.synthetic import criteo_ffm, criteo_like
     from hivemall_amd.prof import MetricsWriter
 
     ctx = init_distributed(device=args.device)
@@ -290,32 +298,38 @@ def main(argv=None):
     # per-rank shard of synthetic Criteo-shaped rows, resident in HBM
     t = time.perf_counter()
     gdev = torch.device("cpu") if args.gen_device == "cpu" else dev
-    idx, y = criteo_like(B * nres, args.hash_bits, seed=1000 + rank, device=gdev)
-    idx, y = idx.to(dev), y.to(dev)
+    def gen(n, seed, logit=False):
+        if args.data == "criteo_ffm":
+            out = criteo_ffm(n, args.hash_bits, seed=seed, device=gdev, return_logit=logit)
+        else:
+            out = criteo_like(n, args.hash_bits, seed=seed, device=gdev, return_logit=logit)
+            out = (out[0], None, None) + tuple(out[1:])
+        return tuple(None if t is None else t.to(dev) for t in out)
+
+    idx, fld, val, y = gen(B * nres, 1000 + rank)
     data = {"eval": None}
     if rank == 0:
-        eidx, ey, elogit = criteo_like(args.eval_rows, args.hash_bits, seed=999_999, device=gdev,
-                                       return_logit=True)
-        data["eval"] = (eidx.to(dev), ey.to(dev), elogit.to(dev))
+        data["eval"] = gen(args.eval_rows, 999_999, logit=True)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t
 
     state = args.state if dev.type == "cuda" else "fp32"
-    main_run = run_schedule(args, ctx, idx, y, state, data, metrics)
-    fp32_run = None
-    if dev.type == "cuda" and state == "bf16" and args.fp32_run:
-        fp32_run = run_schedule(args, ctx, idx, y, "fp32", data, metrics)
+    main_run = run_schedule(args, ctx, idx, fld, val, y, state, data, metrics)
+    alt_state = "fp32" if state == "bf16" else "bf16"
+    alt_run = None
+    if dev.type == "cuda" and args.alt_run:
+        alt_run = run_schedule(args, ctx, idx, fld, val, y, alt_state, data, metrics)
 
     wall = {"gen": round(t_gen, 3)}
     for k, v in main_run["wall"].items():
         wall[k] = round(v, 3)
-    if fp32_run is not None:
-        wall["fp32_run"] = round(sum(fp32_run["wall"].values()), 3)
+    if alt_run is not None:
+        wall[f"{alt_state}_run"] = round(sum(alt_run["wall"].values()), 3)
     wall["total"] = round(time.perf_counter() - t_start, 3)
     if metrics is not None:
         metrics.log(event="summary", wall_s=wall, rows_per_s=main_run["rows_per_s"],
-                    rows_per_s_fp32=fp32_run["rows_per_s"] if fp32_run else None)
+                    **{f"rows_per_s_{alt_state}": alt_run["rows_per_s"] if alt_run else None})
     if rank == 0:
         ll, floor = main_run["ll"], main_run.get("floor")
         out = {
@@ -330,14 +344,21 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if state == "bf16" else "fp32",
-            "data": "synthetic (Criteo-shaped: 39 fields, Kaggle-DAC cardinalities, power-law "
-                    "values, planted FM logit), random-init weights",
+            "data": ("synthetic Criteo-for-FFM field:index:value rows (39 explicit fields; 13 "
+                     "integer fields hashed by log2 bucket with log-scaled count values, 26 "
+                     "categorical with Kaggle-DAC cardinalities and power-law frequencies, value "
+                     "1; planted FFM-style logit), random-init weights"
+                     if args.data == "criteo_ffm" else
+                     "synthetic (Criteo-shaped: 39 implicit fields, Kaggle-DAC cardinalities, "
+                     "power-law frequencies, every value 1.0, planted FM logit), random-init weights"),
             "config": {
                 "model": f"train_ffm (k={args.factors}, 2^{args.hash_bits} hashed features, "
                          f"{F} fields, AdaGrad V + FTRL w, instance L2 norm)",
                 "global_batch": B * world,
                 "seq_len": F,
                 "nnz_per_row": F,
+                "fields": "explicit" if fld is not None else "implicit (slot j = field j)",
+                "values": "explicit" if val is not None else "1.0",
                 "parallelism": f"dp{world}",
                 "mix_every": args.mix_every,
                 "state": (f"{state} V, " + ("fp32 AdaGrad accumulator per (feature, field) slot"
@@ -359,10 +380,10 @@ def main(argv=None):
             "rows_trained_per_rank": B * (args.steps + args.warmup),
             "wall_s": wall,
         }
-        if fp32_run is not None:
-            out["value_fp32_state"] = round(fp32_run["rows_per_s"], 1)
-            out["ms_per_step_fp32_state"] = round(fp32_run["ms_per_step"], 4)
-            out["logloss_heldout_fp32"] = round(fp32_run["ll"], 5)
+        if alt_run is not None:
+            out[f"value_{alt_state}_state"] = round(alt_run["rows_per_s"], 1)
+            out[f"ms_per_step_{alt_state}_state"] = round(alt_run["ms_per_step"], 4)
+            out[f"logloss_heldout_{alt_state}"] = round(alt_run["ll"], 5)
         print(json.dumps(out), flush=True)
     from hivemall_amd.parallel.dist import shutdown
     shutdown()

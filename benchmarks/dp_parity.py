@@ -37,7 +37,7 @@ def run(world: int, steps: int, a, timeout: int) -> dict:
     bargs = ["--gpus", str(world), "--steps", str(steps), "--warmup", str(a.warmup),
              "--batch", str(a.batch), "--hash-bits", str(a.hash_bits), "--mix-every", str(a.mix_every),
              "--mix-overlap", str(a.mix_overlap), "--eval-rows", str(a.eval_rows),
-             "--resident-batches", str(steps + a.warmup), "--mix-probe", "0", "--fp32-run", "0",
+             "--resident-batches", str(steps + a.warmup), "--mix-probe", "0", "--alt-run", "0",
              "--state", a.state, "--mix-mode", a.mix_mode, "--mix-state", str(a.mix_state),
              "--mix-power", str(a.mix_power)]
     if a.device:

@@ -54,6 +54,8 @@ struct FFMParams {
     int sstride;           // elements between consecutive slots: Kp (split) or 2*Kp (packed)
     int fstride;           // slots between consecutive features (>= num_fields; the packed GPU
                            // table pads each feature block to whole 128-B lines)
+    long long vfe;         // generic kernel: V elements between consecutive features (fstride *
+                           // sstride, or the 12-B slot blocks' bytes / 2)
     uint32_t seed;
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
@@ -268,9 +270,8 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     float* s_red = s_x + F;                                              // 16 (+pad)
 
     const int tid = threadIdx.x;
-    const size_t nfld = (size_t)P.fstride;
     const size_t ss = (size_t)P.sstride;
-    auto slot_off = [&](int i, int f) -> size_t { return ((size_t)i * nfld + (size_t)f) * ss; };
+    auto slot_off = [&](int i, int f) -> size_t { return (size_t)i * (size_t)P.vfe + (size_t)f * ss; };
     float* Gs = reinterpret_cast<float*>(G);
 
     for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
@@ -945,7 +946,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS>
+template <int NS, typename OT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -963,8 +964,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
-    const uint32_t vfs = (uint32_t)P.fstride * 16u;                  // V bytes between features
-    const uint32_t gfs = (uint32_t)P.gstride * 4u;                   // G bytes between features
+    const OT vfs = (OT)P.fstride * 16u;                  // V bytes between features
+    const OT gfs = (OT)P.gstride * 4u;                   // G bytes between features
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
@@ -1002,11 +1003,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         }
     };
     // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal, 0 = dead
-    auto slot = [&](int bf, int j, uint32_t& ov, uint32_t& og, float& xab) -> uint32_t {
+    auto slot = [&](int bf, int j, OT& ov, OT& og, float& xab) -> uint32_t {
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
         const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
         const bool live = ok && SA(j) != SB(j);
-        const uint32_t i = ok ? (uint32_t)ma.x : 0u, f = ok ? (uint32_t)mb.y : 0u;
+        const OT i = ok ? (OT)(uint32_t)ma.x : (OT)0, f = ok ? (OT)(uint32_t)mb.y : (OT)0;
         ov = i * vfs + f * 16u;
         og = i * gfs + f * 4u;
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
@@ -1015,7 +1016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     auto dma_slots = [&](int bf) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            uint32_t ov, og;
+            OT ov, og;
             float xab;
             slot(bf, j, ov, og, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * 256 + wave * 64), 16, 0, 0);
@@ -1081,7 +1082,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         float part = 0.f;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            uint32_t ov, og;
+            OT ov, og;
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
@@ -1105,7 +1106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 if (!(wr >> j & 1u)) continue;
-                uint32_t ov, og;
+                OT ov, og;
                 float xj;
                 slot(cur, j, ov, og, xj);
                 const int s = tid + j * 256;
@@ -1135,8 +1136,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                     const int a = q / per, kk = q - a * per;
                     const int i = s_m[cur][a].x;
                     if (i < 0) continue;
-                    char* vblk = vb + (uint32_t)i * vfs;
-                    char* gblk = gb + (uint32_t)i * gfs;
+                    char* vblk = vb + (OT)(uint32_t)i * vfs;
+                    char* gblk = gb + (OT)(uint32_t)i * gfs;
                     if (kk < npad) *reinterpret_cast<uint4*>(vblk + (P.num_fields + kk) * 16) = make_uint4(0u, 0u, 0u, 0u);
                     else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
                     else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
 // per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
 // footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
-template <int NS>
+template <int NS, typename OT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1189,7 +1190,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
-    const uint32_t bs = (uint32_t)P.gstride * 4u;                    // block bytes per feature
+    const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
@@ -1227,18 +1228,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
         }
     };
-    auto slot = [&](int bf, int j, uint32_t& off, float& xab) -> uint32_t {
+    auto slot = [&](int bf, int j, OT& off, float& xab) -> uint32_t {
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
         const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
         const bool live = ok && SA(j) != SB(j);
-        off = ok ? (uint32_t)ma.x * bs + (uint32_t)mb.y * 12u : 0u;
+        off = ok ? (OT)(uint32_t)ma.x * bs + (OT)(uint32_t)mb.y * 12u : (OT)0;
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
     auto dma_slots = [&](int bf) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            uint32_t off;
+            OT off;
             float xab;
             slot(bf, j, off, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + off), (lds_ptr_t)(s_raw + (j * 256 + wave * 64) * 4),
@@ -1303,7 +1304,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         float part = 0.f;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            uint32_t off;
+            OT off;
             const uint32_t k = slot(cur, j, off, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
@@ -1331,7 +1332,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 if (!(wr >> j & 1u)) continue;
-                uint32_t off;
+                OT off;
                 float xj;
                 slot(cur, j, off, xj);
                 const int s = tid + j * 256;
@@ -1361,7 +1362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                     const int a = q / per, kk = q - a * per;
                     const int i = s_m[cur][a].x;
                     if (i < 0) continue;
-                    char* blk = vb + (uint32_t)i * bs;
+                    char* blk = vb + (OT)(uint32_t)i * bs;
                     if (kk < npad) *reinterpret_cast<u3v*>(blk + (P.num_fields + kk) * 12) = u3v{0u, 0u, 0u};
                     else *reinterpret_cast<uint4*>(blk + P.vpad * 12 + 16 * (kk - npad)) = make_uint4(0u, 0u, 0u, 0u);
                 }
@@ -1438,12 +1439,15 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                   const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
                   float* pred, float* loss, int grid, hipStream_t stream) {
     if (P.Kp != 4 || P.F > 45) return -1;
-    if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
+    // tables of 4 GiB and more (-feature_hashing >= 23 at 512-B blocks): 64-bit slot offsets
+    const bool wide = (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
     if (blocks <= 0) return 0;
-#define HM_P12(NSV) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
-                                       fld, val, y, VG, w, wz, wn, bias, pred, loss)
+#define HM_P12(NSV) do { if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+                             P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+                         else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+                             P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
     else if (need <= 6) { HM_P12(6); }
@@ -1459,13 +1463,16 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                   const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
                   float* pred, float* loss, int grid, hipStream_t stream) {
     if (P.Kp != 4 || P.F > 45 || P.vpad <= 0) return -1;
-    if ((size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32)) return -1;
-    if ((size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32)) return -1;
+    // tables of 4 GiB and more (-feature_hashing >= 23 at 896-B blocks): 64-bit slot offsets
+    const bool wide = (size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32) ||
+                      (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-#define HM_P32(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV>), dim3(blocks), dim3(256), 0, stream, P, idx, \
-                                       fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+#define HM_P32(NSV) do { if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+                             P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+                         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+                             P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }
@@ -1513,10 +1520,13 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
              float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream) {
     if (slot_g) {
         if (P.gfstride == 3) {
-            // 12-B {V | G} slots: only the pipelined kernel knows this layout
+            // 12-B {V | G} slots: the pipelined kernel; rows wider than 45 features or tables of
+            // 4 GiB and more (32-bit offsets there) take the generic kernel with 64-bit offsets
+            // (slot stride 6 bf16, feature stride = the block)
             if (!BF) return (int)hipErrorInvalidValue;
-            const int rc = dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
-            return rc == -1 ? (int)hipErrorInvalidValue : rc;
+            const int rc = variant == 1 ? -1 : dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+            if (rc != -1) return rc;
+            return launch_generic<true, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
         }
         if (variant != 1 && !BF && P.gfstride == 1) {
             const int rc = dispatch_sg32(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
@@ -1571,6 +1581,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
+    P.vfe = (long long)P.fstride * P.sstride;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
     P.lambda1 = hp[5]; P.lambda2 = hp[6]; P.min_target = hp[7]; P.max_target = hp[8];
     if (P.F <= 0 || P.F > 256 || (P.Kp & 3)) return (int)hipErrorInvalidValue;
@@ -1581,6 +1592,8 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
             if (!bf16 || P.Kp != 4 || reinterpret_cast<char*>(G) != reinterpret_cast<char*>(V) + 8 ||
                 P.vpad < P.num_fields || (size_t)P.vpad * 12 + (size_t)P.tail16 * 16 != (size_t)P.gstride * 4)
                 return (int)hipErrorInvalidValue;
+            P.sstride = 6;                           // bf16 elements per 12-B slot
+            P.vfe = (long long)P.gstride * 2;        // bf16 elements per feature block
         } else if (P.vpad > 0) {
             // block layout: G right after the V region of the same feature block
             const size_t es = bf16 ? 2 : 4;

@@ -75,6 +75,11 @@ def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs, objd
     hdrs = _headers(CSRC / "kernels")  # shared rule headers are used by host code too
     for s in srcs:
         hdrs.extend(_headers(s.parent))
+    if lib.exists() and not _stale(lib, list(srcs) + hdrs):
+        # the library is newer than every source and header: nothing to do, whether or not the
+        # object files are around (a GPU box gets the tree without build/, and recompiling the
+        # kernels there cost the first launch ~12 s: BENCH_r03.json wall_s.warmup)
+        return lib
     objs = []
     todo = []
     for s in srcs:

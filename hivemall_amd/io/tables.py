@@ -162,7 +162,7 @@ def _text_cell(v, cd: str) -> str:
 
 
 def write_table(df: pd.DataFrame, path: str, fmt: str | None = None, field_delim: str | None = None,
-                collection_delim: str | None = None) -> str:
+                collection_delim: str | None = None, overwrite_dir: bool = False) -> str:
     """Write a query result as Hive would for ``INSERT OVERWRITE DIRECTORY``: parquet, jsonl or
     delimited text (``\\N`` for NULL, arrays joined by the collection delimiter).  A path
     without an extension is a directory; the data goes to ``000000_0`` in it."""
@@ -171,6 +171,14 @@ def write_table(df: pd.DataFrame, path: str, fmt: str | None = None, field_delim
     target = path
     if not os.path.splitext(path)[1]:
         os.makedirs(path, exist_ok=True)
+        # INSERT OVERWRITE DIRECTORY (``overwrite_dir``) replaces the directory's data as Hive
+        # does: every data file (any regular file not hidden by a leading '.' or '_', the files
+        # a directory read picks up) goes first, so a stale 000000_0 of another format is never
+        # read back
+        for name in (os.listdir(path) if overwrite_dir else ()):
+            fp = os.path.join(path, name)
+            if not name.startswith((".", "_")) and os.path.isfile(fp):
+                os.remove(fp)
         target = os.path.join(path, "000000_0" + (".parquet" if f == "parquet" else ""))
     else:
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)

@@ -152,12 +152,51 @@ class Learner:
         return self.cv.is_converged()
 
     # ------------------------------------------------------------------ checkpoint / resume
-    def epochs(self, n: int):
+    def run_fingerprint(self, n: int, data=()) -> dict:
+        """What identifies a training run for ``-checkpoint`` resume: the learner, its option
+        string, the epoch count, the seed, the world size, the model table shapes and a digest of
+        the training rows (sizes + a strided sample of each array)."""
+        import hashlib
+
+        import numpy as np
+
+        h = hashlib.sha1()
+        for t in data:
+            if t is None:
+                h.update(b"-")
+                continue
+            a = t.detach().reshape(-1) if isinstance(t, torch.Tensor) else torch.as_tensor(np.asarray(t)).reshape(-1)
+            step = max(1, a.numel() // 4096)
+            smp = a[::step][:4096].cpu().contiguous()
+            h.update(f"{a.numel()}:{a.dtype}:".encode())
+            h.update(smp.view(torch.uint8).numpy().tobytes() if smp.numel() else b"")
+        state = getattr(self, "state", None)
+        shapes = {}
+        if isinstance(state, dict):
+            shapes = {k: list(v.shape) for k, v in state.items() if isinstance(v, torch.Tensor)}
+        world = self.mixer.world if self.mixer is not None else 1
+        return {"learner": self.NAME, "options": self.options_str, "epochs": int(n),
+                "seed": self.seed, "world": int(world), "tables": shapes, "data": h.hexdigest()}
+
+    def no_checkpoint(self, engine: str) -> None:
+        """Warn that ``-checkpoint`` is not honoured by ``engine`` (its loop state lives outside
+        the learner), instead of silently ignoring the option."""
+        try:
+            ckpt = self.cl.get("checkpoint")
+        except KeyError:
+            ckpt = None
+        if ckpt:
+            log.warning("%s: -checkpoint is not supported by %s; training without checkpoints",
+                        self.NAME, engine)
+
+    def epochs(self, n: int, data=()):
         """The epoch indices of a training loop.  With ``-checkpoint <dir>`` the learner's whole
         state is saved after every ``-checkpoint_every`` epochs (per rank, atomically), and a
         rerun resumes after the newest epoch that every rank completed — the same rows and
-        options replay bit-identically on the deterministic engines.  ``HM_FAULT=rank:epoch``
-        injects a crash before that epoch (parallel.elastic)."""
+        options replay bit-identically on the deterministic engines.  A checkpoint written by a
+        different run (other options, rows ``data``, table shapes, seed or world size:
+        :meth:`run_fingerprint`) is never resumed: training starts fresh and overwrites it.
+        ``HM_FAULT=rank:epoch`` injects a crash before that epoch (parallel.elastic)."""
         try:
             ckpt = self.cl.get("checkpoint")
         except KeyError:
@@ -168,7 +207,8 @@ class Learner:
         from ..parallel.elastic import ResumableLoop, maybe_inject_fault
 
         loop = ResumableLoop(self, ckpt, every=int(self.cl.get("checkpoint_every") or 1),
-                             ctx=getattr(self.mixer, "ctx", None))
+                             ctx=getattr(self.mixer, "ctx", None),
+                             fingerprint=self.run_fingerprint(n, data))
         start = loop.resume(self.device)
         if start > 0:
             keep = {"mixer": self.mixer, "rank": self.rank, "kw": self.kw}

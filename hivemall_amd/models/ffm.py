@@ -224,7 +224,7 @@ class FFMTrainer(Learner):
         self._ensure_state()
         loss_buf = torch.empty(b.n, dtype=torch.float32, device=self.device)
         iters = int(self.cl["iters"])
-        for ep in self.epochs(iters):
+        for ep in self.epochs(iters, data=(b.idx, b.fld, b.val, b.y)):
             if ep == 0:
                 eb = b
             else:  # per-epoch device-side shuffle (replaces rand_amplify / spill replay)

@@ -213,7 +213,7 @@ class FMTrainer(Learner):
             va = _slice_rows(rows, rows.n - nva, rows.n)
             rows = _slice_rows(rows, 0, rows.n - nva)
         loss_buf = torch.empty(rows.n, dtype=torch.float32, device=self.device)
-        for ep in self.epochs(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"]), data=(rows.indptr, rows.idx, rows.val, rows.y)):
             self.train_rows(rows, loss_buf)
             if va is not None:
                 self._adapt_lambda(va)
@@ -244,6 +244,7 @@ class FMTrainer(Learner):
         eng = DenseMinibatchFM(dims, self.k, st["V"].float(), self.device, int(self.cl["mini_batch"]),
                                self.h.eta0, self.h.lambda0, self.h.lambda_w, self.h.lambda_v,
                                self.h.classification, self.h.min_target, self.h.max_target)
+        self.no_checkpoint("-engine minibatch")
         for ep in range(int(self.cl["iters"])):
             if self.epoch_converged(eng.epoch(X, y), rows=X.shape[0]):
                 log.info("train_fm converged at epoch %d", ep + 1)

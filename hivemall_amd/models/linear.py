@@ -385,7 +385,7 @@ class OnlineLinearLearner(Learner):
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         iters = int(self.cl["iters"])
         shared = self.state.meta.get("shared", False)
-        for ep in self.epochs(iters):
+        for ep in self.epochs(iters, data=(rows.indptr, rows.idx, rows.val, rows.y)):
             if shared:
                 loss = LO.train_pass_shared(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
                                             self.rows_seen)

@@ -297,7 +297,7 @@ class MatrixFactorization(_MFBase):
         self.seen_u[u.long()] = True
         self.seen_i[i.long()] = True
         loss = torch.empty(u.numel(), device=dev)
-        for ep in self.epochs(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"]), data=(u, i, r)):
             self._step(u, i, r, loss=loss)
             self._epoch_mix(ep)
             el = self.dp_sum(float(loss.double().sum().item()))
@@ -499,6 +499,7 @@ class BPRMF(_MFBase):
             self.seen_u[tu.long()] = True
             self.seen_i[ti.long()] = True
             self.seen_i[tj.long()] = True
+            self.no_checkpoint("-shard_model")
             for ep in range(int(self.cl["iters"])):
                 el = self.dp_sum(self._step_sharded(tu, ti, tj))
                 self._epoch_end(el)
@@ -513,7 +514,7 @@ class BPRMF(_MFBase):
         self.seen_u[tu.long()] = True
         self.seen_i[ti.long()] = True
         self.seen_i[tj.long()] = True
-        for ep in self.epochs(int(self.cl["iters"])):
+        for ep in self.epochs(int(self.cl["iters"]), data=(tu, ti, tj)):
             el = self.dp_sum(self.step(tu, ti, tj))
             self._epoch_end(el)
             self._epoch_mix(ep)
@@ -549,7 +550,7 @@ class BPRMF(_MFBase):
         self.seen_u[u.long()] = True
         self.seen_i.fill_(True)
         per = int(self.cl["samples_per_epoch"]) or csr[1].numel()
-        for ep in range(int(epochs or self.cl["iters"])):
+        for ep in self.epochs(int(epochs or self.cl["iters"]), data=(u, i)):
             el = self.dp_sum(self.step(n=per, csr=csr))
             self._epoch_end(el)
             self._epoch_mix(ep)

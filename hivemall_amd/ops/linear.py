@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -198,10 +199,12 @@ def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     Cached per index tensor (epochs reuse it).  ``HM_LINEAR_HOT=0`` disables."""
     if not hot_rule(P):
         return None
-    key = (idx.data_ptr(), idx.numel(), st.dims, n_rows)
+    # keyed on the tensor object itself (weakly) and its version counter: a later pass whose
+    # index tensor happens to land at a freed address must not reuse this pass's hot set
+    key = (idx.numel(), st.dims, n_rows, idx._version)
     hit = st.meta.get("hot")
-    if hit is not None and hit[0] == key:
-        return hit[1]
+    if hit is not None and hit[0]() is idx and hit[1] == key:
+        return hit[2]
     W = st.RS.shape[0]
     # counts from a strided sample of the indices (a prime stride: coprime with any row width
     # it does not divide, so every field is sampled): the hot set only needs the frequent features, and a full bincount of
@@ -218,7 +221,7 @@ def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
         slot = torch.full((st.dims,), -1, dtype=torch.int32, device=idx.device)
         slot[feats.long()] = torch.arange(feats.numel(), dtype=torch.int32, device=idx.device)
         res = (slot, feats.contiguous())
-    st.meta["hot"] = (key, res)
+    st.meta["hot"] = (weakref.ref(idx), key, res)
     return res
 
 

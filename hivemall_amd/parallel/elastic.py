@@ -18,6 +18,7 @@ a dead attempt's MixServer contributions).  Here one job = one process per GPU, 
 from __future__ import annotations
 
 import json
+import logging
 import os
 import shutil
 
@@ -25,6 +26,8 @@ import torch
 
 from ..io import checkpoint
 from .dist import DistContext
+
+log = logging.getLogger(__name__)
 
 
 class InjectedFault(RuntimeError):
@@ -48,12 +51,15 @@ class ResumableLoop:
     """Step loop with periodic per-rank checkpoints and consistent resume."""
 
     def __init__(self, learner, ckpt_dir: str, every: int = 1, ctx: DistContext | None = None,
-                 keep: int = 2):
+                 keep: int = 2, fingerprint: dict | None = None):
         self.learner = learner
         self.dir = ckpt_dir
         self.every = max(1, int(every))
         self.ctx = ctx
         self.keep = keep
+        # identity of the run (learner options, data digest, shapes, seed, world): a checkpoint
+        # whose recorded fingerprint differs belongs to another run and is not resumed
+        self.fingerprint = fingerprint
         self.rank = ctx.rank if ctx is not None else 0
         self.rank_dir = os.path.join(ckpt_dir, f"rank{self.rank}")
         os.makedirs(self.rank_dir, exist_ok=True)
@@ -63,7 +69,12 @@ class ResumableLoop:
         if not os.path.exists(p):
             return -1
         with open(p) as f:
-            return int(json.load(f)["step"])
+            meta = json.load(f)
+        if self.fingerprint is not None and meta.get("fingerprint") != self.fingerprint:
+            log.warning("checkpoint %s was written by a different run (options, rows, shapes, "
+                        "seed or world size differ): starting fresh", self.rank_dir)
+            return -1
+        return int(meta["step"])
 
     def _agree(self, step: int) -> int:
         if self.ctx is None or not self.ctx.is_dist:
@@ -88,7 +99,7 @@ class ResumableLoop:
         checkpoint.save(self.learner, path, model_table=False)
         tmp = os.path.join(self.rank_dir, "latest.json.tmp")
         with open(tmp, "w") as f:
-            json.dump({"step": step}, f)
+            json.dump({"step": step, "fingerprint": self.fingerprint}, f)
         os.replace(tmp, os.path.join(self.rank_dir, "latest.json"))
         steps = sorted(int(d[4:]) for d in os.listdir(self.rank_dir) if d.startswith("step"))
         for s in steps[:-self.keep]:

@@ -551,7 +551,7 @@ class Session:
 
             st = ast.storage
             write_table(self.run_query(ast.query).to_df(), ast.path, st.get("stored_as"),
-                        st.get("field_delim"), st.get("collection_delim"))
+                        st.get("field_delim"), st.get("collection_delim"), overwrite_dir=True)
             return None
         if isinstance(ast, Drop):
             n = ast.name.lower()

@@ -169,3 +169,32 @@ def test_learner_checkpoint_option_resumes_bit_identically(kind, tmp_path, monke
     monkeypatch.setenv("HM_FAULT", "0:0:raise")
     got = run(f" -checkpoint {ck}")
     assert torch.equal(got, ref)
+
+
+def test_checkpoint_of_another_run_is_not_resumed(tmp_path, monkeypatch):
+    """A -checkpoint directory written by a different run (other rows, other options) is never
+    resumed: the learner starts fresh (a finished run's checkpoint used to be returned
+    as the new query's model)."""
+    from hivemall_amd.io.synthetic import criteo_like
+    from hivemall_amd.models.ffm import FFMBatch, FFMTrainer
+
+    ck = str(tmp_path / "ck")
+    base = "-c -factors 4 -num_fields 39 -feature_hashing 10 -iters 3 -disable_cv -seed 3"
+
+    def run(seed, opts=""):
+        idx, y = criteo_like(400, 10, seed=seed)
+        t = FFMTrainer(base + opts + f" -checkpoint {ck}", device="cpu")
+        t.fit(batch=FFMBatch(idx, None, None, y))
+        return t
+
+    first = run(4)
+    assert first.cv.epoch == 3
+    # same options, different rows: trains all 3 epochs from scratch, equal to a clean run
+    other = run(5)
+    idx, y = criteo_like(400, 10, seed=5)
+    clean = FFMTrainer(base, device="cpu")
+    clean.fit(batch=FFMBatch(idx, None, None, y))
+    assert other.cv.epoch == 3 and torch.equal(other.state["V"], clean.state["V"])
+    # same rows, different options (-iters 5): not resumed either
+    again = run(5, " -eta0 0.1")
+    assert again.cv.epoch == 3 and not torch.equal(again.state["V"], clean.state["V"])

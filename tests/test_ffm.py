@@ -308,10 +308,107 @@ def test_ffm_gpu_bench_scale_parity_pinned():
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gen-device", "cpu"],
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gen-device", "cpu",
+                        "--data", "criteo_like"],
                        capture_output=True, text=True, timeout=110, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert rec["rows_trained_per_rank"] == 12582912
-    assert abs(rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS) <= 3e-3, rec["logloss_heldout"]
-    assert abs(rec["logloss_heldout_fp32"] - SEQ_BENCH_SCALE_LOGLOSS) <= 1.2e-3, rec["logloss_heldout_fp32"]
+    assert rec["rows_trained_per_rank"] == 12582912 and rec["dtype"] == "fp32"
+    assert abs(rec["logloss_heldout_bf16"] - SEQ_BENCH_SCALE_LOGLOSS) <= 3e-3, rec["logloss_heldout_bf16"]
+    assert abs(rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS) <= 1.2e-3, rec["logloss_heldout"]
+
+
+def _copy_state(tc, tg, rows=None):
+    """CPU trainer state -> GPU state (rows ``rows`` of the GPU tables when given), then the CPU
+    state <- the GPU's stored values (the same bf16-rounded start for both engines)."""
+    for k in tc.state:
+        dst = tg.state[k] if rows is None or k == "bias" else tg.state[k][rows]
+        dst.copy_(tc.state[k].to(dst.device))
+        tc.state[k].copy_(dst.float().cpu())
+
+
+def _assert_state_close(tc, tg, tol, rows=None):
+    for k in ("V", "G", "w", "wz", "wn"):
+        a = tg.state[k] if rows is None else tg.state[k][rows]
+        np.testing.assert_allclose(a.float().cpu().numpy(), tc.state[k].numpy(), rtol=tol,
+                                   atol=tol * 1e-1, err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra,tol", [("", 1e-4), (" -bf16_state", 2e-2)])
+def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol):
+    """field:index:value rows as the SQL / UDTF path hands them to the kernel: an explicit
+    field id per feature (every row a random permutation of the 39 fields, and on every third
+    row two features sharing one field) and random values, through the pipelined sg32 (fp32)
+    and sg12 (bf16) kernels vs the sequential C++ engine on disjoint-feature rows."""
+    g = torch.Generator().manual_seed(7)
+    B, F = 384, 39
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    fld = torch.stack([torch.randperm(F, generator=g) for _ in range(B)]).to(torch.int32)
+    fld[::3, 5] = fld[::3, 6]
+    val = torch.rand(B, F, generator=g) * 3.0 + 0.1
+    y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
+    tc = _trainer("cpu", B * F, F)
+    tg = _trainer("cuda", B * F, F, extra=extra)
+    _copy_state(tc, tg)
+    lc, lg = torch.empty(B), torch.empty(B, device="cuda")
+    ffm_step(tc.state, idx, fld, val, y, tc.hyper, loss=lc)
+    ffm_step(tg.state, idx.cuda(), fld.cuda(), val.cuda(), y.cuda(), tg.hyper, loss=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=1e-4, atol=1e-5)
+    _assert_state_close(tc, tg, tol)
+
+
+@pytest.mark.gpu
+def test_ffm_gpu_bf16_rows_wider_than_45_features():
+    """-bf16_state keeps 12-B {V | G} slots for any row width; rows of more than 45 features
+    (beyond the pipelined kernel's LDS image) take the generic kernel on the same layout."""
+    g = torch.Generator().manual_seed(8)
+    B, F = 96, 46
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    val = torch.rand(B, F, generator=g) + 0.5
+    y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
+    tc = _trainer("cpu", B * F, F)
+    tg = _trainer("cuda", B * F, F, extra=" -bf16_state")
+    assert tg.state["G"].stride(1) == 3                 # the 12-B slot layout
+    _copy_state(tc, tg)
+    lc, lg = torch.empty(B), torch.empty(B, device="cuda")
+    for _ in range(2):
+        ffm_step(tc.state, idx, None, val, y, tc.hyper, loss=lc)
+        ffm_step(tg.state, idx.cuda(), None, val.cuda(), y.cuda(), tg.hyper, loss=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=2e-2, atol=2e-3)
+    _assert_state_close(tc, tg, 2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_ffm_gpu_tables_of_4gib_and_more(dtype):
+    """-feature_hashing 23: the bf16 12-B slot table is 4 GiB and the fp32 block table 7.5 GiB,
+    past the 32-bit slot offsets; the pipelined kernels switch to 64-bit offsets.  The rows use
+    features at the top of the id range (offsets > 4 GiB) and must match the sequential engine
+    run on a small table holding the same rows."""
+    g = torch.Generator().manual_seed(9)
+    B, F, NF = 256, 39, 1 << 23
+    base = NF - B * F
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    val = torch.rand(B, F, generator=g) + 0.5
+    y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
+    tc = _trainer("cpu", B * F, F)
+    tg = FFMTrainer("-classification -factors 4 -seed 3" + (" -bf16_state" if dtype == torch.bfloat16 else ""),
+                    device="cuda")
+    V, G = new_state_tables(NF, F, 4, dtype, "cuda", packed=True, slot_g=True)
+    z = lambda: torch.zeros(NF, dtype=torch.float32, device="cuda")  # noqa: E731
+    tg.state = dict(V=V, G=G, w=z(), wz=z(), wn=z(), bias=torch.zeros(4, device="cuda"))
+    rows = slice(base, NF)
+    _copy_state(tc, tg, rows)
+    lc, lg = torch.empty(B), torch.empty(B, device="cuda")
+    ffm_step(tc.state, idx, None, val, y, tc.hyper, loss=lc)
+    ffm_step(tg.state, (idx + base).cuda(), None, val.cuda(), y.cuda(), tc.hyper, loss=lg)
+    torch.cuda.synchronize()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=1e-4, atol=1e-5)
+    _assert_state_close(tc, tg, tol, rows)
+    assert float(tg.state["V"][:base].abs().amax()) == 0.0            # nothing else written
+    del tg, V, G
+    torch.cuda.empty_cache()

@@ -451,3 +451,20 @@ def test_limit_with_offset():
     assert s.sql("SELECT x FROM t ORDER BY x LIMIT 3, 2")["x"].tolist() == [3, 4]
     assert s.sql("SELECT x FROM t ORDER BY x LIMIT 2")["x"].tolist() == [0, 1]
     assert s.sql("SELECT x FROM t UNION ALL SELECT x FROM t ORDER BY x LIMIT 1, 2")["x"].tolist() == [0, 1]
+
+
+def test_insert_overwrite_directory_replaces_old_data(tmp_path):
+    """INSERT OVERWRITE DIRECTORY replaces the directory's data files (Hive): a stale parquet
+    file from an earlier write is not read back next to the new text output."""
+    import pandas as pd
+
+    from hivemall_amd.io.tables import read_table, write_table
+
+    d = str(tmp_path / "out")
+    write_table(pd.DataFrame({"a": [1, 2, 3]}), d, "parquet", overwrite_dir=True)
+    (tmp_path / "out" / "_SUCCESS").write_text("")
+    write_table(pd.DataFrame({"a": [7]}), d, "textfile", overwrite_dir=True)
+    import os
+
+    assert sorted(os.listdir(d)) == ["000000_0", "_SUCCESS"]
+    assert read_table(d, "textfile", ["a"], ["int"])["a"].tolist() == [7]
