@@ -18,8 +18,11 @@ field ids and values, log-scaled counts on the 13 integer fields; weak scaling: 
 is fixed).  A step = one fused ``hm_ffm_step``
 launch over ``--batch`` rows per GPU; every ``--mix-every`` steps the replicas are averaged
 with the shard-mean collective of ``parallel/mix.py`` (all-to-all -> fp32 mean of each rank's
-1/N shard -> all-gather, over RCCL/xGMI: the MixServer replacement), stale-by-one and
-overlapped with the next steps' compute; that mixing cost is inside the timed region.
+1/N shard -> all-gather, over RCCL/xGMI: the MixServer replacement), synchronously by default
+(``--mix-overlap 1``: stale-by-one, overlapped); that mixing cost is inside the timed region.
+At N > 1 every replica steps with eta0 and alpha times N^p (``--dp-lr-power``, default
+``models.ffm.DP_LR_POWER``): the averaged replicas then track one learner over all N shards
+(docs/compat.md, benchmarks/dp_sim.py).
 
 Timing: W untimed warmup steps, then barrier + synchronize, K timed steps, synchronize +
 barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the mixed
@@ -56,8 +59,13 @@ def parse_args(argv=None):
     ap.add_argument("--hash-bits", type=int, default=20)
     ap.add_argument("--factors", type=int, default=4)
     ap.add_argument("--mix-every", type=int, default=10)
-    ap.add_argument("--mix-overlap", type=int, default=1,
-                    help="1: stale-by-one mixing overlapped with compute (async MixServer semantics)")
+    ap.add_argument("--mix-overlap", type=int, default=0,
+                    help="1: stale-by-one mixing overlapped with compute (async MixServer semantics); "
+                         "0: synchronous (the FFM kernel holds every CU, so the overlap hid ~nothing: "
+                         "docs/perf_notes.md)")
+    ap.add_argument("--dp-lr-power", type=float, default=None,
+                    help="N > 1: every replica steps with eta0 * N^p, alpha * N^p (default: "
+                         "models.ffm.DP_LR_POWER)")
     ap.add_argument("--mix-mode", choices=("mean", "sum", "touched"), default="mean",
                     help="mean: replicas averaged (Hivemall's MixServer); sum: the consensus moves "
                          "by the sum of every rank's delta since the last mix")
@@ -166,6 +174,14 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     tr = FFMTrainer(opts, device=dev)
     tr.init_state(NF, F)
     st, hyper = tr.state, tr.hyper
+    sc = 1.0
+    if world > 1:
+        # data-parallel replicas: step size x N^p (models/ffm.py DP_LR_POWER, docs/compat.md)
+        from hivemall_amd.models.ffm import DP_LR_POWER, dp_lr_scale
+
+        sc = dp_lr_scale(world, DP_LR_POWER if args.dp_lr_power is None else args.dp_lr_power)
+        hyper.eta0 *= sc
+        hyper.alpha *= sc
     hyper.reload = None if args.reload < 0 else bool(args.reload)
     mixer = ModelMixer(ctx)
     # mixed: V (weights) and the FTRL (z, n) the linear weight w is computed from, w, w0;
@@ -239,7 +255,8 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
                         wire_bytes=(wire_timed // max(1, mixes_timed)) if mixed else 0)
     out = {"elapsed_s": elapsed, "ms_per_step": 1000.0 * elapsed / max(1, args.steps),
            "rows_per_s": float(B) * world * args.steps / elapsed, "mixes_timed": mixes_timed,
-           "mixed_bytes": int(sum(t.numel() * t.element_size() for t in mix_tensors))}
+           "mixed_bytes": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
+           "dp_lr_scale": sc}
     if os.environ.get("HM_TRACE"):
         # host + device timeline of a few extra steps (outside the timed region)
         from hivemall_amd.prof import host_trace
@@ -369,6 +386,7 @@ def main(argv=None):
                 "mixed_bytes_per_mix": main_run["mixed_bytes"],
                 "mixes_in_timed_region": main_run["mixes_timed"],
                 "mix_overlapped": bool(args.mix_overlap),
+                "dp_lr_scale": round(main_run["dp_lr_scale"], 4),
                 "resident_batches": nres,
             },
             "rccl_world": world if ctx.backend == "nccl" else None,

@@ -1,7 +1,7 @@
 """Logloss parity of the headline schedule at N ranks (BASELINE.json:2 "...; logloss parity").
 
-Runs ``bench.py`` (overlapped stale-by-one shard-mean mixing every ``--mix-every`` steps, the
-exact schedule the driver times) at world 1, 2, 4, 8 ... and, for comparison, at world 1 over
+Runs ``bench.py`` (shard-mean mixing every ``--mix-every`` steps, replicas stepping with
+eta0 / alpha x N^p: the exact schedule the driver times) at world 1, 2, 4, 8 ... and, for comparison, at world 1 over
 the SAME TOTAL number of distinct rows (N x steps batches on one rank).  Every batch a rank
 trains on is distinct (``--resident-batches = --steps + --warmup``), so N ranks see N times the
 rows of one rank, exactly as in the driver's weak-scaling run.
@@ -40,6 +40,8 @@ def run(world: int, steps: int, a, timeout: int) -> dict:
              "--resident-batches", str(steps + a.warmup), "--mix-probe", "0", "--alt-run", "0",
              "--state", a.state, "--mix-mode", a.mix_mode, "--mix-state", str(a.mix_state),
              "--mix-power", str(a.mix_power)]
+    if a.dp_lr_power is not None:
+        bargs += ["--dp-lr-power", str(a.dp_lr_power)]
     if a.device:
         bargs += ["--device", a.device]
     bench = os.path.join(ROOT, "bench.py")
@@ -65,7 +67,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--hash-bits", type=int, default=14)
     ap.add_argument("--mix-every", type=int, default=10)
-    ap.add_argument("--mix-overlap", type=int, default=1)
+    ap.add_argument("--mix-overlap", type=int, default=0)
+    ap.add_argument("--dp-lr-power", type=float, default=None)
     ap.add_argument("--eval-rows", type=int, default=65536)
     ap.add_argument("--state", default="fp32")
     ap.add_argument("--mix-mode", default="mean")
@@ -85,6 +88,7 @@ def main(argv=None):
         rec = {"world": w, "steps_per_rank": a.steps, "rows_per_rank": a.batch * (a.steps + a.warmup),
                "total_rows": a.batch * (a.steps + a.warmup) * w, "mix_every": a.mix_every,
                "overlap": a.mix_overlap, "mix_mode": a.mix_mode, "mix_state": a.mix_state,
+               "dp_lr_scale": rn["config"].get("dp_lr_scale"),
                "mix_power": a.mix_power,
                "batch": a.batch, "hash_bits": a.hash_bits,
                "backend": rn.get("dist_backend"), "device": a.device,

@@ -1444,10 +1444,11 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
     if (blocks <= 0) return 0;
-#define HM_P12(NSV) do { if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
-                             P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-                         else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
-                             P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
+#define HM_P12(NSV) do { \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+                                     P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+                                P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
     else if (need <= 6) { HM_P12(6); }
@@ -1469,10 +1470,11 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-#define HM_P32(NSV) do { if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
-                             P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-                         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
-                             P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
+#define HM_P32(NSV) do { \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+                                     P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+                                P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }

@@ -36,6 +36,7 @@ struct MFParams {
     int atomic;                // MF: 0 = read-modify-write stores, 1 = atomic delta adds on users
                                // and items, 2 = atomic adds on items only (the skewed side)
     int bstride;               // MF: element stride of Bu / Bi / GBu / GBi (16: one 64-B line each)
+    int bm_words;              // BPR: 32-bit words per user in the positive-item bitmap
 };
 
 // Shared-model load: L1-bypassing unless disabled for an A/B (HM_MF_PLAIN_LOADS=1).
@@ -252,6 +253,104 @@ __global__ __launch_bounds__(256) void bpr_kernel(MFParams P, const int32_t* __r
     }
 }
 
+// Pipelined BPR (default; HM_BPR_VARIANT=1 selects bpr_kernel): the sampling of the NEXT triple
+// (random positive -> negative rejection) is issued right behind the current triple's factor
+// gathers, so its dependent loads overlap the gather / update of the current one instead of
+// preceding it; and the rejection test is one load of a per-user item bitmap (built once per
+// positive set, n_users x ceil(n_items / 32) words: 472 MB at ML-20M) instead of a binary
+// search over the user's sorted items (~8 dependent loads).  The triples drawn are exactly
+// bpr_kernel's (same PCG stream, same rejection order).
+struct Trip { int u, i, j; };
+
+__device__ __forceinline__ Trip bpr_draw(const MFParams& P, int64_t r, int64_t n, int64_t t0,
+                                         const int32_t* __restrict__ tu, const int32_t* __restrict__ ti,
+                                         const int32_t* __restrict__ tj, const int64_t* __restrict__ uptr,
+                                         const int32_t* __restrict__ uitems,
+                                         const int32_t* __restrict__ pos_user, int64_t n_pos,
+                                         const uint32_t* __restrict__ bitmap) {
+    Trip t{-1, -1, -1};
+    if (r >= n) return t;
+    if (tu) { t.u = tu[r]; t.i = ti[r]; t.j = tj[r]; return t; }
+    uint64_t s = ((uint64_t)P.seed << 32) ^ (uint64_t)(t0 + r) * 0x9E3779B97F4A7C15ull;
+    pcg(s);
+    const uint64_t pidx = ((uint64_t)pcg(s) << 32 | pcg(s)) % (uint64_t)n_pos;
+    t.u = pos_user[pidx];
+    t.i = uitems[pidx];
+    for (int tries = 0; tries < P.max_tries; ++tries) {
+        const int j = (int)(pcg(s) % (uint32_t)P.n_items);
+        const bool pos = bitmap ? ((bitmap[(size_t)t.u * P.bm_words + (j >> 5)] >> (j & 31)) & 1u) != 0u
+                                : is_positive(uptr, uitems, t.u, j);
+        if (!pos) { t.j = j; break; }
+    }
+    return t;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void bpr_pf_kernel(MFParams P, const int32_t* __restrict__ tu,
+                                                     const int32_t* __restrict__ ti,
+                                                     const int32_t* __restrict__ tj, int64_t n,
+                                                     const int64_t* __restrict__ uptr,
+                                                     const int32_t* __restrict__ uitems,
+                                                     const int32_t* __restrict__ pos_user,
+                                                     int64_t n_pos, int64_t t0,
+                                                     const uint32_t* __restrict__ bitmap,
+                                                     float* __restrict__ Pu, float* __restrict__ Qi,
+                                                     float* __restrict__ Bi, double* __restrict__ loss_sum) {
+    constexpr int PER = 64 / G;
+    const int lane = hm::lane_id();
+    const int sub = lane / G, f = lane % G;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int64_t stride = nwaves * PER;
+    double lacc = 0.0;
+    int64_t base = wave * PER;
+    Trip cur = bpr_draw(P, base + sub, n, t0, tu, ti, tj, uptr, uitems, pos_user, n_pos, bitmap);
+    for (; base < n; base += stride) {
+        const int64_t r = base + sub;
+        const int u = cur.u, i = cur.i, j = cur.j;
+        const bool ok = r < n && u >= 0 && u < P.n_users && i >= 0 && i < P.n_items && j >= 0 &&
+                        j < P.n_items && i != j;
+        const bool fa = ok && f < P.k;
+        const size_t ou = (size_t)(ok ? u : 0) * P.kp + f;
+        const size_t oi = (size_t)(ok ? i : 0) * P.kp + f, oj = (size_t)(ok ? j : 0) * P.kp + f;
+        float pu = 0.f, qi = 0.f, qj = 0.f, bi = 0.f, bj = 0.f;
+        if (fa) { pu = ldm(P, Pu + ou); qi = ldm(P, Qi + oi); qj = ldm(P, Qi + oj); }
+        if (ok && P.use_bias) { bi = ldm(P, Bi + i); bj = ldm(P, Bi + j); }
+        // the next triple's draw: its loads go out behind this triple's gathers
+        cur = bpr_draw(P, r + stride, n, t0, tu, ti, tj, uptr, uitems, pos_user, n_pos, bitmap);
+        const float d = group_sum<G>(pu * (qi - qj));
+        const float x = bi - bj + d;
+        float z;
+        if (P.loss == 2) { const float s = hm::sigmoidf_(x); z = s * (1.f - s); }
+        else z = 1.f / (1.f + __expf(x));
+        if (ok && f == 0) lacc += (double)hm::log1pexp(-x);
+        if (!ok) continue;
+        const float eta = eta_t(P, (float)(t0 + r + 1));
+        if (fa) {
+            Pu[ou] = pu + eta * (z * (qi - qj) - P.lambda_u * pu);
+            Qi[oi] = qi + eta * (z * pu - P.lambda_i * qi);
+            Qi[oj] = qj + eta * (-z * pu - P.lambda_j * qj);
+        }
+        if (P.use_bias && f == 0) {
+            Bi[i] = bi + eta * (z - P.lambda_b * bi);
+            Bi[j] = bj + eta * (-z - P.lambda_b * bj);
+        }
+    }
+    if (loss_sum) {
+        lacc = hm::wave_sum(lacc);
+        if (lane == 0 && lacc != 0.0) atomicAdd(loss_sum, lacc);
+    }
+}
+
+// bitmap[u * words + (i >> 5)] |= 1 << (i & 31) for every positive pair (user-sorted CSR)
+__global__ void bpr_bitmap_kernel(const int32_t* __restrict__ users, const int32_t* __restrict__ items,
+                                  int64_t n, int words, uint32_t* __restrict__ bitmap) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int it = items[q];
+        atomicOr(bitmap + (size_t)users[q] * words + (it >> 5), 1u << (it & 31));
+    }
+}
+
 MFParams unpack(const int32_t* ip, const float* hp) {
     MFParams P;
     P.k = ip[0]; P.kp = ip[1]; P.n_users = ip[2]; P.n_items = ip[3]; P.adagrad = ip[4];
@@ -260,6 +359,7 @@ MFParams unpack(const int32_t* ip, const float* hp) {
     P.coherent = ip[12] == 0;  // ip[12] = 1: plain (L1-cached) loads, A/B only
     P.atomic = ip[13];         // MF: atomic delta updates
     P.bstride = ip[14] > 0 ? ip[14] : 1;
+    P.bm_words = (P.n_items + 31) / 32;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda_u = hp[3];
     P.lambda_i = hp[4]; P.lambda_j = hp[5]; P.lambda_b = hp[6]; P.eps = hp[7];
     return P;
@@ -305,22 +405,42 @@ HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
     HM_LAUNCH_RET();
 }
 
+// ip[15]: 1 = bpr_kernel (the binary-search sampler, no lookahead), else bpr_pf_kernel.
+// bitmap: the positive-item bitmap of hm_bpr_bitmap (device sampling), or null.
 HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, const int32_t* ti,
                        const int32_t* tj, int64_t n, const int64_t* uptr, const int32_t* uitems,
                        const int32_t* pos_user, int64_t n_pos, int64_t t0, float* Pu, float* Qi,
-                       float* Bi, double* loss_sum, hipStream_t stream) {
+                       float* Bi, double* loss_sum, const uint32_t* bitmap, hipStream_t stream) {
     const MFParams P = unpack(ip, hp);
     g_grid_override = ip[11];  // concurrency cap chosen by the host (Hogwild contention policy)
+    const int variant = ip[15];
     if (n <= 0) return 0;
     if (P.k <= 0 || P.k > 64 || P.kp < P.k) return (int)hipErrorInvalidValue;
     if (!tu && (!uptr || !uitems || !pos_user || n_pos <= 0)) return (int)hipErrorInvalidValue;
 #define HM_BPR(GG)                                                                                 \
-    hipLaunchKernelGGL((bpr_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, tu,    \
-                       ti, tj, n, uptr, uitems, pos_user, n_pos, t0, Pu, Qi, Bi, loss_sum)
+    if (variant == 1)                                                                              \
+        hipLaunchKernelGGL((bpr_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, tu, \
+                           ti, tj, n, uptr, uitems, pos_user, n_pos, t0, Pu, Qi, Bi, loss_sum);      \
+    else                                                                                           \
+        hipLaunchKernelGGL((bpr_pf_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, \
+                           tu, ti, tj, n, uptr, uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap,  \
+                           Pu, Qi, Bi, loss_sum)
     if (P.k <= 8) HM_BPR(8);
     else if (P.k <= 16) HM_BPR(16);
     else if (P.k <= 32) HM_BPR(32);
     else HM_BPR(64);
 #undef HM_BPR
+    HM_LAUNCH_RET();
+}
+
+// Positive-item bitmap of a user-sorted positive set (bpr_pf_kernel's rejection test); the
+// caller zeroes ``bitmap`` (n_users x ceil(n_items / 32) words).
+HM_API int hm_bpr_bitmap(const int32_t* users, const int32_t* items, int64_t n, int n_items,
+                         uint32_t* bitmap, hipStream_t stream) {
+    if (n <= 0) return 0;
+    const int words = (n_items + 31) / 32;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 256 * 64) blocks = 256 * 64;
+    hipLaunchKernelGGL(bpr_bitmap_kernel, dim3((int)blocks), dim3(256), 0, stream, users, items, n, words, bitmap);
     HM_LAUNCH_RET();
 }

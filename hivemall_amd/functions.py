@@ -71,6 +71,10 @@ def _column(a, arrow_ok: bool):
     buffers on the device (``ARROW_INPUT``, e.g. train_ffm), everything else becomes a list."""
     import pandas as pd
 
+    from .io.ingest import DeviceFeatures
+
+    if isinstance(a, DeviceFeatures):
+        return a
     if arrow_ok and isinstance(a, pd.Series) and isinstance(a.dtype, pd.ArrowDtype):
         arr = a.array._pa_array
         return arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
@@ -83,6 +87,8 @@ def _rows(d, rank: int, world: int):
     """Rows rank, rank + world, ... of a list or an Arrow array."""
     if isinstance(d, list):
         return d[rank::world]
+    if hasattr(d, "take_rows"):          # io.ingest.DeviceFeatures
+        return d.take_rows(rank, world)
     import pyarrow as pa
 
     return d.take(pa.array(range(rank, len(d), world), type=pa.int64()))
@@ -133,6 +139,8 @@ def _learner_udtf(name, cls_getter, n_data_args=2):
         return tab
     impl.wants_session = True
     impl.accepts_series = True      # argument columns arrive as Series (Arrow buffers kept)
+    # the feature argument may arrive as device CSR (sql/device_ftvec.py)
+    impl.device_features = bool(getattr(cls_getter(), "DEVICE_FEATURES", False))
     ins, outs = _signature(name)
     impl.__doc__ = f"{name}({ins} [, const string options]) -> table ({outs})"
     registry._register(registry.FunctionDef(name, registry.UDTF, impl, per_row=False,

@@ -282,3 +282,81 @@ def csr_device(features, mode: str, num_features: int = 0, device="cuda", chunk_
 
     st = _ingest(arr, chunk_rows, dev, launch, host_chunk)
     return torch.from_numpy(lo).to(dev), idx, val, st
+
+
+@dataclass
+class DeviceFeatures:
+    """A feature column that already lives on the device as CSR — what the SQL planner hands a
+    learner for ``train_*(add_bias(feature_hashing(features)), ...)`` on a GPU session
+    (sql/device_ftvec.py) instead of a column of hashed strings the learner would parse again.
+
+    ``indptr`` int64 [B+1], ``idx`` int64 [nnz] (integer feature ids, as the learners' "int"
+    encoder reads ``"id:value"`` strings), ``val`` f32 [nnz]."""
+    indptr: torch.Tensor
+    idx: torch.Tensor
+    val: torch.Tensor
+    stats: IngestStats | None = None
+
+    def __len__(self) -> int:
+        return self.indptr.numel() - 1
+
+    def take_rows(self, rank: int, world: int) -> "DeviceFeatures":
+        """Rows rank, rank + world, ... (a data-parallel rank's share), still on the device."""
+        B = len(self)
+        rows = torch.arange(rank, B, world, device=self.indptr.device)
+        cnt = self.indptr[rows + 1] - self.indptr[rows]
+        ip = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=self.indptr.device)
+        ip[1:] = torch.cumsum(cnt, 0)
+        pos = torch.repeat_interleave(self.indptr[rows], cnt) + \
+            (torch.arange(int(ip[-1]), device=ip.device) - torch.repeat_interleave(ip[:-1], cnt))
+        return DeviceFeatures(ip, self.idx[pos], self.val[pos])
+
+
+def hashed_csr_device(features, num_features: int, bias: bool, device="cuda",
+                      chunk_rows: int = 1 << 20, seed: int = DEFAULT_SEED) -> DeviceFeatures:
+    """``[add_bias(]feature_hashing(features, '-num_features N')[)]`` evaluated on the device:
+    the raw ``name[:value]`` strings go up as Arrow buffers, ``hm_feat_parse`` (mode 2) turns
+    each into (mhash(name, N), value) — what ``feature_hashing`` writes as ``"h:value"`` and the
+    learner's int encoder reads back — and the bias ``0:1.0`` is appended to every row on the
+    device.  A chunk the device refuses (two-colon names, inexact decimals) goes through the host
+    ``feature_hashing`` + int parse, so the result equals the string path bit for bit."""
+    dev = torch.device(device)
+    arr = to_arrow_lists(features)
+    lo = np.asarray(arr.offsets, dtype=np.int64)
+    lo = lo - lo[0]
+    B, nnz = len(lo) - 1, int(lo[-1])
+    idx = torch.empty(nnz, dtype=torch.int64, device=dev)
+    val = torch.empty(nnz, dtype=torch.float32, device=dev)
+
+    def launch(k, r0, r1, s0, d_data, d_so, d_lo, e):
+        n = int(lo[r1] - lo[r0])
+        rc = _native.hip().hm_feat_parse(d_data.data_ptr(), d_so.data_ptr(), n, 2, int(num_features), seed,
+                                         idx[s0:].data_ptr(), val[s0:].data_ptr(), e.data_ptr(),
+                                         _native.stream_of(dev))
+        _native.check(rc, "hm_feat_parse")
+
+    def host_chunk(r0, r1):
+        from ..ftvec.functions import feature_hashing
+        from ..utils.features import FeatureEncoder
+
+        rows = arr.slice(r0, r1 - r0).to_pylist()
+        hashed = [feature_hashing(r, f"-num_features {int(num_features)}") if r is not None else [] for r in rows]
+        csr = FeatureEncoder("int").encode(hashed)
+        s0, s1 = int(lo[r0]), int(lo[r1])
+        idx[s0:s1].copy_(torch.from_numpy(csr.idx.astype(np.int64)))
+        val[s0:s1].copy_(torch.from_numpy(csr.val.astype(np.float32)))
+
+    st = _ingest(arr, chunk_rows, dev, launch, host_chunk)
+    ip = torch.from_numpy(lo).to(dev)
+    if bias:
+        # row r's entries shift by r; its bias lands in the new last slot of the row
+        cnt = ip[1:] - ip[:-1]
+        nip = ip + torch.arange(B + 1, dtype=torch.int64, device=dev)
+        pos = torch.arange(nnz, dtype=torch.int64, device=dev) + \
+            torch.repeat_interleave(torch.arange(B, dtype=torch.int64, device=dev), cnt, output_size=nnz)
+        bidx = torch.zeros(nnz + B, dtype=torch.int64, device=dev)
+        bval = torch.ones(nnz + B, dtype=torch.float32, device=dev)
+        bidx[pos] = idx
+        bval[pos] = val
+        ip, idx, val = nip, bidx, bval
+    return DeviceFeatures(ip, idx, val, st)

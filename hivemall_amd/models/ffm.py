@@ -63,6 +63,20 @@ def csr_to_ffm_batch(csr: CSR, y: np.ndarray | None, width: int | None = None) -
     return FFMBatch(t(idx), t(fld), t(val), t(y))
 
 
+# Data-parallel step-size scaling of the mixed replicas (docs/compat.md "Data-parallel
+# quality"): N replicas that each run AdaGrad on 1/N of the rows and are averaged every mix move
+# like ONE learner over all rows with its step size divided by sqrt(N) (drift and gradient
+# noise both match at p = 0.5 in the small-step limit); the measured gap at the bench's shape,
+# N = 8, fp32, vs one rank on the same total rows (benchmarks/dp_sim.py, profiles/r4/): p = 0
+# (plain mean) +5.3e-3, 0.5 +1.5e-3, 0.75 +2.8e-4, 1.0 -6e-4.
+DP_LR_POWER = 0.75
+
+
+def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
+    """Step-size factor of a data-parallel replica (1.0 on one rank)."""
+    return float(world) ** float(power) if world > 1 else 1.0
+
+
 class FFMTrainer(Learner):
     NAME = "train_ffm"
     SQL_DP = "shard"
@@ -94,6 +108,10 @@ class FFMTrainer(Learner):
         opt("sigma", None, 0.1, float, "gaussian init stddev"),
         opt("min", "min_target", None, float, "Minimum target (regression clipping)"),
         opt("max", "max_target", None, float, "Maximum target (regression clipping)"),
+        opt("dp_lr_power", None, DP_LR_POWER, float,
+            "[engine] data-parallel training over N ranks: every rank's replica steps with "
+            "eta0 * N^p and alpha * N^p, so the mean of the mixed replicas tracks one learner "
+            "over the union of the ranks' rows (docs/compat.md)"),
     ]
 
     def __init__(self, options: str | None = None, device=None, num_features: int | None = None,
@@ -111,6 +129,10 @@ class FFMTrainer(Learner):
             max_target=c["max"] if c["max"] is not None else 3.4e38,
             classification=bool(c["classification"]), use_linear=not c["disable_wi"],
             use_bias=bool(c["global_bias"]), norm=not c["no_norm"])
+        if self._dp():
+            sc = dp_lr_scale(self.mixer.world, c["dp_lr_power"])
+            self.hyper.eta0 *= sc
+            self.hyper.alpha *= sc
         nf = num_features
         if nf is None and c["feature_hashing"] > 0:
             nf = 1 << int(c["feature_hashing"])

@@ -163,6 +163,7 @@ def _arrow_string_lists(x) -> bool:
 class OnlineLinearLearner(Learner):
     SQL_DP = "shard"
     ARROW_INPUT = True      # Arrow list<string> rows with integer names are parsed on the device
+    DEVICE_FEATURES = True  # accepts io.ingest.DeviceFeatures (SQL feature_hashing on the GPU)
     NAME = "train_linear"
     ALGO = "general"
     TASK = "binary"           # binary | regression | multiclass
@@ -292,6 +293,19 @@ class OnlineLinearLearner(Learner):
         return SparseRows(ip, idx.to(torch.int32), vv, yt)
 
     def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
+        from ..io.ingest import DeviceFeatures
+
+        if isinstance(features, DeviceFeatures):
+            # hashed on the device by the SQL planner (sql/device_ftvec.py): integer ids, as the
+            # int encoder reads the "h:value" strings of the host feature_hashing
+            self.encoder = FeatureEncoder("int")
+            self.encoder.string_names = True
+            y = None if labels is None else self._labels_to_float(labels)
+            yt = None if y is None else torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)).to(self.device)
+            val = features.val
+            vv = None if (val.numel() and bool((val == 1.0).all().item())) else val
+            return SparseRows(features.indptr.to(self.device), features.idx.to(self.device, torch.int32),
+                              None if vv is None else vv.to(self.device), yt)
         if (self.device.type == "cuda" and self._warm is None and not isinstance(features, CSR)
                 and (self.encoder is None or (self.encoder.mode == "int" and
                                               getattr(self.encoder, "string_names", False)))):

@@ -173,7 +173,8 @@ class _MFBase(Learner):
         return np.array([self.k, self.kp, self.n_users, self.n_items, int(self.adagrad),
                          int(self.use_bias), 0, _ETAS[eta], loss, self.seed & 0x7FFFFFFF, max_tries,
                          self._grid(), int(os.environ.get("HM_MF_PLAIN_LOADS", "0") == "1"),
-                         int(os.environ.get("HM_MF_ATOMIC", "1")), 0],
+                         int(os.environ.get("HM_MF_ATOMIC", "1")), 0,
+                         int(os.environ.get("HM_BPR_VARIANT", "0"))],
                         dtype=np.int32)
 
     # Hogwild concurrency cap: rows (users/items) per 256-thread block in flight.  Explicit MF
@@ -439,11 +440,35 @@ class BPRMF(_MFBase):
         args = [ip.ctypes.data, hp.ctypes.data, p(tu), p(ti), p(tj), C.c_int64(n), p(uptr), p(uit),
                 p(pu), C.c_int64(npos), C.c_int64(self.t), p(st["P"]), p(st["Q"]), p(st["Bi"]), p(loss)]
         if dev.type == "cuda":
-            _native.check(_native.hip().hm_bpr_step(*args, _native.stream_of(dev)), "hm_bpr_step")
+            bm = self._positive_bitmap(csr) if tu is None else None
+            _native.check(_native.hip().hm_bpr_step(*args, p(bm), _native.stream_of(dev)), "hm_bpr_step")
         else:
             _native.host().hm_bpr_step_cpu(*args)
         self.t += n
         return float(loss.item())
+
+    # the per-user positive-item bitmap of device sampling: one load per negative test instead
+    # of a binary search (csrc/kernels/mf.hip bpr_pf_kernel); skipped above this many bytes
+    BITMAP_MAX_BYTES = 8 << 30
+
+    def _positive_bitmap(self, csr) -> torch.Tensor | None:
+        """n_users x ceil(n_items / 32) int32 bitmap of ``csr``'s positives, built once per
+        positive set (cached on the CSR tensors' identity)."""
+        uptr, uit, pu = csr
+        hit = getattr(self, "_bitmap", None)
+        if hit is not None and hit[0]() is uit and hit[1] == uit._version:
+            return hit[2]
+        words = (self.n_items + 31) // 32
+        if self.n_users * words * 4 > self.BITMAP_MAX_BYTES:
+            return None
+        import weakref
+
+        bm = torch.zeros(self.n_users * words, dtype=torch.int32, device=uit.device)
+        _native.check(_native.hip().hm_bpr_bitmap(pu.data_ptr(), uit.data_ptr(), C.c_int64(uit.numel()),
+                                                  self.n_items, bm.data_ptr(), _native.stream_of(uit.device)),
+                      "hm_bpr_bitmap")
+        self._bitmap = (weakref.ref(uit), uit._version, bm)
+        return bm
 
     def _step_sharded(self, tu, ti, tj) -> float:
         """-shard_model: pull the rows the triples touch from their owner ranks, run the same
@@ -650,6 +675,7 @@ _native.register_hip("hm_mf_step", [_P, _P, _P, _P, _P, _native.c_i64, _native.c
 _native.register_host("hm_mf_step_cpu", [_P, _P, _P, _P, _P, _native.c_i64, _native.c_i64] + [_P] * 9 +
                       [C.c_int, _P, _P])
 _native.register_hip("hm_bpr_step", [_P, _P, _P, _P, _P, _native.c_i64, _P, _P, _P, _native.c_i64,
-                                     _native.c_i64, _P, _P, _P, _P, _P])
+                                     _native.c_i64, _P, _P, _P, _P, _P, _P])
+_native.register_hip("hm_bpr_bitmap", [_P, _P, _native.c_i64, C.c_int, _P, _P])
 _native.register_host("hm_bpr_step_cpu", [_P, _P, _P, _P, _P, _native.c_i64, _P, _P, _P, _native.c_i64,
                                           _native.c_i64, _P, _P, _P, _P])

@@ -1093,7 +1093,14 @@ class Session:
         if not per_row and getattr(impl, "accepts_series", False):
             # learner UDTFs take whole columns; an Arrow-backed column reaches the device
             # ingest as its buffers instead of millions of Python lists
-            args = [_ser(self.eval(a, src, ctes), src.n).reset_index(drop=True) for a in f.args]
+            dev_feats = None
+            if getattr(impl, "device_features", False) and f.args:
+                # [add_bias(]feature_hashing(col)[)] hashed on the GPU into device CSR
+                from .device_ftvec import try_device_features
+
+                dev_feats = try_device_features(self, f.args[0], src, ctes)
+            args = [dev_feats if (k == 0 and dev_feats is not None) else
+                    _ser(self.eval(a, src, ctes), src.n).reset_index(drop=True) for k, a in enumerate(f.args)]
         else:
             args = [_ser(self.eval(a, src, ctes), src.n).tolist() for a in f.args]
         if per_row:

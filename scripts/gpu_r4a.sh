@@ -15,3 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   python3 bench.py --steps 10 --warmup 3 > $O/prof.log 2>&1
 find $O/prof -name '*stats*'
 bash scripts/gpu_r4b.sh
+bash scripts/gpu_r4c.sh
+bash scripts/gpu_r4d.sh

@@ -384,16 +384,18 @@ def test_learner_metrics_stream_world2():
 
 def test_ffm_logloss_parity_world4_gloo():
     """The headline's "logloss parity" at N ranks (BASELINE.json:2): bench.py's exact schedule
-    (overlapped stale-by-one shard mean every 10 steps) at world 4 on gloo, against one rank
-    over the same total rows and one rank over its own share.  Bounds from the measurement
-    recorded in docs/compat.md (Δ = 0.0150 vs same rows; 0.4730 vs 0.4748 same steps)."""
+    (synchronous shard mean every 10 steps, replicas stepping with eta0 / alpha x N^0.75) at
+    world 4 on gloo, 2^16 hashed features (most slots are touched by one rank between mixes),
+    against one rank over the same total rows: |delta| <= 1e-3 (SURVEY.md:766, fp32).
+    benchmarks/dp_sim.py at this shape: +1.9e-4 (plain mean +1.27e-2); at the bench's shape,
+    N = 8: +2.8e-4 (plain mean +5.3e-3), profiles/r4/."""
     sys.path.insert(0, ROOT)
     from benchmarks.dp_parity import main as dp_parity
 
-    common = ["--worlds", "4", "--steps", "20", "--batch", "2048", "--hash-bits", "12",
-              "--eval-rows", "32768", "--timeout", "600"]
+    common = ["--worlds", "4", "--steps", "20", "--batch", "2048", "--hash-bits", "16",
+              "--eval-rows", "32768", "--timeout", "900"]
     rec = dp_parity(common)[0]
-    assert rec["mixes_timed"] == 2 and rec["backend"] == "gloo"
-    assert abs(rec["delta"]) <= 0.02, rec
+    assert rec["mixes_timed"] == 2 and rec["backend"] == "gloo" and rec["dp_lr_scale"] > 2.8
+    assert abs(rec["delta"]) <= 1e-3, rec
     # N replicas mixed never do worse than one rank trained on its own share
-    assert rec["logloss_N"] <= rec["logloss_1_same_steps"] + 1e-3, rec
+    assert rec["logloss_N"] <= rec["logloss_1_same_steps"], rec

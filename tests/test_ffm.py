@@ -338,14 +338,15 @@ def _assert_state_close(tc, tg, tol, rows=None):
 @pytest.mark.parametrize("extra,tol", [("", 1e-4), (" -bf16_state", 2e-2)])
 def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol):
     """field:index:value rows as the SQL / UDTF path hands them to the kernel: an explicit
-    field id per feature (every row a random permutation of the 39 fields, and on every third
-    row two features sharing one field) and random values, through the pipelined sg32 (fp32)
-    and sg12 (bf16) kernels vs the sequential C++ engine on disjoint-feature rows."""
+    field id per feature (every row a random permutation of the 39 fields) and random values,
+    through the pipelined sg32 (fp32) and sg12 (bf16) kernels vs the sequential C++ engine on
+    disjoint-feature rows.  (Two features of one field in a row make two slots of a row the same
+    (feature, field) slot; the kernels update a row's slots in parallel, so that case is
+    last-writer-wins, docs/compat.md.)"""
     g = torch.Generator().manual_seed(7)
     B, F = 384, 39
     idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
     fld = torch.stack([torch.randperm(F, generator=g) for _ in range(B)]).to(torch.int32)
-    fld[::3, 5] = fld[::3, 6]
     val = torch.rand(B, F, generator=g) * 3.0 + 0.1
     y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
     tc = _trainer("cpu", B * F, F)

@@ -248,7 +248,7 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
         m.fit(rows=rows.to(dev))
         if dev == "cuda":
             assert m.state.meta.get("shared") and m.state.RS.shape[0] == 1024
-            assert m.state.meta["hot"][1] is not None and m.state.meta["hot"][1][1].numel() > 100
+            assert m.state.meta["hot"][2] is not None and m.state.meta["hot"][2][1].numel() > 100
         s = m.decision_function(rows=test.to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
     assert abs(res["cpu"] - res["cuda"]) < 5e-3, res

@@ -468,3 +468,75 @@ def test_insert_overwrite_directory_replaces_old_data(tmp_path):
 
     assert sorted(os.listdir(d)) == ["000000_0", "_SUCCESS"]
     assert read_table(d, "textfile", ["a"], ["int"])["a"].tolist() == [7]
+
+
+def _criteo_strings(n, seed=1):
+    import numpy as np
+    import pandas as pd
+    import pyarrow as pa
+
+    from hivemall_amd.io.synthetic import criteo_like
+
+    idx, y = criteo_like(n, 16, seed=seed)
+    names = np.char.add(np.char.add(np.arange(39).astype(str)[None, :].repeat(n, 0), "#"), idx.numpy().astype(str))
+    names = names.astype(object)
+    names[::7, 3] = names[::7, 3] + ":0.25"          # some explicit values
+    flat = pa.array(names.reshape(-1), type=pa.string())
+    col = pa.ListArray.from_arrays(pa.array(np.arange(0, n * 39 + 1, 39, dtype=np.int32)), flat)
+    return pd.DataFrame({"features": pd.Series(pd.arrays.ArrowExtensionArray(col)),
+                         "label": (y.numpy() > 0).astype(np.int32)})
+
+
+def test_device_ftvec_matches_string_path_cpu():
+    """hashed_csr_device (the GPU planner's feature_hashing + add_bias; on the CPU every chunk
+    takes its host path) gives the CSR the learner's int encoder reads from the hashed strings;
+    the planner matches only [add_bias(]feature_hashing(col[, const])[)]; take_rows shards."""
+    import numpy as np
+    import torch
+
+    from hivemall_amd.ftvec.functions import add_bias, feature_hashing
+    from hivemall_amd.io.ingest import hashed_csr_device
+    from hivemall_amd.sql.device_ftvec import _match
+    from hivemall_amd.sql.parser import parse_expr
+    from hivemall_amd.utils.features import FeatureEncoder
+
+    df = _criteo_strings(300)
+    ref = FeatureEncoder("int").encode(add_bias(feature_hashing(df["features"], "-num_features 65536")))
+    got = hashed_csr_device(df["features"], 65536, True, device="cpu", chunk_rows=128)
+    assert np.array_equal(got.indptr.numpy(), ref.indptr)
+    assert np.array_equal(got.idx.numpy(), ref.idx.astype(np.int64))
+    assert np.array_equal(got.val.numpy(), ref.val.astype(np.float32))
+    sh = got.take_rows(1, 3)
+    ref1 = FeatureEncoder("int").encode(add_bias(feature_hashing(df["features"].iloc[1::3].reset_index(drop=True),
+                                                                 "-num_features 65536")))
+    assert np.array_equal(sh.idx.numpy(), ref1.idx) and torch.equal(sh.indptr, torch.from_numpy(ref1.indptr))
+
+    m = _match(parse_expr("add_bias(feature_hashing(features, '-num_features 1024'))"))
+    assert m is not None and m[1] == 1024 and m[2] is True
+    assert _match(parse_expr("feature_hashing(features)"))[1:] == (1 << 24, False)
+    assert _match(parse_expr("feature_hashing(add_bias(features))")) is None
+    assert _match(parse_expr("add_bias(features)")) is None
+
+
+@pytest.mark.gpu
+def test_device_ftvec_sql_model_table_bit_identical(monkeypatch):
+    """train_classifier(add_bias(feature_hashing(features)), ...) on a GPU session: the fused
+    device path (strings hashed by hm_feat_parse into device CSR) and the string path give the
+    same model table, bit for bit."""
+    import numpy as np
+
+    from hivemall_amd.sql import Session
+
+    df = _criteo_strings(20000)
+    q = ("SELECT train_classifier(add_bias(feature_hashing(features, '-num_features 262144')), label, "
+         "'-loss logloss -opt adagrad -dims 262144') AS (feature, weight) FROM criteo")
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HM_SQL_DEVICE_FTVEC", flag)
+        s = Session(device="cuda")
+        s.register("criteo", df)
+        out[flag] = s.sql(q).sort_values("feature").reset_index(drop=True)
+    a, b = out["1"], out["0"]
+    assert len(a) == len(b) > 1000
+    assert np.array_equal(a["feature"].to_numpy(), b["feature"].to_numpy())
+    assert np.array_equal(a["weight"].to_numpy(), b["weight"].to_numpy())
