@@ -938,6 +938,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 #undef SB
 }
 
+
+// Cache policy of the "coherent" variants (HM_FFM_VARIANT=7): per-XCD L2s are not coherent and
+// a CU's L1 is never refreshed by other CUs' stores (MI355X_MICROARCH.md §Workgroup dispatch),
+// so a hot feature block read through L1/L2 can be another CU's / XCD's old copy for as long as
+// it stays cached.  SC1 loads bypass L1; SC1 stores write through and drop the line from the
+// writer's L2, so the next read of a hot slot on any XCD fetches the latest written value.
+constexpr int CPOL_SC1 = 16;
+typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
+typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t table_rsrc(void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, -1, 0x00020000);   // 4 GiB - 1 bytes
+}
+template <bool COH, typename OT>
+__device__ __forceinline__ void st_v16(char* base, __amdgpu_buffer_rsrc_t r, OT off, float4 v) {
+    if constexpr (COH)
+        __builtin_amdgcn_raw_buffer_store_b128(u4v_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                                                     __float_as_uint(v.w)}, r, (uint32_t)off, 0, CPOL_SC1);
+    else
+        *reinterpret_cast<float4*>(base + off) = v;
+}
+template <bool COH, typename OT>
+__device__ __forceinline__ void st_f32(char* base, __amdgpu_buffer_rsrc_t r, OT off, float v) {
+    if constexpr (COH) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (uint32_t)off, 0, CPOL_SC1);
+    else *reinterpret_cast<float*>(base + off) = v;
+}
+template <bool COH, typename OT>
+__device__ __forceinline__ void st_u3(char* base, __amdgpu_buffer_rsrc_t r, OT off, u3v_t v) {
+    if constexpr (COH) __builtin_amdgcn_raw_buffer_store_b96(v, r, (uint32_t)off, 0, CPOL_SC1);
+    else *reinterpret_cast<u3v_t*>(base + off) = v;
+}
+template <bool COH>
+__device__ __forceinline__ void st_lin(float* p, float v) {
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout
 // ([V: FS x 16 B | G: FS x fp32 | zero tail] per feature, 896 B): the schedule of
@@ -946,7 +983,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS, typename OT>
+template <int NS, typename OT, bool COH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -969,6 +1006,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
+    const __amdgpu_buffer_rsrc_t rv = table_rsrc(Vt), rg = table_rsrc(Gt);
 
     int ab[NS];
 #pragma unroll
@@ -1019,18 +1057,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             OT ov, og;
             float xab;
             slot(bf, j, ov, og, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * 256 + wave * 64), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * 256 + wave * 64), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * 256 + wave * 64), 16, 0, COH ? CPOL_SC1 : 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * 256 + wave * 64), 4, 0, COH ? CPOL_SC1 : 0);
         }
     };
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
             if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, COH ? CPOL_SC1 : 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, COH ? CPOL_SC1 : 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, COH ? CPOL_SC1 : 0);
                 }
             }
         }
@@ -1123,8 +1161,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
-                *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
-                *reinterpret_cast<float*>(gb + og) = gs;
+                st_v16<COH>(vb, rv, ov, make_float4(o0.x, o0.y, o1.x, o1.y));
+                st_f32<COH>(gb, rg, og, gs);
             }
             // the row's features' pad slots and block tails (never read): zeros, so every line a
             // row touches is written whole; spread over all threads (one wave doing them all
@@ -1150,9 +1188,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[mi] = z1;
-                    wn[mi] = n1;
-                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                    st_lin<COH>(wz + mi, z1);
+                    st_lin<COH>(wn + mi, n1);
+                    st_lin<COH>(w + mi, ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2));
                 }
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
@@ -1171,7 +1209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
 // per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
 // footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
-template <int NS, typename OT>
+template <int NS, typename OT, bool COH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1193,6 +1231,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
+    const __amdgpu_buffer_rsrc_t rv = table_rsrc(Vt);
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 
     int ab[NS];
@@ -1243,17 +1282,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             float xab;
             slot(bf, j, off, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + off), (lds_ptr_t)(s_raw + (j * 256 + wave * 64) * 4),
-                                             12, 0, 0);
+                                             12, 0, COH ? CPOL_SC1 : 0);
         }
     };
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
             if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, COH ? CPOL_SC1 : 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, COH ? CPOL_SC1 : 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, COH ? CPOL_SC1 : 0);
                 }
             }
         }
@@ -1350,9 +1389,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
                 const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
-                *reinterpret_cast<u3v*>(vb + off) = u3v{pack_sr_hi(o0, h, rotl32(h, 16)),
+                st_u3<COH>(vb, rv, off, u3v{pack_sr_hi(o0, h, rotl32(h, 16)),
                                                         pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
-                                                        __float_as_uint(gs)};
+                                                        __float_as_uint(gs)});
             }
             // pad slots + block tails of the row's features, spread over all threads
             {
@@ -1373,9 +1412,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 const float g = kappa * mx * scale;
                 const float n1 = ln + g * g;
                 const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                wz[mi] = z1;
-                wn[mi] = n1;
-                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                st_lin<COH>(wz + mi, z1);
+                st_lin<COH>(wn + mi, n1);
+                st_lin<COH>(w + mi, ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2));
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
@@ -1437,7 +1476,7 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
 // Per-slot-G in 12-B bf16 slots {V | G}, 512-B feature blocks (Kp == 4, F <= 45, table < 4 GiB).
 int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
-                  float* pred, float* loss, int grid, hipStream_t stream) {
+                  float* pred, float* loss, int grid, int variant, hipStream_t stream) {
     if (P.Kp != 4 || P.F > 45) return -1;
     // tables of 4 GiB and more (-feature_hashing >= 23 at 512-B blocks): 64-bit slot offsets
     const bool wide = (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
@@ -1445,9 +1484,11 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
     if (blocks <= 0) return 0;
 #define HM_P12(NSV) do { \
-        if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t, false>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 7) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, true>), dim3(blocks), dim3(256), 0, \
+                                                  stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, false>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
@@ -1462,7 +1503,7 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
 // bf16 default is the 12-B slot layout of dispatch_sg12).
 int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
-                  float* pred, float* loss, int grid, hipStream_t stream) {
+                  float* pred, float* loss, int grid, int variant, hipStream_t stream) {
     if (P.Kp != 4 || P.F > 45 || P.vpad <= 0) return -1;
     // tables of 4 GiB and more (-feature_hashing >= 23 at 896-B blocks): 64-bit slot offsets
     const bool wide = (size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32) ||
@@ -1471,9 +1512,11 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
 #define HM_P32(NSV) do { \
-        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, false>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 7) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, true>), dim3(blocks), dim3(256), 0, \
+                                                  stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, false>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
@@ -1526,13 +1569,13 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
             // 4 GiB and more (32-bit offsets there) take the generic kernel with 64-bit offsets
             // (slot stride 6 bf16, feature stride = the block)
             if (!BF) return (int)hipErrorInvalidValue;
-            const int rc = variant == 1 ? -1 : dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, stream);
+            const int rc = variant == 1 ? -1 : dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
             if (rc != -1) return rc;
             return launch_generic<true, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
         }
         if (variant != 1 && !BF && P.gfstride == 1) {
             const int rc = dispatch_sg32(P, idx, fld, val, y, V, reinterpret_cast<float*>(G), w, wz, wn,
-                                         bias, pred, loss, grid, stream);
+                                         bias, pred, loss, grid, variant, stream);
             if (rc != -1) return rc;
         }
         return launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);

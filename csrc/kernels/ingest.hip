@@ -76,9 +76,11 @@ __global__ __launch_bounds__(256) void ffm_parse_kernel(
     }
 }
 
-// mode 0: integer names; mode 2: mhash(name, num_features) (1-based)
+// mode 0: integer names; mode 2: mhash(name, num_features) (1-based).  OFF: the string
+// offsets' type (Arrow string: int32, large_string / rebased chunks: int64)
+template <typename OFF>
 __global__ __launch_bounds__(256) void feat_parse_kernel(
-    const uint8_t* __restrict__ data, const int64_t* __restrict__ soff, int64_t n, int mode,
+    const uint8_t* __restrict__ data, const OFF* __restrict__ soff, int64_t n, int mode,
     int32_t num_features, uint32_t seed, int64_t* __restrict__ idx_out, float* __restrict__ val_out,
     unsigned long long* __restrict__ err) {
     for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n; s += (int64_t)gridDim.x * 256) {
@@ -128,7 +130,17 @@ HM_API int hm_feat_parse(const uint8_t* data, const int64_t* soff, int64_t n, in
                          uint32_t seed, int64_t* idx, float* val, unsigned long long* err, hipStream_t stream) {
     if (n <= 0) return 0;
     if ((mode != 0 && mode != 2) || (mode == 2 && num_features <= 0)) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(feat_parse_kernel, dim3(blocks_for(n)), dim3(256), 0, stream, data, soff, n, mode,
+    hipLaunchKernelGGL(feat_parse_kernel<int64_t>, dim3(blocks_for(n)), dim3(256), 0, stream, data, soff, n, mode,
+                       num_features, seed, idx, val, err);
+    HM_LAUNCH_RET();
+}
+
+// hm_feat_parse with int32 string offsets (an Arrow string column's own offsets, no widening)
+HM_API int hm_feat_parse32(const uint8_t* data, const int32_t* soff, int64_t n, int mode, int32_t num_features,
+                           uint32_t seed, int64_t* idx, float* val, unsigned long long* err, hipStream_t stream) {
+    if (n <= 0) return 0;
+    if ((mode != 0 && mode != 2) || (mode == 2 && num_features <= 0)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(feat_parse_kernel<int32_t>, dim3(blocks_for(n)), dim3(256), 0, stream, data, soff, n, mode,
                        num_features, seed, idx, val, err);
     HM_LAUNCH_RET();
 }

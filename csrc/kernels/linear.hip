@@ -353,6 +353,17 @@ constexpr int HM_HOT_MAX = 8192;          // <= 96 KB of LDS accumulators
 // is used, so their round trips overlap instead of running back to back.
 constexpr int HM_HOT_U = 4;
 
+// The rules whose hot-feature gradients are pre-aggregated (hot_flush4): the general learner's
+// AdaGrad with no / L2 regularisation and AdaGrad-RDA (its running sums).  Applying a block's
+// MEAN gradient through the other rules' own updates was measured and rejected: momentum /
+// Adam-family / RMSprop-Graves diverge (held-out logloss +0.3 .. +29 vs sequential at 2^24,
+// profiles/r4/linear_rules_mean_step.jsonl); those rules run plain Hogwild with a per-rule cap
+// on the rows in flight (ops/linear.py RULE_WAVES).
+__host__ __device__ __forceinline__ bool hot_rda(const Params& P) { return P.reg == R_RDA && P.opt == O_ADAGRAD; }
+__host__ __device__ __forceinline__ bool hot_sum_rule(const Params& P) {
+    return P.algo == A_GENERAL && P.opt == O_ADAGRAD && (P.reg == R_NO || P.reg == R_L2 || P.reg == R_RDA);
+}
+
 __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__ S, float (&gs)[HM_HOT_U],
                                            float (&g2)[HM_HOT_U], const float (&cnt)[HM_HOT_U],
                                            const int (&f)[HM_HOT_U], const StepK& k) {
@@ -367,7 +378,7 @@ __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__
             gs[u] += cnt[u] * lw;
         }
     }
-    if (P.reg == R_RDA) {
+    if (hot_rda(P)) {
         // AdaGrad-RDA: only the running sums u = sum g, G = sum g^2 are stored; a hot
         // feature's w is recomputed from them where it is read (rda_w) and once after the pass
 #pragma unroll
@@ -461,7 +472,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             }
             F4 cst = {0.f, 0.f, 0.f, 0.f};
             float p = 0.f, sq = 0.f;
-            const bool hrda = HOT && P.reg == R_RDA;
+            const bool hrda = HOT && hot_rda(P);
             if (ci >= 0) {
                 cst = ld4m<NT>(S + ci);
                 p = (hrda && hs >= 0 ? rda_w(P, cst.s1, cst.s2, sk) : cst.w) * cx;
@@ -636,8 +647,7 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
     const bool hot = H > 0;
     const size_t lds = hot ? (size_t)H * 3 * sizeof(float) : 0;
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 || min_rows <= 0 || every <= 0 ||
-                P->algo != A_GENERAL || P->opt != O_ADAGRAD ||
-                (P->reg != R_NO && P->reg != R_L2 && P->reg != R_RDA)))
+                !hot_sum_rule(*P)))
         return (int)hipErrorInvalidValue;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \
@@ -648,7 +658,7 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
         else if (reload) HM_SHARED_LAUNCH(true, false, true);
         else if (nt) HM_SHARED_LAUNCH(false, true, true);
         else HM_SHARED_LAUNCH(false, false, true);
-        if (P->reg == R_RDA) {
+        if (hot_rda(*P)) {
             const int64_t tot = (int64_t)H * R;
             hipLaunchKernelGGL(hot_rda_finalize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *P,
                                reinterpret_cast<float4*>(S), dims, R, hot_feat, H, (float)(t0 + n_rows));

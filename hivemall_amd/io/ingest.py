@@ -33,6 +33,8 @@ _native.register_hip("hm_ffm_parse", [_native.c_p, _native.c_p, _native.c_p, _na
                                       _native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_p])
 _native.register_hip("hm_feat_parse", [_native.c_p, _native.c_p, _native.c_i64, _native.c_int, _native.c_i32,
                                        _native.c_u32, _native.c_p, _native.c_p, _native.c_p, _native.c_p])
+_native.register_hip("hm_feat_parse32", [_native.c_p, _native.c_p, _native.c_i64, _native.c_int, _native.c_i32,
+                                         _native.c_u32, _native.c_p, _native.c_p, _native.c_p, _native.c_p])
 
 NO_ERR = (1 << 64) - 1
 DEFAULT_SEED = 0x9747b28c
@@ -98,9 +100,11 @@ def _all_str_lists(rows) -> bool:
     return True
 
 
-def arrow_buffers(arr):
-    """(data uint8 ndarray, string offsets int64 [n+1], row offsets int64 [B+1]) of a list<string>
-    array, rebased to start at 0 (slices honoured, zero-copy views where possible)."""
+def arrow_buffers(arr, wide: bool = True):
+    """(data uint8 ndarray, string offsets [n+1], row offsets int64 [B+1]) of a list<string>
+    array, rebased to start at 0 (slices honoured, zero-copy views where possible).  The string
+    offsets are int64, or (``wide=False``) the column's own int32 offsets when it has them —
+    a zero-copy view unless they need rebasing."""
     import pyarrow as pa
 
     lo = np.array(arr.offsets, dtype=np.int64)
@@ -109,13 +113,17 @@ def arrow_buffers(arr):
         lo -= lo[0]
     bufs = vals.buffers()
     odt = np.int64 if pa.types.is_large_string(vals.type) else np.int32
-    so = np.frombuffer(bufs[1], dtype=odt)[vals.offset:vals.offset + len(vals) + 1].astype(np.int64) \
-        if bufs[1] is not None else np.zeros(1, np.int64)
+    if bufs[1] is None:
+        so = np.zeros(1, np.int64)
+    else:
+        so = np.frombuffer(bufs[1], dtype=odt)[vals.offset:vals.offset + len(vals) + 1]
+        if wide or odt == np.int64:
+            so = so.astype(np.int64)
     buf = bufs[2]
     data = np.frombuffer(buf, dtype=np.uint8) if buf is not None else np.zeros(0, np.uint8)
     data = data[int(so[0]):int(so[-1])] if len(so) else data[:0]
     if len(so) and so[0]:
-        so -= so[0]        # so is already a fresh int64 copy
+        so = so - so[0]
     return data, so, lo
 
 
@@ -151,7 +159,7 @@ class _Stager:
             ev.record(self.copy)
         self.done[s] = ev
         torch.cuda.current_stream(self.dev).wait_event(ev)
-        tdt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int64): torch.int64}
+        tdt = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32}
         return [dev[o:o + n].view(tdt[np.dtype(dt)]).view(*shape) if n else
                 torch.zeros(shape, dtype=tdt[np.dtype(dt)], device=self.dev) for o, n, dt, shape in views]
 
@@ -171,13 +179,15 @@ def _chunks(lo: np.ndarray, so: np.ndarray, chunk_rows: int):
     return chunks, cap
 
 
-def _ingest(arr, chunk_rows: int, dev, launch, host_chunk) -> IngestStats:
+def _ingest(arr, chunk_rows: int, dev, launch, host_chunk, narrow: bool = False) -> IngestStats:
     """Stage every row chunk's (bytes, string offsets, row offsets) through the double-buffered
     pinned slots, ``launch(k, r0, r1, s0, d_data, d_so, d_lo, err_k)`` its parse kernel, then
-    re-run the chunks the device refused through ``host_chunk(r0, r1)`` (one sync)."""
+    re-run the chunks the device refused through ``host_chunk(r0, r1)`` (one sync).
+    ``narrow``: ``launch`` takes int32 string offsets, so an Arrow string column's own offsets
+    travel as they are (half the offset bytes, no widening pass)."""
     st = IngestStats()
     t0 = time.perf_counter()
-    data, so, lo = arrow_buffers(arr)
+    data, so, lo = arrow_buffers(arr, wide=not narrow)
     B = len(lo) - 1
     st.rows, st.strings, st.bytes = B, len(so) - 1, int(data.size)
     chunks, cap = _chunks(lo, so, chunk_rows)
@@ -194,8 +204,9 @@ def _ingest(arr, chunk_rows: int, dev, launch, host_chunk) -> IngestStats:
             s0, s1 = int(lo[r0]), int(lo[r1])
             th = time.perf_counter()
             b0 = int(so[s0])
-            d_data, d_so, d_lo = stager.stage(k, [data[b0:int(so[s1])], so[s0:s1 + 1] - b0,
-                                                  lo[r0:r1 + 1] - s0])
+            sok = so[s0:s1 + 1] if b0 == 0 else so[s0:s1 + 1] - so.dtype.type(b0)
+            d_data, d_so, d_lo = stager.stage(k, [data[b0:int(so[s1])], sok,
+                                                  lo[r0:r1 + 1] if s0 == 0 else lo[r0:r1 + 1] - s0])
             host_s += time.perf_counter() - th
             launch(k, r0, r1, s0, d_data, d_so, d_lo, err[k:k + 1])
             stager.release(k)
@@ -268,9 +279,9 @@ def csr_device(features, mode: str, num_features: int = 0, device="cuda", chunk_
 
     def launch(k, r0, r1, s0, d_data, d_so, d_lo, e):
         n = int(lo[r1] - lo[r0])
-        rc = _native.hip().hm_feat_parse(d_data.data_ptr(), d_so.data_ptr(), n, m, int(num_features), seed,
-                                         idx[s0:].data_ptr(), val[s0:].data_ptr(), e.data_ptr(),
-                                         _native.stream_of(dev))
+        fn = _native.hip().hm_feat_parse32 if d_so.dtype == torch.int32 else _native.hip().hm_feat_parse
+        rc = fn(d_data.data_ptr(), d_so.data_ptr(), n, m, int(num_features), seed,
+                idx[s0:].data_ptr(), val[s0:].data_ptr(), e.data_ptr(), _native.stream_of(dev))
         _native.check(rc, "hm_feat_parse")
 
     def host_chunk(r0, r1):
@@ -280,7 +291,7 @@ def csr_device(features, mode: str, num_features: int = 0, device="cuda", chunk_
         idx[s0:s1].copy_(torch.from_numpy(csr.idx.astype(np.int64)))
         val[s0:s1].copy_(torch.from_numpy(csr.val.astype(np.float32)))
 
-    st = _ingest(arr, chunk_rows, dev, launch, host_chunk)
+    st = _ingest(arr, chunk_rows, dev, launch, host_chunk, narrow=True)
     return torch.from_numpy(lo).to(dev), idx, val, st
 
 
@@ -330,9 +341,9 @@ def hashed_csr_device(features, num_features: int, bias: bool, device="cuda",
 
     def launch(k, r0, r1, s0, d_data, d_so, d_lo, e):
         n = int(lo[r1] - lo[r0])
-        rc = _native.hip().hm_feat_parse(d_data.data_ptr(), d_so.data_ptr(), n, 2, int(num_features), seed,
-                                         idx[s0:].data_ptr(), val[s0:].data_ptr(), e.data_ptr(),
-                                         _native.stream_of(dev))
+        fn = _native.hip().hm_feat_parse32 if d_so.dtype == torch.int32 else _native.hip().hm_feat_parse
+        rc = fn(d_data.data_ptr(), d_so.data_ptr(), n, 2, int(num_features), seed,
+                idx[s0:].data_ptr(), val[s0:].data_ptr(), e.data_ptr(), _native.stream_of(dev))
         _native.check(rc, "hm_feat_parse")
 
     def host_chunk(r0, r1):
@@ -346,7 +357,7 @@ def hashed_csr_device(features, num_features: int, bias: bool, device="cuda",
         idx[s0:s1].copy_(torch.from_numpy(csr.idx.astype(np.int64)))
         val[s0:s1].copy_(torch.from_numpy(csr.val.astype(np.float32)))
 
-    st = _ingest(arr, chunk_rows, dev, launch, host_chunk)
+    st = _ingest(arr, chunk_rows, dev, launch, host_chunk, narrow=True)
     ip = torch.from_numpy(lo).to(dev)
     if bias:
         # row r's entries shift by r; its bias lands in the new last slot of the row

@@ -433,30 +433,37 @@ class OnlineLinearLearner(Learner):
             self.mix()
         return self._w, self._cov
 
-    def touched_features(self) -> np.ndarray:
+    def touched_features(self, device: bool = False):
+        """Ids of the features any replica (any rank) updated: numpy, or the device tensor."""
         t = self.state.touched.amax(0) if self.state.R > 1 else self.state.touched[0]
         if self._dp():   # one model table on every rank: features seen by any rank
             f = t.to(torch.float32)
             self.mixer.all_reduce_sum([f])
             t = f > 0
-        return torch.nonzero(t).flatten().cpu().numpy()
+        ids = torch.nonzero(t).flatten()
+        return ids if device else ids.cpu().numpy()
 
-    def _feature_names(self, ids: np.ndarray, arrow: bool = False):
+    def _feature_names(self, ids, arrow: bool = False):
+        """Model-table feature names of ``ids`` (numpy, or a device tensor)."""
+        if self.encoder is not None and getattr(self.encoder, "string_names", False) and arrow:
+            # integer-named string features (a feature_hashing result): an Arrow string column,
+            # formatted on the device when the ids live there (ops/touched.py int_strings:
+            # 2.9 M names 126 ms through pyarrow's host cast, 1.2 s as Python str objects)
+            from ..ops.touched import int_strings
+
+            t = ids if torch.is_tensor(ids) else torch.from_numpy(np.asarray(ids, dtype=np.int64))
+            return pd.arrays.ArrowExtensionArray(int_strings(t))
+        if torch.is_tensor(ids):
+            ids = ids.cpu().numpy()
         if self.encoder is not None and self.encoder.mode == "dict":
             return self.encoder.decode(ids)
         if self.encoder is not None and getattr(self.encoder, "string_names", False):
-            if arrow:
-                # integer-named string features (a feature_hashing result): an Arrow string
-                # column, formatted in C++ (2.9 M names: 0.2 s, 1.2 s as Python str objects)
-                import pyarrow as pa
-
-                return pd.arrays.ArrowExtensionArray(pa.array(np.asarray(ids, dtype=np.int64)).cast(pa.string()))
             return list(map(str, ids.tolist()))
         return ids.tolist()
 
     def model_table(self) -> pd.DataFrame:
         w, cov = self.weights()
-        ids = self.touched_features()
+        ids = self.touched_features(device=True)
         W = w[:, ids].cpu().numpy()
         names = self._feature_names(ids, arrow=self.TASK != "multiclass")
         C = cov[:, ids].cpu().numpy() if (cov is not None and self.covar) else None

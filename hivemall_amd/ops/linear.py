@@ -183,8 +183,10 @@ def hot_rule(P: LinParams) -> bool:
     """Rules whose hot features can be pre-aggregated: the general learner's AdaGrad with no / L2
     regularisation and AdaGrad-RDA, whose step is normalised by the accumulated squared
     gradient, so a block's summed gradient takes a bounded step.  Plain SGD applies the sum at
-    full rate and diverges (measured: held-out logloss 273 at eta0 0.05), so it stays Hogwild.
-    ``HM_LINEAR_HOT=0`` disables the pre-aggregation."""
+    full rate and diverges (measured: held-out logloss 273 at eta0 0.05); applying the block's
+    mean gradient through the other rules' updates diverges for momentum and the Adam family
+    (profiles/r4/linear_rules_mean_step.jsonl).  ``HM_LINEAR_HOT=0`` disables the
+    pre-aggregation."""
     if os.environ.get("HM_LINEAR_HOT", "1") == "0":
         return False
     return (P.algo == ALGOS["general"] and P.opt == OPTIMIZERS["adagrad"]

@@ -24,5 +24,6 @@ timeout -k 10 600 python -u benchmarks/sql_ftvec_bench.py 1000000 cuda arrow > $
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fm -o fm -- \
   python3 benchmarks/bench_configs.py fm > $O/prof_fm.log 2>&1
-timeout -k 10 600 python -u -m pytest tests/test_ffm.py tests/test_linear.py tests/test_sql.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || true
+timeout -k 10 900 python -u -m pytest tests/test_ffm.py tests/test_linear.py tests/test_sql.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || true
 tail -4 $O/pytest.log
+timeout -k 10 900 python -u benchmarks/linear_rules_parity.py 1000000 > $O/linear_rules.jsonl 2>&1

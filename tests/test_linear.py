@@ -232,13 +232,19 @@ def test_gpu_shared_engine_one_wave_is_sequential(name, opts, reload):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6"])
+@pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6",
+                                  "-opt adagrad -reg l1 -lambda 1e-6", "-opt sgd -eta0 0.05",
+                                  "-opt momentum -eta0 0.05", "-opt nesterov -eta0 0.05", "-opt rmsprop",
+                                  "-opt rmspropgraves", "-opt adadelta", "-opt adam", "-opt nadam",
+                                  "-opt eve", "-opt adamhd"])
 def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
-    """Hivemall's default -dims 2^24 (hashed Criteo-shaped rows, 39 nnz): auto picks the shared
-    table, 1,024 rows in flight, with the hot features' gradients summed per block in LDS and
-    applied by atomics (csrc/kernels/linear.hip HOT), so no hot update is lost.  Held-out logloss
-    after one epoch within 5e-3 of the sequential CPU engine (plain Hogwild: 0.018 at 2 M rows;
-    pre-aggregated: -7e-4, profiles/linear_hot_r3/)."""
+    """Hivemall's default -dims 2^24 (hashed Criteo-shaped rows, 39 nnz), every -opt of the general
+    learner: auto picks the shared table, 1,024 rows in flight, with the hot features' gradients
+    pre-aggregated per block in LDS (csrc/kernels/linear.hip HOT: AdaGrad sums applied by
+    atomics, every other rule one step of its own update with the block's mean gradient).
+    Held-out logloss after one epoch within 5e-3 of the sequential CPU engine (AdaGrad plain
+    Hogwild: 0.018 at 2 M rows; pre-aggregated: -7e-4, profiles/linear_hot_r3/; every rule:
+    benchmarks/linear_rules_parity.py, profiles/r4/)."""
     rows = _criteo_rows(200000, 24, seed=5)
     test = _criteo_rows(50000, 24, seed=99)
     yy = (test.y > 0).float()
