@@ -36,6 +36,7 @@ struct FMParams {
     float min_target, max_target;
     int use_w0;
     int w0_shards;            // w0 = sum of w0[0..w0_shards) (<= 64)
+    int w0_every;             // fm_pipe_kernel: rows between re-reads of the w0 shards (>= 1)
     uint32_t seed;
 };
 
@@ -257,9 +258,13 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
     // (one row of extra staleness on a parameter every wave of the chip updates anyway)
     float w0part = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
     float yy = y ? y[gw] : 0.f;
-    for (int64_t row = gw; row < n_rows; row += nw) {
+    int it = 0;
+    for (int64_t row = gw; row < n_rows; row += nw, ++it) {
         const int nnz = (int)(e - s);
         int i = (ci >= 0 && ci < P.dims) ? ci : -1;
+        // the w0 shards are re-read every w0_every rows; in between the wave adds its own
+        // deltas to its copy (lane 0), so only the other waves' updates are seen late
+        const bool w0_ref = P.w0_every <= 1 || ((it + 1) % P.w0_every) == 0;
         float x = i >= 0 ? cx : 0.f;
         // ---- gathers of this row (the only loads the forward waits for) ----
         VRow<KP, BF16> vr;
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
         float px = 0.f, pw0 = 0.f, py = 0.f;
         int64_t ns2 = 0, ne2 = 0;
         if (nrow < n_rows) {
-            pw0 = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
+            if (w0_ref) pw0 = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
             py = y ? y[nrow] : 0.f;
             if (lane < ne - ns) {
                 pi = idx[ns + lane];
@@ -365,11 +370,15 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
                 t.load(V, i2);
                 upd(t, i2, x2, w[i2]);
             }
-            if (P.use_w0 && lane == 0)
-                atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, -eta * (d + 2.f * P.lambda0 * w0v));
+            if (P.use_w0 && lane == 0) {
+                const float dw0 = -eta * (d + 2.f * P.lambda0 * w0v);
+                atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, dw0);
+                w0part += dw0;
+            }
         }
         // rotate the pipeline
-        s = ns; e = ne; ci = pi; cx = px; w0part = pw0; yy = py;
+        s = ns; e = ne; ci = pi; cx = px; yy = py;
+        if (w0_ref) w0part = pw0;
         ns = ns2; ne = ne2;
     }
 }
@@ -401,7 +410,8 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 
 }  // namespace
 
-// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant
+// ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant,
+//     w0_every
 //     (variant 0 = fm_pipe_kernel, 1 = fm_kernel)
 // hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
@@ -415,6 +425,7 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     P.seed = (uint32_t)ip[9];
     P.w0_shards = ip[10];
     const int variant = ip[11];
+    P.w0_every = ip[12] > 0 ? ip[12] : 1;
     if (P.w0_shards < 1 || P.w0_shards > 64) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];

@@ -29,6 +29,11 @@ class FMHyper:
     seed: int = 31
 
 
+# rows between a wave's re-reads of the 64 global-bias shards (csrc/kernels/fm.hip fm_pipe_kernel);
+# each re-read is 64 lines the other waves' atomics have just dropped from L2
+W0_EVERY = 1
+
+
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
             y: torch.Tensor | None, h: FMHyper, k: int, train: bool = True, t0: int = 0,
             pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0) -> None:
@@ -52,7 +57,8 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     bf16 = V.dtype == torch.bfloat16
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
-                   int(os.environ.get("HM_FM_VARIANT", "0"))], dtype=np.int32)
+                   int(os.environ.get("HM_FM_VARIANT", "0")),
+                   int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY)))], dtype=np.int32)
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,
                    h.min_target, h.max_target], dtype=np.float32)
