@@ -63,6 +63,10 @@ def parse_args(argv=None):
                     help="1: stale-by-one mixing overlapped with compute (async MixServer semantics); "
                          "0: synchronous (the FFM kernel holds every CU, so the overlap hid ~nothing: "
                          "docs/perf_notes.md)")
+    ap.add_argument("--mix-wire", choices=("auto", "native", "bf16_delta"), default="auto",
+                    help="bf16_delta: fp32 replicas send their step since the last mix in bf16 "
+                         "(half the bytes; fp32 consensus, parallel/mix.py average_delta); auto = "
+                         "bf16_delta for fp32 state, native otherwise")
     ap.add_argument("--dp-lr-power", type=float, default=None,
                     help="N > 1: every replica steps with eta0 * N^p, alpha * N^p (default: "
                          "models.ffm.DP_LR_POWER)")
@@ -190,6 +194,9 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     if args.mix_state:
         mix_tensors.append(st["G"])
     overlap = OverlappedMixer(mixer, args.mix_mode, args.mix_power) if args.mix_overlap else None
+    wire = args.mix_wire if args.mix_wire != "auto" else (
+        "bf16_delta" if st["V"].dtype == torch.float32 and args.mix_mode == "mean" else "native")
+    sync_mix = mixer.average_delta if wire == "bf16_delta" else mixer.average
     loss_buf = torch.empty(B, dtype=torch.float32, device=dev) if metrics is not None else None
     step_loss = []
 
@@ -204,7 +211,7 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
             if overlap is not None:
                 overlap.start(mix_tensors)   # finishes the previous mix, launches this one
             else:
-                mixer.average(mix_tensors)
+                sync_mix(mix_tensors)
 
     def sync():
         if dev.type == "cuda":
@@ -269,11 +276,12 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
             sync()
 
     # ---- mix cost on its own (synchronous, outside the timed region); leaves the model mixed ----
-    out["probe"] = mixer.probe(mix_tensors, args.mix_probe) if world > 1 else {}
+    out["probe"] = mixer.probe(mix_tensors, args.mix_probe, fn=sync_mix) if world > 1 else {}
+    out["mix_wire"] = wire
     # ---- quality: final mix, then held-out logloss vs the planted-model floor ----
     t = time.perf_counter()
     if world > 1:
-        mixer.average(mix_tensors)
+        sync_mix(mix_tensors)
     out["ll"] = None
     if rank == 0:
         eidx, efld, evl, ey, elogit = data["eval"]
@@ -386,6 +394,7 @@ def main(argv=None):
                 "mixed_bytes_per_mix": main_run["mixed_bytes"],
                 "mixes_in_timed_region": main_run["mixes_timed"],
                 "mix_overlapped": bool(args.mix_overlap),
+                "mix_wire": main_run["mix_wire"],
                 "dp_lr_scale": round(main_run["dp_lr_scale"], 4),
                 "resident_batches": nres,
             },

@@ -97,14 +97,14 @@ def _view3(t: torch.Tensor):
 class _FlatGroup:
     """Same-dtype tensors packed into one flat wire buffer, padded to a multiple of 4*world."""
 
-    def __init__(self, tensors: list[torch.Tensor], world: int):
+    def __init__(self, tensors: list[torch.Tensor], world: int, wire: torch.dtype | None = None):
         # weak references: a cached plan must not keep a discarded model alive in HBM
         self._refs = [weakref.ref(t) for t in tensors]
         self.shapes = [tuple(t.shape) for t in tensors]
         self.busy = False            # an OverlappedMixer collective is in flight on the buffers
         self.prepacked = False       # send already holds the current snapshot (fused merge)
-        self.base: torch.Tensor | None = None   # fp32 consensus of the last mix (delta-sum mode)
-        self.dtype = tensors[0].dtype
+        self.base: torch.Tensor | None = None   # fp32 consensus of the last mix (delta modes)
+        self.dtype = wire if wire is not None else tensors[0].dtype     # the wire's dtype
         dev = tensors[0].device
         self.offs = []
         off = 0
@@ -314,6 +314,45 @@ class ModelMixer:
             g.unpack()
         self._count(groups, tensors)
 
+    # ---------------------------------------------------------------- mean of deltas, bf16 wire
+    def average_delta(self, tensors: list[torch.Tensor], wire: torch.dtype = torch.bfloat16) -> None:
+        """In-place replica mean with half the wire bytes for fp32 replicas: every rank keeps the
+        fp32 consensus ``base`` of the last mix and sends ``x - base`` (the progress since then)
+        in ``wire`` (bf16); the shard mean of the deltas is summed in fp32 (csrc/kernels/mix.hip)
+        and gathered in ``wire``; every rank then sets ``x = base = base + mean_delta`` — the same
+        fp32 value everywhere.  Only the step since the last mix is rounded (a relative 2^-9 of
+        the step, not of the weight).  The first call (no consensus yet) is a full-precision
+        :meth:`average`, which also seeds ``base``."""
+        if not self._active():
+            return
+        key = ("delta", wire) + tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) for t in tensors)
+        p = self._plans.get(key)
+        g = p[0] if p is not None else None
+        if g is not None and not g.matches(tensors):
+            del self._plans[key]
+            g = None
+        if g is None:
+            self.average(tensors)
+            g = _FlatGroup(tensors, self.world, wire=wire)
+            g.base = torch.empty(g.n, dtype=torch.float32, device=tensors[0].device)
+            g.buf_bytes += g.n * 4
+            for k, t in enumerate(g.tensors):
+                g.seg(g.base, k).copy_(t)
+            self._plans[key] = [g]
+            self._evict(keep=key)
+            return
+        for k, t in enumerate(g.tensors):
+            g.seg(g.send, k).copy_(t.to(torch.float32) - g.seg(g.base, k))
+        self._a2a(g)
+        g.shard_mean(self.world)
+        self._gather(g)
+        g.base.add_(g.out.to(torch.float32))
+        for k, t in enumerate(g.tensors):
+            t.copy_(g.seg(g.base, k))
+        self.calls += 1
+        self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
+        self.wire_bytes += 2 * (self.world - 1) * g.nbytes // self.world
+
     # ---------------------------------------------------------------- sum all-reduce
     def all_reduce_sum(self, tensors: list[torch.Tensor]) -> None:
         """In-place SUM all-reduce of a list of tensors (bucketed, async).  bf16/fp16 tensors are
@@ -389,16 +428,18 @@ class ModelMixer:
         return float(t.item())
 
     # ---------------------------------------------------------------- measurement
-    def probe(self, tensors: list[torch.Tensor], reps: int = 3) -> dict:
-        """Time ``reps`` synchronous shard-mean mixes of ``tensors`` (device events on the GPU,
-        after a barrier); returns ms per mix, wire bytes per rank and bus GB/s (nccl-tests
-        convention: 2(N-1)/N * payload / time).  The tensors are left mixed."""
+    def probe(self, tensors: list[torch.Tensor], reps: int = 3, fn=None) -> dict:
+        """Time ``reps`` synchronous mixes of ``tensors`` by ``fn`` (default :meth:`average`;
+        device events on the GPU, after a barrier); returns ms per mix, wire bytes per rank and
+        bus GB/s (nccl-tests convention: 2(N-1)/N * payload / time).  The tensors are left mixed."""
         if not self._active() or reps <= 0:
             return {}
-        groups = self.plan(tensors)
-        payload = sum(g.nbytes for g in groups)
-        wire = sum(2 * (self.world - 1) * g.nbytes // self.world for g in groups)
-        self.average(tensors)                      # warm the communicators / buffers
+        fn = fn or self.average
+        fn(tensors)                                # warm the communicators / buffers
+        w1 = self.wire_bytes                       # (average_delta: the first call seeds it)
+        fn(tensors)
+        wire = self.wire_bytes - w1                # bytes one rank sends per mix
+        payload = wire * self.world // max(1, 2 * (self.world - 1))
         self.ctx.barrier()
         cuda = tensors[0].is_cuda
         if cuda:
@@ -407,7 +448,7 @@ class ModelMixer:
             e0.record()
         t0 = time.perf_counter()
         for _ in range(reps):
-            self.average(tensors)
+            fn(tensors)
         if cuda:
             e1.record()
             e1.synchronize()
@@ -418,7 +459,8 @@ class ModelMixer:
         return {"mix_ms": round(ms, 4), "mix_payload_bytes": int(payload),
                 "mix_wire_bytes_per_rank": int(wire),
                 "mix_bus_gbps": round(wire / (ms * 1e-3) / 1e9, 2) if ms > 0 else None,
-                "mix_algo": "all_to_all + fp32 shard mean + all_gather"}
+                "mix_algo": "all_to_all + fp32 shard mean + all_gather" +
+                            (" (bf16 deltas, fp32 consensus)" if fn == self.average_delta else "")}
 
 
 class OverlappedMixer:

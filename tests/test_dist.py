@@ -399,3 +399,34 @@ def test_ffm_logloss_parity_world4_gloo():
     assert abs(rec["delta"]) <= 1e-3, rec
     # N replicas mixed never do worse than one rank trained on its own share
     assert rec["logloss_N"] <= rec["logloss_1_same_steps"], rec
+
+
+def _avg_delta(ctx):
+    """average_delta: bf16 deltas on the wire, fp32 consensus; every rank ends bit-identical,
+    within a bf16 rounding of the step of the exact fp32 mean."""
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    m = ModelMixer(ctx)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(50, 7, 4, generator=g)             # identical start on both ranks
+    v = x[:, :5]                                       # a strided view, as the FFM V blocks
+    m.average_delta([v])                               # first call: full precision + consensus
+    exact = v.clone()
+    res = []
+    for it in range(3):
+        step = torch.randn(50, 5, 4, generator=torch.Generator().manual_seed(10 * it + ctx.rank)) * 1e-2
+        v += step
+        ref = exact + (step + torch.randn(50, 5, 4, generator=torch.Generator().manual_seed(10 * it + 1 - ctx.rank)) * 1e-2) / 2
+        m.average_delta([v])
+        res.append(float((v - ref).abs().max()))
+        exact = ref
+    return res, float(v.double().sum()), float(x[:, 5:].abs().sum())
+
+
+def test_mix_average_delta_bf16_wire():
+    out = run_world("_avg_delta")
+    for r in (0, 1):
+        errs, _, _ = out[r]
+        assert max(errs) < 2e-4, errs            # bf16 rounding of a ~1e-2 step (2^-9 relative)
+    assert out[0][1] == out[1][1]                  # bit-identical replicas
+    assert out[0][2] == out[1][2]                  # elements outside the view untouched
