@@ -983,20 +983,20 @@ __device__ __forceinline__ void st_lin(float* p, float v) {
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS, typename OT, bool COH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffm_pipe_sg32_kernel(
+template <int NS, typename OT, bool COH, int TPB = 256>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
     float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
-    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * 256];    // V DMA landing zone
-    __shared__ __attribute__((aligned(16))) float s_rg[NS * 256];     // G DMA landing zone
-    __shared__ __attribute__((aligned(16))) float4 s_t[NS * 256];     // transposed V image
+    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB];    // V DMA landing zone
+    __shared__ __attribute__((aligned(16))) float s_rg[NS * TPB];     // G DMA landing zone
+    __shared__ __attribute__((aligned(16))) float4 s_t[NS * TPB];     // transposed V image
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
-    __shared__ float s_red[8];                                        // [0..3] sums, [4+b] scale
+    __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     int ab[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-        const int s = tid + j * 256;
+        const int s = tid + j * TPB;
         ab[j] = s < FF ? (s / F) | ((s % F) << 8) : 0;
     }
 #define SA(j) (ab[j] & 0xFF)
@@ -1037,13 +1037,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                 sq = rx * rx;
             }
             const float tot = hm::wave_sum_uniform(sq);
-            if (lane == 0) s_red[4 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
+            if (lane == 0) s_red[TPB / 64 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
         }
     };
     // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal, 0 = dead
     auto slot = [&](int bf, int j, OT& ov, OT& og, float& xab) -> uint32_t {
         const int4 ma = s_m[bf][SA(j)], mb = s_m[bf][SB(j)];
-        const bool ok = (ma.x | mb.x) >= 0 && tid + j * 256 < FF;
+        const bool ok = (ma.x | mb.x) >= 0 && tid + j * TPB < FF;
         const bool live = ok && SA(j) != SB(j);
         const OT i = ok ? (OT)(uint32_t)ma.x : (OT)0, f = ok ? (OT)(uint32_t)mb.y : (OT)0;
         ov = i * vfs + f * 16u;
@@ -1057,8 +1057,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             OT ov, og;
             float xab;
             slot(bf, j, ov, og, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * 256 + wave * 64), 16, 0, COH ? CPOL_SC1 : 0);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * 256 + wave * 64), 4, 0, COH ? CPOL_SC1 : 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, COH ? CPOL_SC1 : 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, COH ? CPOL_SC1 : 0);
         }
     };
     auto dma_lin = [&](int bf) {
@@ -1095,8 +1095,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            cg[j] = s_rg[j * 256 + tid];
-            if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = s_rv[j * 256 + tid];
+            cg[j] = s_rg[j * TPB + tid];
+            if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = s_rv[j * TPB + tid];
         }
         if (more) publish_meta(nxt);
         bar_raw();
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             dma_slots(nxt);
             dma_meta(cur, row + 2 * G);
         }
-        const float scale = s_red[4 + cur];
+        const float scale = s_red[TPB / 64 + cur];
         int mi = -1;
         float mx = 0.f, lw = 0.f;
         if (wave == W_LIN && lane < F) {
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            const int s = tid + j * 256;
+            const int s = tid + j * TPB;
             const float4 pv = s_t[s < FF ? s : 0];
             const float4 cv = s_t[SB(j) * F + SA(j)];
             part += (cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w) * xab[j];
@@ -1134,7 +1134,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         part = hm::wave_sum_uniform(part);
         if (lane == 0) s_red[wave] = part;
         bar_raw();
-        float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        float p = 0.f;
+#pragma unroll
+        for (int q = 0; q < TPB / 64; ++q) p += s_red[q];
         if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
@@ -1147,7 +1149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                 OT ov, og;
                 float xj;
                 slot(cur, j, ov, og, xj);
-                const int s = tid + j * 256;
+                const int s = tid + j * TPB;
                 const float4 pv = s_t[s];
                 const float4 cv = s_t[SB(j) * F + SA(j)];
                 const float c = ks * xab[j];
@@ -1170,7 +1172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             {
                 const int npad = P.vpad - P.num_fields;
                 const int per = 2 * npad + P.tail16;
-                for (int q = tid; q < F * per; q += 256) {
+                for (int q = tid; q < F * per; q += TPB) {
                     const int a = q / per, kk = q - a * per;
                     const int i = s_m[cur][a].x;
                     if (i < 0) continue;
@@ -1518,6 +1520,18 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                                   stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, false>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
+    if (variant == 8 && !wide) {
+        // 512-thread blocks (8 waves per row, half the slots per wave): twice the waves per CU
+        // at the same rows in flight (A/B)
+        const int need5 = (P.F * P.F + 511) / 512;
+#define HM_P32W(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, false, 512>), dim3(blocks), dim3(512), 0, \
+                                        stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
+        if (need5 <= 2) { HM_P32W(2); }
+        else if (need5 <= 3) { HM_P32W(3); }
+        else { HM_P32W(4); }
+#undef HM_P32W
+        HM_LAUNCH_RET();
+    }
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }
