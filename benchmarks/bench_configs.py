@@ -105,7 +105,8 @@ def bench_fm(dev="cuda", n_rows=8 * 262144, bits=24):
     idx, y = criteo_like(n_rows, bits, seed=5, device=dev)
     rows = SparseRows(torch.arange(0, n_rows * 39 + 1, 39, dtype=torch.int64, device=dev),
                       idx.reshape(-1).contiguous(), None, y)
-    t = FMTrainer(f"-c -factors 8 -num_features {1 << bits} -eta0 0.01 -sigma 0.01", device=dev)
+    extra = os.environ.get("HM_BENCH_FM_OPTS", "")         # A/B knobs, e.g. "-grid 512"
+    t = FMTrainer(f"-c -factors 8 -num_features {1 << bits} -eta0 0.01 -sigma 0.01 {extra}", device=dev)
     t.fit(rows=rows)
     _sync(dev)
     t0 = time.perf_counter()

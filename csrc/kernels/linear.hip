@@ -551,8 +551,11 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                     gs[u] = h < H ? s_acc[h] : 0.f;
                     g2[u] = h < H ? s_acc[H + h] : 0.f;
                     cnt[u] = h < H ? s_acc[2 * H + h] : 0.f;
-                    // a hot feature whose rows all had a zero gradient needs no update either
-                    f[u] = g2[u] != 0.f && (all || cnt[u] >= (float)min_rows) ? hot_feat[h] : -1;
+                    // a hot feature whose rows all had a zero loss gradient needs no update —
+                    // unless L2 decays it on every row that holds it (the sequential rule's
+                    // g = 0 + lambda w)
+                    f[u] = (g2[u] != 0.f || (P.reg == R_L2 && cnt[u] > 0.f)) && (all || cnt[u] >= (float)min_rows)
+                               ? hot_feat[h] : -1;
                     if (f[u] >= 0) {
                         s_acc[h] = 0.f;
                         s_acc[H + h] = 0.f;

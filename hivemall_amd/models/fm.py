@@ -80,6 +80,8 @@ FM_OPTS = [
     flag("disable_cv", "disable_cvtest", "Disable convergence check"),
     flag("fp32", None, "[engine] keep V in fp32 on the GPU (default bf16)"),
     opt("batch_size", None, 1 << 20, int, "[engine] rows per kernel launch"),
+    opt("grid", None, 0, int, "[engine] kernel workgroups: the Hogwild rows in flight / 4 "
+                              "(0 = auto: 256)"),
     opt("engine", None, "rowwise", str, "[engine] rowwise (per-row Hogwild kernel) | minibatch "
         "(dense mini-batch GEMMs + AdaGrad; for low-dimensional dense rows, models/fm_dense.py)"),
     opt("mini_batch", None, 8192, int, "[engine] rows per step of -engine minibatch"),
@@ -118,7 +120,7 @@ class FMTrainer(Learner):
             self.dims = (1 << int(c["feature_hashing"])) + 1
         self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
         self.t = 0
-        self.grid = 0
+        self.grid = int(c["grid"])
 
     # ------------------------------------------------------------------ state
     def init_state(self, dims: int) -> dict:
