@@ -247,19 +247,30 @@ def bench_gbdt_dp(n=11_000_000, trees=100, depth=8, xgb=False):
     kw = dict(device=dev, mixer=mixer, rank=ctx.rank)
     if xgb:
         XGBoostClassifier("-num_round 2 -max_depth 6", **kw).fit(X[:100000], y[:100000])
+    else:
+        GradientTreeBoostingClassifier("-trees 2 -max_depth 8", **kw).fit(X[:100000], y[:100000].long())
+    # the per-level histogram all-reduces, timed on the compute stream
+    mixer.time_collectives(True)
+    hist_bytes = mixer.bytes_reduced
+    if xgb:
         m, dt = _timed(ctx, mixer, lambda: XGBoostClassifier(
             f"-num_round {trees} -max_depth {depth} -eta 0.1", **kw).fit(X, y))
     else:
-        GradientTreeBoostingClassifier("-trees 2 -max_depth 8", **kw).fit(X[:100000], y[:100000].long())
         m, dt = _timed(ctx, mixer, lambda: GradientTreeBoostingClassifier(
             f"-trees {trees} -eta 0.1 -max_depth {depth} -subsample 1.0", **kw).fit(X, y.long()))
+    ar_ms = mixer.all_reduce_scalar(mixer.collective_ms(), "max")
+    hist_bytes = mixer.bytes_reduced - hist_bytes
+    mixer.time_collectives(False)
     Xt, yt = higgs_like(500000, seed=9, device=dev)
     auc = roc_auc_score(yt.cpu().numpy(), m.predict_proba(Xt)[:, -1])
     name = "train_xgboost binary:logistic" if xgb else "GBT classifier"
     return {"config": f"{name}, HIGGS-shaped {n} x 28 rows sharded over {ctx.world_size} ranks, depth {depth}, "
                       f"{trees} trees, per-level histogram all-reduce", "device": str(dev), "seconds": round(dt, 3),
             "ms_per_tree": round(dt * 1e3 / trees, 2), "row_trees_per_s": round(n * trees / dt),
-            "test_auc": round(float(auc), 4), **_dist_fields(ctx)}
+            "test_auc": round(float(auc), 4),
+            "hist_allreduce_ms_per_tree": round(ar_ms / trees, 3) if ctx.world_size > 1 else 0.0,
+            "hist_allreduce_mb_per_tree": round(hist_bytes / trees / 2**20, 2),
+            **_dist_fields(ctx)}
 
 
 def bench_rf_dp(n=11_000_000, trees=48, depth=12):

@@ -39,6 +39,8 @@ template <int FGW> struct BinWords;
 template <> struct BinWords<1> { using T = uint32_t; };
 template <> struct BinWords<2> { using T = uint2; };
 template <> struct BinWords<4> { using T = uint4; };
+struct alignas(32) U8W { uint4 a, b; };             // 32 features: one 32-B row of bins
+template <> struct BinWords<8> { using T = U8W; };
 
 // Rows handled per thread per step: all their loads are issued before the first atomic, so a
 // wave keeps HIST_U row gathers (index -> stats + bin words) in flight instead of one.
@@ -69,8 +71,11 @@ __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int 
                     w[u][0] = v;
                 } else if constexpr (FGW == 2) {
                     w[u][0] = v.x; w[u][1] = v.y;
-                } else {
+                } else if constexpr (FGW == 4) {
                     w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                } else {
+                    w[u][0] = v.a.x; w[u][1] = v.a.y; w[u][2] = v.a.z; w[u][3] = v.a.w;
+                    w[u][4] = v.b.x; w[u][5] = v.b.y; w[u][6] = v.b.z; w[u][7] = v.b.w;
                 }
             }
         }
@@ -96,8 +101,8 @@ __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int 
     }
 }
 
-template <int NS, int FGW>
-__global__ __launch_bounds__(256) void hist_kernel(const uint8_t* __restrict__ bins, int d, int dpad,
+template <int NS, int FGW, int TPB = 256>
+__global__ __launch_bounds__(TPB) void hist_kernel(const uint8_t* __restrict__ bins, int d, int dpad,
                                                    int B, const int32_t* __restrict__ rows,
                                                    const int64_t* __restrict__ seg, int n_seg,
                                                    const float* __restrict__ stats,
@@ -794,10 +799,14 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
                          int NS, int FG, float* hist, int nblk, hipStream_t stream) {
     if (n_seg <= 0) return 0;
     if (nblk <= 0) nblk = 1024;
-    if (B > 256 || NS <= 0 || NS > 8 || (FG != 4 && FG != 8 && FG != 16) || (dpad & 15))
+    if (B > 256 || NS <= 0 || NS > 8 || (FG != 4 && FG != 8 && FG != 16 && FG != 32) || (dpad & 15) ||
+        (FG == 32 && (dpad & 31)))
         return (int)hipErrorInvalidValue;
-    const size_t lds = (size_t)FG * B * NS * sizeof(float);
-    if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+    // FG = 32: every feature of a <= 32-feature row in one pass -- one 32-B bins load, one row
+    // index and one stats load per row instead of one each per 16-feature group -- into one LDS
+    // image of up to 160 KB shared by a 1024-thread block (16 waves hide the row gathers).
+    const size_t lds = (size_t)(FG == 32 ? min(d, 32) : FG) * B * NS * sizeof(float);
+    if (lds > (FG == 32 ? 160 * 1024 : 64 * 1024)) return (int)hipErrorInvalidValue;
     const dim3 grid((unsigned)nblk, (unsigned)((d + FG - 1) / FG));
 #define HM_H(K, W)                                                                                  \
     case K * 100 + W:                                                                               \
@@ -805,6 +814,24 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
                            seg, n_seg, stats, smax, hist);                                          \
         break;
 #define HM_HN(K) HM_H(K, 1) HM_H(K, 2) HM_H(K, 4)
+    if (FG == 32) {
+        switch (NS) {
+#define HM_HW(K) case K: { \
+            static bool attr_set = false; \
+            if (!attr_set) { \
+                hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, 8, 1024>), \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+                attr_set = true; \
+            } \
+            hipLaunchKernelGGL((hist_kernel<K, 8, 1024>), grid, dim3(1024), lds, stream, bins, d, dpad, B, rows, seg, \
+                               n_seg, stats, smax, hist); \
+            break; }
+            HM_HW(1) HM_HW(2) HM_HW(3) HM_HW(4)
+#undef HM_HW
+            default: return (int)hipErrorInvalidValue;
+        }
+        HM_LAUNCH_RET();
+    }
     switch (NS * 100 + FG / 4) {
         HM_HN(1) HM_HN(2) HM_HN(3) HM_HN(4) HM_HN(5) HM_HN(6) HM_HN(7) HM_HN(8)
         default: return (int)hipErrorInvalidValue;

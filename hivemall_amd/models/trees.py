@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import math
+import os
 import zlib
 from dataclasses import dataclass, field
 
@@ -37,6 +38,8 @@ MODEL_VERSION = 1
 CAT_FLAG = 1 << 30   # nominal split flag in flattened node arrays (HM_TREE_CAT in trees.hip)
 DLEFT_FLAG = 1 << 29  # missing values go left at this split (HM_TREE_DLEFT)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
+HIST_WIDE = os.environ.get("HM_HIST_WIDE", "0") == "1"   # all-features single-pass histogram
+HIST_WIDE_BLOCKS = int(os.environ.get("HM_HIST_WIDE_BLOCKS", "256"))
 
 
 # ------------------------------------------------------------------ quantisation
@@ -440,11 +443,15 @@ class HistTreeBuilder:
                               "hm_hist_build")
                 hist[..., c0:c1] = sub
         else:
-            # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB
+            # features per group: one aligned 16/8/4-byte bins load per row, LDS image <= 48 KB;
+            # or all <= 32 features in one pass (32-B bins rows, one <= 160 KB image per CU)
             FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
+            nblk = HIST_BLOCKS
+            if HIST_WIDE and q.d <= 32 and q.dpad % 32 == 0 and q.d * q.B * NS * 4 <= 160 * 1024:
+                FG, nblk = 32, HIST_WIDE_BLOCKS
             args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), p(smax), NS, FG, p(hist))
             if dev.type == "cuda":
-                _native.check(_native.hip().hm_hist_build(*args, HIST_BLOCKS, _native.stream_of(dev)),
+                _native.check(_native.hip().hm_hist_build(*args, nblk, _native.stream_of(dev)),
                               "hm_hist_build")
             else:
                 _native.host().hm_hist_build_cpu(*args)

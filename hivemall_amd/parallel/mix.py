@@ -353,12 +353,52 @@ class ModelMixer:
         self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
         self.wire_bytes += 2 * (self.world - 1) * g.nbytes // self.world
 
+    # ---------------------------------------------------------------- collective timing
+    def time_collectives(self, on: bool = True) -> None:
+        """Start (or stop) timing the sum all-reduces: events on the caller's stream bracket each
+        call, from its first enqueue to the point the stream may use the result, so the total is
+        the time the computation waits on the fabric (no host sync per call)."""
+        self._timings = [] if on else None
+
+    def collective_ms(self) -> float:
+        """Milliseconds the timed sum all-reduces held the computation (time_collectives)."""
+        total = 0.0
+        for a, b in getattr(self, "_timings", None) or []:
+            if isinstance(a, float):
+                total += (b - a) * 1e3
+            else:
+                b.synchronize()
+                total += a.elapsed_time(b)
+        return total
+
+    def _time_start(self, t: torch.Tensor):
+        if getattr(self, "_timings", None) is None:
+            return None
+        if t.is_cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        import time
+        return time.perf_counter()
+
+    def _time_end(self, start) -> None:
+        if start is None:
+            return
+        if isinstance(start, float):
+            import time
+            self._timings.append((start, time.perf_counter()))
+        else:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._timings.append((start, e))
+
     # ---------------------------------------------------------------- sum all-reduce
     def all_reduce_sum(self, tensors: list[torch.Tensor]) -> None:
         """In-place SUM all-reduce of a list of tensors (bucketed, async).  bf16/fp16 tensors are
         summed in fp32 (an N-way sum rounded at every ring hop would lose their low bits)."""
         if not self._active():
             return
+        ev = self._time_start(tensors[0])
         small = [t for t in tensors if t.numel() * t.element_size() <= self.small_bytes]
         big = [t for t in tensors if t.numel() * t.element_size() > self.small_bytes]
         works = []
@@ -389,6 +429,7 @@ class ModelMixer:
                 n = t.numel()
                 t.copy_(flat[off:off + n].view_as(t).to(t.dtype))
                 off += n
+        self._time_end(ev)
         self.calls += 1
         nb = sum(t.numel() * t.element_size() for t in tensors)
         self.bytes_reduced += nb
