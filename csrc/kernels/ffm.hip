@@ -939,41 +939,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
 }
 
 
-// Cache policy of the "coherent" variants (HM_FFM_VARIANT=7): per-XCD L2s are not coherent and
-// a CU's L1 is never refreshed by other CUs' stores (MI355X_MICROARCH.md §Workgroup dispatch),
-// so a hot feature block read through L1/L2 can be another CU's / XCD's old copy for as long as
-// it stays cached.  SC1 loads bypass L1; SC1 stores write through and drop the line from the
-// writer's L2, so the next read of a hot slot on any XCD fetches the latest written value.
-constexpr int CPOL_SC1 = 16;
+// Coherent-cache variant (SC1 DMA loads that bypass L1, SC1 write-through stores that drop the
+// line from the writer's L2) was measured and removed: 9.6 M rows/s vs 75.2 M, held-out logloss
+// 0.44742 vs 0.4478 (sequential 0.44501) — the same-stream gap is the concurrency of Hogwild
+// updates itself, not stale L1/L2 copies across XCDs (profiles/r4/ffm_coh_variant_parity.log).
 typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
-typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t table_rsrc(void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, -1, 0x00020000);   // 4 GiB - 1 bytes
-}
-template <bool COH, typename OT>
-__device__ __forceinline__ void st_v16(char* base, __amdgpu_buffer_rsrc_t r, OT off, float4 v) {
-    if constexpr (COH)
-        __builtin_amdgcn_raw_buffer_store_b128(u4v_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                                                     __float_as_uint(v.w)}, r, (uint32_t)off, 0, CPOL_SC1);
-    else
-        *reinterpret_cast<float4*>(base + off) = v;
-}
-template <bool COH, typename OT>
-__device__ __forceinline__ void st_f32(char* base, __amdgpu_buffer_rsrc_t r, OT off, float v) {
-    if constexpr (COH) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (uint32_t)off, 0, CPOL_SC1);
-    else *reinterpret_cast<float*>(base + off) = v;
-}
-template <bool COH, typename OT>
-__device__ __forceinline__ void st_u3(char* base, __amdgpu_buffer_rsrc_t r, OT off, u3v_t v) {
-    if constexpr (COH) __builtin_amdgcn_raw_buffer_store_b96(v, r, (uint32_t)off, 0, CPOL_SC1);
-    else *reinterpret_cast<u3v_t*>(base + off) = v;
-}
-template <bool COH>
-__device__ __forceinline__ void st_lin(float* p, float v) {
-    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
 
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout
@@ -983,7 +953,7 @@ __device__ __forceinline__ void st_lin(float* p, float v) {
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS, typename OT, bool COH, int TPB = 256>
+template <int NS, typename OT, int TPB = 256>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1006,7 +976,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
-    const __amdgpu_buffer_rsrc_t rv = table_rsrc(Vt), rg = table_rsrc(Gt);
 
     int ab[NS];
 #pragma unroll
@@ -1057,18 +1026,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             OT ov, og;
             float xab;
             slot(bf, j, ov, og, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, COH ? CPOL_SC1 : 0);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, COH ? CPOL_SC1 : 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
         }
     };
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
             if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, COH ? CPOL_SC1 : 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, COH ? CPOL_SC1 : 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, COH ? CPOL_SC1 : 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
                 }
             }
         }
@@ -1163,8 +1132,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
-                st_v16<COH>(vb, rv, ov, make_float4(o0.x, o0.y, o1.x, o1.y));
-                st_f32<COH>(gb, rg, og, gs);
+                *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                *reinterpret_cast<float*>(gb + og) = gs;
             }
             // the row's features' pad slots and block tails (never read): zeros, so every line a
             // row touches is written whole; spread over all threads (one wave doing them all
@@ -1190,9 +1159,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    st_lin<COH>(wz + mi, z1);
-                    st_lin<COH>(wn + mi, n1);
-                    st_lin<COH>(w + mi, ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2));
+                    wz[mi] = z1;
+                    wn[mi] = n1;
+                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
@@ -1211,7 +1180,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
 // per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
 // footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
-template <int NS, typename OT, bool COH>
+template <int NS, typename OT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1233,7 +1202,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
-    const __amdgpu_buffer_rsrc_t rv = table_rsrc(Vt);
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 
     int ab[NS];
@@ -1284,17 +1252,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             float xab;
             slot(bf, j, off, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + off), (lds_ptr_t)(s_raw + (j * 256 + wave * 64) * 4),
-                                             12, 0, COH ? CPOL_SC1 : 0);
+                                             12, 0, 0);
         }
     };
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
             if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, COH ? CPOL_SC1 : 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, COH ? CPOL_SC1 : 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, COH ? CPOL_SC1 : 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
                 }
             }
         }
@@ -1391,9 +1359,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
                 const uint32_t h = rotl32(hrow, 5 * j + 1) ^ (0x9E3779B9u * (uint32_t)(j + 1));
-                st_u3<COH>(vb, rv, off, u3v{pack_sr_hi(o0, h, rotl32(h, 16)),
+                *reinterpret_cast<u3v*>(vb + off) = u3v{pack_sr_hi(o0, h, rotl32(h, 16)),
                                                         pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
-                                                        __float_as_uint(gs)});
+                                                        __float_as_uint(gs)};
             }
             // pad slots + block tails of the row's features, spread over all threads
             {
@@ -1414,9 +1382,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 const float g = kappa * mx * scale;
                 const float n1 = ln + g * g;
                 const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                st_lin<COH>(wz + mi, z1);
-                st_lin<COH>(wn + mi, n1);
-                st_lin<COH>(w + mi, ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2));
+                wz[mi] = z1;
+                wn[mi] = n1;
+                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
@@ -1486,11 +1454,9 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
     if (blocks <= 0) return 0;
 #define HM_P12(NSV) do { \
-        if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t, false>), dim3(blocks), dim3(256), 0, stream, \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-        else if (variant == 7) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, true>), dim3(blocks), dim3(256), 0, \
-                                                  stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, false>), dim3(blocks), dim3(256), 0, stream, \
+        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
@@ -1514,17 +1480,15 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
 #define HM_P32(NSV) do { \
-        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, false>), dim3(blocks), dim3(256), 0, stream, \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else if (variant == 7) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, true>), dim3(blocks), dim3(256), 0, \
-                                                  stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, false>), dim3(blocks), dim3(256), 0, stream, \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (variant == 8 && !wide) {
         // 512-thread blocks (8 waves per row, half the slots per wave): twice the waves per CU
         // at the same rows in flight (A/B)
         const int need5 = (P.F * P.F + 511) / 512;
-#define HM_P32W(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, false, 512>), dim3(blocks), dim3(512), 0, \
+#define HM_P32W(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512>), dim3(blocks), dim3(512), 0, \
                                         stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
         if (need5 <= 2) { HM_P32W(2); }
         else if (need5 <= 3) { HM_P32W(3); }
@@ -1618,7 +1582,8 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             separate [.][.][Kp] tables.
 // variant (A/B): 0 = auto (per-slot: the sg12 / sg32 pipelines; per-element bf16:
 // ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel
-// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).
+// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G), 8 = the fp32 sg32 pipeline in
+// 512-thread blocks.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {

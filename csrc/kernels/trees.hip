@@ -46,7 +46,7 @@ template <> struct BinWords<8> { using T = U8W; };
 // wave keeps HIST_U row gathers (index -> stats + bin words) in flight instead of one.
 constexpr int HIST_U = 4;
 
-template <int NS, int FGW, bool GLOBAL>
+template <int NS, int FGW, bool GLOBAL, bool PK = false>
 __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int dpad, int f0, int nf,
                                           int B, const int32_t* __restrict__ rows,
                                           const float* __restrict__ stats, int64_t s0, int64_t s1,
@@ -86,6 +86,24 @@ __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int 
             for (int j = 0; j < FGW * 4; ++j) {
                 if (j < nf) {
                     const int bin = (w[u][j >> 2] >> (8 * (j & 3))) & 0xff;
+                    if constexpr (PK && !GLOBAL) {
+                        // statistics 2p, 2p+1 as one 64-bit LDS add: lo + hi * 2^32 with lo
+                        // sign-extended sums both exactly while |sum lo| < 2^31 (the fixed-point
+                        // scale bounds every sum by 2^30); an odd last statistic is a 32-bit add
+                        constexpr int NP = NS / 2;
+                        unsigned long long* h64 = reinterpret_cast<unsigned long long*>(h);
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const long long lo = __float2int_rn(st[u][2 * q] * scale[2 * q]);
+                            const long long hi = __float2int_rn(st[u][2 * q + 1] * scale[2 * q + 1]);
+                            atomicAdd(h64 + (j * NP + q) * B + bin,
+                                      (unsigned long long)(lo + (long long)((unsigned long long)hi << 32)));
+                        }
+                        if constexpr (NS & 1)
+                            atomicAdd(reinterpret_cast<int*>(h64 + (size_t)nf * NP * B) + j * B + bin,
+                                      __float2int_rn(st[u][NS - 1] * scale[NS - 1]));
+                        continue;
+                    }
 #pragma unroll
                     for (int s = 0; s < NS; ++s) {
                         if constexpr (GLOBAL) {
@@ -101,7 +119,7 @@ __device__ __forceinline__ void hist_rows(const uint8_t* __restrict__ bins, int 
     }
 }
 
-template <int NS, int FGW, int TPB = 256>
+template <int NS, int FGW, int TPB = 256, bool PK = false>
 __global__ __launch_bounds__(TPB) void hist_kernel(const uint8_t* __restrict__ bins, int d, int dpad,
                                                    int B, const int32_t* __restrict__ rows,
                                                    const int64_t* __restrict__ seg, int n_seg,
@@ -147,8 +165,34 @@ __global__ __launch_bounds__(TPB) void hist_kernel(const uint8_t* __restrict__ b
         }
         for (int i = threadIdx.x; i < hsz; i += blockDim.x) s_int[i] = 0;
         __syncthreads();
-        hist_rows<NS, FGW, false>(bins, dpad, f0, nf, B, rows, stats, s0, s1, s_hist, scale);
+        hist_rows<NS, FGW, false, PK>(bins, dpad, f0, nf, B, rows, stats, s0, s1, s_hist, scale);
         __syncthreads();
+        if constexpr (PK) {
+            constexpr int NP = NS / 2;
+            const unsigned long long* s64 = reinterpret_cast<const unsigned long long*>(s_hist);
+            for (int i = threadIdx.x; i < nf * NP * B; i += blockDim.x) {
+                const long long v = (long long)s64[i];
+                if (v == 0) continue;
+                const int f = i / (NP * B);
+                const int rem = i - f * NP * B;
+                const int q = rem / B;
+                const int bin = rem - q * B;
+                const int lo = (int)(unsigned)(unsigned long long)v;
+                const long long hi = (v - lo) >> 32;
+                float* o = gh + ((size_t)f * B + bin) * NS + 2 * q;
+                if (lo != 0) atomicAdd(o, (float)lo * inv[2 * q]);
+                if (hi != 0) atomicAdd(o + 1, (float)hi * inv[2 * q + 1]);
+            }
+            if constexpr (NS & 1) {
+                const int* s32 = reinterpret_cast<const int*>(s64 + (size_t)nf * NP * B);
+                for (int i = threadIdx.x; i < nf * B; i += blockDim.x) {
+                    const int v = s32[i];
+                    if (v != 0) atomicAdd(gh + (size_t)i * NS + NS - 1, (float)v * inv[NS - 1]);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         for (int i = threadIdx.x; i < hsz; i += blockDim.x) {
             const int v = s_int[i];
             if (v != 0) {
@@ -757,13 +801,67 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
     const int64_t chunk = (m + G - 1) / G;
     const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(m, r0 + chunk);
     for (int64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) {
-        const int row = rows[q];
+        const int row = rows ? rows[q] : (int)q;      // rows == NULL: every row, in order
         const int k = part_key(node_of_row, lut, row, nb, nlut, nkeys);
         if (k >= 0) {
             const int64_t pos = atomicAdd(reinterpret_cast<unsigned long long*>(&s_pos[k]), 1ull);
             out[pos] = row;
         }
     }
+}
+
+// A level's routing and the small-children counting of part_count_kernel in one pass, when
+// every row is active (rows 0 .. n-1 in order): each row's bins word, node and lut entry are read
+// once, instead of once by route_kernel over all rows and again (with the row index) by
+// part_count_kernel.  Same (key, block) cells as part_count_kernel (same grid and chunking), so
+// part_scatter_kernel (rows = NULL) places the rows identically.  ROUTE_U rows per thread are in
+// flight: the node -> split -> bins -> child loads are a dependent chain per row.
+constexpr int ROUTE_U = 4;
+__global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n, int dpad,
+                                                          int32_t* __restrict__ node_of_row,
+                                                          const int32_t* __restrict__ split_feat,
+                                                          const int32_t* __restrict__ split_bin,
+                                                          const int32_t* __restrict__ left_child,
+                                                          const int32_t* __restrict__ right_child, int miss_bin,
+                                                          const int16_t* __restrict__ lut, int nb, int nlut,
+                                                          int nkeys, int32_t* __restrict__ counts) {
+    extern __shared__ int s_cnt[];
+    const int G = gridDim.x;
+    for (int k = threadIdx.x; k < nkeys; k += blockDim.x) s_cnt[k] = 0;
+    __syncthreads();
+    const int64_t chunk = (n + G - 1) / G;
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
+    for (int64_t q0 = r0 + threadIdx.x; q0 < r1; q0 += (int64_t)blockDim.x * ROUTE_U) {
+        int nd[ROUTE_U], f[ROUTE_U];
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            nd[u] = q < r1 ? node_of_row[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) f[u] = nd[u] >= 0 ? split_feat[nd[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            if (f[u] < 0) continue;
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            const bool cat = f[u] & HM_TREE_CAT;
+            const bool dl = f[u] & HM_TREE_DLEFT;
+            const int b = bins[q * dpad + (f[u] & ~(HM_TREE_CAT | HM_TREE_DLEFT))];
+            const int sb = split_bin[nd[u]];
+            const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
+            nd[u] = go_left ? left_child[nd[u]] : right_child[nd[u]];
+            node_of_row[q] = nd[u];
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int c = nd[u] - nb;
+            if (nd[u] < 0 || c < 0 || c >= nlut) continue;
+            const int k = lut[c];
+            if (k < nkeys) atomicAdd(&s_cnt[k], 1);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nkeys; k += blockDim.x) counts[(size_t)k * G + blockIdx.x] = s_cnt[k];
 }
 
 // Next-level histograms from the parents' and the smaller children's: for split i (parent
@@ -814,6 +912,24 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
                            seg, n_seg, stats, smax, hist);                                          \
         break;
 #define HM_HN(K) HM_H(K, 1) HM_H(K, 2) HM_H(K, 4)
+    static const bool pack = [] { const char* e = getenv("HM_HIST_PACK"); return e && e[0] == '1'; }();
+    if (pack && (NS == 2 || NS == 3) && (FG == 16 || FG == 32)) {
+#define HM_HP(K, W, T) { \
+            static bool attr_set = false; \
+            if (!attr_set) { \
+                hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, W, T, true>), \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+                attr_set = true; \
+            } \
+            hipLaunchKernelGGL((hist_kernel<K, W, T, true>), grid, dim3(T), lds, stream, bins, d, dpad, B, rows, \
+                               seg, n_seg, stats, smax, hist); }
+        if (NS == 2 && FG == 16) HM_HP(2, 4, 256)
+        else if (NS == 3 && FG == 16) HM_HP(3, 4, 256)
+        else if (NS == 2) HM_HP(2, 8, 1024)
+        else HM_HP(3, 8, 1024)
+#undef HM_HP
+        HM_LAUNCH_RET();
+    }
     if (FG == 32) {
         switch (NS) {
 #define HM_HW(K) case K: { \
@@ -934,6 +1050,19 @@ HM_API int hm_partition_count(const int32_t* rows, int64_t m, const int32_t* nod
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
                        rows, m, node_of_row, lut, nb, nlut, nkeys, counts);
+    HM_LAUNCH_RET();
+}
+
+// route_count_kernel: route rows 0 .. n-1 one level down and count the small children's rows
+// per (key, block) cell; follow with hm_partition_scatter(rows = NULL, m = n, same grid).
+HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, int32_t* node_of_row, const int32_t* split_feat,
+                          const int32_t* split_bin, const int32_t* left_child, const int32_t* right_child,
+                          int miss_bin, const int16_t* lut, int nb, int nlut, int nkeys, int grid,
+                          int32_t* counts, hipStream_t stream) {
+    if (nkeys <= 0 || nkeys > 8192 || grid <= 0 || n <= 0 || n > INT32_MAX) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(route_count_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream, bins, n,
+                       dpad, node_of_row, split_feat, split_bin, left_child, right_child, miss_bin, lut, nb, nlut,
+                       nkeys, counts);
     HM_LAUNCH_RET();
 }
 

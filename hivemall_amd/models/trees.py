@@ -39,6 +39,7 @@ CAT_FLAG = 1 << 30   # nominal split flag in flattened node arrays (HM_TREE_CAT 
 DLEFT_FLAG = 1 << 29  # missing values go left at this split (HM_TREE_DLEFT)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
 HIST_WIDE = os.environ.get("HM_HIST_WIDE", "0") == "1"   # all-features single-pass histogram
+ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-child count in one pass
 HIST_WIDE_BLOCKS = int(os.environ.get("HM_HIST_WIDE_BLOCKS", "256"))
 
 
@@ -423,6 +424,25 @@ class HistTreeBuilder:
                                                          p(seg), st), "hm_partition_scatter")
         return rows, seg
 
+    def _route_partition_gpu(self, n: int, node_of_row, nbuf: "_NodeBuf", nb: int, lut, n_keys: int):
+        """Every row active (rows 0 .. n-1): route the level and count the small children in one
+        pass (hm_route_count), then place them (hm_partition_scatter without a row list)."""
+        q = self.q
+        dev = node_of_row.device
+        G = int(max(1, min(1024, (n + 4095) // 4096)))
+        counts = torch.empty(n_keys * G, dtype=torch.int32, device=dev)
+        p, st = _native.ptr, _native.stream_of(dev)
+        _native.check(_native.hip().hm_route_count(
+            p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
+            (q.B - 1) if self.missing else -1, p(lut), nb, lut.numel(), n_keys, G, p(counts), st), "hm_route_count")
+        incl = torch.cumsum(counts, 0)
+        rows = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+        seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+        _native.check(_native.hip().hm_partition_scatter(None, C.c_int64(n), p(node_of_row), p(lut), nb,
+                                                         lut.numel(), n_keys, G, p(counts), p(incl), p(rows),
+                                                         p(seg), st), "hm_partition_scatter")
+        return rows, seg
+
     def _hist(self, rows, seg, n_seg, stats, smax):
         """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
         q = self.q
@@ -460,7 +480,7 @@ class HistTreeBuilder:
         return hist
 
     def build(self, stats: torch.Tensor, active: torch.Tensor | None = None, smax: torch.Tensor | None = None,
-              act_rows: torch.Tensor | None = None) -> Tree:
+              act_rows: torch.Tensor | None = None, identity_rows: bool = False) -> Tree:
         """Grow one tree level by level.  stats: f32 [n, NS] per-row statistics.
 
         Every level: split search on the device over the level's histograms; one host sync
@@ -468,12 +488,14 @@ class HistTreeBuilder:
         smaller child of each split (sibling = parent - child).  After the call
         ``self.leaf_of_row`` holds the leaf node id of every row (-1: inactive).  ``smax`` (the
         columns' |max|) and ``act_rows`` (int32 ids of the rows with non-zero stats) may be
-        passed in when the caller already has them (the fused GBT statistics kernel)."""
+        passed in when the caller already has them (the fused GBT statistics kernel);
+        ``identity_rows``: act_rows is 0 .. n-1 (every row active, no ``active`` mask)."""
         q = self.q
         dev = stats.device
         n, NS = stats.shape
         d, B = q.d, q.B
         stats = stats.contiguous()
+        identity_rows = bool(identity_rows and active is None and act_rows is not None and act_rows.numel() == n)
         node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
         if active is not None:
             node_of_row[~active] = -1
@@ -531,6 +553,17 @@ class HistTreeBuilder:
                 if n_split == 0:
                     break
                 p = _native.ptr
+                if identity_rows and n_split <= 8192 and ROUTE_FUSED:
+                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, n_split)
+                    Hs = self._hist(rows, seg.contiguous(), n_split, stats, smax)
+                    Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
+                    _native.check(_native.hip().hm_hist_sibling(
+                        _native.ptr(H), _native.ptr(Hs), _native.ptr(li), _native.ptr(small_right),
+                        C.c_int64(d * B * NS), n_split, _native.ptr(Hn), _native.stream_of(dev)), "hm_hist_sibling")
+                    H = Hn
+                    base, L = nb, 2 * n_split
+                    depth += 1
+                    continue
                 _native.check(_native.hip().hm_route_rows(
                     p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
                     (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
@@ -934,7 +967,8 @@ class GradientTreeBoostingClassifier(Learner):
                 b = HistTreeBuilder(q, "gbt", int(c["max_depth"]), c["min_split"], c["min_samples_leaf"],
                                     c["mtry"], c["max_leaf_nodes"], seed=self.seed * 7919 + it * K,
                                     mixer=self.mixer, lam=float(c["lambda"]))
-                tree = b.build(stats_buf, smax=smax, act_rows=all_rows if mask is None else None)
+                tree = b.build(stats_buf, smax=smax, act_rows=all_rows if mask is None else None,
+                               identity_rows=mask is None)
                 self.importance += b.importance
                 vals = b.node_values.float().contiguous()
                 _native.check(_native.hip().hm_gbt_apply(
@@ -1164,6 +1198,8 @@ _native.register_host("hm_split_find_cpu", [_P] * 10)
 _native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P])
 _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
                                               _P, _P, _P])
+_native.register_hip("hm_route_count", [_P, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
 _native.register_hip("hm_xgb_stats", [_P, _P, _P, _I64, _P, _P, _P])

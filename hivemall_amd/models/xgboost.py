@@ -179,7 +179,8 @@ class XGBoostTrainer(Learner):
                                     lam=float(c["lambda"]), alpha=float(c["alpha"]),
                                     min_gain=2.0 * float(c["gamma"]), feature_mask=fmask)
                 if fused:
-                    tree = b.build(stats, smax=smax, act_rows=all_rows if mask is None else None)
+                    tree = b.build(stats, smax=smax, act_rows=all_rows if mask is None else None,
+                                   identity_rows=mask is None)
                 else:
                     tree = b.build(stats)
                 tree.value = [None if v is None else [eta * v[0]] for v in tree.value]

@@ -30,8 +30,11 @@ class FMHyper:
 
 
 # rows between a wave's re-reads of the 64 global-bias shards (csrc/kernels/fm.hip fm_pipe_kernel);
-# each re-read is 64 lines the other waves' atomics have just dropped from L2
-W0_EVERY = 1
+# each re-read is 64 lines the other waves' atomics have just dropped from L2.  Measured on the
+# Criteo-shaped 2^24 bench (profiles/r4/fm_w0_every_ab.log, two reps each): every row 145 M rows/s
+# (held-out 0.4757), every 8 rows 234 M (0.4762), every 32 rows 300 M but 0.54-0.74 (the bias
+# drifts between refreshes) -> 8
+W0_EVERY = 8
 
 
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
