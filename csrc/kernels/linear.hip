@@ -409,6 +409,134 @@ __device__ __forceinline__ float rda_w(const Params& P, float u, float G, const 
     return mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
 }
 
+// The other rules of the general learner (SGD, momentum, Nesterov, RMSprop(-Graves), AdaDelta,
+// the Adam family, AdaGrad with L1 / elastic-net) keep their hot features in "owner" mode: the
+// blocks add their per-chunk sums (sum g, sum g^2, rows) to a global accumulator per hot feature
+// (non-returning atomics, nothing lost), and ONE thread of the grid owns each hot feature: at
+// every chunk end it takes the accumulated sums (atomic exchange) and applies the rule's n-step
+// update (hot_nstep) to the feature's state with plain read-modify-write — a single writer, so no
+// update is lost and none is applied twice.  Rows still read the hot weights Hogwild (stale by at
+// most a chunk).  One table (R = 1) only.
+__host__ __device__ __forceinline__ bool hot_owner_rule(const Params& P) {
+    return P.algo == A_GENERAL && !hot_sum_rule(P) && P.reg != R_RDA;
+}
+
+// Sum of x_i = beta^i x0 + c (1 - beta^i) / (1 - beta) over i = 1 .. n (a geometric EMA / momentum
+// recursion driven by a constant c), and its last term x_n.
+__device__ __forceinline__ void geo_sum(float beta, float n, float x0, float c, float* sum, float* last) {
+    const float bn = powf(beta, n);
+    if (beta >= 1.f) { *sum = n * x0 + c * n * (n + 1.f) * 0.5f; *last = x0 + c * n; return; }
+    const float q = beta * (1.f - bn) / (1.f - beta);       // sum of beta^i, i = 1 .. n
+    *sum = x0 * q + c / (1.f - beta) * (n - q);
+    *last = bn * x0 + c * (1.f - bn) / (1.f - beta);
+}
+
+// n sequential steps of the general learner's rule on one feature, every step with the chunk's
+// mean gradient a = sum g / n and mean squared gradient b = sum g^2 / n (regularisation
+// evaluated at the state the owner read), in closed form: the exponential averages are advanced
+// exactly (beta^n), the weight moves by the sum of the n steps, with each step's normaliser taken
+// at the chunk's midpoint (AdaGrad: the exact integral of 1 / sqrt(G0 + i b)).  SGD and momentum
+// are exact for a constant gradient; the normalised rules differ only in how the normaliser
+// varies inside one chunk.
+__device__ __forceinline__ void hot_nstep(const Params& P, F4& s, float gsum, float g2sum, float n, const StepK& k,
+                                          float eve_d) {
+    if (n <= 0.f) return;
+    float r = 0.f;
+    switch (P.reg) {
+        case R_L1: r = P.lambda * sgnf(s.w); break;
+        case R_L2: r = P.lambda * s.w; break;
+        case R_ELASTIC: r = P.lambda * (P.l1_ratio * sgnf(s.w) + (1.f - P.l1_ratio) * s.w); break;
+        default: break;
+    }
+    const float a0 = gsum / n;
+    const float a = a0 + r;                                   // mean regularised gradient
+    const float b = fmaxf(g2sum / n + 2.f * a0 * r + r * r, 0.f);   // its mean square
+    const float eta = k.eta;
+    const float half = 0.5f * n;
+    switch (P.opt) {
+        case O_SGD: s.w -= eta * n * a; break;
+        case O_MOMENTUM: {                                    // v_i = beta v + eta g; w -= v_i
+            float sum, last;
+            geo_sum(P.beta1, n, s.s1, eta * a, &sum, &last);
+            s.w -= sum;
+            s.s1 = last;
+            break;
+        }
+        case O_NESTEROV: {                                    // v_i = beta v - eta g; w += -beta v_{i-1} + (1+beta) v_i
+            float sum, last;
+            geo_sum(P.beta1, n, s.s1, -eta * a, &sum, &last);
+            const float prev_sum = s.s1 + sum - last;         // v_0 .. v_{n-1}
+            s.w += -P.beta1 * prev_sum + (1.f + P.beta1) * sum;
+            s.s1 = last;
+            break;
+        }
+        case O_ADAGRAD: {                                     // sum_i 1 / sqrt(G0 + i b) ~ 2n / (sqrt(G_n) + sqrt(G0))
+            const float G0 = s.s1, Gn = G0 + n * b;
+            s.w -= eta * a * 2.f * n / (sqrtf(Gn) + sqrtf(G0) + 2.f * P.eps);
+            s.s1 = Gn;
+            break;
+        }
+        case O_RMSPROP: {
+            const float dh = powf(P.decay, half), dn = dh * dh;
+            const float mid = dh * s.s1 + (1.f - dh) * b;
+            s.w -= eta * n * a / (sqrtf(mid) + P.eps);
+            s.s1 = dn * s.s1 + (1.f - dn) * b;
+            break;
+        }
+        case O_RMSPROP_GRAVES: {
+            const float dh = powf(P.decay, half), dn = dh * dh;
+            const float n1 = dh * s.s1 + (1.f - dh) * b, g1 = dh * s.s2 + (1.f - dh) * a;
+            const float den = n1 - g1 * g1 + P.eps;
+            float sum, last;
+            geo_sum(P.beta1, n, s.s3, -eta * P.alpha * a / sqrtf(den > 0.f ? den : P.eps), &sum, &last);
+            s.w += sum;
+            s.s3 = last;
+            s.s1 = dn * s.s1 + (1.f - dn) * b;
+            s.s2 = dn * s.s2 + (1.f - dn) * a;
+            break;
+        }
+        case O_ADADELTA: {
+            const float rh = powf(P.rho, half), rn = rh * rh;
+            const float g2mid = rh * s.s1 + (1.f - rh) * b;
+            const float ratio = sqrtf(s.s2 + P.eps) / sqrtf(g2mid + P.eps);
+            s.w -= n * ratio * a;
+            s.s1 = rn * s.s1 + (1.f - rn) * b;
+            s.s2 = rn * s.s2 + (1.f - rn) * ratio * ratio * b;
+            break;
+        }
+        case O_ADAM: case O_EVE: case O_ADAM_HD: case O_NADAM: {
+            float msum, mlast;
+            geo_sum(P.beta1, n, s.s1, (1.f - P.beta1) * a, &msum, &mlast);
+            const float bh = powf(P.beta2, half), bn = bh * bh;
+            const float vmid = bh * s.s2 + (1.f - bh) * b;
+            const float vlast = bn * s.s2 + (1.f - bn) * b;
+            if (P.opt == O_NADAM) {
+                const float mh = P.beta1 * msum / k.c1n + (1.f - P.beta1) * n * a / k.c1;
+                s.w -= eta * P.alpha * mh / (sqrtf(vmid / k.c2) + P.eps);
+            } else {
+                float vhat = vmid;
+                if (P.opt == O_ADAM && P.amsgrad) { s.s3 = fmaxf(s.s3, vlast); vhat = fmaxf(s.s3, vmid); }
+                float alpha = P.alpha;
+                if (P.opt == O_ADAM_HD) {
+                    // hypergradient of the step size: sum_i g_i u_{i-1} ~ n a u(state read)
+                    if (s.s3 == 0.f) s.s3 = P.alpha;
+                    const float cp1 = k.cp1, cp2 = k.cp2;
+                    const float u = cp1 > 0.f ? (s.s1 / cp1) / (sqrtf(s.s2 / (cp2 > 0.f ? cp2 : 1.f)) + P.eps) : 0.f;
+                    s.s3 += P.beta_hd * n * a * u;
+                    alpha = s.s3;
+                }
+                float lr = eta * alpha * sqrtf(k.c2) / k.c1;
+                if (P.opt == O_EVE) lr /= (eve_d > 0.f ? eve_d : 1.f);
+                s.w -= lr * msum / (sqrtf(vhat) + P.eps);
+            }
+            s.s1 = mlast;
+            s.s2 = vlast;
+            break;
+        }
+        default: break;
+    }
+}
+
 // Block barrier over the LDS accumulators only: waits for this wave's LDS operations, not for
 // its outstanding global atomics (a __syncthreads fence would drain those too)
 __device__ __forceinline__ void lds_barrier() {
@@ -430,8 +558,10 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
     const int32_t* __restrict__ order, float4* __restrict__ S0, uint8_t* __restrict__ touched0,
     float* __restrict__ RSW, double* __restrict__ loss_out, const int32_t* __restrict__ hot_slot,
-    const int32_t* __restrict__ hot_feat, int H, int CH, int min_rows, int every, int coh) {
+    const int32_t* __restrict__ hot_feat, int H, int CH, int min_rows, int every, int coh,
+    float4* __restrict__ hacc) {
     extern __shared__ float s_acc[];             // HOT: 3 x H floats, see hot_add
+    const bool owner = HOT && hacc != nullptr;   // hot features in owner mode (hot_owner_rule)
     // coh: feature-state stores write through and drop the line from this XCD's L2 (SC1), so
     // the other XCDs' next reads of a hot feature fetch the latest value (A/B, HM_LINEAR_COH)
     const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(S0, (short)0, -1, 0x00020000);
@@ -554,7 +684,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                     // a hot feature whose rows all had a zero loss gradient needs no update —
                     // unless L2 decays it on every row that holds it (the sequential rule's
                     // g = 0 + lambda w)
-                    f[u] = (g2[u] != 0.f || (P.reg == R_L2 && cnt[u] > 0.f)) && (all || cnt[u] >= (float)min_rows)
+                    f[u] = (g2[u] != 0.f || ((P.reg == R_L2 || owner) && cnt[u] > 0.f)) && (all || cnt[u] >= (float)min_rows)
                                ? hot_feat[h] : -1;
                     if (f[u] >= 0) {
                         s_acc[h] = 0.f;
@@ -562,9 +692,33 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                         s_acc[2 * H + h] = 0.f;
                     }
                 }
-                hot_flush4(P, S, gs, g2, cnt, f, sk);
+                if (owner) {
+#pragma unroll
+                    for (int u = 0; u < HM_HOT_U; ++u) {
+                        if (f[u] < 0) continue;
+                        float4* A = hacc + h0 + u * 256;
+                        atomicAdd(&A->x, gs[u]);
+                        atomicAdd(&A->y, g2[u]);
+                        atomicAdd(&A->z, cnt[u]);
+                    }
+                } else {
+                    hot_flush4(P, S, gs, g2, cnt, f, sk);
+                }
             }
             lds_barrier();
+            if (owner) {
+                // the hot features this thread owns: h = block + gridDim.x * (thread + 256 j)
+                for (int h = blockIdx.x + gridDim.x * threadIdx.x; h < H; h += gridDim.x * 256) {
+                    const float n = atomicExch(&hacc[h].z, 0.f);
+                    if (n <= 0.f) continue;
+                    const float gsum = atomicExch(&hacc[h].x, 0.f);
+                    const float g2sum = atomicExch(&hacc[h].y, 0.f);
+                    float4* p = S + hot_feat[h];
+                    F4 st = ld4m<true>(p);
+                    hot_nstep(P, st, gsum, g2sum, n, sk, rs[RS_EVE_D]);
+                    store(p, st);
+                }
+            }
         }
     }
     if (active && lane == 0) {
@@ -585,6 +739,22 @@ __global__ __launch_bounds__(256) void hot_rda_finalize_kernel(Params P, float4*
         float4* s = S0 + (size_t)r * dims + hot_feat[h];
         s->x = rda_w(P, s->y, s->z, k);
     }
+}
+
+// After an owner-mode pass: the sums the owners had not taken yet (pushed after their last
+// exchange) applied at the pass's last step.
+__global__ __launch_bounds__(256) void hot_owner_final_kernel(Params P, float4* __restrict__ S, float4* __restrict__ hacc,
+                                                              const int32_t* __restrict__ hot_feat, int H, float t,
+                                                              const float* __restrict__ RSW) {
+    const StepK k = step_consts(P, t);
+    const int h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= H) return;
+    const float4 A = hacc[h];
+    hacc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (A.z <= 0.f) return;
+    F4 st = ld4(S + hot_feat[h]);
+    hot_nstep(P, st, A.x, A.y, A.z, k, RSW[RS_EVE_D]);
+    st4(S + hot_feat[h], st);
 }
 
 }  // namespace
@@ -655,26 +825,37 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
                                   int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,
                                   float* RSW, double* loss_out, const int32_t* hot_slot, const int32_t* hot_feat,
-                                  int H, int CH, int min_rows, int every, int coh, hipStream_t stream) {
+                                  int H, int CH, int min_rows, int every, int coh, float* hacc,
+                                  hipStream_t stream) {
     if (n_rows <= 0) return 0;
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
     if (coh && (size_t)R * (size_t)dims * 16 >= ((size_t)1 << 32)) coh = 0;   // 32-bit buffer offsets
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
     const bool hot = H > 0;
     const size_t lds = hot ? (size_t)H * 3 * sizeof(float) : 0;
+    // hot features: pre-aggregated sums (hot_sum_rule), or owner mode (hot_owner_rule, R = 1, with
+    // the zeroed float4 [H] accumulators hacc)
+    const bool own = hot && hacc != nullptr;
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 || min_rows <= 0 || every <= 0 ||
-                !hot_sum_rule(*P)))
+                !(own ? (hot_owner_rule(*P) && R == 1) : hot_sum_rule(*P))))
         return (int)hipErrorInvalidValue;
+    // owner stores: write-through (SC1) so the other XCDs' next reads fetch them
+    if (own && (size_t)dims * 16 < ((size_t)1 << 32)) coh = 1;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \
                        dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
-                       RSW, loss_out, hot_slot, hot_feat, H, CH, min_rows, every, coh)
+                       RSW, loss_out, hot_slot, hot_feat, H, CH, min_rows, every, coh,                  \
+                       own ? reinterpret_cast<float4*>(hacc) : nullptr)
     if (hot) {
         if (reload && nt) HM_SHARED_LAUNCH(true, true, true);
         else if (reload) HM_SHARED_LAUNCH(true, false, true);
         else if (nt) HM_SHARED_LAUNCH(false, true, true);
         else HM_SHARED_LAUNCH(false, false, true);
-        if (hot_rda(*P)) {
+        if (own) {
+            hipLaunchKernelGGL(hot_owner_final_kernel, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, stream, *P,
+                               reinterpret_cast<float4*>(S), reinterpret_cast<float4*>(hacc), hot_feat, H,
+                               (float)(t0 + n_rows), RSW);
+        } else if (hot_rda(*P)) {
             const int64_t tot = (int64_t)H * R;
             hipLaunchKernelGGL(hot_rda_finalize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *P,
                                reinterpret_cast<float4*>(S), dims, R, hot_feat, H, (float)(t0 + n_rows));

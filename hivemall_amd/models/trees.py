@@ -38,8 +38,9 @@ MODEL_VERSION = 1
 CAT_FLAG = 1 << 30   # nominal split flag in flattened node arrays (HM_TREE_CAT in trees.hip)
 DLEFT_FLAG = 1 << 29  # missing values go left at this split (HM_TREE_DLEFT)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
-HIST_WIDE = os.environ.get("HM_HIST_WIDE", "0") == "1"   # all-features single-pass histogram
+HIST_WIDE = os.environ.get("HM_HIST_WIDE", "1") == "1"   # all-features single-pass histogram
 ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-child count in one pass
+GBT2 = os.environ.get("HM_GBT2", "1") == "1"    # GBT histograms of (r, w), Newton leaves summed per leaf
 HIST_WIDE_BLOCKS = int(os.environ.get("HM_HIST_WIDE_BLOCKS", "256"))
 
 
@@ -307,6 +308,9 @@ class HistTreeBuilder:
         if c == "gbt":           # S = (Σr, Σh, n): least squares on the residual
             return torch.where(S[..., 2] > 0, S[..., 0] ** 2 / (S[..., 2] + self.lam),
                                torch.zeros_like(S[..., 0]))
+        if c == "gbt2":          # S = (Σr, n); Σh is summed per leaf after the tree is grown
+            return torch.where(S[..., 1] > 0, S[..., 0] ** 2 / (S[..., 1] + self.lam),
+                               torch.zeros_like(S[..., 0]))
         if c == "xgb":           # S = (Σg, Σh): T_alpha(G)^2 / (H + lambda)
             G = self._soft(S[..., 0])
             return torch.where(S[..., 1] > 0, G * G / (S[..., 1] + self.lam), torch.zeros_like(G))
@@ -322,7 +326,7 @@ class HistTreeBuilder:
         c = self.criterion
         if c in ("gini", "entropy"):
             return S.sum(-1)
-        if c in ("variance", "xgb"):
+        if c in ("variance", "xgb", "gbt2"):
             return S[..., 1]
         return S[..., 2]
 
@@ -332,7 +336,7 @@ class HistTreeBuilder:
         if c in ("gini", "entropy"):
             w = S.sum(1, keepdim=True)
             return torch.where(w > 0, S / w.clamp_min(1e-30), torch.full_like(S, 1.0 / S.shape[1]))
-        if c == "variance":
+        if c in ("variance", "gbt2"):   # gbt2: the mean residual until the per-leaf Newton values
             return torch.where(S[:, 1:2] > 0, S[:, 0:1] / S[:, 1:2].clamp_min(1e-30), torch.zeros_like(S[:, :1]))
         if c == "xgb":           # Newton step -T(G) / (H + lambda)
             den = S[:, 1:2] + self.lam
@@ -341,7 +345,7 @@ class HistTreeBuilder:
         return torch.where(ok, S[:, 0:1] / torch.where(ok, S[:, 1:2], torch.ones_like(S[:, 1:2])),
                            torch.zeros_like(S[:, :1]))
 
-    _CRIT = {"gini": 0, "entropy": 1, "variance": 2, "gbt": 3, "xgb": 4}
+    _CRIT = {"gini": 0, "entropy": 1, "variance": 2, "gbt": 3, "xgb": 4, "gbt2": 5}
 
     def _split_find(self, H: torch.Tensor, node_base: int):
         """Best split of every node of the level (csrc hm_split_find: one fused kernel instead
@@ -480,7 +484,8 @@ class HistTreeBuilder:
         return hist
 
     def build(self, stats: torch.Tensor, active: torch.Tensor | None = None, smax: torch.Tensor | None = None,
-              act_rows: torch.Tensor | None = None, identity_rows: bool = False) -> Tree:
+              act_rows: torch.Tensor | None = None, identity_rows: bool = False,
+              leaf_h: torch.Tensor | None = None) -> Tree:
         """Grow one tree level by level.  stats: f32 [n, NS] per-row statistics.
 
         Every level: split search on the device over the level's histograms; one host sync
@@ -489,7 +494,9 @@ class HistTreeBuilder:
         ``self.leaf_of_row`` holds the leaf node id of every row (-1: inactive).  ``smax`` (the
         columns' |max|) and ``act_rows`` (int32 ids of the rows with non-zero stats) may be
         passed in when the caller already has them (the fused GBT statistics kernel);
-        ``identity_rows``: act_rows is 0 .. n-1 (every row active, no ``active`` mask)."""
+        ``identity_rows``: act_rows is 0 .. n-1 (every row active, no ``active`` mask).
+        ``leaf_h`` (criterion gbt2, stats = (r, w)): per-row hessians; the leaves get the Newton
+        values sum r / sum h over their rows (csrc hm_leaf_sums / hm_leaf_newton)."""
         q = self.q
         dev = stats.device
         n, NS = stats.shape
@@ -653,6 +660,21 @@ class HistTreeBuilder:
             depth += 1
         self.importance = self.importance + imp.cpu().numpy()
         self.leaf_of_row = node_of_row
+        if fused and leaf_h is not None:
+            t = base + L
+            sums = torch.zeros((t, 2), dtype=torch.float32, device=dev)
+            p, st_ = _native.ptr, _native.stream_of(dev)
+            if t <= 8192:
+                _native.check(_native.hip().hm_leaf_sums(p(node_of_row), p(stats), p(leaf_h), C.c_int64(n), t,
+                                                         p(sums), st_), "hm_leaf_sums")
+            else:
+                ok = node_of_row >= 0
+                nd = node_of_row[ok].long()
+                sums[:, 0].index_add_(0, nd, stats[ok, 0])
+                sums[:, 1].index_add_(0, nd, leaf_h[ok])
+            if self.mixer is not None and self.mixer.world > 1:
+                self.mixer.all_reduce_sum([sums])
+            _native.check(_native.hip().hm_leaf_newton(p(sums), p(nbuf.sf), t, p(nbuf.vals), st_), "hm_leaf_newton")
         if fused:
             t = base + L                                   # nodes written, ids 0 .. t - 1
             F, Lc, Rc = torch.stack([nbuf.sf[:t], nbuf.lc[:t], nbuf.rc[:t]]).cpu().numpy()
@@ -949,8 +971,13 @@ class GradientTreeBoostingClassifier(Learner):
             # binary logistic on the GPU: one fused statistics pass and one fused leaf update per
             # tree instead of ~12 tensor passes over the n rows (profiles/gbt_r2/)
             y1 = Y[:, 0].contiguous()
-            stats_buf = torch.empty((n, 3), dtype=torch.float32, device=self.device)
-            smax = torch.zeros(3, dtype=torch.float32, device=self.device)
+            # gbt2: the histograms carry (r, w) and the Newton leaf values sum h per leaf afterwards
+            # (2 LDS statistics instead of 3); HM_GBT2=0 keeps (r, h, w) histograms
+            gbt2 = GBT2 and c["max_leaf_nodes"] is None      # (the level-fused builder only)
+            ns = 2 if gbt2 else 3
+            stats_buf = torch.empty((n, ns), dtype=torch.float32, device=self.device)
+            hh = torch.empty(n, dtype=torch.float32, device=self.device) if gbt2 else None
+            smax = torch.zeros(ns, dtype=torch.float32, device=self.device)
             all_rows = torch.arange(n, dtype=torch.int32, device=self.device)
             st = _native.stream_of(self.device)
         for it in range(int(c["trees"])):
@@ -961,14 +988,19 @@ class GradientTreeBoostingClassifier(Learner):
                     mask = torch.zeros(n, dtype=torch.bool, device=self.device)
                     mask[sel] = True
                 smax.zero_()
-                _native.check(_native.hip().hm_gbt_stats(
-                    _native.ptr(F), _native.ptr(y1), _native.ptr(mask), C.c_int64(n), _native.ptr(stats_buf),
-                    _native.ptr(smax), st), "hm_gbt_stats")
-                b = HistTreeBuilder(q, "gbt", int(c["max_depth"]), c["min_split"], c["min_samples_leaf"],
-                                    c["mtry"], c["max_leaf_nodes"], seed=self.seed * 7919 + it * K,
-                                    mixer=self.mixer, lam=float(c["lambda"]))
+                if gbt2:
+                    _native.check(_native.hip().hm_gbt2_stats(
+                        _native.ptr(F), _native.ptr(y1), _native.ptr(mask), C.c_int64(n), _native.ptr(stats_buf),
+                        _native.ptr(smax), _native.ptr(hh), st), "hm_gbt2_stats")
+                else:
+                    _native.check(_native.hip().hm_gbt_stats(
+                        _native.ptr(F), _native.ptr(y1), _native.ptr(mask), C.c_int64(n), _native.ptr(stats_buf),
+                        _native.ptr(smax), st), "hm_gbt_stats")
+                b = HistTreeBuilder(q, "gbt2" if gbt2 else "gbt", int(c["max_depth"]), c["min_split"],
+                                    c["min_samples_leaf"], c["mtry"], c["max_leaf_nodes"],
+                                    seed=self.seed * 7919 + it * K, mixer=self.mixer, lam=float(c["lambda"]))
                 tree = b.build(stats_buf, smax=smax, act_rows=all_rows if mask is None else None,
-                               identity_rows=mask is None)
+                               identity_rows=mask is None, leaf_h=hh)
                 self.importance += b.importance
                 vals = b.node_values.float().contiguous()
                 _native.check(_native.hip().hm_gbt_apply(
@@ -1198,6 +1230,9 @@ _native.register_host("hm_split_find_cpu", [_P] * 10)
 _native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P])
 _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
                                               _P, _P, _P])
+_native.register_hip("hm_gbt2_stats", [_P, _P, _P, _I64, _P, _P, _P, _P])
+_native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, _P])
+_native.register_hip("hm_leaf_newton", [_P, _P, C.c_int, _P, _P])
 _native.register_hip("hm_route_count", [_P, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])

@@ -193,13 +193,22 @@ def hot_rule(P: LinParams) -> bool:
             and P.reg in (REGS["no"], REGS["l2"], REGS["rda"]) and P.n_labels == 1)
 
 
+def hot_owner_rule(P: LinParams) -> bool:
+    """The general learner's other rules (csrc/kernels/linear.hip hot_owner_rule): their hot
+    features are applied by one owner thread each, as n sequential steps of the chunk's mean
+    gradient (hot_nstep), on a single table.  ``HM_LINEAR_HOT_OWNER=0`` leaves them Hogwild."""
+    if os.environ.get("HM_LINEAR_HOT", "1") == "0" or os.environ.get("HM_LINEAR_HOT_OWNER", "1") == "0":
+        return False
+    return P.algo == ALGOS["general"] and not hot_rule(P) and P.reg != REGS["rda"] and P.n_labels == 1
+
+
 def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     """The features the shared-table kernel pre-aggregates per block instead of updating them
     Hogwild (csrc/kernels/linear.hip, HOT): the at most ``HOT_MAX`` most frequent features of
     the pass that more than one in-flight row is expected to hit (count >= n_rows / W), for the
     rules of ``hot_rule``.  Returns (hot_slot i32 [dims], hot_feat i32 [H]) or None.
     Cached per index tensor (epochs reuse it).  ``HM_LINEAR_HOT=0`` disables."""
-    if not hot_rule(P):
+    if not (hot_rule(P) or (hot_owner_rule(P) and st.R == 1)):
         return None
     # keyed on the tensor object itself (weakly) and its version counter: a later pass whose
     # index tensor happens to land at a freed address must not reuse this pass's hot set
@@ -245,6 +254,11 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     p = _native.ptr
     hot = hot_features(st, P, idx, n) if W > 1 else None
     hs, hf, H = (hot[0], hot[1], hot[1].numel()) if hot is not None else (None, None, 0)
+    hacc = None
+    if H and not hot_rule(P):                 # owner mode: zeroed [H] accumulators (re-zeroed by the pass)
+        hacc = st.meta.get("hacc")
+        if hacc is None or hacc.shape[0] < H:
+            hacc = st.meta["hacc"] = torch.zeros((max(H, HOT_MAX), 4), dtype=torch.float32, device=dev)
     ch = int(os.environ.get("HM_LINEAR_HOT_CH", HOT_CHUNK))
     hmin = int(os.environ.get("HM_LINEAR_HOT_MIN", HOT_MIN_ROWS))
     hevery = int(os.environ.get("HM_LINEAR_HOT_EVERY", HOT_EVERY))
@@ -253,7 +267,8 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
                                               int(st.meta.get("nt", True)),
                                               p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
                                               p(st.touched), p(st.RS), p(loss), p(hs), p(hf), H, ch, hmin, hevery,
-                                              int(os.environ.get("HM_LINEAR_COH", "0")), _native.stream_of(dev))
+                                              int(os.environ.get("HM_LINEAR_COH", "0")), p(hacc),
+                                              _native.stream_of(dev))
     _native.check(rc, "hm_linear_train_shared")
     return loss
 
@@ -338,7 +353,7 @@ _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
                                               C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 5
-                     + [_P])
+                     + [_P, _P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
 _native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])
