@@ -1484,18 +1484,6 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
-    if (variant == 8 && !wide) {
-        // 512-thread blocks (8 waves per row, half the slots per wave): twice the waves per CU
-        // at the same rows in flight (A/B)
-        const int need5 = (P.F * P.F + 511) / 512;
-#define HM_P32W(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512>), dim3(blocks), dim3(512), 0, \
-                                        stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (need5 <= 2) { HM_P32W(2); }
-        else if (need5 <= 3) { HM_P32W(3); }
-        else { HM_P32W(4); }
-#undef HM_P32W
-        HM_LAUNCH_RET();
-    }
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }
@@ -1582,8 +1570,8 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             separate [.][.][Kp] tables.
 // variant (A/B): 0 = auto (per-slot: the sg12 / sg32 pipelines; per-element bf16:
 // ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel
-// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G), 8 = the fp32 sg32 pipeline in
-// 512-thread blocks.
+// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).  (512-thread sg32 blocks measured
+// 75.7-76.1 vs 75.6 M rows/s, profiles/r4/ffm_512_thread_ab.log: removed.)
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {

@@ -37,7 +37,6 @@ struct FMParams {
     int use_w0;
     int w0_shards;            // w0 = sum of w0[0..w0_shards) (<= 64)
     int w0_every;             // fm_pipe_kernel: rows between re-reads of the w0 shards (>= 1)
-    int coh;                  // fm_pipe_kernel: L1-bypassing loads, write-through (SC1) stores (A/B)
     uint32_t seed;
 };
 
@@ -53,24 +52,17 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     return h;
 }
 
-typedef uint32_t fm_u4 __attribute__((ext_vector_type(4)));
 
 template <int KP, bool BF16>
 struct VRow {
     float v[KP];
-    __device__ __forceinline__ void load(const void* V, int i, int coh = 0) {
+    __device__ __forceinline__ void load(const void* V, int i) {
         if constexpr (BF16) {
             const uint16_t* p = reinterpret_cast<const uint16_t*>(V) + (size_t)i * KP;
             if constexpr (KP % 8 == 0) {
 #pragma unroll
                 for (int c = 0; c < KP / 8; ++c) {
-                    uint4 q;
-                    if (coh) {
-                        const fm_u4 t = __builtin_nontemporal_load(reinterpret_cast<const fm_u4*>(p) + c);
-                        q = make_uint4(t.x, t.y, t.z, t.w);
-                    } else {
-                        q = reinterpret_cast<const uint4*>(p)[c];
-                    }
+                    const uint4 q = reinterpret_cast<const uint4*>(p)[c];
                     const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -94,7 +86,7 @@ struct VRow {
             }
         }
     }
-    __device__ __forceinline__ void store(void* V, int i, uint32_t rbase, int coh = 0) const {
+    __device__ __forceinline__ void store(void* V, int i, uint32_t rbase) const {
         if constexpr (BF16) {
             uint16_t* p = reinterpret_cast<uint16_t*>(V) + (size_t)i * KP;
             uint32_t wds[KP / 2];
@@ -104,15 +96,9 @@ struct VRow {
                 wds[j] = hm::pack_bf16x2_sr(v[2 * j], r, v[2 * j + 1], r >> 16 | r << 16);
             }
             if constexpr (KP % 8 == 0) {
-                const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(V, (short)0, -1, 0x00020000);
 #pragma unroll
-                for (int c = 0; c < KP / 8; ++c) {
-                    if (coh)   // SC1: write through, drop the line from this XCD's L2 (< 4 GiB tables)
-                        __builtin_amdgcn_raw_buffer_store_b128(fm_u4{wds[4 * c], wds[4 * c + 1], wds[4 * c + 2], wds[4 * c + 3]},
-                                                               rsrc, (uint32_t)(((size_t)i * KP + 8 * c) * 2), 0, 16);
-                    else
-                        reinterpret_cast<uint4*>(p)[c] = make_uint4(wds[4 * c], wds[4 * c + 1], wds[4 * c + 2], wds[4 * c + 3]);
-                }
+                for (int c = 0; c < KP / 8; ++c)
+                    reinterpret_cast<uint4*>(p)[c] = make_uint4(wds[4 * c], wds[4 * c + 1], wds[4 * c + 2], wds[4 * c + 3]);
             } else {
                 *reinterpret_cast<uint2*>(p) = make_uint2(wds[0], wds[1]);
             }
@@ -285,8 +271,8 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
         VRow<KP, BF16> vr;
         float wi = 0.f;
         if (i >= 0) {
-            vr.load(V, i, P.coh);
-            wi = P.coh ? __builtin_nontemporal_load(w + i) : w[i];
+            vr.load(V, i);
+            wi = w[i];
         } else {
 #pragma unroll
             for (int f = 0; f < KP; ++f) vr.v[f] = 0.f;
@@ -366,13 +352,13 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
             const float eta = fm_eta(P, (float)(t0 + row + 1));
             const uint32_t rbase = P.seed ^ (uint32_t)(t0 + row) * 0x9E3779B9u;
             auto upd = [&](VRow<KP, BF16>& t, int ii, float xx, float ww) {
-                { const float wnew = ww - eta * (d * xx + 2.f * P.lambda_w * ww); if (P.coh) __hip_atomic_store(w + ii, wnew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); else w[ii] = wnew; }
+                w[ii] = ww - eta * (d * xx + 2.f * P.lambda_w * ww);
 #pragma unroll
                 for (int f = 0; f < KP; ++f) {
                     const float g = d * xx * (S[f] - t.v[f] * xx) + 2.f * P.lambda_v * t.v[f];
                     t.v[f] = f < P.k ? t.v[f] - eta * g : 0.f;
                 }
-                t.store(V, ii, rbase, P.coh);
+                t.store(V, ii, rbase);
             };
             if (i >= 0) upd(vr, i, x, wi);
             for (int base = 64; base < nnz; base += 64) {
@@ -426,7 +412,7 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 }  // namespace
 
 // ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant,
-//     w0_every, coh
+//     w0_every
 //     (variant 0 = fm_pipe_kernel, 1 = fm_kernel)
 // hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
@@ -441,7 +427,6 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     P.w0_shards = ip[10];
     const int variant = ip[11];
     P.w0_every = ip[12] > 0 ? ip[12] : 1;
-    P.coh = ip[13];
     if (P.w0_shards < 1 || P.w0_shards > 64) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];

@@ -558,22 +558,11 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
     const int32_t* __restrict__ order, float4* __restrict__ S0, uint8_t* __restrict__ touched0,
     float* __restrict__ RSW, double* __restrict__ loss_out, const int32_t* __restrict__ hot_slot,
-    const int32_t* __restrict__ hot_feat, int H, int CH, int min_rows, int every, int coh,
-    float4* __restrict__ hacc) {
+    const int32_t* __restrict__ hot_feat, int H, int CH, int min_rows, int every, float4* __restrict__ hacc) {
     extern __shared__ float s_acc[];             // HOT: 3 x H floats, see hot_add
     const bool owner = HOT && hacc != nullptr;   // hot features in owner mode (hot_owner_rule)
-    // coh: feature-state stores write through and drop the line from this XCD's L2 (SC1), so
-    // the other XCDs' next reads of a hot feature fetch the latest value (A/B, HM_LINEAR_COH)
     const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(S0, (short)0, -1, 0x00020000);
-    auto store = [&](float4* p, const F4& v) {
-        if (coh)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (__attribute__((ext_vector_type(4))) uint32_t){__float_as_uint(v.w), __float_as_uint(v.s1),
-                                                                __float_as_uint(v.s2), __float_as_uint(v.s3)},
-                rs0, (uint32_t)((const char*)p - (const char*)S0), 0, 16);
-        else
-            st4(p, v);
-    };
+    auto store = [&](float4* p, const F4& v) { st4(p, v); };
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool active = g < W;
@@ -716,7 +705,15 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                     float4* p = S + hot_feat[h];
                     F4 st = ld4m<true>(p);
                     hot_nstep(P, st, gsum, g2sum, n, sk, rs[RS_EVE_D]);
-                    store(p, st);
+                    // write-through (SC1): the line leaves this XCD's L2, so the other XCDs'
+                    // next reads of the hot feature fetch it (the cold features' stores stay plain)
+                    if (dims <= (1 << 28))
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            (__attribute__((ext_vector_type(4))) uint32_t){__float_as_uint(st.w), __float_as_uint(st.s1),
+                                                                            __float_as_uint(st.s2), __float_as_uint(st.s3)},
+                            rs0, (uint32_t)((const char*)p - (const char*)S0), 0, 16);
+                    else
+                        st4(p, st);
                 }
             }
         }
@@ -825,11 +822,10 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
                                   int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,
                                   float* RSW, double* loss_out, const int32_t* hot_slot, const int32_t* hot_feat,
-                                  int H, int CH, int min_rows, int every, int coh, float* hacc,
+                                  int H, int CH, int min_rows, int every, float* hacc,
                                   hipStream_t stream) {
     if (n_rows <= 0) return 0;
     if (W <= 0 || dims <= 0 || P->n_labels != 1 || has_covar(P->algo)) return (int)hipErrorInvalidValue;
-    if (coh && (size_t)R * (size_t)dims * 16 >= ((size_t)1 << 32)) coh = 0;   // 32-bit buffer offsets
     if (R != 1 && (R % 8 != 0 || (W + 3) / 4 < R)) return (int)hipErrorInvalidValue;
     const bool hot = H > 0;
     const size_t lds = hot ? (size_t)H * 3 * sizeof(float) : 0;
@@ -839,12 +835,10 @@ HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int
     if (hot && (hot_slot == nullptr || hot_feat == nullptr || H > HM_HOT_MAX || CH <= 0 || min_rows <= 0 || every <= 0 ||
                 !(own ? (hot_owner_rule(*P) && R == 1) : hot_sum_rule(*P))))
         return (int)hipErrorInvalidValue;
-    // owner stores: write-through (SC1) so the other XCDs' next reads fetch them
-    if (own && (size_t)dims * 16 < ((size_t)1 << 32)) coh = 1;
 #define HM_SHARED_LAUNCH(RL, NTT, HT)                                                                  \
     hipLaunchKernelGGL((linear_shared_kernel<RL, NTT, HT>), dim3((W + 3) / 4), dim3(256), lds, stream, *P, n_rows, \
                        dims, t0, W, R, indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched,   \
-                       RSW, loss_out, hot_slot, hot_feat, H, CH, min_rows, every, coh,                  \
+                       RSW, loss_out, hot_slot, hot_feat, H, CH, min_rows, every,                       \
                        own ? reinterpret_cast<float4*>(hacc) : nullptr)
     if (hot) {
         if (reload && nt) HM_SHARED_LAUNCH(true, true, true);

@@ -61,8 +61,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),
-                   int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY))),
-                   int(os.environ.get("HM_FM_COH", "0")) if dims * KP * 2 < (1 << 32) else 0],
+                   int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY)))],
                   dtype=np.int32)
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,

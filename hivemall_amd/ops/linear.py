@@ -267,7 +267,7 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
                                               int(st.meta.get("nt", True)),
                                               p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
                                               p(st.touched), p(st.RS), p(loss), p(hs), p(hf), H, ch, hmin, hevery,
-                                              int(os.environ.get("HM_LINEAR_COH", "0")), p(hacc),
+                                              p(hacc),
                                               _native.stream_of(dev))
     _native.check(rc, "hm_linear_train_shared")
     return loss
@@ -352,7 +352,7 @@ _P = _native.c_p
 _native.register_hip("hm_linear_train", [_P, _P, _native.c_i64] + [_P] * 11 + [_P])
 _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
-                                              C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 5
+                                              C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 4
                      + [_P, _P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
