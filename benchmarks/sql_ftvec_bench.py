@@ -55,10 +55,25 @@ def main():
         for mode in (("fused", "strings") if dev.startswith("cuda") else ("strings",)):
             os.environ["HM_SQL_DEVICE_FTVEC"] = "1" if mode == "fused" else "0"
             for rep in range(2):                     # the first run pays one-time setup
+                prof = None
+                if rep == 1 and os.environ.get("HM_SQL_PROFILE") == "1":
+                    import cProfile
+                    prof = cProfile.Profile()
+                    prof.enable()
                 t = time.perf_counter()
                 m = s.sql("SELECT train_classifier(add_bias(feature_hashing(features)), label, "
                           "'-loss logloss -opt adagrad') AS (feature, weight) FROM criteo")
+                if dev.startswith("cuda"):
+                    import torch
+                    torch.cuda.synchronize()
                 t_all = time.perf_counter() - t
+                if prof is not None:
+                    import io
+                    import pstats
+                    prof.disable()
+                    buf = io.StringIO()
+                    pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(30)
+                    print(f"== profile {mode}\n" + buf.getvalue(), file=sys.stderr, flush=True)
             res[mode] = {"train_stmt_s": round(t_all, 3), "train_stmt_rows_per_s": round(n / t_all),
                          "ingest": ingest.LAST_STATS.as_dict()}
             tabs[mode] = m.sort_values("feature").reset_index(drop=True)

@@ -300,13 +300,26 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const int32_t* __restric
     extern __shared__ float s_sum[];
     for (int k = threadIdx.x; k < 2 * T; k += blockDim.x) s_sum[k] = 0.f;
     __syncthreads();
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-        const int l = leaf[r];
-        if (l < 0 || l >= T) continue;
-        const float h = hh[r];
-        if (h == 0.f) continue;
-        atomicAdd(&s_sum[2 * l], st2[2 * r]);
-        atomicAdd(&s_sum[2 * l + 1], h);
+    // LEAF_U rows per thread with every load issued before the first LDS add
+    constexpr int LEAF_U = 8;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r0 < n; r0 += step * LEAF_U) {
+        int l[LEAF_U];
+        float h[LEAF_U], g[LEAF_U];
+#pragma unroll
+        for (int u = 0; u < LEAF_U; ++u) {
+            const int64_t r = r0 + u * step;
+            const bool in = r < n;
+            l[u] = in ? leaf[r] : -1;
+            h[u] = in ? hh[r] : 0.f;
+            g[u] = in ? st2[2 * r] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < LEAF_U; ++u) {
+            if (l[u] < 0 || l[u] >= T || h[u] == 0.f) continue;
+            atomicAdd(&s_sum[2 * l[u]], g[u]);
+            atomicAdd(&s_sum[2 * l[u] + 1], h[u]);
+        }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < 2 * T; k += blockDim.x)
@@ -857,6 +870,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
 // part_scatter_kernel (rows = NULL) places the rows identically.  ROUTE_U rows per thread are in
 // flight: the node -> split -> bins -> child loads are a dependent chain per row.
 constexpr int ROUTE_U = 4;
+constexpr int ROUTE_BALLOT_KEYS = 16;
 __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n, int dpad,
                                                           int32_t* __restrict__ node_of_row,
                                                           const int32_t* __restrict__ split_feat,
@@ -871,7 +885,11 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
     __syncthreads();
     const int64_t chunk = (n + G - 1) / G;
     const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
-    for (int64_t q0 = r0 + threadIdx.x; q0 < r1; q0 += (int64_t)blockDim.x * ROUTE_U) {
+    uint32_t wcnt[ROUTE_BALLOT_KEYS];
+#pragma unroll
+    for (int q = 0; q < ROUTE_BALLOT_KEYS; ++q) wcnt[q] = 0;
+    // every wave runs the same trip count (ballots need the whole wave): the bound is the block's
+    for (int64_t q0 = r0 + threadIdx.x; q0 - threadIdx.x < r1; q0 += (int64_t)blockDim.x * ROUTE_U) {
         int nd[ROUTE_U], f[ROUTE_U];
 #pragma unroll
         for (int u = 0; u < ROUTE_U; ++u) {
@@ -895,10 +913,26 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
 #pragma unroll
         for (int u = 0; u < ROUTE_U; ++u) {
             const int c = nd[u] - nb;
-            if (nd[u] < 0 || c < 0 || c >= nlut) continue;
-            const int k = lut[c];
-            if (k < nkeys) atomicAdd(&s_cnt[k], 1);
+            int k = -1;
+            if (nd[u] >= 0 && c >= 0 && c < nlut) {
+                k = lut[c];
+                if (k >= nkeys) k = -1;
+            }
+            if (nkeys <= ROUTE_BALLOT_KEYS) {
+                // few keys (the upper levels): every row of a wave hits one of <= 16 LDS words,
+                // so count them with ballots into wave-uniform registers instead
+#pragma unroll
+                for (int q = 0; q < ROUTE_BALLOT_KEYS; ++q)
+                    if (q < nkeys) wcnt[q] += __popcll(__ballot(k == q));
+            } else if (k >= 0) {
+                atomicAdd(&s_cnt[k], 1);
+            }
         }
+    }
+    if (nkeys <= ROUTE_BALLOT_KEYS && (threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int q = 0; q < ROUTE_BALLOT_KEYS; ++q)
+            if (q < nkeys && wcnt[q]) atomicAdd(&s_cnt[q], (int)wcnt[q]);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) counts[(size_t)k * G + blockIdx.x] = s_cnt[k];
