@@ -15,9 +15,13 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-RULES = ["-opt sgd -eta0 0.05", "-opt momentum -eta0 0.05", "-opt nesterov -eta0 0.05", "-opt adagrad",
-         "-opt adagrad -reg l1 -lambda 1e-6", "-opt rmsprop", "-opt rmspropgraves", "-opt adadelta",
-         "-opt adam", "-opt nadam", "-opt eve", "-opt adamhd"]
+# every rule at a step size where the sequential learner converges on these rows (held-out
+# 0.476-0.487 at 300 K rows; a diverging or oscillating sequential run, e.g. momentum at eta0 0.05
+# or Adam at eta0 0.1, has no trajectory for a parallel engine to match)
+RULES = ["-opt sgd -eta0 0.05", "-opt momentum -eta0 0.005", "-opt nesterov -eta0 0.005", "-opt adagrad",
+         "-opt adagrad -reg l1 -lambda 1e-6", "-opt rmsprop -eta0 0.01", "-opt rmspropgraves -eta0 0.001",
+         "-opt adadelta", "-opt adam -eta0 0.01", "-opt nadam -eta0 0.01", "-opt eve -eta0 0.01",
+         "-opt adamhd -eta0 0.01"]
 
 
 def rows_of(n, bits, seed):

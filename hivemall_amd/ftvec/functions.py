@@ -54,7 +54,8 @@ def _list_column(col):
         return None
     if isinstance(col.dtype, pd.ArrowDtype):
         a = col.array._pa_array
-        a = a.combine_chunks() if isinstance(a, pa.ChunkedArray) else a
+        if isinstance(a, pa.ChunkedArray):      # one chunk: its array as is (combine_chunks copies)
+            a = a.chunk(0) if a.num_chunks == 1 else a.combine_chunks()
         if (pa.types.is_list(a.type) or pa.types.is_large_list(a.type)) and \
                 (pa.types.is_string(a.type.value_type) or pa.types.is_large_string(a.type.value_type)):
             return a
@@ -165,7 +166,8 @@ def _numeric_list_column(col):
 
     if isinstance(col.dtype, pd.ArrowDtype):
         a = col.array._pa_array
-        a = a.combine_chunks() if isinstance(a, pa.ChunkedArray) else a
+        if isinstance(a, pa.ChunkedArray):      # one chunk: its array as is (combine_chunks copies)
+            a = a.chunk(0) if a.num_chunks == 1 else a.combine_chunks()
         if not (pa.types.is_list(a.type) or pa.types.is_large_list(a.type)):
             return None
         vt = a.type.value_type

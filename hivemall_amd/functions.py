@@ -80,6 +80,8 @@ def _column(a, arrow_ok: bool):
         return arr.combine_chunks() if arr.num_chunks != 1 else arr.chunk(0)
     if isinstance(a, pd.Series) and isinstance(a.dtype, pd.ArrowDtype):
         return a.array._pa_array.to_pylist()
+    if isinstance(a, pd.Series) and a.dtype.kind in "biuf":
+        return a.to_numpy()          # labels / targets / ids: no Python object per row
     return a.tolist() if isinstance(a, pd.Series) else list(a)
 
 

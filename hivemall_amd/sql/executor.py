@@ -1099,7 +1099,9 @@ class Session:
                 from .device_ftvec import try_device_features
 
                 dev_feats = try_device_features(self, f.args[0], src, ctes)
+            # a constant string (the options) is read once: no n-row object column for it
             args = [dev_feats if (k == 0 and dev_feats is not None) else
+                    pd.Series([a.value], dtype=object) if (isinstance(a, Lit) and isinstance(a.value, str)) else
                     _ser(self.eval(a, src, ctes), src.n).reset_index(drop=True) for k, a in enumerate(f.args)]
         else:
             args = [_ser(self.eval(a, src, ctes), src.n).tolist() for a in f.args]
