@@ -63,8 +63,9 @@ LEARNER_BASE_OPTS = [
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
     opt("shared_waves", None, 0, int,
-        "[engine] shared engine: rows in flight (0 = auto: 1024 when the hot features are "
-        "pre-aggregated per block (AdaGrad / AdaGrad-RDA general learners), else 512)"),
+        "[engine] shared engine: rows in flight (0 = auto per rule, ops/linear.py rule_waves: "
+        "1024 AdaGrad / AdaGrad-RDA, 512 AdaGrad-L1 / AdaDelta / RMSprop-Graves, 8 for the other "
+        "general-learner rules, whose parity with the sequential learner needs it)"),
 ] + CKPT_OPTS
 
 GENERAL_OPTS = [
@@ -360,7 +361,7 @@ class OnlineLinearLearner(Learner):
                 self.state = LO.new_shared_state(
                     dims, self.device, rows.n, replicas=int(self.cl["shared_replicas"]),
                     waves=LO.shared_waves(rows.n, int(self.cl["shared_waves"])
-                                          or (1024 if LO.hot_rule(self.P) else 512)))
+                                          or LO.rule_waves(self.P)))
             except ValueError as e:
                 raise UDFArgumentException(f"{self.NAME}: {e}") from None
             if self._warm is not None:

@@ -202,6 +202,35 @@ def hot_owner_rule(P: LinParams) -> bool:
     return P.algo == ALGOS["general"] and not hot_rule(P) and P.reg != REGS["rda"] and P.n_labels == 1
 
 
+# Rows in flight of the shared-table engine per rule (``-shared_waves 0``), from the held-out
+# logloss vs the sequential CPU engine at -dims 2^24 (1 M Criteo-shaped rows, every rule at a
+# step size where the sequential learner converges; benchmarks/linear_rules_parity.py,
+# profiles/r4/linear_rules_*.jsonl, docs/compat.md "Shared-table engine: per-rule parity"):
+#  * AdaGrad with no / L2 regularisation and AdaGrad-RDA (hot features pre-aggregated as sums):
+#    -6e-4 .. -1.1e-3 at 512 and 1,024 rows in flight -> 1,024 (~98 M rows/s);
+#  * AdaGrad-L1 / elastic net, AdaDelta, RMSprop-Graves (hot features in owner mode):
+#    +2e-3 .. +4.8e-3 at 512 (two runs) -> 512 (~94 M rows/s);
+#  * SGD, momentum, Nesterov, RMSprop and the Adam family: +2.5e-3 .. +1e-2 at 16 .. 1,024 rows
+#    in flight whatever the hot-feature handling (owner mode, its flush schedule, or none:
+#    linear_owner_schedule_sweep.log) — the gap is the Hogwild staleness of the other features —
+#    and within 1.3e-3 at <= 8 (linear_rules_fewwaves.jsonl) -> routed to 8 rows in flight
+#    (~1.7 M rows/s, 3x the CPU engine).  -shared_waves 512 buys ~55x the rate at that gap.
+SEQ_WAVES = 8
+
+
+def rule_waves(P: LinParams) -> int:
+    """Default rows in flight of the shared-table engine for the rule (see above)."""
+    if hot_rule(P):
+        return 1024
+    general = P.algo == ALGOS["general"]
+    if general and (P.opt == OPTIMIZERS["adadelta"] or P.opt == OPTIMIZERS["rmspropgraves"]
+                    or (P.opt == OPTIMIZERS["adagrad"] and P.reg in (REGS["l1"], REGS["elasticnet"]))):
+        return 512
+    if general:
+        return SEQ_WAVES
+    return SHARED_WAVES
+
+
 def hot_features(st: LinearState, P: LinParams, idx: torch.Tensor, n_rows: int):
     """The features the shared-table kernel pre-aggregates per block instead of updating them
     Hogwild (csrc/kernels/linear.hip, HOT): the at most ``HOT_MAX`` most frequent features of

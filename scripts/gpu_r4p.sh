@@ -1,0 +1,13 @@
+#!/bin/bash
+# Full GPU test suite after the round-4 changes (per-rule rows in flight, gbt2, packed histograms,
+# owner-mode hot features, FM w0 refresh), then smoke and a 1-GPU bench.
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r4p
+mkdir -p $O
+export HM_NO_AUTOBUILD=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || true
+tail -5 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1
+tail -1 $O/bench.log
