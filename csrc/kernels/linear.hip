@@ -418,7 +418,7 @@ __device__ __forceinline__ float rda_w(const Params& P, float u, float G, const 
 // update is lost and none is applied twice.  Rows still read the hot weights Hogwild (stale by at
 // most a chunk).  One table (R = 1) only.
 __host__ __device__ __forceinline__ bool hot_owner_rule(const Params& P) {
-    return P.algo == A_GENERAL && !hot_sum_rule(P) && P.reg != R_RDA;
+    return P.algo == A_GENERAL && !hot_sum_rule(P);   // (R_RDA regularises AdaGrad only)
 }
 
 // Sum of x_i = beta^i x0 + c (1 - beta^i) / (1 - beta) over i = 1 .. n (a geometric EMA / momentum

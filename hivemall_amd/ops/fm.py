@@ -33,8 +33,12 @@ class FMHyper:
 # each re-read is 64 lines the other waves' atomics have just dropped from L2.  Measured on the
 # Criteo-shaped 2^24 bench (profiles/r4/fm_w0_every_ab.log, two reps each): every row 145 M rows/s
 # (held-out 0.4757), every 8 rows 234 M (0.4762), every 32 rows 300 M but 0.54-0.74 (the bias
-# drifts between refreshes) -> 8
+# drifts between refreshes) -> 8.  Early in training the bias is far from its optimum and the
+# delayed view turns the waves' bias steps into an overshoot (200 K rows, bf16 V: held-out 0.546
+# vs 0.486 for the 8-mapper average), so a pass that starts within the first W0_WARM_ROWS rows of
+# the stream re-reads every row.
 W0_EVERY = 8
+W0_WARM_ROWS = 1 << 20
 
 
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
@@ -61,7 +65,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),
-                   int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY)))],
+                   int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1)))],
                   dtype=np.int32)
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,

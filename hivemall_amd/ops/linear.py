@@ -199,7 +199,9 @@ def hot_owner_rule(P: LinParams) -> bool:
     gradient (hot_nstep), on a single table.  ``HM_LINEAR_HOT_OWNER=0`` leaves them Hogwild."""
     if os.environ.get("HM_LINEAR_HOT", "1") == "0" or os.environ.get("HM_LINEAR_HOT_OWNER", "1") == "0":
         return False
-    return P.algo == ALGOS["general"] and not hot_rule(P) and P.reg != REGS["rda"] and P.n_labels == 1
+    # (-reg rda is the general learner's default: for every optimiser but AdaGrad it means no
+    # regularisation, and AdaGrad-RDA is a hot_rule)
+    return P.algo == ALGOS["general"] and not hot_rule(P) and P.n_labels == 1
 
 
 # Rows in flight of the shared-table engine per rule (``-shared_waves 0``), from the held-out
