@@ -480,7 +480,10 @@ class ModelMixer:
         w1 = self.wire_bytes                       # (average_delta: the first call seeds it)
         fn(tensors)
         wire = self.wire_bytes - w1                # bytes one rank sends per mix
-        payload = wire * self.world // max(1, 2 * (self.world - 1))
+        if self.world > 1:
+            payload = wire * self.world // (2 * (self.world - 1))
+        else:                                      # one rank sends nothing: the mixed bytes
+            payload = sum(t.numel() * (2 if fn == self.average_delta else t.element_size()) for t in tensors)
         self.ctx.barrier()
         cuda = tensors[0].is_cuda
         if cuda:
