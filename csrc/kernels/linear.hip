@@ -409,132 +409,34 @@ __device__ __forceinline__ float rda_w(const Params& P, float u, float G, const 
     return mean < 0.f ? 0.f : -sign * k.eta * k.t * mean / sqrtf(G);
 }
 
-// The other rules of the general learner (SGD, momentum, Nesterov, RMSprop(-Graves), AdaDelta,
-// the Adam family, AdaGrad with L1 / elastic-net) keep their hot features in "owner" mode: the
+// AdaGrad with L1 / elastic-net regularisation keeps its hot features in "owner" mode (its
+// sign(w) term is not a function of summed gradients, so hot_flush4's atomics do not apply): the
 // blocks add their per-chunk sums (sum g, sum g^2, rows) to a global accumulator per hot feature
 // (non-returning atomics, nothing lost), and ONE thread of the grid owns each hot feature: at
-// every chunk end it takes the accumulated sums (atomic exchange) and applies the rule's n-step
-// update (hot_nstep) to the feature's state with plain read-modify-write — a single writer, so no
-// update is lost and none is applied twice.  Rows still read the hot weights Hogwild (stale by at
-// most a chunk).  One table (R = 1) only.
+// every chunk end it takes the accumulated sums (atomic exchange) and applies the n-step update
+// (hot_nstep) with plain read-modify-write — a single writer, so no update is lost and none is
+// applied twice.  Rows still read the hot weights Hogwild (stale by at most a chunk).  One table
+// (R = 1) only.  Closed forms of the same n steps for SGD, momentum, RMSprop(-Graves), AdaDelta
+// and the Adam family were measured and removed: without the sequential learner's feedback a
+// chunk's thousands of steps diverge (profiles/r4/linear_rules_owner_all_rules.jsonl).
 __host__ __device__ __forceinline__ bool hot_owner_rule(const Params& P) {
-    return P.algo == A_GENERAL && !hot_sum_rule(P);   // (R_RDA regularises AdaGrad only)
+    return P.algo == A_GENERAL && P.opt == O_ADAGRAD && (P.reg == R_L1 || P.reg == R_ELASTIC);
 }
 
-// Sum of x_i = beta^i x0 + c (1 - beta^i) / (1 - beta) over i = 1 .. n (a geometric EMA / momentum
-// recursion driven by a constant c), and its last term x_n.
-__device__ __forceinline__ void geo_sum(float beta, float n, float x0, float c, float* sum, float* last) {
-    const float bn = powf(beta, n);
-    if (beta >= 1.f) { *sum = n * x0 + c * n * (n + 1.f) * 0.5f; *last = x0 + c * n; return; }
-    const float q = beta * (1.f - bn) / (1.f - beta);       // sum of beta^i, i = 1 .. n
-    *sum = x0 * q + c / (1.f - beta) * (n - q);
-    *last = bn * x0 + c * (1.f - bn) / (1.f - beta);
-}
-
-// n sequential steps of the general learner's rule on one feature, every step with the chunk's
-// mean gradient a = sum g / n and mean squared gradient b = sum g^2 / n (regularisation
-// evaluated at the state the owner read), in closed form: the exponential averages are advanced
-// exactly (beta^n), the weight moves by the sum of the n steps, with each step's normaliser taken
-// at the chunk's midpoint (AdaGrad: the exact integral of 1 / sqrt(G0 + i b)).  SGD and momentum
-// are exact for a constant gradient; the normalised rules differ only in how the normaliser
-// varies inside one chunk.
-__device__ __forceinline__ void hot_nstep(const Params& P, F4& s, float gsum, float g2sum, float n, const StepK& k,
-                                          float eve_d) {
+// n sequential AdaGrad steps on one feature with the chunk's mean gradient a = sum g / n and mean
+// squared gradient b = sum g^2 / n, regularisation evaluated at the state the owner read:
+// G += n b; w moves by eta a sum_i 1 / sqrt(G0 + i b) ~ eta a 2n / (sqrt(G_n) + sqrt(G0)) (the
+// integral of the normaliser, exact in the limit of many small steps).
+__device__ __forceinline__ void hot_nstep(const Params& P, F4& s, float gsum, float g2sum, float n, const StepK& k) {
     if (n <= 0.f) return;
-    float r = 0.f;
-    switch (P.reg) {
-        case R_L1: r = P.lambda * sgnf(s.w); break;
-        case R_L2: r = P.lambda * s.w; break;
-        case R_ELASTIC: r = P.lambda * (P.l1_ratio * sgnf(s.w) + (1.f - P.l1_ratio) * s.w); break;
-        default: break;
-    }
+    const float r = P.reg == R_L1 ? P.lambda * sgnf(s.w)
+                                  : P.lambda * (P.l1_ratio * sgnf(s.w) + (1.f - P.l1_ratio) * s.w);
     const float a0 = gsum / n;
-    const float a = a0 + r;                                   // mean regularised gradient
-    const float b = fmaxf(g2sum / n + 2.f * a0 * r + r * r, 0.f);   // its mean square
-    const float eta = k.eta;
-    const float half = 0.5f * n;
-    switch (P.opt) {
-        case O_SGD: s.w -= eta * n * a; break;
-        case O_MOMENTUM: {                                    // v_i = beta v + eta g; w -= v_i
-            float sum, last;
-            geo_sum(P.beta1, n, s.s1, eta * a, &sum, &last);
-            s.w -= sum;
-            s.s1 = last;
-            break;
-        }
-        case O_NESTEROV: {                                    // v_i = beta v - eta g; w += -beta v_{i-1} + (1+beta) v_i
-            float sum, last;
-            geo_sum(P.beta1, n, s.s1, -eta * a, &sum, &last);
-            const float prev_sum = s.s1 + sum - last;         // v_0 .. v_{n-1}
-            s.w += -P.beta1 * prev_sum + (1.f + P.beta1) * sum;
-            s.s1 = last;
-            break;
-        }
-        case O_ADAGRAD: {                                     // sum_i 1 / sqrt(G0 + i b) ~ 2n / (sqrt(G_n) + sqrt(G0))
-            const float G0 = s.s1, Gn = G0 + n * b;
-            s.w -= eta * a * 2.f * n / (sqrtf(Gn) + sqrtf(G0) + 2.f * P.eps);
-            s.s1 = Gn;
-            break;
-        }
-        case O_RMSPROP: {
-            const float dh = powf(P.decay, half), dn = dh * dh;
-            const float mid = dh * s.s1 + (1.f - dh) * b;
-            s.w -= eta * n * a / (sqrtf(mid) + P.eps);
-            s.s1 = dn * s.s1 + (1.f - dn) * b;
-            break;
-        }
-        case O_RMSPROP_GRAVES: {
-            const float dh = powf(P.decay, half), dn = dh * dh;
-            const float n1 = dh * s.s1 + (1.f - dh) * b, g1 = dh * s.s2 + (1.f - dh) * a;
-            const float den = n1 - g1 * g1 + P.eps;
-            float sum, last;
-            geo_sum(P.beta1, n, s.s3, -eta * P.alpha * a / sqrtf(den > 0.f ? den : P.eps), &sum, &last);
-            s.w += sum;
-            s.s3 = last;
-            s.s1 = dn * s.s1 + (1.f - dn) * b;
-            s.s2 = dn * s.s2 + (1.f - dn) * a;
-            break;
-        }
-        case O_ADADELTA: {
-            const float rh = powf(P.rho, half), rn = rh * rh;
-            const float g2mid = rh * s.s1 + (1.f - rh) * b;
-            const float ratio = sqrtf(s.s2 + P.eps) / sqrtf(g2mid + P.eps);
-            s.w -= n * ratio * a;
-            s.s1 = rn * s.s1 + (1.f - rn) * b;
-            s.s2 = rn * s.s2 + (1.f - rn) * ratio * ratio * b;
-            break;
-        }
-        case O_ADAM: case O_EVE: case O_ADAM_HD: case O_NADAM: {
-            float msum, mlast;
-            geo_sum(P.beta1, n, s.s1, (1.f - P.beta1) * a, &msum, &mlast);
-            const float bh = powf(P.beta2, half), bn = bh * bh;
-            const float vmid = bh * s.s2 + (1.f - bh) * b;
-            const float vlast = bn * s.s2 + (1.f - bn) * b;
-            if (P.opt == O_NADAM) {
-                const float mh = P.beta1 * msum / k.c1n + (1.f - P.beta1) * n * a / k.c1;
-                s.w -= eta * P.alpha * mh / (sqrtf(vmid / k.c2) + P.eps);
-            } else {
-                float vhat = vmid;
-                if (P.opt == O_ADAM && P.amsgrad) { s.s3 = fmaxf(s.s3, vlast); vhat = fmaxf(s.s3, vmid); }
-                float alpha = P.alpha;
-                if (P.opt == O_ADAM_HD) {
-                    // hypergradient of the step size: sum_i g_i u_{i-1} ~ n a u(state read)
-                    if (s.s3 == 0.f) s.s3 = P.alpha;
-                    const float cp1 = k.cp1, cp2 = k.cp2;
-                    const float u = cp1 > 0.f ? (s.s1 / cp1) / (sqrtf(s.s2 / (cp2 > 0.f ? cp2 : 1.f)) + P.eps) : 0.f;
-                    s.s3 += P.beta_hd * n * a * u;
-                    alpha = s.s3;
-                }
-                float lr = eta * alpha * sqrtf(k.c2) / k.c1;
-                if (P.opt == O_EVE) lr /= (eve_d > 0.f ? eve_d : 1.f);
-                s.w -= lr * msum / (sqrtf(vhat) + P.eps);
-            }
-            s.s1 = mlast;
-            s.s2 = vlast;
-            break;
-        }
-        default: break;
-    }
+    const float a = a0 + r;
+    const float b = fmaxf(g2sum / n + 2.f * a0 * r + r * r, 0.f);
+    const float G0 = s.s1, Gn = G0 + n * b;
+    s.w -= k.eta * a * 2.f * n / (sqrtf(Gn) + sqrtf(G0) + 2.f * P.eps);
+    s.s1 = Gn;
 }
 
 // Block barrier over the LDS accumulators only: waits for this wave's LDS operations, not for
@@ -704,7 +606,7 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
                     const float g2sum = atomicExch(&hacc[h].y, 0.f);
                     float4* p = S + hot_feat[h];
                     F4 st = ld4m<true>(p);
-                    hot_nstep(P, st, gsum, g2sum, n, sk, rs[RS_EVE_D]);
+                    hot_nstep(P, st, gsum, g2sum, n, sk);
                     // write-through (SC1): the line leaves this XCD's L2, so the other XCDs'
                     // next reads of the hot feature fetch it (the cold features' stores stay plain)
                     if (dims <= (1 << 28))
@@ -750,7 +652,7 @@ __global__ __launch_bounds__(256) void hot_owner_final_kernel(Params P, float4* 
     hacc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (A.z <= 0.f) return;
     F4 st = ld4(S + hot_feat[h]);
-    hot_nstep(P, st, A.x, A.y, A.z, k, RSW[RS_EVE_D]);
+    hot_nstep(P, st, A.x, A.y, A.z, k);
     st4(S + hot_feat[h], st);
 }
 

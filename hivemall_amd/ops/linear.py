@@ -199,9 +199,14 @@ def hot_owner_rule(P: LinParams) -> bool:
     gradient (hot_nstep), on a single table.  ``HM_LINEAR_HOT_OWNER=0`` leaves them Hogwild."""
     if os.environ.get("HM_LINEAR_HOT", "1") == "0" or os.environ.get("HM_LINEAR_HOT_OWNER", "1") == "0":
         return False
-    # (-reg rda is the general learner's default: for every optimiser but AdaGrad it means no
-    # regularisation, and AdaGrad-RDA is a hot_rule)
-    return P.algo == ALGOS["general"] and not hot_rule(P) and P.n_labels == 1
+    # AdaGrad with L1 / elastic-net regularisation only: its n-step update is normalised by the
+    # accumulated squared gradient, so a chunk's thousands of steps stay bounded.  The closed
+    # forms of the unnormalised or exponentially-averaged rules take those steps without the
+    # sequential learner's feedback and diverge (held-out logloss +0.5 .. +278 for SGD, momentum,
+    # RMSprop, AdaDelta and the Adam family at 512 rows in flight,
+    # profiles/r4/linear_rules_owner_all_rules.jsonl)
+    return (P.algo == ALGOS["general"] and P.opt == OPTIMIZERS["adagrad"]
+            and P.reg in (REGS["l1"], REGS["elasticnet"]) and P.n_labels == 1)
 
 
 # Rows in flight of the shared-table engine per rule (``-shared_waves 0``), from the held-out
@@ -210,12 +215,11 @@ def hot_owner_rule(P: LinParams) -> bool:
 # profiles/r4/linear_rules_*.jsonl, docs/compat.md "Shared-table engine: per-rule parity"):
 #  * AdaGrad with no / L2 regularisation and AdaGrad-RDA (hot features pre-aggregated as sums):
 #    -6e-4 .. -1.1e-3 at 512 and 1,024 rows in flight -> 1,024 (~98 M rows/s);
-#  * AdaGrad-L1 / elastic net, AdaDelta, RMSprop-Graves (hot features in owner mode):
-#    +2e-3 .. +4.8e-3 at 512 (two runs) -> 512 (~94 M rows/s);
-#  * SGD, momentum, Nesterov, RMSprop and the Adam family: +2.5e-3 .. +1e-2 at 16 .. 1,024 rows
-#    in flight whatever the hot-feature handling (owner mode, its flush schedule, or none:
-#    linear_owner_schedule_sweep.log) — the gap is the Hogwild staleness of the other features —
-#    and within 1.3e-3 at <= 8 (linear_rules_fewwaves.jsonl) -> routed to 8 rows in flight
+#  * AdaGrad-L1 / elastic net (hot features in owner mode): +1.8e-3 .. +1.9e-3 at 512 -> 512;
+#  * AdaDelta (plain Hogwild): +3.4e-3 .. +4.1e-3 at 512 -> 512 (~94 M rows/s);
+#  * SGD, momentum, Nesterov, RMSprop(-Graves) and the Adam family: +2.5e-3 .. +1e-2 at 16 ..
+#    1,024 rows in flight (plain Hogwild; their closed-form hot-feature updates diverge), and
+#    within 1.3e-3 at <= 8 (linear_rules_fewwaves.jsonl) -> routed to 8 rows in flight
 #    (~1.7 M rows/s, 3x the CPU engine).  -shared_waves 512 buys ~55x the rate at that gap.
 SEQ_WAVES = 8
 
@@ -225,8 +229,7 @@ def rule_waves(P: LinParams) -> int:
     if hot_rule(P):
         return 1024
     general = P.algo == ALGOS["general"]
-    if general and (P.opt == OPTIMIZERS["adadelta"] or P.opt == OPTIMIZERS["rmspropgraves"]
-                    or (P.opt == OPTIMIZERS["adagrad"] and P.reg in (REGS["l1"], REGS["elasticnet"]))):
+    if general and (P.opt == OPTIMIZERS["adadelta"] or hot_owner_rule(P)):
         return 512
     if general:
         return SEQ_WAVES
