@@ -367,8 +367,8 @@ __host__ __device__ __forceinline__ bool hot_sum_rule(const Params& P) {
 __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__ S, float (&gs)[HM_HOT_U],
                                            float (&g2)[HM_HOT_U], const float (&cnt)[HM_HOT_U],
                                            const int (&f)[HM_HOT_U], const StepK& k) {
-    // only non-returning atomics: they retire at L2 without the issuing wave waiting, so blocks
-    // that flush the same hot address at once no longer queue behind each other's round trips
+    // the RDA sums and the weight deltas are non-returning atomics (they retire at L2 without the
+    // issuing wave waiting); AdaGrad's accumulator add returns the value it found
     if (P.reg == R_L2) {
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u) {
@@ -388,14 +388,18 @@ __device__ __forceinline__ void hot_flush4(const Params& P, float4* __restrict__
             atomicAdd(&S[f[u]].z, g2[u]);
         }
     } else if (P.opt == O_ADAGRAD) {
+        // the accumulator's value BEFORE this block's add comes back from the atomic: blocks that
+        // flush one feature at once are serialised there and each normalises by every earlier
+        // block's squared gradients, as the sequential learner would.  (A separately loaded G
+        // let up to all blocks normalise by the same stale G: early in a pass, G ~ 0, that is a
+        // step sqrt(#blocks) too large — held-out logloss +0.006 .. +0.77 for -reg no.)
         float G0[HM_HOT_U];
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u)
-            G0[u] = f[u] >= 0 ? __builtin_nontemporal_load(&S[f[u]].y) : 0.f;
+            G0[u] = f[u] >= 0 ? atomicAdd(&S[f[u]].y, g2[u]) : 0.f;
 #pragma unroll
         for (int u = 0; u < HM_HOT_U; ++u) {
             if (f[u] < 0) continue;
-            atomicAdd(&S[f[u]].y, g2[u]);
             atomicAdd(&S[f[u]].x, -k.eta * gs[u] / (sqrtf(G0[u] + g2[u]) + P.eps));
         }
     }
