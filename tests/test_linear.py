@@ -255,7 +255,9 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
     yy = (test.y > 0).float()
     res = {}
     for dev in ("cpu", "cuda"):
-        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216", device=dev)
+        # one epoch: over more, the convergence check can stop the two engines at different
+        # epochs (train_classifier's default is up to 10)
+        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216 -iters 1", device=dev)
         m.fit(rows=rows.to(dev))
         if dev == "cuda":
             W = LO.rule_waves(m.P)
