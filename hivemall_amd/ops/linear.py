@@ -293,9 +293,16 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
         hacc = st.meta.get("hacc")
         if hacc is None or hacc.shape[0] < H:
             hacc = st.meta["hacc"] = torch.zeros((max(H, HOT_MAX), 4), dtype=torch.float32, device=dev)
-    ch = int(os.environ.get("HM_LINEAR_HOT_CH", HOT_CHUNK))
-    hmin = int(os.environ.get("HM_LINEAR_HOT_MIN", HOT_MIN_ROWS))
-    hevery = int(os.environ.get("HM_LINEAR_HOT_EVERY", HOT_EVERY))
+    # rows per wave per chunk: HOT_CHUNK, or fewer so that a short pass still has >= 32 chunk
+    # ends at which the hot features' sums are applied
+    ch = int(os.environ.get("HM_LINEAR_HOT_CH", max(1, min(HOT_CHUNK, n // max(1, W * 32)))))
+    hmin = int(os.environ.get("HM_LINEAR_HOT_MIN", min(HOT_MIN_ROWS, 4 * ch)))
+    # a feature below min_rows per block per chunk is applied every `hevery` chunks: at most
+    # HOT_EVERY, and at least 16 times over the pass — a short pass (200 K rows at 1,024 rows in
+    # flight is 7 chunks) would otherwise hold most hot features' sums until its last chunk,
+    # one huge step at the end (held-out logloss 0.61-0.67 vs the sequential 0.479-0.487)
+    nchunks = -(-n // max(1, W * ch))
+    hevery = int(os.environ.get("HM_LINEAR_HOT_EVERY", max(1, min(HOT_EVERY, nchunks // 16))))
     rc = _native.hip().hm_linear_train_shared(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
                                               st.R, int(st.meta.get("reload", False)),
                                               int(st.meta.get("nt", True)),

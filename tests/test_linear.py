@@ -262,7 +262,7 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
         if dev == "cuda":
             W = LO.rule_waves(m.P)
             assert m.state.meta.get("shared") and m.state.RS.shape[0] == W
-            if W >= 512:
+            if LO.hot_rule(m.P) or LO.hot_owner_rule(m.P):
                 assert m.state.meta["hot"][2] is not None and m.state.meta["hot"][2][1].numel() > 100
         s = m.decision_function(rows=test.to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
