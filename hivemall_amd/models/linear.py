@@ -64,7 +64,7 @@ LEARNER_BASE_OPTS = [
         "after every pass"),
     opt("shared_waves", None, 0, int,
         "[engine] shared engine: rows in flight (0 = auto per rule, ops/linear.py rule_waves: "
-        "1024 AdaGrad / AdaGrad-RDA, 512 AdaGrad-L1 / AdaDelta / RMSprop-Graves, 8 for the other "
+        "1024 AdaGrad / AdaGrad-RDA, 512 AdaGrad-L1 / elastic net, 8 for the other "
         "general-learner rules, whose parity with the sequential learner needs it)"),
 ] + CKPT_OPTS
 

@@ -215,9 +215,10 @@ def hot_owner_rule(P: LinParams) -> bool:
 # profiles/r4/linear_rules_*.jsonl, docs/compat.md "Shared-table engine: per-rule parity"):
 #  * AdaGrad with no / L2 regularisation and AdaGrad-RDA (hot features pre-aggregated as sums):
 #    -6e-4 .. -1.1e-3 at 512 and 1,024 rows in flight -> 1,024 (~98 M rows/s);
-#  * AdaGrad-L1 / elastic net (hot features in owner mode): +1.8e-3 .. +1.9e-3 at 512 -> 512;
-#  * AdaDelta (plain Hogwild): +3.4e-3 .. +4.1e-3 at 512 -> 512 (~94 M rows/s);
-#  * SGD, momentum, Nesterov, RMSprop(-Graves) and the Adam family: +2.5e-3 .. +1e-2 at 16 ..
+#  * AdaGrad-L1 / elastic net (hot features in owner mode): +1.8e-3 .. +1.9e-3 at 512 -> 512
+#    (~94 M rows/s);
+#  * SGD, momentum, Nesterov, RMSprop(-Graves), AdaDelta (+3.4e-3 .. +8e-3 at 512) and the Adam
+#    family: +2.5e-3 .. +1e-2 at 16 ..
 #    1,024 rows in flight (plain Hogwild; their closed-form hot-feature updates diverge), and
 #    within 1.3e-3 at <= 8 (linear_rules_fewwaves.jsonl) -> routed to 8 rows in flight
 #    (~1.7 M rows/s, 3x the CPU engine).  -shared_waves 512 buys ~55x the rate at that gap.
@@ -229,7 +230,7 @@ def rule_waves(P: LinParams) -> int:
     if hot_rule(P):
         return 1024
     general = P.algo == ALGOS["general"]
-    if general and (P.opt == OPTIMIZERS["adadelta"] or hot_owner_rule(P)):
+    if hot_owner_rule(P):
         return 512
     if general:
         return SEQ_WAVES

@@ -244,8 +244,8 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
     learner at a step size where the sequential learner converges: auto picks the shared table
     with the rule's rows in flight (ops/linear.py rule_waves) — 1,024 with the hot features'
     gradients summed per block (AdaGrad, AdaGrad-RDA), 512 with the hot features in owner mode
-    (AdaGrad-L1 / elastic net, AdaDelta, RMSprop-Graves), and 8 for SGD, momentum, Nesterov,
-    RMSprop and the Adam family, whose Hogwild gap at 16+ rows in flight is +2.5e-3 .. +1e-2
+    (AdaGrad-L1 / elastic net), and 8 for SGD, momentum, Nesterov, RMSprop(-Graves), AdaDelta and
+    the Adam family, whose Hogwild gap at 16+ rows in flight is +2.5e-3 .. +1e-2
     (profiles/r4/linear_rules_*.jsonl).  Held-out logloss after one epoch within 5e-3 of the
     sequential CPU engine."""
     from hivemall_amd.ops import linear as LO
