@@ -1175,255 +1175,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 }
 
 // ---------------------------------------------------------------------------------------------
-// Paired-slot variant of ffm_pipe_sg32_kernel (A/B: HM_FFM_VARIANT=9).  A thread owns whole
-// interaction pairs — slots (a, b) and (b, a), each the other's partner — so the partner V comes
-// from the thread's own registers, not from a transposed LDS image: 24.6 KB less LDS per block
-// (4 blocks = rows in flight per CU instead of 2) and no LDS transpose traffic.  Units: the
-// F (F - 1) / 2 pairs, then the F diagonal slots two per unit (zero step, written back
-// unchanged); unit u = tid + k * TPB holds slots j = 2k, 2k + 1.
-// LDS-DMA pipelined kernel for per-slot AdaGrad with fp32 V in the block layout
-// ([V: FS x 16 B | G: FS x fp32 | zero tail] per feature, 896 B): the schedule of
-// ffm_pipe_kernel (A..F above) with two DMAs per slot (V 16 B, G 4 B) into separate landing
-// zones.  A register-prefetch variant of this layout reached 66-68 M rows/s (70 % of the
-// access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
-// removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
-// block -> 2 blocks/CU).
-template <int NS, typename OT, int TPB = 256>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg32p_kernel(
-    FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
-    const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
-    float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
-    float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
-{
-    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB];    // V DMA landing zone
-    __shared__ __attribute__((aligned(16))) float s_rg[NS * TPB];     // G DMA landing zone
-    __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
-    __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
-    __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
-    __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
-    const int F = P.F;
-    const int FF = F * F;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
-    const OT vfs = (OT)P.fstride * 16u;                  // V bytes between features
-    const OT gfs = (OT)P.gstride * 4u;                   // G bytes between features
-    const int G = gridDim.x;
-    char* vb = reinterpret_cast<char*>(Vt);
-    char* gb = reinterpret_cast<char*>(Gt);
-
-    constexpr int DEAD = 0xFFFF;
-    int ab[NS];
-    {
-        const int NPAIR = F * (F - 1) / 2;
-#pragma unroll
-        for (int k = 0; k < NS / 2; ++k) {
-            const int u = tid + k * TPB;
-            if (u < NPAIR) {
-                int p = u, a = 0;
-                while (p >= F - 1 - a) { p -= F - 1 - a; ++a; }
-                const int b = a + 1 + p;
-                ab[2 * k] = a | (b << 8);
-                ab[2 * k + 1] = b | (a << 8);
-            } else {
-                const int d0 = 2 * (u - NPAIR), d1 = d0 + 1;
-                ab[2 * k] = d0 < F ? d0 | (d0 << 8) : DEAD;
-                ab[2 * k + 1] = d1 < F ? d1 | (d1 << 8) : DEAD;
-            }
-        }
-    }
-    (void)FF;
-#define SA(j) (ab[j] & 0xFF)
-#define SB(j) (ab[j] >> 8)
-
-    auto dma_meta = [&](int bf, int row) {
-        if (wave == W_DMA && lane < F && row < P.B) {
-            const size_t o = (size_t)row * F + lane;
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(idx + o), (lds_ptr_t)&s_mr[bf][0][0], 4, 0, 0);
-            if (fld) __builtin_amdgcn_global_load_lds((glb_ptr_t)(fld + o), (lds_ptr_t)&s_mr[bf][1][0], 4, 0, 0);
-            if (val) __builtin_amdgcn_global_load_lds((glb_ptr_t)(val + o), (lds_ptr_t)&s_mr[bf][2][0], 4, 0, 0);
-        }
-    };
-    auto publish_meta = [&](int bf) {
-        if (wave == W_META) {
-            float sq = 0.f;
-            if (lane < F) {
-                int ri = s_mr[bf][0][lane];
-                int rf = fld ? s_mr[bf][1][lane] : lane;
-                float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
-                if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
-                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
-                sq = rx * rx;
-            }
-            const float tot = hm::wave_sum_uniform(sq);
-            if (lane == 0) s_red[TPB / 64 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
-        }
-    };
-    // slot j of the row in s_m[bf]: V / G byte offsets, x_a x_b; 1 = live, 2 = diagonal, 0 = dead
-    auto slot = [&](int bf, int j, OT& ov, OT& og, float& xab) -> uint32_t {
-        const bool inr = ab[j] != DEAD;
-        const int4 ma = s_m[bf][inr ? SA(j) : 0], mb = s_m[bf][inr ? SB(j) : 0];
-        const bool ok = (ma.x | mb.x) >= 0 && inr;
-        const bool live = ok && SA(j) != SB(j);
-        const OT i = ok ? (OT)(uint32_t)ma.x : (OT)0, f = ok ? (OT)(uint32_t)mb.y : (OT)0;
-        ov = i * vfs + f * 16u;
-        og = i * gfs + f * 4u;
-        xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
-        return live ? 1u : (ok ? 2u : 0u);
-    };
-    auto dma_slots = [&](int bf) {
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            OT ov, og;
-            float xab;
-            slot(bf, j, ov, og, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
-        }
-    };
-    auto dma_lin = [&](int bf) {
-        if (P.use_linear && wave == W_LIN && lane < F) {
-            const int i = s_m[bf][lane].x;
-            if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
-                if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
-                }
-            }
-        }
-    };
-
-    int row = blockIdx.x;
-    if (row >= P.B) return;
-    dma_meta(0, row);
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    bar_raw();
-    publish_meta(0);
-    bar_raw();
-    dma_slots(0);
-    dma_lin(0);
-    dma_meta(1, row + G);
-
-    for (int cur = 0; row < P.B; row += G, cur ^= 1) {
-        const int nxt = cur ^ 1;
-        const bool more = row + G < P.B;
-        // ---- A: this wave's DMAs have landed, then every wave's ----
-        __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
-        bar_raw();
-        // ---- B: landing zones -> registers (V and G of the thread's pairs); meta(row + G) ----
-        float cg[NS];
-        float4 own[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            cg[j] = s_rg[j * TPB + tid];
-            own[j] = s_rv[j * TPB + tid];
-        }
-        if (more) publish_meta(nxt);
-        bar_raw();
-        // ---- C: next row's slot DMA (the landing zones are free: read in B), its meta after ----
-        if (more) {
-            dma_slots(nxt);
-            dma_meta(cur, row + 2 * G);
-        }
-        const float scale = s_red[TPB / 64 + cur];
-        int mi = -1;
-        float mx = 0.f, lw = 0.f;
-        if (wave == W_LIN && lane < F) {
-            const int4 m = s_m[cur][lane];
-            mi = m.x;
-            mx = __int_as_float(m.z);
-            lw = s_lin[cur][0][lane];
-        }
-        // ---- D: forward ----
-        uint32_t live = 0u, wr = 0u;
-        float xab[NS];
-        float part = 0.f;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            OT ov, og;
-            const uint32_t k = slot(cur, j, ov, og, xab[j]);
-            live |= (k & 1u) << j;
-            wr |= (uint32_t)(k != 0u) << j;
-            const float4 pv = own[j ^ 1];            // the pair's other slot (diagonal: xab 0)
-            const float4 cv = own[j];
-            part += (cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w) * xab[j];
-        }
-        part *= 0.5f * scale * scale;
-        part += lw * mx * scale;
-        part = hm::wave_sum_uniform(part);
-        if (lane == 0) s_red[wave] = part;
-        bar_raw();
-        float p = 0.f;
-#pragma unroll
-        for (int q = 0; q < TPB / 64; ++q) p += s_red[q];
-        if (P.use_bias) p += bias_w0(P, bias);
-        const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
-
-        // ---- E: updates ----
-        if (P.train) {
-            const float ks = kappa * scale * scale;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                if (!(wr >> j & 1u)) continue;
-                OT ov, og;
-                float xj;
-                slot(cur, j, ov, og, xj);
-                const float4 pv = own[j ^ 1];        // pre-update: own[] is never written
-                const float4 cv = own[j];
-                const float c = ks * xab[j];
-                const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
-                const f2 cc = {c, c}, ll = {lj, lj};
-                f2 o0 = f2{cv.x, cv.y}, o1 = f2{cv.z, cv.w};
-                const f2 p0 = f2{pv.x, pv.y}, p1 = f2{pv.z, pv.w};
-                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
-                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
-                const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
-                const f2 rr = {r, r};
-                o0 = o0 + rr * d0;
-                o1 = o1 + rr * d1;
-                *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
-                *reinterpret_cast<float*>(gb + og) = gs;
-            }
-            // the row's features' pad slots and block tails (never read): zeros, so every line a
-            // row touches is written whole; spread over all threads (one wave doing them all
-            // was the last to reach the barrier)
-            {
-                const int npad = P.vpad - P.num_fields;
-                const int per = 2 * npad + P.tail16;
-                for (int q = tid; q < F * per; q += TPB) {
-                    const int a = q / per, kk = q - a * per;
-                    const int i = s_m[cur][a].x;
-                    if (i < 0) continue;
-                    char* vblk = vb + (OT)(uint32_t)i * vfs;
-                    char* gblk = gb + (OT)(uint32_t)i * gfs;
-                    if (kk < npad) *reinterpret_cast<uint4*>(vblk + (P.num_fields + kk) * 16) = make_uint4(0u, 0u, 0u, 0u);
-                    else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
-                    else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
-                }
-            }
-            if (mi >= 0) {
-                if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                    const float lz = s_lin[cur][1][lane];
-                    const float ln = s_lin[cur][2][lane];
-                    const float g = kappa * mx * scale;
-                    const float n1 = ln + g * g;
-                    const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[mi] = z1;
-                    wn[mi] = n1;
-                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
-                }
-            }
-            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
-        }
-        // ---- F: linear state of the next row (after this row's FTRL stores) ----
-        if (more) dma_lin(nxt);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
-#undef SA
-#undef SB
-}
-
-// ---------------------------------------------------------------------------------------------
 // LDS-DMA pipelined kernel for per-slot AdaGrad with bf16 V in 12-B slots {V bf16 x 4 | G fp32}:
 // 40 slots per feature = 480 B + a 32-B zero tail = one 512-B block (4 lines; the 16-B
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
@@ -1733,19 +1484,6 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
-    if (variant == 9 && !wide) {
-        // paired slots (ffm_pipe_sg32p_kernel): units = pairs + diagonal pairs, 2 slots each
-        const int units = P.F * (P.F - 1) / 2 + (P.F + 1) / 2;
-        const int nsp = 2 * ((units + 255) / 256);
-#define HM_P32P(NSV) hipLaunchKernelGGL((ffm_pipe_sg32p_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
-                                        P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (nsp <= 2) { HM_P32P(2); }
-        else if (nsp <= 4) { HM_P32P(4); }
-        else if (nsp <= 6) { HM_P32P(6); }
-        else { HM_P32P(8); }
-#undef HM_P32P
-        HM_LAUNCH_RET();
-    }
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }
@@ -1832,8 +1570,13 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             separate [.][.][Kp] tables.
 // variant (A/B): 0 = auto (per-slot: the sg12 / sg32 pipelines; per-element bf16:
 // ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel
-// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).  (512-thread sg32 blocks measured
-// 75.7-76.1 vs 75.6 M rows/s, profiles/r4/ffm_512_thread_ab.log: removed.)
+// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).  Measured and removed: 512-thread sg32
+// blocks (75.7-76.1 vs 75.6 M rows/s, profiles/r4/ffm_512_thread_ab.log); a paired-slot sg32
+// kernel holding each (a, b) / (b, a) slot pair in one thread's registers instead of a transposed
+// LDS image (4 rows in flight per CU instead of 2): 58.1-58.4 vs 74.9-75.5 M rows/s — the (b, a)
+// halves of a wave's pairs are V[i_b][f_a] for 64 different features, 16-B loads from 64
+// feature blocks where the row-major order reads whole runs of one block
+// (profiles/r4/ffm_paired_slots_ab.log).
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
