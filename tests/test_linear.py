@@ -247,8 +247,8 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
     (AdaGrad-L1 / elastic net), and 8 for SGD, momentum, Nesterov, RMSprop(-Graves), AdaDelta and
     the Adam family, whose Hogwild gap at 16+ rows in flight is +2.5e-3 .. +1e-2
     (profiles/r4/linear_rules_*.jsonl).  Held-out logloss after one epoch over 1 M rows within
-    5e-3 of the sequential CPU engine (over the first 200 K rows the 8-row routing is +2e-3 ..
-    +4e-3 ahead of convergence, profiles/r4/linear_rules_fewwaves_200k.jsonl)."""
+    5e-3 of the sequential CPU engine (over only the first 200 K rows the 8-row routing sits +2e-3 ..
+    +4e-3 above it, profiles/r4/linear_rules_fewwaves_200k.jsonl)."""
     from hivemall_amd.ops import linear as LO
 
     rows = _criteo_rows(1000000, 24, seed=5)
