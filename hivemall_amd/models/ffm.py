@@ -23,6 +23,7 @@ keyed as in :mod:`models.ffm_keys`: ``i = -1`` bias, ``i = feature`` linear weig
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -70,6 +71,10 @@ def csr_to_ffm_batch(csr: CSR, y: np.ndarray | None, width: int | None = None) -
 # N = 8, fp32, vs one rank on the same total rows (benchmarks/dp_sim.py, profiles/r4/): p = 0
 # (plain mean) +5.3e-3, 0.5 +1.5e-3, 0.75 +2.8e-4, 1.0 -6e-4.
 DP_LR_POWER = 0.75
+
+# early-training concurrency ramp of the GPU kernel (train_batch)
+RAMP_ROWS = int(os.environ.get("HM_FFM_RAMP_ROWS", "0"))
+RAMP_GRID = int(os.environ.get("HM_FFM_RAMP_GRID", "1024"))
 
 
 def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
@@ -224,8 +229,12 @@ class FFMTrainer(Learner):
             sub = b.slice(s, min(b.n, s + bs))
             lb = None if loss_buf is None else loss_buf[s:s + sub.n]
             if sub.n:
+                # the first RAMP_ROWS rows of a learner run on RAMP_GRID blocks (fewer rows in
+                # flight) unless -grid is given: early in training every row moves the same
+                # few parameters and concurrent stale reads cost the most
+                grid = self.grid or (RAMP_GRID if self.rows_seen < RAMP_ROWS else 0)
                 ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True,
-                         loss=lb, grid=self.grid)
+                         loss=lb, grid=grid)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:
