@@ -1054,6 +1054,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     dma_lin(0);
     dma_meta(1, row + G);
 
+    // Forwarding of the block's own updates into its next row: the next row's slots are DMA'd
+    // (phase C) before this row's updates land (phase E), so a slot both rows hold — the same
+    // (feature, field), hence the same slot index and thread when the rows share a feature at one
+    // position — would be read one update stale.  The updating thread keeps the new V / G and
+    // their offset, and phase B of the next row takes them instead of the landing zone.
+    float4 fv[NS];
+    float fg[NS];
+    OT fo[NS];
+    uint32_t fwd = 0u;
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
@@ -1065,8 +1074,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             cg[j] = s_rg[j * TPB + tid];
-            if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = s_rv[j * TPB + tid];
+            float4 v = s_rv[j * TPB + tid];
+            if (fwd >> j & 1u) {
+                OT ov, og;
+                float xq;
+                if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) { v = fv[j]; cg[j] = fg[j]; }
+            }
+            if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = v;
         }
+        fwd = 0u;
         if (more) publish_meta(nxt);
         bar_raw();
         // ---- C: next row's slot DMA (the landing zones are free: read in B), its meta after ----
@@ -1132,7 +1148,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
-                *reinterpret_cast<float4*>(vb + ov) = make_float4(o0.x, o0.y, o1.x, o1.y);
+                fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
+                fg[j] = gs;
+                fo[j] = ov;
+                fwd |= 1u << j;
+                *reinterpret_cast<float4*>(vb + ov) = fv[j];
                 *reinterpret_cast<float*>(gb + og) = gs;
             }
             // the row's features' pad slots and block tails (never read): zeros, so every line a

@@ -485,7 +485,7 @@ class HistTreeBuilder:
 
     def build(self, stats: torch.Tensor, active: torch.Tensor | None = None, smax: torch.Tensor | None = None,
               act_rows: torch.Tensor | None = None, identity_rows: bool = False,
-              leaf_h: torch.Tensor | None = None) -> Tree:
+              leaf_h: torch.Tensor | None = None, defer: bool = False):
         """Grow one tree level by level.  stats: f32 [n, NS] per-row statistics.
 
         Every level: split search on the device over the level's histograms; one host sync
@@ -496,7 +496,10 @@ class HistTreeBuilder:
         passed in when the caller already has them (the fused GBT statistics kernel);
         ``identity_rows``: act_rows is 0 .. n-1 (every row active, no ``active`` mask).
         ``leaf_h`` (criterion gbt2, stats = (r, w)): per-row hessians; the leaves get the Newton
-        values sum r / sum h over their rows (csrc hm_leaf_sums / hm_leaf_newton)."""
+        values sum r / sum h over their rows (csrc hm_leaf_sums / hm_leaf_newton).
+        ``defer`` (level-fused builder): return a :class:`PendingTree` whose node arrays stay on
+        the device (no host read at the end of the tree, importance left in ``imp_dev``) — the
+        boosting loops materialise all trees after the last one."""
         q = self.q
         dev = stats.device
         n, NS = stats.shape
@@ -658,7 +661,11 @@ class HistTreeBuilder:
             H = Hn
             base, L = nb, 2 * n_split
             depth += 1
-        self.importance = self.importance + imp.cpu().numpy()
+        defer = defer and fused
+        if defer:
+            self.imp_dev = imp
+        else:
+            self.importance = self.importance + imp.cpu().numpy()
         self.leaf_of_row = node_of_row
         if fused and leaf_h is not None:
             t = base + L
@@ -677,9 +684,11 @@ class HistTreeBuilder:
             _native.check(_native.hip().hm_leaf_newton(p(sums), p(nbuf.sf), t, p(nbuf.vals), st_), "hm_leaf_newton")
         if fused:
             t = base + L                                   # nodes written, ids 0 .. t - 1
+            self.node_values = nbuf.vals[:t]
+            if defer:
+                return PendingTree(nbuf.sf[:t], nbuf.thr[:t], nbuf.lc[:t], nbuf.rc[:t], nbuf.vals[:t], n_out)
             F, Lc, Rc = torch.stack([nbuf.sf[:t], nbuf.lc[:t], nbuf.rc[:t]]).cpu().numpy()
             T = nbuf.thr[:t].cpu().numpy()
-            self.node_values = nbuf.vals[:t]
             V = self.node_values.double().cpu().numpy()
         else:
             F = torch.cat(feats).cpu().numpy()
@@ -688,17 +697,42 @@ class HistTreeBuilder:
             Rc = torch.cat(rights).cpu().numpy()
             V = torch.cat(vals).double().cpu().numpy()
             self.node_values = torch.cat(vals)
-        tree = Tree(n_out=n_out)
-        cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
-        tree.cat = cflag if any(cflag) else []
-        dflag = [1 if (f >= 0 and int(f) & DLEFT_FLAG) else 0 for f in F]
-        tree.dleft = dflag if any(dflag) else []
-        tree.feature = [int(f) & ~(CAT_FLAG | DLEFT_FLAG) if f >= 0 else int(f) for f in F]
-        tree.threshold = [float(t) for t in T]
-        tree.left = [int(x) for x in Lc]
-        tree.right = [int(x) for x in Rc]
-        tree.value = [None if F[k] >= 0 else V[k].tolist() for k in range(len(F))]
-        return tree
+        return _tree_from_arrays(F, T, Lc, Rc, V, n_out)
+
+
+def _tree_from_arrays(F, T, Lc, Rc, V, n_out: int) -> Tree:
+    tree = Tree(n_out=n_out)
+    cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
+    tree.cat = cflag if any(cflag) else []
+    dflag = [1 if (f >= 0 and int(f) & DLEFT_FLAG) else 0 for f in F]
+    tree.dleft = dflag if any(dflag) else []
+    tree.feature = [int(f) & ~(CAT_FLAG | DLEFT_FLAG) if f >= 0 else int(f) for f in F]
+    tree.threshold = [float(t) for t in T]
+    tree.left = [int(x) for x in Lc]
+    tree.right = [int(x) for x in Rc]
+    tree.value = [None if F[k] >= 0 else V[k].tolist() for k in range(len(F))]
+    return tree
+
+
+class PendingTree:
+    """A grown tree whose node arrays are still on the device (HistTreeBuilder.build(defer=True)):
+    the boosting loop keeps the GPU busy with the next tree instead of waiting on five host reads
+    and the Python node lists per tree; :meth:`materialize` builds the :class:`Tree`."""
+
+    def __init__(self, sf, thr, lc, rc, vals, n_out: int):
+        self.arrays = (sf, thr, lc, rc, vals)
+        self.n_out = n_out
+        self.scale = 1.0          # leaf values x scale (XGBoost's eta)
+
+    def materialize(self) -> Tree:
+        sf, thr, lc, rc, vals = self.arrays
+        F, Lc, Rc = torch.stack([sf, lc, rc]).cpu().numpy()
+        return _tree_from_arrays(F, thr.cpu().numpy(), Lc, Rc, vals.double().cpu().numpy() * self.scale, self.n_out)
+
+
+def materialize_trees(iters: list) -> list:
+    """Boosting rounds with any PendingTree replaced by its Tree."""
+    return [[t.materialize() if isinstance(t, PendingTree) else t for t in it] for it in iters]
 
 
 # ------------------------------------------------------------------ learners
@@ -980,6 +1014,7 @@ class GradientTreeBoostingClassifier(Learner):
             smax = torch.zeros(ns, dtype=torch.float32, device=self.device)
             all_rows = torch.arange(n, dtype=torch.int32, device=self.device)
             st = _native.stream_of(self.device)
+        imp_dev = None
         for it in range(int(c["trees"])):
             if fused:
                 mask = None
@@ -1000,8 +1035,11 @@ class GradientTreeBoostingClassifier(Learner):
                                     c["min_samples_leaf"], c["mtry"], c["max_leaf_nodes"],
                                     seed=self.seed * 7919 + it * K, mixer=self.mixer, lam=float(c["lambda"]))
                 tree = b.build(stats_buf, smax=smax, act_rows=all_rows if mask is None else None,
-                               identity_rows=mask is None, leaf_h=hh)
-                self.importance += b.importance
+                               identity_rows=mask is None, leaf_h=hh, defer=True)
+                if isinstance(tree, PendingTree):
+                    imp_dev = b.imp_dev if imp_dev is None else imp_dev + b.imp_dev
+                else:
+                    self.importance += b.importance
                 vals = b.node_values.float().contiguous()
                 _native.check(_native.hip().hm_gbt_apply(
                     _native.ptr(F), F.shape[1], 0, _native.ptr(vals), vals.shape[1], _native.ptr(b.leaf_of_row),
@@ -1044,6 +1082,9 @@ class GradientTreeBoostingClassifier(Learner):
                 self.oob_rates.append(float((pred != yi[oob]).float().mean().item()))
             else:
                 self.oob_rates.append(0.0)
+        self.iters = materialize_trees(self.iters)
+        if imp_dev is not None:
+            self.importance += imp_dev.cpu().numpy()
         return self
 
     def decision_function(self, features) -> np.ndarray:

@@ -35,7 +35,8 @@ from ..registry import udtf
 from ..utils import base91
 from ..utils.options import UDFArgumentException, opt
 from .base import Learner
-from .trees import HistTreeBuilder, Tree, _encode_classes_dp, _to_dense, predict_forest, quantize
+from .trees import (HistTreeBuilder, PendingTree, Tree, _encode_classes_dp, _to_dense, materialize_trees,
+                    predict_forest, quantize)
 
 XGB_OPTS = [
     opt("objective", None, "binary:logistic", str,
@@ -148,6 +149,7 @@ class XGBoostTrainer(Learner):
             stats_buf = torch.empty((n, 2), dtype=torch.float32, device=dev)
             smax = torch.zeros(2, dtype=torch.float32, device=dev)
             all_rows = torch.arange(n, dtype=torch.int32, device=dev)
+        imp_dev = None
         for it in range(int(c["num_round"])):
             if fused:
                 mask = None
@@ -180,10 +182,13 @@ class XGBoostTrainer(Learner):
                                     min_gain=2.0 * float(c["gamma"]), feature_mask=fmask)
                 if fused:
                     tree = b.build(stats, smax=smax, act_rows=all_rows if mask is None else None,
-                                   identity_rows=mask is None)
+                                   identity_rows=mask is None, defer=True)
                 else:
                     tree = b.build(stats)
-                tree.value = [None if v is None else [eta * v[0]] for v in tree.value]
+                if isinstance(tree, PendingTree):       # node arrays still on the device
+                    tree.scale = eta
+                else:
+                    tree.value = [None if v is None else [eta * v[0]] for v in tree.value]
                 if F.is_cuda:   # fused leaf update (trees.hip gbt_apply_kernel)
                     vals = b.node_values.float().contiguous()
                     _native.check(_native.hip().hm_gbt_apply(
@@ -191,9 +196,15 @@ class XGBoostTrainer(Learner):
                         C.c_int64(n), C.c_float(eta), _native.stream_of(F.device)), "hm_gbt_apply")
                 else:
                     F[:, k] += eta * b.node_values[b.leaf_of_row.long(), 0]
-                self.importance += b.importance
+                if isinstance(tree, PendingTree):
+                    imp_dev = b.imp_dev if imp_dev is None else imp_dev + b.imp_dev
+                else:
+                    self.importance += b.importance
                 round_trees.append(tree)
             self.trees.append(round_trees)
+        self.trees = materialize_trees(self.trees)
+        if imp_dev is not None:
+            self.importance += imp_dev.cpu().numpy()
         return self
 
     # -- inference
