@@ -212,10 +212,11 @@ def test_ffm_gpu_bf16_state_close_to_fp32_engine(layout, adagrad):
 @pytest.mark.gpu
 @pytest.mark.parametrize("adagrad", ["", "-elementwise_adagrad"])
 def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
-    """grid=1: one workgroup walks the rows in order = Hivemall's per-row semantics (the
-    generic kernel, variant 1, has no lookahead); the pipelined default reads row r+1's slots
-    before row r's updates land, one row of staleness: within 3e-3 of the sequential order
-    (measured 2.05e-3 per-slot, 1.4e-3 per-element)."""
+    """grid=1: one workgroup walks the rows in order = Hivemall's per-row semantics.  The generic
+    kernel (variant 1) has no lookahead; the pipelined default DMAs row r+1's slots before row
+    r's updates land, and forwards its own updates into the slots both rows hold (ffm.hip
+    ffm_pipe_sg32_kernel): measured 4.2e-5 / 3.2e-5 from the sequential engine (2.05e-3 before
+    the forwarding, profiles/r4/ffm_single_block_forwarding.log)."""
     from hivemall_amd.ops import ffm as ffm_op
 
     idx, y = criteo_like(20000, hash_bits=16, seed=5)
@@ -235,7 +236,7 @@ def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
     finally:
         ffm_op._VARIANT = old
     assert abs(res[("cpu", 0)] - res[("cuda", 1)]) < 1e-4, res
-    assert abs(res[("cpu", 0)] - res[("cuda", 0)]) < 3e-3, res
+    assert abs(res[("cpu", 0)] - res[("cuda", 0)]) < 3e-4, res
 
 
 @pytest.mark.gpu
