@@ -960,6 +960,35 @@ __global__ __launch_bounds__(256) void hist_sibling_kernel(const float* __restri
         dbig[e] = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
     }
 }
+// Heap-layout next level: parent l's children are 2l, 2l+1 of Hn; split parents get Hs[l] (the
+// smaller child's histogram) and H[l] - Hs[l], the children slots of parents that did not split
+// get zeros (their nodes exist in the fixed-shape level but hold no rows: no split is found).
+__global__ __launch_bounds__(256) void hist_sibling_heap_kernel(const float* __restrict__ H,
+                                                                const float* __restrict__ Hs,
+                                                                const int32_t* __restrict__ split_feat,
+                                                                const uint8_t* __restrict__ small_right,
+                                                                int64_t per, int L, float* __restrict__ Hn) {
+    const int l = blockIdx.y;
+    if (l >= L) return;
+    const bool split = split_feat[l] >= 0;
+    const float4* hp = reinterpret_cast<const float4*>(H + (size_t)l * per);
+    const float4* hs = reinterpret_cast<const float4*>(Hs + (size_t)l * per);
+    const int sr = small_right[l] ? 1 : 0;
+    float4* dsmall = reinterpret_cast<float4*>(Hn + (size_t)(2 * l + sr) * per);
+    float4* dbig = reinterpret_cast<float4*>(Hn + (size_t)(2 * l + 1 - sr) * per);
+    const int64_t n4 = per / 4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+        if (split) {
+            const float4 a = hp[e], b = hs[e];
+            dsmall[e] = b;
+            dbig[e] = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+        } else {
+            dsmall[e] = z;
+            dbig[e] = z;
+        }
+    }
+}
 }  // namespace
 
 // hist [n_seg, d, B, NS] (zeroed by the caller) += statistics of rows[seg[k]..seg[k+1]) for
@@ -1164,6 +1193,18 @@ HM_API int hm_hist_sibling(const float* H, const float* Hs, const int64_t* li, c
     HM_LAUNCH_RET();
 }
 
+// Heap-layout sibling histograms (hist_sibling_heap_kernel): H, Hs [L, per], Hn [2L, per].
+HM_API int hm_hist_sibling_heap(const float* H, const float* Hs, const int32_t* split_feat, const uint8_t* small_right,
+                                int64_t per, int L, float* Hn, hipStream_t stream) {
+    if (L <= 0) return 0;
+    if (per % 4) return (int)hipErrorInvalidValue;
+    int64_t bx = (per / 4 + 255) / 256;
+    if (bx > 64) bx = 64;
+    hipLaunchKernelGGL(hist_sibling_heap_kernel, dim3((unsigned)bx, (unsigned)L), dim3(256), 0, stream, H, Hs,
+                       split_feat, small_right, per, L, Hn);
+    HM_LAUNCH_RET();
+}
+
 // Fused binary-logistic GBT statistics (see gbt_stats_kernel): F, y [n] fp32, mask [n] uint8
 // or NULL; stats [n, 3] fp32 out; smax [3] zeroed by the caller.
 HM_API int hm_gbt_stats(const float* F, const float* y, const uint8_t* mask, int64_t n, float* stats,
@@ -1239,6 +1280,7 @@ HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, co
 // cumsum-based host path does.
 struct LevelParams {
     int L, NS, d, E, crit, n_out, nb, has_cat;
+    int heap;   // children at nb + 2l, nb + 2l + 1 for parent l (fixed-shape levels, no host read)
     float lam, alpha, min_gain, min_split;
 };
 
@@ -1305,6 +1347,11 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
             thrs_out[l] = INFINITY;
             lc_out[l] = -1;
             rc_out[l] = -1;
+            if (P.heap) {
+                small_right[l] = 0;
+                lut[2 * l] = (int16_t)32767;
+                lut[2 * l + 1] = (int16_t)32767;
+            }
             continue;
         }
         const bool fok = bf >= 0 && bf < P.d;
@@ -1313,7 +1360,7 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
         if ((br >> 16) & 1) flag |= HM_TREE_DLEFT;
         feats_out[l] = flag;
         thrs_out[l] = (fok && bb < P.E) ? edges[(size_t)bf * P.E + bb] : INFINITY;
-        const int lc = P.nb + 2 * rank;
+        const int lc = P.nb + 2 * (P.heap ? l : rank);
         lc_out[l] = lc;
         rc_out[l] = lc + 1;
         li_out[rank] = l;
@@ -1330,9 +1377,10 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
             for (int s = 0; s < P.NS; ++s) { wl += Lf[s]; wr += S[s] - Lf[s]; }
         }
         const int sr = wr < wl ? 1 : 0;
-        small_right[rank] = (uint8_t)sr;
-        lut[2 * rank + sr] = (int16_t)rank;
-        lut[2 * rank + 1 - sr] = (int16_t)32767;
+        const int key = P.heap ? l : rank;     // heap: segments / histograms indexed by parent
+        small_right[key] = (uint8_t)sr;
+        lut[2 * key + sr] = (int16_t)key;
+        lut[2 * key + 1 - sr] = (int16_t)32767;
         ++rank;
     }
 }
@@ -1348,6 +1396,7 @@ HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* ga
     LevelParams P;
     P.L = ip[0]; P.NS = ip[1]; P.d = ip[2]; P.E = ip[3]; P.crit = ip[4]; P.n_out = ip[5]; P.nb = ip[6];
     P.has_cat = ip[7];
+    P.heap = ip[8];
     P.lam = fp[0]; P.alpha = fp[1]; P.min_gain = fp[2]; P.min_split = fp[3];
     if (P.L <= 0 || P.NS <= 0 || (P.crit > 1 && P.NS > 8) || P.E <= 0) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream, P, gain, feat, bins_raw, left, tot,

@@ -41,6 +41,8 @@ HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/his
 HIST_WIDE = os.environ.get("HM_HIST_WIDE", "1") == "1"   # all-features single-pass histogram
 ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-child count in one pass
 GBT2 = os.environ.get("HM_GBT2", "1") == "1"    # GBT histograms of (r, w), Newton leaves summed per leaf
+HEAP_TREES = os.environ.get("HM_TREE_HEAP", "1") == "1"   # fixed-shape levels, no per-level host read
+HEAP_MAX_DEPTH = 10
 HIST_WIDE_BLOCKS = int(os.environ.get("HM_HIST_WIDE_BLOCKS", "256"))
 
 
@@ -384,10 +386,13 @@ class HistTreeBuilder:
                 raise RuntimeError("hm_split_find_cpu: invalid arguments")
         return gain, feat, bins, left, tot
 
-    def _level_finalize(self, gain, feat, braw, left, tot, base: int, nb: int, edges, buf: "_NodeBuf", imp):
+    def _level_finalize(self, gain, feat, braw, left, tot, base: int, nb: int, edges, buf: "_NodeBuf", imp,
+                        heap: bool = False):
         """GPU: the level's split decisions and bookkeeping in one kernel (hm_level_finalize),
         written straight into the tree's node arrays at [base, base + L); returns
-        (li int64, small_right, lut, n_split) of the splitting nodes."""
+        (li int64, small_right, lut, n_split) of the splitting nodes.  ``heap``: the children of
+        parent l are nodes nb + 2l, nb + 2l + 1 and small_right / lut are indexed by l; returns
+        (small_right [L], lut [2L]) without reading the split count on the host."""
         L, NS = tot.shape
         dev = tot.device
         buf.ensure(base + L)
@@ -397,7 +402,7 @@ class HistTreeBuilder:
         nsp = torch.empty(1, dtype=torch.int32, device=dev)
         cat = self._masks[1]
         ip = np.array([L, NS, self.q.d, edges.shape[1], self._CRIT[self.criterion], buf.n_out, nb,
-                       int(cat is not None)], dtype=np.int32)
+                       int(cat is not None), int(heap)], dtype=np.int32)
         fp = np.array([self.lam, self.alpha, self.min_gain, float(self.min_split)], dtype=np.float32)
         p = _native.ptr
         o4, ov = 4 * base, 4 * base * buf.n_out          # byte offsets of node `base`
@@ -406,6 +411,8 @@ class HistTreeBuilder:
             p(edges), p(cat), p(buf.vals) + ov, p(buf.sf) + o4, p(buf.thr) + o4, p(buf.lc) + o4,
             p(buf.rc) + o4, p(buf.sb) + o4, p(li), p(sr), p(lut), p(nsp), p(imp),
             _native.stream_of(dev)), "hm_level_finalize")
+        if heap:
+            return sr, lut
         n_split = int(nsp.item())                                            # the level's one sync
         return li[:n_split], sr[:n_split], lut[:2 * n_split], n_split
 
@@ -506,6 +513,11 @@ class HistTreeBuilder:
         d, B = q.d, q.B
         stats = stats.contiguous()
         identity_rows = bool(identity_rows and active is None and act_rows is not None and act_rows.numel() == n)
+        # heap layout (no host read per level): shallow trees without per-node feature draws,
+        # whose node ids (the draw's key) would differ from the compact numbering
+        heap = (HEAP_TREES and dev.type == "cuda" and self.max_leaves is None
+                and self.max_depth <= HEAP_MAX_DEPTH and not (self.mtry is not None and self.mtry < d)
+                and (NS <= 8 or self.criterion in ("gini", "entropy")))
         node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
         if active is not None:
             node_of_row[~active] = -1
@@ -555,6 +567,29 @@ class HistTreeBuilder:
                 lefts.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 rights.append(torch.full((L,), -1, dtype=torch.int32, device=dev))
                 break
+            if fused and heap:
+                # fixed-shape level (L = 2^depth node slots, heap numbering): nothing is read on
+                # the host, the next level's kernels queue behind this one's
+                gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
+                nb = base + L
+                sr, lut = self._level_finalize(gain, bf, braw, left_all, tot, base, nb, edges, nbuf, imp, heap=True)
+                p = _native.ptr
+                if identity_rows and ROUTE_FUSED:
+                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, L)
+                else:
+                    _native.check(_native.hip().hm_route_rows(
+                        p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc),
+                        p(nbuf.rc), (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
+                    rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, L)
+                Hs = self._hist(rows, seg.contiguous(), L, stats, smax)
+                Hn = torch.empty((2 * L, d, B, NS), dtype=torch.float32, device=dev)
+                _native.check(_native.hip().hm_hist_sibling_heap(
+                    p(H), p(Hs), p(nbuf.sf) + 4 * base, p(sr), C.c_int64(d * B * NS), L, p(Hn),
+                    _native.stream_of(dev)), "hm_hist_sibling_heap")
+                H = Hn
+                base, L = nb, 2 * L
+                depth += 1
+                continue
             if fused:
                 gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
                 nb = base + L
@@ -701,6 +736,23 @@ class HistTreeBuilder:
 
 
 def _tree_from_arrays(F, T, Lc, Rc, V, n_out: int) -> Tree:
+    # a heap-layout build holds node slots no parent points to (children of parents that did not
+    # split): keep the reachable nodes in id order — level by level, parents in order, which is
+    # the compact numbering of the per-level build — and renumber the children
+    reach = np.zeros(len(F), dtype=bool)
+    if len(F):
+        reach[0] = True
+    for k in range(len(F)):
+        if reach[k] and F[k] >= 0:
+            reach[Lc[k]] = True
+            reach[Rc[k]] = True
+    if not reach.all():
+        keep = np.nonzero(reach)[0]
+        remap = np.full(len(F), -1, dtype=np.int64)
+        remap[keep] = np.arange(keep.size)
+        F, T, V = F[keep], T[keep], V[keep]
+        Lc = np.where(F >= 0, remap[np.maximum(Lc[keep], 0)], -1)
+        Rc = np.where(F >= 0, remap[np.maximum(Rc[keep], 0)], -1)
     tree = Tree(n_out=n_out)
     cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
     tree.cat = cflag if any(cflag) else []
@@ -1274,6 +1326,7 @@ _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int
 _native.register_hip("hm_gbt2_stats", [_P, _P, _P, _I64, _P, _P, _P, _P])
 _native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_leaf_newton", [_P, _P, C.c_int, _P, _P])
+_native.register_hip("hm_hist_sibling_heap", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_route_count", [_P, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
