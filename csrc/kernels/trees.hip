@@ -294,7 +294,8 @@ __global__ __launch_bounds__(256) void gbt_stats_kernel(const float* __restrict_
 }
 
 // Per-node sums {sum r, sum h} of the rows' final nodes (leaf[r] < T), block-private in LDS.
-__global__ __launch_bounds__(256) void leaf_sums_kernel(const int32_t* __restrict__ leaf, const float* __restrict__ st2,
+template <typename NT>
+__global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ leaf, const float* __restrict__ st2,
                                                         const float* __restrict__ hh, int64_t n, int T,
                                                         float* __restrict__ sums) {
     extern __shared__ float s_sum[];
@@ -336,9 +337,10 @@ __global__ __launch_bounds__(256) void leaf_newton_kernel(const float* __restric
 }
 
 // F[r * ldf + k] += scale * vals[leaf[r] * ldv] for every routed row (leaf >= 0).
+template <typename NT>
 __global__ __launch_bounds__(256) void gbt_apply_kernel(float* __restrict__ F, int ldf, int k,
                                                         const float* __restrict__ vals, int ldv,
-                                                        const int32_t* __restrict__ leaf, int64_t n, float scale) {
+                                                        const NT* __restrict__ leaf, int64_t n, float scale) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         const int l = leaf[r];
@@ -413,8 +415,9 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 
 // Row routing after a level's splits: node_of_row[r] -> child id (or stays when the node
 // became a leaf).  split_feat[node] < 0 means leaf; HM_TREE_CAT marks a nominal split.
+template <typename NT>
 __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ bins, int64_t n,
-                                                    int dpad, int32_t* __restrict__ node_of_row,
+                                                    int dpad, NT* __restrict__ node_of_row,
                                                     const int32_t* __restrict__ split_feat,
                                                     const int32_t* __restrict__ split_bin,
                                                     const int32_t* __restrict__ left_child,
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
         const int b = bins[r * dpad + f];
         const int sb = split_bin[nd];
         const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
-        node_of_row[r] = go_left ? left_child[nd] : right_child[nd];
+        node_of_row[r] = (NT)(go_left ? left_child[nd] : right_child[nd]);
     }
 }
 
@@ -804,7 +807,8 @@ __global__ __launch_bounds__(256) void split_find_wide_kernel(SplitParams P, con
 // fixed row chunks (one per block): count per (key, block) in LDS, a device-wide inclusive scan
 // of the key-major counts (torch.cumsum), then scatter with LDS rank counters.  Order inside a
 // (key, block) cell is arbitrary; the histogram sums do not depend on it (32-bit fixed point).
-__device__ __forceinline__ int part_key(const int32_t* __restrict__ node_of_row,
+template <typename NT>
+__device__ __forceinline__ int part_key(const NT* __restrict__ node_of_row,
                                         const int16_t* __restrict__ lut, int row, int nb, int nlut,
                                         int nkeys) {
     const int c = node_of_row[row] - nb;
@@ -813,11 +817,12 @@ __device__ __forceinline__ int part_key(const int32_t* __restrict__ node_of_row,
     return k < nkeys ? k : -1;
 }
 
+template <typename NT>
 __global__ __launch_bounds__(256) void part_count_kernel(const int32_t* __restrict__ rows, int64_t m,
-                                                         const int32_t* __restrict__ node_of_row,
+                                                         const NT* __restrict__ node_of_row,
                                                          const int16_t* __restrict__ lut, int nb,
                                                          int nlut, int nkeys,
-                                                         int32_t* __restrict__ counts /* [nkeys][G] */) {
+                                                         int64_t* __restrict__ counts /* [nkeys][G] */) {
     extern __shared__ int s_cnt[];
     const int G = gridDim.x;
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) s_cnt[k] = 0;
@@ -832,11 +837,12 @@ __global__ __launch_bounds__(256) void part_count_kernel(const int32_t* __restri
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) counts[(size_t)k * G + blockIdx.x] = s_cnt[k];
 }
 
+template <typename NT>
 __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __restrict__ rows, int64_t m,
-                                                           const int32_t* __restrict__ node_of_row,
+                                                           const NT* __restrict__ node_of_row,
                                                            const int16_t* __restrict__ lut, int nb,
                                                            int nlut, int nkeys,
-                                                           const int32_t* __restrict__ counts,
+                                                           const int64_t* __restrict__ counts,
                                                            const int64_t* __restrict__ incl,
                                                            int32_t* __restrict__ out,
                                                            int64_t* __restrict__ seg /* [nkeys+1] */) {
@@ -871,14 +877,15 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
 // flight: the node -> split -> bins -> child loads are a dependent chain per row.
 constexpr int ROUTE_U = 4;
 constexpr int ROUTE_BALLOT_KEYS = 16;
+template <typename NT>
 __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n, int dpad,
-                                                          int32_t* __restrict__ node_of_row,
+                                                          NT* __restrict__ node_of_row,
                                                           const int32_t* __restrict__ split_feat,
                                                           const int32_t* __restrict__ split_bin,
                                                           const int32_t* __restrict__ left_child,
                                                           const int32_t* __restrict__ right_child, int miss_bin,
                                                           const int16_t* __restrict__ lut, int nb, int nlut,
-                                                          int nkeys, int32_t* __restrict__ counts) {
+                                                          int nkeys, int64_t* __restrict__ counts) {
     extern __shared__ int s_cnt[];
     const int G = gridDim.x;
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) s_cnt[k] = 0;
@@ -908,7 +915,7 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
             const int sb = split_bin[nd[u]];
             const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
             nd[u] = go_left ? left_child[nd[u]] : right_child[nd[u]];
-            node_of_row[q] = nd[u];
+            node_of_row[q] = (NT)nd[u];
         }
 #pragma unroll
         for (int u = 0; u < ROUTE_U; ++u) {
@@ -1103,15 +1110,20 @@ HM_API int hm_quantize(const float* X, int64_t n, int d, int dpad, const float* 
 }
 
 // miss_bin: the bin of missing values (rows there follow the split's HM_TREE_DLEFT flag), or -1.
-HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int32_t* node_of_row,
+// node16: node_of_row is int16 (trees of < 32,767 nodes: half the bytes per routing pass).
+HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, void* node_of_row,
                          const int32_t* split_feat, const int32_t* split_bin,
-                         const int32_t* left_child, const int32_t* right_child, int miss_bin,
+                         const int32_t* left_child, const int32_t* right_child, int miss_bin, int node16,
                          hipStream_t stream) {
     if (n <= 0) return 0;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(route_kernel, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
-                       node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
+    if (node16)
+        hipLaunchKernelGGL(route_kernel<int16_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
+                           (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
+    else
+        hipLaunchKernelGGL(route_kernel<int32_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
+                           (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
     HM_LAUNCH_RET();
 }
 
@@ -1146,38 +1158,51 @@ HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, 
     HM_LAUNCH_RET();
 }
 
-// Row partition of a level, pass 1: counts [nkeys][G] (int32, G = grid) of the active rows per
+// Row partition of a level, pass 1: counts [nkeys][G] (int64, G = grid) of the active rows per
 // small-child key.  Pass 2 (after incl = inclusive cumsum of the flattened counts, int64):
 // rows grouped by key into out[0 .. seg[nkeys]), segment starts seg [nkeys + 1].
-HM_API int hm_partition_count(const int32_t* rows, int64_t m, const int32_t* node_of_row,
+HM_API int hm_partition_count(const int32_t* rows, int64_t m, const void* node_of_row,
                               const int16_t* lut, int nb, int nlut, int nkeys, int grid,
-                              int32_t* counts, hipStream_t stream) {
+                              int64_t* counts, int node16, hipStream_t stream) {
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
-                       rows, m, node_of_row, lut, nb, nlut, nkeys, counts);
+    if (node16)
+        hipLaunchKernelGGL(part_count_kernel<int16_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
+                           rows, m, (const int16_t*)node_of_row, lut, nb, nlut, nkeys, counts);
+    else
+        hipLaunchKernelGGL(part_count_kernel<int32_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
+                           rows, m, (const int32_t*)node_of_row, lut, nb, nlut, nkeys, counts);
     HM_LAUNCH_RET();
 }
 
 // route_count_kernel: route rows 0 .. n-1 one level down and count the small children's rows
 // per (key, block) cell; follow with hm_partition_scatter(rows = NULL, m = n, same grid).
-HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, int32_t* node_of_row, const int32_t* split_feat,
+HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, void* node_of_row, const int32_t* split_feat,
                           const int32_t* split_bin, const int32_t* left_child, const int32_t* right_child,
                           int miss_bin, const int16_t* lut, int nb, int nlut, int nkeys, int grid,
-                          int32_t* counts, hipStream_t stream) {
+                          int64_t* counts, int node16, hipStream_t stream) {
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0 || n <= 0 || n > INT32_MAX) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(route_count_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream, bins, n,
-                       dpad, node_of_row, split_feat, split_bin, left_child, right_child, miss_bin, lut, nb, nlut,
-                       nkeys, counts);
+    if (node16)
+        hipLaunchKernelGGL(route_count_kernel<int16_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
+                           bins, n, dpad, (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child,
+                           miss_bin, lut, nb, nlut, nkeys, counts);
+    else
+        hipLaunchKernelGGL(route_count_kernel<int32_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
+                           bins, n, dpad, (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child,
+                           miss_bin, lut, nb, nlut, nkeys, counts);
     HM_LAUNCH_RET();
 }
 
-HM_API int hm_partition_scatter(const int32_t* rows, int64_t m, const int32_t* node_of_row,
+HM_API int hm_partition_scatter(const int32_t* rows, int64_t m, const void* node_of_row,
                                 const int16_t* lut, int nb, int nlut, int nkeys, int grid,
-                                const int32_t* counts, const int64_t* incl, int32_t* out,
-                                int64_t* seg, hipStream_t stream) {
+                                const int64_t* counts, const int64_t* incl, int32_t* out,
+                                int64_t* seg, int node16, hipStream_t stream) {
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int64_t), stream,
-                       rows, m, node_of_row, lut, nb, nlut, nkeys, counts, incl, out, seg);
+    if (node16)
+        hipLaunchKernelGGL(part_scatter_kernel<int16_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int64_t),
+                           stream, rows, m, (const int16_t*)node_of_row, lut, nb, nlut, nkeys, counts, incl, out, seg);
+    else
+        hipLaunchKernelGGL(part_scatter_kernel<int32_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int64_t),
+                           stream, rows, m, (const int32_t*)node_of_row, lut, nb, nlut, nkeys, counts, incl, out, seg);
     HM_LAUNCH_RET();
 }
 
@@ -1240,14 +1265,18 @@ HM_API int hm_gbt2_stats(const float* F, const float* y, const uint8_t* mask, in
 }
 
 // sums [T, 2] (zeroed by the caller) += {sum r, sum h} of the rows of every node (leaf [n] ids < T).
-HM_API int hm_leaf_sums(const int32_t* leaf, const float* st2, const float* hh, int64_t n, int T, float* sums,
-                        hipStream_t stream) {
+HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int64_t n, int T, float* sums,
+                        int node16, hipStream_t stream) {
     if (n <= 0) return 0;
     if (T <= 0 || T > 8192) return (int)hipErrorInvalidValue;
     int64_t blocks = (n + 4095) / 4096;
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(leaf_sums_kernel, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream, leaf, st2,
-                       hh, n, T, sums);
+    if (node16)
+        hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream,
+                           (const int16_t*)leaf, st2, hh, n, T, sums);
+    else
+        hipLaunchKernelGGL(leaf_sums_kernel<int32_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream,
+                           (const int32_t*)leaf, st2, hh, n, T, sums);
     HM_LAUNCH_RET();
 }
 
@@ -1259,13 +1288,17 @@ HM_API int hm_leaf_newton(const float* sums, const int32_t* sf, int T, float* va
 }
 
 // F[r * ldf + k] += scale * vals[leaf[r] * ldv] for leaf[r] >= 0.
-HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, const int32_t* leaf, int64_t n,
-                        float scale, hipStream_t stream) {
+HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, const void* leaf, int64_t n,
+                        float scale, int node16, hipStream_t stream) {
     if (n <= 0) return 0;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(gbt_apply_kernel, dim3((int)blocks), dim3(256), 0, stream, F, ldf, k, vals, ldv, leaf, n,
-                       scale);
+    if (node16)
+        hipLaunchKernelGGL(gbt_apply_kernel<int16_t>, dim3((int)blocks), dim3(256), 0, stream, F, ldf, k, vals, ldv,
+                           (const int16_t*)leaf, n, scale);
+    else
+        hipLaunchKernelGGL(gbt_apply_kernel<int32_t>, dim3((int)blocks), dim3(256), 0, stream, F, ldf, k, vals, ldv,
+                           (const int32_t*)leaf, n, scale);
     HM_LAUNCH_RET();
 }
 

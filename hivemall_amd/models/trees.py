@@ -423,16 +423,17 @@ class HistTreeBuilder:
         dev = act_rows.device
         m = act_rows.numel()
         G = int(max(1, min(1024, (m + 4095) // 4096)))
-        counts = torch.empty(n_keys * G, dtype=torch.int32, device=dev)
+        counts = torch.empty(n_keys * G, dtype=torch.int64, device=dev)
         p, st = _native.ptr, _native.stream_of(dev)
+        n16 = int(node_of_row.dtype == torch.int16)
         _native.check(_native.hip().hm_partition_count(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
-                                                       lut.numel(), n_keys, G, p(counts), st), "hm_partition_count")
+                                                       lut.numel(), n_keys, G, p(counts), n16, st), "hm_partition_count")
         incl = torch.cumsum(counts, 0)                     # int64
         rows = torch.empty(max(1, m), dtype=torch.int32, device=dev)
         seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
         _native.check(_native.hip().hm_partition_scatter(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
                                                          lut.numel(), n_keys, G, p(counts), p(incl), p(rows),
-                                                         p(seg), st), "hm_partition_scatter")
+                                                         p(seg), n16, st), "hm_partition_scatter")
         return rows, seg
 
     def _route_partition_gpu(self, n: int, node_of_row, nbuf: "_NodeBuf", nb: int, lut, n_keys: int):
@@ -441,17 +442,19 @@ class HistTreeBuilder:
         q = self.q
         dev = node_of_row.device
         G = int(max(1, min(1024, (n + 4095) // 4096)))
-        counts = torch.empty(n_keys * G, dtype=torch.int32, device=dev)
+        counts = torch.empty(n_keys * G, dtype=torch.int64, device=dev)
         p, st = _native.ptr, _native.stream_of(dev)
+        n16 = int(node_of_row.dtype == torch.int16)
         _native.check(_native.hip().hm_route_count(
             p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
-            (q.B - 1) if self.missing else -1, p(lut), nb, lut.numel(), n_keys, G, p(counts), st), "hm_route_count")
+            (q.B - 1) if self.missing else -1, p(lut), nb, lut.numel(), n_keys, G, p(counts), n16, st),
+            "hm_route_count")
         incl = torch.cumsum(counts, 0)
         rows = torch.empty(max(1, n), dtype=torch.int32, device=dev)
         seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
         _native.check(_native.hip().hm_partition_scatter(None, C.c_int64(n), p(node_of_row), p(lut), nb,
                                                          lut.numel(), n_keys, G, p(counts), p(incl), p(rows),
-                                                         p(seg), st), "hm_partition_scatter")
+                                                         p(seg), n16, st), "hm_partition_scatter")
         return rows, seg
 
     def _hist(self, rows, seg, n_seg, stats, smax):
@@ -518,7 +521,9 @@ class HistTreeBuilder:
         heap = (HEAP_TREES and dev.type == "cuda" and self.max_leaves is None
                 and self.max_depth <= HEAP_MAX_DEPTH and not (self.mtry is not None and self.mtry < d)
                 and (NS <= 8 or self.criterion in ("gini", "entropy")))
-        node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
+        # heap levels hold at most 2^(HEAP_MAX_DEPTH + 1) - 1 node ids: int16 halves the bytes of
+        # the per-level routing / partition / leaf passes over the rows
+        node_of_row = torch.zeros(n, dtype=torch.int16 if heap else torch.int32, device=dev)
         if active is not None:
             node_of_row[~active] = -1
         if act_rows is None:
@@ -579,7 +584,8 @@ class HistTreeBuilder:
                 else:
                     _native.check(_native.hip().hm_route_rows(
                         p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc),
-                        p(nbuf.rc), (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
+                        p(nbuf.rc), (q.B - 1) if self.missing else -1, int(node_of_row.dtype == torch.int16),
+                        _native.stream_of(dev)), "hm_route_rows")
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, L)
                 Hs = self._hist(rows, seg.contiguous(), L, stats, smax)
                 Hn = torch.empty((2 * L, d, B, NS), dtype=torch.float32, device=dev)
@@ -611,7 +617,8 @@ class HistTreeBuilder:
                     continue
                 _native.check(_native.hip().hm_route_rows(
                     p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
-                    (q.B - 1) if self.missing else -1, _native.stream_of(dev)), "hm_route_rows")
+                    (q.B - 1) if self.missing else -1, int(node_of_row.dtype == torch.int16),
+                        _native.stream_of(dev)), "hm_route_rows")
                 if n_split <= 8192:
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, n_split)
                 else:
@@ -663,7 +670,8 @@ class HistTreeBuilder:
             args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all),
                     (q.B - 1) if self.missing else -1)
             if dev.type == "cuda":
-                _native.check(_native.hip().hm_route_rows(*args, _native.stream_of(dev)), "hm_route_rows")
+                _native.check(_native.hip().hm_route_rows(*args, int(node_of_row.dtype == torch.int16),
+                                                          _native.stream_of(dev)), "hm_route_rows")
             else:
                 _native.host().hm_route_rows_cpu(*args)
             # next level: histogram the smaller child of every split, derive the sibling
@@ -708,7 +716,8 @@ class HistTreeBuilder:
             p, st_ = _native.ptr, _native.stream_of(dev)
             if t <= 8192:
                 _native.check(_native.hip().hm_leaf_sums(p(node_of_row), p(stats), p(leaf_h), C.c_int64(n), t,
-                                                         p(sums), st_), "hm_leaf_sums")
+                                                         p(sums), int(node_of_row.dtype == torch.int16), st_),
+                              "hm_leaf_sums")
             else:
                 ok = node_of_row >= 0
                 nd = node_of_row[ok].long()
@@ -736,16 +745,18 @@ class HistTreeBuilder:
 
 
 def _tree_from_arrays(F, T, Lc, Rc, V, n_out: int) -> Tree:
+    F, T, Lc, Rc, V = (np.asarray(a) for a in (F, T, Lc, Rc, V))
     # a heap-layout build holds node slots no parent points to (children of parents that did not
     # split): keep the reachable nodes in id order — level by level, parents in order, which is
     # the compact numbering of the per-level build — and renumber the children
     reach = np.zeros(len(F), dtype=bool)
     if len(F):
         reach[0] = True
-    for k in range(len(F)):
-        if reach[k] and F[k] >= 0:
-            reach[Lc[k]] = True
-            reach[Rc[k]] = True
+        front = np.array([0])
+        while front.size:
+            sp = front[F[front] >= 0]
+            front = np.concatenate([Lc[sp], Rc[sp]])
+            reach[front] = True
     if not reach.all():
         keep = np.nonzero(reach)[0]
         remap = np.full(len(F), -1, dtype=np.int64)
@@ -753,16 +764,19 @@ def _tree_from_arrays(F, T, Lc, Rc, V, n_out: int) -> Tree:
         F, T, V = F[keep], T[keep], V[keep]
         Lc = np.where(F >= 0, remap[np.maximum(Lc[keep], 0)], -1)
         Rc = np.where(F >= 0, remap[np.maximum(Rc[keep], 0)], -1)
+    F = F.astype(np.int64)
+    split = F >= 0
     tree = Tree(n_out=n_out)
-    cflag = [1 if (f >= 0 and int(f) & CAT_FLAG) else 0 for f in F]
-    tree.cat = cflag if any(cflag) else []
-    dflag = [1 if (f >= 0 and int(f) & DLEFT_FLAG) else 0 for f in F]
-    tree.dleft = dflag if any(dflag) else []
-    tree.feature = [int(f) & ~(CAT_FLAG | DLEFT_FLAG) if f >= 0 else int(f) for f in F]
-    tree.threshold = [float(t) for t in T]
-    tree.left = [int(x) for x in Lc]
-    tree.right = [int(x) for x in Rc]
-    tree.value = [None if F[k] >= 0 else V[k].tolist() for k in range(len(F))]
+    cflag = (split & ((F & CAT_FLAG) != 0)).astype(int)
+    tree.cat = cflag.tolist() if cflag.any() else []
+    dflag = (split & ((F & DLEFT_FLAG) != 0)).astype(int)
+    tree.dleft = dflag.tolist() if dflag.any() else []
+    tree.feature = np.where(split, F & ~(CAT_FLAG | DLEFT_FLAG), F).tolist()
+    tree.threshold = T.astype(np.float64).tolist()
+    tree.left = Lc.astype(np.int64).tolist()
+    tree.right = Rc.astype(np.int64).tolist()
+    vl = V.tolist()
+    tree.value = [None if sp else v for sp, v in zip(split.tolist(), vl)]
     return tree
 
 
@@ -783,8 +797,21 @@ class PendingTree:
 
 
 def materialize_trees(iters: list) -> list:
-    """Boosting rounds with any PendingTree replaced by its Tree."""
-    return [[t.materialize() if isinstance(t, PendingTree) else t for t in it] for it in iters]
+    """Boosting rounds with every PendingTree replaced by its Tree: the node arrays of all of
+    them come to the host in one copy per array kind (one sync, not five per tree)."""
+    pend = [t for it in iters for t in it if isinstance(t, PendingTree)]
+    if not pend:
+        return iters
+    sizes = [t.arrays[0].numel() for t in pend]
+    ints = torch.cat([torch.stack([t.arrays[0], t.arrays[2], t.arrays[3]]) for t in pend], 1).cpu().numpy()
+    thr = torch.cat([t.arrays[1] for t in pend]).cpu().numpy()
+    vals = torch.cat([t.arrays[4] for t in pend]).double().cpu().numpy()
+    out, o = {}, 0
+    for t, n in zip(pend, sizes):
+        out[id(t)] = _tree_from_arrays(ints[0, o:o + n], thr[o:o + n], ints[1, o:o + n], ints[2, o:o + n],
+                                       vals[o:o + n] * t.scale, t.n_out)
+        o += n
+    return [[out[id(t)] if isinstance(t, PendingTree) else t for t in it] for it in iters]
 
 
 # ------------------------------------------------------------------ learners
@@ -1095,7 +1122,7 @@ class GradientTreeBoostingClassifier(Learner):
                 vals = b.node_values.float().contiguous()
                 _native.check(_native.hip().hm_gbt_apply(
                     _native.ptr(F), F.shape[1], 0, _native.ptr(vals), vals.shape[1], _native.ptr(b.leaf_of_row),
-                    C.c_int64(n), C.c_float(eta), st), "hm_gbt_apply")
+                    C.c_int64(n), C.c_float(eta), int(b.leaf_of_row.dtype == torch.int16), st), "hm_gbt_apply")
                 self.iters.append([tree])
                 if mask is None:
                     self.oob_rates.append(0.0)
@@ -1316,21 +1343,21 @@ _native.register_host("hm_tree_predict_cpu", [_P, _I64, C.c_int] + [_P] * 7 + [C
 _native.register_hip("hm_quantize", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P, _P])
 _native.register_host("hm_quantize_cpu", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_absmax_cols", [_P, _I64, C.c_int, _P, _P])
-_native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int, _P])
+_native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int, C.c_int, _P])
 _native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int])
 _native.register_hip("hm_split_find", [_P] * 10 + [_P])
 _native.register_host("hm_split_find_cpu", [_P] * 10)
-_native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P])
+_native.register_hip("hm_partition_count", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_partition_scatter", [_P, _I64, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P,
-                                              _P, _P, _P])
+                                              _P, _P, C.c_int, _P])
 _native.register_hip("hm_gbt2_stats", [_P, _P, _P, _I64, _P, _P, _P, _P])
-_native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, _P])
+_native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_leaf_newton", [_P, _P, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling_heap", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_route_count", [_P, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
-                                        C.c_int, C.c_int, _P, _P])
+                                        C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
 _native.register_hip("hm_xgb_stats", [_P, _P, _P, _I64, _P, _P, _P])
 _native.register_hip("hm_level_finalize", [_P] * 21)
-_native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, _P])
+_native.register_hip("hm_gbt_apply", [_P, C.c_int, C.c_int, _P, C.c_int, _P, _I64, C.c_float, C.c_int, _P])

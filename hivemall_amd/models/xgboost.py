@@ -193,7 +193,8 @@ class XGBoostTrainer(Learner):
                     vals = b.node_values.float().contiguous()
                     _native.check(_native.hip().hm_gbt_apply(
                         _native.ptr(F), F.shape[1], k, _native.ptr(vals), vals.shape[1], _native.ptr(b.leaf_of_row),
-                        C.c_int64(n), C.c_float(eta), _native.stream_of(F.device)), "hm_gbt_apply")
+                        C.c_int64(n), C.c_float(eta), int(b.leaf_of_row.dtype == torch.int16),
+                        _native.stream_of(F.device)), "hm_gbt_apply")
                 else:
                     F[:, k] += eta * b.node_values[b.leaf_of_row.long(), 0]
                 if isinstance(tree, PendingTree):
