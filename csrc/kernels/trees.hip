@@ -512,8 +512,13 @@ __device__ __forceinline__ float split_score(const float* S, int crit, float lam
     return s1 > 0.f ? g * g / (s1 + lam) : 0.f;
 }
 
+// 16 waves per node: every wave scans <= 2 features (d <= 32) instead of 7 in series — the
+// kernel is a chain of dependent histogram reads per feature, and the upper levels have only
+// 1 .. 64 nodes (blocks) for 256 CUs
+// (512 for > 4 statistics: their per-lane state fits 128 VGPRs only at 1024 without spilling)
+template <int NS> constexpr int sf_threads() { return NS <= 4 ? 1024 : 512; }
 template <int NS>
-__global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const float* __restrict__ hist,
+__global__ __launch_bounds__(sf_threads<NS>()) void split_find_kernel(SplitParams P, const float* __restrict__ hist,
                                                          const uint8_t* __restrict__ cat,
                                                          const uint8_t* __restrict__ fmask,
                                                          float* __restrict__ out_gain,
@@ -521,9 +526,10 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
                                                          int32_t* __restrict__ out_bin,
                                                          float* __restrict__ out_left,
                                                          float* __restrict__ out_tot) {
-    __shared__ float s_gain[4];
-    __shared__ int s_idx[4];
-    __shared__ float s_left[4][NS];
+    constexpr int NW = sf_threads<NS>() / 64;
+    __shared__ float s_gain[NW];
+    __shared__ int s_idx[NW];
+    __shared__ float s_left[NW][NS];
     const int node = blockIdx.x;
     const int lane = hm::lane_id(), wave = hm::wave_id();
     const int B = P.B, d = P.d;
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
     float best_left[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) best_left[s] = 0.f;
-    for (int f = wave; f < d; f += 4) {
+    for (int f = wave; f < d; f += NW) {   // <= 2 features per wave at d <= 32
         if (fmask && !fmask[f]) continue;
         if (P.mtry > 0 && P.mtry < d) {
             // candidate iff fewer than mtry features rank before f (wave-uniform loop)
@@ -650,7 +656,7 @@ __global__ __launch_bounds__(256) void split_find_kernel(SplitParams P, const fl
     __syncthreads();
     if (threadIdx.x == 0) {
         int w = 0;
-        for (int k = 1; k < 4; ++k)
+        for (int k = 1; k < NW; ++k)
             if (s_gain[k] > s_gain[w] || (s_gain[k] == s_gain[w] && s_idx[k] < s_idx[w])) w = k;
         const bool found = s_idx[w] != 0x7FFFFFFF;
         const int fb = s_idx[w] >> 1;
@@ -1148,7 +1154,7 @@ HM_API int hm_split_find(const float* hist, const int32_t* ip, const float* fp, 
         HM_LAUNCH_RET();
     }
 #define HM_SF(K) \
-    case K: hipLaunchKernelGGL((split_find_kernel<K>), dim3(P.L), dim3(256), 0, stream, P, hist, cat, fmask, \
+    case K: hipLaunchKernelGGL((split_find_kernel<K>), dim3(P.L), dim3(sf_threads<K>()), 0, stream, P, hist, cat, fmask, \
                                gain, feat, bin, left, tot); break;
     switch (P.NS) {
         HM_SF(1) HM_SF(2) HM_SF(3) HM_SF(4) HM_SF(5) HM_SF(6) HM_SF(7) HM_SF(8)
@@ -1269,8 +1275,9 @@ HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int
                         int node16, hipStream_t stream) {
     if (n <= 0) return 0;
     if (T <= 0 || T > 8192) return (int)hipErrorInvalidValue;
+    // at most 256 blocks: every block ends with 2T atomic adds onto the same 2T addresses
     int64_t blocks = (n + 4095) / 4096;
-    if (blocks > 1024) blocks = 1024;
+    if (blocks > 256) blocks = 256;
     if (node16)
         hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream,
                            (const int16_t*)leaf, st2, hh, n, T, sums);

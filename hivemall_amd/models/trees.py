@@ -458,12 +458,13 @@ class HistTreeBuilder:
                                                          p(seg), n16, st), "hm_partition_scatter")
         return rows, seg
 
-    def _hist(self, rows, seg, n_seg, stats, smax):
-        """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]]."""
+    def _hist(self, rows, seg, n_seg, stats, smax, out: torch.Tensor | None = None):
+        """[n_seg, d, B, NS] histograms of the row segments rows[seg[k]:seg[k+1]] (into ``out``,
+        zeroed by the caller, when given)."""
         q = self.q
         NS = stats.shape[1]
         dev = stats.device
-        hist = torch.zeros((n_seg, q.d, q.B, NS), dtype=torch.float32, device=dev)
+        hist = out if out is not None else torch.zeros((n_seg, q.d, q.B, NS), dtype=torch.float32, device=dev)
         p = _native.ptr
         if dev.type == "cuda" and NS > 8:
             # many classes: the LDS kernel sums <= 8 statistics per pass -> class tiles of 8
@@ -525,6 +526,7 @@ class HistTreeBuilder:
         # heap levels hold at most 2^(HEAP_MAX_DEPTH + 1) - 1 node ids: int16 halves the bytes of
         # the per-level routing / partition / leaf passes over the rows
         node_of_row = torch.zeros(n, dtype=torch.int16 if heap else torch.int32, device=dev)
+        arena = None
         if active is not None:
             node_of_row[~active] = -1
         if act_rows is None:
@@ -588,7 +590,9 @@ class HistTreeBuilder:
                         p(nbuf.rc), (q.B - 1) if self.missing else -1, int(node_of_row.dtype == torch.int16),
                         _native.stream_of(dev)), "hm_route_rows")
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, L)
-                Hs = self._hist(rows, seg.contiguous(), L, stats, smax)
+                if arena is None:   # every level's smaller-child histograms, zeroed in one fill
+                    arena = torch.zeros((((1 << self.max_depth) - 1), d, B, NS), dtype=torch.float32, device=dev)
+                Hs = self._hist(rows, seg.contiguous(), L, stats, smax, out=arena[L - 1:2 * L - 1])
                 Hn = torch.empty((2 * L, d, B, NS), dtype=torch.float32, device=dev)
                 _native.check(_native.hip().hm_hist_sibling_heap(
                     p(H), p(Hs), p(nbuf.sf) + 4 * base, p(sr), C.c_int64(d * B * NS), L, p(Hn),
