@@ -299,8 +299,12 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ l
                                                         const float* __restrict__ hh, int64_t n, int T,
                                                         float* __restrict__ sums) {
     extern __shared__ float s_sum[];
-    for (int k = threadIdx.x; k < 2 * T; k += blockDim.x) s_sum[k] = 0.f;
+    // one copy of the sums per wave when they fit (copies = 4: a tree's 256 leaves drew most of a
+    // wave's 64 adds onto the same few words), folded into copy 0 at the end
+    const int copies = 2 * T <= 2048 ? 4 : 1;
+    for (int k = threadIdx.x; k < 2 * T * copies; k += blockDim.x) s_sum[k] = 0.f;
     __syncthreads();
+    float* my = s_sum + (copies > 1 ? (threadIdx.x >> 6) % copies : 0) * 2 * T;
     // LEAF_U rows per thread with every load issued before the first LDS add
     constexpr int LEAF_U = 8;
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
@@ -318,13 +322,16 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ l
 #pragma unroll
         for (int u = 0; u < LEAF_U; ++u) {
             if (l[u] < 0 || l[u] >= T || h[u] == 0.f) continue;
-            atomicAdd(&s_sum[2 * l[u]], g[u]);
-            atomicAdd(&s_sum[2 * l[u] + 1], h[u]);
+            atomicAdd(&my[2 * l[u]], g[u]);
+            atomicAdd(&my[2 * l[u] + 1], h[u]);
         }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < 2 * T; k += blockDim.x)
-        if (s_sum[k] != 0.f) atomicAdd(sums + k, s_sum[k]);
+    for (int k = threadIdx.x; k < 2 * T; k += blockDim.x) {
+        float v = s_sum[k];
+        for (int c = 1; c < copies; ++c) v += s_sum[c * 2 * T + k];
+        if (v != 0.f) atomicAdd(sums + k, v);
+    }
 }
 
 // Leaf values of the nodes that are leaves (split_feat < 0): sum r / sum h (0 when sum h ~ 0).
@@ -1279,10 +1286,10 @@ HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int
     int64_t blocks = (n + 4095) / 4096;
     if (blocks > 256) blocks = 256;
     if (node16)
-        hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream,
+        hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float) * (2 * T <= 2048 ? 4 : 1), stream,
                            (const int16_t*)leaf, st2, hh, n, T, sums);
     else
-        hipLaunchKernelGGL(leaf_sums_kernel<int32_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float), stream,
+        hipLaunchKernelGGL(leaf_sums_kernel<int32_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float) * (2 * T <= 2048 ? 4 : 1), stream,
                            (const int32_t*)leaf, st2, hh, n, T, sums);
     HM_LAUNCH_RET();
 }
