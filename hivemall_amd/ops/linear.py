@@ -167,7 +167,7 @@ def new_shared_state(dims: int, device, n_rows: int, waves: int | None = None, r
                      torch.zeros((R, dims), dtype=torch.uint8, device=device),
                      torch.zeros((W, 8), dtype=torch.float32, device=device), False)
     st.meta["shared"] = True
-    st.meta["reload"] = bool(reload)
+    st.meta["reload"] = bool(int(os.environ.get("HM_LINEAR_RELOAD", int(reload))))
     st.meta["nt"] = bool(nt)
     return st
 
