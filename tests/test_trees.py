@@ -445,3 +445,35 @@ def test_rf_ten_classes_gpu_matches_cpu():
                                np.asarray(tg.threshold, dtype=np.float64))
     rf = RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device="cuda").fit(X, y)
     assert (rf.predict(X) == y).mean() > 0.9
+
+
+def test_heap_layout_tree_compaction_matches_compact_numbering():
+    """A heap-layout build (children of node k at 2k+1, 2k+2; slots of parents that did not
+    split stay in the arrays) materialises to the per-level build's compact numbering: the
+    reachable nodes in id order, children renumbered (models/trees.py _tree_from_arrays)."""
+    from hivemall_amd.models.trees import PendingTree, _tree_from_arrays, materialize_trees
+
+    # depth-2 heap: root 0 splits; node 1 splits, node 2 is a leaf -> slots 5, 6 unreachable
+    F = np.array([3, 1, -1, -1, -1, -1, -1], dtype=np.int32)
+    T = np.array([0.5, 1.5, np.inf, np.inf, np.inf, np.inf, np.inf], dtype=np.float32)
+    Lc = np.array([1, 3, -1, -1, -1, -1, -1], dtype=np.int32)
+    Rc = np.array([2, 4, -1, -1, -1, -1, -1], dtype=np.int32)
+    V = np.arange(7, dtype=np.float64)[:, None]
+    t = _tree_from_arrays(F, T, Lc, Rc, V, 1)
+    assert t.feature == [3, 1, -1, -1, -1]
+    assert t.left == [1, 3, -1, -1, -1] and t.right == [2, 4, -1, -1, -1]
+    assert t.value == [None, None, [2.0], [3.0], [4.0]]
+    # a parent that did not split at level 1 (node 1), its sibling did: slots 3, 4 dropped
+    F2 = np.array([0, -1, 2, -1, -1, -1, -1], dtype=np.int32)
+    Lc2 = np.array([1, -1, 5, -1, -1, -1, -1], dtype=np.int32)
+    Rc2 = np.array([2, -1, 6, -1, -1, -1, -1], dtype=np.int32)
+    t2 = _tree_from_arrays(F2, T, Lc2, Rc2, V, 1)
+    assert t2.feature == [0, -1, 2, -1, -1]
+    assert t2.left == [1, -1, 3, -1, -1] and t2.right == [2, -1, 4, -1, -1]
+    assert t2.value == [None, [1.0], None, [5.0], [6.0]]
+    # deferred trees: one host copy for all of them, leaf values scaled (XGBoost's eta)
+    p = PendingTree(torch.from_numpy(F2), torch.from_numpy(T), torch.from_numpy(Lc2), torch.from_numpy(Rc2),
+                    torch.from_numpy(V.astype(np.float32)), 1)
+    p.scale = 0.5
+    (t3,), = materialize_trees([[p]])
+    assert t3.feature == t2.feature and t3.value == [None, [0.5], None, [2.5], [3.0]]
