@@ -951,16 +951,17 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // ffm_pipe_kernel (A..F above) with two DMAs per slot (V 16 B, G 4 B) into separate landing
 // zones.  A register-prefetch variant of this layout reached 66-68 M rows/s (70 % of the
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
-// removed); here the next row's V lands in LDS (DMA) and only its 4-B G values in registers
-// (53 KB per block -> 3 blocks/CU).
+// removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
+// block -> 2 blocks/CU).
 template <int NS, typename OT, int TPB = 256>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3 * TPB / 256))) void ffm_pipe_sg32_kernel(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
     float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
     __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB];    // V DMA landing zone
+    __shared__ __attribute__((aligned(16))) float s_rg[NS * TPB];     // G DMA landing zone
     __shared__ __attribute__((aligned(16))) float4 s_t[NS * TPB];     // transposed V image
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
@@ -1019,9 +1020,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3 * TPB / 2
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
-    // the next row's per-slot G: loaded to registers in phase C, read in phase B (an LDS landing
-    // zone for it made the block 59 KB, 2 per CU; without it 53 KB, 3 blocks = rows in flight)
-    float gnx[NS];
     auto dma_slots = [&](int bf) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -1029,7 +1027,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3 * TPB / 2
             float xab;
             slot(bf, j, ov, og, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, 0);
-            gnx[j] = *reinterpret_cast<const float*>(gb + og);   // G to registers (no LDS zone)
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
         }
     };
     auto dma_lin = [&](int bf) {
@@ -1075,7 +1073,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3 * TPB / 2
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            cg[j] = gnx[j];
+            cg[j] = s_rg[j * TPB + tid];
             float4 v = s_rv[j * TPB + tid];
             if (fwd >> j & 1u) {
                 OT ov, og;
