@@ -953,17 +953,15 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-// GREG (A/B, HM_FFM_VARIANT=10): the next row's 4-B G values prefetched into registers instead
-// of an LDS landing zone: 53 KB per block -> 3 blocks (rows in flight) per CU instead of 2.
-template <int NS, typename OT, int TPB = 256, bool GREG = false>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GREG ? 3 * TPB / 256 : TPB / 128))) void ffm_pipe_sg32_kernel(
+template <int NS, typename OT, int TPB = 256>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
     float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
     __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB];    // V DMA landing zone
-    __shared__ __attribute__((aligned(16))) float s_rg[GREG ? 1 : NS * TPB];   // G DMA landing zone
+    __shared__ __attribute__((aligned(16))) float s_rg[NS * TPB];     // G DMA landing zone
     __shared__ __attribute__((aligned(16))) float4 s_t[NS * TPB];     // transposed V image
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
@@ -1022,7 +1020,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GREG ? 3 * 
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
-    float gnx[NS];                                                    // GREG: next row's G
     auto dma_slots = [&](int bf) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -1030,10 +1027,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GREG ? 3 * 
             float xab;
             slot(bf, j, ov, og, xab);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, 0);
-            if constexpr (GREG)
-                gnx[j] = *reinterpret_cast<const float*>(gb + og);
-            else
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
         }
     };
     auto dma_lin = [&](int bf) {
@@ -1079,7 +1073,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(GREG ? 3 * 
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            cg[j] = GREG ? gnx[j] : s_rg[j * TPB + tid];
+            cg[j] = s_rg[j * TPB + tid];
             float4 v = s_rv[j * TPB + tid];
             if (fwd >> j & 1u) {
                 OT ov, og;
@@ -1510,16 +1504,6 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
-    if (variant == 10 && !wide) {
-#define HM_P32G(NSV) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, true>), dim3(blocks), dim3(256), 0, \
-                                        stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss)
-        if (need <= 2) { HM_P32G(2); }
-        else if (need <= 4) { HM_P32G(4); }
-        else if (need <= 6) { HM_P32G(6); }
-        else { HM_P32G(8); }
-#undef HM_P32G
-        HM_LAUNCH_RET();
-    }
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
     else if (need <= 6) { HM_P32(6); }
@@ -1612,7 +1596,10 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 // LDS image (4 rows in flight per CU instead of 2): 58.1-58.4 vs 74.9-75.5 M rows/s — the (b, a)
 // halves of a wave's pairs are V[i_b][f_a] for 64 different features, 16-B loads from 64
 // feature blocks where the row-major order reads whole runs of one block
-// (profiles/r4/ffm_paired_slots_ab.log).
+// (profiles/r4/ffm_paired_slots_ab.log); the sg32 kernel with the next row's G prefetched into
+// registers instead of an LDS landing zone (53 KB per block: 3 rows in flight per CU instead of
+// 2): 73.6-73.8 vs 73.9-74.2 M rows/s (profiles/r4/ffm_register_g_ab.log) — more rows in flight
+// per CU does not move this kernel.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
