@@ -489,46 +489,23 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
     const int ch = HOT ? CH : 1;
     const int64_t span = (int64_t)W * ch;
     const int64_t nchunks = (n_rows + span - 1) / span;
-    // Row-ahead pipeline: a wave's rows are q, q + W, q + 2W, ...  While row q computes, the
-    // bounds of row q + 2W and the first 64 (index, value) pairs and label of row q + W are in
-    // flight, so the row's own chain starts at its state gathers (the CSR loads were two
-    // dependent round trips per row at the head of it).
-    auto row_of = [&](int64_t qq) -> int64_t { return order ? (int64_t)order[qq] : qq; };
-    int64_t qa = g;                                   // this wave's first row
-    int64_t s_cur = 0, e_cur = 0, s_nx = 0, e_nx = 0;
-    int ci_cur = -1;
-    float cx_cur = 0.f, y_cur = 0.f;
-    if (active && qa < n_rows) {
-        const int64_t r0 = row_of(qa);
-        s_cur = indptr[r0]; e_cur = indptr[r0 + 1]; y_cur = y[r0];
-        if (s_cur + lane < e_cur) { ci_cur = idx[s_cur + lane]; cx_cur = val ? val[s_cur + lane] : 1.f; }
-        if (qa + W < n_rows) { const int64_t r1 = row_of(qa + W); s_nx = indptr[r1]; e_nx = indptr[r1 + 1]; }
-    }
     for (int64_t ck = 0; ck < nchunks; ++ck) {
         for (int j = 0; j < ch && active; ++j) {
             const int64_t q = ck * span + (int64_t)j * W + g;
             if (q >= n_rows) break;
-            const int64_t s = s_cur, e = e_cur;
-            const float yy = y_cur;
-            int ci = ci_cur, hs = -1;
-            float cx = cx_cur;
-            // prefetch: row q + W's indices / label (its bounds arrived last row), q + 2W's bounds
-            if (q + W < n_rows) {
-                const int64_t r1 = row_of(q + W);
-                y_cur = y[r1];
-                ci_cur = -1; cx_cur = 0.f;
-                if (s_nx + lane < e_nx) { ci_cur = idx[s_nx + lane]; cx_cur = val ? val[s_nx + lane] : 1.f; }
-                s_cur = s_nx; e_cur = e_nx;
-                if (q + 2 * W < n_rows) { const int64_t r2 = row_of(q + 2 * W); s_nx = indptr[r2]; e_nx = indptr[r2 + 1]; }
-            }
+            const int64_t row = order ? (int64_t)order[q] : q;
+            const int64_t s = indptr[row], e = indptr[row + 1];
+            const float yy = y[row];
             const float t = (float)(t0 + q + 1);
             rs[RS_T] = t;
             const StepK sk = step_consts(P, t);
+            int ci = -1, hs = -1;
+            float cx = 0.f;
             if (s + lane < e) {
+                ci = idx[s + lane];
+                cx = val ? val[s + lane] : 1.f;
                 if (ci < 0 || ci >= dims) ci = -1;
                 if (HOT && ci >= 0) hs = hot_slot[ci];
-            } else {
-                ci = -1;
             }
             F4 cst = {0.f, 0.f, 0.f, 0.f};
             float p = 0.f, sq = 0.f;
