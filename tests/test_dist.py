@@ -343,6 +343,8 @@ def test_bench_configs_n_gpu_entry_point_cpu_world2():
         assert d["world"] == 2 and d["n_gpus"] == 2 and d["dist_backend"] == "gloo"
     assert recs[1]["trees_in_forest"] == 4
     assert 0.6 < recs[0]["test_auc"] and 0.6 < recs[2]["sampled_auc"]
+    # the per-level histogram all-reduce of data-parallel boosting, broken out per tree
+    assert recs[0]["hist_allreduce_ms_per_tree"] > 0 and recs[0]["hist_allreduce_mb_per_tree"] > 0
 
 
 def _metrics_dp(ctx):
