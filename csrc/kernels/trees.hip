@@ -422,9 +422,12 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 
 // Row routing after a level's splits: node_of_row[r] -> child id (or stays when the node
 // became a leaf).  split_feat[node] < 0 means leaf; HM_TREE_CAT marks a nominal split.
+// Bin of (row r, feature f) at bins[r * rs + f * cs]: row-major (rs = dpad, cs = 1) or the
+// feature-major copy (rs = 1, cs = n), where a wave's rows read one 64-B run per distinct split
+// feature instead of 64 whole 32-B rows.
 template <typename NT>
 __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ bins, int64_t n,
-                                                    int dpad, NT* __restrict__ node_of_row,
+                                                    int64_t rs, int64_t cs, NT* __restrict__ node_of_row,
                                                     const int32_t* __restrict__ split_feat,
                                                     const int32_t* __restrict__ split_bin,
                                                     const int32_t* __restrict__ left_child,
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ 
         const bool cat = f & HM_TREE_CAT;
         const bool dl = f & HM_TREE_DLEFT;
         f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
-        const int b = bins[r * dpad + f];
+        const int b = bins[r * rs + f * cs];
         const int sb = split_bin[nd];
         const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
         node_of_row[r] = (NT)(go_left ? left_child[nd] : right_child[nd]);
@@ -891,7 +894,8 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
 constexpr int ROUTE_U = 4;
 constexpr int ROUTE_BALLOT_KEYS = 16;
 template <typename NT>
-__global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n, int dpad,
+__global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n,
+                                                          int64_t rs, int64_t cs,
                                                           NT* __restrict__ node_of_row,
                                                           const int32_t* __restrict__ split_feat,
                                                           const int32_t* __restrict__ split_bin,
@@ -924,7 +928,7 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
             const int64_t q = q0 + (int64_t)u * blockDim.x;
             const bool cat = f[u] & HM_TREE_CAT;
             const bool dl = f[u] & HM_TREE_DLEFT;
-            const int b = bins[q * dpad + (f[u] & ~(HM_TREE_CAT | HM_TREE_DLEFT))];
+            const int b = bins[q * rs + (int64_t)(f[u] & ~(HM_TREE_CAT | HM_TREE_DLEFT)) * cs];
             const int sb = split_bin[nd[u]];
             const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
             nd[u] = go_left ? left_child[nd[u]] : right_child[nd[u]];
@@ -1124,18 +1128,21 @@ HM_API int hm_quantize(const float* X, int64_t n, int d, int dpad, const float* 
 
 // miss_bin: the bin of missing values (rows there follow the split's HM_TREE_DLEFT flag), or -1.
 // node16: node_of_row is int16 (trees of < 32,767 nodes: half the bytes per routing pass).
-HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, void* node_of_row,
+// col_stride > 0: bins is the feature-major copy [d, col_stride] (dpad unused).
+HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, void* node_of_row,
                          const int32_t* split_feat, const int32_t* split_bin,
                          const int32_t* left_child, const int32_t* right_child, int miss_bin, int node16,
                          hipStream_t stream) {
     if (n <= 0) return 0;
+    if (col_stride > 0 && col_stride < n) return (int)hipErrorInvalidValue;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
+    const int64_t rs = col_stride > 0 ? 1 : dpad, cs = col_stride > 0 ? col_stride : 1;
     if (node16)
-        hipLaunchKernelGGL(route_kernel<int16_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
+        hipLaunchKernelGGL(route_kernel<int16_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, rs, cs,
                            (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
     else
-        hipLaunchKernelGGL(route_kernel<int32_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, dpad,
+        hipLaunchKernelGGL(route_kernel<int32_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, rs, cs,
                            (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
     HM_LAUNCH_RET();
 }
@@ -1189,18 +1196,22 @@ HM_API int hm_partition_count(const int32_t* rows, int64_t m, const void* node_o
 
 // route_count_kernel: route rows 0 .. n-1 one level down and count the small children's rows
 // per (key, block) cell; follow with hm_partition_scatter(rows = NULL, m = n, same grid).
-HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, void* node_of_row, const int32_t* split_feat,
+// col_stride > 0: bins is the feature-major copy [d, col_stride] (see route_kernel).
+HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, void* node_of_row,
+                          const int32_t* split_feat,
                           const int32_t* split_bin, const int32_t* left_child, const int32_t* right_child,
                           int miss_bin, const int16_t* lut, int nb, int nlut, int nkeys, int grid,
                           int64_t* counts, int node16, hipStream_t stream) {
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0 || n <= 0 || n > INT32_MAX) return (int)hipErrorInvalidValue;
+    if (col_stride > 0 && col_stride < n) return (int)hipErrorInvalidValue;
+    const int64_t rs = col_stride > 0 ? 1 : dpad, cs = col_stride > 0 ? col_stride : 1;
     if (node16)
         hipLaunchKernelGGL(route_count_kernel<int16_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
-                           bins, n, dpad, (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child,
+                           bins, n, rs, cs, (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child,
                            miss_bin, lut, nb, nlut, nkeys, counts);
     else
         hipLaunchKernelGGL(route_count_kernel<int32_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
-                           bins, n, dpad, (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child,
+                           bins, n, rs, cs, (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child,
                            miss_bin, lut, nb, nlut, nkeys, counts);
     HM_LAUNCH_RET();
 }

@@ -41,6 +41,7 @@ DLEFT_FLAG = 1 << 29  # missing values go left at this split (HM_TREE_DLEFT)
 HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/hist_sweep.py, profiles/hist_sweep_r1.jsonl
 HIST_WIDE = os.environ.get("HM_HIST_WIDE", "1") == "1"   # all-features single-pass histogram
 ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-child count in one pass
+ROUTE_COLS = os.environ.get("HM_ROUTE_COLS", "1") == "1"    # routing reads a feature-major bins copy
 GBT2 = os.environ.get("HM_GBT2", "1") == "1"    # GBT histograms of (r, w), Newton leaves summed per leaf
 HEAP_TREES = os.environ.get("HM_TREE_HEAP", "1") == "1"   # fixed-shape levels, no per-level host read
 HEAP_MAX_DEPTH = 10
@@ -69,10 +70,21 @@ class Quantized:
     B: int
     cat: torch.Tensor | None = None   # bool [d]: nominal columns (bin = category index)
     missing: bool = False             # bin B-1 holds exactly the NaN values
+    _bins_t: torch.Tensor | None = field(default=None, repr=False)
 
     @property
     def dpad(self) -> int:
         return self.bins.shape[1]
+
+    def route_src(self):
+        """(bins pointer, column stride) for the routing kernels: the feature-major copy
+        [d, n] on a GPU (built once per matrix; a wave's rows then read one 64-B run per distinct
+        split feature instead of their whole 32-B rows), else row-major (stride 0)."""
+        if not (ROUTE_COLS and self.bins.is_cuda):
+            return _native.ptr(self.bins), 0
+        if self._bins_t is None:
+            self._bins_t = self.bins[:, : self.d].t().contiguous()
+        return _native.ptr(self._bins_t), self.bins.shape[0]
 
 
 def quantize(X: torch.Tensor, num_bins: int = 256, sample: int = 200_000, seed: int = 0,
@@ -446,8 +458,9 @@ class HistTreeBuilder:
         counts = torch.empty(n_keys * G, dtype=torch.int64, device=dev)
         p, st = _native.ptr, _native.stream_of(dev)
         n16 = int(node_of_row.dtype == torch.int16)
+        src, cs = q.route_src()
         _native.check(_native.hip().hm_route_count(
-            p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
+            src, C.c_int64(n), q.dpad, C.c_int64(cs), p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
             (q.B - 1) if self.missing else -1, p(lut), nb, lut.numel(), n_keys, G, p(counts), n16, st),
             "hm_route_count")
         incl = torch.cumsum(counts, 0)
@@ -585,8 +598,9 @@ class HistTreeBuilder:
                 if identity_rows and ROUTE_FUSED:
                     rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, L)
                 else:
+                    src, cs = q.route_src()
                     _native.check(_native.hip().hm_route_rows(
-                        p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc),
+                        src, C.c_int64(n), q.dpad, C.c_int64(cs), p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc),
                         p(nbuf.rc), (q.B - 1) if self.missing else -1, int(node_of_row.dtype == torch.int16),
                         _native.stream_of(dev)), "hm_route_rows")
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, L)
@@ -620,8 +634,9 @@ class HistTreeBuilder:
                     base, L = nb, 2 * n_split
                     depth += 1
                     continue
+                src, cs = q.route_src()
                 _native.check(_native.hip().hm_route_rows(
-                    p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
+                    src, C.c_int64(n), q.dpad, C.c_int64(cs), p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
                     (q.B - 1) if self.missing else -1, int(node_of_row.dtype == torch.int16),
                         _native.stream_of(dev)), "hm_route_rows")
                 if n_split <= 8192:
@@ -672,13 +687,14 @@ class HistTreeBuilder:
             lc_all = torch.cat([lc_all, lc])
             rc_all = torch.cat([rc_all, rc])
             p = _native.ptr
-            args = (p(q.bins), C.c_int64(n), q.dpad, p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all),
-                    (q.B - 1) if self.missing else -1)
+            rest = (p(node_of_row), p(sf_all), p(sb_all), p(lc_all), p(rc_all), (q.B - 1) if self.missing else -1)
             if dev.type == "cuda":
-                _native.check(_native.hip().hm_route_rows(*args, int(node_of_row.dtype == torch.int16),
+                src, cs = q.route_src()
+                _native.check(_native.hip().hm_route_rows(src, C.c_int64(n), q.dpad, C.c_int64(cs), *rest,
+                                                          int(node_of_row.dtype == torch.int16),
                                                           _native.stream_of(dev)), "hm_route_rows")
             else:
-                _native.host().hm_route_rows_cpu(*args)
+                _native.host().hm_route_rows_cpu(p(q.bins), C.c_int64(n), q.dpad, *rest)
             # next level: histogram the smaller child of every split, derive the sibling
             left_tot = left_all[li]                                            # [S, NS]
             right_tot = tot[li] - left_tot
@@ -1365,7 +1381,7 @@ _native.register_host("hm_tree_predict_cpu", [_P, _I64, C.c_int] + [_P] * 7 + [C
 _native.register_hip("hm_quantize", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P, _P])
 _native.register_host("hm_quantize_cpu", [_P, _I64, C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_absmax_cols", [_P, _I64, C.c_int, _P, _P])
-_native.register_hip("hm_route_rows", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int, C.c_int, _P])
+_native.register_hip("hm_route_rows", [_P, _I64, C.c_int, _I64] + [_P] * 5 + [C.c_int, C.c_int, _P])
 _native.register_host("hm_route_rows_cpu", [_P, _I64, C.c_int] + [_P] * 5 + [C.c_int])
 _native.register_hip("hm_split_find", [_P] * 10 + [_P])
 _native.register_host("hm_split_find_cpu", [_P] * 10)
@@ -1376,7 +1392,7 @@ _native.register_hip("hm_gbt2_stats", [_P, _P, _P, _I64, _P, _P, _P, _P])
 _native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_leaf_newton", [_P, _P, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling_heap", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
-_native.register_hip("hm_route_count", [_P, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
+_native.register_hip("hm_route_count", [_P, _I64, C.c_int, _I64, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
