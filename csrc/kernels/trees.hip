@@ -853,6 +853,8 @@ __global__ __launch_bounds__(256) void part_count_kernel(const int32_t* __restri
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) counts[(size_t)k * G + blockIdx.x] = s_cnt[k];
 }
 
+constexpr int PART_U = 4;
+constexpr int PART_LUT = 2048;
 template <typename NT>
 __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __restrict__ rows, int64_t m,
                                                            const NT* __restrict__ node_of_row,
@@ -863,11 +865,14 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
                                                            int32_t* __restrict__ out,
                                                            int64_t* __restrict__ seg /* [nkeys+1] */) {
     extern __shared__ int64_t s_pos[];
+    __shared__ int16_t s_lut[PART_LUT];
     const int G = gridDim.x;
+    const int nl = min(nlut, PART_LUT);
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) {
         const size_t c = (size_t)k * G + blockIdx.x;
         s_pos[k] = incl[c] - counts[c];               // first slot of this (key, block) cell
     }
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_lut[i] = lut[i];
     if (blockIdx.x == 0) {
         for (int k = threadIdx.x; k <= nkeys; k += blockDim.x)
             seg[k] = k == 0 ? 0 : incl[(size_t)k * G - 1];
@@ -875,24 +880,43 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
     __syncthreads();
     const int64_t chunk = (m + G - 1) / G;
     const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(m, r0 + chunk);
-    for (int64_t q = r0 + threadIdx.x; q < r1; q += blockDim.x) {
-        const int row = rows ? rows[q] : (int)q;      // rows == NULL: every row, in order
-        const int k = part_key(node_of_row, lut, row, nb, nlut, nkeys);
-        if (k >= 0) {
+    // PART_U rows per thread in flight (the row -> node -> key chain is latency-bound); the lut
+    // in LDS.  The rank within a (key, block) cell is whatever the LDS atomics hand out.
+    for (int64_t q0 = r0 + threadIdx.x; q0 < r1; q0 += (int64_t)blockDim.x * PART_U) {
+        int row[PART_U], nd[PART_U];
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            row[u] = q < r1 ? (rows ? rows[q] : (int)q) : -1;     // rows == NULL: every row, in order
+        }
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) nd[u] = row[u] >= 0 ? (int)node_of_row[row[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const int c = nd[u] - nb;
+            if (row[u] < 0 || nd[u] < 0 || c < 0 || c >= nlut) continue;
+            const int k = c < PART_LUT ? s_lut[c] : lut[c];
+            if (k >= nkeys) continue;
             const int64_t pos = atomicAdd(reinterpret_cast<unsigned long long*>(&s_pos[k]), 1ull);
-            out[pos] = row;
+            out[pos] = row[u];
         }
     }
 }
 
 // A level's routing and the small-children counting of part_count_kernel in one pass, when
-// every row is active (rows 0 .. n-1 in order): each row's bins word, node and lut entry are read
+// every row is active (rows 0 .. n-1 in order): each row's bins byte, node and lut entry are read
 // once, instead of once by route_kernel over all rows and again (with the row index) by
 // part_count_kernel.  Same (key, block) cells as part_count_kernel (same grid and chunking), so
-// part_scatter_kernel (rows = NULL) places the rows identically.  ROUTE_U rows per thread are in
-// flight: the node -> split -> bins -> child loads are a dependent chain per row.
-constexpr int ROUTE_U = 4;
+// part_scatter_kernel (rows = NULL) places the rows identically.
+// The pass is latency-bound, not bandwidth-bound (the root level, 55 MB, took as long as the
+// deepest): per row node -> split -> bins -> child is a dependent chain.  So the split tables
+// of the level's nodes [lo, lo + ROUTE_TAB) and the lut sit in LDS (two of the four dependent
+// loads become LDS reads) and ROUTE_U rows per thread are in flight.  Node ids below lo are
+// leaves of earlier levels (their rows stay); ids in [lo + ROUTE_TAB, nb) read global memory.
+constexpr int ROUTE_U = 8;
 constexpr int ROUTE_BALLOT_KEYS = 16;
+constexpr int ROUTE_TAB = 1024;
+constexpr int ROUTE_LUT = 2048;
 template <typename NT>
 __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n,
                                                           int64_t rs, int64_t cs,
@@ -902,10 +926,17 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
                                                           const int32_t* __restrict__ left_child,
                                                           const int32_t* __restrict__ right_child, int miss_bin,
                                                           const int16_t* __restrict__ lut, int nb, int nlut,
-                                                          int nkeys, int64_t* __restrict__ counts) {
+                                                          int nkeys, int64_t* __restrict__ counts, int lo) {
     extern __shared__ int s_cnt[];
+    __shared__ int4 s_tab[ROUTE_TAB];          // {split_feat, split_bin, left, right} of node lo + i
+    __shared__ int16_t s_lut[ROUTE_LUT];
     const int G = gridDim.x;
+    const int ntab = max(0, min(ROUTE_TAB, nb - lo));
+    const int nl = min(nlut, ROUTE_LUT);
     for (int k = threadIdx.x; k < nkeys; k += blockDim.x) s_cnt[k] = 0;
+    for (int i = threadIdx.x; i < ntab; i += blockDim.x)
+        s_tab[i] = make_int4(split_feat[lo + i], split_bin[lo + i], left_child[lo + i], right_child[lo + i]);
+    for (int i = threadIdx.x; i < nl; i += blockDim.x) s_lut[i] = lut[i];
     __syncthreads();
     const int64_t chunk = (n + G - 1) / G;
     const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
@@ -914,24 +945,34 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
     for (int q = 0; q < ROUTE_BALLOT_KEYS; ++q) wcnt[q] = 0;
     // every wave runs the same trip count (ballots need the whole wave): the bound is the block's
     for (int64_t q0 = r0 + threadIdx.x; q0 - threadIdx.x < r1; q0 += (int64_t)blockDim.x * ROUTE_U) {
-        int nd[ROUTE_U], f[ROUTE_U];
+        int nd[ROUTE_U];
+        int4 t[ROUTE_U];
+        int b[ROUTE_U];
 #pragma unroll
         for (int u = 0; u < ROUTE_U; ++u) {
             const int64_t q = q0 + (int64_t)u * blockDim.x;
             nd[u] = q < r1 ? node_of_row[q] : -1;
         }
 #pragma unroll
-        for (int u = 0; u < ROUTE_U; ++u) f[u] = nd[u] >= 0 ? split_feat[nd[u]] : -1;
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int i = nd[u] - lo;
+            if (nd[u] < lo) t[u] = make_int4(-1, 0, 0, 0);              // -1 or an earlier leaf
+            else if (i < ntab) t[u] = s_tab[i];
+            else t[u] = make_int4(split_feat[nd[u]], split_bin[nd[u]], left_child[nd[u]], right_child[nd[u]]);
+        }
 #pragma unroll
         for (int u = 0; u < ROUTE_U; ++u) {
-            if (f[u] < 0) continue;
             const int64_t q = q0 + (int64_t)u * blockDim.x;
-            const bool cat = f[u] & HM_TREE_CAT;
-            const bool dl = f[u] & HM_TREE_DLEFT;
-            const int b = bins[q * rs + (int64_t)(f[u] & ~(HM_TREE_CAT | HM_TREE_DLEFT)) * cs];
-            const int sb = split_bin[nd[u]];
-            const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
-            nd[u] = go_left ? left_child[nd[u]] : right_child[nd[u]];
+            b[u] = t[u].x >= 0 ? bins[q * rs + (int64_t)(t[u].x & ~(HM_TREE_CAT | HM_TREE_DLEFT)) * cs] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            if (t[u].x < 0) continue;
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            const bool cat = t[u].x & HM_TREE_CAT;
+            const bool dl = t[u].x & HM_TREE_DLEFT;
+            const bool go_left = b[u] == miss_bin ? dl : (cat ? b[u] == t[u].y : b[u] <= t[u].y);
+            nd[u] = go_left ? t[u].z : t[u].w;
             node_of_row[q] = (NT)nd[u];
         }
 #pragma unroll
@@ -939,7 +980,7 @@ __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restr
             const int c = nd[u] - nb;
             int k = -1;
             if (nd[u] >= 0 && c >= 0 && c < nlut) {
-                k = lut[c];
+                k = c < ROUTE_LUT ? s_lut[c] : lut[c];
                 if (k >= nkeys) k = -1;
             }
             if (nkeys <= ROUTE_BALLOT_KEYS) {
@@ -1197,22 +1238,23 @@ HM_API int hm_partition_count(const int32_t* rows, int64_t m, const void* node_o
 // route_count_kernel: route rows 0 .. n-1 one level down and count the small children's rows
 // per (key, block) cell; follow with hm_partition_scatter(rows = NULL, m = n, same grid).
 // col_stride > 0: bins is the feature-major copy [d, col_stride] (see route_kernel).
-HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, void* node_of_row,
-                          const int32_t* split_feat,
+HM_API int hm_route_count(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, int lo,
+                          void* node_of_row, const int32_t* split_feat,
                           const int32_t* split_bin, const int32_t* left_child, const int32_t* right_child,
                           int miss_bin, const int16_t* lut, int nb, int nlut, int nkeys, int grid,
                           int64_t* counts, int node16, hipStream_t stream) {
     if (nkeys <= 0 || nkeys > 8192 || grid <= 0 || n <= 0 || n > INT32_MAX) return (int)hipErrorInvalidValue;
     if (col_stride > 0 && col_stride < n) return (int)hipErrorInvalidValue;
+    if (lo < 0 || lo > nb) return (int)hipErrorInvalidValue;
     const int64_t rs = col_stride > 0 ? 1 : dpad, cs = col_stride > 0 ? col_stride : 1;
     if (node16)
         hipLaunchKernelGGL(route_count_kernel<int16_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
                            bins, n, rs, cs, (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child,
-                           miss_bin, lut, nb, nlut, nkeys, counts);
+                           miss_bin, lut, nb, nlut, nkeys, counts, lo);
     else
         hipLaunchKernelGGL(route_count_kernel<int32_t>, dim3(grid), dim3(256), (size_t)nkeys * sizeof(int), stream,
                            bins, n, rs, cs, (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child,
-                           miss_bin, lut, nb, nlut, nkeys, counts);
+                           miss_bin, lut, nb, nlut, nkeys, counts, lo);
     HM_LAUNCH_RET();
 }
 

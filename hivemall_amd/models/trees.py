@@ -42,6 +42,8 @@ HIST_BLOCKS = 256    # histogram grid (blocks per feature group); benchmarks/his
 HIST_WIDE = os.environ.get("HM_HIST_WIDE", "1") == "1"   # all-features single-pass histogram
 ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-child count in one pass
 ROUTE_COLS = os.environ.get("HM_ROUTE_COLS", "1") == "1"    # routing reads a feature-major bins copy
+# heap trees: the last level's leaf statistics from the split search, not from histograms
+LAST_FROM_SPLITS = os.environ.get("HM_TREE_LAST_FROM_SPLITS", "1") == "1"
 GBT2 = os.environ.get("HM_GBT2", "1") == "1"    # GBT histograms of (r, w), Newton leaves summed per leaf
 HEAP_TREES = os.environ.get("HM_TREE_HEAP", "1") == "1"   # fixed-shape levels, no per-level host read
 HEAP_MAX_DEPTH = 10
@@ -449,9 +451,10 @@ class HistTreeBuilder:
                                                          p(seg), n16, st), "hm_partition_scatter")
         return rows, seg
 
-    def _route_partition_gpu(self, n: int, node_of_row, nbuf: "_NodeBuf", nb: int, lut, n_keys: int):
+    def _route_partition_gpu(self, n: int, node_of_row, nbuf: "_NodeBuf", nb: int, lut, n_keys: int, lo: int):
         """Every row active (rows 0 .. n-1): route the level and count the small children in one
-        pass (hm_route_count), then place them (hm_partition_scatter without a row list)."""
+        pass (hm_route_count), then place them (hm_partition_scatter without a row list).
+        Nodes [lo, nb) are the level's (lower ids: leaves of earlier levels)."""
         q = self.q
         dev = node_of_row.device
         G = int(max(1, min(1024, (n + 4095) // 4096)))
@@ -460,7 +463,7 @@ class HistTreeBuilder:
         n16 = int(node_of_row.dtype == torch.int16)
         src, cs = q.route_src()
         _native.check(_native.hip().hm_route_count(
-            src, C.c_int64(n), q.dpad, C.c_int64(cs), p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
+            src, C.c_int64(n), q.dpad, C.c_int64(cs), lo, p(node_of_row), p(nbuf.sf), p(nbuf.sb), p(nbuf.lc), p(nbuf.rc),
             (q.B - 1) if self.missing else -1, p(lut), nb, lut.numel(), n_keys, G, p(counts), n16, st),
             "hm_route_count")
         incl = torch.cumsum(counts, 0)
@@ -595,8 +598,27 @@ class HistTreeBuilder:
                 nb = base + L
                 sr, lut = self._level_finalize(gain, bf, braw, left_all, tot, base, nb, edges, nbuf, imp, heap=True)
                 p = _native.ptr
+                if LAST_FROM_SPLITS and depth + 1 >= self.max_depth:
+                    # the children are leaves: route the rows, and take the children's statistics
+                    # from the split search (left, total - left) instead of histogramming them
+                    # (no partition, histogram or sibling pass for the last level)
+                    src, cs = q.route_src()
+                    _native.check(_native.hip().hm_route_rows(
+                        src, C.c_int64(n), q.dpad, C.c_int64(cs), p(node_of_row), p(nbuf.sf), p(nbuf.sb),
+                        p(nbuf.lc), p(nbuf.rc), (q.B - 1) if self.missing else -1,
+                        int(node_of_row.dtype == torch.int16), _native.stream_of(dev)), "hm_route_rows")
+                    nbuf.ensure(nb + 2 * L)
+                    cs_ = torch.stack([left_all, tot - left_all], 1).reshape(2 * L, NS)
+                    nbuf.vals[nb:nb + 2 * L] = self._leaf_values(cs_)
+                    nbuf.sf[nb:nb + 2 * L] = -1
+                    nbuf.thr[nb:nb + 2 * L] = math.inf
+                    nbuf.lc[nb:nb + 2 * L] = -1
+                    nbuf.rc[nb:nb + 2 * L] = -1
+                    base, L = nb, 2 * L
+                    depth += 1
+                    break
                 if identity_rows and ROUTE_FUSED:
-                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, L)
+                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, L, base)
                 else:
                     src, cs = q.route_src()
                     _native.check(_native.hip().hm_route_rows(
@@ -624,7 +646,7 @@ class HistTreeBuilder:
                     break
                 p = _native.ptr
                 if identity_rows and n_split <= 8192 and ROUTE_FUSED:
-                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, n_split)
+                    rows, seg = self._route_partition_gpu(n, node_of_row, nbuf, nb, lut, n_split, base)
                     Hs = self._hist(rows, seg.contiguous(), n_split, stats, smax)
                     Hn = torch.empty((2 * n_split, d, B, NS), dtype=torch.float32, device=dev)
                     _native.check(_native.hip().hm_hist_sibling(
@@ -1392,7 +1414,7 @@ _native.register_hip("hm_gbt2_stats", [_P, _P, _P, _I64, _P, _P, _P, _P])
 _native.register_hip("hm_leaf_sums", [_P, _P, _P, _I64, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_leaf_newton", [_P, _P, C.c_int, _P, _P])
 _native.register_hip("hm_hist_sibling_heap", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
-_native.register_hip("hm_route_count", [_P, _I64, C.c_int, _I64, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
+_native.register_hip("hm_route_count", [_P, _I64, C.c_int, _I64, C.c_int, _P, _P, _P, _P, _P, C.c_int, _P, C.c_int, C.c_int,
                                         C.c_int, C.c_int, _P, C.c_int, _P])
 _native.register_hip("hm_hist_sibling", [_P, _P, _P, _P, _I64, C.c_int, _P, _P])
 _native.register_hip("hm_gbt_stats", [_P, _P, _P, _I64, _P, _P, _P])
