@@ -31,10 +31,17 @@ def main():
         print(json.dumps({"ll": one(sys.argv[2], int(sys.argv[3]))}), flush=True)
         return
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 500000
-    grids = [int(g) for g in sys.argv[2:]] or [0, 256, 1024, 2048]
+    # each argument: a ramp grid for all n rows ("0": none), or "vV:R" = kernel variant V for the
+    # first R rows at the default grid
+    grids = sys.argv[2:] or ["0", "256", "1024", "2048"]
     seq = one("cpu", n)
     for g in grids:
-        env = dict(os.environ, HM_FFM_RAMP_ROWS=str(n if g else 0), HM_FFM_RAMP_GRID=str(g or 1))
+        if g.startswith("v"):
+            v, r = g[1:].split(":")
+            env = dict(os.environ, HM_FFM_RAMP_ROWS=r, HM_FFM_RAMP_VARIANT=v)
+        else:
+            g = int(g)
+            env = dict(os.environ, HM_FFM_RAMP_ROWS=str(n if g else 0), HM_FFM_RAMP_GRID=str(g or 1))
         r = subprocess.run([sys.executable, __file__, "--one", "cuda", str(n)], env=env, capture_output=True,
                            text=True, timeout=600)
         ll = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["ll"]

@@ -953,7 +953,7 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS, typename OT, int TPB = 256>
+template <int NS, typename OT, int TPB = 256, int ATOM = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1152,13 +1152,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 fg[j] = gs;
                 fo[j] = ov;
                 fwd |= 1u << j;
+                if (ATOM) {
+                    // concurrent rows' updates of one slot all land (no read-modify-write race)
+                    if (live >> j & 1u) {
+                        float* vp = reinterpret_cast<float*>(vb + ov);
+                        const f2 e0 = rr * d0, e1 = rr * d1;
+                        atomicAdd(vp + 0, e0.x);
+                        atomicAdd(vp + 1, e0.y);
+                        atomicAdd(vp + 2, e1.x);
+                        atomicAdd(vp + 3, e1.y);
+                        atomicAdd(reinterpret_cast<float*>(gb + og), gs - cg[j]);
+                    }
+                    continue;
+                }
                 *reinterpret_cast<float4*>(vb + ov) = fv[j];
                 *reinterpret_cast<float*>(gb + og) = gs;
             }
             // the row's features' pad slots and block tails (never read): zeros, so every line a
             // row touches is written whole; spread over all threads (one wave doing them all
             // was the last to reach the barrier)
-            {
+            if (!ATOM) {
                 const int npad = P.vpad - P.num_fields;
                 const int per = 2 * npad + P.tail16;
                 for (int q = tid; q < F * per; q += TPB) {
@@ -1179,8 +1192,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[mi] = z1;
-                    wn[mi] = n1;
+                    if (ATOM) {
+                        atomicAdd(wz + mi, z1 - lz);
+                        atomicAdd(wn + mi, g * g);
+                    } else {
+                        wz[mi] = z1;
+                        wn[mi] = n1;
+                    }
                     w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
@@ -1502,6 +1520,9 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
 #define HM_P32(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 1>), dim3(blocks), \
+                                                  dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                  bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
@@ -1590,7 +1611,10 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 //             separate [.][.][Kp] tables.
 // variant (A/B): 0 = auto (per-slot: the sg12 / sg32 pipelines; per-element bf16:
 // ffm_pipe_kernel, fp32: ffm_lean_kernel), 1 = the generic ffm_row_kernel, 2 = ffm_lean_kernel
-// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G).  Measured and removed: 512-thread sg32
+// for bf16, 3 = ffm_pipe_kernel for fp32 (per-element G), 6 = ffm_pipe_sg32_kernel with every
+// slot update added by float atomics (no lost update; the learner's early-training ramp,
+// models/ffm.py RAMP_*; G-only atomics were measured as variant 7 and removed: the full gap at
+// 12 M rows/s, profiles/r4/ffm_g_atomic_bench_ab.log).  Measured and removed: 512-thread sg32
 // blocks (75.7-76.1 vs 75.6 M rows/s, profiles/r4/ffm_512_thread_ab.log); a paired-slot sg32
 // kernel holding each (a, b) / (b, a) slot pair in one thread's registers instead of a transposed
 // LDS image (4 rows in flight per CU instead of 2): 58.1-58.4 vs 74.9-75.5 M rows/s — the (b, a)

@@ -30,6 +30,7 @@ import numpy as np
 import pandas as pd
 import torch
 
+from ..ops import ffm as _ffm_ops
 from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
 from ..ops.touched import mark_touched
 from ..utils.features import CSR, parse_ffm_rows
@@ -72,9 +73,18 @@ def csr_to_ffm_batch(csr: CSR, y: np.ndarray | None, width: int | None = None) -
 # (plain mean) +5.3e-3, 0.5 +1.5e-3, 0.75 +2.8e-4, 1.0 -6e-4.
 DP_LR_POWER = 0.75
 
-# early-training concurrency ramp of the GPU kernel (train_batch)
-RAMP_ROWS = int(os.environ.get("HM_FFM_RAMP_ROWS", "0"))
+# Early-training ramp of the GPU kernel (train_batch).  In the first rows of a run every row
+# moves the same hot (feature, field) slots, and the Hogwild kernel's concurrent read-modify-
+# write of a slot keeps one of the racing rows' updates: held-out logloss after 500 K rows is
+# 0.0195 above the sequential engine, 0.0107 even on 8 blocks, 0 on one
+# (profiles/r4/ffm_early_grid_curve.jsonl).  Kernel variant 6 (fp32 state) adds every slot's
+# update with float atomics instead (4 M rows/s: the hot addresses serialise): over the first
+# 2^18 rows it takes the gap at 500 K rows to 0.0026 and at 2 M rows from 0.0069 to 0.0031
+# (profiles/r4/ffm_early_ramp_atomic*.jsonl).  HM_FFM_RAMP_VARIANT=-1 runs the ramp rows on
+# HM_FFM_RAMP_GRID blocks of the default kernel instead (0.017 at 256 blocks).
+RAMP_ROWS = int(os.environ.get("HM_FFM_RAMP_ROWS", str(1 << 18)))
 RAMP_GRID = int(os.environ.get("HM_FFM_RAMP_GRID", "1024"))
+RAMP_VARIANT = int(os.environ.get("HM_FFM_RAMP_VARIANT", "6"))   # kernel variant of the ramp rows
 
 
 def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
@@ -228,13 +238,19 @@ class FFMTrainer(Learner):
             s = min(b.n, k * bs)
             sub = b.slice(s, min(b.n, s + bs))
             lb = None if loss_buf is None else loss_buf[s:s + sub.n]
-            if sub.n:
-                # the first RAMP_ROWS rows of a learner run on RAMP_GRID blocks (fewer rows in
-                # flight) unless -grid is given: early in training every row moves the same
-                # few parameters and concurrent stale reads cost the most
-                grid = self.grid or (RAMP_GRID if self.rows_seen < RAMP_ROWS else 0)
-                ffm_step(self.state, sub.idx, sub.fld, sub.val, sub.y, self.hyper, train=True,
-                         loss=lb, grid=grid)
+            # the first RAMP_ROWS rows of a learner: the atomic-update kernel (RAMP_VARIANT), or
+            # RAMP_GRID blocks unless -grid is given — early in training every row moves the same
+            # few parameters and concurrent read-modify-writes lose the most
+            cut = min(sub.n, max(0, RAMP_ROWS - self.rows_seen))
+            for r0, r1, ramp in ((0, cut, True), (cut, sub.n, False)):
+                if r1 <= r0:
+                    continue
+                part = sub if (r0, r1) == (0, sub.n) else sub.slice(r0, r1)
+                grid = self.grid or (RAMP_GRID if ramp and RAMP_VARIANT < 0 else 0)
+                ffm_step(self.state, part.idx, part.fld, part.val, part.y, self.hyper, train=True,
+                         loss=None if lb is None else lb[r0:r1], grid=grid,
+                         # (an explicit HM_FFM_VARIANT selects the kernel for every row)
+                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:

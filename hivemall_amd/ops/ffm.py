@@ -137,7 +137,7 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
              y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
              pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
-             grid: int = 0) -> None:
+             grid: int = 0, variant: int | None = None) -> None:
     """One fused pass over a padded-ELL batch.
 
     state: dict with V, G ([NF, NFLD, Kp] f32 or bf16; either two contiguous tables or the two
@@ -200,7 +200,8 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     ip = np.array([B, F, NF, NFLD, Kp, int(hyper.classification), int(train), int(hyper.use_linear),
                    int(hyper.use_bias), int(hyper.norm), int(grid),
                    int((not packed) if hyper.reload is None else hyper.reload), int(bf16),
-                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed), _VARIANT,
+                   (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
+                   _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
                    G.stride(1) if slot_g else 0],
                   dtype=np.int32)

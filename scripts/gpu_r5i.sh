@@ -1,0 +1,16 @@
+#!/bin/bash
+# Full GPU suite, smoke, 1-GPU bench after the tree routing changes and the FFM atomic ramp;
+# RandomForest kernel trace.
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r5i
+mkdir -p $O
+export HM_NO_AUTOBUILD=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || true
+tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1
+tail -1 $O/bench.log | cut -c1-200
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_rf -o rf -- \
+  python3 benchmarks/bench_configs.py rf > $O/prof_rf.log 2>&1

@@ -262,31 +262,38 @@ def test_ffm_gpu_global_bias_loses_no_updates():
 @pytest.mark.gpu
 def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
     """Full-chip Hogwild vs the sequential engine at 500 K rows (an early-training regime, where
-    concurrent stale reads cost the most): the generic kernel (no lookahead, ~1,000 rows in
-    flight) measured 0.0117, the pipelined default (one more row per block read before its
-    predecessor's update lands) 0.0221 (profiles/ffm_r3/hogwild_probe.log); at the bench's
-    12.6 M rows the gap is ~1e-3 (profiles/ffm_parity_bench_scale.log).  Bounds = measurement +
-    margin."""
+    concurrent read-modify-writes of the hot slots lose the most): the generic kernel (no
+    lookahead, ~1,000 rows in flight) measured 0.0117, the pipelined kernel 0.0195-0.0221
+    (profiles/ffm_r3/hogwild_probe.log, profiles/r4/ffm_early_grid_curve.jsonl); the learner's
+    default atomic-update ramp over the first 2^18 rows 0.0026.  At the bench's 12.6 M rows the
+    gap is ~1e-3 (profiles/ffm_parity_bench_scale.log).  Bounds = measurement + margin."""
+    from hivemall_amd.models import ffm as ffm_model
     from hivemall_amd.ops import ffm as ffm_op
 
     idx, y = criteo_like(500000, hash_bits=20, seed=5)
     eidx, ey = criteo_like(100000, hash_bits=20, seed=99)
     yy = (ey > 0).float()
     res = {}
-    old = ffm_op._VARIANT
+    old = ffm_op._VARIANT, ffm_model.RAMP_ROWS
     try:
-        for dev, v in (("cpu", 0), ("cuda", 1), ("cuda", 0)):
+        # (device, kernel variant, early-training ramp rows)
+        for dev, v, ramp in (("cpu", 0, 0), ("cuda", 1, 0), ("cuda", 0, 0), ("cuda", 0, 1 << 18)):
             ffm_op._VARIANT = v
+            ffm_model.RAMP_ROWS = ramp
             t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 20 -seed 1",
                            device=dev)
             t.fit(batch=FFMBatch(idx, None, None, y).to(dev))
             ffm_op._VARIANT = 0
             p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
-            res[(dev, v)] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+            res[(dev, v, ramp)] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
     finally:
-        ffm_op._VARIANT = old
-    assert abs(res[("cpu", 0)] - res[("cuda", 1)]) < 0.016, res
-    assert abs(res[("cpu", 0)] - res[("cuda", 0)]) < 0.026, res
+        ffm_op._VARIANT, ffm_model.RAMP_ROWS = old
+    seq = res[("cpu", 0, 0)]
+    assert abs(seq - res[("cuda", 1, 0)]) < 0.016, res
+    assert abs(seq - res[("cuda", 0, 0)]) < 0.026, res
+    # the learner's default: the first 2^18 rows through the atomic-update kernel (measured
+    # 0.0026, profiles/r4/ffm_early_ramp_atomic.jsonl)
+    assert abs(seq - res[("cuda", 0, 1 << 18)]) < 0.006, res
 
 
 # Held-out logloss of the sequential C++ engine (per-slot AdaGrad, fp32) on bench.py's exact
