@@ -335,6 +335,35 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ l
 }
 
 // Leaf values of the nodes that are leaves (split_feat < 0): sum r / sum h (0 when sum h ~ 0).
+// Bootstrap multiplicities (RandomForest bagging): the m draws with replacement over n rows are
+// split into K chunks of c rows by a multinomial drawn on the host (exact: the chunk counts of m
+// uniform draws), then block k draws its chunk's cnt[k] rows uniformly with a counter hash of
+// (seed, k, j) and counts them in an LDS histogram.  Replaces torch.bincount over m random ids
+// (450 µs for 11 M: global atomics onto random addresses) with LDS atomics.
+constexpr int BOOT_CHUNK = 12288;
+__global__ __launch_bounds__(1024) void bootstrap_counts_kernel(const int64_t* __restrict__ cnt, int64_t n, int c,
+                                                                uint64_t seed, float* __restrict__ out) {
+    __shared__ int s_h[BOOT_CHUNK];
+    const int k = blockIdx.x;
+    const int64_t r0 = (int64_t)k * c;
+    const int len = (int)min((int64_t)c, n - r0);
+    for (int i = threadIdx.x; i < len; i += blockDim.x) s_h[i] = 0;
+    __syncthreads();
+    const int64_t m = cnt[k];
+    const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
+    for (int64_t j = threadIdx.x; j < m; j += blockDim.x) {
+        // splitmix-style mix of (seed, chunk, draw)
+        uint64_t z = ((uint64_t)(s0 ^ (uint32_t)k * 0x9E3779B9u) << 32 | (uint32_t)j) + (uint64_t)s1 * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        const int i = (int)(((z >> 32) * (uint64_t)len) >> 32);
+        atomicAdd(&s_h[i], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < len; i += blockDim.x) out[r0 + i] = (float)s_h[i];
+}
+
 __global__ __launch_bounds__(256) void leaf_newton_kernel(const float* __restrict__ sums, const int32_t* __restrict__ sf,
                                                           int T, float* __restrict__ vals) {
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -425,26 +454,55 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 // Bin of (row r, feature f) at bins[r * rs + f * cs]: row-major (rs = dpad, cs = 1) or the
 // feature-major copy (rs = 1, cs = n), where a wave's rows read one 64-B run per distinct split
 // feature instead of 64 whole 32-B rows.
+// Latency-bound like route_count_kernel below (node -> split -> bins -> child per row): the split
+// tables of nodes [lo, lo + ROUTE_TAB) in LDS and ROUTE_U rows per thread in flight; node ids
+// below lo are leaves of earlier levels (or -1) and keep their id.
+constexpr int ROUTE_U = 8;
+constexpr int ROUTE_TAB = 1024;
 template <typename NT>
 __global__ __launch_bounds__(256) void route_kernel(const uint8_t* __restrict__ bins, int64_t n,
                                                     int64_t rs, int64_t cs, NT* __restrict__ node_of_row,
                                                     const int32_t* __restrict__ split_feat,
                                                     const int32_t* __restrict__ split_bin,
                                                     const int32_t* __restrict__ left_child,
-                                                    const int32_t* __restrict__ right_child, int miss_bin) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
-         r += (int64_t)gridDim.x * blockDim.x) {
-        const int nd = node_of_row[r];
-        if (nd < 0) continue;
-        int f = split_feat[nd];
-        if (f < 0) continue;
-        const bool cat = f & HM_TREE_CAT;
-        const bool dl = f & HM_TREE_DLEFT;
-        f &= ~(HM_TREE_CAT | HM_TREE_DLEFT);
-        const int b = bins[r * rs + f * cs];
-        const int sb = split_bin[nd];
-        const bool go_left = b == miss_bin ? dl : (cat ? b == sb : b <= sb);
-        node_of_row[r] = (NT)(go_left ? left_child[nd] : right_child[nd]);
+                                                    const int32_t* __restrict__ right_child, int miss_bin,
+                                                    int lo, int hi) {
+    __shared__ int4 s_tab[ROUTE_TAB];          // {split_feat, split_bin, left, right} of node lo + i
+    const int ntab = max(0, min(ROUTE_TAB, hi - lo));
+    for (int i = threadIdx.x; i < ntab; i += blockDim.x)
+        s_tab[i] = make_int4(split_feat[lo + i], split_bin[lo + i], left_child[lo + i], right_child[lo + i]);
+    __syncthreads();
+    const int G = gridDim.x;
+    const int64_t chunk = (n + G - 1) / G;
+    const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
+    for (int64_t q0 = r0 + threadIdx.x; q0 < r1; q0 += (int64_t)blockDim.x * ROUTE_U) {
+        int nd[ROUTE_U], b[ROUTE_U];
+        int4 t[ROUTE_U];
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            nd[u] = q < r1 ? (int)node_of_row[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int i = nd[u] - lo;
+            if (nd[u] < lo) t[u] = make_int4(-1, 0, 0, 0);
+            else if (i < ntab) t[u] = s_tab[i];
+            else t[u] = make_int4(split_feat[nd[u]], split_bin[nd[u]], left_child[nd[u]], right_child[nd[u]]);
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * blockDim.x;
+            b[u] = t[u].x >= 0 ? bins[q * rs + (int64_t)(t[u].x & ~(HM_TREE_CAT | HM_TREE_DLEFT)) * cs] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < ROUTE_U; ++u) {
+            if (t[u].x < 0) continue;
+            const bool cat = t[u].x & HM_TREE_CAT;
+            const bool dl = t[u].x & HM_TREE_DLEFT;
+            const bool go_left = b[u] == miss_bin ? dl : (cat ? b[u] == t[u].y : b[u] <= t[u].y);
+            node_of_row[q0 + (int64_t)u * blockDim.x] = (NT)(go_left ? t[u].z : t[u].w);
+        }
     }
 }
 
@@ -913,9 +971,7 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(const int32_t* __rest
 // of the level's nodes [lo, lo + ROUTE_TAB) and the lut sit in LDS (two of the four dependent
 // loads become LDS reads) and ROUTE_U rows per thread are in flight.  Node ids below lo are
 // leaves of earlier levels (their rows stay); ids in [lo + ROUTE_TAB, nb) read global memory.
-constexpr int ROUTE_U = 8;
 constexpr int ROUTE_BALLOT_KEYS = 16;
-constexpr int ROUTE_TAB = 1024;
 constexpr int ROUTE_LUT = 2048;
 template <typename NT>
 __global__ __launch_bounds__(256) void route_count_kernel(const uint8_t* __restrict__ bins, int64_t n,
@@ -1170,21 +1226,24 @@ HM_API int hm_quantize(const float* X, int64_t n, int d, int dpad, const float* 
 // miss_bin: the bin of missing values (rows there follow the split's HM_TREE_DLEFT flag), or -1.
 // node16: node_of_row is int16 (trees of < 32,767 nodes: half the bytes per routing pass).
 // col_stride > 0: bins is the feature-major copy [d, col_stride] (dpad unused).
-HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, void* node_of_row,
+// [lo, hi): the level's node ids (lower ids are leaves of earlier levels or -1).
+HM_API int hm_route_rows(const uint8_t* bins, int64_t n, int dpad, int64_t col_stride, int lo, int hi,
+                         void* node_of_row,
                          const int32_t* split_feat, const int32_t* split_bin,
                          const int32_t* left_child, const int32_t* right_child, int miss_bin, int node16,
                          hipStream_t stream) {
     if (n <= 0) return 0;
     if (col_stride > 0 && col_stride < n) return (int)hipErrorInvalidValue;
-    int64_t blocks = (n + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
+    if (lo < 0 || hi < lo) return (int)hipErrorInvalidValue;
+    int64_t blocks = (n + 4095) / 4096;
+    if (blocks > 1024) blocks = 1024;
     const int64_t rs = col_stride > 0 ? 1 : dpad, cs = col_stride > 0 ? col_stride : 1;
     if (node16)
         hipLaunchKernelGGL(route_kernel<int16_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, rs, cs,
-                           (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
+                           (int16_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin, lo, hi);
     else
         hipLaunchKernelGGL(route_kernel<int32_t>, dim3((int)blocks), dim3(256), 0, stream, bins, n, rs, cs,
-                           (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin);
+                           (int32_t*)node_of_row, split_feat, split_bin, left_child, right_child, miss_bin, lo, hi);
     HM_LAUNCH_RET();
 }
 
@@ -1348,6 +1407,18 @@ HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int
 }
 
 // vals[k] = sums[k, 0] / sums[k, 1] for the leaves (sf[k] < 0) among nodes 0 .. T-1.
+// out [n] = bootstrap multiplicities; cnt [K] = draws per chunk of `chunk` rows (sum = m),
+// K = ceil(n / chunk), chunk <= 12288.
+HM_API int hm_bootstrap_counts(const int64_t* cnt, int64_t n, int chunk, uint64_t seed, float* out,
+                               hipStream_t stream) {
+    if (n <= 0) return 0;
+    if (chunk <= 0 || chunk > BOOT_CHUNK) return (int)hipErrorInvalidValue;
+    const int64_t K = (n + chunk - 1) / chunk;
+    if (K > INT32_MAX) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bootstrap_counts_kernel, dim3((unsigned)K), dim3(1024), 0, stream, cnt, n, chunk, seed, out);
+    HM_LAUNCH_RET();
+}
+
 HM_API int hm_leaf_newton(const float* sums, const int32_t* sf, int T, float* vals, hipStream_t stream) {
     if (T <= 0) return 0;
     hipLaunchKernelGGL(leaf_newton_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, stream, sums, sf, T, vals);

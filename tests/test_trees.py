@@ -477,3 +477,26 @@ def test_heap_layout_tree_compaction_matches_compact_numbering():
     p.scale = 0.5
     (t3,), = materialize_trees([[p]])
     assert t3.feature == t2.feature and t3.value == [None, [0.5], None, [2.5], [3.0]]
+
+
+@pytest.mark.gpu
+def test_gpu_bootstrap_weights_are_a_multinomial_draw():
+    """RandomForest bagging on the GPU (csrc hm_bootstrap_counts): per-chunk draw counts from an
+    exact multinomial, each chunk's draws counted in LDS.  The multiplicities sum to m, repeat
+    for one seed, differ across seeds, and have the bootstrap's moments (mean rate, P(0) =
+    e^-rate, variance ~ rate)."""
+    from hivemall_amd.models.trees import BOOT_CHUNK, bootstrap_weights
+
+    n = 3 * BOOT_CHUNK + 777
+    for rate in (1.0, 0.5):
+        m = int(round(n * rate))
+        w = [bootstrap_weights(n, rate, torch.Generator(device="cuda").manual_seed(s), "cuda") for s in (5, 5, 6)]
+        assert w[0].dtype == torch.float32 and w[0].shape == (n,)
+        assert int(w[0].sum().item()) == m and torch.equal(w[0], w[1]) and not torch.equal(w[0], w[2])
+        a = w[0].double()
+        assert (a == a.round()).all() and (a >= 0).all()
+        assert abs(a.mean().item() - rate) < 1e-9 + 1.0 / n
+        assert abs((a == 0).double().mean().item() - np.exp(-rate)) < 0.01
+        assert abs(a.var().item() - rate) < 0.05
+        # no chunk boundary artefact: the last (short) chunk has the same mean
+        assert abs(a[-777:].mean().item() - rate) < 0.15
