@@ -293,18 +293,22 @@ __global__ __launch_bounds__(256) void gbt_stats_kernel(const float* __restrict_
     block_absmax_flush<NS>(m, smax);
 }
 
-// Per-node sums {sum r, sum h} of the rows' final nodes (leaf[r] < T), block-private in LDS.
+// Per-node sums {sum r, sum h} of the rows' final nodes (leaf[r] < T), block-private in LDS as
+// 64-bit fixed point (r, h scaled by 2^24; |r| <= 1, h <= 1/4 for the logistic GBT): integer LDS
+// adds instead of ds_add_f32 (~10x slower on gfx950), exact sums within the block.
+constexpr float LEAF_FIX = 16777216.f;
+constexpr int LEAF_BLOCKS = 1024;
 template <typename NT>
 __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ leaf, const float* __restrict__ st2,
                                                         const float* __restrict__ hh, int64_t n, int T,
                                                         float* __restrict__ sums) {
-    extern __shared__ float s_sum[];
+    extern __shared__ unsigned long long s_sum[];
     // one copy of the sums per wave when they fit (copies = 4: a tree's 256 leaves drew most of a
     // wave's 64 adds onto the same few words), folded into copy 0 at the end
     const int copies = 2 * T <= 2048 ? 4 : 1;
-    for (int k = threadIdx.x; k < 2 * T * copies; k += blockDim.x) s_sum[k] = 0.f;
+    for (int k = threadIdx.x; k < 2 * T * copies; k += blockDim.x) s_sum[k] = 0ull;
     __syncthreads();
-    float* my = s_sum + (copies > 1 ? (threadIdx.x >> 6) % copies : 0) * 2 * T;
+    unsigned long long* my = s_sum + (copies > 1 ? (threadIdx.x >> 6) % copies : 0) * 2 * T;
     // LEAF_U rows per thread with every load issued before the first LDS add
     constexpr int LEAF_U = 8;
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
@@ -322,19 +326,18 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ l
 #pragma unroll
         for (int u = 0; u < LEAF_U; ++u) {
             if (l[u] < 0 || l[u] >= T || h[u] == 0.f) continue;
-            atomicAdd(&my[2 * l[u]], g[u]);
-            atomicAdd(&my[2 * l[u] + 1], h[u]);
+            atomicAdd(&my[2 * l[u]], (unsigned long long)llrintf(g[u] * LEAF_FIX));
+            atomicAdd(&my[2 * l[u] + 1], (unsigned long long)llrintf(h[u] * LEAF_FIX));
         }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < 2 * T; k += blockDim.x) {
-        float v = s_sum[k];
+        unsigned long long v = s_sum[k];
         for (int c = 1; c < copies; ++c) v += s_sum[c * 2 * T + k];
-        if (v != 0.f) atomicAdd(sums + k, v);
+        if (v != 0ull) atomicAdd(sums + k, (float)(long long)v * (1.f / LEAF_FIX));
     }
 }
 
-// Leaf values of the nodes that are leaves (split_feat < 0): sum r / sum h (0 when sum h ~ 0).
 // Bootstrap multiplicities (RandomForest bagging): the m draws with replacement over n rows are
 // split into K chunks of c rows by a multinomial drawn on the host (exact: the chunk counts of m
 // uniform draws), then block k draws its chunk's cnt[k] rows uniformly with a counter hash of
@@ -364,6 +367,7 @@ __global__ __launch_bounds__(1024) void bootstrap_counts_kernel(const int64_t* _
     for (int i = threadIdx.x; i < len; i += blockDim.x) out[r0 + i] = (float)s_h[i];
 }
 
+// Leaf values of the nodes that are leaves (split_feat < 0): sum r / sum h (0 when sum h ~ 0).
 __global__ __launch_bounds__(256) void leaf_newton_kernel(const float* __restrict__ sums, const int32_t* __restrict__ sf,
                                                           int T, float* __restrict__ vals) {
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -1394,14 +1398,23 @@ HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int
                         int node16, hipStream_t stream) {
     if (n <= 0) return 0;
     if (T <= 0 || T > 8192) return (int)hipErrorInvalidValue;
-    // at most 256 blocks: every block ends with 2T atomic adds onto the same 2T addresses
+    // every block ends with 2T float atomic adds onto the same 2T addresses; the row loop is
+    // latency-bound, so up to 1,024 blocks (95 -> 55 µs per 11 M rows vs 256 blocks)
     int64_t blocks = (n + 4095) / 4096;
-    if (blocks > 256) blocks = 256;
+    if (blocks > LEAF_BLOCKS) blocks = LEAF_BLOCKS;
+    static bool attr_set = false;     // 64-bit sums of up to 8,192 nodes: 128 KB of LDS
+    if (!attr_set) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int16_t>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int32_t>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
     if (node16)
-        hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float) * (2 * T <= 2048 ? 4 : 1), stream,
+        hipLaunchKernelGGL(leaf_sums_kernel<int16_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(unsigned long long) * (2 * T <= 2048 ? 4 : 1), stream,
                            (const int16_t*)leaf, st2, hh, n, T, sums);
     else
-        hipLaunchKernelGGL(leaf_sums_kernel<int32_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(float) * (2 * T <= 2048 ? 4 : 1), stream,
+        hipLaunchKernelGGL(leaf_sums_kernel<int32_t>, dim3((int)blocks), dim3(256), (size_t)T * 2 * sizeof(unsigned long long) * (2 * T <= 2048 ? 4 : 1), stream,
                            (const int32_t*)leaf, st2, hh, n, T, sums);
     HM_LAUNCH_RET();
 }
