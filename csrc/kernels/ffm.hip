@@ -1168,23 +1168,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 *reinterpret_cast<float4*>(vb + ov) = fv[j];
                 *reinterpret_cast<float*>(gb + og) = gs;
             }
-            // the row's features' pad slots and block tails (never read): zeros, so every line a
-            // row touches is written whole; spread over all threads (one wave doing them all
-            // was the last to reach the barrier)
-            if (!ATOM) {
-                const int npad = P.vpad - P.num_fields;
-                const int per = 2 * npad + P.tail16;
-                for (int q = tid; q < F * per; q += TPB) {
-                    const int a = q / per, kk = q - a * per;
-                    const int i = s_m[cur][a].x;
-                    if (i < 0) continue;
-                    char* vblk = vb + (OT)(uint32_t)i * vfs;
-                    char* gblk = gb + (OT)(uint32_t)i * gfs;
-                    if (kk < npad) *reinterpret_cast<uint4*>(vblk + (P.num_fields + kk) * 16) = make_uint4(0u, 0u, 0u, 0u);
-                    else if (kk < 2 * npad) *reinterpret_cast<float*>(gblk + (P.num_fields + kk - npad) * 4) = 0.f;
-                    else *reinterpret_cast<uint4*>(gblk + P.vpad * 4 + 16 * (kk - 2 * npad)) = make_uint4(0u, 0u, 0u, 0u);
-                }
-            }
+            // (The pad slots and block tails are never read.  Zeroing them so that every line a
+            // row touches is written whole cost 1.5 %: 73.7-74.0 vs 75.0-75.2 M rows/s, same
+            // held-out logloss, profiles/r4/ffm_no_pad_stores_ab.log.)
             if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
                     const float lz = s_lin[cur][1][lane];
@@ -1401,7 +1387,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                                                         pack_sr_hi(o1, rotl32(h, 8), rotl32(h, 24)),
                                                         __float_as_uint(gs)};
             }
-            // pad slots + block tails of the row's features, spread over all threads
+            // pad slots + block tails of the row's features, spread over all threads (here they
+            // pay: without them 117.3-117.6 vs 118.1-118.6 M rows/s, profiles/r4/ffm_no_pad_stores_ab.log;
+            // the fp32 kernel is faster without)
             {
                 const int npad = P.vpad - P.num_fields;
                 const int per = npad + P.tail16;
