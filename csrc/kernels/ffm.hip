@@ -1170,7 +1170,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             }
             // (The pad slots and block tails are never read.  Zeroing them so that every line a
             // row touches is written whole cost 1.5 %: 73.7-74.0 vs 75.0-75.2 M rows/s, same
-            // held-out logloss, profiles/r4/ffm_no_pad_stores_ab.log.)
+            // held-out logloss, profiles/r4/ffm_no_pad_stores_ab.log.  Skipping the DMA and the
+            // store of the diagonal / dead slots too was slower: 72.4-72.7 vs 74.9-75.5 M,
+            // profiles/r4/ffm_skip_diagonal_ab.log.)
             if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
                     const float lz = s_lin[cur][1][lane];
