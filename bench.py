@@ -25,7 +25,9 @@ At N > 1 every replica steps with eta0 and alpha times N^p (``--dp-lr-power``, d
 (docs/compat.md, benchmarks/dp_sim.py).
 
 Timing: W untimed warmup steps, then barrier + synchronize, K timed steps, synchronize +
-barrier; the max over ranks is reported.  After timing, rank 0 evaluates logloss of the mixed
+barrier; the max over ranks is reported.  With fp32 state the first warmup step runs the
+learner's early-training ramp (``--ramp-rows``, the atomic-update kernel that ``train_ffm`` uses
+for its first 2^18 rows, docs/compat.md); the timed steps always run the default kernel.  After timing, rank 0 evaluates logloss of the mixed
 model on held-out rows and the planted model's logloss (the Bayes floor).
 
 On the GPU the same schedule then runs a second time with the other state precision in the
@@ -55,6 +57,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--ramp-rows", type=int, default=None,
+                    help="fp32 state: the first rows (whole steps, inside the untimed warmup only) run "
+                         "the atomic-update kernel, as the learner does (models/ffm.py RAMP_ROWS; "
+                         "default = the learner's 2^18; 0 = off)")
     ap.add_argument("--batch", type=int, default=262144, help="rows per GPU per step")
     ap.add_argument("--hash-bits", type=int, default=20)
     ap.add_argument("--factors", type=int, default=4)
@@ -200,11 +206,18 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     loss_buf = torch.empty(B, dtype=torch.float32, device=dev) if metrics is not None else None
     step_loss = []
 
+    from hivemall_amd.models import ffm as ffm_model
+
+    ramp_rows = ffm_model.RAMP_ROWS if args.ramp_rows is None else int(args.ramp_rows)
+    ramp_steps = 0
+    if state == "fp32" and dev.type == "cuda" and ramp_rows > 0 and ffm_model.RAMP_VARIANT >= 0:
+        ramp_steps = min(args.warmup, (ramp_rows + B - 1) // B)   # never inside the timed region
+
     def step(i):
         s = (i % nres) * B
         ffm_step(st, idx[s:s + B], None if fld is None else fld[s:s + B],
                  None if val is None else val[s:s + B], y[s:s + B], hyper, train=True,
-                 grid=args.grid, loss=loss_buf)
+                 grid=args.grid, loss=loss_buf, variant=ffm_model.RAMP_VARIANT if i < ramp_steps else None)
         if loss_buf is not None:
             step_loss.append(loss_buf.mean())          # device scalar, read after timing
         if world > 1 and (i + 1) % args.mix_every == 0:
@@ -263,7 +276,7 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     out = {"elapsed_s": elapsed, "ms_per_step": 1000.0 * elapsed / max(1, args.steps),
            "rows_per_s": float(B) * world * args.steps / elapsed, "mixes_timed": mixes_timed,
            "mixed_bytes": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
-           "dp_lr_scale": sc}
+           "dp_lr_scale": sc, "ramp_steps": ramp_steps}
     if os.environ.get("HM_TRACE"):
         # host + device timeline of a few extra steps (outside the timed region)
         from hivemall_amd.prof import host_trace
@@ -396,6 +409,7 @@ def main(argv=None):
                 "mix_overlapped": bool(args.mix_overlap),
                 "mix_wire": main_run["mix_wire"],
                 "dp_lr_scale": round(main_run["dp_lr_scale"], 4),
+                "early_ramp_warmup_steps": main_run["ramp_steps"],
                 "resident_batches": nres,
             },
             "rccl_world": world if ctx.backend == "nccl" else None,

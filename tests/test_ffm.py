@@ -306,10 +306,11 @@ SEQ_BENCH_SCALE_LOGLOSS = 0.46426
 def test_ffm_gpu_bench_scale_parity_pinned():
     """The bench-scale parity record as a test: bench.py --gen-device cpu trains the same
     12.6 M-row stream as the sequential engine's reference run; the held-out logloss of the
-    bf16 (driver's value) and fp32 (reference precision) runs must stay near it.  Measured over
+    bf16 and fp32 (reference precision, the driver's value) runs must stay near it.  Measured over
     4 runs on 2 boxes: bf16 +1.45e-3 .. +1.69e-3 (SURVEY.md bf16 tolerance 3e-3), fp32
-    +8.6e-4 .. +9.5e-4 (fp32 tolerance 1e-3); the fp32 bound carries 2e-4 of run-to-run margin
-    (profiles/ffm_r3/parity_variance.log)."""
+    +8.6e-4 .. +9.5e-4 (profiles/ffm_r3/parity_variance.log); with the learner's early ramp in
+    the warmup (round 4) fp32 +5.9e-4 (profiles/r4/bench_ramp_in_warmup.log) — bound at
+    SURVEY.md's fp32 tolerance 1e-3."""
     import json
     import os
     import subprocess
@@ -323,7 +324,8 @@ def test_ffm_gpu_bench_scale_parity_pinned():
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["rows_trained_per_rank"] == 12582912 and rec["dtype"] == "fp32"
     assert abs(rec["logloss_heldout_bf16"] - SEQ_BENCH_SCALE_LOGLOSS) <= 3e-3, rec["logloss_heldout_bf16"]
-    assert abs(rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS) <= 1.2e-3, rec["logloss_heldout"]
+    assert rec["config"]["early_ramp_warmup_steps"] == 1
+    assert abs(rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS) <= 1.0e-3, rec["logloss_heldout"]
 
 
 def _copy_state(tc, tg, rows=None):
