@@ -1465,8 +1465,26 @@ HM_API int hm_gbt_apply(float* F, int ldf, int k, const float* vals, int ldv, co
 struct LevelParams {
     int L, NS, d, E, crit, n_out, nb, has_cat;
     int heap;   // children at nb + 2l, nb + 2l + 1 for parent l (fixed-shape levels, no host read)
+    int last;   // the children are leaves: write their records too, values from (left, tot - left)
     float lam, alpha, min_gain, min_split;
 };
+
+// Leaf output(s) of statistics S(s), s < NS (models/trees.py _leaf_values).
+template <typename SF>
+__device__ __forceinline__ void leaf_value(const LevelParams& P, SF S, float* v) {
+    if (P.crit <= 1) {
+        float w = 0.f;
+        for (int s = 0; s < P.NS; ++s) w += S(s);
+        for (int s = 0; s < P.NS; ++s) v[s] = w > 0.f ? S(s) / fmaxf(w, 1e-30f) : 1.f / (float)P.NS;
+    } else if (P.crit == 2 || P.crit == 5) {   // gbt2: the mean residual until hm_gbt2_leaf_values
+        v[0] = S(1) > 0.f ? S(0) / fmaxf(S(1), 1e-30f) : 0.f;
+    } else if (P.crit == 4) {
+        const float den = S(1) + P.lam;
+        v[0] = den > 0.f ? -soft_thr(S(0), P.alpha) / fmaxf(den, 1e-30f) : 0.f;
+    } else {
+        v[0] = fabsf(S(1)) > 1e-12f ? S(0) / S(1) : 0.f;
+    }
+}
 
 __device__ __forceinline__ float node_weight(const float* S, int NS, int crit) {
     if (crit <= 1) {                         // gini / entropy: sum of class counts
@@ -1510,18 +1528,22 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
     for (int l = l0; l < l1; ++l) {
         const float* S = tot + (size_t)l * P.NS;
         // leaf value(s) of the node
-        float* v = vals + (size_t)l * P.n_out;
-        if (P.crit <= 1) {
-            const float w = node_weight(S, P.NS, P.crit);
-            for (int s = 0; s < P.NS; ++s) v[s] = w > 0.f ? S[s] / fmaxf(w, 1e-30f) : 1.f / (float)P.NS;
-        } else if (P.crit == 2 || P.crit == 5) {   // gbt2: the mean residual until hm_gbt2_leaf_values
-            v[0] = S[1] > 0.f ? S[0] / fmaxf(S[1], 1e-30f) : 0.f;
-        } else if (P.crit == 4) {
-            const float den = S[1] + P.lam;
-            v[0] = den > 0.f ? -soft_thr(S[0], P.alpha) / fmaxf(den, 1e-30f) : 0.f;
-        } else {
-            v[0] = fabsf(S[1]) > 1e-12f ? S[0] / S[1] : 0.f;
-        }
+        leaf_value(P, [&](int s) { return S[s]; }, vals + (size_t)l * P.n_out);
+        // last level: the children's records (relative to this level's first node, nb - L)
+        auto leaf_child = [&](int c, const float* Lf, bool right) {
+            const int rel = c - P.nb + P.L;
+            if (Lf) {
+                if (right) leaf_value(P, [&](int s) { return S[s] - Lf[s]; }, vals + (size_t)rel * P.n_out);
+                else leaf_value(P, [&](int s) { return Lf[s]; }, vals + (size_t)rel * P.n_out);
+            } else {
+                for (int s = 0; s < P.n_out; ++s) vals[(size_t)rel * P.n_out + s] = 0.f;
+            }
+            feats_out[rel] = -1;
+            thrs_out[rel] = INFINITY;
+            lc_out[rel] = -1;
+            rc_out[rel] = -1;
+            sb_out[rel] = 0;
+        };
         const int bf = feat[l];
         const int br = bins_raw[l];
         const int bb = br & 0xFFFF;
@@ -1535,6 +1557,10 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
                 small_right[l] = 0;
                 lut[2 * l] = (int16_t)32767;
                 lut[2 * l + 1] = (int16_t)32767;
+                if (P.last) {                    // unreachable slots, still valid records
+                    leaf_child(P.nb + 2 * l, nullptr, false);
+                    leaf_child(P.nb + 2 * l + 1, nullptr, true);
+                }
             }
             continue;
         }
@@ -1547,6 +1573,10 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
         const int lc = P.nb + 2 * (P.heap ? l : rank);
         lc_out[l] = lc;
         rc_out[l] = lc + 1;
+        if (P.last) {
+            leaf_child(lc, left + (size_t)l * P.NS, false);
+            leaf_child(lc + 1, left + (size_t)l * P.NS, true);
+        }
         li_out[rank] = l;
         if (fok) atomicAdd(imp + bf, (double)gain[l]);   // split-gain importance
         const float* Lf = left + (size_t)l * P.NS;
@@ -1569,7 +1599,9 @@ __global__ __launch_bounds__(1024) void level_finalize_kernel(
     }
 }
 
-// ip: L, NS, d, E, crit, n_out, nb, has_cat;  fp: lam, alpha, min_gain, min_split.  The per-node
+// ip: L, NS, d, E, crit, n_out, nb, has_cat, heap, last;  fp: lam, alpha, min_gain, min_split.
+// last = 1: the children are leaves and their records are written too, at [L, L + 2 * splits)
+// (heap: [L, 3L)) of the same pointers — the caller sizes them.  The per-node
 // outputs (vals .. sb_out) are written at [0, L) of the pointers given (the caller offsets them to
 // the level's first node id); li_out / small_right / lut are per split; imp [d] += split gains.
 HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* gain, const int32_t* feat,
@@ -1581,6 +1613,7 @@ HM_API int hm_level_finalize(const int32_t* ip, const float* fp, const float* ga
     P.L = ip[0]; P.NS = ip[1]; P.d = ip[2]; P.E = ip[3]; P.crit = ip[4]; P.n_out = ip[5]; P.nb = ip[6];
     P.has_cat = ip[7];
     P.heap = ip[8];
+    P.last = ip[9];
     P.lam = fp[0]; P.alpha = fp[1]; P.min_gain = fp[2]; P.min_split = fp[3];
     if (P.L <= 0 || P.NS <= 0 || (P.crit > 1 && P.NS > 8) || P.E <= 0) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(level_finalize_kernel, dim3(1), dim3(1024), 0, stream, P, gain, feat, bins_raw, left, tot,

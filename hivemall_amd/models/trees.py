@@ -364,17 +364,6 @@ class HistTreeBuilder:
 
     _CRIT = {"gini": 0, "entropy": 1, "variance": 2, "gbt": 3, "xgb": 4, "gbt2": 5}
 
-    def _leaf_level(self, nbuf: "_NodeBuf", nb: int, left: torch.Tensor, tot: torch.Tensor) -> None:
-        """Leaves nb .. nb + 2S - 1 = the children (left, right) of S splits whose left and total
-        statistics [S, NS] the split search returned (no histograms of the last level)."""
-        S, NS = tot.shape
-        nbuf.ensure(nb + 2 * S)
-        nbuf.vals[nb:nb + 2 * S] = self._leaf_values(torch.stack([left, tot - left], 1).reshape(2 * S, NS))
-        nbuf.sf[nb:nb + 2 * S] = -1
-        nbuf.thr[nb:nb + 2 * S] = math.inf
-        nbuf.lc[nb:nb + 2 * S] = -1
-        nbuf.rc[nb:nb + 2 * S] = -1
-
     def _split_find(self, H: torch.Tensor, node_base: int):
         """Best split of every node of the level (csrc hm_split_find: one fused kernel instead
         of ~30 tensor ops over [L, d, B, NS]).  Returns gain [L] (-inf: no valid split), feature
@@ -413,22 +402,24 @@ class HistTreeBuilder:
         return gain, feat, bins, left, tot
 
     def _level_finalize(self, gain, feat, braw, left, tot, base: int, nb: int, edges, buf: "_NodeBuf", imp,
-                        heap: bool = False):
+                        heap: bool = False, last: bool = False):
         """GPU: the level's split decisions and bookkeeping in one kernel (hm_level_finalize),
         written straight into the tree's node arrays at [base, base + L); returns
         (li int64, small_right, lut, n_split) of the splitting nodes.  ``heap``: the children of
         parent l are nodes nb + 2l, nb + 2l + 1 and small_right / lut are indexed by l; returns
-        (small_right [L], lut [2L]) without reading the split count on the host."""
+        (small_right [L], lut [2L]) without reading the split count on the host.  ``last``: the
+        children are leaves and their records (values from the split's left / total statistics)
+        are written by the same kernel at nb .. nb + 2 * splits (heap: nb .. nb + 2L)."""
         L, NS = tot.shape
         dev = tot.device
-        buf.ensure(base + L)
+        buf.ensure(base + (3 * L if last else L))
         li = torch.empty(L, dtype=torch.int64, device=dev)
         sr = torch.empty(L, dtype=torch.uint8, device=dev)
         lut = torch.empty(2 * L, dtype=torch.int16, device=dev)
         nsp = torch.empty(1, dtype=torch.int32, device=dev)
         cat = self._masks[1]
         ip = np.array([L, NS, self.q.d, edges.shape[1], self._CRIT[self.criterion], buf.n_out, nb,
-                       int(cat is not None), int(heap)], dtype=np.int32)
+                       int(cat is not None), int(heap), int(last)], dtype=np.int32)
         fp = np.array([self.lam, self.alpha, self.min_gain, float(self.min_split)], dtype=np.float32)
         p = _native.ptr
         o4, ov = 4 * base, 4 * base * buf.n_out          # byte offsets of node `base`
@@ -454,7 +445,7 @@ class HistTreeBuilder:
         n16 = int(node_of_row.dtype == torch.int16)
         _native.check(_native.hip().hm_partition_count(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
                                                        lut.numel(), n_keys, G, p(counts), n16, st), "hm_partition_count")
-        incl = torch.cumsum(counts, 0)                     # int64
+        incl = torch.cumsum(counts, 0)
         rows = torch.empty(max(1, m), dtype=torch.int32, device=dev)
         seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
         _native.check(_native.hip().hm_partition_scatter(p(act_rows), C.c_int64(m), p(node_of_row), p(lut), nb,
@@ -607,9 +598,11 @@ class HistTreeBuilder:
                 # the host, the next level's kernels queue behind this one's
                 gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
                 nb = base + L
-                sr, lut = self._level_finalize(gain, bf, braw, left_all, tot, base, nb, edges, nbuf, imp, heap=True)
+                last = LAST_FROM_SPLITS and depth + 1 >= self.max_depth
+                sr, lut = self._level_finalize(gain, bf, braw, left_all, tot, base, nb, edges, nbuf, imp, heap=True,
+                                               last=last)
                 p = _native.ptr
-                if LAST_FROM_SPLITS and depth + 1 >= self.max_depth:
+                if last:
                     # the children are leaves: route the rows, and take the children's statistics
                     # from the split search (left, total - left) instead of histogramming them
                     # (no partition, histogram or sibling pass for the last level)
@@ -618,7 +611,6 @@ class HistTreeBuilder:
                         src, C.c_int64(n), q.dpad, C.c_int64(cs), base, base + L, p(node_of_row), p(nbuf.sf), p(nbuf.sb),
                         p(nbuf.lc), p(nbuf.rc), (q.B - 1) if self.missing else -1,
                         int(node_of_row.dtype == torch.int16), _native.stream_of(dev)), "hm_route_rows")
-                    self._leaf_level(nbuf, nb, left_all, tot)
                     base, L = nb, 2 * L
                     depth += 1
                     break
@@ -645,12 +637,13 @@ class HistTreeBuilder:
             if fused:
                 gain, bf, braw, left_all, tot = self._split_find_raw(H, base)
                 nb = base + L
+                last = LAST_FROM_SPLITS and depth + 1 >= self.max_depth
                 li, small_right, lut, n_split = self._level_finalize(gain, bf, braw, left_all, tot, base, nb,
-                                                                     edges, nbuf, imp)
+                                                                     edges, nbuf, imp, last=last)
                 if n_split == 0:
                     break
                 p = _native.ptr
-                if LAST_FROM_SPLITS and depth + 1 >= self.max_depth:
+                if last:
                     # children are leaves: route, and their statistics from the split search
                     # (split k's children are nb + 2k, nb + 2k + 1)
                     src, cs = q.route_src()
@@ -658,7 +651,6 @@ class HistTreeBuilder:
                         src, C.c_int64(n), q.dpad, C.c_int64(cs), base, base + L, p(node_of_row), p(nbuf.sf), p(nbuf.sb),
                         p(nbuf.lc), p(nbuf.rc), (q.B - 1) if self.missing else -1,
                         int(node_of_row.dtype == torch.int16), _native.stream_of(dev)), "hm_route_rows")
-                    self._leaf_level(nbuf, nb, left_all[li], tot[li])
                     base, L = nb, 2 * n_split
                     depth += 1
                     break
