@@ -44,6 +44,7 @@ ROUTE_FUSED = os.environ.get("HM_ROUTE_FUSED", "1") == "1"  # route + small-chil
 ROUTE_COLS = os.environ.get("HM_ROUTE_COLS", "1") == "1"    # routing reads a feature-major bins copy
 # heap trees: the last level's leaf statistics from the split search, not from histograms
 LAST_FROM_SPLITS = os.environ.get("HM_TREE_LAST_FROM_SPLITS", "1") == "1"
+ROUTE_GRID = int(os.environ.get("HM_ROUTE_GRID", "2048"))   # blocks of the fused route + count pass
 GBT2 = os.environ.get("HM_GBT2", "1") == "1"    # GBT histograms of (r, w), Newton leaves summed per leaf
 HEAP_TREES = os.environ.get("HM_TREE_HEAP", "1") == "1"   # fixed-shape levels, no per-level host read
 HEAP_MAX_DEPTH = 10
@@ -459,7 +460,9 @@ class HistTreeBuilder:
         Nodes [lo, nb) are the level's (lower ids: leaves of earlier levels)."""
         q = self.q
         dev = node_of_row.device
-        G = int(max(1, min(1024, (n + 4095) // 4096)))
+        # the pass is latency-bound: more blocks help (GBDT 2.12 -> 2.10-2.11 ms per tree at 2,048,
+        # 2.40 at 512; profiles/r4/route_grid_ab.log) while the (key, block) counts stay small
+        G = int(max(1, min(ROUTE_GRID if n_keys <= 256 else 1024, (n + 4095) // 4096)))
         counts = torch.empty(n_keys * G, dtype=torch.int64, device=dev)
         p, st = _native.ptr, _native.stream_of(dev)
         n16 = int(node_of_row.dtype == torch.int16)
