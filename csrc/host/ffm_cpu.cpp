@@ -54,6 +54,11 @@ int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
     std::vector<int> ri(F), rf(F);
     std::vector<float> rx(F);
     std::vector<float> snap((size_t)F * F * Kp);
+    // multi-hot rows: a row updates each (feature, field) address once with its summed gradient
+    // (docs/compat.md).  ni / nf: next position with the same feature / field (-1: none);
+    // first: bit 0 = first position of its feature, bit 1 = first of its field
+    std::vector<int> ni(F), nf(F), first(F);
+    std::vector<float> gsum(Kp);
     for (int r = 0; r < B; ++r) {
         float sq = 0.f;
         for (int a = 0; a < F; ++a) {
@@ -68,11 +73,23 @@ int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
             sq += x * x;
         }
         const float scale = (norm && sq > 0.f) ? 1.f / std::sqrt(sq) : 1.f;
-        // snapshot of the row's slot vectors (matches the LDS staging of the GPU kernel)
+        bool multi = false;
+        for (int a = 0; a < F; ++a) {
+            ni[a] = nf[a] = -1;
+            first[a] = 3;
+            if (ri[a] < 0) continue;
+            for (int b = 0; b < F; ++b) {
+                if (b == a || ri[b] < 0) continue;
+                if (ri[b] == ri[a]) { if (b < a) first[a] &= ~1; else if (ni[a] < 0) ni[a] = b; multi = true; }
+                if (rf[b] == rf[a]) { if (b < a) first[a] &= ~2; else if (nf[a] < 0) nf[a] = b; multi = true; }
+            }
+        }
+        // snapshot of the row's slot vectors (matches the LDS staging of the GPU kernel; the
+        // diagonal (a, a) is staged for multi-hot rows, where it can own an address)
         for (int a = 0; a < F; ++a)
             for (int b = 0; b < F; ++b) {
                 float* dst = &snap[((size_t)a * F + b) * Kp];
-                if (a != b && ri[a] >= 0 && ri[b] >= 0) {
+                if ((a != b || multi) && ri[a] >= 0 && ri[b] >= 0) {
                     const float* src = V + ((size_t)ri[a] * FS + rf[b]) * ss;
                     for (int k = 0; k < Kp; ++k) dst[k] = src[k];
                 } else {
@@ -110,20 +127,37 @@ int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
         const float ks = kappa * scale * scale;
         for (int a = 0; a < F; ++a)
             for (int b = 0; b < F; ++b) {
-                if (a == b || ri[a] < 0 || ri[b] < 0) continue;
-                const float coef = ks * rx[a] * rx[b];
+                if (ri[a] < 0 || ri[b] < 0) continue;
                 float* pv = V + ((size_t)ri[a] * FS + rf[b]) * ss;
                 const float* own = &snap[((size_t)a * F + b) * Kp];
-                const float* par = &snap[((size_t)b * F + a) * Kp];
+                float* gk = gsum.data();
+                if (!multi) {
+                    if (a == b) continue;
+                    const float coef = ks * rx[a] * rx[b];
+                    const float* par = &snap[((size_t)b * F + a) * Kp];
+                    for (int k = 0; k < Kp; ++k) gk[k] = coef * par[k] + lv * own[k];
+                } else {
+                    // the address (i_a, f_b) is updated by its owner slot (first position of the
+                    // feature, first of the field) with the sum over every pair that maps to it
+                    if (!(first[a] & 1) || !(first[b] & 2)) continue;
+                    bool any = false;
+                    for (int k = 0; k < Kp; ++k) gk[k] = 0.f;
+                    for (int a2 = a; a2 >= 0; a2 = ni[a2])
+                        for (int b2 = b; b2 >= 0; b2 = nf[b2]) {
+                            if (a2 == b2) continue;
+                            any = true;
+                            const float coef = ks * rx[a2] * rx[b2];
+                            const float* par = &snap[((size_t)b2 * F + a2) * Kp];
+                            for (int k = 0; k < Kp; ++k) gk[k] += coef * par[k];
+                        }
+                    if (!any) continue;
+                    for (int k = 0; k < Kp; ++k) gk[k] += lv * own[k];
+                }
                 if (slot_g) {
                     // G += sum_f g_f^2 (fp32, factor order), then every factor steps with it
                     float* pg = G + (size_t)ri[a] * GS + (size_t)rf[b] * GF;
                     float gs = *pg;
-                    float gk[64];
-                    for (int k = 0; k < Kp; ++k) {
-                        gk[k] = coef * par[k] + lv * own[k];
-                        gs += gk[k] * gk[k];
-                    }
+                    for (int k = 0; k < Kp; ++k) gs += gk[k] * gk[k];
                     *pg = gs;
                     const float r = 1.f / std::sqrt(gs + eps);
                     for (int k = 0; k < Kp; ++k) pv[k] = own[k] - eta0 * gk[k] * r;
@@ -131,7 +165,7 @@ int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
                 }
                 float* pg = G + ((size_t)ri[a] * FS + rf[b]) * ss;
                 for (int k = 0; k < Kp; ++k) {
-                    const float g = coef * par[k] + lv * own[k];
+                    const float g = gk[k];
                     pg[k] += g * g;
                     pv[k] = own[k] - eta0 * g / std::sqrt(pg[k] + eps);
                 }
@@ -139,8 +173,11 @@ int ffm_step_cpu(const int32_t* ip, const float* hp, const int32_t* idx,
         if (use_lin)
             for (int a = 0; a < F; ++a) {
                 const int i = ri[a];
-                if (i < 0) continue;
-                w[i] = ftrl_update(wz + i, wn + i, w[i], kappa * rx[a] * scale, alpha, beta, l1, l2);
+                if (i < 0 || !(first[a] & 1)) continue;
+                // a feature repeated in the row: one FTRL step with the summed gradient
+                float xs = rx[a];
+                for (int a2 = ni[a]; a2 >= 0; a2 = ni[a2]) xs += rx[a2];
+                w[i] = ftrl_update(wz + i, wn + i, w[i], kappa * xs * scale, alpha, beta, l1, l2);
             }
         if (use_bias) bias[0] = ftrl_update(bias + 1, bias + 2, bias[0], kappa, alpha, beta, 0.f, 0.f);
     }

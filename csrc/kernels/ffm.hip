@@ -60,6 +60,16 @@ struct FFMParams {
     float eta0, eps, lambda_v;
     float alpha, beta, lambda1, lambda2;
     float min_target, max_target;  // regression clipping of the prediction
+    const uint8_t* hot;            // per-feature flags (ffm_pipe_sg32_kernel ATOM = 2), or null
+    // Multi-hot rows (two features of one field, or one feature twice: two slots of the row are
+    // the same (feature, field) address).  A row updates each address once with its summed
+    // gradient (docs/compat.md).  The pipelined kernels detect such rows in their forward pass
+    // and, instead of updating, append them to defer = {count, rows...}; ffm_row_kernel then
+    // trains them in list mode (it implements the grouped update).  null: no deferral.
+    int32_t* defer;
+    int list_mode;
+    const int32_t* hot_ids;        // ffm_pipe_sg32_kernel HOTL: hot feature ids (<= 64), or null
+    int hot_n, hot_flush;          // their count; rows between the blocks' delta flushes
 };
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
@@ -226,20 +236,18 @@ __device__ __forceinline__ float row_loss(const FFMParams& P, int row, float p,
     return kappa;
 }
 
-// FTRL updates of the linear terms and the global bias (after the V updates of a row).
-__device__ __forceinline__ void linear_updates(const FFMParams& P, float kappa, float scale,
-                                               const int* s_idx, const float* s_x,
-                                               float* __restrict__ w, float* __restrict__ wz,
-                                               float* __restrict__ wn, float* __restrict__ bias) {
-    const int tid = threadIdx.x;
-    if (P.use_linear && tid < P.F) {
-        const int i = s_idx[tid];
-        if (i >= 0) {
-            const float g = kappa * s_x[tid] * scale;
-            w[i] = ftrl_update(wz + i, wn + i, w[i], g, P.alpha, P.beta, P.lambda1, P.lambda2);
-        }
+// Multi-hot detection in the pipelined kernels: slot (a, b), a < b, of a row shares an address
+// with another slot when the two positions hold the same feature or the same field.
+__device__ __forceinline__ bool slot_repeats(int a, int b, int4 ma, int4 mb) {
+    return a < b && (ma.x | mb.x) >= 0 && (ma.x == mb.x || ma.y == mb.y);
+}
+
+// Appends a multi-hot row to the deferred list (thread 0; the block skips the row's updates).
+__device__ __forceinline__ void defer_row(const FFMParams& P, int row) {
+    if (threadIdx.x == 0) {
+        const int k = atomicAdd(P.defer, 1);
+        P.defer[1 + k] = row;
     }
-    if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -267,23 +275,48 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
     int* s_idx = reinterpret_cast<int*>(smem + vbytes);                  // F
     int* s_fld = s_idx + F;                                              // F
     float* s_x = reinterpret_cast<float*>(s_fld + F);                    // F
-    float* s_red = s_x + F;                                              // 16 (+pad)
+    int* s_ni = reinterpret_cast<int*>(s_x + F);                         // F: next position, same feature
+    int* s_nf = s_ni + F;                                                // F: next position, same field
+    int* s_first = s_nf + F;                                             // F: bit 0 first of feature, 1 of field
+    float* s_red = reinterpret_cast<float*>(s_first + F);                // 16 (+pad)
 
     const int tid = threadIdx.x;
     const size_t ss = (size_t)P.sstride;
     auto slot_off = [&](int i, int f) -> size_t { return (size_t)i * (size_t)P.vfe + (size_t)f * ss; };
     float* Gs = reinterpret_cast<float*>(G);
+    // list mode: the rows the pipelined kernel deferred (count written by the previous launch)
+    const int nrows = P.list_mode ? P.defer[0] : P.B;
 
-    for (int row = blockIdx.x; row < P.B; row += gridDim.x) {
+    for (int k = blockIdx.x; k < nrows; k += gridDim.x) {
+        const int row = P.list_mode ? P.defer[1 + k] : k;
         // ---- 1. row metadata -> LDS (+ instance-wise L2 normalisation) ----
         const float scale = load_row_meta(P, row, idx, fld, val, s_idx, s_fld, s_x, s_red);
+        // ---- 1b. repeated features / fields: chains to the next position of the same feature
+        //      and field, owner flags; multi = the row has any (one block-wide OR) ----
+        int rep = 0;
+        if (tid < F) {
+            const int ia = s_idx[tid], fa = s_fld[tid];
+            int ni = -1, nf = -1, first = 3;
+            if (ia >= 0) {
+                for (int b = 0; b < F; ++b) {
+                    if (b == tid || s_idx[b] < 0) continue;
+                    if (s_idx[b] == ia) { if (b < tid) first &= ~1; else if (ni < 0) ni = b; rep = 1; }
+                    if (s_fld[b] == fa) { if (b < tid) first &= ~2; else if (nf < 0) nf = b; rep = 1; }
+                }
+            }
+            s_ni[tid] = ni;
+            s_nf[tid] = nf;
+            s_first[tid] = first;
+        }
+        const bool multi = __syncthreads_or(rep) != 0;
 
-        // ---- 2. gather the row's slot vectors (coalesced) ----
+        // ---- 2. gather the row's slot vectors (coalesced; the diagonal too in multi-hot rows,
+        //      where it can be the owner of an address) ----
         if (STAGE) {
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
                 const int ia = s_idx[a];
-                const bool live = a != b && ia >= 0 && s_idx[b] >= 0;
+                const bool live = (a != b || multi) && ia >= 0 && s_idx[b] >= 0;
                 const size_t off = live ? slot_off(ia, s_fld[b]) : 0;
 #pragma unroll
                 for (int c = 0; c < KC; ++c)
@@ -325,40 +358,54 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
         // ---- 4. loss ----
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
-        // ---- 5. updates (Hogwild) ----
+        // ---- 5. updates (Hogwild across rows; each address of the row written once) ----
         if (P.train) {
             const float ks = kappa * scale * scale;
             const uint32_t rrow = P.seed ^ ((uint32_t)row * 0x85EBCA77u);
             for (int s = tid; s < FF; s += blockDim.x) {
                 const int a = s / F, b = s - (s / F) * F;
-                if (a == b) continue;
+                if (a == b && !multi) continue;
                 const int ia = s_idx[a], ib = s_idx[b];
                 if (ia < 0 || ib < 0) continue;
-                const float coef = ks * s_x[a] * s_x[b];
+                // multi-hot row: the slot (first position of the feature, first of the field)
+                // owns the address (i_a, f_b) and sums the partner terms of every pair mapping
+                // to it; the other slots of the address do not write
+                if (multi && (!(s_first[a] & 1) || !(s_first[b] & 2))) continue;
                 const size_t ov = slot_off(ia, s_fld[b]);
-                float4 own[KC], par[KC], gg[KC];
+                float4 own[KC], gg[KC], g[KC];
                 if (!SG) {
 #pragma unroll
                     for (int c = 0; c < KC; ++c) gg[c] = ld_chunk<BF>(G, ov + 4 * c);
                 }
-                if (STAGE) {
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) {
-                        own[c] = P.reload ? ld_chunk<BF>(V, ov + 4 * c) : to_f4<BF>(s_v[s * KC + c]);
-                        par[c] = to_f4<BF>(s_v[(b * F + a) * KC + c]);
-                    }
-                } else {
-                    const size_t op = slot_off(ib, s_fld[a]);
-#pragma unroll
-                    for (int c = 0; c < KC; ++c) { own[c] = ld_chunk<BF>(V, ov + 4 * c); par[c] = ld_chunk<BF>(V, op + 4 * c); }
-                }
-                float4 g[KC];
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-                    g[c].x = coef * par[c].x + P.lambda_v * own[c].x;
-                    g[c].y = coef * par[c].y + P.lambda_v * own[c].y;
-                    g[c].z = coef * par[c].z + P.lambda_v * own[c].z;
-                    g[c].w = coef * par[c].w + P.lambda_v * own[c].w;
+                    own[c] = (STAGE && !P.reload) ? to_f4<BF>(s_v[s * KC + c]) : ld_chunk<BF>(V, ov + 4 * c);
+                    g[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                bool any = false;
+                for (int a2 = a; a2 >= 0; a2 = multi ? s_ni[a2] : -1) {
+                    for (int b2 = b; b2 >= 0; b2 = multi ? s_nf[b2] : -1) {
+                        if (a2 == b2) continue;
+                        any = true;
+                        const float coef = ks * s_x[a2] * s_x[b2];
+                        const size_t op = STAGE ? 0 : slot_off(s_idx[b2], s_fld[a2]);
+#pragma unroll
+                        for (int c = 0; c < KC; ++c) {
+                            const float4 par = STAGE ? to_f4<BF>(s_v[(b2 * F + a2) * KC + c]) : ld_chunk<BF>(V, op + 4 * c);
+                            g[c].x += coef * par.x;
+                            g[c].y += coef * par.y;
+                            g[c].z += coef * par.z;
+                            g[c].w += coef * par.w;
+                        }
+                    }
+                }
+                if (!any) continue;       // a diagonal address no pair of the row reads
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    g[c].x += P.lambda_v * own[c].x;
+                    g[c].y += P.lambda_v * own[c].y;
+                    g[c].z += P.lambda_v * own[c].z;
+                    g[c].w += P.lambda_v * own[c].w;
                 }
                 if constexpr (SG) {
                     // one accumulator per slot: G += sum of the k squared gradients (factor
@@ -394,7 +441,15 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                     }
                 }
             }
-            linear_updates(P, kappa, scale, s_idx, s_x, w, wz, wn, bias);
+            // FTRL: one step per distinct feature of the row, with the summed gradient
+            if (P.use_linear && tid < F && s_idx[tid] >= 0 && (!multi || (s_first[tid] & 1))) {
+                const int i = s_idx[tid];
+                float xs = s_x[tid];
+                if (multi)
+                    for (int a2 = s_ni[tid]; a2 >= 0; a2 = s_ni[a2]) xs += s_x[a2];
+                w[i] = ftrl_update(wz + i, wn + i, w[i], kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
+            }
+            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
         __syncthreads();  // LDS reuse by the next row
     }
@@ -517,9 +572,11 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
         uint32_t off[NS];
         float xab[NS];
         bool live[NS];
+        int rep = 0;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int4 ma = s_m[sa[j]], mb = s_m[sb[j]];
+            rep |= (int)slot_repeats(sa[j], sb[j], ma, mb);
             live[j] = sa[j] != sb[j] && ma.x >= 0 && mb.x >= 0;
             off[j] = live[j] ? ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * SLOT_B : 0u;
             xab[j] = live[j] ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
@@ -532,7 +589,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
                 s_t[sb[j] * F + sa[j]] = qv[j];
             }
         }
-        __syncthreads();
+        const bool rdup = __syncthreads_or(rep) != 0;
 
         // ---- forward: every slot (a, b) adds its pair dot weighted by x_a x_b (0 if dead); the
         //      sum over ordered pairs counts each unordered pair twice -> halved ----
@@ -557,7 +614,9 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- AdaGrad(V) update (Hogwild), packed fp32 math; only the store is predicated ----
-        if (P.train) {
+        if (P.train && rdup && P.defer) {
+            defer_row(P, row);                  // multi-hot row: ffm_row_kernel trains it
+        } else if (P.train) {
             float lz = 0.f, ln = 0.f;
             if (P.use_linear && mi >= 0) { lz = wz[mi]; ln = wn[mi]; }
             const float ks = kappa * scale * scale;
@@ -673,6 +732,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
     __shared__ float s_red[8];                                        // [0..3] sums, [4+b] scale
+    __shared__ int s_rep[4];                                          // per wave: a multi-hot slot
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -806,11 +866,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
         uint32_t off[NS];
         float xab[NS];
         uint32_t live = 0u, wr = 0u;
+        int rep = 0;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const uint32_t k = slot(cur, j, off[j], xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
+            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
         }
         if (more) publish_meta(nxt);
         bar_raw();
@@ -846,14 +908,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;
         part = hm::wave_sum_uniform(part);
-        if (lane == 0) s_red[wave] = part;
+        const int wrep = __any(rep);
+        if (lane == 0) { s_red[wave] = part; s_rep[wave] = wrep; }
         bar_raw();
         float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        const bool rdup = (s_rep[0] | s_rep[1] | s_rep[2] | s_rep[3]) != 0;
         if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
-        // ---- E: updates ----
-        if (P.train) {
+        // ---- E: updates (a multi-hot row is deferred to ffm_row_kernel) ----
+        if (P.train && rdup && P.defer) {
+            defer_row(P, row);
+        } else if (P.train) {
             const float ks = kappa * scale * scale;
             const f2 eps = {P.eps, P.eps};
             const f2 meta = {-P.eta0, -P.eta0};
@@ -953,7 +1019,17 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-template <int NS, typename OT, int TPB = 256, int ATOM = 0>
+// HOTL = 1: the slots of the hot features (P.hot_ids, the most frequent features of the pass) are
+// never read-modify-written in HBM by a row.  The block keeps its own pending delta of each hot
+// slot in LDS (s_hv / s_hg), reads a hot slot as (DMA'd global value + own delta), updates the
+// delta, and every P.hot_flush rows (and at its last row) adds the deltas to HBM with float
+// atomics.  Concurrent rows of other blocks then lose none of each other's updates on the slots
+// nearly every row touches (the Hogwild store keeps one of the racing rows' updates: the
+// same-stream logloss gap, docs/perf_notes.md), at the cost of up to hot_flush rows of staleness
+// per block.  LDS: HOT_SLOTS x 20 B more, still 2 blocks/CU.
+constexpr int HOT_SLOTS = 1080;       // hot feature blocks x field stride (27 x 40 at Criteo)
+
+template <int NS, typename OT, int TPB = 256, int ATOM = 0, int HOTL = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -967,6 +1043,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
     __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
+    __shared__ int s_rep[TPB / 64];                                   // per wave: a multi-hot slot
+    __shared__ __attribute__((aligned(16))) float4 s_hv[HOTL ? HOT_SLOTS : 1];   // hot V deltas
+    __shared__ float s_hg[HOTL ? HOT_SLOTS : 1];                      // hot G deltas
+    __shared__ unsigned long long s_hmask[2];                         // row positions holding a hot feature
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -985,6 +1065,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     }
 #define SA(j) (ab[j] & 0xFF)
 #define SB(j) (ab[j] >> 8)
+    // hot features: H blocks of P.fstride slots in LDS; lane h of wave W_META holds hot id h
+    const int H = HOTL ? min(P.hot_n, HOT_SLOTS / P.fstride) : 0;
+    int hot_lane = -2;
+    if (HOTL) {
+        for (int q = tid; q < HOT_SLOTS; q += TPB) {
+            s_hv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_hg[q] = 0.f;
+        }
+        if (wave == W_META && lane < H) hot_lane = P.hot_ids[lane];
+    }
 
     auto dma_meta = [&](int bf, int row) {
         if (wave == W_DMA && lane < F && row < P.B) {
@@ -1002,8 +1092,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 int rf = fld ? s_mr[bf][1][lane] : lane;
                 float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
                 if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
-                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), 0);
+                int hb = (ATOM == 2 && ri >= 0) ? (int)P.hot[ri] : 0;
+                if (HOTL) {
+                    hb = -1;
+                    for (int h = 0; h < H; ++h)
+                        if (__builtin_amdgcn_readlane(hot_lane, h) == ri && ri >= 0) hb = h;
+                }
+                s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), hb);
                 sq = rx * rx;
+            }
+            if (HOTL) {
+                const int hid = lane < F ? s_m[bf][lane].w : -1;
+                const unsigned long long hm_ = __ballot(hid >= 0);
+                if (lane == 0) s_hmask[bf] = hm_;
             }
             const float tot = hm::wave_sum_uniform(sq);
             if (lane == 0) s_red[TPB / 64 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
@@ -1063,6 +1164,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     float fg[NS];
     OT fo[NS];
     uint32_t fwd = 0u;
+    int it = 0;
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
@@ -1079,6 +1181,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 OT ov, og;
                 float xq;
                 if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) { v = fv[j]; cg[j] = fg[j]; }
+            }
+            if (HOTL && (s_hmask[cur] >> SA(j) & 1ull) && tid + j * TPB < FF) {
+                // a hot slot: the global value plus this block's pending delta
+                const int e = s_m[cur][SA(j)].w * P.fstride + s_m[cur][SB(j)].y;
+                const float4 d = s_hv[e];
+                v = make_float4(v.x + d.x, v.y + d.y, v.z + d.z, v.w + d.w);
+                cg[j] += s_hg[e];
             }
             if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = v;
         }
@@ -1103,12 +1212,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         uint32_t live = 0u, wr = 0u;
         float xab[NS];
         float part = 0.f;
+        int rep = 0;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT ov, og;
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
+            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * TPB;
             const float4 pv = s_t[s < FF ? s : 0];
             const float4 cv = s_t[SB(j) * F + SA(j)];
@@ -1117,16 +1228,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;
         part = hm::wave_sum_uniform(part);
-        if (lane == 0) s_red[wave] = part;
+        const int wrep = __any(rep);
+        if (lane == 0) { s_red[wave] = part; s_rep[wave] = wrep; }
         bar_raw();
         float p = 0.f;
+        int rdup = 0;
 #pragma unroll
-        for (int q = 0; q < TPB / 64; ++q) p += s_red[q];
+        for (int q = 0; q < TPB / 64; ++q) { p += s_red[q]; rdup |= s_rep[q]; }
         if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
-        // ---- E: updates ----
-        if (P.train) {
+        // ---- E: updates (a multi-hot row is deferred to ffm_row_kernel) ----
+        if (P.train && rdup && P.defer) {
+            defer_row(P, row);
+        } else if (P.train) {
             const float ks = kappa * scale * scale;
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
@@ -1148,11 +1263,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
+                if (HOTL && (s_hmask[cur] >> SA(j) & 1ull)) {
+                    // hot slot: only this block's LDS delta moves (single writer in the row)
+                    const int e = s_m[cur][SA(j)].w * P.fstride + s_m[cur][SB(j)].y;
+                    const float4 hd = s_hv[e];
+                    s_hv[e] = make_float4(hd.x + (o0.x - cv.x), hd.y + (o0.y - cv.y), hd.z + (o1.x - cv.z),
+                                          hd.w + (o1.y - cv.w));
+                    s_hg[e] += gs - cg[j];
+                    continue;
+                }
                 fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
                 fg[j] = gs;
                 fo[j] = ov;
                 fwd |= 1u << j;
-                if (ATOM) {
+                if (ATOM == 1 || (ATOM == 2 && s_m[cur][SA(j)].w != 0)) {
                     // concurrent rows' updates of one slot all land (no read-modify-write race)
                     if (live >> j & 1u) {
                         float* vp = reinterpret_cast<float*>(vb + ov);
@@ -1180,7 +1304,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    if (ATOM) {
+                    if (ATOM == 1 || (ATOM == 2 && s_m[cur][lane].w != 0)) {
                         atomicAdd(wz + mi, z1 - lz);
                         atomicAdd(wn + mi, g * g);
                     } else {
@@ -1194,6 +1318,31 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
         if (more) dma_lin(nxt);
+        // ---- G (HOTL): every hot_flush rows and after the last row, the hot deltas go to HBM
+        //      (float atomics, each wave-instruction over consecutive words of one feature's V
+        //      or G region) and the LDS deltas restart from 0 ----
+        if (HOTL && P.train && (++it >= P.hot_flush || !more)) {
+            it = 0;
+            bar_raw();
+            const int nv = H * P.fstride * 4;
+            for (int q = tid; q < nv; q += TPB) {
+                const int h = q / (P.fstride * 4), r = q - h * (P.fstride * 4);
+                float* pd = reinterpret_cast<float*>(s_hv) + h * P.fstride * 4 + r;
+                const float d = *pd;
+                if (d != 0.f) {
+                    atomicAdd(reinterpret_cast<float*>(vb + (OT)(uint32_t)P.hot_ids[h] * vfs) + r, d);
+                    *pd = 0.f;
+                }
+            }
+            for (int q = tid; q < H * P.fstride; q += TPB) {
+                const int h = q / P.fstride, f = q - h * P.fstride;
+                const float d = s_hg[q];
+                if (d != 0.f) {
+                    atomicAdd(reinterpret_cast<float*>(gb + (OT)(uint32_t)P.hot_ids[h] * gfs) + f, d);
+                    s_hg[q] = 0.f;
+                }
+            }
+        }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
 #undef SA
@@ -1221,6 +1370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];
     __shared__ float s_red[8];
+    __shared__ int s_rep[4];                                                  // per wave: a multi-hot slot
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1337,12 +1487,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         uint32_t live = 0u, wr = 0u;
         float xab[NS];
         float part = 0.f;
+        int rep = 0;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT off;
             const uint32_t k = slot(cur, j, off, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
+            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * 256;
             const uint2 pv = s_t[s < FF ? s : 0];
             const uint2 cv = s_t[SB(j) * F + SA(j)];
@@ -1351,14 +1503,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;
         part = hm::wave_sum_uniform(part);
-        if (lane == 0) s_red[wave] = part;
+        const int wrep = __any(rep);
+        if (lane == 0) { s_red[wave] = part; s_rep[wave] = wrep; }
         bar_raw();
         float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        const bool rdup = (s_rep[0] | s_rep[1] | s_rep[2] | s_rep[3]) != 0;
         if (P.use_bias) p += bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
-        // ---- E: updates ----
-        if (P.train) {
+        // ---- E: updates (a multi-hot row is deferred to ffm_row_kernel) ----
+        if (P.train && rdup && P.defer) {
+            defer_row(P, row);
+        } else if (P.train) {
             const float ks = kappa * scale * scale;
             uint32_t hrow = (P.seed ^ ((uint32_t)row * 0x85EBCA77u)) + tid_h;
             hrow ^= hrow >> 16;
@@ -1507,10 +1663,18 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
+    const bool hotl = P.hot_ids != nullptr && P.hot_n > 0 && P.train && (variant == 0 || variant == 9);
 #define HM_P32(NSV) do { \
-        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+        if (hotl && wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, 256, 0, 1>), dim3(blocks), dim3(256), 0, \
+                                             stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else if (hotl) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1>), dim3(blocks), dim3(256), 0, \
+                                          stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 1>), dim3(blocks), \
+                                                  dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                  bias, pred, loss); \
+        else if (variant == 8 && P.hot) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 2>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
@@ -1527,7 +1691,7 @@ template <int KC, bool BF, bool SG>
 int launch_ffm(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
                float* pred, float* loss, int grid, hipStream_t stream) {
-    const size_t meta = (size_t)3 * P.F * 4 + 16 * 4;
+    const size_t meta = (size_t)6 * P.F * 4 + 16 * 4;
     const size_t stage = (size_t)P.F * P.F * KC * (BF ? 8 : 16);
     const bool use_stage = stage + meta <= 64 * 1024;
     const int blocks = default_blocks(P.B, grid);
@@ -1556,10 +1720,13 @@ int launch_generic(const FFMParams& P, const int32_t* idx, const int32_t* fld, c
     }
 }
 
+// *fast = 1 when a pipelined / lean kernel ran (it defers multi-hot rows when P.defer is set).
 template <bool BF>
 int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
              const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
-             float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream) {
+             float* pred, float* loss, int grid, int packed, int slot_g, int variant, hipStream_t stream,
+             int* fast) {
+    *fast = 1;
     if (slot_g) {
         if (P.gfstride == 3) {
             // 12-B {V | G} slots: the pipelined kernel; rows wider than 45 features or tables of
@@ -1568,6 +1735,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
             if (!BF) return (int)hipErrorInvalidValue;
             const int rc = variant == 1 ? -1 : dispatch_sg12(P, idx, fld, val, y, V, w, wz, wn, bias, pred, loss, grid, variant, stream);
             if (rc != -1) return rc;
+            *fast = 0;
             return launch_generic<true, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
         }
         if (variant != 1 && !BF && P.gfstride == 1) {
@@ -1575,6 +1743,7 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
                                          bias, pred, loss, grid, variant, stream);
             if (rc != -1) return rc;
         }
+        *fast = 0;
         return launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
     }
     if (packed && variant != 1) {
@@ -1582,7 +1751,22 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
         if (rc != -1) return rc;
         // other shapes: the generic kernel handles the packed strides too (G = V + Kp)
     }
+    *fast = 0;
     return launch_generic<BF, false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
+}
+
+// The deferred multi-hot rows of a pipelined launch: ffm_row_kernel over the list (grid of
+// DEFER_BLOCKS blocks; each exits at once when the count is 0).
+constexpr int DEFER_BLOCKS = 512;
+
+template <bool BF>
+int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const float* val,
+                    const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
+                    float* pred, float* loss, int slot_g, hipStream_t stream) {
+    P.list_mode = 1;
+    const int grid = P.B < DEFER_BLOCKS ? P.B : DEFER_BLOCKS;
+    return slot_g ? launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream)
+                  : launch_generic<BF, false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
 }
 
 }  // namespace
@@ -1614,10 +1798,23 @@ int dispatch(const FFMParams& P, const int32_t* idx, const int32_t* fld, const f
 // registers instead of an LDS landing zone (53 KB per block: 3 rows in flight per CU instead of
 // 2): 73.6-73.8 vs 73.9-74.2 M rows/s (profiles/r4/ffm_register_g_ab.log) — more rows in flight
 // per CU does not move this kernel.
+// aux (host array of 5 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
+// or null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
+// updated slot by slot by the pipelined kernels: racing stores of one address, one wins);
+// aux[2] = hot feature ids int32 [<= 64] for the fp32 kernel's LDS delta path (HOTL) or null,
+// aux[3] = their count, aux[4] = rows between a block's hot-delta flushes.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
-                       float* wn, float* bias, float* pred, float* loss, hipStream_t stream) {
+                       float* wn, float* bias, float* pred, float* loss, void* const* aux,
+                       hipStream_t stream) {
     FFMParams P;
+    P.hot = aux ? reinterpret_cast<const uint8_t*>(aux[0]) : nullptr;
+    P.defer = aux ? reinterpret_cast<int32_t*>(aux[1]) : nullptr;
+    P.list_mode = 0;
+    P.hot_ids = aux ? reinterpret_cast<const int32_t*>(aux[2]) : nullptr;
+    P.hot_n = aux ? (int)reinterpret_cast<intptr_t>(aux[3]) : 0;
+    P.hot_flush = aux ? (int)reinterpret_cast<intptr_t>(aux[4]) : 0;
+    if (P.hot_n > 64 || (P.hot_ids && P.hot_flush <= 0)) return (int)hipErrorInvalidValue;
     P.B = ip[0]; P.F = ip[1]; P.num_features = ip[2]; P.num_fields = ip[3]; P.Kp = ip[4];
     P.classification = ip[5]; P.train = ip[6]; P.use_linear = ip[7]; P.use_bias = ip[8];
     P.norm = ip[9];
@@ -1664,6 +1861,15 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
         // 32-bit slot indices in the packed kernel
         if ((size_t)P.num_features * (size_t)P.fstride >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
     }
-    return bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream)
-                : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream);
+    if (!P.train || P.B <= 0) P.defer = nullptr;
+    if (P.defer) {
+        const hipError_t e = hipMemsetAsync(P.defer, 0, sizeof(int32_t), stream);
+        if (e != hipSuccess) return (int)e;
+    }
+    int fast = 0;
+    const int rc = bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast)
+                        : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast);
+    if (rc != 0 || !fast || !P.defer) return rc;
+    return bf16 ? launch_deferred<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream)
+                : launch_deferred<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream);
 }

@@ -36,7 +36,9 @@ struct FMParams {
     float min_target, max_target;
     int use_w0;
     int w0_shards;            // w0 = sum of w0[0..w0_shards) (<= 64)
-    int w0_every;             // fm_pipe_kernel: rows between re-reads of the w0 shards (>= 1)
+    int w0_every;             // fm_pipe_kernel: most rows between re-reads of the w0 shards (>= 1)
+    float w0_tol;             // ... and a re-read as soon as the wave's own bias steps since the
+                              // last one add up to more than w0_tol x eta (0: off)
     uint32_t seed;
 };
 
@@ -259,13 +261,18 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
     // (one row of extra staleness on a parameter every wave of the chip updates anyway)
     float w0part = (P.use_w0 && lane < P.w0_shards) ? w0[lane * W0_STRIDE] : 0.f;
     float yy = y ? y[gw] : 0.f;
-    int it = 0;
-    for (int64_t row = gw; row < n_rows; row += nw, ++it) {
+    int since = 0;            // rows since the last re-read of the shards
+    float acc = 0.f;          // the wave's own bias steps since then (wave-uniform)
+    for (int64_t row = gw; row < n_rows; row += nw) {
         const int nnz = (int)(e - s);
         int i = (ci >= 0 && ci < P.dims) ? ci : -1;
-        // the w0 shards are re-read every w0_every rows; in between the wave adds its own
-        // deltas to its copy (lane 0), so only the other waves' updates are seen late
-        const bool w0_ref = P.w0_every <= 1 || ((it + 1) % P.w0_every) == 0;
+        // the w0 shards are re-read at most every w0_every rows; in between the wave adds its
+        // own deltas to its copy (lane 0), so only the other waves' updates are seen late.  The
+        // re-read comes early when the wave's own steps drift one way (|sum| > w0_tol x eta):
+        // the bias is then moving, and every other wave's copy with it (early training)
+        const float eta_r = fm_eta(P, (float)(t0 + row + 1));
+        const bool w0_ref = P.w0_every <= 1 || since + 1 >= P.w0_every ||
+                            (P.w0_tol > 0.f && fabsf(acc) > P.w0_tol * eta_r);
         float x = i >= 0 ? cx : 0.f;
         // ---- gathers of this row (the only loads the forward waits for) ----
         VRow<KP, BF16> vr;
@@ -371,15 +378,18 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
                 t.load(V, i2);
                 upd(t, i2, x2, w[i2]);
             }
-            if (P.use_w0 && lane == 0) {
+            if (P.use_w0) {
                 const float dw0 = -eta * (d + 2.f * P.lambda0 * w0v);
-                atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, dw0);
-                w0part += dw0;
+                if (lane == 0) {
+                    atomicAdd(w0 + (int)(gw % P.w0_shards) * W0_STRIDE, dw0);
+                    w0part += dw0;
+                }
+                acc += dw0;
             }
         }
         // rotate the pipeline
         s = ns; e = ne; ci = pi; cx = px; yy = py;
-        if (w0_ref) w0part = pw0;
+        if (w0_ref) { w0part = pw0; since = 0; acc = 0.f; } else { ++since; }
         ns = ns2; ne = ne2;
     }
 }
@@ -414,7 +424,7 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 // ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant,
 //     w0_every
 //     (variant 0 = fm_pipe_kernel, 1 = fm_kernel)
-// hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target
+// hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target, w0_tol
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
                       const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
                       float* w, void* V, float* w0, float* pred, float* loss, hipStream_t stream) {
@@ -430,6 +440,7 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     if (P.w0_shards < 1 || P.w0_shards > 64) return (int)hipErrorInvalidValue;
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
+    P.w0_tol = hp[8];
     if (n_rows <= 0) return 0;
 #define HM_FM_CASE(K)                                                                            \
     case K:                                                                                      \

@@ -71,22 +71,66 @@ __global__ __launch_bounds__(64) void linear_train_kernel(
     int32_t* TL = minib ? tlist + (size_t)r * G.touched_cap : nullptr;
     int n_touched = 0, in_batch = 0;
 
+    // Row pipeline: the replica's rows are strictly sequential (each row reads the state the
+    // previous one wrote), but their CSR bounds, first-chunk indices / values and labels do not
+    // depend on the state: row q + 1's are loaded while row q computes and row q + 2's bounds one
+    // row earlier, so a row waits on one dependent round trip (the state gather) instead of three.
+    auto row_of = [&](int64_t q) -> int64_t { return order ? (int64_t)order[q] : q; };
+    int64_t cs = 0, ce = 0;              // bounds of row q
+    int64_t pb_s = 0, pb_e = 0;          // bounds of row q + 1
+    int pci = -1;                        // first-chunk index / value / label of row q
+    float pcx = 0.f, pyy = 0.f;
+    if (r0 < r1) {
+        const int64_t row0 = row_of(r0);
+        cs = indptr[row0];
+        ce = indptr[row0 + 1];
+        if (lane < (int)(ce - cs)) {
+            pci = idx[cs + lane];
+            pcx = val ? val[cs + lane] : 1.f;
+        }
+        pyy = y[row0];
+        if (r0 + 1 < r1) {
+            const int64_t row1 = row_of(r0 + 1);
+            pb_s = indptr[row1];
+            pb_e = indptr[row1 + 1];
+        }
+    }
+
     for (int64_t q = r0; q < r1; ++q) {
-        const int64_t row = order ? (int64_t)order[q] : q;
-        const int64_t s = indptr[row], e = indptr[row + 1];
+        const int64_t s = cs, e = ce;
         const int nnz = (int)(e - s);
-        const float yy = y[row];
+        const float yy = pyy;
         rs[RS_T] += 1.f;
         const float t = rs[RS_T];
         const StepK sk = step_consts(P, t);
-        // ---- cached first chunk ----
-        int ci = -1;
-        float cx = 0.f;
+        // ---- cached first chunk (prefetched one row ahead) ----
+        int ci = pci;
+        float cx = pcx;
         if (lane < nnz) {
-            ci = idx[s + lane];
-            cx = val ? val[s + lane] : 1.f;
             if (ci < 0 || ci >= dims) ci = -1;
             if (ci >= 0) T[ci] = 1;
+        } else {
+            ci = -1;
+            cx = 0.f;
+        }
+        // ---- prefetch: row q + 1's first chunk and label (its bounds are in pb_*), row q + 2's
+        //      bounds ----
+        cs = pb_s;
+        ce = pb_e;
+        pci = -1;
+        pcx = 0.f;
+        if (q + 1 < r1) {
+            const int n1 = (int)(ce - cs);
+            if (lane < n1) {
+                pci = idx[cs + lane];
+                pcx = val ? val[cs + lane] : 1.f;
+            }
+            pyy = y[row_of(q + 1)];
+            if (q + 2 < r1) {
+                const int64_t row2 = row_of(q + 2);
+                pb_s = indptr[row2];
+                pb_e = indptr[row2 + 1];
+            }
         }
         if (!mc) {
             F4 cst = {0.f, 0.f, 0.f, 0.f};
@@ -602,7 +646,13 @@ __global__ __launch_bounds__(256) void linear_shared_kernel(
             }
             lds_barrier();
             if (owner) {
-                // the hot features this thread owns: h = block + gridDim.x * (thread + 256 j)
+                // the hot features this thread owns: h = block + gridDim.x * (thread + 256 j).
+                // Bounded skew: another block's (x, y, z) adds are three atomics to
+                // different words, so one block's chunk can straddle this exchange — its count in
+                // this drain and its gradient sums in the next, or the reverse.  Nothing is lost
+                // (every add lands in exactly one drain); the split moves one block-chunk's
+                // contribution (<= 32 rows per wave) between two consecutive n-step applications
+                // of the feature, i.e. the mean gradient of a drain is off by at most that share.
                 for (int h = blockIdx.x + gridDim.x * threadIdx.x; h < H; h += gridDim.x * 256) {
                     const float n = atomicExch(&hacc[h].z, 0.f);
                     if (n <= 0.f) continue;

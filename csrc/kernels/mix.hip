@@ -137,6 +137,54 @@ __global__ __launch_bounds__(256) void view3_kernel(void* __restrict__ x, const 
     }
 }
 
+// Delta mixing of fp32 (or bf16) replicas over a [n0][d1][inner] view, base = the fp32 consensus
+// of the last mix (contiguous, like the wire buffers).  One pass each, no payload-sized
+// temporaries (the torch formulation ran 3-5 elementwise passes with fp32 temporaries):
+// MODE 2 (pack):          wire[q] <- x[view(q)] - base[q]            (fp32 math, RNE to the wire)
+// MODE 3 (merge, sync):   base[q] += m[q];  x[view(q)] <- base[q]    (average_delta)
+// MODE 4 (merge, overlap): base[q] += m[q] (rounded to x's dtype);  x += m[q] - sent[q]
+//                          (OverlappedMixer delta-sum modes: x keeps its progress since the snapshot)
+// XBF: x in bf16; WBF: wire (m, sent) in bf16.  Rounding as torch's copy_ (RNE), so the
+// results are bit-identical to the torch formulation.
+__device__ __forceinline__ float rne_bf16(float v) {
+    return __uint_as_float((uint32_t)hm::f32_to_bf16(v) << 16);
+}
+
+template <int MODE, bool XBF, bool WBF, bool ALN>
+__global__ __launch_bounds__(256) void delta3_kernel(void* __restrict__ x, float* __restrict__ base,
+                                                     void* __restrict__ wire, const void* __restrict__ sent,
+                                                     int64_t n0, int d1, int inner, int64_t s0, int64_t s1) {
+    const int qps = inner >> 2;
+    const int64_t per0 = (int64_t)d1 * qps;
+    const int64_t nq = n0 * per0;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+        const int64_t i0 = q / per0;
+        const int64_t rem = q - i0 * per0;
+        const int64_t i1 = rem / qps;
+        const int c = (int)(rem - i1 * qps) * 4;
+        const int64_t xe = i0 * s0 + i1 * s1 + c, qe = 4 * q;
+        float4 b = *reinterpret_cast<const float4*>(base + qe);
+        if constexpr (MODE == 2) {
+            const float4 a = ldx<XBF, ALN>(x, xe);
+            st4<WBF>(wire, qe, make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w));
+        } else {
+            const float4 m = ld4<WBF>(wire, qe);
+            b = make_float4(b.x + m.x, b.y + m.y, b.z + m.z, b.w + m.w);
+            if constexpr (MODE == 3) {
+                *reinterpret_cast<float4*>(base + qe) = b;
+                stx<XBF, ALN>(x, xe, b);
+            } else {
+                if constexpr (XBF) b = make_float4(rne_bf16(b.x), rne_bf16(b.y), rne_bf16(b.z), rne_bf16(b.w));
+                *reinterpret_cast<float4*>(base + qe) = b;
+                const float4 sn = ld4<WBF>(sent, qe);
+                const float4 a = ldx<XBF, ALN>(x, xe);
+                stx<XBF, ALN>(x, xe, make_float4(a.x + (m.x - sn.x), a.y + (m.y - sn.y), a.z + (m.z - sn.z),
+                                                 a.w + (m.w - sn.w)));
+            }
+        }
+    }
+}
+
 int grid_for(int64_t quads) {
     const int64_t b = (quads + 255) / 256;
     return (int)(b < 256 * 16 ? (b > 0 ? b : 1) : 256 * 16);
@@ -209,4 +257,31 @@ HM_API int hm_mix_pack3(const void* x, void* out, int64_t n0, int d1, int inner,
 HM_API int hm_mix_merge3(void* x, const void* mean, const void* snap, void* out, int64_t n0, int d1, int inner,
                          int64_t s0, int64_t s1, int dtype, hipStream_t stream) {
     return launch_view3<1>(x, mean, snap, out, n0, d1, inner, s0, s1, dtype, stream);
+}
+
+// Delta mixing over a view (see delta3_kernel).  mode 2 = pack, 3 = sync merge, 4 = overlapped
+// merge; xdtype / wdtype: 0 = fp32, 1 = bf16; base: fp32, contiguous; sent: mode 4 only.
+HM_API int hm_mix_delta3(void* x, float* base, void* wire, const void* sent, int64_t n0, int d1, int inner,
+                         int64_t s0, int64_t s1, int mode, int xdtype, int wdtype, hipStream_t stream) {
+    if (n0 < 0 || d1 <= 0 || inner <= 0 || (inner & 3) || s1 < inner || s0 < (int64_t)(d1 - 1) * s1 + inner ||
+        mode < 2 || mode > 4 || (xdtype | wdtype) & ~1 || (mode == 4 && sent == nullptr) ||
+        (uintptr_t)base % 16 != 0)
+        return (int)hipErrorInvalidValue;
+    if (n0 == 0) return 0;
+    const int64_t nq = n0 * d1 * (inner >> 2);
+    const bool aln = (s0 % 4 == 0) && (s1 % 4 == 0) && ((uintptr_t)x % (xdtype == 1 ? 8 : 16) == 0);
+    const int key = mode * 8 + xdtype * 4 + wdtype * 2 + (aln ? 1 : 0);
+    const dim3 g(grid_for(nq)), b(256);
+#define HM_D3(M, XB, WB, AL) case M * 8 + XB * 4 + WB * 2 + AL: \
+        hipLaunchKernelGGL((delta3_kernel<M, (bool)XB, (bool)WB, (bool)AL>), g, b, 0, stream, x, base, wire, sent, \
+                           n0, d1, inner, s0, s1); break;
+#define HM_D3M(M) HM_D3(M, 0, 0, 0) HM_D3(M, 0, 0, 1) HM_D3(M, 0, 1, 0) HM_D3(M, 0, 1, 1) \
+                  HM_D3(M, 1, 0, 0) HM_D3(M, 1, 0, 1) HM_D3(M, 1, 1, 0) HM_D3(M, 1, 1, 1)
+    switch (key) {
+        HM_D3M(2) HM_D3M(3) HM_D3M(4)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HM_D3M
+#undef HM_D3
+    HM_LAUNCH_RET();
 }

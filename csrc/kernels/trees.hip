@@ -325,9 +325,11 @@ __global__ __launch_bounds__(256) void leaf_sums_kernel(const NT* __restrict__ l
         }
 #pragma unroll
         for (int u = 0; u < LEAF_U; ++u) {
-            if (l[u] < 0 || l[u] >= T || h[u] == 0.f) continue;
-            atomicAdd(&my[2 * l[u]], (unsigned long long)llrintf(g[u] * LEAF_FIX));
-            atomicAdd(&my[2 * l[u] + 1], (unsigned long long)llrintf(h[u] * LEAF_FIX));
+            // masked / inactive rows have no leaf; a saturated row (|r| = 1 in fp32: h = 0) still
+            // adds its residual to the Newton numerator, as the host formulation does
+            if (l[u] < 0 || l[u] >= T) continue;
+            if (g[u] != 0.f) atomicAdd(&my[2 * l[u]], (unsigned long long)llrintf(g[u] * LEAF_FIX));
+            if (h[u] != 0.f) atomicAdd(&my[2 * l[u] + 1], (unsigned long long)llrintf(h[u] * LEAF_FIX));
         }
     }
     __syncthreads();

@@ -14,6 +14,7 @@ per-file compiles in parallel.  ``python -m hivemall_amd._build`` builds everyth
 from __future__ import annotations
 
 import concurrent.futures as _cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -69,19 +70,63 @@ def _run(cmd, verbose):
     return r
 
 
-def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs, objdir: Path = OBJDIR):
-    objdir.mkdir(parents=True, exist_ok=True)
-    lib.parent.mkdir(parents=True, exist_ok=True)
+def source_hash(srcs, hdrs, flags) -> str:
+    """sha256 over the sources and headers a library is built from (path relative to csrc,
+    contents) and the compile flags: the library's provenance."""
+    h = hashlib.sha256()
+    for f in sorted(set(srcs) | set(hdrs)):
+        h.update(str(Path(f).relative_to(CSRC)).encode())
+        h.update(b"\0")
+        h.update(Path(f).read_bytes())
+        h.update(b"\0")
+    h.update(" ".join(map(str, flags)).encode())
+    return h.hexdigest()[:32]
+
+
+def _deps(srcs):
     hdrs = _headers(CSRC / "kernels")  # shared rule headers are used by host code too
     for s in srcs:
         hdrs.extend(_headers(s.parent))
-    if lib.exists() and not _stale(lib, list(srcs) + hdrs):
-        # the library is newer than every source and header: nothing to do, whether or not the
-        # object files are around (a GPU box gets the tree without build/, and recompiling the
-        # kernels there cost the first launch ~12 s: BENCH_r03.json wall_s.warmup)
+    return sorted(set(hdrs))
+
+
+def lib_hash_file(lib: Path) -> Path:
+    return lib.with_name(lib.name + ".srchash")
+
+
+def expected_hash(kind: str) -> str:
+    """Source hash the in-tree ``kind`` ("hip" / "host") library must carry."""
+    if kind == "hip":
+        srcs = sorted((CSRC / "kernels").glob("*.hip"))
+        return source_hash(srcs, _deps(srcs), HIP_FLAGS)
+    srcs = sorted((CSRC / "host").glob("*.cpp"))
+    return source_hash(srcs, _deps(srcs), HOST_FLAGS)
+
+
+def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs, objdir: Path = OBJDIR):
+    objdir.mkdir(parents=True, exist_ok=True)
+    lib.parent.mkdir(parents=True, exist_ok=True)
+    hdrs = _deps(srcs)
+    want = source_hash(srcs, hdrs, flags)
+    hf = lib_hash_file(lib)
+    if lib.exists() and hf.exists() and hf.read_text().strip() == want:
+        # the library was built from exactly these sources and flags (content hash, embedded in
+        # the library as hm_build_id() and checked at load by _native): nothing to do, whether
+        # or not the object files are around (a GPU box gets the tree without build/, and
+        # recompiling the kernels there cost the first launch ~12 s: BENCH_r03.json)
         return lib
     objs = []
     todo = []
+    # the provenance object: hm_build_id() returns the source hash of this build
+    gen = objdir / f"build_id_{lib.stem}{srcs[0].suffix if srcs else '.cpp'}"
+    gen_txt = ('extern "C" __attribute__((visibility("default"))) const char* hm_build_id() '
+               f'{{ return "{want}"; }}\n')
+    if not gen.exists() or gen.read_text() != gen_txt:
+        gen.write_text(gen_txt)
+    go = gen.with_suffix(gen.suffix + ".o")
+    objs.append(go)
+    if _stale(go, [gen]):
+        todo.append((gen, go))
     for s in srcs:
         o = objdir / (s.parent.name + "_" + s.name + ".o")
         objs.append(o)
@@ -92,10 +137,11 @@ def _build_lib(srcs, compiler, flags, lib: Path, link_flags, verbose, jobs, objd
             futs = [ex.submit(_run, [compiler, *flags, "-c", s, "-o", o], verbose) for s, o in todo]
             for f in futs:
                 f.result()
-    if todo or _stale(lib, objs):
+    if todo or _stale(lib, objs) or not hf.exists() or hf.read_text().strip() != want:
         tmp = lib.with_suffix(".so.tmp")
         _run([compiler, "-shared", "-o", tmp, *objs, *link_flags], verbose)
         os.replace(tmp, lib)
+        hf.write_text(want + "\n")
     return lib
 
 

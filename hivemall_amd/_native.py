@@ -43,6 +43,7 @@ def host():
             if _autobuild():
                 _build.build_host()
             lib = C.CDLL(str(_build.HOST_LIB))
+            _check_build_id(lib, "host", _build.HOST_LIB)
             _declare_host(lib)
             _host = lib
     return _host
@@ -62,9 +63,37 @@ def hip():
             if not _build.HIP_LIB.exists():
                 raise RuntimeError(f"HIP kernel library missing: {_build.HIP_LIB} (run build())")
             lib = C.CDLL(str(_build.HIP_LIB))
+            _check_build_id(lib, "hip", _build.HIP_LIB)
             _declare_hip(lib)
             _hip = lib
     return _hip
+
+
+BUILD_IDS: dict = {}   # kind -> source hash embedded in the loaded library
+
+
+def _check_build_id(lib, kind: str, path) -> None:
+    """The loaded library must have been built from the sources in this tree: its embedded
+    hm_build_id() (the content hash of csrc + flags, _build.source_hash) must equal the hash of
+    the sources here.  A library from another tree, or one whose sources changed without a
+    rebuild, is an error (HM_SKIP_BUILD_ID=1 skips the check; so does an out-of-tree library
+    chosen by HM_HIP_LIB / HM_HOST_LIB)."""
+    fn = getattr(lib, "hm_build_id", None)
+    got = None
+    if fn is not None:
+        fn.restype = C.c_char_p
+        fn.argtypes = []
+        got = fn().decode()
+    BUILD_IDS[kind] = got
+    in_tree = str(path) == str(_build.LIBDIR / ("libhm_hip.so" if kind == "hip" else "libhm_host.so"))
+    if os.environ.get("HM_SKIP_BUILD_ID") == "1" or not in_tree:
+        # an explicitly chosen library (HM_HIP_LIB / HM_HOST_LIB, e.g. the sanitizer build with
+        # its own flags) is the caller's responsibility
+        return
+    want = _build.expected_hash(kind)
+    if got != want:
+        raise RuntimeError(f"{path}: built from other sources (build id {got}, this tree {want}); "
+                           "rebuild with `python -m hivemall_amd._build`")
 
 
 def hip_available() -> bool:
@@ -160,5 +189,5 @@ def _declare_hip(lib):
 
 
 # Kernel launchers: every one returns hipError_t and takes the stream last.
-register_hip("hm_ffm_step", [c_p] * 15)
+register_hip("hm_ffm_step", [c_p] * 16)
 register_host("hm_ffm_step_cpu", [c_p] * 14)

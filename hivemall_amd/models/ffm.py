@@ -87,6 +87,51 @@ RAMP_GRID = int(os.environ.get("HM_FFM_RAMP_GRID", "1024"))
 RAMP_VARIANT = int(os.environ.get("HM_FFM_RAMP_VARIANT", "6"))   # kernel variant of the ramp rows
 
 
+# Divergence guard of the step rule (FFMTrainer._dp_guard): a rise of the mean training loss
+# between two mix intervals by more than this fraction drops p to DP_GUARD_POWER.
+DP_GUARD_RISE = 0.02
+DP_GUARD_POWER = 0.5
+
+
+# Hot-slot deltas of the fp32 kernel (csrc/kernels/ffm.hip ffm_pipe_sg32_kernel HOTL): the
+# HOT_FEATURES most frequent features of a batch have their (feature, field) slots updated through
+# per-block LDS deltas flushed to HBM by float atomics every HOT_FLUSH rows of a block, instead of
+# Hogwild stores that lose concurrent rows' updates.  HM_FFM_HOT=0 disables.
+HOT_FEATURES = int(os.environ.get("HM_FFM_HOT", "27"))
+HOT_FLUSH = int(os.environ.get("HM_FFM_HOT_FLUSH", "16"))
+_HOT_CACHE: dict = {}
+
+
+def hot_feature_ids(idx: torch.Tensor, num_features: int, n: int | None = None,
+                    rows_in_flight: int = 512) -> torch.Tensor | None:
+    """The at most HOT_FEATURES most frequent features of the padded-ELL batch ``idx`` that more
+    than one of the kernel's ~``rows_in_flight`` concurrent rows is expected to hold (count >=
+    rows / rows_in_flight), as int32 on idx's device; None when there are none.  Counted from a
+    strided sample of the rows (a full bincount of a large batch costs as much as a step); cached
+    per index tensor (weakly, with its version counter)."""
+    import weakref
+
+    H = min(HOT_FEATURES, 64)
+    if H <= 0 or idx.numel() == 0:
+        return None
+    key = (idx.data_ptr(), idx.numel(), idx._version, num_features)
+    hit = _HOT_CACHE.get(key)
+    if hit is not None and hit[0]() is idx:
+        return hit[1]
+    rows = idx.shape[0]
+    stride = max(1, rows // (1 << 16))
+    ids = idx[::stride].reshape(-1).long()
+    ids = ids[(ids >= 0) & (ids < num_features)]
+    cnt = torch.bincount(ids, minlength=num_features)
+    vals, feats = torch.topk(cnt, min(H, num_features))
+    feats = feats[vals * stride >= max(2, rows // max(1, rows_in_flight))].to(torch.int32).contiguous()
+    res = feats if feats.numel() else None
+    if len(_HOT_CACHE) > 16:
+        _HOT_CACHE.clear()
+    _HOT_CACHE[key] = (weakref.ref(idx), res)
+    return res
+
+
 def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
     """Step-size factor of a data-parallel replica (1.0 on one rank)."""
     return float(world) ** float(power) if world > 1 else 1.0
@@ -144,10 +189,14 @@ class FFMTrainer(Learner):
             max_target=c["max"] if c["max"] is not None else 3.4e38,
             classification=bool(c["classification"]), use_linear=not c["disable_wi"],
             use_bias=bool(c["global_bias"]), norm=not c["no_norm"])
-        if self._dp():
-            sc = dp_lr_scale(self.mixer.world, c["dp_lr_power"])
-            self.hyper.eta0 *= sc
-            self.hyper.alpha *= sc
+        # the N^p step rule was fitted for replicas mixed every few batches (benchmarks/dp_sim.py,
+        # mix every 10); with the default -mix_interval 0 (average once at the end: Hivemall's
+        # mappers, each on the plain eta0) the replicas keep the learner's step size
+        self._dp_power = float(c["dp_lr_power"]) if (self._dp() and int(c["mix_interval"]) > 0) else 0.0
+        self._base_eta0, self._base_alpha = self.hyper.eta0, self.hyper.alpha
+        self._set_dp_power(self._dp_power)
+        self._mix_loss = None      # device [sum, rows] of the training loss since the last mix
+        self._prev_mix_loss = None
         nf = num_features
         if nf is None and c["feature_hashing"] > 0:
             nf = 1 << int(c["feature_hashing"])
@@ -160,6 +209,36 @@ class FFMTrainer(Learner):
         self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
         self.rows_seen = 0
         self.grid = 0  # kernel grid override (0 = auto); bounds the Hogwild concurrency
+        self.dp_guard_tripped = False
+
+    def _set_dp_power(self, power: float) -> None:
+        sc = dp_lr_scale(self.mixer.world, power) if self._dp() else 1.0
+        self.hyper.eta0 = self._base_eta0 * sc
+        self.hyper.alpha = self._base_alpha * sc
+        self._dp_power = float(power) if self._dp() else 0.0
+
+    def _dp_guard(self) -> None:
+        """Divergence guard of the N^p step rule, checked at every mix: the mean training loss
+        of the interval since the last mix (over all ranks) must not rise by more than
+        ``DP_GUARD_RISE`` relative to the previous interval's; if it does while p > 0.5, the
+        replicas fall back to p = 0.5 (the drift-matching power, docs/compat.md) for the rest of
+        the run."""
+        if self._mix_loss is None or self._dp_power <= DP_GUARD_POWER:
+            self._mix_loss = None
+            return
+        tot = self._mix_loss.clone()
+        self._mix_loss = None
+        self.mixer.all_reduce_sum([tot])
+        s, n = (float(v) for v in tot.tolist())
+        if n <= 0:
+            return
+        cur = s / n
+        prev, self._prev_mix_loss = self._prev_mix_loss, cur
+        if prev is not None and cur > prev * (1.0 + DP_GUARD_RISE):
+            log.warning("%s: mixed-interval loss rose %.5f -> %.5f at N=%d, p=%.2f: falling back to p=%.2f",
+                        self.NAME, prev, cur, self.mixer.world, self._dp_power, DP_GUARD_POWER)
+            self._set_dp_power(DP_GUARD_POWER)
+            self.dp_guard_tripped = True
 
     # ------------------------------------------------------------------ model state
     def init_state(self, num_features: int, num_fields: int) -> dict:
@@ -247,17 +326,32 @@ class FFMTrainer(Learner):
                     continue
                 part = sub if (r0, r1) == (0, sub.n) else sub.slice(r0, r1)
                 grid = self.grid or (RAMP_GRID if ramp and RAMP_VARIANT < 0 else 0)
+                hot = None
+                if not ramp and self._hot_path():
+                    hot = hot_feature_ids(part.idx, self.num_features)
                 ffm_step(self.state, part.idx, part.fld, part.val, part.y, self.hyper, train=True,
                          loss=None if lb is None else lb[r0:r1], grid=grid,
                          # (an explicit HM_FFM_VARIANT selects the kernel for every row)
-                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None)
+                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None,
+                         hot_ids=hot, hot_flush=HOT_FLUSH)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:
+                if lb is not None and self._dp_power > DP_GUARD_POWER:
+                    part_sum = torch.stack([lb[:sub.n].double().sum(),
+                                            torch.tensor(float(sub.n), dtype=torch.float64, device=lb.device)])
+                    self._mix_loss = part_sum if self._mix_loss is None else self._mix_loss + part_sum
                 self._nbatches = getattr(self, "_nbatches", 0) + 1
                 if self._nbatches % mi == 0:
+                    self._dp_guard()
                     self.mix()
         self._mark_touched(b)
+
+    def _hot_path(self) -> bool:
+        """The fp32 GPU kernel's hot-slot delta path applies (fp32 V in the feature-block layout)."""
+        st = self.state
+        return (HOT_FEATURES > 0 and self.device.type == "cuda" and st["V"].dtype == torch.float32
+                and st["G"].dim() == 2 and _ffm_ops._VARIANT in (0, 9))
 
     def _mark_touched(self, b: FFMBatch) -> None:
         mark_touched(self.touched, b.idx, self.num_features)

@@ -504,7 +504,9 @@ class HistTreeBuilder:
             # or all <= 32 features in one pass (32-B bins rows, one <= 160 KB image per CU)
             FG = next((f for f in (16, 8) if f * q.B * NS * 4 <= 48 * 1024), 4)
             nblk = HIST_BLOCKS
-            if HIST_WIDE and q.d <= 32 and q.dpad % 32 == 0 and q.d * q.B * NS * 4 <= 160 * 1024:
+            # (hm_hist_build instantiates the one-pass kernel for NS <= 4; 5..8 statistics take
+            # the feature-group kernel)
+            if HIST_WIDE and NS <= 4 and q.d <= 32 and q.dpad % 32 == 0 and q.d * q.B * NS * 4 <= 160 * 1024:
                 FG, nblk = 32, HIST_WIDE_BLOCKS
             args = (p(q.bins), q.d, q.dpad, q.B, p(rows), p(seg), n_seg, p(stats), p(smax), NS, FG, p(hist))
             if dev.type == "cuda":
@@ -627,7 +629,10 @@ class HistTreeBuilder:
                         _native.stream_of(dev)), "hm_route_rows")
                     rows, seg = self._partition_gpu(act_rows, node_of_row, nb, lut, L)
                 if arena is None:   # every level's smaller-child histograms, zeroed in one fill
-                    arena = torch.zeros((((1 << self.max_depth) - 1), d, B, NS), dtype=torch.float32, device=dev)
+                    # levels 0 .. max_depth - 1 histogram L = 2^depth children into slots
+                    # [L - 1, 2L - 1); with LAST_FROM_SPLITS the last split level histograms nothing
+                    top = self.max_depth - (1 if LAST_FROM_SPLITS else 0)
+                    arena = torch.zeros((((1 << top) - 1), d, B, NS), dtype=torch.float32, device=dev)
                 Hs = self._hist(rows, seg.contiguous(), L, stats, smax, out=arena[L - 1:2 * L - 1])
                 Hn = torch.empty((2 * L, d, B, NS), dtype=torch.float32, device=dev)
                 _native.check(_native.hip().hm_hist_sibling_heap(

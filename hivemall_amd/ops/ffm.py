@@ -4,6 +4,7 @@ Kernel: ``csrc/kernels/ffm.hip`` (hm_ffm_step).  CPU twin: ``csrc/host/ffm_cpu.c
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 
@@ -134,10 +135,22 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
             torch.zeros(shape, dtype=dtype, device=device))
 
 
+_DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
+
+
+def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
+    buf = _DEFER.get(device)
+    if buf is None or buf.numel() < 1 + B:
+        buf = torch.empty(1 + max(B, 1 << 16), dtype=torch.int32, device=device)
+        _DEFER[device] = buf
+    return buf
+
+
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
              y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
              pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
-             grid: int = 0, variant: int | None = None) -> None:
+             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None,
+             hot_ids: torch.Tensor | None = None, hot_flush: int = 16) -> None:
     """One fused pass over a padded-ELL batch.
 
     state: dict with V, G ([NF, NFLD, Kp] f32 or bf16; either two contiguous tables or the two
@@ -210,7 +223,16 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
     args = (ip.ctypes.data, hp.ctypes.data, p(idx), p(fld), p(val), p(y), p(V), p(G),
             p(state["w"]), p(state["wz"]), p(state["wn"]), p(state["bias"]), p(pred), p(loss))
     if V.is_cuda:
-        rc = _native.hip().hm_ffm_step(*args, _native.stream_of(V.device))
+        if hot is not None:
+            assert hot.dtype == torch.uint8 and hot.numel() >= NF and hot.device == V.device
+        # multi-hot rows (a repeated field or feature) are deferred by the pipelined kernels to
+        # the grouped-update kernel through this buffer (same stream, no host sync)
+        if hot_ids is not None:
+            assert hot_ids.dtype == torch.int32 and hot_ids.device == V.device and hot_ids.numel() <= 64
+        aux = (ctypes.c_void_p * 5)(p(hot), p(_defer_buffer(V.device, B)) if train else None,
+                                    p(hot_ids), hot_ids.numel() if hot_ids is not None else 0,
+                                    int(hot_flush))
+        rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
         if train and hyper.use_bias:
             # w0 = f(z0, n0): the kernel accumulates z0/n0 atomically and its cached bias[0] is

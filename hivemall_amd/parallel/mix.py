@@ -54,6 +54,12 @@ _native.register_hip("hm_mix_merge3", [_native.c_p, _native.c_p, _native.c_p, _n
                                        _native.c_p])
 _native.register_hip("hm_mix_merge", [_native.c_p, _native.c_p, _native.c_p, _native.c_i64,
                                       _native.c_int, _native.c_i64, _native.c_int, _native.c_p])
+_native.register_hip("hm_mix_delta3", [_native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_i64,
+                                       _native.c_int, _native.c_int, _native.c_i64, _native.c_i64, _native.c_int,
+                                       _native.c_int, _native.c_int, _native.c_p])
+
+# fused delta passes (csrc/kernels/mix.hip hm_mix_delta3); 0 = the torch formulation (A/B, tests)
+_FUSED_DELTA = True
 
 _LOWP = (torch.bfloat16, torch.float16)
 
@@ -156,9 +162,26 @@ class _FlatGroup:
         for k, t in enumerate(self.tensors):
             t.copy_(self.seg(self.out, k))
 
+    def _delta3(self, k: int, t: torch.Tensor, mode: int) -> bool:
+        """One fused delta pass over tensor k (hm_mix_delta3); False when it does not apply."""
+        xc, wc = _dtype_code(t.dtype), _dtype_code(self.dtype)
+        v3 = _view3(t) if (_FUSED_DELTA and t.is_cuda and xc is not None and wc is not None) else None
+        if v3 is None:
+            return False
+        b = self.seg(self.base, k)
+        wire = self.seg(self.send if mode == 2 else self.out, k)
+        sent = self.seg(self.send, k) if mode == 4 else None
+        rc = _native.hip().hm_mix_delta3(t.data_ptr(), b.data_ptr(), wire.data_ptr(),
+                                         sent.data_ptr() if sent is not None else None, *v3, mode, xc, wc,
+                                         _native.stream_of(t.device))
+        _native.check(rc, "hm_mix_delta3")
+        return True
+
     def pack_delta(self) -> None:
         """send <- x - base (the local progress since the last consensus), in the wire dtype."""
         for k, t in enumerate(self.tensors):
+            if self._delta3(k, t, 2):
+                continue
             d = self.seg(self.send, k)
             d.copy_(t.to(torch.float32) - self.seg(self.base, k))
 
@@ -167,12 +190,24 @@ class _FlatGroup:
         base <- base + m (rounded to the storage dtype, identically on every rank) and x keeps
         its progress since the snapshot: x <- x + m - delta_local."""
         for k, t in enumerate(self.tensors):
+            if self._delta3(k, t, 4):
+                continue
             m = self.seg(self.out, k).to(torch.float32)
             b = self.seg(self.base, k)
             b.add_(m)
             if t.dtype != torch.float32:
                 b.copy_(b.to(t.dtype))               # exactly representable: untouched x == base
             t.copy_(t.to(torch.float32) + (m - self.seg(self.send, k).to(torch.float32)))
+
+    def merge_delta_sync(self) -> None:
+        """Synchronous delta merge (:meth:`ModelMixer.average_delta`): base <- base + m and
+        x <- base."""
+        for k, t in enumerate(self.tensors):
+            if self._delta3(k, t, 3):
+                continue
+            b = self.seg(self.base, k)
+            b.add_(self.seg(self.out, k).to(torch.float32))
+            t.copy_(b)
 
     def shard_mean(self, world: int, changers: bool = False) -> None:
         """mean = fp32 sum over ranks of recv[r] / world, rounded once to the wire dtype.
@@ -341,14 +376,11 @@ class ModelMixer:
             self._plans[key] = [g]
             self._evict(keep=key)
             return
-        for k, t in enumerate(g.tensors):
-            g.seg(g.send, k).copy_(t.to(torch.float32) - g.seg(g.base, k))
+        g.pack_delta()                  # send <- x - base (one fused pass per tensor)
         self._a2a(g)
         g.shard_mean(self.world)
         self._gather(g)
-        g.base.add_(g.out.to(torch.float32))
-        for k, t in enumerate(g.tensors):
-            t.copy_(g.seg(g.base, k))
+        g.merge_delta_sync()            # base <- base + mean delta; x <- base
         self.calls += 1
         self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
         self.wire_bytes += 2 * (self.world - 1) * g.nbytes // self.world

@@ -40,6 +40,71 @@ def test_ffm_cpu_engine_matches_oracle(use_bias, adagrad):
         np.testing.assert_allclose(t.state[k].numpy(), ref[k], rtol=2e-4, atol=2e-5, err_msg=k)
 
 
+def _multihot_rows(B, F, NF, NFLD, seed):
+    """Rows whose fields repeat (several features of one field) and, now and then, a feature
+    twice in one row."""
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, NF, size=(B, F)).astype(np.int32)
+    fld = rng.integers(0, NFLD, size=(B, F)).astype(np.int32)
+    idx[::5, 1] = idx[::5, 0]                       # a repeated feature
+    val = rng.uniform(0.5, 2.0, size=(B, F)).astype(np.float32)
+    y = np.where(rng.random(B) < 0.4, 1.0, -1.0).astype(np.float32)
+    return idx, fld, val, y
+
+
+@pytest.mark.parametrize("adagrad", ["", "-elementwise_adagrad"])
+def test_ffm_cpu_engine_matches_oracle_multihot_fields(adagrad):
+    """field:index:value rows with repeated fields: each (feature, field)
+    address is updated once per row with the summed gradient of every pair that maps to it."""
+    B, F, NF, NFLD = 40, 7, 32, 3
+    idx, fld, val, y = _multihot_rows(B, F, NF, NFLD, 11)
+    assert any(len(set(r)) < F for r in fld)
+    t = _trainer("cpu", NF, NFLD, extra="-w0 " + adagrad)
+    ref = _np_state(t)
+    h = t.hyper
+    hp = dict(eta0=h.eta0, eps=h.eps, lambda_v=h.lambda_v, alpha=h.alpha, beta=h.beta,
+              lambda1=h.lambda1, lambda2=h.lambda2)
+    ref_loss, _ = ffm_train_rows(ref, idx, y, hp, fld=fld, val=val, use_bias=True)
+    loss = torch.empty(B)
+    ffm_step(t.state, torch.from_numpy(idx), torch.from_numpy(fld), torch.from_numpy(val),
+             torch.from_numpy(y), h, loss=loss)
+    np.testing.assert_allclose(loss.numpy(), ref_loss, rtol=2e-4, atol=2e-5)
+    for k in ("V", "G", "w", "wz", "wn", "bias"):
+        np.testing.assert_allclose(t.state[k].numpy(), ref[k], rtol=2e-4, atol=2e-5, err_msg=k)
+
+
+def test_ffm_oracle_row_gradient_is_the_objective_gradient():
+    """fp64 autograd of one row's FFM objective (logistic loss of p plus lambda_v/2 |V|^2 over
+    the addresses the row touches) equals the oracle's per-address gradient, repeated fields
+    and a repeated feature included."""
+    from tests.oracle.ffm_oracle import row_grads
+
+    rng = np.random.default_rng(3)
+    F, NF, NFLD, K = 6, 7, 3, 4
+    ii = np.array([0, 1, 2, 0, 3, 4])                 # feature 0 twice
+    ff = np.array([0, 1, 1, 2, 1, 0])                 # fields 0 and 1 repeated
+    xx = rng.uniform(0.5, 2.0, size=F)
+    y, lam = 1.0, 0.01
+    V = torch.tensor(rng.normal(size=(NF, NFLD, K)), dtype=torch.float64, requires_grad=True)
+    p = sum((V[ii[a], ff[b]] * V[ii[b], ff[a]]).sum() * xx[a] * xx[b]
+            for a in range(F) for b in range(a + 1, F))
+    touched = sorted({(int(ii[a]), int(ff[b])) for a in range(F) for b in range(F) if a != b})
+    reg = 0.5 * lam * sum((V[i, f] ** 2).sum() for i, f in touched)
+    loss = torch.nn.functional.softplus(-y * p) + reg
+    loss.backward()
+    kappa = float(-y / (1 + torch.exp(y * p)))
+    Vn = V.detach().numpy()
+    g = row_grads(lambda i, f: Vn[i, f], ii, ff, xx, kappa, lam)
+    assert sorted(g) == touched
+    for (i, f), gv in g.items():
+        np.testing.assert_allclose(gv, V.grad[i, f].numpy(), rtol=1e-10, atol=1e-12)
+    # untouched addresses get no gradient
+    mask = np.ones((NF, NFLD), bool)
+    for i, f in touched:
+        mask[i, f] = False
+    assert np.abs(V.grad.numpy()[mask]).max() == 0.0
+
+
 def _to_packed(t):
     """Copy a trainer's split V/G tables into the packed [NF, NFLD, 2, Kp] layout."""
     NF, NFLD, kp = t.state["V"].shape
@@ -350,9 +415,7 @@ def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol):
     """field:index:value rows as the SQL / UDTF path hands them to the kernel: an explicit
     field id per feature (every row a random permutation of the 39 fields) and random values,
     through the pipelined sg32 (fp32) and sg12 (bf16) kernels vs the sequential C++ engine on
-    disjoint-feature rows.  (Two features of one field in a row make two slots of a row the same
-    (feature, field) slot; the kernels update a row's slots in parallel, so that case is
-    last-writer-wins, docs/compat.md.)"""
+    disjoint-feature rows.  (Rows with a repeated field: test_ffm_gpu_multihot_rows_match_cpu_engine.)"""
     g = torch.Generator().manual_seed(7)
     B, F = 384, 39
     idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
@@ -367,6 +430,34 @@ def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol):
     ffm_step(tg.state, idx.cuda(), fld.cuda(), val.cuda(), y.cuda(), tg.hyper, loss=lg)
     torch.cuda.synchronize()
     np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=1e-4, atol=1e-5)
+    _assert_state_close(tc, tg, tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra,tol", [("", 1e-4), (" -bf16_state", 2e-2), (" -elementwise_adagrad", 1e-4)])
+def test_ffm_gpu_multihot_rows_match_cpu_engine(extra, tol):
+    """Rows with repeated fields (39 features over 10 fields) and, in every 4th row, one feature
+    twice: the pipelined kernels defer these rows to the grouped-update kernel, which updates
+    each (feature, field) address once with the summed gradient, as the C++ engine and the
+    oracle do.  Rows use disjoint features, so the Hogwild order does not matter; every 3rd row
+    has distinct fields and takes the pipelined path in the same launch."""
+    g = torch.Generator().manual_seed(17)
+    B, F, NFLD = 384, 39, 39
+    idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
+    idx[::4, 5] = idx[::4, 2]
+    fld = torch.randint(0, 10, (B, F), generator=g, dtype=torch.int32)
+    fld[::3] = torch.stack([torch.randperm(F, generator=g) for _ in range(B)])[::3].to(torch.int32)
+    val = torch.rand(B, F, generator=g) * 3.0 + 0.1
+    y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
+    tc = _trainer("cpu", B * F, NFLD, extra=extra)
+    tg = _trainer("cuda", B * F, NFLD, extra=extra)
+    _copy_state(tc, tg)
+    lc, lg = torch.empty(B), torch.empty(B, device="cuda")
+    for _ in range(2):
+        ffm_step(tc.state, idx, fld, val, y, tc.hyper, loss=lc)
+        ffm_step(tg.state, idx.cuda(), fld.cuda(), val.cuda(), y.cuda(), tg.hyper, loss=lg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(lg.cpu().numpy(), lc.numpy(), rtol=max(tol, 1e-4), atol=1e-5 if tol < 1e-3 else 2e-3)
     _assert_state_close(tc, tg, tol)
 
 

@@ -65,3 +65,53 @@ def test_shard_mean_collectives_through_rccl_one_rank():
         assert pr["mix_ms"] > 0 and pr["mix_payload_bytes"] > 0
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_fused_delta_mixing_bit_identical_to_torch_path():
+    """average_delta (bf16 wire, fp32 replicas) and the overlapped delta-sum merge run as fused
+    HIP passes over the strided V view of the fp32 FFM feature blocks (hm_mix_delta3); through a
+    one-rank nccl group they must produce exactly the torch formulation's bits."""
+    import torch.distributed as dist
+
+    from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.parallel import mix as M
+    from hivemall_amd.parallel.dist import DistContext
+
+    assert not dist.is_initialized()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    old = M._FUSED_DELTA
+    try:
+        ctx = DistContext(0, 1, 0, dev, "nccl")
+        res = {}
+        for fused in (False, True):
+            M._FUSED_DELTA = fused
+            tr = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 14 -seed 3", device=dev)
+            tr.init_state(1 << 14, 39)
+            st = tr.state
+            assert M._view3(st["V"]) is not None and not st["V"].is_contiguous()
+            g = torch.Generator(device="cuda").manual_seed(1)
+            for k in ("wz", "wn", "w"):
+                st[k].copy_(torch.randn(st[k].shape, generator=g, device=dev))
+            tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+            m = M.ModelMixer(ctx, min_world=1)
+            for step in range(3):                      # seed the consensus, then two delta mixes
+                for t in tensors:
+                    t.add_(torch.randn(t.shape, generator=g, device=dev) * 1e-3)
+                m.average_delta(tensors)
+            ov = M.OverlappedMixer(m, mode="sum")
+            for step in range(3):                      # first mix seeds base, then delta-sum mixes
+                ov.start(tensors)
+                for t in tensors:
+                    t.add_(torch.randn(t.shape, generator=g, device=dev) * 1e-3)
+            ov.finish()
+            torch.cuda.synchronize()
+            res[fused] = [t.clone() for t in tensors]
+            del tr, st, tensors, m, ov
+        for a, b in zip(res[False], res[True]):
+            assert torch.equal(a, b)
+    finally:
+        M._FUSED_DELTA = old
+        dist.destroy_process_group()

@@ -447,6 +447,30 @@ def test_rf_ten_classes_gpu_matches_cpu():
     assert (rf.predict(X) == y).mean() > 0.9
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_classes", [5, 7, 8])
+def test_rf_5_to_8_classes_wide_rows_gpu_matches_cpu(n_classes):
+    """5..8 classes on 20 features: the statistics fit one <= 160 KB all-features LDS image, but
+    the one-pass histogram kernel is instantiated for <= 4 statistics only, so these take the
+    feature-group kernel (this shape used to fail with hipErrorInvalidValue)."""
+    from hivemall_amd.models.trees import HistTreeBuilder, Quantized
+
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(12000, 20)).astype(np.float32)
+    y = (np.floor((X[:, 3] + 3) * n_classes / 6).clip(0, n_classes - 1)).astype(int)
+    q = quantize(torch.from_numpy(X), 256)
+    stats = torch.nn.functional.one_hot(torch.from_numpy(y), n_classes).float()
+    trees = []
+    for dev in ("cpu", "cuda"):
+        qd = q if dev == "cpu" else Quantized(q.bins.to(dev), q.edges, q.d, q.B, q.cat)
+        b = HistTreeBuilder(qd, "gini", 5, 2.0, 1.0, seed=11)
+        trees.append(b.build(stats.to(dev)))
+    tc, tg = trees
+    assert list(tc.feature) == list(tg.feature)
+    rf = RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device="cuda").fit(X, y)
+    assert (rf.predict(X) == y).mean() > 0.9
+
+
 def test_heap_layout_tree_compaction_matches_compact_numbering():
     """A heap-layout build (children of node k at 2k+1, 2k+2; slots of parents that did not
     split stay in the arrays) materialises to the per-level build's compact numbering: the
