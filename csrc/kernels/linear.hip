@@ -774,6 +774,95 @@ HM_API int hm_linear_predict(const float* w, int dims, int L, const int64_t* ind
 // Shared-table Hogwild pass (see linear_shared_kernel).  S f32 [R][dims][4], touched u8
 // [R][dims]; W waves (RSW f32 [W][8], loss_out f64 [W]); R = 1 or a multiple of 8 with W / 4 >= R
 // workgroups so that every replica gets waves.
+// ---------------------------------------------------------------------------------------------
+// Mini-batch engine (the general learner's -mini_batch M > 1 on one shared table): Hivemall's
+// mini-batch rule, as the sequential engines run it (csrc/host/linear_cpu.cpp train_replica):
+// the M rows of a batch are scored against the SAME weights, each row's dloss * x is summed per
+// feature, and at the batch end every touched feature takes ONE optimizer step with the batch's
+// mean gradient (sum / M) at the step t of the batch's last row.  The rows of a batch are
+// independent given the weights, so the whole chip works on one batch at a time:
+//   mb_grad:  one wave per row: gather w, dot, row rule; float atomics add dloss * x into GA[i];
+//             the first toucher of a feature (atomicOr on its mark) appends it to the batch list;
+//   mb_apply: one thread per listed feature: optimizer_update with GA[i] / M, clears GA / mark.
+// Two launches per batch, no host sync.  Exact up to the order of the fp32 gradient sums.
+// Eve (a per-row loss feedback chain) is not a batch rule and is refused.
+__global__ __launch_bounds__(256) void linear_mb_grad_kernel(
+    Params P, int dims, int64_t b0, int64_t b1, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
+    const int32_t* __restrict__ order, const float4* __restrict__ S, uint8_t* __restrict__ touched,
+    float* __restrict__ GA, uint32_t* __restrict__ mark, int32_t* __restrict__ list, int32_t* __restrict__ cnt,
+    double* __restrict__ loss_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    float rs[HM_REP_SCALARS] = {};
+    double lsum = 0.0;
+    for (int64_t q = b0 + w0; q < b1; q += nw) {
+        const int64_t row = order ? (int64_t)order[q] : q;
+        const int64_t s = indptr[row], e = indptr[row + 1];
+        float p = 0.f;
+        for (int64_t k = s + lane; k < e; k += 64) {
+            const int i = idx[k];
+            if (i < 0 || i >= dims) continue;
+            p += S[i].x * (val ? val[k] : 1.f);
+        }
+        p = hm::wave_sum(p);
+        const RowCoef c = row_rule(P, p, y[row], 0.f, 0.f, rs);
+        lsum += c.loss;
+        for (int64_t k = s + lane; k < e; k += 64) {
+            const int i = idx[k];
+            if (i < 0 || i >= dims) continue;
+            touched[i] = 1;
+            if (!c.update) continue;
+            atomicAdd(GA + i, c.dloss * (val ? val[k] : 1.f));
+            if (atomicOr(mark + i, 1u) == 0u) list[atomicAdd(cnt, 1)] = i;
+        }
+    }
+    if (lane == 0 && lsum != 0.0) atomicAdd(loss_out, lsum);
+}
+
+__global__ __launch_bounds__(256) void linear_mb_apply_kernel(
+    Params P, float4* __restrict__ S, float* __restrict__ GA, uint32_t* __restrict__ mark,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ cnt, int32_t* __restrict__ cnt_next,
+    float t_last, float inv) {
+    const int n = *cnt;
+    const StepK sk = step_consts(P, t_last);
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const int i = list[k];
+        F4 st = ld4(S + i);
+        optimizer_update(P, st, GA[i] * inv, sk, 1.f);
+        st4(S + i, st);
+        GA[i] = 0.f;
+        mark[i] = 0u;
+    }
+    // the counter the NEXT batch appends to (its last reader was the previous apply launch)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
+}
+
+// One pass of the mini-batch engine over n_rows (step of row q = t0 + q + 1).  GA f32 [dims] and
+// mark u32 [dims] zeroed, list i32 [cap >= min(dims, M * max nnz)], cnt i32 [2] zeroed (all left
+// zeroed again at the end).
+HM_API int hm_linear_train_minibatch(const Params* P, int64_t n_rows, int dims, int64_t t0, int M,
+                                     const int64_t* indptr, const int32_t* idx, const float* val,
+                                     const float* y, const int32_t* order, float* S, uint8_t* touched,
+                                     float* GA, uint32_t* mark, int32_t* list, int32_t* cnt,
+                                     double* loss_out, hipStream_t stream) {
+    if (n_rows <= 0) return 0;
+    if (M <= 1 || dims <= 0 || P->n_labels != 1 || P->algo != A_GENERAL || P->opt == O_EVE)
+        return (int)hipErrorInvalidValue;
+    const int gb = (int)((M + 3) / 4 < 4096 ? (M + 3) / 4 : 4096);     // one wave per row
+    int b = 0;
+    for (int64_t b0 = 0; b0 < n_rows; b0 += M, ++b) {
+        const int64_t b1 = b0 + M < n_rows ? b0 + M : n_rows;
+        int32_t* c = cnt + (b & 1);
+        int32_t* cn = cnt + ((b + 1) & 1);
+        hipLaunchKernelGGL(linear_mb_grad_kernel, dim3(gb), dim3(256), 0, stream, *P, dims, b0, b1, indptr, idx, val, y,
+                           order, reinterpret_cast<const float4*>(S), touched, GA, mark, list, c, loss_out);
+        hipLaunchKernelGGL(linear_mb_apply_kernel, dim3(1024), dim3(256), 0, stream, *P, reinterpret_cast<float4*>(S),
+                           GA, mark, list, c, cn, (float)(t0 + b1), 1.f / (float)(b1 - b0));
+    }
+    HM_LAUNCH_RET();
+}
+
 HM_API int hm_linear_train_shared(const Params* P, int64_t n_rows, int dims, int64_t t0, int W, int R,
                                   int reload, int nt, const int64_t* indptr, const int32_t* idx, const float* val,
                                   const float* y, const int32_t* order, float* S, uint8_t* touched,

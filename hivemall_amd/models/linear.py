@@ -57,8 +57,9 @@ LEARNER_BASE_OPTS = [
     opt("replicas", None, 0, int, "[engine] model replicas (0 = auto; CPU default 1)"),
     opt("engine", None, "auto", str,
         "[engine] GPU execution: replica (private model per wave, mixed), shared (one Hogwild "
-        "table for the whole chip, large -dims), auto (shared when the replicas would exceed "
-        "2 GiB)"),
+        "table for the whole chip, large -dims), minibatch (general learner with -mini_batch > 1: "
+        "the whole chip on each batch, exact mini-batch rule), auto (minibatch for -mini_batch > 1, "
+        "else shared when the replicas would exceed 2 GiB)"),
     opt("shared_replicas", None, 1, int,
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
@@ -356,6 +357,12 @@ class OnlineLinearLearner(Learner):
         self.P.n_labels = L
         R = self._auto_replicas(rows.n)
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
+        if self._use_minibatch(L, mb):
+            nnz = int((rows.indptr[1:] - rows.indptr[:-1]).max().item()) if rows.n else 1
+            self.state = LO.new_minibatch_state(dims, self.device, mb, nnz)
+            if self._warm is not None:
+                self.load_model_table(self._warm)
+            return
         if self._use_shared(R, L, dims, mb):
             try:
                 W = LO.shared_waves(rows.n, int(self.cl["shared_waves"]) or LO.rule_waves(self.P))
@@ -377,13 +384,26 @@ class OnlineLinearLearner(Learner):
         if self._warm is not None:
             self.load_model_table(self._warm)
 
+    def _use_minibatch(self, L: int, mb: int) -> bool:
+        """Mini-batch engine (``-mini_batch M > 1`` of the general learner on a GPU, one table,
+        the whole chip on each batch; ops/linear.py train_pass_minibatch): the default for
+        -mini_batch > 1 unless -engine replica / -replicas ask for per-wave replicas."""
+        eng = str(self.cl["engine"]).lower()
+        if eng == "minibatch":
+            if not (self.device.type == "cuda" and mb > 1 and L == 1 and LO.minibatch_rule(self.P)):
+                raise UDFArgumentException(f"{self.NAME}: -engine minibatch needs a GPU, -mini_batch > 1, "
+                                           "a binary/regression general learner and -opt other than eve")
+            return True
+        return (eng == "auto" and int(self.cl["replicas"]) <= 0 and self.device.type == "cuda"
+                and mb > 1 and L == 1 and LO.minibatch_rule(self.P))
+
     def _use_shared(self, R: int, L: int, dims: int, mb: int) -> bool:
         """Shared-table Hogwild engine: device only, binary/regression rules
         without covariance, per-row updates.  auto picks it when R private replicas of
         ``dims x 16 B`` would exceed 2 GiB (e.g. Hivemall's default 2^24 hashed dims)."""
         eng = str(self.cl["engine"]).lower()
-        if eng not in ("auto", "replica", "shared"):
-            raise UDFArgumentException(f"{self.NAME}: -engine must be auto, replica or shared")
+        if eng not in ("auto", "replica", "shared", "minibatch"):
+            raise UDFArgumentException(f"{self.NAME}: -engine must be auto, replica, shared or minibatch")
         ok = (self.device.type == "cuda" and not self.covar and L == 1 and mb == 1)
         if eng == "shared" and not ok:
             raise UDFArgumentException(f"{self.NAME}: -engine shared needs a GPU, a rule without "
@@ -403,8 +423,12 @@ class OnlineLinearLearner(Learner):
         mb = int(self.cl["mini_batch"]) if self.ALGO == "general" else 1
         iters = int(self.cl["iters"])
         shared = self.state.meta.get("shared", False)
+        minibatch = self.state.meta.get("minibatch", False)
         for ep in self.epochs(iters, data=(rows.indptr, rows.idx, rows.val, rows.y)):
-            if shared:
+            if minibatch:
+                loss = LO.train_pass_minibatch(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
+                                               self.rows_seen, mb)
+            elif shared:
                 loss = LO.train_pass_shared(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
                                             self.rows_seen)
             else:

@@ -136,6 +136,9 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
 
 
 _DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
+# HM_FFM_DEFER=0 (A/B only): no multi-hot detection in the pipelined kernels (a row with a
+# repeated field or feature is then updated slot by slot: racing stores of one address)
+_DEFER_ON = os.environ.get("HM_FFM_DEFER", "1") != "0"
 
 
 def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
@@ -229,7 +232,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
         # the grouped-update kernel through this buffer (same stream, no host sync)
         if hot_ids is not None:
             assert hot_ids.dtype == torch.int32 and hot_ids.device == V.device and hot_ids.numel() <= 64
-        aux = (ctypes.c_void_p * 5)(p(hot), p(_defer_buffer(V.device, B)) if train else None,
+        aux = (ctypes.c_void_p * 5)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
                                     p(hot_ids), hot_ids.numel() if hot_ids is not None else 0,
                                     int(hot_flush))
         rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))

@@ -315,6 +315,55 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     return loss
 
 
+def new_minibatch_state(dims: int, device, max_rows_per_batch: int, max_nnz: int) -> LinearState:
+    """Mini-batch engine state (csrc/kernels/linear.hip hm_linear_train_minibatch): one table
+    S [1, 1, dims, 4] plus the batch buffers (gradient sums, touched marks, the batch's feature
+    list and two list counters), all zeroed."""
+    st = LinearState(torch.zeros((1, 1, dims, 4), dtype=torch.float32, device=device),
+                     torch.zeros((1, dims), dtype=torch.uint8, device=device),
+                     torch.zeros((1, 8), dtype=torch.float32, device=device), False)
+    cap = int(min(dims, max(1, max_rows_per_batch) * max(1, max_nnz)))
+    st.meta.update(minibatch=True, ga=torch.zeros(dims, dtype=torch.float32, device=device),
+                   mark=torch.zeros(dims, dtype=torch.int32, device=device),
+                   list=torch.zeros(cap, dtype=torch.int32, device=device),
+                   cnt=torch.zeros(2, dtype=torch.int32, device=device))
+    return st
+
+
+def minibatch_rule(P: LinParams) -> bool:
+    """Rules of the mini-batch engine: the general learner, one label, any optimizer but Eve
+    (whose per-row loss feedback is a sequential chain, not a batch rule)."""
+    return P.algo == ALGOS["general"] and P.n_labels == 1 and P.opt != OPTIMIZERS["eve"]
+
+
+def train_pass_minibatch(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.Tensor,
+                         val: torch.Tensor | None, y: torch.Tensor, t0: int, M: int,
+                         order: torch.Tensor | None = None) -> torch.Tensor:
+    """One pass of the mini-batch engine (batches of M rows in order; row q's step t0 + q + 1).
+    Returns the pass's loss sum (device, [1])."""
+    n = indptr.numel() - 1
+    dev = st.device
+    assert dev.type == "cuda" and st.meta.get("minibatch"), "mini-batch engine state on a GPU"
+    assert indptr.dtype == torch.int64 and idx.dtype == torch.int32 and y.dtype == torch.float32
+    for t in (indptr, idx, val, y, order):
+        if t is not None:
+            assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    if n > 0:
+        nnz = int((indptr[1:] - indptr[:-1]).max().item())
+        need = min(st.dims, M * max(1, nnz))
+        if st.meta["list"].numel() < need:
+            st.meta["list"] = torch.zeros(need, dtype=torch.int32, device=dev)
+    loss = torch.zeros(1, dtype=torch.float64, device=dev)
+    p = _native.ptr
+    rc = _native.hip().hm_linear_train_minibatch(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), int(M),
+                                                 p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
+                                                 p(st.touched), p(st.meta["ga"]), p(st.meta["mark"]),
+                                                 p(st.meta["list"]), p(st.meta["cnt"]), p(loss),
+                                                 _native.stream_of(dev))
+    _native.check(rc, "hm_linear_train_minibatch")
+    return loss
+
+
 def mix_reduce(st: LinearState, kld: bool):
     """Compact per-element sums (num, den, cnt) over the touching replicas."""
     R, L, dims = st.R, st.L, st.dims
@@ -396,6 +445,8 @@ _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
                                               C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 4
                      + [_P, _P])
+_native.register_hip("hm_linear_train_minibatch", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int]
+                     + [_P] * 12 + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _native.register_hip("hm_linear_mix_apply", [_P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P])
 _native.register_hip("hm_linear_predict", [_P, C.c_int, C.c_int, _P, _P, _P, _native.c_i64, _P, _P, _P, _P])

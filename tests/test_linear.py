@@ -268,3 +268,30 @@ def test_gpu_shared_engine_hashed_2p24_logloss_parity(opts):
         s = m.decision_function(rows=test.to(dev)).cpu()
         res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
     assert abs(res["cpu"] - res["cuda"]) < 5e-3, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opts", ["-opt adam -eta0 0.01", "-opt sgd -eta0 0.05", "-opt rmsprop -eta0 0.01",
+                                  "-opt adadelta", "-opt adagrad", "-opt momentum -eta0 0.005"])
+def test_gpu_minibatch_engine_matches_sequential_minibatch_learner(opts):
+    """-mini_batch M at Hivemall's default -dims 2^24: the GPU mini-batch engine (the whole chip on
+    each batch of M rows; csrc/kernels/linear.hip hm_linear_train_minibatch) runs the sequential
+    learner's mini-batch rule — every row scored against the batch's weights, one optimizer step
+    per touched feature with the batch's mean gradient — so held-out logloss and weights match the
+    CPU engine's -mini_batch M run up to the order of the fp32 gradient sums."""
+    rows = _criteo_rows(300000, 24, seed=5)
+    test = _criteo_rows(50000, 24, seed=99)
+    yy = (test.y > 0).float()
+    res, ws = {}, {}
+    for dev in ("cpu", "cuda"):
+        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216 -iters 1 -mini_batch 1024", device=dev)
+        m.fit(rows=rows.to(dev))
+        if dev == "cuda":
+            assert m.state.meta.get("minibatch")
+        s = m.decision_function(rows=test.to(dev)).cpu()
+        res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(s, yy).item()
+        ws[dev] = m.weights()[0][0].cpu()
+    assert abs(res["cpu"] - res["cuda"]) < 1e-3, res
+    touched = ws["cpu"] != 0
+    rel = (ws["cuda"][touched] - ws["cpu"][touched]).abs().max() / ws["cpu"][touched].abs().max()
+    assert rel < 2e-2, float(rel)
