@@ -213,29 +213,12 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     if state == "fp32" and dev.type == "cuda" and ramp_rows > 0 and ffm_model.RAMP_VARIANT >= 0:
         ramp_steps = min(args.warmup, (ramp_rows + B - 1) // B)   # never inside the timed region
 
-    # hot-slot deltas of the fp32 kernel (models/ffm.py HOT_FEATURES): the hot set of each resident
-    # batch (its most frequent features, drawn from a row sample) is data preparation like the
-    # padded-ELL packing; the learner draws it when a batch is first used, here every resident
-    # batch's before timing (its host read would otherwise sit between two timed launches)
-    hot_sets: dict = {}
-    use_hot = (state == "fp32" and dev.type == "cuda" and ffm_model.HOT_FEATURES > 0
-               and args.adagrad == "slot" and args.layout == "packed")
-    if use_hot:
-        for k in range(nres):
-            hot_sets[k * B] = ffm_model.hot_feature_ids(idx[k * B:(k + 1) * B], NF)
-
     def step(i):
         s = (i % nres) * B
         ramp = i < ramp_steps
-        hot = None
-        if use_hot and not ramp:
-            if s not in hot_sets:
-                hot_sets[s] = ffm_model.hot_feature_ids(idx[s:s + B], NF)
-            hot = hot_sets[s]
         ffm_step(st, idx[s:s + B], None if fld is None else fld[s:s + B],
                  None if val is None else val[s:s + B], y[s:s + B], hyper, train=True,
-                 grid=args.grid, loss=loss_buf, variant=ffm_model.RAMP_VARIANT if ramp else None,
-                 hot_ids=hot, hot_flush=ffm_model.HOT_FLUSH)
+                 grid=args.grid, loss=loss_buf, variant=ffm_model.RAMP_VARIANT if ramp else None)
         if loss_buf is not None:
             step_loss.append(loss_buf.mean())          # device scalar, read after timing
         if world > 1 and (i + 1) % args.mix_every == 0:
@@ -294,8 +277,7 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     out = {"elapsed_s": elapsed, "ms_per_step": 1000.0 * elapsed / max(1, args.steps),
            "rows_per_s": float(B) * world * args.steps / elapsed, "mixes_timed": mixes_timed,
            "mixed_bytes": int(sum(t.numel() * t.element_size() for t in mix_tensors)),
-           "dp_lr_scale": sc, "ramp_steps": ramp_steps,
-           "hot_features": max((0 if h is None else int(h.numel()) for h in hot_sets.values()), default=0)}
+           "dp_lr_scale": sc, "ramp_steps": ramp_steps}
     if os.environ.get("HM_TRACE"):
         # host + device timeline of a few extra steps (outside the timed region)
         from hivemall_amd.prof import host_trace
@@ -331,12 +313,6 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     mixer.release()
     del tr, st
     return out
-
-
-def ffm_model_flush() -> int:
-    from hivemall_amd.models import ffm as ffm_model
-
-    return ffm_model.HOT_FLUSH
 
 
 def main(argv=None):
@@ -435,8 +411,6 @@ def main(argv=None):
                 "mix_wire": main_run["mix_wire"],
                 "dp_lr_scale": round(main_run["dp_lr_scale"], 4),
                 "early_ramp_warmup_steps": main_run["ramp_steps"],
-                "hot_slot_features": main_run["hot_features"],
-                "hot_slot_flush_rows": ffm_model_flush(),
                 "resident_batches": nres,
             },
             "rccl_world": world if ctx.backend == "nccl" else None,

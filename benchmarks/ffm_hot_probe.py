@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--variant", type=int, default=8)
     ap.add_argument("--reps", type=int, default=1)
-    ap.add_argument("--lds", default="", help="LDS-delta path (HOTL): H:flush pairs, e.g. 27:16,27:32")
+    ap.add_argument("--plain", default="", help="kernel variants without a hot set, e.g. 0,10")
     a = ap.parse_args()
     dev = torch.device("cuda")
     idx, fld, val, y = (t.to(dev) for t in criteo_ffm(B * NRES, BITS, seed=1000))
@@ -45,7 +45,7 @@ def main():
     order = torch.argsort(cnt, descending=True)
     tot = float(cnt.sum())
     yy = (ey > 0).float()
-    def run(H, var, hot, hot_ids, flush):
+    def run(H, var, hot):
         tr = FFMTrainer(OPTS, device=dev)
         tr.init_state(1 << BITS, F)
         torch.cuda.synchronize()
@@ -57,8 +57,7 @@ def main():
             s = (i % NRES) * B
             v = ffm_model.RAMP_VARIANT if i == 0 else var
             ffm_step(tr.state, idx[s:s + B], fld[s:s + B], val[s:s + B], y[s:s + B], tr.hyper,
-                     train=True, variant=v, hot=hot, hot_ids=None if i == 0 else hot_ids,
-                     hot_flush=flush)
+                     train=True, variant=v, hot=hot)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         pred = torch.empty(B, device=dev)
@@ -67,14 +66,10 @@ def main():
         return B * (a.steps - a.warmup) / dt / 1e6, ll
 
     for rep in range(a.reps):
-        for hf in [x for x in a.lds.split(",") if x]:
-            H, flush = (int(v) for v in hf.split(":"))
-            hot_ids = order[:H].to(torch.int32).contiguous() if H > 0 else None
-            cover = float(cnt[order[:H]].sum()) / tot if H > 0 else 0.0
-            rate, ll = run(H, 0, None, hot_ids, flush)
-            print(json.dumps({"mode": "lds", "H": H, "flush": flush, "row_cover": round(cover, 4), "rep": rep,
-                              "rows_per_s": round(rate, 2), "logloss_heldout": round(ll, 5),
-                              "gap_vs_seq": round(ll - SEQ, 5)}), flush=True)
+        for v in [int(x) for x in a.plain.split(",") if x]:
+            rate, ll = run(0, v, None)
+            print(json.dumps({"mode": "plain", "variant": v, "rep": rep, "rows_per_s": round(rate, 2),
+                              "logloss_heldout": round(ll, 5), "gap_vs_seq": round(ll - SEQ, 5)}), flush=True)
         for H in [int(h) for h in a.hs.split(",") if h]:
             hot = torch.zeros(1 << BITS, dtype=torch.uint8, device=dev)
             if H > 0:

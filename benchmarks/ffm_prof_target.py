@@ -1,8 +1,8 @@
 """Small fixed FFM workload for rocprofv3 counter runs: 6 train steps of 262,144 rows at the
 driver's headline config by default — ``criteo_ffm`` rows (explicit fields and values: the fld /
 val DMAs), fp32 V + per-slot fp32 G (``ffm_pipe_sg32_kernel``).  BF16=1 selects bf16 state
-(``ffm_pipe_sg12_kernel``), DATA=criteo_like the round-1..3 implicit-field rows, HOT=1 the
-hot-slot LDS delta path (models/ffm.py HOT_FEATURES)."""
+(``ffm_pipe_sg12_kernel``), DATA=criteo_like the round-1..3 implicit-field rows, HM_FFM_VARIANT a
+kernel variant (csrc/kernels/ffm.hip hm_ffm_step)."""
 import os
 import sys
 
@@ -10,7 +10,6 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hivemall_amd.io.synthetic import criteo_ffm, criteo_like  # noqa: E402
-from hivemall_amd.models import ffm as ffm_model  # noqa: E402
 from hivemall_amd.models.ffm import FFMTrainer  # noqa: E402
 from hivemall_amd.ops.ffm import ffm_step  # noqa: E402
 
@@ -24,12 +23,10 @@ else:
 t = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 20" +
                (" -bf16_state" if os.environ.get("BF16") == "1" else ""), device=dev)
 t.init_state(1 << 20, 39)
-hot = os.environ.get("HOT") == "1"
-hs = [ffm_model.hot_feature_ids(idx[s:s + B], 1 << 20) if hot else None for s in (0, B)]
 for i in range(6):
     s = (i % 2) * B
     ffm_step(t.state, idx[s:s + B], None if fld is None else fld[s:s + B],
-             None if val is None else val[s:s + B], y[s:s + B], t.hyper, hot_ids=hs[i % 2],
-             hot_flush=ffm_model.HOT_FLUSH)
+             None if val is None else val[s:s + B], y[s:s + B], t.hyper,
+             variant=int(os.environ.get("HM_FFM_VARIANT", "0")))
 torch.cuda.synchronize()
 print("done")

@@ -68,8 +68,7 @@ struct FFMParams {
     // trains them in list mode (it implements the grouped update).  null: no deferral.
     int32_t* defer;
     int list_mode;
-    const int32_t* hot_ids;        // ffm_pipe_sg32_kernel HOTL: hot feature ids (<= 64), or null
-    int hot_n, hot_flush;          // their count; rows between the blocks' delta flushes
+    int xcd_only;                  // experiment: only blocks with blockIdx % 8 == 0 work (one XCD)
 };
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
@@ -1019,17 +1018,7 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
-// HOTL = 1: the slots of the hot features (P.hot_ids, the most frequent features of the pass) are
-// never read-modify-written in HBM by a row.  The block keeps its own pending delta of each hot
-// slot in LDS (s_hv / s_hg), reads a hot slot as (DMA'd global value + own delta), updates the
-// delta, and every P.hot_flush rows (and at its last row) adds the deltas to HBM with float
-// atomics.  Concurrent rows of other blocks then lose none of each other's updates on the slots
-// nearly every row touches (the Hogwild store keeps one of the racing rows' updates: the
-// same-stream logloss gap, docs/perf_notes.md), at the cost of up to hot_flush rows of staleness
-// per block.  LDS: HOT_SLOTS x 20 B more, still 2 blocks/CU.
-constexpr int HOT_SLOTS = 1080;       // hot feature blocks x field stride (27 x 40 at Criteo)
-
-template <int NS, typename OT, int TPB = 256, int ATOM = 0, int HOTL = 0>
+template <int NS, typename OT, int TPB = 256, int ATOM = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1044,16 +1033,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
     __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
     __shared__ int s_rep[TPB / 64];                                   // per wave: a multi-hot slot
-    __shared__ __attribute__((aligned(16))) float4 s_hv[HOTL ? HOT_SLOTS : 1];   // hot V deltas
-    __shared__ float s_hg[HOTL ? HOT_SLOTS : 1];                      // hot G deltas
-    __shared__ unsigned long long s_hmask[2];                         // row positions holding a hot feature
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
     const OT vfs = (OT)P.fstride * 16u;                  // V bytes between features
     const OT gfs = (OT)P.gstride * 4u;                   // G bytes between features
-    const int G = gridDim.x;
+    // xcd_only (experiment): the work of a grid of gridDim.x / 8 blocks, done by the blocks the
+    // round-robin dispatch puts on XCD 0 (block b on XCD b % 8); the others exit at once
+    if (P.xcd_only && (blockIdx.x & 7) != 0) return;
+    const int G = P.xcd_only ? (int)(gridDim.x >> 3) : (int)gridDim.x;
+    const int bid = P.xcd_only ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
 
@@ -1065,16 +1055,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     }
 #define SA(j) (ab[j] & 0xFF)
 #define SB(j) (ab[j] >> 8)
-    // hot features: H blocks of P.fstride slots in LDS; lane h of wave W_META holds hot id h
-    const int H = HOTL ? min(P.hot_n, HOT_SLOTS / P.fstride) : 0;
-    int hot_lane = -2;
-    if (HOTL) {
-        for (int q = tid; q < HOT_SLOTS; q += TPB) {
-            s_hv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_hg[q] = 0.f;
-        }
-        if (wave == W_META && lane < H) hot_lane = P.hot_ids[lane];
-    }
 
     auto dma_meta = [&](int bf, int row) {
         if (wave == W_DMA && lane < F && row < P.B) {
@@ -1092,19 +1072,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 int rf = fld ? s_mr[bf][1][lane] : lane;
                 float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
                 if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
-                int hb = (ATOM == 2 && ri >= 0) ? (int)P.hot[ri] : 0;
-                if (HOTL) {
-                    hb = -1;
-                    for (int h = 0; h < H; ++h)
-                        if (__builtin_amdgcn_readlane(hot_lane, h) == ri && ri >= 0) hb = h;
-                }
+                const int hb = (ATOM == 2 && ri >= 0) ? (int)P.hot[ri] : 0;
                 s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), hb);
                 sq = rx * rx;
-            }
-            if (HOTL) {
-                const int hid = lane < F ? s_m[bf][lane].w : -1;
-                const unsigned long long hm_ = __ballot(hid >= 0);
-                if (lane == 0) s_hmask[bf] = hm_;
             }
             const float tot = hm::wave_sum_uniform(sq);
             if (lane == 0) s_red[TPB / 64 + bf] = (P.norm && tot > 0.f) ? rsqrtf(tot) : 1.f;
@@ -1144,7 +1114,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         }
     };
 
-    int row = blockIdx.x;
+    int row = bid;
     if (row >= P.B) return;
     dma_meta(0, row);
     __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1164,7 +1134,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     float fg[NS];
     OT fo[NS];
     uint32_t fwd = 0u;
-    int it = 0;
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
@@ -1181,13 +1150,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 OT ov, og;
                 float xq;
                 if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) { v = fv[j]; cg[j] = fg[j]; }
-            }
-            if (HOTL && (s_hmask[cur] >> SA(j) & 1ull) && tid + j * TPB < FF) {
-                // a hot slot: the global value plus this block's pending delta
-                const int e = s_m[cur][SA(j)].w * P.fstride + s_m[cur][SB(j)].y;
-                const float4 d = s_hv[e];
-                v = make_float4(v.x + d.x, v.y + d.y, v.z + d.z, v.w + d.w);
-                cg[j] += s_hg[e];
             }
             if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = v;
         }
@@ -1213,12 +1175,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         float xab[NS];
         float part = 0.f;
         int rep = 0;
+        float4 rv[NS];          // ATOM = 3: the slot's V / G re-read here, updated by the delta in E
+        float rgv[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT ov, og;
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
+            if (ATOM == 3 && k != 0u) {
+                rv[j] = *reinterpret_cast<const float4*>(vb + ov);
+                rgv[j] = *reinterpret_cast<const float*>(gb + og);
+            }
             if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * TPB;
             const float4 pv = s_t[s < FF ? s : 0];
@@ -1263,17 +1231,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
-                if (HOTL && (s_hmask[cur] >> SA(j) & 1ull)) {
-                    // hot slot: only this block's LDS delta moves (single writer in the row)
-                    const int e = s_m[cur][SA(j)].w * P.fstride + s_m[cur][SB(j)].y;
-                    const float4 hd = s_hv[e];
-                    s_hv[e] = make_float4(hd.x + (o0.x - cv.x), hd.y + (o0.y - cv.y), hd.z + (o1.x - cv.z),
-                                          hd.w + (o1.y - cv.w));
-                    s_hg[e] += gs - cg[j];
-                    continue;
+                if (ATOM == 3) {
+                    // the step taken from the row's snapshot, applied to the value re-read during
+                    // the forward pass: concurrent rows' updates are lost only inside that
+                    // shorter window (the snapshot is DMA'd one row ahead)
+                    fv[j] = make_float4(rv[j].x + (o0.x - cv.x), rv[j].y + (o0.y - cv.y), rv[j].z + (o1.x - cv.z),
+                                        rv[j].w + (o1.y - cv.w));
+                    fg[j] = rgv[j] + (gs - cg[j]);
+                } else {
+                    fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
+                    fg[j] = gs;
                 }
-                fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
-                fg[j] = gs;
                 fo[j] = ov;
                 fwd |= 1u << j;
                 if (ATOM == 1 || (ATOM == 2 && s_m[cur][SA(j)].w != 0)) {
@@ -1290,7 +1258,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     continue;
                 }
                 *reinterpret_cast<float4*>(vb + ov) = fv[j];
-                *reinterpret_cast<float*>(gb + og) = gs;
+                *reinterpret_cast<float*>(gb + og) = fg[j];
             }
             // (The pad slots and block tails are never read.  Zeroing them so that every line a
             // row touches is written whole cost 1.5 %: 73.7-74.0 vs 75.0-75.2 M rows/s, same
@@ -1318,31 +1286,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
         if (more) dma_lin(nxt);
-        // ---- G (HOTL): every hot_flush rows and after the last row, the hot deltas go to HBM
-        //      (float atomics, each wave-instruction over consecutive words of one feature's V
-        //      or G region) and the LDS deltas restart from 0 ----
-        if (HOTL && P.train && (++it >= P.hot_flush || !more)) {
-            it = 0;
-            bar_raw();
-            const int nv = H * P.fstride * 4;
-            for (int q = tid; q < nv; q += TPB) {
-                const int h = q / (P.fstride * 4), r = q - h * (P.fstride * 4);
-                float* pd = reinterpret_cast<float*>(s_hv) + h * P.fstride * 4 + r;
-                const float d = *pd;
-                if (d != 0.f) {
-                    atomicAdd(reinterpret_cast<float*>(vb + (OT)(uint32_t)P.hot_ids[h] * vfs) + r, d);
-                    *pd = 0.f;
-                }
-            }
-            for (int q = tid; q < H * P.fstride; q += TPB) {
-                const int h = q / P.fstride, f = q - h * P.fstride;
-                const float d = s_hg[q];
-                if (d != 0.f) {
-                    atomicAdd(reinterpret_cast<float*>(gb + (OT)(uint32_t)P.hot_ids[h] * gfs) + f, d);
-                    s_hg[q] = 0.f;
-                }
-            }
-        }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
 #undef SA
@@ -1663,13 +1606,8 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
-    const bool hotl = P.hot_ids != nullptr && P.hot_n > 0 && P.train && (variant == 0 || variant == 9);
 #define HM_P32(NSV) do { \
-        if (hotl && wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, 256, 0, 1>), dim3(blocks), dim3(256), 0, \
-                                             stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else if (hotl) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1>), dim3(blocks), dim3(256), 0, \
-                                          stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
         else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 1>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
@@ -1677,6 +1615,9 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (variant == 8 && P.hot) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 2>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
+        else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 3>), dim3(blocks), \
+                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                   bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
@@ -1798,11 +1739,9 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // registers instead of an LDS landing zone (53 KB per block: 3 rows in flight per CU instead of
 // 2): 73.6-73.8 vs 73.9-74.2 M rows/s (profiles/r4/ffm_register_g_ab.log) — more rows in flight
 // per CU does not move this kernel.
-// aux (host array of 5 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
-// or null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
-// updated slot by slot by the pipelined kernels: racing stores of one address, one wins);
-// aux[2] = hot feature ids int32 [<= 64] for the fp32 kernel's LDS delta path (HOTL) or null,
-// aux[3] = their count, aux[4] = rows between a block's hot-delta flushes.
+// aux (host array of 2 device pointers, or null): aux[0] = per-feature hot flags (variant 8) or
+// null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
+// updated slot by slot by the pipelined kernels: racing stores of one address, one wins).
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, void* const* aux,
@@ -1811,10 +1750,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.hot = aux ? reinterpret_cast<const uint8_t*>(aux[0]) : nullptr;
     P.defer = aux ? reinterpret_cast<int32_t*>(aux[1]) : nullptr;
     P.list_mode = 0;
-    P.hot_ids = aux ? reinterpret_cast<const int32_t*>(aux[2]) : nullptr;
-    P.hot_n = aux ? (int)reinterpret_cast<intptr_t>(aux[3]) : 0;
-    P.hot_flush = aux ? (int)reinterpret_cast<intptr_t>(aux[4]) : 0;
-    if (P.hot_n > 64 || (P.hot_ids && P.hot_flush <= 0)) return (int)hipErrorInvalidValue;
     P.B = ip[0]; P.F = ip[1]; P.num_features = ip[2]; P.num_fields = ip[3]; P.Kp = ip[4];
     P.classification = ip[5]; P.train = ip[6]; P.use_linear = ip[7]; P.use_bias = ip[8];
     P.norm = ip[9];
@@ -1831,6 +1766,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.vpad = ip[19];
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
+    P.xcd_only = ip[22];
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.vfe = (long long)P.fstride * P.sstride;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];

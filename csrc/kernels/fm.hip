@@ -270,9 +270,8 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
         // own deltas to its copy (lane 0), so only the other waves' updates are seen late.  The
         // re-read comes early when the wave's own steps drift one way (|sum| > w0_tol x eta):
         // the bias is then moving, and every other wave's copy with it (early training)
-        const float eta_r = fm_eta(P, (float)(t0 + row + 1));
         const bool w0_ref = P.w0_every <= 1 || since + 1 >= P.w0_every ||
-                            (P.w0_tol > 0.f && fabsf(acc) > P.w0_tol * eta_r);
+                            (P.w0_tol > 0.f && fabsf(acc) > P.w0_tol * fm_eta(P, (float)(t0 + row + 1)));
         float x = i >= 0 ? cx : 0.f;
         // ---- gathers of this row (the only loads the forward waits for) ----
         VRow<KP, BF16> vr;

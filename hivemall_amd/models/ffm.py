@@ -93,45 +93,6 @@ DP_GUARD_RISE = 0.02
 DP_GUARD_POWER = 0.5
 
 
-# Hot-slot deltas of the fp32 kernel (csrc/kernels/ffm.hip ffm_pipe_sg32_kernel HOTL): the
-# HOT_FEATURES most frequent features of a batch have their (feature, field) slots updated through
-# per-block LDS deltas flushed to HBM by float atomics every HOT_FLUSH rows of a block, instead of
-# Hogwild stores that lose concurrent rows' updates.  HM_FFM_HOT=0 disables.
-HOT_FEATURES = int(os.environ.get("HM_FFM_HOT", "27"))
-HOT_FLUSH = int(os.environ.get("HM_FFM_HOT_FLUSH", "16"))
-_HOT_CACHE: dict = {}
-
-
-def hot_feature_ids(idx: torch.Tensor, num_features: int, n: int | None = None,
-                    rows_in_flight: int = 512) -> torch.Tensor | None:
-    """The at most HOT_FEATURES most frequent features of the padded-ELL batch ``idx`` that more
-    than one of the kernel's ~``rows_in_flight`` concurrent rows is expected to hold (count >=
-    rows / rows_in_flight), as int32 on idx's device; None when there are none.  Counted from a
-    strided sample of the rows (a full bincount of a large batch costs as much as a step); cached
-    per index tensor (weakly, with its version counter)."""
-    import weakref
-
-    H = min(HOT_FEATURES, 64)
-    if H <= 0 or idx.numel() == 0:
-        return None
-    key = (idx.data_ptr(), idx.numel(), idx._version, num_features)
-    hit = _HOT_CACHE.get(key)
-    if hit is not None and hit[0]() is idx:
-        return hit[1]
-    rows = idx.shape[0]
-    stride = max(1, rows // (1 << 16))
-    ids = idx[::stride].reshape(-1).long()
-    ids = ids[(ids >= 0) & (ids < num_features)]
-    cnt = torch.bincount(ids, minlength=num_features)
-    vals, feats = torch.topk(cnt, min(H, num_features))
-    feats = feats[vals * stride >= max(2, rows // max(1, rows_in_flight))].to(torch.int32).contiguous()
-    res = feats if feats.numel() else None
-    if len(_HOT_CACHE) > 16:
-        _HOT_CACHE.clear()
-    _HOT_CACHE[key] = (weakref.ref(idx), res)
-    return res
-
-
 def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
     """Step-size factor of a data-parallel replica (1.0 on one rank)."""
     return float(world) ** float(power) if world > 1 else 1.0
@@ -326,14 +287,10 @@ class FFMTrainer(Learner):
                     continue
                 part = sub if (r0, r1) == (0, sub.n) else sub.slice(r0, r1)
                 grid = self.grid or (RAMP_GRID if ramp and RAMP_VARIANT < 0 else 0)
-                hot = None
-                if not ramp and self._hot_path():
-                    hot = hot_feature_ids(part.idx, self.num_features)
                 ffm_step(self.state, part.idx, part.fld, part.val, part.y, self.hyper, train=True,
                          loss=None if lb is None else lb[r0:r1], grid=grid,
                          # (an explicit HM_FFM_VARIANT selects the kernel for every row)
-                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None,
-                         hot_ids=hot, hot_flush=HOT_FLUSH)
+                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None)
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:
@@ -346,12 +303,6 @@ class FFMTrainer(Learner):
                     self._dp_guard()
                     self.mix()
         self._mark_touched(b)
-
-    def _hot_path(self) -> bool:
-        """The fp32 GPU kernel's hot-slot delta path applies (fp32 V in the feature-block layout)."""
-        st = self.state
-        return (HOT_FEATURES > 0 and self.device.type == "cuda" and st["V"].dtype == torch.float32
-                and st["G"].dim() == 2 and _ffm_ops._VARIANT in (0, 9))
 
     def _mark_touched(self, b: FFMBatch) -> None:
         mark_touched(self.touched, b.idx, self.num_features)

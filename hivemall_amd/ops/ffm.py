@@ -152,8 +152,7 @@ def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
              y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
              pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
-             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None,
-             hot_ids: torch.Tensor | None = None, hot_flush: int = 16) -> None:
+             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None) -> None:
     """One fused pass over a padded-ELL batch.
 
     state: dict with V, G ([NF, NFLD, Kp] f32 or bf16; either two contiguous tables or the two
@@ -219,7 +218,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0],
+                   G.stride(1) if slot_g else 0, int(os.environ.get("HM_FFM_XCD_ONLY", "0"))],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
@@ -230,11 +229,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
             assert hot.dtype == torch.uint8 and hot.numel() >= NF and hot.device == V.device
         # multi-hot rows (a repeated field or feature) are deferred by the pipelined kernels to
         # the grouped-update kernel through this buffer (same stream, no host sync)
-        if hot_ids is not None:
-            assert hot_ids.dtype == torch.int32 and hot_ids.device == V.device and hot_ids.numel() <= 64
-        aux = (ctypes.c_void_p * 5)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
-                                    p(hot_ids), hot_ids.numel() if hot_ids is not None else 0,
-                                    int(hot_flush))
+        aux = (ctypes.c_void_p * 2)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None)
         rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
         if train and hyper.use_bias:

@@ -37,15 +37,19 @@ class FMHyper:
 # delayed view turns the waves' bias steps into an overshoot (200 K rows, bf16 V: held-out 0.546
 # vs 0.486 for the 8-mapper average), so a pass that starts within the first W0_WARM_ROWS rows of
 # the stream re-reads every row.
-# Round 5: the re-read is adaptive instead of "every row for the first 2^20 rows": a wave re-reads
-# the shards after at most W0_EVERY rows, or as soon as its own bias steps since the last re-read
-# add up to more than W0_TOL x eta in one direction (the bias is drifting, so every other wave's
-# view of it is drifting too: early training re-reads nearly every row, a calibrated bias every
-# W0_EVERY rows).  HM_FM_W0_EVERY overrides the row bound, clamped to W0_EVERY_MAX: the 32-row
-# setting of the cliff above is not reachable.
+# Round 5: HM_FM_W0_EVERY overrides the row bound, clamped to W0_EVERY_MAX, so the 32-row setting
+# of the cliff above is not reachable.  An adaptive re-read (also re-read as soon as the wave's
+# own bias steps since the last re-read add up to more than W0_TOL x eta) was measured and is off
+# by default: on 3 M rows (2^20 features, bf16 V; benchmarks/fm_w0_probe.py,
+# profiles/r5/fm_w0_probe.jsonl) held-out logloss vs the 8-mapper average is +2.87e-3 re-reading
+# every row, +2.89e-3 every 8 rows after the warm rows, +3.5e-3 with tol 2 and +3.2e-3 with tol 0.5
+# from row 0 — the bias schedule is not what separates the GPU from the mapper average there, and
+# the adaptive rule alone from row 0 lost early (200 K rows fp32: 0.510 vs 0.486,
+# profiles/r5/pytest_gpu_a.log).  The first W0_WARM_ROWS rows re-read every row.
 W0_EVERY = 8
 W0_EVERY_MAX = 16
-W0_TOL = float(os.environ.get("HM_FM_W0_TOL", "2.0"))
+W0_WARM_ROWS = 1 << 20
+W0_TOL = float(os.environ.get("HM_FM_W0_TOL", "0"))
 
 
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
@@ -72,7 +76,8 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),
-                   max(1, min(W0_EVERY_MAX, int(os.environ.get("HM_FM_W0_EVERY", str(W0_EVERY)))))],
+                   max(1, min(W0_EVERY_MAX, int(os.environ.get(
+                       "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1)))))],
                   dtype=np.int32)
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,

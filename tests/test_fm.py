@@ -115,13 +115,14 @@ def test_fm_gpu_logloss_parity(fp32):
 
 @pytest.mark.gpu
 def test_fm_gpu_logloss_parity_past_2p20_rows():
-    """The stale-bias regime (ops/fm.py W0_EVERY: a wave re-reads the 64 bias shards at most every
-    8 rows, earlier when its own bias steps drift, W0_TOL) on a stream well past 2^20 rows, bf16 V
-    (the config-2 engine): held-out logloss within SURVEY.md's bf16 tolerance 3e-3 of Hivemall's
-    8-mapper average on the same rows."""
+    """The stale-bias regime (ops/fm.py W0_EVERY: past the first 2^20 rows a wave re-reads the 64
+    bias shards every 8 rows, and no override reaches the 32-row cliff) on a stream well past
+    2^20 rows, bf16 V (the config-2 engine): held-out logloss within SURVEY.md's bf16 tolerance
+    3e-3 of Hivemall's 8-mapper average on the same rows (measured +2.89e-3; re-reading every row
+    +2.87e-3: the bias schedule costs nothing measurable, profiles/r5/fm_w0_probe.jsonl)."""
     from hivemall_amd.ops import fm as fm_ops
 
-    assert fm_ops.W0_EVERY == 8 and fm_ops.W0_TOL > 0
+    assert fm_ops.W0_EVERY == 8 and fm_ops.W0_EVERY_MAX < 32
     n = 3 << 20
     idx, y = criteo_like(n, 20, seed=5)
     eidx, ey = criteo_like(100000, 20, seed=77)

