@@ -44,8 +44,9 @@ def main():
     print(json.dumps({"rows": n, "seq": round(ll_seq, 5), "cpu_s": round(time.time() - t0, 1)}), flush=True)
     dev = torch.device("cuda")
     gi, gf, gv, gy = (t.to(dev) for t in (idx, fld, val, y))
-    for G in grids:
-        for one_xcd in ((0, 1) if G else (0,)):
+    mems = os.environ.get("PROBE_MEM", "default").split(",")
+    for mem, G, one_xcd in [(m, G, x) for m in mems for G in grids for x in ((0, 1) if G else (0,))]:
+            os.environ["HM_FFM_MEM"] = mem
             os.environ["HM_FFM_XCD_ONLY"] = str(one_xcd)
             tr = FFMTrainer(OPTS, device=dev)
             tr.init_state(1 << BITS, F)
@@ -57,7 +58,7 @@ def main():
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
             ll = heldout(tr, dev)
-            print(json.dumps({"blocks_working": G or "default", "one_xcd": bool(one_xcd), "gpu": round(ll, 5),
+            print(json.dumps({"mem": mem, "blocks_working": G or "default", "one_xcd": bool(one_xcd), "gpu": round(ll, 5),
                               "gap": round(ll - ll_seq, 5), "rows_per_s": round(n / dt)}), flush=True)
     os.environ["HM_FFM_XCD_ONLY"] = "0"
 

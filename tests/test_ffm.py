@@ -514,3 +514,44 @@ def test_ffm_gpu_tables_of_4gib_and_more(dtype):
     assert float(tg.state["V"][:base].abs().amax()) == 0.0            # nothing else written
     del tg, V, G
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_ffm_xcd_replicas_train_and_merge():
+    """XCD replicas of the fp32 table (ops/ffm.py xcd_replicate / xcd_merge, the kernel's xrep):
+    replica r is trained only by blocks b % R == r; the merge averages V and the FTRL state into
+    every replica and leaves each replica's AdaGrad accumulators its own; with disjoint-feature
+    rows and R = 1 block per replica the result equals the CPU engine on each replica's rows."""
+    from hivemall_amd.ops.ffm import xcd_merge, xcd_replicate
+
+    R, F, NF = 8, 39, 4096
+    tg = _trainer("cuda", NF, F)
+    st = xcd_replicate(tg.state, R)
+    xr = st["xrep"]
+    V_all = xr["buf"][:, :, :xr["vbytes"]].view(torch.float32)
+    base = V_all[0].clone()
+    for r in range(R):                       # replica r: V + r, w + r
+        V_all[r] += float(r)
+        xr["lin"]["w"][r] += float(r)
+    xcd_merge(st)
+    torch.cuda.synchronize()
+    for r in range(R):
+        torch.testing.assert_close(V_all[r], base + (R - 1) / 2)
+        torch.testing.assert_close(xr["lin"]["w"][r], torch.full((NF,), (R - 1) / 2, device="cuda"))
+    # training: 8 rows, grid 8 -> row k trains replica k % 8 only (disjoint features)
+    g = torch.Generator().manual_seed(3)
+    idx = torch.arange(R * F, dtype=torch.int32).reshape(R, F)
+    val = torch.rand(R, F, generator=g) + 0.5
+    y = torch.where(torch.rand(R, generator=g) < 0.5, 1.0, -1.0)
+    before = V_all.clone()
+    ffm_step(st, idx.cuda(), None, val.cuda(), y.cuda(), tg.hyper, grid=R)
+    torch.cuda.synchronize()
+    for r in range(R):
+        changed = (V_all[r] != before[r]).any(-1)          # per feature
+        feats = torch.nonzero(changed).flatten().cpu()
+        assert set(feats.tolist()) <= set(range(r * F, (r + 1) * F)), r
+        assert len(feats) > 0
+    xcd_merge(st, broadcast=True)
+    torch.cuda.synchronize()
+    for r in range(1, R):
+        assert torch.equal(V_all[r], V_all[0])

@@ -160,9 +160,9 @@ def test_builder_leaf_routing_matches_predict_gpu():
     _leaf_vs_predict("cuda")
 
 
-def _hist_case():
+def _hist_case(NS=3, d=27):
     g = torch.Generator().manual_seed(1)
-    n, d, dpad, B, NS = 300000, 27, 32, 256, 3
+    n, dpad, B = 300000, 32, 256
     bins = torch.zeros(n, dpad, dtype=torch.uint8)
     bins[:, :d] = torch.randint(0, B, (n, d), generator=g, dtype=torch.uint8)
     stats = torch.randn(n, NS, generator=g)
@@ -180,9 +180,9 @@ def _hist_case():
     return (bins, rows, seg, stats), ref.view(S, d, B, NS), (d, dpad, B, NS, S)
 
 
-def _run_hist(dev, FG):
+def _run_hist(dev, FG, NS=3, d=27):
     from hivemall_amd import _native
-    (bins, rows, seg, stats), ref, (d, dpad, B, NS, S) = _hist_case()
+    (bins, rows, seg, stats), ref, (d, dpad, B, NS, S) = _hist_case(NS, d)
     hb, hr, hs, hst = (t.to(dev) for t in (bins, rows, seg, stats))
     out = torch.zeros(S, d, B, NS, device=dev)
     p = _native.ptr
@@ -206,6 +206,14 @@ def test_hist_kernel_segments_vs_torch():
     against a torch fp64 scatter-add reference; two feature-group widths."""
     for FG in (16, 8, 4):
         _run_hist("cuda", FG)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("NS", [5, 7, 8])
+def test_hist_kernel_5_to_8_statistics_vs_torch(NS):
+    """5..8 statistics (RandomForest with 5..8 classes) on 20 features: the feature-group
+    kernel with 4-feature groups (the shape models/trees.py routes there) against fp64."""
+    _run_hist("cuda", 4, NS=NS, d=20)
 
 
 def _nominal_data(n=4000, seed=3):
