@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--variant", type=int, default=8)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--plain", default="", help="kernel variants without a hot set, e.g. 0,10")
+    ap.add_argument("--grid", type=int, default=0, help="plain runs: blocks (0 = the kernel's default)")
+    ap.add_argument("--ramp-steps", type=int, default=1, help="plain runs: steps on the atomic ramp kernel")
     a = ap.parse_args()
     dev = torch.device("cuda")
     idx, fld, val, y = (t.to(dev) for t in criteo_ffm(B * NRES, BITS, seed=1000))
@@ -55,9 +57,11 @@ def main():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
             s = (i % NRES) * B
-            v = ffm_model.RAMP_VARIANT if i == 0 else var
+            if i % 8 == 0:
+                print(f"step {i}", file=sys.stderr, flush=True)
+            v = ffm_model.RAMP_VARIANT if i < a.ramp_steps else var
             ffm_step(tr.state, idx[s:s + B], fld[s:s + B], val[s:s + B], y[s:s + B], tr.hyper,
-                     train=True, variant=v, hot=hot)
+                     train=True, variant=v, hot=hot, grid=a.grid)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         pred = torch.empty(B, device=dev)
@@ -68,7 +72,8 @@ def main():
     for rep in range(a.reps):
         for v in [int(x) for x in a.plain.split(",") if x]:
             rate, ll = run(0, v, None)
-            print(json.dumps({"mode": "plain", "variant": v, "rep": rep, "rows_per_s": round(rate, 2),
+            print(json.dumps({"mode": "plain", "variant": v, "grid": a.grid, "ramp_steps": a.ramp_steps,
+                              "rep": rep, "rows_per_s": round(rate, 2),
                               "logloss_heldout": round(ll, 5), "gap_vs_seq": round(ll - SEQ, 5)}), flush=True)
         for H in [int(h) for h in a.hs.split(",") if h]:
             hot = torch.zeros(1 << BITS, dtype=torch.uint8, device=dev)

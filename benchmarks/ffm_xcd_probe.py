@@ -1,11 +1,14 @@
-"""Is the FFM kernel's same-stream gap an XCD-coherence effect?  MI355X has 8 XCDs, each with its
-own L2; plain loads of a line another XCD keeps updating can hit this XCD's stale copy.  Same
-rows in flight, different XCD spread: G blocks dealt round-robin over the 8 XCDs, against the
-same G blocks all on XCD 0 (HM_FFM_XCD_ONLY=1: a grid of 8G where only blocks b % 8 == 0 work).
-Held-out logloss after N rows of the bench stream (criteo_ffm, seed 1000, fp32, no ramp) vs the
-sequential engine on the same rows.
+"""Early-training gap of the FFM kernel by launch grid: held-out logloss after N rows of the bench
+stream (criteo_ffm, seed 1000, fp32, no ramp) vs the sequential engine on the same rows, per
+kernel variant and grid (0 = the kernel's default).
 
-    python benchmarks/ffm_xcd_probe.py [n_rows] [grids...]
+The round-5 attribution runs of this probe (profiles/r5/ffm_xcd_probe.jsonl, ffm_sc1_probe.jsonl,
+ffm_uncached_xcd8.jsonl, ffm_reload_wt_probe.jsonl, ffm_inflight_probe.jsonl) also swept
+experiment switches (table memory type, one-XCD placement, SC1 / write-through / acquire
+variants, rows in flight per CU) that were removed after the measurement: they ran at commit
+7cffa38 plus the variants described in docs/perf_notes.md.
+
+    [PROBE_VARIANTS=0,6] python benchmarks/ffm_xcd_probe.py [n_rows] [grids...]
 """
 import json
 import os
@@ -44,23 +47,19 @@ def main():
     print(json.dumps({"rows": n, "seq": round(ll_seq, 5), "cpu_s": round(time.time() - t0, 1)}), flush=True)
     dev = torch.device("cuda")
     gi, gf, gv, gy = (t.to(dev) for t in (idx, fld, val, y))
-    mems = os.environ.get("PROBE_MEM", "default").split(",")
-    for mem, G, one_xcd in [(m, G, x) for m in mems for G in grids for x in ((0, 1) if G else (0,))]:
-            os.environ["HM_FFM_MEM"] = mem
-            os.environ["HM_FFM_XCD_ONLY"] = str(one_xcd)
-            tr = FFMTrainer(OPTS, device=dev)
-            tr.init_state(1 << BITS, F)
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            for s in range(0, n, B):
-                ffm_step(tr.state, gi[s:s + B], gf[s:s + B], gv[s:s + B], gy[s:s + B], tr.hyper, variant=0,
-                         grid=(8 * G if one_xcd else G))
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t
-            ll = heldout(tr, dev)
-            print(json.dumps({"mem": mem, "blocks_working": G or "default", "one_xcd": bool(one_xcd), "gpu": round(ll, 5),
-                              "gap": round(ll - ll_seq, 5), "rows_per_s": round(n / dt)}), flush=True)
-    os.environ["HM_FFM_XCD_ONLY"] = "0"
+    variants = [int(v) for v in os.environ.get("PROBE_VARIANTS", "0").split(",")]
+    for var, G in [(v, G) for v in variants for G in grids]:
+        tr = FFMTrainer(OPTS, device=dev)
+        tr.init_state(1 << BITS, F)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for s in range(0, n, B):
+            ffm_step(tr.state, gi[s:s + B], gf[s:s + B], gv[s:s + B], gy[s:s + B], tr.hyper, variant=var, grid=G)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        ll = heldout(tr, dev)
+        print(json.dumps({"variant": var, "blocks": G or "default", "gpu": round(ll, 5),
+                          "gap": round(ll - ll_seq, 5), "rows_per_s": round(n / dt)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -68,13 +68,6 @@ struct FFMParams {
     // trains them in list mode (it implements the grouped update).  null: no deferral.
     int32_t* defer;
     int list_mode;
-    int xcd_only;                  // experiment: only blocks with blockIdx % 8 == 0 work (one XCD)
-    int inv_every;                 // experiment (ATOM = 4): an agent-scope acquire every n rows
-    // XCD replicas (ffm_pipe_sg32_kernel): xrep model replicas, block b trains replica b % xrep
-    // (the XCD the round-robin dispatch puts it on); vrep = bytes between the replicas' V|G block
-    // tables, lrep = floats between their w / wz / wn vectors
-    int xrep;
-    long long vrep, lrep;
 };
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
@@ -1045,24 +1038,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
     const OT vfs = (OT)P.fstride * 16u;                  // V bytes between features
     const OT gfs = (OT)P.gstride * 4u;                   // G bytes between features
-    // XCD replica of this block: the 8 XCDs' L2s are not coherent with each other inside a
-    // kernel, so a table every XCD read-modify-writes lets each XCD keep working on its own stale
-    // lines of the hot features (profiles/r5/ffm_xcd_probe.jsonl: 8 rows in flight on 8 XCDs
-    // +4.5e-3 vs sequential, on one XCD +1.3e-4).  One replica per XCD is coherent in its L2;
-    // the replicas are averaged between launches (hm_ffm_xrep).
-    const int xr = P.xrep > 1 ? (int)(blockIdx.x % (unsigned)P.xrep) : 0;
-    if (xr) {
-        Vt = reinterpret_cast<char*>(Vt) + (size_t)xr * (size_t)P.vrep;
-        Gt = reinterpret_cast<float*>(reinterpret_cast<char*>(Gt) + (size_t)xr * (size_t)P.vrep);
-        w += (size_t)xr * (size_t)P.lrep;
-        wz += (size_t)xr * (size_t)P.lrep;
-        wn += (size_t)xr * (size_t)P.lrep;
-    }
-    // xcd_only (experiment): the work of a grid of gridDim.x / 8 blocks, done by the blocks the
-    // round-robin dispatch puts on XCD 0 (block b on XCD b % 8); the others exit at once
-    if (P.xcd_only && (blockIdx.x & 7) != 0) return;
-    const int G = P.xcd_only ? (int)(gridDim.x >> 3) : (int)gridDim.x;
-    const int bid = P.xcd_only ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    // (One table replica per XCD, averaged between launches, was measured and removed: +3.1e-3 ..
+    // +5.4e-3 vs sequential on the bench stream instead of +2.4e-3; profiles/r5/ffm_xrep_probe.jsonl.)
+    const int G = (int)gridDim.x;
+    const int bid = (int)blockIdx.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
 
@@ -1176,12 +1155,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         if (more) publish_meta(nxt);
         bar_raw();
         // ---- C: next row's slot DMA (the landing zones are free: read in B), its meta after ----
-        if (ATOM >= 4 && more && ((row / G) % P.inv_every) == 0) {
-            // experiment: invalidate cached lines before the gather (4: agent acquire, buffer_inv
-            // sc1; 5: system acquire, buffer_inv sc0 sc1)
-            if (ATOM == 4) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        }
         if (more) {
             dma_slots(nxt);
             dma_meta(cur, row + 2 * G);
@@ -1200,18 +1173,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         float xab[NS];
         float part = 0.f;
         int rep = 0;
-        float4 rv[NS];          // ATOM = 3: the slot's V / G re-read here, updated by the delta in E
-        float rgv[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT ov, og;
             const uint32_t k = slot(cur, j, ov, og, xab[j]);
             live |= (k & 1u) << j;
             wr |= (uint32_t)(k != 0u) << j;
-            if (ATOM == 3 && k != 0u) {
-                rv[j] = *reinterpret_cast<const float4*>(vb + ov);
-                rgv[j] = *reinterpret_cast<const float*>(gb + og);
-            }
             if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * TPB;
             const float4 pv = s_t[s < FF ? s : 0];
@@ -1256,17 +1223,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 const f2 rr = {r, r};
                 o0 = o0 + rr * d0;
                 o1 = o1 + rr * d1;
-                if (ATOM == 3) {
-                    // the step taken from the row's snapshot, applied to the value re-read during
-                    // the forward pass: concurrent rows' updates are lost only inside that
-                    // shorter window (the snapshot is DMA'd one row ahead)
-                    fv[j] = make_float4(rv[j].x + (o0.x - cv.x), rv[j].y + (o0.y - cv.y), rv[j].z + (o1.x - cv.z),
-                                        rv[j].w + (o1.y - cv.w));
-                    fg[j] = rgv[j] + (gs - cg[j]);
-                } else {
-                    fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
-                    fg[j] = gs;
-                }
+                fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
+                fg[j] = gs;
                 fo[j] = ov;
                 fwd |= 1u << j;
                 if (ATOM == 1 || (ATOM == 2 && s_m[cur][SA(j)].w != 0)) {
@@ -1640,15 +1598,6 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (variant == 8 && P.hot) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 2>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
-        else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 3>), dim3(blocks), \
-                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
-                                                   bias, pred, loss); \
-        else if (variant == 11) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 4>), dim3(blocks), \
-                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
-                                                   bias, pred, loss); \
-        else if (variant == 12) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 5>), dim3(blocks), \
-                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
-                                                   bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
@@ -1770,11 +1719,13 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // registers instead of an LDS landing zone (53 KB per block: 3 rows in flight per CU instead of
 // 2): 73.6-73.8 vs 73.9-74.2 M rows/s (profiles/r4/ffm_register_g_ab.log) — more rows in flight
 // per CU does not move this kernel.
-// aux (host array of 5 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
+// aux (host array of 2 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
 // or null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
-// updated slot by slot by the pipelined kernels: racing stores of one address, one wins);
-// aux[2] = XCD replicas (fp32 block layout; 0/1 = one table), aux[3] = bytes between the
-// replicas' block tables, aux[4] = floats between their w / wz / wn.
+// updated slot by slot by the pipelined kernels: racing stores of one address, one wins).
+// Measured and removed in round 5 (docs/perf_notes.md "where the fp32 same-stream gap comes
+// from"): reload-delta stores, SC1 DMA loads, write-through (device-scope) stores, agent / system
+// acquires, a coherent re-read, 512-thread and one-block-per-CU launches, one table replica per
+// XCD, and the one-XCD probe switch.
 HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, const int32_t* fld,
                        const float* val, const float* y, void* V, void* G, float* w, float* wz,
                        float* wn, float* bias, float* pred, float* loss, void* const* aux,
@@ -1783,10 +1734,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.hot = aux ? reinterpret_cast<const uint8_t*>(aux[0]) : nullptr;
     P.defer = aux ? reinterpret_cast<int32_t*>(aux[1]) : nullptr;
     P.list_mode = 0;
-    P.xrep = aux ? (int)reinterpret_cast<intptr_t>(aux[2]) : 1;
-    P.vrep = aux ? (long long)reinterpret_cast<intptr_t>(aux[3]) : 0;
-    P.lrep = aux ? (long long)reinterpret_cast<intptr_t>(aux[4]) : 0;
-    if (P.xrep < 1) P.xrep = 1;
     P.B = ip[0]; P.F = ip[1]; P.num_features = ip[2]; P.num_fields = ip[3]; P.Kp = ip[4];
     P.classification = ip[5]; P.train = ip[6]; P.use_linear = ip[7]; P.use_bias = ip[8];
     P.norm = ip[9];
@@ -1803,8 +1750,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.vpad = ip[19];
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
-    P.xcd_only = ip[22];
-    P.inv_every = ip[23] > 0 ? ip[23] : 1;
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.vfe = (long long)P.fstride * P.sstride;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];
@@ -1846,60 +1791,4 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     if (rc != 0 || !fast || !P.defer) return rc;
     return bf16 ? launch_deferred<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream)
                 : launch_deferred<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream);
-}
-
-// XCD replicas of the fp32 block table (ffm_pipe_sg32_kernel xrep): over R replicas of
-// [NF][bs] bytes, the V region (the first vbytes of each feature block) and w / wz / wn
-// ([R][lrep] floats, NF used) are averaged and the mean written to every replica (mode 0), or
-// replica 0 is copied to the others (mode 1).  The AdaGrad accumulators stay per replica.
-namespace {
-__global__ __launch_bounds__(256) void xrep_kernel(char* __restrict__ buf, int R, int64_t NF, int64_t bs, int vq,
-                                                   float* __restrict__ w, float* __restrict__ wz,
-                                                   float* __restrict__ wn, int64_t lrep, int mode) {
-    const int64_t nv = NF * vq;                    // float4 quads of V
-    const int64_t tot = nv + NF;
-    const float inv = 1.f / (float)R;
-    for (int64_t q = blockIdx.x * (int64_t)256 + threadIdx.x; q < tot; q += (int64_t)gridDim.x * 256) {
-        if (q < nv) {
-            const int64_t i = q / vq, c = q - i * vq;
-            const size_t off = (size_t)i * bs + (size_t)c * 16;
-            float4 m = *reinterpret_cast<const float4*>(buf + off);
-            if (mode == 0) {
-                for (int r = 1; r < R; ++r) {
-                    const float4 v = *reinterpret_cast<const float4*>(buf + (size_t)r * NF * bs + off);
-                    m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w;
-                }
-                m.x *= inv; m.y *= inv; m.z *= inv; m.w *= inv;
-                *reinterpret_cast<float4*>(buf + off) = m;
-            }
-            for (int r = 1; r < R; ++r) *reinterpret_cast<float4*>(buf + (size_t)r * NF * bs + off) = m;
-        } else {
-            const int64_t i = q - nv;
-            float* vs[3] = {w, wz, wn};
-            for (int k = 0; k < 3; ++k) {
-                float* p = vs[k];
-                float m = p[i];
-                if (mode == 0) {
-                    for (int r = 1; r < R; ++r) m += p[(size_t)r * lrep + i];
-                    m *= inv;
-                    p[i] = m;
-                }
-                for (int r = 1; r < R; ++r) p[(size_t)r * lrep + i] = m;
-            }
-        }
-    }
-}
-}  // namespace
-
-HM_API int hm_ffm_xrep(void* buf, int R, int64_t NF, int64_t bs, int vbytes, float* w, float* wz, float* wn,
-                       int64_t lrep, int mode, hipStream_t stream) {
-    if (R <= 1 || NF <= 0) return 0;
-    if ((vbytes & 15) || bs < vbytes || (bs & 15) || lrep < NF || (mode != 0 && mode != 1))
-        return (int)hipErrorInvalidValue;
-    const int vq = vbytes / 16;
-    const int64_t tot = NF * vq + NF;
-    const int64_t blocks = (tot + 255) / 256;
-    hipLaunchKernelGGL(xrep_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, stream,
-                       reinterpret_cast<char*>(buf), R, NF, bs, vq, w, wz, wn, lrep, mode);
-    HM_LAUNCH_RET();
 }

@@ -87,18 +87,3 @@ HM_API int hm_mark_touched(const int32_t* idx, int64_t n, int32_t dims, uint8_t*
     HM_LAUNCH_RET();
 }
 
-// Device memory with an explicit coherence type (hipExtMallocWithFlags): flags 0 = default
-// (coarse-grained: each XCD's L2 may keep its own copy of a line within a kernel), 1 =
-// fine-grained (coherent across XCDs), 3 = uncached.  Zero-filled.  Returns null on failure.
-// Used for A/B of the Hogwild tables' cross-XCD visibility (ops/memory.py).
-HM_API void* hm_malloc_flags(size_t bytes, unsigned flags) {
-    void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, bytes, flags) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, bytes) != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    return p;
-}
-
-HM_API int hm_free(void* p) { return (int)hipFree(p); }

@@ -119,13 +119,7 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
         if packed:
             fs, bs, goff = slot_block_layout(num_fields, kp, dtype)
             es = torch.empty(0, dtype=dtype).element_size()
-            mem = os.environ.get("HM_FFM_MEM", "default")     # A/B: HIP memory coherence type
-            if mem != "default" and torch.device(device).type == "cuda":
-                from . import memory
-
-                buf = memory.zeros((num_features, bs), torch.uint8, device, kind=mem)
-            else:
-                buf = torch.zeros((num_features, bs), dtype=torch.uint8, device=device)
+            buf = torch.zeros((num_features, bs), dtype=torch.uint8, device=device)
             V = buf[:, :goff].view(dtype).view(num_features, fs, kp)[:, :num_fields]
             G = buf[:, goff:goff + fs * 4].view(torch.float32)[:, :num_fields]
             assert V.stride(0) * es == bs and G.stride(0) * 4 == bs
@@ -141,10 +135,6 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
             torch.zeros(shape, dtype=dtype, device=device))
 
 
-_native.register_hip("hm_ffm_xrep", [_native.c_p, _native.c_int, _native.c_i64, _native.c_i64, _native.c_int,
-                                     _native.c_p, _native.c_p, _native.c_p, _native.c_i64, _native.c_int,
-                                     _native.c_p])
-
 _DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
 # HM_FFM_DEFER=0 (A/B only): no multi-hot detection in the pipelined kernels (a row with a
 # repeated field or feature is then updated slot by slot: racing stores of one address)
@@ -159,55 +149,10 @@ def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
     return buf
 
 
-def xcd_replicate(state: dict, R: int = 8) -> dict:
-    """Give a GPU fp32 FFM state (per-slot G, block layout) R XCD replicas: ``ffm_pipe_sg32_kernel``
-    then trains replica b % R with block b (each of the 8 XCDs on its own copy, coherent in its
-    own L2), and :func:`xcd_merge` averages them.  The state's V / G / w / wz / wn become views of
-    replica 0 (the model every other op reads); ``state["xrep"]`` holds the replica buffers.
-    Every replica starts as a copy of the current model."""
-    V, G = state["V"], state["G"]
-    assert V.is_cuda and V.dtype == torch.float32 and G.dim() == 2 and G.stride(1) == 1, \
-        "XCD replicas: fp32 V, per-slot G in the feature-block layout"
-    NF, NFLD, kp = V.shape
-    bs = V.stride(0) * V.element_size()
-    goff = G.data_ptr() - V.data_ptr()
-    assert G.stride(0) * 4 == bs and 0 < goff < bs
-    buf = torch.empty((R, NF, bs), dtype=torch.uint8, device=V.device)
-    # the current block table as bytes (whole feature blocks, G included), copied into every replica
-    base = torch.empty(0, dtype=torch.uint8, device=V.device).set_(
-        V.untyped_storage(), V.storage_offset() * V.element_size(), (NF, bs), (bs, 1))
-    buf.copy_(base.unsqueeze(0).expand(R, NF, bs))
-    fs = V.stride(0) // V.stride(1)
-    V0 = buf[0, :, :fs * kp * 4].view(torch.float32).view(NF, fs, kp)[:, :NFLD]
-    G0 = buf[0, :, goff:goff + fs * 4].view(torch.float32)[:, :NFLD]
-    lin = {k: torch.empty((R, NF), dtype=torch.float32, device=V.device) for k in ("w", "wz", "wn")}
-    for k, t in lin.items():
-        t.copy_(state[k].unsqueeze(0).expand(R, NF))
-    state.update(V=V0, G=G0, w=lin["w"][0], wz=lin["wz"][0], wn=lin["wn"][0],
-                 xrep=dict(R=R, buf=buf, bs=bs, vbytes=fs * kp * 4, lin=lin))
-    return state
-
-
-def xcd_merge(state: dict, broadcast: bool = False) -> None:
-    """Average the XCD replicas' V and FTRL (w, z, n) into every replica (AdaGrad G stays per
-    replica, as a data-parallel mapper's); ``broadcast``: copy replica 0 to the others instead."""
-    xr = state.get("xrep")
-    if not xr or xr["R"] <= 1:
-        return
-    lin = xr["lin"]
-    NF = xr["buf"].shape[1]
-    rc = _native.hip().hm_ffm_xrep(_native.ptr(xr["buf"]), xr["R"], ctypes.c_int64(NF), ctypes.c_int64(xr["bs"]),
-                                   xr["vbytes"], _native.ptr(lin["w"]), _native.ptr(lin["wz"]),
-                                   _native.ptr(lin["wn"]), ctypes.c_int64(NF), int(broadcast),
-                                   _native.stream_of(xr["buf"].device))
-    _native.check(rc, "hm_ffm_xrep")
-
-
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
              y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
              pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
-             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None,
-             xrep_off: bool = False) -> None:
+             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None) -> None:
     """One fused pass over a padded-ELL batch.
 
     state: dict with V, G ([NF, NFLD, Kp] f32 or bf16; either two contiguous tables or the two
@@ -273,8 +218,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0, int(os.environ.get("HM_FFM_XCD_ONLY", "0")),
-                   int(os.environ.get("HM_FFM_INV_EVERY", "1"))],
+                   G.stride(1) if slot_g else 0],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
@@ -285,11 +229,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
             assert hot.dtype == torch.uint8 and hot.numel() >= NF and hot.device == V.device
         # multi-hot rows (a repeated field or feature) are deferred by the pipelined kernels to
         # the grouped-update kernel through this buffer (same stream, no host sync)
-        xr = state.get("xrep") if train else None
-        use_x = xr is not None and xr["R"] > 1 and not xrep_off
-        aux = (ctypes.c_void_p * 5)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
-                                    xr["R"] if use_x else 1, xr["buf"].shape[1] * xr["bs"] if use_x else 0,
-                                    xr["buf"].shape[1] if use_x else 0)
+        aux = (ctypes.c_void_p * 2)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None)
         rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
         if train and hyper.use_bias:
