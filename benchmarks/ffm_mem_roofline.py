@@ -37,13 +37,24 @@ def run():
     VG = torch.zeros(NF * 896 // 2, dtype=torch.bfloat16, device=dev)   # large enough for every mode
     out = torch.zeros(B * 8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
-    modes = [int(m) for m in os.environ.get("MODES", "0,1,3,4,5,6").split(",")]
+    modes = [int(m) for m in os.environ.get("MODES", "0,1,3,4,5,6,7").split(",")]
+    if 7 in modes:
+        from hivemall_amd.io.synthetic import criteo_ffm
+
+        lib.hm_probe_ffm_mem_fv.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_int, C.c_void_p]
+        fidx, ffld, fval, _ = criteo_ffm(B * 8, 20, seed=1000, device=dev)
     for mode in modes:
         for blocks in (4096, 8192):
             def launch(k):
                 s = (k % 8) * B
-                rc = lib.hm_probe_ffm_mem(idx[s:s + B].data_ptr(), B, F, F, VG.data_ptr(),
-                                          out.data_ptr(), mode, blocks, st)
+                if mode == 7:
+                    rc = lib.hm_probe_ffm_mem_fv(fidx[s:s + B].data_ptr(), ffld[s:s + B].data_ptr(),
+                                                 fval[s:s + B].data_ptr(), B, F, VG.data_ptr(), out.data_ptr(),
+                                                 blocks, st)
+                else:
+                    rc = lib.hm_probe_ffm_mem(idx[s:s + B].data_ptr(), B, F, F, VG.data_ptr(),
+                                              out.data_ptr(), mode, blocks, st)
                 assert rc == 0
             for k in range(3):
                 launch(k)
@@ -57,7 +68,7 @@ def run():
             print(json.dumps({"mode": mode, "blocks": blocks, "ms": round(dt * 1e3, 3),
                               "rows_per_s": round(B / dt / 1e6, 1),
                               "requested_TBps": round(B * 1482 * 16 * (1 if mode == 0 else 2) / dt / 1e12, 2)
-                              if mode < 5 else round(B * 39 * (896 if mode == 5 else 512) * 2 / dt / 1e12, 2)}),
+                              if mode < 5 else round(B * 39 * (512 if mode == 6 else 896) * 2 / dt / 1e12, 2)}),
                   flush=True)
 
 

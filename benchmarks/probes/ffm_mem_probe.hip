@@ -112,7 +112,63 @@ __global__ __launch_bounds__(256) void probe_sg_kernel(const int32_t* __restrict
     }
 }
 
+// mode 7: the fp32 block layout of mode 5 at the driver's round-4+ config: criteo_ffm rows (a
+// field id and a value per row position, read next to the index) and no pad / tail stores
+// (ffm_pipe_sg32_kernel dropped them in round 4).
+template <int NS>
+__global__ __launch_bounds__(256) void probe_sg_fv_kernel(const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
+                                                          const float* __restrict__ val, int B, int F,
+                                                          char* __restrict__ tab, float* __restrict__ out) {
+    constexpr uint32_t VSB = 16u, BS = 896u, GOFF = 40u * VSB;
+    __shared__ int s_i[64], s_f[64];
+    __shared__ float s_x[64];
+    const int tid = threadIdx.x;
+    const int FF = F * F;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    float acc = 0.f;
+    for (int row = blockIdx.x; row < B; row += gridDim.x) {
+        if (tid < F) {
+            s_i[tid] = idx[(size_t)row * F + tid];
+            s_f[tid] = fld[(size_t)row * F + tid];
+            s_x[tid] = val[(size_t)row * F + tid];
+        }
+        __syncthreads();
+        f4v v[NS];
+        float g[NS];
+        uint32_t ov[NS], og[NS];
+        bool ok[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int s = tid + j * 256;
+            const int a = s < FF ? s / F : 0, b = s < FF ? s % F : 0;
+            ok[j] = s < FF;
+            const uint32_t i = (uint32_t)s_i[a], f = (uint32_t)s_f[b];
+            ov[j] = i * BS + f * VSB;
+            og[j] = i * BS + GOFF + f * 4u;
+            v[j] = *reinterpret_cast<const f4v*>(tab + ov[j]);
+            g[j] = *reinterpret_cast<const float*>(tab + og[j]);
+            acc += s_x[a] * s_x[b];
+        }
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            if (!ok[j]) continue;
+            v[j].x += 1;
+            *reinterpret_cast<f4v*>(tab + ov[j]) = v[j];
+            *reinterpret_cast<float*>(tab + og[j]) = g[j] + 1.f;
+        }
+        __syncthreads();
+    }
+    if (acc == -1.f) out[0] = acc;     // keeps the value loads
+}
+
 }  // namespace
+
+extern "C" int hm_probe_ffm_mem_fv(const int32_t* idx, const int32_t* fld, const float* val, int B, int F,
+                                   void* vg, float* out, int blocks, hipStream_t stream) {
+    if (F != 39) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((probe_sg_fv_kernel<6>), dim3(blocks), dim3(256), 0, stream, idx, fld, val, B, F, (char*)vg, out);
+    return (int)hipGetLastError();
+}
 
 extern "C" int hm_probe_ffm_mem(const int32_t* idx, int B, int F, int nfld, void* vg, float* out, int mode,
                                 int blocks, hipStream_t stream) {

@@ -475,11 +475,13 @@ def test_rf_5_to_8_classes_wide_rows_gpu_matches_cpu(n_classes):
         trees.append(b.build(stats.to(dev)))
     tc, tg = trees
     assert list(tc.feature) == list(tg.feature)
-    # the forest trains end to end on the GPU path; its accuracy equals the CPU engine's (a 4-tree
-    # forest drawing ~4 of the 20 features per node: 0.78-0.93 with 5..8 bands, both engines)
-    acc = {dev: (RandomForestClassifier("-trees 4 -max_depth 8 -seed 3", device=dev).fit(X, y).predict(X) == y).mean()
+    # the forest trains end to end on the GPU path; its accuracy matches the CPU engine's.  The
+    # engines draw different bootstrap / feature-subset streams, so a 4-tree forest's accuracy is
+    # seed noise (8 classes, seeds 1..8: CPU 0.86-0.95, GPU 0.78-0.95); at 32 trees CPU
+    # 0.883-0.918 (mean 0.897), GPU 0.899-0.944 (mean 0.914) (profiles/r5/rf_multiclass_probe.jsonl)
+    acc = {dev: (RandomForestClassifier("-trees 32 -max_depth 8 -seed 3", device=dev).fit(X, y).predict(X) == y).mean()
            for dev in ("cpu", "cuda")}
-    assert acc["cuda"] > acc["cpu"] - 0.05, acc
+    assert acc["cuda"] > acc["cpu"] - 0.03, acc
 
 
 def test_heap_layout_tree_compaction_matches_compact_numbering():
