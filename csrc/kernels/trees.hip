@@ -210,6 +210,12 @@ __global__ __launch_bounds__(TPB) void hist_kernel(const uint8_t* __restrict__ b
     }
 }
 
+// (Round 5, measured and removed: a feature-lane all-features histogram -- the image laid out
+// [bin][32 features], each lane adding one feature of a staged row, so a wave's adds hit distinct
+// banks whatever the bins.  Bank conflicts fell from 6.7 to 0.2-0.3 cycles per LDS instruction,
+// but the kernel ran 1.5-2.0x slower (root 11 M x 28, NS = 2: 269 vs 178 us; GBDT 2.85-2.93 vs
+// 2.09 ms per tree): the staging adds LDS instructions and the larger LDS footprint halves the
+// blocks per CU.  docs/perf_notes.md, profiles/r5/hist_fl/.)
 // Column |max| finish: every wave's maxima -> LDS -> one integer atomicMax per column per BLOCK
 // (non-negative floats order like their bit patterns).  Per-wave atomics on the same 3 words
 // serialised: 8,192 of them cost ~0.28 ms per 11M-row tree (profiles/gbt_r2/).
@@ -1149,7 +1155,7 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
 #define HM_HP(K, W, T) { \
             static bool attr_set = false; \
             if (!attr_set) { \
-                hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, W, T, true>), \
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, W, T, true>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
                 attr_set = true; \
             } \
@@ -1167,7 +1173,7 @@ HM_API int hm_hist_build(const uint8_t* bins, int d, int dpad, int B, const int3
 #define HM_HW(K) case K: { \
             static bool attr_set = false; \
             if (!attr_set) { \
-                hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, 8, 1024>), \
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hist_kernel<K, 8, 1024>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
                 attr_set = true; \
             } \
@@ -1406,9 +1412,9 @@ HM_API int hm_leaf_sums(const void* leaf, const float* st2, const float* hh, int
     if (blocks > LEAF_BLOCKS) blocks = LEAF_BLOCKS;
     static bool attr_set = false;     // 64-bit sums of up to 8,192 nodes: 128 KB of LDS
     if (!attr_set) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int16_t>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int16_t>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int32_t>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&leaf_sums_kernel<int32_t>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
