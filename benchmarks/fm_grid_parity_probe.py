@@ -1,0 +1,45 @@
+"""train_fm (bf16 V, config-2 engine) held-out logloss vs Hivemall's 8-mapper average on the
+3 x 2^20-row stream of tests/test_fm.py::test_fm_gpu_logloss_parity_past_2p20_rows, by kernel grid
+(Hogwild rows in flight = 4 x grid) and repetition: the spread of the Hogwild gap.
+
+    python benchmarks/fm_grid_parity_probe.py [grids...]
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hivemall_amd.io.synthetic import criteo_like  # noqa: E402
+from hivemall_amd.models.fm import FMTrainer  # noqa: E402
+from tests.test_fm import _rows, mapper_average_fm  # noqa: E402
+
+
+def main():
+    grids = [int(g) for g in sys.argv[1:]] or [64, 128, 256]
+    n = 3 << 20
+    idx, y = criteo_like(n, 20, seed=5)
+    eidx, ey = criteo_like(100000, 20, seed=77)
+    yy = (ey > 0).float()
+    opts = "-c -factors 8 -num_features 1048576 -eta0 0.01 -sigma 0.01"
+    ll = lambda t, dev: torch.nn.functional.binary_cross_entropy_with_logits(  # noqa: E731
+        t.predict_raw(rows=_rows(eidx).to(dev)).cpu(), yy).item()
+    m8 = ll(mapper_average_fm(opts, idx, y, 8, 1 << 20), "cpu")
+    print(json.dumps({"mappers8": round(m8, 5)}), flush=True)
+    rows = _rows(idx, y).to("cuda")
+    for rep in range(3):
+        for g in grids:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            m = FMTrainer(opts + f" -grid {g}", device="cuda").fit(rows=rows)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            v = ll(m, "cuda")
+            print(json.dumps({"grid": g, "rep": rep, "gpu": round(v, 5), "delta_vs_mappers8": round(v - m8, 5),
+                              "rows_per_s": round(n / dt)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

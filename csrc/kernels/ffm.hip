@@ -1683,9 +1683,12 @@ constexpr int DEFER_BLOCKS = 512;
 template <bool BF>
 int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const float* val,
                     const float* y, void* V, void* G, float* w, float* wz, float* wn, float* bias,
-                    float* pred, float* loss, int slot_g, hipStream_t stream) {
+                    float* pred, float* loss, int slot_g, int grid_req, hipStream_t stream) {
     P.list_mode = 1;
-    const int grid = P.B < DEFER_BLOCKS ? P.B : DEFER_BLOCKS;
+    // an explicit grid bounds the deferred rows' concurrency too (grid = 1: one block trains
+    // them in list order, after the batch's other rows)
+    const int cap = grid_req > 0 && grid_req < DEFER_BLOCKS ? grid_req : DEFER_BLOCKS;
+    const int grid = P.B < cap ? P.B : cap;
     return slot_g ? launch_generic<BF, true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream)
                   : launch_generic<BF, false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, stream);
 }
@@ -1789,6 +1792,6 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     const int rc = bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast)
                         : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast);
     if (rc != 0 || !fast || !P.defer) return rc;
-    return bf16 ? launch_deferred<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream)
-                : launch_deferred<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, stream);
+    return bf16 ? launch_deferred<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, grid, stream)
+                : launch_deferred<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, grid, stream);
 }

@@ -280,15 +280,25 @@ def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
     """grid=1: one workgroup walks the rows in order = Hivemall's per-row semantics.  The generic
     kernel (variant 1) has no lookahead; the pipelined default DMAs row r+1's slots before row
     r's updates land, and forwards its own updates into the slots both rows hold (ffm.hip
-    ffm_pipe_sg32_kernel): measured 4.2e-5 / 3.2e-5 from the sequential engine (2.05e-3 before
-    the forwarding, profiles/r4/ffm_single_block_forwarding.log)."""
+    ffm_pipe_sg32_kernel): on rows without a repeated feature, 3e-8 / 6e-8 from the sequential
+    engine (profiles/r5/pytest_ffm_q.log; 2.05e-3 before the forwarding,
+    profiles/r4/ffm_single_block_forwarding.log)."""
+    from hivemall_amd.models import ffm as ffm_model
     from hivemall_amd.ops import ffm as ffm_op
 
     idx, y = criteo_like(20000, hash_bits=16, seed=5)
     eidx, ey = criteo_like(5000, hash_bits=16, seed=99)
+    # field-disjoint ids (field f owns [1024 f, 1024 f + 1024)): no row repeats a feature, so no
+    # row is deferred to the grouped-update kernel -- a deferred (multi-hot) row trains after its
+    # batch's other rows, a reordering that moved this logloss by -4e-4 at 2^16 hashed ids
+    # (~1 % of the rows hold a hash collision; profiles/r5/pytest_ffm_q.log)
+    fid = torch.arange(39, dtype=idx.dtype)
+    idx = idx % 1024 + fid * 1024
+    eidx = eidx % 1024 + fid * 1024
     yy = (ey > 0).float()
     res = {}
-    old = ffm_op._VARIANT
+    old = ffm_op._VARIANT, ffm_model.RAMP_ROWS
+    ffm_model.RAMP_ROWS = 0          # the store kernel itself, not the learner's atomic ramp
     try:
         for dev, v in (("cpu", 0), ("cuda", 1), ("cuda", 0)):
             ffm_op._VARIANT = v
@@ -299,9 +309,10 @@ def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
             p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
             res[(dev, v)] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
     finally:
-        ffm_op._VARIANT = old
+        ffm_op._VARIANT, ffm_model.RAMP_ROWS = old
+    print("single-block", adagrad, res)
     assert abs(res[("cpu", 0)] - res[("cuda", 1)]) < 1e-4, res
-    assert abs(res[("cpu", 0)] - res[("cuda", 0)]) < 3e-4, res
+    assert abs(res[("cpu", 0)] - res[("cuda", 0)]) < 1e-4, res
 
 
 @pytest.mark.gpu
