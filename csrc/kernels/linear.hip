@@ -839,8 +839,8 @@ __global__ __launch_bounds__(256) void linear_mb_apply_kernel(
 }
 
 // One pass of the mini-batch engine over n_rows (step of row q = t0 + q + 1).  GA f32 [dims] and
-// mark u32 [dims] zeroed, list i32 [cap >= min(dims, M * max nnz)], cnt i32 [2] zeroed (all left
-// zeroed again at the end).
+// mark u32 [dims] zeroed (left zeroed again at the end), list i32 [cap >= min(dims, M * max nnz)],
+// cnt i32 [2] (zeroed here).
 HM_API int hm_linear_train_minibatch(const Params* P, int64_t n_rows, int dims, int64_t t0, int M,
                                      const int64_t* indptr, const int32_t* idx, const float* val,
                                      const float* y, const int32_t* order, float* S, uint8_t* touched,
@@ -850,6 +850,9 @@ HM_API int hm_linear_train_minibatch(const Params* P, int64_t n_rows, int dims, 
     if (M <= 1 || dims <= 0 || P->n_labels != 1 || P->algo != A_GENERAL || P->opt == O_EVE)
         return (int)hipErrorInvalidValue;
     const int gb = (int)((M + 3) / 4 < 4096 ? (M + 3) / 4 : 4096);     // one wave per row
+    // both batch counters start at 0 (the last batch of a previous pass leaves its own set)
+    const hipError_t ze = hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), stream);
+    if (ze != hipSuccess) return (int)ze;
     int b = 0;
     for (int64_t b0 = 0; b0 < n_rows; b0 += M, ++b) {
         const int64_t b1 = b0 + M < n_rows ? b0 + M : n_rows;

@@ -278,13 +278,15 @@ def test_gpu_minibatch_engine_matches_sequential_minibatch_learner(opts):
     each batch of M rows; csrc/kernels/linear.hip hm_linear_train_minibatch) runs the sequential
     learner's mini-batch rule — every row scored against the batch's weights, one optimizer step
     per touched feature with the batch's mean gradient — so held-out logloss and weights match the
-    CPU engine's -mini_batch M run up to the order of the fp32 gradient sums."""
+    CPU engine's -mini_batch M run up to the order of the fp32 gradient sums.  Two epochs of 293
+    batches: the second pass starts from zeroed batch counters (an odd batch count used to leave a
+    stale count behind)."""
     rows = _criteo_rows(300000, 24, seed=5)
     test = _criteo_rows(50000, 24, seed=99)
     yy = (test.y > 0).float()
     res, ws = {}, {}
     for dev in ("cpu", "cuda"):
-        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216 -iters 1 -mini_batch 1024", device=dev)
+        m = L.TrainClassifier(f"-loss logloss {opts} -dims 16777216 -iters 2 -disable_cv -mini_batch 1024", device=dev)
         m.fit(rows=rows.to(dev))
         if dev == "cuda":
             assert m.state.meta.get("minibatch")
