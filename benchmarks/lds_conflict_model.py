@@ -4,9 +4,11 @@ statistic pairs) when a wave's 64 lanes add at independent uniformly random bins
 gfx950 services an 8-byte LDS write-class access in 4 groups of 16 lanes, bank = (address / 4) mod
 32 (MI355X_MICROARCH.md §LDS), so an 8-B histogram entry at bin b occupies bank pair b mod 16 of
 its feature's sub-histogram (whose base is a multiple of 32 banks).  Each extra distinct address
-on a busy bank pair adds one cycle.  This prints the expectation per wave-instruction, which any
-row -> lane or feature -> bank mapping leaves unchanged while the bins are random: the bank of
-every lane is set by its bin.
+on a busy bank pair adds one cycle.  This prints the expectation per wave-instruction of the
+row-per-lane mapping (every lane of an instruction adds the same feature, so its bank is set by
+its random bin): 7.7-8.3, against 6.7-7.7 measured.  A feature-per-lane mapping with a
+[bin][feature] image takes the bin out of the bank; round 5 built it and measured 0.2-0.3
+conflict cycles per instruction, but a slower kernel (docs/perf_notes.md, profiles/r5/hist_fl/).
 
     python benchmarks/lds_conflict_model.py
 """
