@@ -19,25 +19,28 @@ from tests.test_fm import _rows, mapper_average_fm  # noqa: E402
 
 def main():
     grids = [int(g) for g in sys.argv[1:]] or [64, 128, 256]
+    extra = os.environ.get("PROBE_OPTS", "")          # e.g. "-fp32" (with HM_FM_VARIANT=2)
+    reps = int(os.environ.get("PROBE_REPS", "3"))
     n = 3 << 20
     idx, y = criteo_like(n, 20, seed=5)
     eidx, ey = criteo_like(100000, 20, seed=77)
     yy = (ey > 0).float()
     opts = "-c -factors 8 -num_features 1048576 -eta0 0.01 -sigma 0.01"
+    gopts = opts + " " + extra
     ll = lambda t, dev: torch.nn.functional.binary_cross_entropy_with_logits(  # noqa: E731
         t.predict_raw(rows=_rows(eidx).to(dev)).cpu(), yy).item()
     m8 = ll(mapper_average_fm(opts, idx, y, 8, 1 << 20), "cpu")
     print(json.dumps({"mappers8": round(m8, 5)}), flush=True)
     rows = _rows(idx, y).to("cuda")
-    for rep in range(3):
+    for rep in range(reps):
         for g in grids:
             torch.cuda.synchronize()
             t = time.perf_counter()
-            m = FMTrainer(opts + f" -grid {g}", device="cuda").fit(rows=rows)
+            m = FMTrainer(gopts + f" -grid {g}", device="cuda").fit(rows=rows)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
             v = ll(m, "cuda")
-            print(json.dumps({"grid": g, "rep": rep, "gpu": round(v, 5), "delta_vs_mappers8": round(v - m8, 5),
+            print(json.dumps({"opts": extra, "variant": os.environ.get("HM_FM_VARIANT", "0"), "grid": g, "rep": rep, "gpu": round(v, 5), "delta_vs_mappers8": round(v - m8, 5),
                               "rows_per_s": round(n / dt)}), flush=True)
 
 
