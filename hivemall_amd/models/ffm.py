@@ -129,6 +129,12 @@ class FFMTrainer(Learner):
         opt("sigma", None, 0.1, float, "gaussian init stddev"),
         opt("min", "min_target", None, float, "Minimum target (regression clipping)"),
         opt("max", "max_target", None, float, "Maximum target (regression clipping)"),
+        opt("grid", None, 0, int, "[engine] kernel workgroups: bounds the Hogwild rows in flight "
+            "(0 = auto; 1 = one block, the sequential learner)"),
+        opt("atomic_rows", None, None, int,
+            "[engine] a learner's first N rows run on the kernel that adds every slot update with "
+            "float atomics (no update lost to concurrent rows; ~4 M rows/s fp32): the quality / "
+            "speed knob of the Hogwild learner; default 2^18, docs/compat.md)"),
         opt("dp_lr_power", None, DP_LR_POWER, float,
             "[engine] data-parallel training over N ranks: every rank's replica steps with "
             "eta0 * N^p and alpha * N^p, so the mean of the mixed replicas tracks one learner "
@@ -169,7 +175,8 @@ class FFMTrainer(Learner):
         self.state: dict | None = None
         self.cv = ConversionState(not c["disable_cv"], c["cv_rate"])
         self.rows_seen = 0
-        self.grid = 0  # kernel grid override (0 = auto); bounds the Hogwild concurrency
+        self.grid = int(c["grid"])  # kernel grid override (0 = auto); bounds the Hogwild concurrency
+        self.atomic_rows = RAMP_ROWS if c["atomic_rows"] is None else max(0, int(c["atomic_rows"]))
         self.dp_guard_tripped = False
 
     def _set_dp_power(self, power: float) -> None:
@@ -281,7 +288,7 @@ class FFMTrainer(Learner):
             # the first RAMP_ROWS rows of a learner: the atomic-update kernel (RAMP_VARIANT), or
             # RAMP_GRID blocks unless -grid is given — early in training every row moves the same
             # few parameters and concurrent read-modify-writes lose the most
-            cut = min(sub.n, max(0, RAMP_ROWS - self.rows_seen))
+            cut = min(sub.n, max(0, self.atomic_rows - self.rows_seen))
             for r0, r1, ramp in ((0, cut, True), (cut, sub.n, False)):
                 if r1 <= r0:
                     continue

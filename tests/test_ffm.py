@@ -524,3 +524,19 @@ def test_ffm_gpu_tables_of_4gib_and_more(dtype):
     assert float(tg.state["V"][:base].abs().amax()) == 0.0            # nothing else written
     del tg, V, G
     torch.cuda.empty_cache()
+
+
+def test_ffm_engine_options_grid_and_atomic_rows():
+    """train_ffm -grid / -atomic_rows (docs/compat.md: the Hogwild quality / speed knobs) reach the
+    learner; the -atomic_rows default is the module's RAMP_ROWS read at construction."""
+    from hivemall_amd.models import ffm as ffm_model
+
+    t = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 10 -grid 4 -atomic_rows 1000", device="cpu")
+    assert (t.grid, t.atomic_rows) == (4, 1000)
+    old = ffm_model.RAMP_ROWS
+    try:
+        ffm_model.RAMP_ROWS = 12345
+        t = FFMTrainer("-c -factors 4 -num_fields 39 -feature_hashing 10", device="cpu")
+        assert (t.grid, t.atomic_rows) == (0, 12345)
+    finally:
+        ffm_model.RAMP_ROWS = old
