@@ -68,6 +68,7 @@ struct FFMParams {
     // trains them in list mode (it implements the grouped update).  null: no deferral.
     int32_t* defer;
     int list_mode;
+    int lin_defer;                 // sg32: the W_LIN wave waits for the linear DMA at its first use
 };
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
@@ -1017,6 +1018,8 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // access-pattern ceiling, 97.5 M rows/s: profiles/ffm_r3/roofline_sg.log, ab_fp32_sg_reg_*.log;
 // removed); here no VGPR holds the next row and the LDS image is the only staging (55 KB per
 // block -> 2 blocks/CU).
+// s_waitcnt immediate: vmcnt(n) (n <= 63), expcnt / lgkmcnt not waited on
+#define VMCNT_ENC(n) ((((n) & 15) | (((n) >> 4) << 14)) | 0x0F70)
 template <int NS, typename OT, int TPB = 256, int ATOM = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1099,15 +1102,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
         }
     };
+    // The linear state of the next row is DMA'd after this row's FTRL stores (phase F), so it is
+    // the W_LIN wave's youngest load at the next phase A.  That wave therefore waits there only for
+    // its older slot DMAs (vmcnt(NLIN)), and for the linear DMA right before its first read in D
+    // (vmcnt(2 NS): only the next row's slot DMAs, issued in C, may still be in flight).  Every
+    // lane < F issues the DMAs (an invalid feature reads w[0], unused), so the counts are exact.
+    const int nlin = (P.use_linear && P.lin_defer) ? (P.train ? 3 : 1) : 0;
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
-            const int i = s_m[bf][lane].x;
-            if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
-                if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
-                }
+            const int i = max(s_m[bf][lane].x, 0);
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+            if (P.train) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
             }
         }
     };
@@ -1136,7 +1143,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
         // ---- A: this wave's DMAs have landed, then every wave's ----
-        __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
+        if (wave == W_LIN && nlin == 3) __builtin_amdgcn_s_waitcnt(0x0F73);      // vmcnt(3)
+        else if (wave == W_LIN && nlin == 1) __builtin_amdgcn_s_waitcnt(0x0F71); // vmcnt(1)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                                // vmcnt(0)
         bar_raw();
         // ---- B: landing zone -> registers (G) and the transposed image (V); meta(row + G) ----
         float cg[NS];
@@ -1162,6 +1171,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         const float scale = s_red[TPB / 64 + cur];
         int mi = -1;
         float mx = 0.f, lw = 0.f;
+        if (wave == W_LIN && nlin) {
+            // the linear DMA of this row has landed (older than the C-phase slot DMAs)
+            if (more) __builtin_amdgcn_s_waitcnt(VMCNT_ENC(2 * NS));
+            else __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
         if (wave == W_LIN && lane < F) {
             const int4 m = s_m[cur][lane];
             mi = m.x;
@@ -1698,7 +1712,7 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
-//                     slot_g, gstride, vpad, tail16, gfstride
+//                     slot_g, gstride, vpad, tail16, gfstride, lin_defer
 // slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f * gfstride];
 //             bf16 V in 12-B slots {V | G} (G = V + 8 B, gfstride 3): ffm_pipe_sg12_kernel; fp32 V
 //             in the block layout (G = V + vpad * 16 B, vpad > 0): ffm_pipe_sg32_kernel (K <= 4,
@@ -1753,6 +1767,7 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.vpad = ip[19];
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
+    P.lin_defer = ip[22];
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.vfe = (long long)P.fstride * P.sstride;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];

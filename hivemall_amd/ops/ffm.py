@@ -139,6 +139,9 @@ _DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows 
 # HM_FFM_DEFER=0 (A/B only): no multi-hot detection in the pipelined kernels (a row with a
 # repeated field or feature is then updated slot by slot: racing stores of one address)
 _DEFER_ON = os.environ.get("HM_FFM_DEFER", "1") != "0"
+# HM_FFM_LIN_DEFER=0 (A/B only): the fp32 kernel's W_LIN wave waits for the next row's linear-state
+# DMA at phase A with the slot DMAs, instead of at its first use in the forward pass
+_LIN_DEFER = int(os.environ.get("HM_FFM_LIN_DEFER", "1") != "0")
 
 
 def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
@@ -218,7 +221,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0],
+                   G.stride(1) if slot_g else 0, _LIN_DEFER],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
