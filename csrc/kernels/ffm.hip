@@ -69,6 +69,13 @@ struct FFMParams {
     int32_t* defer;
     int list_mode;
     int lin_defer;                 // sg32: the W_LIN wave waits for the linear DMA at its first use
+    // Global-bias FTRL state sharded over bias_s 128-B lines during a training launch (sg32 /
+    // sg12): z0 = sum of bias_sh[32 s], n0 = sum of bias_sh[32 s + 1]; a row adds its step to
+    // shard (block % bias_s).  Null: the single {w0, z0, n0} address (every row's two atomics
+    // and a same-address reload serialised the whole chip: 5.5 M rows/s with -w0).
+    float* bias_sh;
+    int bias_s;
+    int bias_every;                // rows between a block's re-reads of the bias shards
 };
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
@@ -109,6 +116,19 @@ __device__ __forceinline__ void bias_update(const FFMParams& P, float g, float* 
     atomicAdd(bias + 1, dz);
     atomicAdd(bias + 2, g * g);
     bias[0] = ftrl_weight(z0 + dz, n0 + g * g, P.alpha, P.beta, 0.f, 0.f);
+}
+
+// bias_update on the sharded state: (z0, n0) is the row's snapshot of the shard sums
+// (adds the step to acc[0..1]: the block's own steps its copy of the shard sums lacks)
+__device__ __forceinline__ void bias_update_sh(const FFMParams& P, float g, float z0, float n0, float* sh,
+                                               float* acc) {
+    const float w = ftrl_weight(z0, n0, P.alpha, P.beta, 0.f, 0.f);
+    const float sigma = (sqrtf(n0 + g * g) - sqrtf(n0)) / P.alpha;
+    const float dz = g - sigma * w;
+    atomicAdd(sh, dz);
+    atomicAdd(sh + 1, g * g);
+    acc[0] += dz;
+    acc[1] += g * g;
 }
 
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
@@ -1035,6 +1055,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
     __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
     __shared__ int s_rep[TPB / 64];                                   // per wave: a multi-hot slot
+    __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
+    __shared__ float s_bcur[2];                                       // own bias steps since the read
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1121,6 +1143,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 
     int row = bid;
     if (row >= P.B) return;
+    if (tid == 0) { s_bcur[0] = 0.f; s_bcur[1] = 0.f; }
     dma_meta(0, row);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     bar_raw();
@@ -1139,6 +1162,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     float fg[NS];
     OT fo[NS];
     uint32_t fwd = 0u;
+    const bool bsh = P.use_bias && P.bias_sh;
+    // A block re-reads the 64 shard lines every bias_every rows (loads of lines the other blocks'
+    // atomics keep updating are slow: every row took -w0 from 75 to 40 M rows/s) and adds its own
+    // steps since that read (s_bcur) in between; the other blocks' steps arrive with the next read.
+    int bit = 0;                    // rows of this block so far
+    float bz = 0.f, bn = 0.f;       // the W_META lanes' copy of the shard sums, loaded a row ahead
+    if (bsh && wave == W_META && lane < P.bias_s) {
+        bz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
@@ -1147,6 +1180,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         else if (wave == W_LIN && nlin == 1) __builtin_amdgcn_s_waitcnt(0x0F71); // vmcnt(1)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                // vmcnt(0)
         bar_raw();
+        // the bias shards for the NEXT row (one row of extra staleness on one parameter, as
+        // train_fm's w0): issued here, landed by the next phase A's vmcnt(0), used in its D
+        const bool bre = bsh && (bit % P.bias_every) == 0;      // this row re-reads (block-uniform)
+        float nbz = bz, nbn = bn;
+        if (bre && wave == W_META && lane < P.bias_s) {
+            nbz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nbn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // ---- B: landing zone -> registers (G) and the transposed image (V); meta(row + G) ----
         float cg[NS];
 #pragma unroll
@@ -1203,16 +1244,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         part += lw * mx * scale;
         part = hm::wave_sum_uniform(part);
         const int wrep = __any(rep);
+        if (bsh && wave == W_META) {
+            const float z = hm::wave_sum_uniform(bz) + s_bcur[0], n = hm::wave_sum_uniform(bn) + s_bcur[1];
+            if (lane == 0) { s_bias[0] = ftrl_weight(z, n, P.alpha, P.beta, 0.f, 0.f); s_bias[1] = z; s_bias[2] = n; }
+        }
         if (lane == 0) { s_red[wave] = part; s_rep[wave] = wrep; }
         bar_raw();
         float p = 0.f;
         int rdup = 0;
 #pragma unroll
         for (int q = 0; q < TPB / 64; ++q) { p += s_red[q]; rdup |= s_rep[q]; }
-        if (P.use_bias) p += bias_w0(P, bias);
+        if (P.use_bias) p += bsh ? s_bias[0] : bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- E: updates (a multi-hot row is deferred to ffm_row_kernel) ----
+        // the shards read at this row's B lack only this row's own step (wave 0 waits for its
+        // atomics at every phase A, so all earlier ones had landed)
+        if (bre && tid == 0) { s_bcur[0] = 0.f; s_bcur[1] = 0.f; }
         if (P.train && rdup && P.defer) {
             defer_row(P, row);
         } else if (P.train) {
@@ -1279,10 +1327,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
-            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
+            if (P.use_bias && tid == 0) {
+                if (bsh) bias_update_sh(P, kappa, s_bias[1], s_bias[2], P.bias_sh + (blockIdx.x % P.bias_s) * 32, s_bcur);
+                else bias_update(P, kappa, bias);
+            }
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
         if (more) dma_lin(nxt);
+        bz = nbz;
+        bn = nbn;
+        ++bit;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
 #undef SA
@@ -1311,6 +1365,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];
     __shared__ float s_red[8];
     __shared__ int s_rep[4];                                                  // per wave: a multi-hot slot
+    __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
+    __shared__ float s_bcur[2];                                       // own bias steps since the read
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1386,6 +1442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 
     int row = blockIdx.x;
     if (row >= P.B) return;
+    if (tid == 0) { s_bcur[0] = 0.f; s_bcur[1] = 0.f; }
     dma_meta(0, row);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     bar_raw();
@@ -1395,11 +1452,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     dma_lin(0);
     dma_meta(1, row + G);
 
+    const bool bsh = P.use_bias && P.bias_sh;
+    // A block re-reads the 64 shard lines every bias_every rows (loads of lines the other blocks'
+    // atomics keep updating are slow: every row took -w0 from 75 to 40 M rows/s) and adds its own
+    // steps since that read (s_bcur) in between; the other blocks' steps arrive with the next read.
+    int bit = 0;                    // rows of this block so far
+    float bz = 0.f, bn = 0.f;       // the W_META lanes' copy of the shard sums, loaded a row ahead
+    if (bsh && wave == W_META && lane < P.bias_s) {
+        bz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     for (int cur = 0; row < P.B; row += G, cur ^= 1) {
         const int nxt = cur ^ 1;
         const bool more = row + G < P.B;
         __builtin_amdgcn_s_waitcnt(0x0F70);                                     // vmcnt(0)
         bar_raw();
+        // the bias shards for the NEXT row (one row of extra staleness on one parameter, as
+        // train_fm's w0): issued here, landed by the next phase A's vmcnt(0), used in its D
+        const bool bre = bsh && (bit % P.bias_every) == 0;      // this row re-reads (block-uniform)
+        float nbz = bz, nbn = bn;
+        if (bre && wave == W_META && lane < P.bias_s) {
+            nbz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nbn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // ---- B: landing zone -> G registers + transposed V image ----
         float cg[NS];
 #pragma unroll
@@ -1444,14 +1519,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         part += lw * mx * scale;
         part = hm::wave_sum_uniform(part);
         const int wrep = __any(rep);
+        if (bsh && wave == W_META) {
+            const float z = hm::wave_sum_uniform(bz) + s_bcur[0], n = hm::wave_sum_uniform(bn) + s_bcur[1];
+            if (lane == 0) { s_bias[0] = ftrl_weight(z, n, P.alpha, P.beta, 0.f, 0.f); s_bias[1] = z; s_bias[2] = n; }
+        }
         if (lane == 0) { s_red[wave] = part; s_rep[wave] = wrep; }
         bar_raw();
         float p = s_red[0] + s_red[1] + s_red[2] + s_red[3];
         const bool rdup = (s_rep[0] | s_rep[1] | s_rep[2] | s_rep[3]) != 0;
-        if (P.use_bias) p += bias_w0(P, bias);
+        if (P.use_bias) p += bsh ? s_bias[0] : bias_w0(P, bias);
         const float kappa = row_loss(P, row, p, y, pred_out, loss_out);
 
         // ---- E: updates (a multi-hot row is deferred to ffm_row_kernel) ----
+        // the shards read at this row's B lack only this row's own step (wave 0 waits for its
+        // atomics at every phase A, so all earlier ones had landed)
+        if (bre && tid == 0) { s_bcur[0] = 0.f; s_bcur[1] = 0.f; }
         if (P.train && rdup && P.defer) {
             defer_row(P, row);
         } else if (P.train) {
@@ -1510,11 +1592,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 wn[mi] = n1;
                 w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
             }
-            if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
+            if (P.use_bias && tid == 0) {
+                if (bsh) bias_update_sh(P, kappa, s_bias[1], s_bias[2], P.bias_sh + (blockIdx.x % P.bias_s) * 32, s_bcur);
+                else bias_update(P, kappa, bias);
+            }
         }
         if (more) dma_lin(nxt);
+        bz = nbz;
+        bn = nbn;
+        ++bit;
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
 #undef SA
 #undef SB
 }
@@ -1768,6 +1856,10 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
     P.lin_defer = ip[22];
+    P.bias_sh = aux ? reinterpret_cast<float*>(aux[2]) : nullptr;
+    P.bias_s = aux ? (int)reinterpret_cast<intptr_t>(aux[3]) : 0;
+    if (!P.bias_sh || P.bias_s < 1 || P.bias_s > 64 || !P.train) { P.bias_sh = nullptr; P.bias_s = 0; }
+    P.bias_every = ip[23] > 0 ? ip[23] : 16;
     if (P.fstride < P.num_fields) return (int)hipErrorInvalidValue;
     P.vfe = (long long)P.fstride * P.sstride;
     P.eta0 = hp[0]; P.eps = hp[1]; P.lambda_v = hp[2]; P.alpha = hp[3]; P.beta = hp[4];

@@ -136,6 +136,20 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
 
 
 _DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
+# Global-bias FTRL state sharded over this many 128-B lines during a training launch (csrc/kernels/
+# ffm.hip FFMParams.bias_sh): one same-address pair of atomics per row held -w0 runs at 5.5 M
+# rows/s (profiles/r5/ffm_w0_rate.jsonl).  HM_FFM_BIAS_SHARDS=0: the single address (A/B only).
+BIAS_SHARDS = int(os.environ.get("HM_FFM_BIAS_SHARDS", "64"))
+BIAS_EVERY = int(os.environ.get("HM_FFM_BIAS_EVERY", "16"))   # rows between a block's re-reads
+_BIAS_SH: dict = {}
+
+
+def _bias_shards(device: torch.device) -> torch.Tensor:
+    sh = _BIAS_SH.get(device)
+    if sh is None or sh.shape[0] != BIAS_SHARDS:
+        sh = torch.zeros((BIAS_SHARDS, 32), dtype=torch.float32, device=device)
+        _BIAS_SH[device] = sh
+    return sh
 # HM_FFM_DEFER=0 (A/B only): no multi-hot detection in the pipelined kernels (a row with a
 # repeated field or feature is then updated slot by slot: racing stores of one address)
 _DEFER_ON = os.environ.get("HM_FFM_DEFER", "1") != "0"
@@ -221,7 +235,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0, _LIN_DEFER],
+                   G.stride(1) if slot_g else 0, _LIN_DEFER, BIAS_EVERY],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
@@ -232,9 +246,21 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
             assert hot.dtype == torch.uint8 and hot.numel() >= NF and hot.device == V.device
         # multi-hot rows (a repeated field or feature) are deferred by the pipelined kernels to
         # the grouped-update kernel through this buffer (same stream, no host sync)
-        aux = (ctypes.c_void_p * 2)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None)
+        bsh = _bias_shards(V.device) if (train and hyper.use_bias and BIAS_SHARDS > 0) else None
+        if bsh is not None:
+            # shard 0 <- the bias FTRL state (z0, n0), the other shards 0; the pipelined kernels add
+            # each row's step to shard (block % S), the generic kernel (deferred rows) to bias itself
+            b = state["bias"]
+            zn0 = b[1:3].clone()
+            bsh.zero_()
+            bsh[0, :2] = zn0
+        aux = (ctypes.c_void_p * 4)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
+                                    p(bsh), bsh.shape[0] if bsh is not None else 0)
         rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
+        if bsh is not None:
+            # (z0, n0) = the shard sums plus whatever the generic kernel added to bias directly
+            b[1:3] = bsh[:, :2].sum(0) + (b[1:3] - zn0)
         if train and hyper.use_bias:
             # w0 = f(z0, n0): the kernel accumulates z0/n0 atomically and its cached bias[0] is
             # whichever block wrote last; refresh it (FTRL weight with l1 = l2 = 0)

@@ -275,7 +275,7 @@ def test_ffm_gpu_bf16_state_close_to_fp32_engine(layout, adagrad):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("adagrad", ["", "-elementwise_adagrad"])
+@pytest.mark.parametrize("adagrad", ["", "-elementwise_adagrad", "-w0"])
 def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
     """grid=1: one workgroup walks the rows in order = Hivemall's per-row semantics.  The generic
     kernel (variant 1) has no lookahead; the pipelined default DMAs row r+1's slots before row
