@@ -69,6 +69,12 @@ struct FFMParams {
     int32_t* defer;
     int list_mode;
     int lin_defer;                 // sg32: the W_LIN wave waits for the linear DMA at its first use
+    // Linear FTRL state addressing: w / wz / wn of feature i at [i * lstride].  lpack: wz = w + 1,
+    // wn = w + 2, 16-B aligned records (the GPU block layouts keep {w, z, n} in the 16-B chunk
+    // after each feature's G region, a line the row reads and writes anyway): one 16-B DMA and
+    // one 16-B store per feature instead of three scattered 4-B ones into three more lines.
+    long long lstride;
+    int lpack;
     // Global-bias FTRL state sharded over bias_s 128-B lines during a training launch (sg32 /
     // sg12): z0 = sum of bias_sh[32 s], n0 = sum of bias_sh[32 s + 1]; a row adds its step to
     // shard (block % bias_s).  Null: the single {w0, z0, n0} address (every row's two atomics
@@ -77,6 +83,9 @@ struct FFMParams {
     int bias_s;
     int bias_every;                // rows between a block's re-reads of the bias shards
 };
+
+// the linear state of feature i (FFMParams.lstride)
+#define LW(p, i) ((p)[(size_t)(i) * (size_t)P.lstride])
 
 __device__ __forceinline__ float ftrl_weight(float z, float n, float alpha, float beta,
                                              float l1, float l2) {
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
             part += d * s_x[a] * s_x[b];
         }
         part *= scale * scale;
-        if (P.use_linear && tid < F && s_idx[tid] >= 0) part += w[s_idx[tid]] * s_x[tid] * scale;
+        if (P.use_linear && tid < F && s_idx[tid] >= 0) part += LW(w, s_idx[tid]) * s_x[tid] * scale;
         float p = hm::block_sum(part, s_red);
         if (P.use_bias) p += bias_w0(P, bias);
 
@@ -466,7 +475,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 float xs = s_x[tid];
                 if (multi)
                     for (int a2 = s_ni[tid]; a2 >= 0; a2 = s_ni[a2]) xs += s_x[a2];
-                w[i] = ftrl_update(wz + i, wn + i, w[i], kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
+                LW(w, i) = ftrl_update(&LW(wz, i), &LW(wn, i), LW(w, i), kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
@@ -582,7 +591,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
             __syncthreads();
         }
         float lw = 0.f;
-        if (P.use_linear && mi >= 0) lw = w[mi];
+        if (P.use_linear && mi >= 0) lw = LW(w, mi);
 
         // ---- gather (branch-free): own raw slot -> registers, own V -> transposed LDS image.
         //      Dead slots (a == b, padding) load slot 0 and get x_a x_b = 0. ----
@@ -637,7 +646,7 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
             defer_row(P, row);                  // multi-hot row: ffm_row_kernel trains it
         } else if (P.train) {
             float lz = 0.f, ln = 0.f;
-            if (P.use_linear && mi >= 0) { lz = wz[mi]; ln = wn[mi]; }
+            if (P.use_linear && mi >= 0) { lz = LW(wz, mi); ln = LW(wn, mi); }
             const float ks = kappa * scale * scale;
             const f2 lam = {P.lambda_v, P.lambda_v}, eps = {P.eps, P.eps};
             const f2 meta = {-P.eta0, -P.eta0};
@@ -688,9 +697,9 @@ __global__ __launch_bounds__(256) void ffm_lean_kernel(
                 const float g = kappa * mx * scale;
                 const float n1 = ln + g * g;
                 const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                wz[mi] = z1;
-                wn[mi] = n1;
-                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                LW(wz, mi) = z1;
+                LW(wn, mi) = n1;
+                LW(w, mi) = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
@@ -835,10 +844,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
             if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wz, i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wn, i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
                 }
             }
         }
@@ -1008,9 +1017,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 4 : 2)
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                    wz[mi] = z1;
-                    wn[mi] = n1;
-                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                    LW(wz, mi) = z1;
+                    LW(wn, mi) = n1;
+                    LW(w, mi) = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
@@ -1053,6 +1062,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
+    __shared__ __attribute__((aligned(16))) float4 s_lin4[2][48];     // ... as {w, z, n, _} (lpack)
     __shared__ float s_red[TPB / 64 + 2];                             // [0..NW) sums, [NW+b] scale
     __shared__ int s_rep[TPB / 64];                                   // per wave: a multi-hot slot
     __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
@@ -1129,14 +1139,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     // its older slot DMAs (vmcnt(NLIN)), and for the linear DMA right before its first read in D
     // (vmcnt(2 NS): only the next row's slot DMAs, issued in C, may still be in flight).  Every
     // lane < F issues the DMAs (an invalid feature reads w[0], unused), so the counts are exact.
-    const int nlin = (P.use_linear && P.lin_defer) ? (P.train ? 3 : 1) : 0;
+    const int nlin = (P.use_linear && P.lin_defer) ? ((P.lpack || !P.train) ? 1 : 3) : 0;
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = max(s_m[bf][lane].x, 0);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+            if (P.lpack) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin4[bf][0], 16, 0, 0);
+                return;
+            }
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
             if (P.train) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wz, i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wn, i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
             }
         }
     };
@@ -1221,7 +1235,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             const int4 m = s_m[cur][lane];
             mi = m.x;
             mx = __int_as_float(m.z);
-            lw = s_lin[cur][0][lane];
+            lw = P.lpack ? s_lin4[cur][lane].x : s_lin[cur][0][lane];
         }
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
@@ -1312,19 +1326,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             // profiles/r4/ffm_skip_diagonal_ab.log.)
             if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                    const float lz = s_lin[cur][1][lane];
-                    const float ln = s_lin[cur][2][lane];
+                    const float lz = P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane];
+                    const float ln = P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane];
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
+                    const float w1 = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                     if (ATOM == 1 || (ATOM == 2 && s_m[cur][lane].w != 0)) {
-                        atomicAdd(wz + mi, z1 - lz);
-                        atomicAdd(wn + mi, g * g);
+                        atomicAdd(&LW(wz, mi), z1 - lz);
+                        atomicAdd(&LW(wn, mi), g * g);
+                        LW(w, mi) = w1;
+                    } else if (P.lpack) {
+                        *reinterpret_cast<float4*>(&LW(w, mi)) = make_float4(w1, z1, n1, 0.f);
                     } else {
-                        wz[mi] = z1;
-                        wn[mi] = n1;
+                        LW(wz, mi) = z1;
+                        LW(wn, mi) = n1;
+                        LW(w, mi) = w1;
                     }
-                    w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
                 }
             }
             if (P.use_bias && tid == 0) {
@@ -1363,6 +1381,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];
+    __shared__ __attribute__((aligned(16))) float4 s_lin4[2][48];     // ... as {w, z, n, _} (lpack)
     __shared__ float s_red[8];
     __shared__ int s_rep[4];                                                  // per wave: a multi-hot slot
     __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
@@ -1374,6 +1393,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
+    // lpack with the records inside the blocks (the first 16-B chunk after the 12-B slots)
+    const bool lin_in_tail = P.lpack && reinterpret_cast<const char*>(w) == vb + (size_t)P.vpad * 12;
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 
     int ab[NS];
@@ -1430,11 +1451,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = s_m[bf][lane].x;
-            if (i >= 0) {
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(w + i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
+            if (i >= 0 && P.lpack) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin4[bf][0], 16, 0, 0);
+            } else if (i >= 0) {
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wz + i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wn + i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wz, i), (lds_ptr_t)&s_lin[bf][1][0], 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(wn, i), (lds_ptr_t)&s_lin[bf][2][0], 4, 0, 0);
                 }
             }
         }
@@ -1496,7 +1519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             const int4 m = s_m[cur][lane];
             mi = m.x;
             mx = __int_as_float(m.z);
-            lw = s_lin[cur][0][lane];
+            lw = P.lpack ? s_lin4[cur][lane].x : s_lin[cur][0][lane];
         }
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
@@ -1579,18 +1602,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                     if (i < 0) continue;
                     char* blk = vb + (OT)(uint32_t)i * bs;
                     if (kk < npad) *reinterpret_cast<u3v*>(blk + (P.num_fields + kk) * 12) = u3v{0u, 0u, 0u};
-                    else *reinterpret_cast<uint4*>(blk + P.vpad * 12 + 16 * (kk - npad)) = make_uint4(0u, 0u, 0u, 0u);
+                    else if (!(lin_in_tail && kk == npad))   // the first tail chunk holds {w, z, n}
+                        *reinterpret_cast<uint4*>(blk + P.vpad * 12 + 16 * (kk - npad)) = make_uint4(0u, 0u, 0u, 0u);
                 }
             }
             if (mi >= 0 && P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                const float lz = s_lin[cur][1][lane];
-                const float ln = s_lin[cur][2][lane];
+                const float lz = P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane];
+                const float ln = P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane];
                 const float g = kappa * mx * scale;
                 const float n1 = ln + g * g;
                 const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
-                wz[mi] = z1;
-                wn[mi] = n1;
-                w[mi] = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                const float w1 = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
+                if (P.lpack) {
+                    *reinterpret_cast<float4*>(&LW(w, mi)) = make_float4(w1, z1, n1, 0.f);
+                } else {
+                    LW(wz, mi) = z1;
+                    LW(wn, mi) = n1;
+                    LW(w, mi) = w1;
+                }
             }
             if (P.use_bias && tid == 0) {
                 if (bsh) bias_update_sh(P, kappa, s_bias[1], s_bias[2], P.bias_sh + (blockIdx.x % P.bias_s) * 32, s_bcur);
@@ -1856,6 +1885,10 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.tail16 = ip[20];
     P.gfstride = ip[21] > 0 ? ip[21] : 1;
     P.lin_defer = ip[22];
+    P.lstride = ip[24] > 0 ? ip[24] : 1;
+    P.lpack = ip[25];
+    if (P.lpack && (wz != w + 1 || wn != w + 2 || (P.lstride & 3) || (reinterpret_cast<uintptr_t>(w) & 15)))
+        return (int)hipErrorInvalidValue;
     P.bias_sh = aux ? reinterpret_cast<float*>(aux[2]) : nullptr;
     P.bias_s = aux ? (int)reinterpret_cast<intptr_t>(aux[3]) : 0;
     if (!P.bias_sh || P.bias_s < 1 || P.bias_s > 64 || !P.train) { P.bias_sh = nullptr; P.bias_s = 0; }

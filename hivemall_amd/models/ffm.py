@@ -31,7 +31,11 @@ import pandas as pd
 import torch
 
 from ..ops import ffm as _ffm_ops
-from ..ops.ffm import FFMHyper, ffm_step, is_packed, new_state_tables
+from ..ops.ffm import FFMHyper, ffm_step, is_packed, lin_record_views, new_state_tables
+
+# GPU block layouts: w / wz / wn as the 16-B record after each feature's slots (ops/ffm.py
+# lin_record_views); HM_FFM_LIN_SEPARATE=1 keeps three separate arrays (A/B only)
+LIN_IN_BLOCK = os.environ.get("HM_FFM_LIN_SEPARATE", "0") != "1"
 from ..ops.touched import mark_touched
 from ..utils.features import CSR, parse_ffm_rows
 from ..utils.options import opt, flag, UDFArgumentException
@@ -228,12 +232,16 @@ class FFMTrainer(Learner):
             e = min(self.num_features, s + rows_per)
             chunk = init((e - s) * self.num_fields * self.k).view(e - s, self.num_fields, self.k)
             V[s:e, :, : self.k].copy_(chunk.to(dev))
+        # the GPU block layouts hold each feature's FTRL {w, z, n} in the 16-B chunk after its slots
+        lin = lin_record_views(V, G) if LIN_IN_BLOCK else None
+        if lin is None:
+            lin = tuple(torch.zeros(self.num_features, dtype=torch.float32, device=dev) for _ in range(3))
         self.state = dict(
             V=V,
             G=G,
-            w=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
-            wz=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
-            wn=torch.zeros(self.num_features, dtype=torch.float32, device=dev),
+            w=lin[0],
+            wz=lin[1],
+            wn=lin[2],
             bias=torch.zeros(4, dtype=torch.float32, device=dev),
         )
         self.touched = torch.zeros(self.num_features, dtype=torch.bool, device=dev)

@@ -98,6 +98,46 @@ def slot12_layout(num_fields: int) -> tuple[int, int]:
     return fs, (fs * 12 + 127) // 128 * 128
 
 
+def lin_record_views(V: torch.Tensor, G: torch.Tensor) -> tuple | None:
+    """(w, wz, wn) as views of the 16-B chunk after each feature's slots in the GPU per-slot block
+    layouts (fp32 V: after the G region, byte 800 of 896 for 39 fields; bf16 12-B slots: byte 480
+    of 512), or None when V / G are not such a layout.  The kernels then read and write a feature's
+    {w, z, n} as one 16-B record in a line the row already touches (csrc/kernels/ffm.hip
+    FFMParams.lpack)."""
+    if not V.is_cuda or G.dim() != 2 or V.dim() != 3:
+        return None
+    NF, nfld, kp = V.shape
+    es = V.element_size()
+    bs = V.stride(0) * es
+    d = G.data_ptr() - V.data_ptr()
+    if V.dtype == torch.bfloat16 and d == 8:                 # 12-B slots {V bf16 x 4 | G}
+        fs, bs12 = slot12_layout(nfld)
+        off, ok = fs * 12, bs12 == bs
+    elif V.dtype == torch.float32 and d > 0:
+        fs, bs32, goff = slot_block_layout(nfld, kp, V.dtype)
+        off, ok = goff + fs * 4, bs32 == bs and goff == d
+    else:
+        return None
+    if not ok or off + 16 > bs or off % 16 or bs % 16:
+        return None
+    raw = torch.empty(0, dtype=torch.uint8, device=V.device).set_(
+        V.untyped_storage(), V.storage_offset() * es, (NF, bs), (bs, 1))
+    rec = raw[:, off:off + 16].view(torch.float32)          # [NF, 4]: w, z, n, pad
+    return rec[:, 0], rec[:, 1], rec[:, 2]
+
+
+def _lin_addressing(state: dict) -> tuple[int, int]:
+    """(lstride, lpack) of the state's linear tables for hm_ffm_step."""
+    w, wz, wn = state["w"], state["wz"], state["wn"]
+    ls = w.stride(0) if w.dim() == 1 else 1
+    pack = int(w.is_cuda and ls > 1 and wz.stride(0) == ls and wn.stride(0) == ls
+               and wz.data_ptr() == w.data_ptr() + 4 and wn.data_ptr() == w.data_ptr() + 8
+               and w.data_ptr() % 16 == 0 and ls % 4 == 0)
+    if not pack:
+        assert ls == 1 or w.is_cuda, "CPU FFM state: contiguous linear tables"
+    return ls, pack
+
+
 def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
                      packed: bool, slot_g: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """Zeroed (V, G).
@@ -235,7 +275,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0, _LIN_DEFER, BIAS_EVERY],
+                   G.stride(1) if slot_g else 0, _LIN_DEFER, BIAS_EVERY] + list(_lin_addressing(state)),
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
