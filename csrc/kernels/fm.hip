@@ -40,7 +40,13 @@ struct FMParams {
     float w0_tol;             // ... and a re-read as soon as the wave's own bias steps since the
                               // last one add up to more than w0_tol x eta (0: off)
     uint32_t seed;
+    long long vstride;        // V elements between feature rows (>= KP)
+    long long wstride;        // floats between features' w (1: its own array; a record: inside
+                              // the feature's V row, so the gather and the store touch one line)
 };
+
+// w of feature i (strided: separate array or a field of the feature's record)
+#define FW(i) w[(size_t)(i) * (size_t)P.wstride]
 
 __device__ __forceinline__ float fm_eta(const FMParams& P, float t) {
     if (P.eta_kind == 0) return P.eta0;
@@ -58,9 +64,9 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 template <int KP, bool BF16>
 struct VRow {
     float v[KP];
-    __device__ __forceinline__ void load(const void* V, int i) {
+    __device__ __forceinline__ void load(const void* V, int i, size_t vs) {
         if constexpr (BF16) {
-            const uint16_t* p = reinterpret_cast<const uint16_t*>(V) + (size_t)i * KP;
+            const uint16_t* p = reinterpret_cast<const uint16_t*>(V) + (size_t)i * vs;
             if constexpr (KP % 8 == 0) {
 #pragma unroll
                 for (int c = 0; c < KP / 8; ++c) {
@@ -80,7 +86,7 @@ struct VRow {
                 v[3] = __uint_as_float(q.y & 0xFFFF0000u);
             }
         } else {
-            const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(V) + (size_t)i * KP);
+            const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(V) + (size_t)i * vs);
 #pragma unroll
             for (int c = 0; c < KP / 4; ++c) {
                 const float4 q = p[c];
@@ -88,9 +94,9 @@ struct VRow {
             }
         }
     }
-    __device__ __forceinline__ void store(void* V, int i, uint32_t rbase) const {
+    __device__ __forceinline__ void store(void* V, int i, size_t vs, uint32_t rbase) const {
         if constexpr (BF16) {
-            uint16_t* p = reinterpret_cast<uint16_t*>(V) + (size_t)i * KP;
+            uint16_t* p = reinterpret_cast<uint16_t*>(V) + (size_t)i * vs;
             uint32_t wds[KP / 2];
 #pragma unroll
             for (int j = 0; j < KP / 2; ++j) {
@@ -105,7 +111,7 @@ struct VRow {
                 *reinterpret_cast<uint2*>(p) = make_uint2(wds[0], wds[1]);
             }
         } else {
-            float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(V) + (size_t)i * KP);
+            float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(V) + (size_t)i * vs);
 #pragma unroll
             for (int c = 0; c < KP / 4; ++c) p[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
         }
@@ -149,8 +155,8 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             VRow<KP, BF16> t;
             float wi = 0.f;
             if (i >= 0) {
-                t.load(V, i);
-                wi = w[i];
+                t.load(V, i, P.vstride);
+                wi = FW(i);
             } else {
 #pragma unroll
                 for (int f = 0; f < KP; ++f) t.v[f] = 0.f;
@@ -197,13 +203,13 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
         const float eta = fm_eta(P, (float)(t0 + row + 1));
         const uint32_t rbase = P.seed ^ (uint32_t)(t0 + row) * 0x9E3779B9u;
         auto upd = [&](VRow<KP, BF16>& t, int i, float x, float wi) {
-            w[i] = wi - eta * (d * x + 2.f * P.lambda_w * wi);
+            FW(i) = wi - eta * (d * x + 2.f * P.lambda_w * wi);
 #pragma unroll
             for (int f = 0; f < KP; ++f) {
                 const float g = d * x * (S[f] - t.v[f] * x) + 2.f * P.lambda_v * t.v[f];
                 t.v[f] = f < P.k ? t.v[f] - eta * g : 0.f;
             }
-            t.store(V, i, rbase);
+            t.store(V, i, P.vstride, rbase);
         };
         if (ci >= 0) upd(vr, ci, cx, cw);
         for (int base = 64; base < nnz; base += 64) {  // rows wider than one wave
@@ -213,8 +219,8 @@ __global__ __launch_bounds__(256) void fm_kernel(FMParams P, const int64_t* __re
             if (i < 0 || i >= P.dims) continue;
             const float x = val ? val[s + j] : 1.f;
             VRow<KP, BF16> t;
-            t.load(V, i);
-            upd(t, i, x, w[i]);
+            t.load(V, i, P.vstride);
+            upd(t, i, x, FW(i));
         }
         // per-row atomic (batching w0 deltas per wave was measured to diverge: every wave's
         // locally-converged delta is summed -> ~#waves x overshoot on the hottest parameter),
@@ -277,8 +283,8 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
         VRow<KP, BF16> vr;
         float wi = 0.f;
         if (i >= 0) {
-            vr.load(V, i);
-            wi = w[i];
+            vr.load(V, i, P.vstride);
+            wi = FW(i);
         } else {
 #pragma unroll
             for (int f = 0; f < KP; ++f) vr.v[f] = 0.f;
@@ -317,8 +323,8 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
             }
             if (i2 >= 0) {
                 VRow<KP, BF16> t;
-                t.load(V, i2);
-                lin += w[i2] * x2;
+                t.load(V, i2, P.vstride);
+                lin += FW(i2) * x2;
 #pragma unroll
                 for (int f = 0; f < KP; ++f) {
                     const float vx = t.v[f] * x2;
@@ -358,13 +364,13 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
             const float eta = fm_eta(P, (float)(t0 + row + 1));
             const uint32_t rbase = P.seed ^ (uint32_t)(t0 + row) * 0x9E3779B9u;
             auto upd = [&](VRow<KP, BF16>& t, int ii, float xx, float ww) {
-                w[ii] = ww - eta * (d * xx + 2.f * P.lambda_w * ww);
+                FW(ii) = ww - eta * (d * xx + 2.f * P.lambda_w * ww);
 #pragma unroll
                 for (int f = 0; f < KP; ++f) {
                     const float g = d * xx * (S[f] - t.v[f] * xx) + 2.f * P.lambda_v * t.v[f];
                     t.v[f] = f < P.k ? t.v[f] - eta * g : 0.f;
                 }
-                t.store(V, ii, rbase);
+                t.store(V, ii, P.vstride, rbase);
             };
             if (i >= 0) upd(vr, i, x, wi);
             for (int base = 64; base < nnz; base += 64) {
@@ -374,8 +380,8 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
                 if (i2 < 0 || i2 >= P.dims) continue;
                 const float x2 = val ? val[s + j] : 1.f;
                 VRow<KP, BF16> t;
-                t.load(V, i2);
-                upd(t, i2, x2, w[i2]);
+                t.load(V, i2, P.vstride);
+                upd(t, i2, x2, FW(i2));
             }
             if (P.use_w0) {
                 const float dw0 = -eta * (d + 2.f * P.lambda0 * w0v);
@@ -421,8 +427,10 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 }  // namespace
 
 // ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant,
-//     w0_every
-//     (variant 0 = fm_pipe_kernel, 1 = fm_kernel)
+//     w0_every, vstride, wstride
+//     (variant 0 = fm_pipe_kernel, 1 = fm_kernel; vstride = V elements per feature row (0: KP),
+//     wstride = floats between consecutive w (0: 1); models/fm.py keeps w in the padding of each
+//     feature's V row on the GPU)
 // hp: eta0, power_t, total_steps, lambda0, lambda_w, lambda_v, min_target, max_target, w0_tol
 HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_t t0,
                       const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
@@ -440,6 +448,14 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
     P.w0_tol = hp[8];
+    P.vstride = ip[13] > 0 ? ip[13] : KP;
+    P.wstride = ip[14] > 0 ? ip[14] : 1;
+    {
+        // rows are read / written as 16-B (8-B for KP == 4 bf16) vectors
+        const size_t es = bf16 ? 2 : 4, vec = (bf16 && KP == 4) ? 8 : 16;
+        if (P.vstride < KP || ((size_t)P.vstride * es) % vec || reinterpret_cast<uintptr_t>(V) % vec)
+            return (int)hipErrorInvalidValue;
+    }
     if (n_rows <= 0) return 0;
 #define HM_FM_CASE(K)                                                                            \
     case K:                                                                                      \

@@ -20,7 +20,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from ..ops.fm import FMHyper, fm_step
+from ..ops.fm import FMHyper, fm_step, new_state_tables
 from ..ops.touched import mark_touched
 
 # global-bias shards on the GPU (see ops/fm.py): one same-address atomic per row capped train_fm
@@ -145,8 +145,13 @@ class FMTrainer(Learner):
                 self.cl["maxval"] / math.sqrt(self.k))
         else:
             V[:, : self.k] = torch.randn(self.dims, self.k, generator=g) * self.cl["sigma"]
-        self.state = dict(w=torch.zeros(self.dims, dtype=torch.float32, device=dev),
-                          V=V.to(dev, torch.bfloat16 if bf16 else torch.float32).contiguous(),
+        if dev.type == "cuda":
+            # w in the padding of each feature's V row (ops/fm.py new_state_tables)
+            w, Vt = new_state_tables(self.dims, self.kp, torch.bfloat16 if bf16 else torch.float32, dev)
+            Vt.copy_(V)
+        else:
+            w, Vt = torch.zeros(self.dims, dtype=torch.float32), V.contiguous()
+        self.state = dict(w=w, V=Vt,
                           w0=torch.zeros(W0_SHARDS * W0_STRIDE if dev.type == "cuda" else 1,
                                          dtype=torch.float32, device=dev))
         self.touched = torch.zeros(self.dims, dtype=torch.bool, device=dev)

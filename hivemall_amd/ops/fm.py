@@ -52,6 +52,32 @@ W0_WARM_ROWS = 1 << 20
 W0_TOL = float(os.environ.get("HM_FM_W0_TOL", "0"))
 
 
+# w inside each feature's V record (new_state_tables): measured and not the default.  Config 2
+# (2^24 features, k = 8, bf16), same box, 3 interleaved pairs (profiles/r5/fm_w_record_ab.log):
+# 249-254 M rows/s vs 233-237 M (+7.5 %), but held-out 0.4773-0.4777 vs 0.4753-0.4759; against
+# the 8-mapper average (benchmarks/fm_grid_parity_probe.py, grid 256, 3 reps) +4.0e-3 .. +4.5e-3
+# vs +2.9e-3 .. +3.7e-3.  One line per feature instead of two stays longer in each XCD's L2, and
+# the non-coherent L2s then serve older copies to the other XCDs (docs/perf_notes.md).
+W_RECORD = os.environ.get("HM_FM_W_RECORD", "0") == "1"
+
+
+def new_state_tables(dims: int, KP: int, dtype: torch.dtype, device) -> tuple:
+    """(w, V) for the GPU kernel.  Default: a separate w array and a contiguous V.  With
+    HM_FM_W_RECORD=1 each feature's w lives in the padding of its V row (a 16-B aligned record
+    {V[0..KP), w}), so a row's gather and its update store touch one line per feature instead of
+    two; w is then a strided fp32 view and V a row-strided view, ordinary tensors to everything
+    else (mixing, model tables, checkpoints)."""
+    es = torch.empty(0, dtype=dtype).element_size()
+    if not W_RECORD:
+        return (torch.zeros(dims, dtype=torch.float32, device=device),
+                torch.zeros((dims, KP), dtype=dtype, device=device))
+    rec = (KP * es + 4 + 15) // 16 * 16                       # bytes per feature record
+    buf = torch.zeros((dims, rec // 4), dtype=torch.float32, device=device)
+    w = buf[:, KP * es // 4]
+    V = buf.view(dtype)[:, :KP]
+    return w, V
+
+
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
             y: torch.Tensor | None, h: FMHyper, k: int, train: bool = True, t0: int = 0,
             pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0) -> None:
@@ -77,8 +103,10 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),
                    max(1, min(W0_EVERY_MAX, int(os.environ.get(
-                       "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1)))))],
+                       "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1))))),
+                   V.stride(0), w.stride(0)],
                   dtype=np.int32)
+    assert V.stride(1) == 1 and V.stride(0) >= KP, "V rows must be contiguous"
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
     hp = np.array([h.eta0, h.power_t, h.total_steps, h.lambda0, h.lambda_w, h.lambda_v,
                    h.min_target, h.max_target, W0_TOL], dtype=np.float32)
@@ -90,6 +118,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
         _native.check(rc, "hm_fm_step")
     else:
         assert not bf16, "CPU FM engine keeps V in fp32"
+        assert V.is_contiguous() and w.is_contiguous(), "CPU FM engine: contiguous w and V"
         rc = _native.host().hm_fm_step_cpu(*args)
         if rc != 0:
             raise RuntimeError(f"hm_fm_step_cpu failed: {rc}")

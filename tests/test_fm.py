@@ -53,8 +53,25 @@ def test_train_fm_string_features_regression():
     assert set(tab["feature"][1:]) == {"a", "b", "c"}
 
 
+@pytest.mark.parametrize("KP,dt", [(4, torch.bfloat16), (8, torch.bfloat16), (16, torch.bfloat16),
+                                   (8, torch.float32)])
+def test_fm_w_record_views(monkeypatch, KP, dt):
+    """HM_FM_W_RECORD layout: w in the padding of each feature's V row, 16-B aligned records."""
+    from hivemall_amd.ops import fm as fmop
+    monkeypatch.setattr(fmop, "W_RECORD", True)
+    w, V = fmop.new_state_tables(7, KP, dt, "cpu")
+    assert V.shape == (7, KP) and V.stride(1) == 1 and (V.stride(0) * V.element_size()) % 16 == 0
+    assert w.untyped_storage().data_ptr() == V.untyped_storage().data_ptr()
+    V.fill_(1.5)
+    w.copy_(torch.arange(7, dtype=torch.float32))
+    assert (V == 1.5).all() and torch.equal(w, torch.arange(7, dtype=torch.float32))
+
+
 @pytest.mark.gpu
-def test_fm_gpu_fp32_matches_cpu_on_distinct_features():
+@pytest.mark.parametrize("record", [False, True])
+def test_fm_gpu_fp32_matches_cpu_on_distinct_features(monkeypatch, record):
+    from hivemall_amd.ops import fm as fmop
+    monkeypatch.setattr(fmop, "W_RECORD", record)
     B, F = 256, 39
     idx = torch.arange(B * F, dtype=torch.int32).reshape(B, F)
     y = torch.where(torch.rand(B) < 0.3, 1.0, -1.0)
@@ -65,6 +82,8 @@ def test_fm_gpu_fp32_matches_cpu_on_distinct_features():
         t.init_state(B * F)
         rows = _rows(idx, y).to(dev)
         t.train_rows(rows)
+        if dev == "cuda":
+            assert (t.state["w"].stride(0) > 1) == record
         res[dev] = {k: v.float().cpu() for k, v in t.state.items()}
     for k in ("w", "V"):
         np.testing.assert_allclose(res["cuda"][k].numpy(), res["cpu"][k].numpy(), rtol=1e-4, atol=1e-6)
