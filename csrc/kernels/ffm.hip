@@ -1638,9 +1638,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 
 
 // 8,192 blocks (8 per CU, 4 resident at a time) unless the batch is smaller or a grid is given.
-// The bf16 12-B-slot kernel takes 32,768 (8 rows per block at the bench batch): finer blocks even
-// out the end of the launch, +1.5 % rows/s same-box (profiles/ffm_r3/grid_sweep_*.log; the fp32
-// kernel is flat to slightly slower there, logloss unchanged for both).
+// The bf16 12-B-slot kernel takes 16,384 (16 rows per block at the bench batch).  Round 3 measured
+// 32,768 best (+1.5 %, profiles/ffm_r3/grid_sweep_*.log); with the linear records in the feature
+// blocks 8-16 K lead: 129.5-129.8 M rows/s vs 127.6 M at 32 K (profiles/r5/bench_grid_sweep_linrec.log;
+// the fp32 kernel is flat from 2 K to 16 K, logloss unchanged for both).
 int default_blocks(int B, int grid, int cap = 256 * 8 * 4) {
     return grid > 0 ? grid : (B < cap ? B : cap);
 }
@@ -1692,7 +1693,7 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     // tables of 4 GiB and more (-feature_hashing >= 23 at 512-B blocks): 64-bit slot offsets
     const bool wide = (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
     const int need = (P.F * P.F + 255) / 256;
-    const int blocks = default_blocks(P.B, grid, 256 * 8 * 16);
+    const int blocks = default_blocks(P.B, grid, 256 * 8 * 8);
     if (blocks <= 0) return 0;
 #define HM_P12(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
