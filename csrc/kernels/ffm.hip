@@ -1393,8 +1393,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
-    // lpack with the records inside the blocks (the first 16-B chunk after the 12-B slots)
-    const bool lin_in_tail = P.lpack && reinterpret_cast<const char*>(w) == vb + (size_t)P.vpad * 12;
+    // linear records inside the blocks (the first 16-B chunk after the 12-B slots), whether they
+    // are accessed as one 16-B record (lpack) or as three 4-B words: the tail zeroing skips them
+    const bool lin_in_tail = reinterpret_cast<const char*>(w) == vb + (size_t)P.vpad * 12;
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 
     int ab[NS];
@@ -1830,7 +1831,10 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
-//                     slot_g, gstride, vpad, tail16, gfstride, lin_defer
+//                     slot_g, gstride, vpad, tail16, gfstride, lin_defer, bias_every, lstride, lpack
+// lstride = floats between consecutive features' w / wz / wn (1: separate arrays; the records of
+//           ops/ffm.py lin_record_views: the feature block's size); lpack = 1: {w, z, n} are one
+//           16-B record (wz = w + 1, wn = w + 2), DMA'd and stored as one 16-B access
 // slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f * gfstride];
 //             bf16 V in 12-B slots {V | G} (G = V + 8 B, gfstride 3): ffm_pipe_sg12_kernel; fp32 V
 //             in the block layout (G = V + vpad * 16 B, vpad > 0): ffm_pipe_sg32_kernel (K <= 4,

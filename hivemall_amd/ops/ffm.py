@@ -132,7 +132,8 @@ def _lin_addressing(state: dict) -> tuple[int, int]:
     ls = w.stride(0) if w.dim() == 1 else 1
     pack = int(w.is_cuda and ls > 1 and wz.stride(0) == ls and wn.stride(0) == ls
                and wz.data_ptr() == w.data_ptr() + 4 and wn.data_ptr() == w.data_ptr() + 8
-               and w.data_ptr() % 16 == 0 and ls % 4 == 0)
+               and w.data_ptr() % 16 == 0 and ls % 4 == 0
+               and os.environ.get("HM_FFM_LPACK", "1") != "0")   # 0: 4-B accesses (A/B only)
     if not pack:
         assert ls == 1 or w.is_cuda, "CPU FFM state: contiguous linear tables"
     return ls, pack
