@@ -165,7 +165,7 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
 
     ``state``: "bf16" or "fp32" V|G storage.  Returns the timing / quality record."""
     from hivemall_amd.models.ffm import FFMTrainer
-    from hivemall_amd.ops.ffm import ffm_step
+    from hivemall_amd.ops.ffm import ffm_step, linear_mix_tensors
     from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
 
     dev = ctx.device
@@ -196,7 +196,8 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     mixer = ModelMixer(ctx)
     # mixed: V (weights) and the FTRL (z, n) the linear weight w is computed from, w, w0;
     # AdaGrad's G stays local (parallel/mix.py)
-    mix_tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+    # (the linear {w, z, n} records in the feature blocks mix as one [NF, 4] row view)
+    mix_tensors = [st["V"], *linear_mix_tensors(st), st["bias"]]
     if args.mix_state:
         mix_tensors.append(st["G"])
     overlap = OverlappedMixer(mixer, args.mix_mode, args.mix_power) if args.mix_overlap else None

@@ -31,7 +31,8 @@ import pandas as pd
 import torch
 
 from ..ops import ffm as _ffm_ops
-from ..ops.ffm import FFMHyper, ffm_step, is_packed, lin_record_views, new_state_tables
+from ..ops.ffm import (FFMHyper, ffm_step, is_packed, lin_record_views, linear_mix_tensors,
+                       new_state_tables)
 
 # GPU block layouts: w / wz / wn as the 16-B record after each feature's slots (ops/ffm.py
 # lin_record_views); HM_FFM_LIN_SEPARATE=1 keeps three separate arrays (A/B only)
@@ -323,8 +324,8 @@ class FFMTrainer(Learner):
         mark_touched(self.touched, b.idx, self.num_features)
 
     def mix(self) -> None:
-        self.mix_tensors([self.state["V"], self.state["wz"], self.state["wn"], self.state["w"],
-                          self.state["bias"]], [self.touched])
+        self.mix_tensors([self.state["V"], *linear_mix_tensors(self.state), self.state["bias"]],
+                         [self.touched])
 
     def fit(self, features=None, labels=None, batch: FFMBatch | None = None) -> "FFMTrainer":
         b = batch if batch is not None else self.prepare(features, labels)

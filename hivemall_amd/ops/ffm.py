@@ -139,6 +139,18 @@ def _lin_addressing(state: dict) -> tuple[int, int]:
     return ls, pack
 
 
+def linear_mix_tensors(state: dict) -> list:
+    """The FTRL linear state as the replica mixer should see it: with the 16-B records of
+    :func:`lin_record_views` one [NF, 4] row view {w, z, n, pad} (a uniform row view, so the fused
+    mix kernels of parallel/mix.py take it in one pass; the pad stays 0 on every rank), otherwise
+    the three arrays [wz, wn, w]."""
+    w = state["w"]
+    ls, pack = _lin_addressing(state)
+    if pack:
+        return [torch.as_strided(w, (w.shape[0], 4), (ls, 1))]
+    return [state["wz"], state["wn"], w]
+
+
 def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
                      packed: bool, slot_g: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """Zeroed (V, G).

@@ -24,6 +24,7 @@ def test_shard_mean_collectives_through_rccl_one_rank():
     import torch.distributed as dist
 
     from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.ops.ffm import linear_mix_tensors
     from hivemall_amd.parallel.dist import DistContext
     from hivemall_amd.parallel.mix import ModelMixer, OverlappedMixer
 
@@ -41,8 +42,11 @@ def test_shard_mean_collectives_through_rccl_one_rank():
         st["V"].copy_(torch.randn(st["V"].shape, generator=g, device=dev).to(torch.bfloat16))
         for k in ("wz", "wn", "w"):
             st[k].copy_(torch.randn(st[k].shape, generator=g, device=dev))
-        tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+        tensors = [st["V"], *linear_mix_tensors(st), st["bias"]]
+        if "wz" in st and st["w"].stride(0) > 1:             # the {w, z, n} records: one row view
+            assert len(tensors) == 3 and tensors[1].shape == (1 << 14, 4)
         ref = [t.clone() for t in tensors]
+        ref_w = st["w"].clone()
         m = ModelMixer(ctx, min_world=1)
         m.average(tensors)                                   # all_to_all + shard mean + all_gather
         torch.cuda.synchronize()
@@ -55,7 +59,7 @@ def test_shard_mean_collectives_through_rccl_one_rank():
         ov.start(tensors)                                    # finishes mix 1 (fused merge + repack)
         ov.finish()
         torch.cuda.synchronize()
-        assert torch.equal(st["w"], ref[3] + 1.0)
+        assert torch.equal(st["w"], ref_w + 1.0)
         assert torch.equal(st["V"], (ref[0].float() + 1.0).to(torch.bfloat16))
         x = torch.arange(10, dtype=torch.float32, device=dev)
         m.all_reduce_sum([x])
@@ -75,6 +79,7 @@ def test_fused_delta_mixing_bit_identical_to_torch_path():
     import torch.distributed as dist
 
     from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.ops.ffm import linear_mix_tensors
     from hivemall_amd.parallel import mix as M
     from hivemall_amd.parallel.dist import DistContext
 
@@ -95,7 +100,8 @@ def test_fused_delta_mixing_bit_identical_to_torch_path():
             g = torch.Generator(device="cuda").manual_seed(1)
             for k in ("wz", "wn", "w"):
                 st[k].copy_(torch.randn(st[k].shape, generator=g, device=dev))
-            tensors = [st["V"], st["wz"], st["wn"], st["w"], st["bias"]]
+            tensors = [st["V"], *linear_mix_tensors(st), st["bias"]]
+            assert all(M._view3(t) is not None for t in tensors[:2])   # both on the fused path
             m = M.ModelMixer(ctx, min_world=1)
             for step in range(3):                      # seed the consensus, then two delta mixes
                 for t in tensors:
