@@ -1049,16 +1049,19 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // block -> 2 blocks/CU).
 // s_waitcnt immediate: vmcnt(n) (n <= 63), expcnt / lgkmcnt not waited on
 #define VMCNT_ENC(n) ((((n) & 15) | (((n) >> 4) << 14)) | 0x0F70)
-template <int NS, typename OT, int TPB = 256, int ATOM = 0>
+// KV = 16-B quads per slot: 1 for k <= 4 (the 896-B blocks above), 2 for k <= 8 (32-B V slots,
+// 1,536-B blocks; the landing zone and the image double, 107 KB of LDS at 39 fields: one block
+// per CU, launched with 512 threads so that each SIMD still holds two waves).
+template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
     float* __restrict__ Gt, float* __restrict__ w, float* __restrict__ wz, float* __restrict__ wn,
     float* __restrict__ bias, float* __restrict__ pred_out, float* __restrict__ loss_out)
 {
-    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB];    // V DMA landing zone
+    __shared__ __attribute__((aligned(16))) float4 s_rv[NS * TPB * KV]; // V DMA landing zone [q][j][tid]
     __shared__ __attribute__((aligned(16))) float s_rg[NS * TPB];     // G DMA landing zone
-    __shared__ __attribute__((aligned(16))) float4 s_t[NS * TPB];     // transposed V image
+    __shared__ __attribute__((aligned(16))) float4 s_t[NS * TPB * KV];  // transposed V image [slot][q]
     __shared__ __attribute__((aligned(16))) int4 s_m[2][48];          // validated meta {i, f, x}
     __shared__ __attribute__((aligned(16))) int s_mr[2][3][48];       // raw meta DMA {idx, fld, val}
     __shared__ __attribute__((aligned(16))) float s_lin[2][3][48];    // DMA of w, z, n [mi]
@@ -1071,7 +1074,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     constexpr int W_META = 1, W_LIN = 2, W_DMA = 3;
-    const OT vfs = (OT)P.fstride * 16u;                  // V bytes between features
+    const OT vfs = (OT)P.fstride * (16u * KV);           // V bytes between features
     const OT gfs = (OT)P.gstride * 4u;                   // G bytes between features
     // (One table replica per XCD, averaged between launches, was measured and removed: +3.1e-3 ..
     // +5.4e-3 vs sequential on the bench stream instead of +2.4e-3; profiles/r5/ffm_xrep_probe.jsonl.)
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         const bool ok = (ma.x | mb.x) >= 0 && tid + j * TPB < FF;
         const bool live = ok && SA(j) != SB(j);
         const OT i = ok ? (OT)(uint32_t)ma.x : (OT)0, f = ok ? (OT)(uint32_t)mb.y : (OT)0;
-        ov = i * vfs + f * 16u;
+        ov = i * vfs + f * (16u * KV);
         og = i * gfs + f * 4u;
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
@@ -1130,7 +1133,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             OT ov, og;
             float xab;
             slot(bf, j, ov, og, xab);
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov), (lds_ptr_t)(s_rv + j * TPB + wave * 64), 16, 0, 0);
+#pragma unroll
+            for (int q = 0; q < KV; ++q)
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov + 16u * q),
+                                                 (lds_ptr_t)(s_rv + (q * NS + j) * TPB + wave * 64), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
         }
     };
@@ -1172,7 +1178,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     // (feature, field), hence the same slot index and thread when the rows share a feature at one
     // position — would be read one update stale.  The updating thread keeps the new V / G and
     // their offset, and phase B of the next row takes them instead of the landing zone.
-    float4 fv[NS];
+    float4 fv[NS][KV];
     float fg[NS];
     OT fo[NS];
     uint32_t fwd = 0u;
@@ -1207,13 +1213,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             cg[j] = s_rg[j * TPB + tid];
-            float4 v = s_rv[j * TPB + tid];
+            float4 v[KV];
+#pragma unroll
+            for (int q = 0; q < KV; ++q) v[q] = s_rv[(q * NS + j) * TPB + tid];
             if (fwd >> j & 1u) {
                 OT ov, og;
                 float xq;
-                if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) { v = fv[j]; cg[j] = fg[j]; }
+                if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) {
+#pragma unroll
+                    for (int q = 0; q < KV; ++q) v[q] = fv[j][q];
+                    cg[j] = fg[j];
+                }
             }
-            if (tid + j * TPB < FF) s_t[SB(j) * F + SA(j)] = v;
+            if (tid + j * TPB < FF) {
+#pragma unroll
+                for (int q = 0; q < KV; ++q) s_t[(SB(j) * F + SA(j)) * KV + q] = v[q];
+            }
         }
         fwd = 0u;
         if (more) publish_meta(nxt);
@@ -1250,9 +1265,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             wr |= (uint32_t)(k != 0u) << j;
             if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
             const int s = tid + j * TPB;
-            const float4 pv = s_t[s < FF ? s : 0];
-            const float4 cv = s_t[SB(j) * F + SA(j)];
-            part += (cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w) * xab[j];
+            float dot = 0.f;
+#pragma unroll
+            for (int q = 0; q < KV; ++q) {
+                const float4 pv = s_t[(s < FF ? s : 0) * KV + q];
+                const float4 cv = s_t[(SB(j) * F + SA(j)) * KV + q];
+                dot += cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w;
+            }
+            part += dot * xab[j];
         }
         part *= 0.5f * scale * scale;
         part += lw * mx * scale;
@@ -1286,20 +1306,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 float xj;
                 slot(cur, j, ov, og, xj);
                 const int s = tid + j * TPB;
-                const float4 pv = s_t[s];
-                const float4 cv = s_t[SB(j) * F + SA(j)];
                 const float c = ks * xab[j];
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
                 const f2 cc = {c, c}, ll = {lj, lj};
-                f2 o0 = f2{cv.x, cv.y}, o1 = f2{cv.z, cv.w};
-                const f2 p0 = f2{pv.x, pv.y}, p1 = f2{pv.z, pv.w};
-                const f2 d0 = cc * p0 + ll * o0, d1 = cc * p1 + ll * o1;
-                const float gs = (((cg[j] + d0.x * d0.x) + d0.y * d0.y) + d1.x * d1.x) + d1.y * d1.y;
+                f2 o0[KV], o1[KV], d0[KV], d1[KV];
+                float gs = cg[j];
+#pragma unroll
+                for (int q = 0; q < KV; ++q) {
+                    const float4 pv = s_t[s * KV + q];
+                    const float4 cv = s_t[(SB(j) * F + SA(j)) * KV + q];
+                    o0[q] = f2{cv.x, cv.y};
+                    o1[q] = f2{cv.z, cv.w};
+                    const f2 p0 = f2{pv.x, pv.y}, p1 = f2{pv.z, pv.w};
+                    d0[q] = cc * p0 + ll * o0[q];
+                    d1[q] = cc * p1 + ll * o1[q];
+                    gs = (((gs + d0[q].x * d0[q].x) + d0[q].y * d0[q].y) + d1[q].x * d1[q].x) + d1[q].y * d1[q].y;
+                }
                 const float r = __builtin_amdgcn_rsqf(gs + P.eps) * -P.eta0;
                 const f2 rr = {r, r};
-                o0 = o0 + rr * d0;
-                o1 = o1 + rr * d1;
-                fv[j] = make_float4(o0.x, o0.y, o1.x, o1.y);
+#pragma unroll
+                for (int q = 0; q < KV; ++q) {
+                    const f2 n0 = o0[q] + rr * d0[q], n1 = o1[q] + rr * d1[q];
+                    fv[j][q] = make_float4(n0.x, n0.y, n1.x, n1.y);
+                }
                 fg[j] = gs;
                 fo[j] = ov;
                 fwd |= 1u << j;
@@ -1307,16 +1336,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                     // concurrent rows' updates of one slot all land (no read-modify-write race)
                     if (live >> j & 1u) {
                         float* vp = reinterpret_cast<float*>(vb + ov);
-                        const f2 e0 = rr * d0, e1 = rr * d1;
-                        atomicAdd(vp + 0, e0.x);
-                        atomicAdd(vp + 1, e0.y);
-                        atomicAdd(vp + 2, e1.x);
-                        atomicAdd(vp + 3, e1.y);
+#pragma unroll
+                        for (int q = 0; q < KV; ++q) {
+                            const f2 e0 = rr * d0[q], e1 = rr * d1[q];
+                            atomicAdd(vp + 4 * q + 0, e0.x);
+                            atomicAdd(vp + 4 * q + 1, e0.y);
+                            atomicAdd(vp + 4 * q + 2, e1.x);
+                            atomicAdd(vp + 4 * q + 3, e1.y);
+                        }
                         atomicAdd(reinterpret_cast<float*>(gb + og), gs - cg[j]);
                     }
                     continue;
                 }
-                *reinterpret_cast<float4*>(vb + ov) = fv[j];
+#pragma unroll
+                for (int q = 0; q < KV; ++q) *reinterpret_cast<float4*>(vb + ov + 16u * q) = fv[j][q];
                 *reinterpret_cast<float*>(gb + og) = fg[j];
             }
             // (The pad slots and block tails are never read.  Zeroing them so that every line a
@@ -1709,16 +1742,36 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
-// Per-slot-G fp32 pipelined dispatch (Kp == 4, F <= 45, block layout, tables < 4 GiB): the
+// Per-slot-G fp32 pipelined dispatch (Kp == 4 or 8, F <= 45, block layout, tables < 4 GiB): the
 // LDS-DMA ffm_pipe_sg32_kernel; -1 otherwise (bf16 V in this layout: the generic kernel; the
 // bf16 default is the 12-B slot layout of dispatch_sg12).
 int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* V, float* G, float* w, float* wz, float* wn, float* bias,
                   float* pred, float* loss, int grid, int variant, hipStream_t stream) {
-    if (P.Kp != 4 || P.F > 45 || P.vpad <= 0) return -1;
+    if ((P.Kp != 4 && P.Kp != 8) || P.F > 45 || P.vpad <= 0) return -1;
     // tables of 4 GiB and more (-feature_hashing >= 23 at 896-B blocks): 64-bit slot offsets
-    const bool wide = (size_t)P.num_features * (size_t)P.fstride * 16 >= ((size_t)1 << 32) ||
+    const bool wide = (size_t)P.num_features * (size_t)P.fstride * (size_t)(P.Kp * 4) >= ((size_t)1 << 32) ||
                       (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
+    if (P.Kp == 8) {
+        // 32-B slots: 512-thread blocks, one per CU (107 KB of LDS at 39 fields)
+        if (variant == 8) return -1;
+        const int need = (P.F * P.F + 511) / 512;
+        const int blocks = default_blocks(P.B, grid);
+        if (blocks <= 0) return 0;
+#define HM_P32K8(NSV) do { \
+        if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, 512, 0, 2>), dim3(blocks), dim3(512), 0, stream, \
+                                     P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 1, 2>), dim3(blocks), \
+                                                  dim3(512), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                  bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 0, 2>), dim3(blocks), dim3(512), 0, stream, \
+                                P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
+        if (need <= 2) { HM_P32K8(2); }
+        else if (need <= 3) { HM_P32K8(3); }
+        else { HM_P32K8(4); }
+#undef HM_P32K8
+        HM_LAUNCH_RET();
+    }
     const int need = (P.F * P.F + 255) / 256;
     const int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;

@@ -221,8 +221,9 @@ def test_train_ffm_udtf_strings():
                                              ("packed", False, 8)])
 def test_ffm_gpu_matches_cpu_engine(layout, reload, k, adagrad):
     """HIP kernels vs the sequential C++ engine: identical on rows with disjoint features (no
-    Hogwild interaction).  Per-slot AdaGrad (default): the pipelined sg12 / sg32 kernels on the
-    feature-block layout (k = 4), the generic kernel for k = 8 and for split tables; per-element
+    Hogwild interaction).  Per-slot AdaGrad (default): the pipelined sg32 kernel on the
+    feature-block layout (k = 4: 16-B slots; k = 8: 32-B slots, 512-thread blocks), the generic
+    kernel for split tables; per-element
     (-elementwise_adagrad): the packed-slot and split-table kernels, with and without reload."""
     torch.manual_seed(0)
     B, F, NFLD = 512, 39, 39
@@ -275,8 +276,8 @@ def test_ffm_gpu_bf16_state_close_to_fp32_engine(layout, adagrad):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("adagrad", ["", "-elementwise_adagrad", "-w0"])
-def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
+@pytest.mark.parametrize("adagrad,k", [("", 4), ("-elementwise_adagrad", 4), ("-w0", 4), ("", 8)])
+def test_ffm_gpu_single_block_is_exactly_sequential(adagrad, k):
     """grid=1: one workgroup walks the rows in order = Hivemall's per-row semantics.  The generic
     kernel (variant 1) has no lookahead; the pipelined default DMAs row r+1's slots before row
     r's updates land, and forwards its own updates into the slots both rows hold (ffm.hip
@@ -302,7 +303,7 @@ def test_ffm_gpu_single_block_is_exactly_sequential(adagrad):
     try:
         for dev, v in (("cpu", 0), ("cuda", 1), ("cuda", 0)):
             ffm_op._VARIANT = v
-            t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 16 -seed 1 "
+            t = FFMTrainer(f"-classification -factors {k} -num_fields 39 -feature_hashing 16 -seed 1 "
                            + adagrad, device=dev)
             t.grid = 1
             t.fit(batch=FFMBatch(idx, None, None, y).to(dev))
@@ -424,8 +425,8 @@ def _assert_state_close(tc, tg, tol, rows=None):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lpack", ["1", "0"])
-@pytest.mark.parametrize("extra,tol", [("", 1e-4), (" -bf16_state", 2e-2)])
-def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol, lpack, monkeypatch):
+@pytest.mark.parametrize("extra,tol,k", [("", 1e-4, 4), (" -bf16_state", 2e-2, 4), ("", 1e-4, 8)])
+def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol, k, lpack, monkeypatch):
     """field:index:value rows as the SQL / UDTF path hands them to the kernel: an explicit
     field id per feature (every row a random permutation of the 39 fields) and random values,
     through the pipelined sg32 (fp32) and sg12 (bf16) kernels vs the sequential C++ engine on
@@ -439,8 +440,8 @@ def test_ffm_gpu_explicit_fields_and_values_match_cpu_engine(extra, tol, lpack, 
     fld = torch.stack([torch.randperm(F, generator=g) for _ in range(B)]).to(torch.int32)
     val = torch.rand(B, F, generator=g) * 3.0 + 0.1
     y = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0)
-    tc = _trainer("cpu", B * F, F)
-    tg = _trainer("cuda", B * F, F, extra=extra)
+    tc = _trainer("cpu", B * F, F, k=k)
+    tg = _trainer("cuda", B * F, F, k=k, extra=extra)
     _copy_state(tc, tg)
     lc, lg = torch.empty(B), torch.empty(B, device="cuda")
     ffm_step(tc.state, idx, fld, val, y, tc.hyper, loss=lc)
