@@ -410,8 +410,12 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
     //          256: 117.0 M, 0.4759                          512: 122.9 M, 0.4787
     // (single address, 64 blocks: 38.7 M, 0.4730).  256 keeps the logloss within 0.003 of the
     // single-address run at 3x the rows/s; more Hogwild concurrency costs more logloss than it
-    // buys.
-    int64_t blocks = grid > 0 ? grid : 256;
+    // buys.  Round 5: against Hivemall's 8-mapper average on two boxes (3 + 5 reps,
+    // profiles/r5/fm_grid_parity_yy.jsonl, fm_grid_parity_ab.jsonl; rates fm_grid_rate_yy.log):
+    // 256 +2.9e-3 .. +4.1e-3 (218-234 M rows/s on config 2), 192 +2.4e-3 .. +3.6e-3 (199 M),
+    // 160 +2.2e-3 .. +2.9e-3 (180 M), 128 +1.9e-3 .. +2.6e-3 (164 M).  128 (512 rows in flight)
+    // is the largest grid that stays inside SURVEY's bf16 3e-3 tolerance on every box measured.
+    int64_t blocks = grid > 0 ? grid : 128;
     if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;

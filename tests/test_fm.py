@@ -139,9 +139,11 @@ def test_fm_gpu_logloss_parity_past_2p20_rows():
     2^20 rows, bf16 V (the config-2 engine), against Hivemall's 8-mapper average on the same rows.
     The gap is the Hogwild concurrency, not the bias schedule (re-reading every row: +2.87e-3 vs
     +2.89e-3, profiles/r5/fm_w0_probe.jsonl), and it moves with the grid (rows in flight = 4 x
-    grid; 3 reps each, profiles/r5/fm_grid_parity_probe.jsonl): 256 (the default, 234 M rows/s at
-    config 2) +3.3e-3 .. +4.1e-3, 128 (164 M rows/s) +1.7e-3 .. +2.2e-3, 64 (89 M) +0.6e-3 ..
-    +1.5e-3.  SURVEY.md's bf16 tolerance 3e-3 holds at -grid 128; the default is bounded at 5e-3."""
+    grid; profiles/r5/fm_grid_parity_probe.jsonl, fm_grid_parity_yy.jsonl, fm_grid_parity_ab.jsonl):
+    256 (218-234 M rows/s at config 2) +2.9e-3 .. +4.1e-3, 192 (199 M) +2.4e-3 .. +3.6e-3, 160
+    (180 M) +2.2e-3 .. +2.9e-3, 128 (the default since round 5, 164 M rows/s) +1.7e-3 .. +2.6e-3,
+    64 (89 M) +0.6e-3 .. +1.5e-3.  SURVEY.md's bf16 tolerance 3e-3 bounds the default grid; -grid 256
+    (the round-4 default) is reported, bounded at 5e-3."""
     from hivemall_amd.ops import fm as fm_ops
 
     assert fm_ops.W0_EVERY == 8 and fm_ops.W0_EVERY_MAX < 32
@@ -154,12 +156,12 @@ def test_fm_gpu_logloss_parity_past_2p20_rows():
         t.predict_raw(rows=_rows(eidx).to(dev)).cpu(), yy).item()
     rows = _rows(idx, y).to("cuda")
     gpu = FMTrainer(opts, device="cuda").fit(rows=rows)
-    gpu128 = FMTrainer(opts + " -grid 128", device="cuda").fit(rows=rows)
+    gpu256 = FMTrainer(opts + " -grid 256", device="cuda").fit(rows=rows)
     ref = mapper_average_fm(opts, idx, y, 8, 1 << 20)
-    res = {"mappers8": ll(ref, "cpu"), "gpu": ll(gpu, "cuda"), "gpu_grid128": ll(gpu128, "cuda")}
+    res = {"mappers8": ll(ref, "cpu"), "gpu": ll(gpu, "cuda"), "gpu_grid256": ll(gpu256, "cuda")}
     print(res)
-    assert res["gpu"] <= res["mappers8"] + 5e-3, res
-    assert res["gpu_grid128"] <= res["mappers8"] + 3e-3, res
+    assert res["gpu"] <= res["mappers8"] + 3e-3, res
+    assert res["gpu_grid256"] <= res["mappers8"] + 5e-3, res
 
 
 def _dense_rows(X, y=None, device="cpu"):
