@@ -127,9 +127,12 @@ def test_fm_gpu_logloss_parity(fp32):
     ref = mapper_average_fm(opts, idx, y, 8, 262144)
     res = {"sequential": ll(seq, "cpu"), "mappers8": ll(ref, "cpu"), "gpu": ll(gpu, "cuda")}
     print(res)
-    # measured (profiles/fm_sweep_r1.log): default 256-wave Hogwild lands ~0.01 above the
-    # 8-mapper average; plain SGD (no AdaGrad) is the most staleness-sensitive learner
-    assert res["gpu"] <= res["mappers8"] + 0.015, res
+    # measured (profiles/fm_sweep_r1.log): the 256-block Hogwild grid landed ~0.01 above the
+    # 8-mapper average on these 200 K early-training rows; the 128-block default +7.9e-3 /
+    # +9.8e-3 (fp32 / bf16, profiles/r5/pytest_fm_zz.log).  Plain SGD (no AdaGrad) is the most
+    # staleness-sensitive learner, and early training the most sensitive regime (the steady
+    # state past 2^20 rows is bounded at SURVEY's 3e-3 below)
+    assert res["gpu"] <= res["mappers8"] + 0.012, res
 
 
 @pytest.mark.gpu
