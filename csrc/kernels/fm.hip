@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
 template <int KP, bool BF16>
 int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const float* val,
            const float* y, int64_t n, int64_t t0, float* w, void* V, float* w0, float* pred,
-           float* loss, int grid, int variant, hipStream_t st) {
+           float* loss, int grid, int variant, int wpb, hipStream_t st) {
     // Default: 256 blocks x 4 waves.  With the global bias behind ONE atomic address every
     // grid topped out near 40 M rows/s (64 blocks was best; profiles/fm_sweep_r1.log); with 64
     // line-padded shards (profiles/fm_grid_probe_r1.log, 2M rows, 2^24 features, k=8 bf16):
@@ -419,11 +419,14 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
     if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;
+    // `grid` counts 4-wave workgroups (the Hogwild rows in flight / 4); the waves are launched
+    // wpb to a workgroup (1, 2 or 4), so the same rows in flight spread over more CUs
+    const int64_t lb = blocks * 4 / wpb;
     if (variant == 1)
-        hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
+        hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)lb), dim3(64 * wpb), 0, st, P, indptr, idx,
                            val, y, n, t0, w, V, w0, pred, loss);
     else
-        hipLaunchKernelGGL((fm_pipe_kernel<KP, BF16>), dim3((int)blocks), dim3(256), 0, st, P, indptr, idx,
+        hipLaunchKernelGGL((fm_pipe_kernel<KP, BF16>), dim3((int)lb), dim3(64 * wpb), 0, st, P, indptr, idx,
                            val, y, n, t0, w, V, w0, pred, loss);
     HM_LAUNCH_RET();
 }
@@ -431,7 +434,7 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
 }  // namespace
 
 // ip: dims, k, KP, classification, train, eta_kind, use_w0, bf16, grid, seed, w0_shards, variant,
-//     w0_every, vstride, wstride
+//     w0_every, vstride, wstride, wpb (waves per launched workgroup: 1, 2 or 4 = default)
 //     (variant 0 = fm_pipe_kernel, 1 = fm_kernel; vstride = V elements per feature row (0: KP),
 //     wstride = floats between consecutive w (0: 1); models/fm.py keeps w in the padding of each
 //     feature's V row on the GPU)
@@ -452,6 +455,7 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     P.eta0 = hp[0]; P.power_t = hp[1]; P.total_steps = hp[2]; P.lambda0 = hp[3];
     P.lambda_w = hp[4]; P.lambda_v = hp[5]; P.min_target = hp[6]; P.max_target = hp[7];
     P.w0_tol = hp[8];
+    const int wpb = ip[15] == 1 || ip[15] == 2 ? ip[15] : 4;
     P.vstride = ip[13] > 0 ? ip[13] : KP;
     P.wstride = ip[14] > 0 ? ip[14] : 1;
     {
@@ -463,8 +467,8 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     if (n_rows <= 0) return 0;
 #define HM_FM_CASE(K)                                                                            \
     case K:                                                                                      \
-        return bf16 ? launch<K, true>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, stream) \
-                    : launch<K, false>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, stream);
+        return bf16 ? launch<K, true>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, wpb, stream) \
+                    : launch<K, false>(P, indptr, idx, val, y, n_rows, t0, w, V, w0, pred, loss, grid, variant, wpb, stream);
     switch (KP) {
         HM_FM_CASE(4)
         HM_FM_CASE(8)

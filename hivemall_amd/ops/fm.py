@@ -59,6 +59,12 @@ W0_TOL = float(os.environ.get("HM_FM_W0_TOL", "0"))
 # vs +2.9e-3 .. +3.7e-3.  One line per feature instead of two stays longer in each XCD's L2, and
 # the non-coherent L2s then serve older copies to the other XCDs (docs/perf_notes.md).
 W_RECORD = os.environ.get("HM_FM_W_RECORD", "0") == "1"
+# waves per launched workgroup (csrc/kernels/fm.hip launch): the grid's 4-wave workgroups
+# (rows in flight / 4) are launched as 4 / WPB workgroups of WPB waves, so the 512 rows in flight
+# of the default grid spread over all 256 CUs instead of 128.  Config 2, same box, 2 reps
+# (profiles/r5/fm_wpb_ab.log): 1 wave 165.7-166.4 M rows/s, 2 waves 166.2-166.6 M, 4 waves
+# 162.0-163.0 M; parity vs the 8-mapper average unchanged (+1.8e-3 .. +2.1e-3 vs +1.5e-3 .. +1.9e-3)
+WPB = int(os.environ.get("HM_FM_WPB", "2"))
 
 
 def new_state_tables(dims: int, KP: int, dtype: torch.dtype, device) -> tuple:
@@ -104,7 +110,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
                    int(os.environ.get("HM_FM_VARIANT", "0")),
                    max(1, min(W0_EVERY_MAX, int(os.environ.get(
                        "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1))))),
-                   V.stride(0), w.stride(0)],
+                   V.stride(0), w.stride(0), WPB],
                   dtype=np.int32)
     assert V.stride(1) == 1 and V.stride(0) >= KP, "V rows must be contiguous"
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
