@@ -21,7 +21,7 @@ B, NRES = 262144, 4
 idx, fld, val, y = criteo_ffm(B * NRES, 20, seed=3, device=dev)
 yr = torch.where(y > 0, 1.0, 0.0)      # regression targets
 base = "-factors 4 -num_fields 39 -feature_hashing 20"
-cases = ["-c", "-c -w0", "-c -disable_wi", "-c -no_norm", "", "-c -elementwise_adagrad", "-c -bf16_state",
+cases = sys.argv[1:] or ["-c", "-c -w0", "-c -disable_wi", "-c -no_norm", "", "-c -elementwise_adagrad", "-c -bf16_state",
          "-c -bf16_state -w0", "-c -factors 8", "-c -w0 -disable_wi"]
 for extra in cases:
     opts = base + " " + extra

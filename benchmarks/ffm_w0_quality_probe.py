@@ -2,7 +2,7 @@
 criteo_ffm rows (2 passes), for the sharded bias state re-read every HM_FFM_BIAS_EVERY rows and the
 single-address state (HM_FFM_BIAS_SHARDS=0).
 
-    python benchmarks/ffm_w0_quality_probe.py
+    python benchmarks/ffm_w0_quality_probe.py [every ...]     # 64 shards at each re-read interval
 """
 import json
 import os
@@ -33,7 +33,8 @@ def run(dev):
 
 seq, dt, b = run("cpu")
 print(json.dumps({"engine": "cpu sequential", "logloss": round(seq, 5), "w0": round(b, 4), "s": round(dt, 1)}), flush=True)
-for shards, every in ((64, 8), (64, 16), (64, 1), (0, 1)):
+cases = [(64, int(a)) for a in sys.argv[1:]] or [(64, 8), (64, 16), (64, 1), (0, 1)]
+for shards, every in cases:
     ffm_ops.BIAS_SHARDS, ffm_ops.BIAS_EVERY = shards, every
     ll, dt, b = run("cuda")
     print(json.dumps({"bias_shards": shards, "bias_every": every, "logloss": round(ll, 5), "gap": round(ll - seq, 5),

@@ -1202,7 +1202,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         bar_raw();
         // the bias shards for the NEXT row (one row of extra staleness on one parameter, as
         // train_fm's w0): issued here, landed by the next phase A's vmcnt(0), used in its D
-        const bool bre = bsh && (bit % P.bias_every) == 0;      // this row re-reads (block-uniform)
+        // this row re-reads (block-uniform); not the block's first row: the shards were just read
+        const bool bre = bsh && bit > 0 && (bit % P.bias_every) == 0;
         float nbz = bz, nbn = bn;
         if (bre && wave == W_META && lane < P.bias_s) {
             nbz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1526,7 +1527,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         bar_raw();
         // the bias shards for the NEXT row (one row of extra staleness on one parameter, as
         // train_fm's w0): issued here, landed by the next phase A's vmcnt(0), used in its D
-        const bool bre = bsh && (bit % P.bias_every) == 0;      // this row re-reads (block-uniform)
+        // this row re-reads (block-uniform); not the block's first row: the shards were just read
+        const bool bre = bsh && bit > 0 && (bit % P.bias_every) == 0;
         float nbz = bz, nbn = bn;
         if (bre && wave == W_META && lane < P.bias_s) {
             nbz = __hip_atomic_load(P.bias_sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

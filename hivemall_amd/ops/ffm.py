@@ -193,7 +193,10 @@ _DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows 
 # ffm.hip FFMParams.bias_sh): one same-address pair of atomics per row held -w0 runs at 5.5 M
 # rows/s (profiles/r5/ffm_w0_rate.jsonl).  HM_FFM_BIAS_SHARDS=0: the single address (A/B only).
 BIAS_SHARDS = int(os.environ.get("HM_FFM_BIAS_SHARDS", "64"))
-BIAS_EVERY = int(os.environ.get("HM_FFM_BIAS_EVERY", "16"))   # rows between a block's re-reads
+# rows between a block's re-reads of the shards: 16 -> 32 in round 5 (fp32 -w0 77.1 -> 80.2 M
+# rows/s, held-out gap vs sequential +1.9e-3 / +2.0e-3 / +1.8e-3 at 16 / 32 / 64, i.e. noise;
+# profiles/r5/ffm_w0_every_quality.jsonl, ffm_w0_every_rate_*.jsonl)
+BIAS_EVERY = int(os.environ.get("HM_FFM_BIAS_EVERY", "32"))
 _BIAS_SH: dict = {}
 
 
