@@ -192,7 +192,14 @@ def load(path: str, device=None, restore_rng: bool = False, **kw):
     kind = meta["state_kind"]
     st_t = {k[6:]: v.to(dev) for k, v in tensors.items() if k.startswith("state.")}
     if kind == "dict":
-        learner.state = st_t
+        # learners whose device state lives in a layout of views into one table (FFM's feature
+        # blocks, FM's V records) rebuild that layout and copy the saved values in: torch.save of
+        # each view on its own wrote plain contiguous tensors, which would otherwise send the
+        # resumed learner down the generic kernels
+        if hasattr(learner, "adopt_state"):
+            learner.adopt_state(st_t)
+        else:
+            learner.state = st_t
     elif kind == "dataclass":
         from ..ops.linear import LinearState
         learner.state = LinearState(st_t["S"], st_t["touched"], st_t["RS"], bool(meta["state_covar"]),

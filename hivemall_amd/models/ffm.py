@@ -248,6 +248,14 @@ class FFMTrainer(Learner):
         self.touched = torch.zeros(self.num_features, dtype=torch.bool, device=dev)
         return self.state
 
+    def adopt_state(self, st: dict) -> dict:
+        """Checkpoint load (io/checkpoint.py): the saved tensors copied into this device's layout
+        (per-slot feature blocks with the linear records on the GPU)."""
+        self.num_features, self.num_fields = int(st["V"].shape[0]), int(st["V"].shape[1])
+        self.state = {k: v.to(self.device) for k, v in st.items()}
+        self.pack_state()
+        return self.state
+
     # ------------------------------------------------------------------ data
     def prepare(self, features, labels=None) -> FFMBatch:
         """Rows of ``field:index[:value]`` strings -> device-resident padded-ELL batch.
@@ -426,15 +434,19 @@ class FFMTrainer(Learner):
         elif not slot_g and G.dim() == 2:
             G = (G / self.kp).unsqueeze(-1).expand(*G.shape, self.kp).to(V.dtype)
         packed = self.device.type == "cuda" and not self.cl["split_state"]
-        if slot_g and G is st["G"] and (not packed or _is_block(V, G)):
-            return
-        if not slot_g and G is st["G"] and (not packed or is_packed(V, G)):
-            return
-        NF, NFLD, kp = V.shape
-        V2, G2 = new_state_tables(NF, NFLD, kp, V.dtype, V.device, packed=packed, slot_g=slot_g)
-        V2.copy_(V)
-        G2.copy_(G)
-        st["V"], st["G"] = V2, G2
+        keep = G is st["G"] and (not packed or (_is_block(V, G) if slot_g else is_packed(V, G)))
+        if not keep:
+            NF, NFLD, kp = V.shape
+            V2, G2 = new_state_tables(NF, NFLD, kp, V.dtype, V.device, packed=packed, slot_g=slot_g)
+            V2.copy_(V)
+            G2.copy_(G)
+            st["V"], st["G"] = V2, G2
+        # the linear FTRL state into the feature blocks' 16-B records (init_state's layout)
+        lin = lin_record_views(st["V"], st["G"]) if LIN_IN_BLOCK and "w" in st else None
+        if lin is not None and lin[0].data_ptr() != st["w"].data_ptr():
+            for dst, key in zip(lin, ("w", "wz", "wn")):
+                dst.copy_(st[key])
+                st[key] = dst
 
 
 def _is_block(V: torch.Tensor, G: torch.Tensor) -> bool:

@@ -158,6 +158,18 @@ class FMTrainer(Learner):
         self.touched = torch.zeros(self.dims, dtype=torch.bool, device=dev)
         return self.state
 
+    def adopt_state(self, st: dict) -> dict:
+        """Checkpoint load (io/checkpoint.py): the saved tensors copied into this device's layout
+        (w inside the V records with HM_FM_W_RECORD=1)."""
+        self.init_state(int(st["V"].shape[0]))
+        for k, v in st.items():
+            cur = self.state.get(k)
+            if cur is not None and cur.shape == v.shape and cur.dtype == v.dtype:
+                cur.copy_(v)
+            else:
+                self.state[k] = v
+        return self.state
+
     # ------------------------------------------------------------------ data
     def prepare(self, features, labels=None, train: bool = True) -> SparseRows:
         """Feature rows -> device CSR.  With -feature_hashing on the GPU, string rows are parsed

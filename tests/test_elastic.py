@@ -45,6 +45,52 @@ def test_checkpoint_roundtrip_ffm_and_fm(tmp_path):
     np.testing.assert_array_equal(f.predict(rows[:20]), g.predict(rows[:20]))
 
 
+@pytest.mark.gpu
+def test_checkpoint_roundtrip_gpu_record_layouts(tmp_path):
+    """GPU state in the record layouts (FFM: {w, z, n} inside each fp32 feature block; FM with
+    HM_FM_W_RECORD: w inside each V row) saves and loads as the same views of one table, predicts
+    identically, and keeps training (the kernels take whatever strides the loaded tensors have)."""
+    from hivemall_amd.io.synthetic import criteo_ffm
+    from hivemall_amd.models.ffm import FFMBatch, FFMTrainer
+    from hivemall_amd.models.fm import FMTrainer
+    from hivemall_amd.models.linear import SparseRows
+    from hivemall_amd.ops import fm as fm_ops
+
+    idx, fld, val, y = criteo_ffm(20000, 14, seed=1)
+    b = FFMBatch(idx, fld, val, y).to("cuda")
+    ev = FFMBatch(idx[:2000], fld[:2000], val[:2000], None).to("cuda")
+    a = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 14 -seed 3", device="cuda")
+    a.fit(batch=b)
+    assert a.state["w"].stride(0) > 1                        # the records are in use
+    checkpoint.save(a, str(tmp_path / "ffm"))
+    c = checkpoint.load(str(tmp_path / "ffm"), device="cuda")
+    # back in the pipelined kernels' layout: feature blocks with the linear records inside
+    assert c.state["w"].stride(0) == a.state["w"].stride(0) and c.state["V"].stride() == a.state["V"].stride()
+    for k in ("V", "G", "w", "wz", "wn", "bias"):
+        assert torch.equal(a.state[k], c.state[k]), k
+    assert torch.equal(a.predict_raw(batch=ev), c.predict_raw(batch=ev))
+    c.fit(batch=b)                                          # trains on the loaded views
+    assert torch.isfinite(c.predict_raw(batch=ev)).all()
+
+    old = fm_ops.W_RECORD
+    fm_ops.W_RECORD = True
+    try:
+        cidx, cy = criteo_like(20000, 14, seed=2)
+        rows = SparseRows(torch.arange(0, 20000 * 39 + 1, 39, dtype=torch.int64), cidx.reshape(-1).contiguous(),
+                          None, cy).to("cuda")
+        f = FMTrainer("-c -factors 8 -num_features 16384 -seed 3", device="cuda").fit(rows=rows)
+        assert f.state["w"].stride(0) > 1
+        checkpoint.save(f, str(tmp_path / "fm"))
+        g = checkpoint.load(str(tmp_path / "fm"), device="cuda")
+        assert g.state["w"].stride(0) == f.state["w"].stride(0) > 1
+        assert torch.equal(f.state["w"], g.state["w"]) and torch.equal(f.state["V"], g.state["V"])
+        assert torch.equal(f.predict_raw(rows=rows), g.predict_raw(rows=rows))
+        g.fit(rows=rows)
+        assert torch.isfinite(g.predict_raw(rows=rows)).all()
+    finally:
+        fm_ops.W_RECORD = old
+
+
 def _run_job(ckpt, fault=None, world=2, steps=6):
     env = dict(os.environ, PYTHONPATH=ROOT, HM_CKPT=str(ckpt), HM_STEPS=str(steps),
                MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
