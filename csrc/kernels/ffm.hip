@@ -1892,8 +1892,9 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 //           16-B record (wz = w + 1, wn = w + 2), DMA'd and stored as one 16-B access
 // slot_g = 1: one fp32 AdaGrad accumulator per (feature, field) slot, G[i * gstride + f * gfstride];
 //             bf16 V in 12-B slots {V | G} (G = V + 8 B, gfstride 3): ffm_pipe_sg12_kernel; fp32 V
-//             in the block layout (G = V + vpad * 16 B, vpad > 0): ffm_pipe_sg32_kernel (K <= 4,
-//             F <= 45); anything else the generic kernel.  tail16 = zero 16-B chunks after each
+//             in the block layout (G = V + vpad * Kp * 4 B, vpad > 0): ffm_pipe_sg32_kernel (Kp 4:
+//             256-thread blocks; Kp 8: 32-B slots, 512-thread blocks; F <= 45); anything else the
+//             generic kernel.  tail16 = zero 16-B chunks after each
 //             feature's G region (line completion).
 // slot_g = 0 (per-element G shaped like V): packed = 1: V and G are the two halves of one
 //             [num_features][fstride][2][Kp] table (G == V + Kp elements, slot stride 2*Kp); 0:
