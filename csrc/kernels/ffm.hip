@@ -1913,7 +1913,9 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // (profiles/r4/ffm_paired_slots_ab.log); the sg32 kernel with the next row's G prefetched into
 // registers instead of an LDS landing zone (53 KB per block: 3 rows in flight per CU instead of
 // 2): 73.6-73.8 vs 73.9-74.2 M rows/s (profiles/r4/ffm_register_g_ab.log) — more rows in flight
-// per CU does not move this kernel.
+// per CU does not move this kernel.  Round 5 re-tried it after the linear records (53.4 KB of LDS
+// with the 4-B linear zone aliased onto the 16-B one, forced to 3 waves per SIMD): 168 VGPRs with
+// 21 spilled, 63.2 vs 89.6 M rows/s (profiles/r5/bench_rg_ab.log).
 // aux (host array of 2 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
 // or null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
 // updated slot by slot by the pipelined kernels: racing stores of one address, one wins).
