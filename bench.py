@@ -105,9 +105,14 @@ def parse_args(argv=None):
                     help="1: re-read the own slot right before its update (short Hogwild window); "
                          "0: keep the gathered slot in registers; -1: by layout (packed -> 0)")
     ap.add_argument("--device", default=None)
-    ap.add_argument("--gen-device", choices=("auto", "cpu"), default="auto",
-                    help="where the synthetic rows are drawn (cpu = the exact stream of "
-                         "benchmarks/ffm_parity_bench_scale.py, copied to the GPU before timing)")
+    ap.add_argument("--gen-device", choices=("auto", "cpu"), default="cpu",
+                    help="where the synthetic rows are drawn: cpu (default) = the exact stream "
+                         "benchmarks/ffm_seq_ref.py replays through the sequential engine, copied to "
+                         "the GPU before timing (the JSON then carries logloss_seq_ref / "
+                         "logloss_gap); auto = drawn on the training device (a different stream)")
+    ap.add_argument("--row-order", choices=("none", "spread", "xcd"), default="none",
+                    help="row order inside each resident batch (ops/ffm_sched.py, a host pass "
+                         "before timing; experiment: conflict-aware scheduling, docs/perf_notes.md)")
     ap.add_argument("--mix-probe", type=int, default=3,
                     help="synchronous mixes timed after the run (ms, wire bytes, bus GB/s)")
     return ap.parse_args(argv)
@@ -316,6 +321,19 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
     return out
 
 
+def seq_reference(args, world: int):
+    """Held-out logloss of the sequential engine on this run's exact row stream, if pinned
+    (resources/bench_seq_ref.json, written by benchmarks/ffm_seq_ref.py); else None."""
+    if args.gen_device != "cpu" or args.data != "criteo_ffm":
+        return None      # rows drawn on the device: a stream no reference was computed for
+    from benchmarks.ffm_seq_ref import load_refs, ref_key
+
+    key = ref_key(world, args.steps, args.warmup, args.batch, args.hash_bits, args.factors,
+                  max(1, args.resident_batches), args.eval_rows, order=args.row_order)
+    rec = load_refs().get(key)
+    return None if rec is None else round(float(rec["logloss_seq"]), 5)
+
+
 def main(argv=None):
     t_start = time.perf_counter()
     args = parse_args(argv)
@@ -347,6 +365,15 @@ def main(argv=None):
         return tuple(None if t is None else t.to(dev) for t in out)
 
     idx, fld, val, y = gen(B * nres, 1000 + rank)
+    if args.row_order != "none":
+        from hivemall_amd.ops.ffm_sched import schedule_rows
+
+        for b in range(nres):
+            sl = slice(b * B, (b + 1) * B)
+            p = schedule_rows(idx[sl].cpu(), args.row_order, nf=1 << args.hash_bits).to(dev)
+            for ten in (idx, fld, val, y):
+                if ten is not None:
+                    ten[sl] = ten[sl][p]
     data = {"eval": None}
     if rank == 0:
         data["eval"] = gen(args.eval_rows, 999_999, logit=True)
@@ -372,6 +399,7 @@ def main(argv=None):
                     **{f"rows_per_s_{alt_state}": alt_run["rows_per_s"] if alt_run else None})
     if rank == 0:
         ll, floor = main_run["ll"], main_run.get("floor")
+        seq_ref = seq_reference(args, world)
         out = {
             "metric": BASELINE_METRIC,
             "value": round(main_run["rows_per_s"], 1),
@@ -420,6 +448,11 @@ def main(argv=None):
             **main_run["probe"],
             "logloss_heldout": round(ll, 5) if ll is not None else None,
             "logloss_planted_floor": round(floor, 5) if floor is not None else None,
+            # the sequential C++ engine (Hivemall's per-row semantics, one learner over every
+            # rank's rows) on this exact stream, pinned offline by benchmarks/ffm_seq_ref.py
+            "logloss_seq_ref": seq_ref,
+            "logloss_gap": (round(ll - seq_ref, 5) if (ll is not None and seq_ref is not None)
+                            else None),
             "rows_trained_per_rank": B * (args.steps + args.warmup),
             "wall_s": wall,
         }
@@ -427,6 +460,8 @@ def main(argv=None):
             out[f"value_{alt_state}_state"] = round(alt_run["rows_per_s"], 1)
             out[f"ms_per_step_{alt_state}_state"] = round(alt_run["ms_per_step"], 4)
             out[f"logloss_heldout_{alt_state}"] = round(alt_run["ll"], 5)
+            if seq_ref is not None:
+                out[f"logloss_gap_{alt_state}"] = round(alt_run["ll"] - seq_ref, 5)
         print(json.dumps(out), flush=True)
     from hivemall_amd.parallel.dist import shutdown
     shutdown()

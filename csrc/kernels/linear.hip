@@ -710,7 +710,142 @@ __global__ __launch_bounds__(256) void hot_owner_final_kernel(Params P, float4* 
     st4(S + hot_feat[h], st);
 }
 
+// Near-sequential shared-table pass (the "seq" engine): Hivemall's per-row rule
+// for every optimizer at -mini_batch 1 on ONE table, W rows in flight.  Row q goes to wave q % W,
+// so the rows in flight are always W consecutive rows of the stream (the sequential learner's
+// order, each row reading the state up to W - 1 rows stale).  Per wave the rows are software-
+// pipelined as in linear_train_kernel: the next row's CSR bounds, first-chunk indices / values and
+// label are loaded while this row computes, so a row waits on one dependent round trip (its state
+// gather) instead of the shared kernel's three (order -> indptr -> idx -> S; 1.7 M rows/s at 8
+// rows in flight).  One-wave blocks; with spread = 8 only every 8th block works, which puts all W
+// waves on one XCD under round-robin placement (speed / staleness only, never correctness): its
+// L2 is then the one coherent copy every wave reads and writes, instead of 8 write-back L2s whose
+// dirty lines the other XCDs do not see (docs/perf_notes.md, the FFM XCD probe: 8 blocks on one
+// XCD +1.3e-4 vs +4.3e-3 on 8).  NT loads bypass the CU's L1, which other CUs' stores never refresh.
+template <bool NT>
+__global__ __launch_bounds__(64) void linear_seq_kernel(
+    Params P, int64_t n_rows, int dims, int64_t t0, int W, int spread, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ idx, const float* __restrict__ val, const float* __restrict__ y,
+    const int32_t* __restrict__ order, float4* __restrict__ S, uint8_t* __restrict__ touched,
+    float* __restrict__ RSW, double* __restrict__ loss_out) {
+    const int b = blockIdx.x;
+    if (b % spread) return;
+    const int g = b / spread;
+    if (g >= W) return;
+    const int lane = threadIdx.x;
+    float rs[HM_REP_SCALARS];
+#pragma unroll
+    for (int k = 0; k < HM_REP_SCALARS; ++k) rs[k] = RSW[(size_t)g * HM_REP_SCALARS + k];
+    double loss_acc = 0.0;
+    auto row_of = [&](int64_t q) -> int64_t { return order ? (int64_t)order[q] : q; };
+    int64_t cs = 0, ce = 0, pb_s = 0, pb_e = 0;
+    int pci = -1;
+    float pcx = 0.f, pyy = 0.f;
+    if (g < n_rows) {
+        const int64_t row0 = row_of(g);
+        cs = indptr[row0];
+        ce = indptr[row0 + 1];
+        if (lane < (int)(ce - cs)) {
+            pci = idx[cs + lane];
+            pcx = val ? val[cs + lane] : 1.f;
+        }
+        pyy = y[row0];
+        if (g + W < n_rows) {
+            const int64_t row1 = row_of(g + W);
+            pb_s = indptr[row1];
+            pb_e = indptr[row1 + 1];
+        }
+    }
+    for (int64_t q = g; q < n_rows; q += W) {
+        const int64_t s = cs, e = ce;
+        const int nnz = (int)(e - s);
+        const float yy = pyy;
+        const float t = (float)(t0 + q + 1);
+        rs[RS_T] = t;
+        const StepK sk = step_consts(P, t);
+        int ci = pci;
+        float cx = pcx;
+        if (lane >= nnz || ci < 0 || ci >= dims) { ci = -1; cx = 0.f; }
+        // ---- the state gather first (the one round trip the row waits on), then the prefetch ----
+        F4 cst = {0.f, 0.f, 0.f, 0.f};
+        if (ci >= 0) cst = ld4m<NT>(S + ci);
+        cs = pb_s;
+        ce = pb_e;
+        pci = -1;
+        pcx = 0.f;
+        if (q + W < n_rows) {
+            const int n1 = (int)(ce - cs);
+            if (lane < n1) {
+                pci = idx[cs + lane];
+                pcx = val ? val[cs + lane] : 1.f;
+            }
+            pyy = y[row_of(q + W)];
+            if (q + 2 * (int64_t)W < n_rows) {
+                const int64_t row2 = row_of(q + 2 * (int64_t)W);
+                pb_s = indptr[row2];
+                pb_e = indptr[row2 + 1];
+            }
+        }
+        float p = 0.f, sq = 0.f;
+        if (ci >= 0) {
+            p = cst.w * cx;
+            sq = cx * cx;
+            touched[ci] = 1;
+        }
+        for (int64_t k = s + 64 + lane; k < e; k += 64) {      // rows wider than a wave
+            const int i = idx[k];
+            const float x = val ? val[k] : 1.f;
+            if (i < 0 || i >= dims) continue;
+            const F4 st = ld4m<NT>(S + i);
+            p += st.w * x;
+            sq += x * x;
+            touched[i] = 1;
+        }
+        p = hm::wave_sum(p);
+        sq = hm::wave_sum(sq);
+        const RowCoef c = row_rule(P, p, yy, 0.f, sq, rs);
+        loss_acc += c.loss;
+        if (!c.update) continue;
+        if (ci >= 0) {
+            feature_update(P, c, cst, cx, sk, rs[RS_EVE_D]);
+            st4(S + ci, cst);
+        }
+        for (int64_t k = s + 64 + lane; k < e; k += 64) {
+            const int i = idx[k];
+            const float x = val ? val[k] : 1.f;
+            if (i < 0 || i >= dims) continue;
+            F4 st = ld4m<NT>(S + i);
+            feature_update(P, c, st, x, sk, rs[RS_EVE_D]);
+            st4(S + i, st);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < HM_REP_SCALARS; ++k) RSW[(size_t)g * HM_REP_SCALARS + k] = rs[k];
+        loss_out[g] = loss_acc;
+    }
+}
+
 }  // namespace
+
+// Near-sequential pass (linear_seq_kernel): one table S f32 [dims][4], touched u8 [dims], W waves
+// (RSW f32 [W][8], loss_out f64 [W]); spread 1 (waves dealt over every XCD) or 8 (one XCD).
+HM_API int hm_linear_train_seq(const Params* P, int64_t n_rows, int dims, int64_t t0, int W, int spread, int nt,
+                               const int64_t* indptr, const int32_t* idx, const float* val, const float* y,
+                               const int32_t* order, float* S, uint8_t* touched, float* RSW, double* loss_out,
+                               hipStream_t stream) {
+    if (n_rows <= 0) return 0;
+    if (W <= 0 || W > 65536 || dims <= 0 || (spread != 1 && spread != 8) || P->n_labels != 1 || has_covar(P->algo))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)(W * spread));
+    if (nt)
+        hipLaunchKernelGGL((linear_seq_kernel<true>), grid, dim3(64), 0, stream, *P, n_rows, dims, t0, W, spread,
+                           indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched, RSW, loss_out);
+    else
+        hipLaunchKernelGGL((linear_seq_kernel<false>), grid, dim3(64), 0, stream, *P, n_rows, dims, t0, W, spread,
+                           indptr, idx, val, y, order, reinterpret_cast<float4*>(S), touched, RSW, loss_out);
+    HM_LAUNCH_RET();
+}
 
 // ip: R, dims, L, mini_batch, touched_cap, (n_rows as int64 separately)
 HM_API int hm_linear_train(const Params* P, const int32_t* ip, int64_t n_rows,

@@ -156,6 +156,7 @@ _HOST_SIGS: dict[str, tuple] = {
     "hm_dict_dump": (c_i64, [c_p, c_p, c_p]),
     "hm_parse_features": (c_i64, [c_p, c_p, c_i64, c_int, c_p, c_int, c_i32, c_u32, c_i64, c_p, c_p]),
     "hm_parse_ffm_features": (c_i64, [c_p, c_p, c_i64, c_i32, c_i32, c_int, c_u32, c_p, c_p, c_p]),
+    "hm_ffm_schedule_slots": (c_i64, [c_p, c_int, c_int, c_p, c_int, c_int, c_int, c_int, c_p]),
 }
 
 

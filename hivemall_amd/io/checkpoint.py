@@ -94,7 +94,10 @@ def save(learner, path: str, model_table: bool = True) -> str:
             "scalars": {k: _jsonable(getattr(learner, k)) for k in _SCALARS
                         if hasattr(learner, k) and isinstance(getattr(learner, k), (int, float, str, list, tuple, type(None), np.integer, np.floating))},
             "state_kind": "dataclass" if dataclasses.is_dataclass(st) else ("dict" if isinstance(st, dict) else None),
-            "state_meta": dict(st.meta) if dataclasses.is_dataclass(st) and hasattr(st, "meta") else None,
+            # JSON scalars only: tensors kept in meta are scratch buffers the engines rebuild
+            # (ops/linear.py train_pass_minibatch), caches (the hot set) are recomputed
+            "state_meta": ({k: v for k, v in st.meta.items() if isinstance(v, (bool, int, float, str))}
+                           if dataclasses.is_dataclass(st) and hasattr(st, "meta") else None),
             "state_covar": bool(getattr(st, "covar", False)) if dataclasses.is_dataclass(st) else None,
             "encoder": _encoder_meta(getattr(learner, "encoder", None)),
             "cv": vars(learner.cv) if hasattr(learner, "cv") else None,

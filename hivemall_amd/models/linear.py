@@ -58,8 +58,12 @@ LEARNER_BASE_OPTS = [
     opt("engine", None, "auto", str,
         "[engine] GPU execution: replica (private model per wave, mixed), shared (one Hogwild "
         "table for the whole chip, large -dims), minibatch (general learner with -mini_batch > 1: "
-        "the whole chip on each batch, exact mini-batch rule), auto (minibatch for -mini_batch > 1, "
-        "else shared when the replicas would exceed 2 GiB)"),
+        "the whole chip on each batch, exact mini-batch rule), seq (one table, -shared_waves "
+        "consecutive rows in flight on one XCD, software-pipelined: the near-sequential engine), "
+        "auto (minibatch for -mini_batch > 1, else shared when the replicas would exceed 2 GiB)"),
+    opt("seq_spread", None, 8, int,
+        "[engine] seq engine: 8 = every wave on one XCD (one coherent L2), 1 = waves dealt over "
+        "all 8 XCDs"),
     opt("shared_replicas", None, 1, int,
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
@@ -363,6 +367,15 @@ class OnlineLinearLearner(Learner):
             if self._warm is not None:
                 self.load_model_table(self._warm)
             return
+        if self._use_seq(L, mb):
+            W = int(self.cl["shared_waves"]) or LO.SEQ_ENGINE_WAVES
+            if int(self.cl["seq_spread"]) not in (1, 8):
+                raise UDFArgumentException(f"{self.NAME}: -seq_spread must be 1 or 8")
+            self.state = LO.new_seq_state(dims, self.device, max(1, min(W, max(1, rows.n))),
+                                          int(self.cl["seq_spread"]))
+            if self._warm is not None:
+                self.load_model_table(self._warm)
+            return
         if self._use_shared(R, L, dims, mb):
             try:
                 W = LO.shared_waves(rows.n, int(self.cl["shared_waves"]) or LO.rule_waves(self.P))
@@ -397,13 +410,26 @@ class OnlineLinearLearner(Learner):
         return (eng == "auto" and int(self.cl["replicas"]) <= 0 and self.device.type == "cuda"
                 and mb > 1 and L == 1 and LO.minibatch_rule(self.P))
 
+    def _use_seq(self, L: int, mb: int) -> bool:
+        """Near-sequential engine (ops/linear.py train_pass_seq): ``-engine seq``, or auto for the
+        general-learner rules whose parity needs few rows in flight (ops/linear.py seq_rule)."""
+        eng = str(self.cl["engine"]).lower()
+        ok = self.device.type == "cuda" and not self.covar and L == 1 and mb == 1
+        if eng == "seq":
+            if not ok:
+                raise UDFArgumentException(f"{self.NAME}: -engine seq needs a GPU, a rule without "
+                                           "covariance, a binary/regression task and -mini_batch 1")
+            return True
+        return (eng == "auto" and ok and int(self.cl["replicas"]) <= 0
+                and int(self.cl["shared_replicas"]) == 1 and LO.seq_rule(self.P))
+
     def _use_shared(self, R: int, L: int, dims: int, mb: int) -> bool:
         """Shared-table Hogwild engine: device only, binary/regression rules
         without covariance, per-row updates.  auto picks it when R private replicas of
         ``dims x 16 B`` would exceed 2 GiB (e.g. Hivemall's default 2^24 hashed dims)."""
         eng = str(self.cl["engine"]).lower()
-        if eng not in ("auto", "replica", "shared", "minibatch"):
-            raise UDFArgumentException(f"{self.NAME}: -engine must be auto, replica, shared or minibatch")
+        if eng not in ("auto", "replica", "shared", "minibatch", "seq"):
+            raise UDFArgumentException(f"{self.NAME}: -engine must be auto, replica, shared, seq or minibatch")
         ok = (self.device.type == "cuda" and not self.covar and L == 1 and mb == 1)
         if eng == "shared" and not ok:
             raise UDFArgumentException(f"{self.NAME}: -engine shared needs a GPU, a rule without "
@@ -424,8 +450,12 @@ class OnlineLinearLearner(Learner):
         iters = int(self.cl["iters"])
         shared = self.state.meta.get("shared", False)
         minibatch = self.state.meta.get("minibatch", False)
+        seq = self.state.meta.get("seq", False)
         for ep in self.epochs(iters, data=(rows.indptr, rows.idx, rows.val, rows.y)):
-            if minibatch:
+            if seq:
+                loss = LO.train_pass_seq(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
+                                         self.rows_seen)
+            elif minibatch:
                 loss = LO.train_pass_minibatch(self.state, self.P, rows.indptr, rows.idx, rows.val, rows.y,
                                                self.rows_seen, mb)
             elif shared:

@@ -225,6 +225,19 @@ def hot_owner_rule(P: LinParams) -> bool:
 SEQ_WAVES = 8
 
 
+# Rows in flight of the near-sequential engine (linear_seq_kernel, ``-engine seq``) by default.
+SEQ_ENGINE_WAVES = 32
+# HM_LINEAR_SEQ=0: the rules of seq_rule stay on the shared engine at SEQ_WAVES rows in flight
+_SEQ_AUTO = os.environ.get("HM_LINEAR_SEQ", "0") != "0"
+
+
+def seq_rule(P: LinParams) -> bool:
+    """Rules routed to the near-sequential engine by ``-engine auto``: the general learner's
+    rules that neither pre-aggregate (hot_rule) nor own (hot_owner_rule) their hot features."""
+    return (_SEQ_AUTO and P.algo == ALGOS["general"] and P.n_labels == 1 and not hot_rule(P)
+            and not hot_owner_rule(P))
+
+
 def rule_waves(P: LinParams) -> int:
     """Default rows in flight of the shared-table engine for the rule (see above)."""
     if hot_rule(P):
@@ -315,6 +328,41 @@ def train_pass_shared(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: 
     return loss
 
 
+def new_seq_state(dims: int, device, waves: int, spread: int = 8) -> LinearState:
+    """Near-sequential engine state (csrc/kernels/linear.hip linear_seq_kernel): one table
+    S [1, 1, dims, 4], touched [1, dims], per-wave scalars RS [W, 8]; ``spread`` 8 keeps the W
+    waves on one XCD (1: dealt over all of them)."""
+    st = LinearState(torch.zeros((1, 1, dims, 4), dtype=torch.float32, device=device),
+                     torch.zeros((1, dims), dtype=torch.uint8, device=device),
+                     torch.zeros((int(waves), 8), dtype=torch.float32, device=device), False)
+    st.meta.update(seq=True, spread=int(spread), nt=True)
+    return st
+
+
+def train_pass_seq(st: LinearState, P: LinParams, indptr: torch.Tensor, idx: torch.Tensor,
+                   val: torch.Tensor | None, y: torch.Tensor, t0: int,
+                   order: torch.Tensor | None = None) -> torch.Tensor:
+    """One pass of the near-sequential engine (row q on wave q % W, step t0 + q + 1).  Returns
+    per-wave loss sums."""
+    n = indptr.numel() - 1
+    dev = st.device
+    assert dev.type == "cuda" and st.meta.get("seq"), "near-sequential engine state on a GPU"
+    assert indptr.dtype == torch.int64 and idx.dtype == torch.int32 and y.dtype == torch.float32
+    assert y.numel() >= n and (val is None or val.numel() == idx.numel())
+    for t in (indptr, idx, val, y, order):
+        if t is not None:
+            assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    W = st.RS.shape[0]
+    loss = torch.zeros(W, dtype=torch.float64, device=dev)
+    p = _native.ptr
+    rc = _native.hip().hm_linear_train_seq(C.addressof(P), C.c_int64(n), st.dims, C.c_int64(int(t0)), W,
+                                           int(st.meta.get("spread", 8)), int(st.meta.get("nt", True)),
+                                           p(indptr), p(idx), p(val), p(y), p(order), p(st.S),
+                                           p(st.touched), p(st.RS), p(loss), _native.stream_of(dev))
+    _native.check(rc, "hm_linear_train_seq")
+    return loss
+
+
 def new_minibatch_state(dims: int, device, max_rows_per_batch: int, max_nnz: int) -> LinearState:
     """Mini-batch engine state (csrc/kernels/linear.hip hm_linear_train_minibatch): one table
     S [1, 1, dims, 4] plus the batch buffers (gradient sums, touched marks, the batch's feature
@@ -348,6 +396,12 @@ def train_pass_minibatch(st: LinearState, P: LinParams, indptr: torch.Tensor, id
     for t in (indptr, idx, val, y, order):
         if t is not None:
             assert t.device == dev and t.is_contiguous(), "tensor device/layout mismatch"
+    # the batch buffers are zeroed scratch (every batch leaves them zeroed): a state restored from
+    # a checkpoint (io/checkpoint.py keeps only JSON scalars of state.meta) gets fresh ones
+    for k, shape, dt in (("ga", (st.dims,), torch.float32), ("mark", (st.dims,), torch.int32),
+                         ("cnt", (2,), torch.int32), ("list", (1,), torch.int32)):
+        if not isinstance(st.meta.get(k), torch.Tensor) or st.meta[k].device != dev:
+            st.meta[k] = torch.zeros(shape, dtype=dt, device=dev)
     if n > 0:
         nnz = int((indptr[1:] - indptr[:-1]).max().item())
         need = min(st.dims, M * max(1, nnz))
@@ -445,6 +499,8 @@ _native.register_host("hm_linear_train_cpu", [_P, _P, _native.c_i64] + [_P] * 9)
 _native.register_hip("hm_linear_train_shared", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int,
                                               C.c_int, C.c_int] + [_P] * 9 + [_P, _P] + [C.c_int] * 4
                      + [_P, _P])
+_native.register_hip("hm_linear_train_seq", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int, C.c_int, C.c_int]
+                     + [_P] * 9 + [_P])
 _native.register_hip("hm_linear_train_minibatch", [_P, _native.c_i64, C.c_int, _native.c_i64, C.c_int]
                      + [_P] * 12 + [_P])
 _native.register_hip("hm_linear_mix_reduce", [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])

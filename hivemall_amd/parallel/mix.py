@@ -100,12 +100,25 @@ def _view3(t: torch.Tensor):
     return None
 
 
+def _shard_mean(recv: torch.Tensor, world: int, shard: int, dtype: torch.dtype, out: torch.Tensor) -> None:
+    """out <- fp32 sum over ranks 0..world-1 of recv[r] / world, one rounding (recv [world, shard])."""
+    code = _dtype_code(dtype)
+    if recv.is_cuda and code is not None and shard % 4 == 0:
+        rc = _native.hip().hm_mix_shard_mean(recv.data_ptr(), world, shard, code, out.data_ptr(),
+                                             _native.stream_of(recv.device))
+        _native.check(rc, "hm_mix_shard_mean")
+    else:
+        s = recv.view(world, shard).sum(0, dtype=torch.float32)
+        out.copy_(s.mul_(1.0 / world))
+
+
 class _FlatGroup:
     """Same-dtype tensors packed into one flat wire buffer, padded to a multiple of 4*world."""
 
     def __init__(self, tensors: list[torch.Tensor], world: int, wire: torch.dtype | None = None):
         # weak references: a cached plan must not keep a discarded model alive in HBM
         self._refs = [weakref.ref(t) for t in tensors]
+        self.world = world
         self.shapes = [tuple(t.shape) for t in tensors]
         self.busy = False            # an OverlappedMixer collective is in flight on the buffers
         self.prepacked = False       # send already holds the current snapshot (fused merge)
@@ -173,6 +186,116 @@ class _FlatGroup:
         sent = self.seg(self.send, k) if mode == 4 else None
         rc = _native.hip().hm_mix_delta3(t.data_ptr(), b.data_ptr(), wire.data_ptr(),
                                          sent.data_ptr() if sent is not None else None, *v3, mode, xc, wc,
+                                         _native.stream_of(t.device))
+        _native.check(rc, "hm_mix_delta3")
+        return True
+
+    # ---- row ranges (the bucketed pipeline of ModelMixer.average / average_delta) ----
+    def rows_of(self, k: int, t: torch.Tensor) -> tuple[int, int]:
+        """(rows, elements per row) of tensor k: the n0 rows of its _view3 (one feature's slots of
+        the FFM V view, one 4-element quad of a contiguous tensor), else one row."""
+        v3 = _view3(t)
+        n = t.numel()
+        if v3 is not None and n:
+            return v3[0], v3[1] * v3[2]
+        return 1, n
+
+    def sub(self, t: torch.Tensor, ra: int, rb: int, rl: int) -> torch.Tensor:
+        """Rows [ra, rb) of tensor t (rl elements per row) as a view of t."""
+        if rb - ra == t.numel() // max(1, rl) and ra == 0:
+            return t
+        if t.is_contiguous():
+            return t.view(-1)[ra * rl:rb * rl]
+        return t[ra:rb]
+
+    def flat(self, buf: torch.Tensor, k: int, ra: int, rb: int, rl: int) -> torch.Tensor:
+        return buf[self.offs[k] + ra * rl:self.offs[k] + rb * rl]
+
+    def buckets(self, elems: int) -> list[tuple[int, int, list, list]]:
+        """Contiguous buckets of the flat wire buffer, each a multiple of 4 * world elements and
+        about ``elems`` long: (lo, hi, pack_rows, merge_rows), the row ranges per tensor as
+        (k, ra, rb).  A bucket packs every row that has an element in [lo, hi) (a row straddling
+        two buckets is packed by both: the pack is idempotent while x and base are unchanged) and
+        merges the rows whose LAST element is in [lo, hi) — every element of those is in this or
+        an earlier bucket, so its mean has arrived; each row is merged exactly once."""
+        q = 4 * self.world
+        step = max(q, (int(elems) // q) * q)
+        ts = self.tensors
+        spans = []
+        for k, t in enumerate(ts):
+            nr, rl = self.rows_of(k, t)
+            spans.append((k, self.offs[k], nr, rl))
+        out = []
+        for lo in range(0, self.n, step):
+            hi = min(self.n, lo + step)
+            pk, mg = [], []
+            for k, off, nr, rl in spans:
+                if rl == 0 or nr == 0:
+                    continue
+                a, b = off, off + nr * rl                    # tensor k's flat range
+                if b <= lo or a >= hi:
+                    continue
+                ra = max(0, (lo - a) // rl)
+                rb = min(nr, -(-(hi - a) // rl))
+                pk.append((k, ra, rb))
+                # rows whose last element a + (r + 1) rl - 1 lies in [lo, hi)
+                ma = max(0, -((a - lo - 1) // rl) - 1)      # ceil((lo - a + 1) / rl) - 1
+                mb = min(nr, (hi - a) // rl)
+                if mb > ma:
+                    mg.append((k, ma, mb))
+            out.append((lo, hi, pk, mg))
+        return out
+
+    def pack_rows(self, rows, delta: bool) -> None:
+        """pack (delta: send <- x - base; else send <- x) over the given row ranges."""
+        code = _dtype_code(self.dtype)
+        ts = self.tensors
+        for k, ra, rb in rows:
+            t = ts[k]
+            nr, rl = self.rows_of(k, t)
+            x = self.sub(t, ra, rb, rl)
+            d = self.flat(self.send, k, ra, rb, rl)
+            if delta:
+                if self._delta3_rows(k, t, 2, ra, rb, rl):
+                    continue
+                d.copy_(x.reshape(-1).to(torch.float32) - self.flat(self.base, k, ra, rb, rl))
+                continue
+            v3 = _view3(x) if x.is_cuda and code is not None else None
+            if v3 is not None:
+                rc = _native.hip().hm_mix_pack3(x.data_ptr(), d.data_ptr(), *v3, code,
+                                                _native.stream_of(x.device))
+                _native.check(rc, "hm_mix_pack3")
+            else:
+                d.copy_(x.reshape(-1))
+
+    def merge_rows(self, rows, delta: bool) -> None:
+        """delta: base <- base + m, x <- base; else x <- out; over the given row ranges."""
+        ts = self.tensors
+        for k, ra, rb in rows:
+            t = ts[k]
+            nr, rl = self.rows_of(k, t)
+            x = self.sub(t, ra, rb, rl)
+            m = self.flat(self.out, k, ra, rb, rl)
+            if delta:
+                if self._delta3_rows(k, t, 3, ra, rb, rl):
+                    continue
+                b = self.flat(self.base, k, ra, rb, rl)
+                b.add_(m.to(torch.float32))
+                x.copy_(b.view(x.shape))
+            else:
+                x.copy_(m.view(x.shape))
+
+    def _delta3_rows(self, k: int, t: torch.Tensor, mode: int, ra: int, rb: int, rl: int) -> bool:
+        xc, wc = _dtype_code(t.dtype), _dtype_code(self.dtype)
+        v3 = _view3(t) if (_FUSED_DELTA and t.is_cuda and xc is not None and wc is not None) else None
+        if v3 is None:
+            return False
+        n0, d1, inner, s0, s1 = v3
+        es = t.element_size()
+        b = self.flat(self.base, k, ra, rb, rl)
+        wire = self.flat(self.send if mode == 2 else self.out, k, ra, rb, rl)
+        rc = _native.hip().hm_mix_delta3(t.data_ptr() + ra * s0 * es, b.data_ptr(), wire.data_ptr(), None,
+                                         rb - ra, d1, inner, s0, s1, mode, xc, wc,
                                          _native.stream_of(t.device))
         _native.check(rc, "hm_mix_delta3")
         return True
@@ -335,18 +458,66 @@ class ModelMixer:
     def _gather(self, g: _FlatGroup, async_op: bool = False):
         return dist.all_gather_into_tensor(g.out, g.mean, async_op=async_op)
 
+    # wire bytes per bucket of the pipelined shard mean (SURVEY.md:739-742: 32-128 MB buckets);
+    # 0 = one monolithic collective pair per dtype group (A/B, tests)
+    PIPE_BUCKET_MB = 32.0
+
+    def _pipelined(self, g: _FlatGroup, delta: bool) -> None:
+        """Bucketed, software-pipelined shard mean of one flat group: bucket b+1's pack (compute
+        stream) and its all-to-all (the RCCL stream) are issued before bucket b's shard mean and
+        all-gather, and bucket b-1's merge runs while bucket b's gather is in flight, so at most
+        one bucket's device work is exposed next to the wire.  Every element's mean is the same
+        fp32 sum over ranks 0..N-1 as in the monolithic path, rounded once: bit-identical."""
+        elems = int(self.PIPE_BUCKET_MB * (1 << 20)) // g.send.element_size()
+        bks = g.buckets(elems) if elems > 0 else []
+        if len(bks) <= 1:
+            (g.pack_delta if delta else g.pack)()
+            self._a2a(g)
+            g.shard_mean(self.world)
+            self._gather(g)
+            (g.merge_delta_sync if delta else g.unpack)()
+            return
+        W = self.world
+        views = []
+        for lo, hi, pk, mg in bks:
+            sh = (hi - lo) // W
+            views.append((g.send[lo:hi], g.recv[lo:hi], g.out[lo:hi], sh))
+        # two bucket-sized shard-mean buffers, alternating: bucket b + 2's mean overwrites bucket
+        # b's only after bucket b's gather was waited on (the wait orders the compute stream after it)
+        mbuf = getattr(g, "mbuf", None)
+        if mbuf is None or mbuf[0].numel() < views[0][3]:
+            mbuf = g.mbuf = [torch.empty(views[0][3], dtype=g.dtype, device=g.send.device) for _ in range(2)]
+        a2a, gat = [None] * len(bks), [None] * len(bks)
+
+        def start(b):
+            g.pack_rows(bks[b][2], delta)
+            a2a[b] = dist.all_to_all_single(views[b][1], views[b][0], async_op=True)
+
+        start(0)
+        for b in range(len(bks)):
+            if b + 1 < len(bks):
+                start(b + 1)
+            a2a[b].wait()
+            _, r, o, sh = views[b]
+            mb = mbuf[b & 1][:sh]
+            _shard_mean(r, W, sh, g.dtype, mb)
+            gat[b] = dist.all_gather_into_tensor(o, mb, async_op=True)
+            if b >= 1:
+                gat[b - 1].wait()
+                g.merge_rows(bks[b - 1][3], delta)
+        gat[-1].wait()
+        g.merge_rows(bks[-1][3], delta)
+
     def average(self, tensors: list[torch.Tensor]) -> None:
-        """In-place replica mean (shard-mean collective, see the module docstring)."""
+        """In-place replica mean (shard-mean collective, see the module docstring), bucketed and
+        pipelined (:meth:`_pipelined`)."""
         if not self._active():
             return
         groups = self.plan(tensors)
         for g in groups:
-            g.pack()
-        for g in groups:
-            self._a2a(g)
-            g.shard_mean(self.world)
-            self._gather(g)
-            g.unpack()
+            if g.prepacked:          # an overlapped mix left a snapshot: repack from x
+                g.prepacked = False
+            self._pipelined(g, delta=False)
         self._count(groups, tensors)
 
     # ---------------------------------------------------------------- mean of deltas, bf16 wire
@@ -376,11 +547,9 @@ class ModelMixer:
             self._plans[key] = [g]
             self._evict(keep=key)
             return
-        g.pack_delta()                  # send <- x - base (one fused pass per tensor)
-        self._a2a(g)
-        g.shard_mean(self.world)
-        self._gather(g)
-        g.merge_delta_sync()            # base <- base + mean delta; x <- base
+        # per bucket: send <- x - base; all-to-all; fp32 shard mean; all-gather; base <- base +
+        # mean delta, x <- base (fused passes per tensor row range, pipelined over the buckets)
+        self._pipelined(g, delta=True)
         self.calls += 1
         self.bytes_reduced += sum(t.numel() * t.element_size() for t in tensors)
         self.wire_bytes += 2 * (self.world - 1) * g.nbytes // self.world

@@ -514,3 +514,48 @@ def test_mix_average_delta_bf16_wire():
         assert max(errs) < 2e-4, errs            # bf16 rounding of a ~1e-2 step (2^-9 relative)
     assert out[0][1] == out[1][1]                  # bit-identical replicas
     assert out[0][2] == out[1][2]                  # elements outside the view untouched
+
+
+def _pipe_bitident(ctx):
+    """The bucketed, pipelined shard mean (ModelMixer._pipelined) against the monolithic one
+    (PIPE_BUCKET_MB = 0) on the FFM-shaped tensor list: the strided V view of the feature blocks,
+    a strided [NF, 4] record view, an odd-length contiguous tensor and a 4-element bias; plain
+    average and the bf16-wire average_delta, several mixes each."""
+    from hivemall_amd.parallel.mix import ModelMixer
+
+    def model(seed):
+        g = torch.Generator().manual_seed(seed)
+        blk = torch.randn(331, 7, 6, 4, generator=g)            # [NF][FS][slots..] blocks
+        V = blk[:, :5, 1, :]                                     # strided [331, 5, 4]
+        rec = torch.randn(331, 12, generator=g)[:, 4:8]          # strided [331, 4]
+        odd = torch.randn(1001, generator=g)
+        bias = torch.randn(4, generator=g)
+        return [V, rec, odd, bias]
+
+    out = {}
+    for mb in (0.0, 0.002, 0.0007):
+        for delta in (False, True):
+            ts = model(7 + ctx.rank)
+            m = ModelMixer(ctx)
+            m.PIPE_BUCKET_MB = mb
+            fn = m.average_delta if delta else m.average
+            for it in range(3):
+                g = torch.Generator().manual_seed(100 * it + ctx.rank)
+                for t in ts:
+                    t += torch.randn(t.shape, generator=g) * 1e-2
+                fn(ts)
+            out[(mb, delta)] = [t.clone() for t in ts]
+    res = []
+    for delta in (False, True):
+        ref = out[(0.0, delta)]
+        for mb in (0.002, 0.0007):
+            res.append(all(torch.equal(a, b) for a, b in zip(ref, out[(mb, delta)])))
+    return res, float(sum(float(t.double().sum()) for t in out[(0.0007, True)]))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_mix_pipelined_buckets_bit_identical_to_monolithic(world):
+    out = run_world("_pipe_bitident", world=world)
+    for r in range(world):
+        assert out[r][0] == [True] * 4, out[r][0]
+        assert out[r][1] == out[0][1]                  # every rank bit-identical

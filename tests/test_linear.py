@@ -232,6 +232,52 @@ def test_gpu_shared_engine_one_wave_is_sequential(name, opts, reload):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spread", [1, 8])
+@pytest.mark.parametrize("opts", ["-loss logloss -opt adam -eta0 0.01", "-loss logloss -opt sgd -eta0 0.05",
+                                  "-loss logloss -opt rmsprop -eta0 0.01", "-loss logloss -opt adadelta",
+                                  "-loss hinge -opt momentum -eta0 0.005 -reg l2"])
+def test_gpu_seq_engine_one_wave_is_sequential(opts, spread):
+    """The near-sequential engine (csrc/kernels/linear.hip linear_seq_kernel) with ONE wave walks
+    the rows in order with step t0 + q + 1 through its software pipeline (next row's indices,
+    values and label prefetched): the sequential learner, i.e. the CPU engine with one replica,
+    over two passes (t0 carries over), whichever XCD placement."""
+    from hivemall_amd.ops import linear as LO
+
+    rows = _criteo_rows(3000, 12, seed=3, distinct=True)
+    cpu = L.TrainClassifier(opts + " -replicas 1", device="cpu")
+    cpu._ensure_state(rows)
+    st = LO.new_seq_state(cpu.state.dims, "cuda", waves=1, spread=spread)
+    rg = rows.to("cuda")
+    for ep in range(2):
+        LO.train_pass(cpu.state, cpu.P, rows.indptr, rows.idx, rows.val, rows.y)
+        LO.train_pass_seq(st, cpu.P, rg.indptr, rg.idx, rg.val, rg.y, t0=ep * rows.n)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(st.S[0, 0].cpu().numpy(), cpu.state.S[0, 0].numpy(), rtol=2e-4, atol=2e-5)
+    assert torch.equal(st.touched[0].cpu(), cpu.state.touched[0])
+
+
+@pytest.mark.gpu
+def test_gpu_minibatch_engine_resumes_from_checkpoint(tmp_path):
+    """the mini-batch engine's batch buffers are scratch tensors in state.meta, which
+    the checkpoint does not keep; a restored learner rebuilds them and trains on."""
+    from hivemall_amd.io import checkpoint as ck
+
+    rows = _criteo_rows(20000, 20, seed=5).to("cuda")
+    m = L.TrainClassifier("-loss logloss -opt adam -eta0 0.01 -dims 1048576 -iters 1 -mini_batch 256",
+                          device="cuda")
+    m.fit(rows=rows)
+    assert m.state.meta.get("minibatch")
+    ck.save(m, str(tmp_path / "ck"))
+    m2 = ck.load(str(tmp_path / "ck"), device="cuda")
+    assert m2.state.meta.get("minibatch") and not isinstance(m2.state.meta.get("ga"), torch.Tensor)
+    m.fit(rows=rows)
+    m2.fit(rows=rows)
+    torch.cuda.synchronize()
+    w1, w2 = m.weights()[0][0].cpu(), m2.weights()[0][0].cpu()
+    assert torch.allclose(w1, w2, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("opts", ["-opt adagrad", "-opt adagrad -reg no", "-opt adagrad -reg l2 -lambda 1e-6",
                                   "-opt adagrad -reg rda -lambda 1e-6", "-opt adagrad -reg l1 -lambda 1e-6",
                                   "-opt adagrad -reg elasticnet -lambda 1e-6", "-opt adadelta",

@@ -121,3 +121,50 @@ def test_fused_delta_mixing_bit_identical_to_torch_path():
     finally:
         M._FUSED_DELTA = old
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_pipelined_buckets_bit_identical_through_rccl_one_rank():
+    """The bucketed, pipelined shard mean (ModelMixer._pipelined: per-bucket fused pack of the
+    tensor row ranges, all_to_all on the RCCL stream, shard mean, all_gather, fused merge of the
+    rows whose means have all arrived) leaves exactly the bits of the monolithic path, for
+    average_delta on fp32 replicas and average on bf16 ones, on the FFM feature-block views."""
+    import torch.distributed as dist
+
+    from hivemall_amd.models.ffm import FFMTrainer
+    from hivemall_amd.ops.ffm import linear_mix_tensors
+    from hivemall_amd.parallel import mix as M
+    from hivemall_amd.parallel.dist import DistContext
+
+    assert not dist.is_initialized()
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        ctx = DistContext(0, 1, 0, dev, "nccl")
+        for bf16 in (False, True):
+            res = {}
+            for mb in (0.0, 0.37):
+                tr = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 14 -seed 3"
+                                + (" -bf16_state" if bf16 else ""), device=dev)
+                tr.init_state(1 << 14, 39)
+                st = tr.state
+                g = torch.Generator(device="cuda").manual_seed(5)
+                tensors = [st["V"], *linear_mix_tensors(st), st["bias"]]
+                m = M.ModelMixer(ctx, min_world=1)
+                m.PIPE_BUCKET_MB = mb
+                fn = m.average if bf16 else m.average_delta
+                for step in range(3):
+                    for t in tensors:
+                        t.add_((torch.randn(t.shape, generator=g, device=dev) * 1e-3).to(t.dtype))
+                    fn(tensors)
+                if mb:
+                    grp = next(iter(m._plans.values()))[0]
+                    assert len(grp.buckets(int(mb * (1 << 20)) // grp.send.element_size())) >= 4
+                torch.cuda.synchronize()
+                res[mb] = [t.clone() for t in tensors]
+                del tr, st, tensors, m
+            for a, b in zip(res[0.0], res[0.37]):
+                assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
