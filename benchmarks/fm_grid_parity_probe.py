@@ -32,16 +32,28 @@ def main():
     m8 = ll(mapper_average_fm(opts, idx, y, 8, 1 << 20), "cpu")
     print(json.dumps({"mappers8": round(m8, 5)}), flush=True)
     rows = _rows(idx, y).to("cuda")
+    # PROBE_VARIANTS="0,2,3": kernel variants (HM_FM_VARIANT) interleaved in one process
+    variants = os.environ.get("PROBE_VARIANTS", os.environ.get("HM_FM_VARIANT", "0")).split(",")
+    # PROBE_HOT="0.01,0": the hot-feature write-through threshold (ops/fm.py HOT_FRAC; 0 = off)
+    import hivemall_amd.ops.fm as fm_ops
+    hots = [float(h) for h in os.environ.get("PROBE_HOT", str(fm_ops.HOT_FRAC)).split(",")]
+    # PROBE_HOT_EVERY="1,8,32": write-through on one hot update in N (ops/fm.py HOT_EVERY)
+    evs = [int(e) for e in os.environ.get("PROBE_HOT_EVERY", str(fm_ops.HOT_EVERY)).split(",")]
     for rep in range(reps):
         for g in grids:
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            m = FMTrainer(gopts + f" -grid {g}", device="cuda").fit(rows=rows)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t
-            v = ll(m, "cuda")
-            print(json.dumps({"opts": extra, "variant": os.environ.get("HM_FM_VARIANT", "0"), "grid": g, "rep": rep, "gpu": round(v, 5), "delta_vs_mappers8": round(v - m8, 5),
-                              "rows_per_s": round(n / dt)}), flush=True)
+            for var, hot, ev in [(v, h, e) for v in variants for h in hots for e in evs]:
+                fm_ops.HOT_FRAC = hot
+                fm_ops.HOT_EVERY = ev
+                os.environ["HM_FM_VARIANT"] = var
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                m = FMTrainer(gopts + f" -grid {g}", device="cuda").fit(rows=rows)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t
+                os.environ["HM_FM_VARIANT"] = "0"
+                v = ll(m, "cuda")
+                print(json.dumps({"opts": extra, "variant": var, "hot_frac": hot, "hot_every": ev, "grid": g, "rep": rep, "gpu": round(v, 5),
+                                  "delta_vs_mappers8": round(v - m8, 5), "rows_per_s": round(n / dt)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -58,14 +58,15 @@ def main():
     ap.add_argument("--spread", default="8,1")
     ap.add_argument("--rules", default=None, help="';'-separated option strings")
     ap.add_argument("--shared", type=int, default=1, help="also the shared engine at its rule waves")
+    ap.add_argument("--seed", type=int, default=5, help="training rows' seed")
     a = ap.parse_args()
     rules = a.rules.split(";") if a.rules else RULES
-    rows = rows_of(a.rows, 24, 5)
+    rows = rows_of(a.rows, 24, a.seed)
     test = rows_of(100_000, 24, 99)
     for opts in rules:
         mc, rc = fit(opts, rows, "cpu")
         ll_c = heldout(mc, test, "cpu")
-        print(json.dumps({"opts": opts, "engine": "cpu-seq", "rows": a.rows, "logloss": round(ll_c, 5),
+        print(json.dumps({"opts": opts, "engine": "cpu-seq", "rows": a.rows, "seed": a.seed, "logloss": round(ll_c, 5),
                           "rows_per_s": round(rc)}), flush=True)
         if a.shared:
             m, r = fit(opts + " -engine shared", rows, "cuda")

@@ -61,7 +61,8 @@ def main():
                 fn(tensors)
             e1.record()
             torch.cuda.synchronize()
-            grp = next(iter(m._plans.values()))[0]
+            grp = [p for k, p in m._plans.items() if k[0] == "delta"] or list(m._plans.values())
+            grp = grp[0][0]
             nb = len(grp.buckets(int(mb * (1 << 20)) // grp.send.element_size())) if mb else 1
             print(json.dumps({"state": state, "fn": fn.__name__, "payload_MB": round(payload / 2**20, 1),
                               "wire_MB": round(grp.nbytes / 2**20, 1), "bucket_MB": mb, "buckets": nb,

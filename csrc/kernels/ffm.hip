@@ -475,7 +475,17 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                 float xs = s_x[tid];
                 if (multi)
                     for (int a2 = s_ni[tid]; a2 >= 0; a2 = s_ni[a2]) xs += s_x[a2];
-                LW(w, i) = ftrl_update(&LW(wz, i), &LW(wn, i), LW(w, i), kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
+                if (P.lpack) {
+                    // the {w, z, n} record: one 16-B read and one 16-B store (never a torn record)
+                    float4* rp = reinterpret_cast<float4*>(&LW(w, i));
+                    const float4 r = *rp;
+                    float z = r.y, n = r.z;
+                    const float nw = ftrl_update(&z, &n, r.x, kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
+                    *rp = make_float4(nw, z, n, 0.f);
+                } else {
+                    LW(w, i) = ftrl_update(&LW(wz, i), &LW(wn, i), LW(w, i), kappa * xs * scale, P.alpha, P.beta,
+                                           P.lambda1, P.lambda2);
+                }
             }
             if (P.use_bias && tid == 0) bias_update(P, kappa, bias);
         }
@@ -1916,9 +1926,11 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // per CU does not move this kernel.  Round 5 re-tried it after the linear records (53.4 KB of LDS
 // with the 4-B linear zone aliased onto the 16-B one, forced to 3 waves per SIMD): 168 VGPRs with
 // 21 spilled, 63.2 vs 89.6 M rows/s (profiles/r5/bench_rg_ab.log).
-// aux (host array of 2 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
+// aux (host array of 4 pointer-sized entries, or null): aux[0] = per-feature hot flags (variant 8)
 // or null; aux[1] = the multi-hot deferral buffer int32 [1 + B] or null (then a multi-hot row is
-// updated slot by slot by the pipelined kernels: racing stores of one address, one wins).
+// updated slot by slot by the pipelined kernels: racing stores of one address, one wins);
+// aux[2] = the global-bias shards fp32 [S][32] (training with -w0) or null; aux[3] = S, the
+// shard count (1 .. 64), as an integer.
 // Measured and removed in round 5 (docs/perf_notes.md "where the fp32 same-stream gap comes
 // from"): reload-delta stores, SC1 DMA loads, write-through (device-scope) stores, agent / system
 // acquires, a coherent re-read, 512-thread and one-block-per-CU launches, one table replica per

@@ -342,6 +342,139 @@ __global__ __launch_bounds__(256) void bpr_pf_kernel(MFParams P, const int32_t* 
     }
 }
 
+// Three-stage software pipeline (default with device sampling and the bitmap).
+// bpr_pf_kernel still waits per triple on the next draw's dependent rejection load (u from
+// pos_user, then the bitmap word of (u, j)) and on its own factor gathers.  Here every triple's
+// work is split across three loop iterations of its wave:
+//   D1 (iteration q - 3 ... issued): the PCG draw (pure arithmetic: positive index, first negative
+//      candidate j0) and the loads of u, i;
+//   D2 (q - 2): the bitmap word of (u, j0);
+//   G  (q - 1): the rejection test (a positive j0 falls back to bpr_draw's serial loop over the
+//      following candidates: same PCG stream, so the triples are exactly bpr_kernel's) and the
+//      factor / bias gathers;
+//   C  (q):     dot product, loss, SGD stores.
+// Each iteration issues D1 of triple q + 3, D2 of q + 2, G of q + 1 in that order and then
+// computes q, so every wait is on loads issued one iteration earlier.  The gathers of q + 1 are
+// issued before q's stores: if the two triples share a user or item row (a wave's consecutive
+// triples are a whole grid's stride apart in the stream), q + 1 reads it one update stale.
+struct Draw { uint64_t s; int u, i, j0; };
+
+__device__ __forceinline__ Draw bpr_d1(const MFParams& P, int64_t r, int64_t n, int64_t t0,
+                                       const int32_t* __restrict__ tu, const int32_t* __restrict__ ti,
+                                       const int32_t* __restrict__ tj, const int32_t* __restrict__ uitems,
+                                       const int32_t* __restrict__ pos_user, int64_t n_pos) {
+    Draw d{0ull, -1, -1, -1};
+    if (r >= n) return d;
+    if (tu) { d.u = tu[r]; d.i = ti[r]; d.j0 = tj[r]; return d; }
+    uint64_t s = ((uint64_t)P.seed << 32) ^ (uint64_t)(t0 + r) * 0x9E3779B97F4A7C15ull;
+    pcg(s);
+    const uint64_t pidx = ((uint64_t)pcg(s) << 32 | pcg(s)) % (uint64_t)n_pos;
+    d.u = pos_user[pidx];
+    d.i = uitems[pidx];
+    d.j0 = P.max_tries > 0 ? (int)(pcg(s) % (uint32_t)P.n_items) : -1;
+    d.s = s;
+    return d;
+}
+
+__device__ __forceinline__ uint32_t bpr_d2(const MFParams& P, const Draw& d, const uint32_t* __restrict__ bitmap,
+                                           bool sampled) {
+    if (!sampled || d.u < 0 || d.u >= P.n_users || d.j0 < 0) return 0u;
+    return bitmap[(size_t)d.u * P.bm_words + (d.j0 >> 5)];
+}
+
+__device__ __forceinline__ Trip bpr_resolve(const MFParams& P, Draw d, uint32_t word,
+                                            const uint32_t* __restrict__ bitmap, bool sampled) {
+    Trip t{d.u, d.i, d.j0};
+    if (!sampled || d.u < 0) return t;
+    if (d.u >= P.n_users) { t.j = -1; return t; }
+    if (d.j0 >= 0 && !((word >> (d.j0 & 31)) & 1u)) return t;
+    t.j = -1;                                   // j0 is a positive: the serial rejection loop
+    uint64_t s = d.s;
+    for (int tries = 1; tries < P.max_tries; ++tries) {
+        const int j = (int)(pcg(s) % (uint32_t)P.n_items);
+        if (!((bitmap[(size_t)d.u * P.bm_words + (j >> 5)] >> (j & 31)) & 1u)) { t.j = j; break; }
+    }
+    return t;
+}
+
+struct Gath { float pu, qi, qj, bi, bj; };
+
+template <int G>
+__global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t* __restrict__ tu,
+                                                      const int32_t* __restrict__ ti,
+                                                      const int32_t* __restrict__ tj, int64_t n,
+                                                      const int32_t* __restrict__ uitems,
+                                                      const int32_t* __restrict__ pos_user,
+                                                      int64_t n_pos, int64_t t0,
+                                                      const uint32_t* __restrict__ bitmap,
+                                                      float* __restrict__ Pu, float* __restrict__ Qi,
+                                                      float* __restrict__ Bi, double* __restrict__ loss_sum) {
+    constexpr int PER = 64 / G;
+    const int lane = hm::lane_id();
+    const int sub = lane / G, f = lane % G;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int64_t stride = nwaves * PER;
+    const bool sampled = tu == nullptr;
+    double lacc = 0.0;
+    auto valid = [&](int64_t r, const Trip& t) {
+        return r < n && t.u >= 0 && t.u < P.n_users && t.i >= 0 && t.i < P.n_items && t.j >= 0 &&
+               t.j < P.n_items && t.i != t.j;
+    };
+    auto gather = [&](int64_t r, const Trip& t) -> Gath {
+        Gath g{0.f, 0.f, 0.f, 0.f, 0.f};
+        const bool ok = valid(r, t);
+        if (ok && f < P.k) {
+            g.pu = ldm(P, Pu + (size_t)t.u * P.kp + f);
+            g.qi = ldm(P, Qi + (size_t)t.i * P.kp + f);
+            g.qj = ldm(P, Qi + (size_t)t.j * P.kp + f);
+        }
+        if (ok && P.use_bias) { g.bi = ldm(P, Bi + t.i); g.bj = ldm(P, Bi + t.j); }
+        return g;
+    };
+    const int64_t r0 = wave * PER + sub;
+    // prologue: triple r0 resolved and gathered, r0 + stride's bitmap word and r0 + 2 stride's u / i in flight
+    Draw da = bpr_d1(P, r0, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
+    Draw db = bpr_d1(P, r0 + stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
+    Trip ta = bpr_resolve(P, da, bpr_d2(P, da, bitmap, sampled), bitmap, sampled);
+    Gath ga = gather(r0, ta);
+    uint32_t wb = bpr_d2(P, db, bitmap, sampled);
+    Draw dc = bpr_d1(P, r0 + 2 * stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
+    for (int64_t base = wave * PER; base < n; base += stride) {
+        const int64_t r = base + sub;
+        // ---- issue: D1 of r + 3 stride, D2 of r + 2 stride, G of r + stride ----
+        const Draw dn = bpr_d1(P, r + 3 * stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
+        const uint32_t wc = bpr_d2(P, dc, bitmap, sampled);
+        const Trip tb = bpr_resolve(P, db, wb, bitmap, sampled);
+        const Gath gb = gather(r + stride, tb);
+        // ---- compute triple r ----
+        const bool ok = valid(r, ta);
+        const float d = group_sum<G>(ga.pu * (ga.qi - ga.qj));
+        const float x = ga.bi - ga.bj + d;
+        float z;
+        if (P.loss == 2) { const float sg = hm::sigmoidf_(x); z = sg * (1.f - sg); }
+        else z = 1.f / (1.f + __expf(x));
+        if (ok && f == 0) lacc += (double)hm::log1pexp(-x);
+        if (ok) {
+            const float eta = eta_t(P, (float)(t0 + r + 1));
+            if (f < P.k) {
+                Pu[(size_t)ta.u * P.kp + f] = ga.pu + eta * (z * (ga.qi - ga.qj) - P.lambda_u * ga.pu);
+                Qi[(size_t)ta.i * P.kp + f] = ga.qi + eta * (z * ga.pu - P.lambda_i * ga.qi);
+                Qi[(size_t)ta.j * P.kp + f] = ga.qj + eta * (-z * ga.pu - P.lambda_j * ga.qj);
+            }
+            if (P.use_bias && f == 0) {
+                Bi[ta.i] = ga.bi + eta * (z - P.lambda_b * ga.bi);
+                Bi[ta.j] = ga.bj + eta * (-z - P.lambda_b * ga.bj);
+            }
+        }
+        ta = tb; ga = gb; db = dc; wb = wc; dc = dn;
+    }
+    if (loss_sum) {
+        lacc = hm::wave_sum(lacc);
+        if (lane == 0 && lacc != 0.0) atomicAdd(loss_sum, lacc);
+    }
+}
+
 // bitmap[u * words + (i >> 5)] |= 1 << (i & 31) for every positive pair (user-sorted CSR)
 __global__ void bpr_bitmap_kernel(const int32_t* __restrict__ users, const int32_t* __restrict__ items,
                                   int64_t n, int words, uint32_t* __restrict__ bitmap) {
@@ -405,7 +538,8 @@ HM_API int hm_mf_step(const int32_t* ip, const float* hp, const int32_t* users,
     HM_LAUNCH_RET();
 }
 
-// ip[15]: 1 = bpr_kernel (the binary-search sampler, no lookahead), else bpr_pf_kernel.
+// ip[15]: 1 = bpr_kernel (the binary-search sampler, no lookahead), 2 = bpr_pf_kernel, else
+// bpr_pf3_kernel (bpr_pf_kernel when sampling without the bitmap).
 // bitmap: the positive-item bitmap of hm_bpr_bitmap (device sampling), or null.
 HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, const int32_t* ti,
                        const int32_t* tj, int64_t n, const int64_t* uptr, const int32_t* uitems,
@@ -421,9 +555,13 @@ HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, co
     if (variant == 1)                                                                              \
         hipLaunchKernelGGL((bpr_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, tu, \
                            ti, tj, n, uptr, uitems, pos_user, n_pos, t0, Pu, Qi, Bi, loss_sum);      \
-    else                                                                                           \
+    else if (variant == 2 || (!tu && !bitmap))                                                     \
         hipLaunchKernelGGL((bpr_pf_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, \
                            tu, ti, tj, n, uptr, uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap,  \
+                           Pu, Qi, Bi, loss_sum);                                                    \
+    else                                                                                           \
+        hipLaunchKernelGGL((bpr_pf3_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, \
+                           tu, ti, tj, n, uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap,        \
                            Pu, Qi, Bi, loss_sum)
     if (P.k <= 8) HM_BPR(8);
     else if (P.k <= 16) HM_BPR(16);

@@ -101,10 +101,28 @@ __device__ __forceinline__ void stx(void* p, int64_t e, float4 v) {
     }
 }
 
-// MODE 0 (pack):  out[q] = x[view(q)]
-// MODE 1 (merge): x[view(q)] += mean[q] - snap[q]; when out != nullptr also out[q] = the new x
-//                 (merge of the finished mix fused with the snapshot of the next one; out may
-//                 alias snap: each quad is read before it is written by the same thread)
+// Quad q of a [n0][d1][inner] view -> its element offset in x.  The divisions are 32-bit while
+// the view has fewer than 2^31 quads (every FFM table below 2^23 features): 64-bit integer division
+// is a ~40-instruction software sequence per quad.
+__device__ __forceinline__ int64_t view3_elem(int64_t q, int64_t per0, int qps, int64_t s0, int64_t s1, bool small) {
+    if (small) {
+        const uint32_t uq = (uint32_t)q, up = (uint32_t)per0;
+        const uint32_t i0 = uq / up, rem = uq - i0 * up;
+        const uint32_t i1 = rem / (uint32_t)qps, c = (rem - i1 * (uint32_t)qps) * 4u;
+        return (int64_t)i0 * s0 + (int64_t)i1 * s1 + c;
+    }
+    const int64_t i0 = q / per0;
+    const int64_t rem = q - i0 * per0;
+    const int64_t i1 = rem / qps;
+    const int c = (int)(rem - i1 * qps) * 4;
+    return i0 * s0 + i1 * s1 + c;
+}
+
+// MODE 0 (pack):   out[q] = x[view(q)]
+// MODE 1 (merge):  x[view(q)] += mean[q] - snap[q]; when out != nullptr also out[q] = the new x
+//                  (merge of the finished mix fused with the snapshot of the next one; out may
+//                  alias snap: each quad is read before it is written by the same thread)
+// MODE 2 (unpack): x[view(q)] = mean[q] (the inverse of pack: bit-exact)
 template <int MODE, bool BF, bool ALN>
 __global__ __launch_bounds__(256) void view3_kernel(void* __restrict__ x, const void* __restrict__ mean,
                                                     const void* snap, void* out, int64_t n0, int d1,
@@ -112,12 +130,13 @@ __global__ __launch_bounds__(256) void view3_kernel(void* __restrict__ x, const 
     const int qps = inner >> 2;
     const int64_t per0 = (int64_t)d1 * qps;
     const int64_t nq = n0 * per0;
+    const bool small = nq < ((int64_t)1 << 31);
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
-        const int64_t i0 = q / per0;
-        const int64_t rem = q - i0 * per0;
-        const int64_t i1 = rem / qps;
-        const int c = (int)(rem - i1 * qps) * 4;
-        const int64_t xe = i0 * s0 + i1 * s1 + c, qe = 4 * q;
+        const int64_t xe = view3_elem(q, per0, qps, s0, s1, small), qe = 4 * q;
+        if constexpr (MODE == 2) {
+            stx<BF, ALN>(x, xe, ld4<BF>(mean, qe));
+            continue;
+        }
         float4 a = ldx<BF, ALN>(x, xe);
         if constexpr (MODE == 1) {
             const float4 m = ld4<BF>(mean, qe), sn = ld4<BF>(snap, qe);
@@ -157,12 +176,9 @@ __global__ __launch_bounds__(256) void delta3_kernel(void* __restrict__ x, float
     const int qps = inner >> 2;
     const int64_t per0 = (int64_t)d1 * qps;
     const int64_t nq = n0 * per0;
+    const bool small = nq < ((int64_t)1 << 31);
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
-        const int64_t i0 = q / per0;
-        const int64_t rem = q - i0 * per0;
-        const int64_t i1 = rem / qps;
-        const int c = (int)(rem - i1 * qps) * 4;
-        const int64_t xe = i0 * s0 + i1 * s1 + c, qe = 4 * q;
+        const int64_t xe = view3_elem(q, per0, qps, s0, s1, small), qe = 4 * q;
         float4 b = *reinterpret_cast<const float4*>(base + qe);
         if constexpr (MODE == 2) {
             const float4 a = ldx<XBF, ALN>(x, xe);
@@ -251,6 +267,12 @@ int launch_view3(void* x, const void* mean, const void* snap, void* out, int64_t
 HM_API int hm_mix_pack3(const void* x, void* out, int64_t n0, int d1, int inner, int64_t s0, int64_t s1,
                         int dtype, hipStream_t stream) {
     return launch_view3<0>(const_cast<void*>(x), nullptr, nullptr, out, n0, d1, inner, s0, s1, dtype, stream);
+}
+
+// x <- mean over the view (mean contiguous n0*d1*inner; bit-exact inverse of hm_mix_pack3).
+HM_API int hm_mix_unpack3(void* x, const void* mean, int64_t n0, int d1, int inner, int64_t s0, int64_t s1,
+                          int dtype, hipStream_t stream) {
+    return launch_view3<2>(x, mean, nullptr, nullptr, n0, d1, inner, s0, s1, dtype, stream);
 }
 
 // x += mean - snap over the view; out (nullable, may alias snap) <- the merged x.

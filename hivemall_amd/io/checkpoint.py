@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 _SCALARS = ("t", "rows_seen", "num_features", "num_fields", "dims", "n_users", "n_items", "labels",
-            "classes", "k", "kp", "grid", "K")
+            "classes", "k", "kp", "grid", "K", "dp_power", "dp_guard_tripped")
 
 
 def _collect_tensors(learner) -> dict:

@@ -184,6 +184,16 @@ class FFMTrainer(Learner):
         self.atomic_rows = RAMP_ROWS if c["atomic_rows"] is None else max(0, int(c["atomic_rows"]))
         self.dp_guard_tripped = False
 
+    @property
+    def dp_power(self) -> float:
+        """The step rule's effective power p (eta0 * N^p), after any divergence-guard fallback;
+        a checkpoint scalar (io/checkpoint.py), so a resumed run keeps the fallback."""
+        return self._dp_power
+
+    @dp_power.setter
+    def dp_power(self, power: float) -> None:
+        self._set_dp_power(float(power))
+
     def _set_dp_power(self, power: float) -> None:
         sc = dp_lr_scale(self.mixer.world, power) if self._dp() else 1.0
         self.hyper.eta0 = self._base_eta0 * sc

@@ -20,7 +20,7 @@ import numpy as np
 import pandas as pd
 import torch
 
-from ..ops.fm import FMHyper, fm_step, new_state_tables
+from ..ops.fm import FMHyper, fm_step, hot_flags, new_state_tables
 from ..ops.touched import mark_touched
 
 # global-bias shards on the GPU (see ops/fm.py): one same-address atomic per row capped train_fm
@@ -210,6 +210,8 @@ class FMTrainer(Learner):
         self._ensure(rows)
         bs = int(self.cl["batch_size"])
         n = rows.n
+        # hot features of this pass: their stores go out write-through (ops/fm.py HOT_FRAC)
+        self._hot = hot_flags(self.state, rows.idx, n, buf=getattr(self, "_hot", None))
         for k in range(self.dp_batches(n, bs)):
             s = min(n, k * bs)
             e = min(n, s + bs)
@@ -217,7 +219,7 @@ class FMTrainer(Learner):
             lb = None if loss_buf is None else loss_buf[s:e]
             if e > s:
                 fm_step(self.state, ip, rows.idx, rows.val, rows.y[s:e], self.h, self.k, train=True,
-                        t0=self.t, loss=lb, grid=self.grid)
+                        t0=self.t, loss=lb, grid=self.grid, hot=self._hot)
             self.t += e - s
             mi = int(self.cl["mix_interval"])
             if mi > 0 and self._dp():

@@ -68,9 +68,10 @@ LEARNER_BASE_OPTS = [
         "[engine] shared engine: model tables (1, or a multiple of 8: one set per XCD), averaged "
         "after every pass"),
     opt("shared_waves", None, 0, int,
-        "[engine] shared engine: rows in flight (0 = auto per rule, ops/linear.py rule_waves: "
-        "1024 AdaGrad / AdaGrad-RDA, 512 AdaGrad-L1 / elastic net, 8 for the other "
-        "general-learner rules, whose parity with the sequential learner needs it)"),
+        "[engine] shared / seq engine: rows in flight (0 = auto per rule: ops/linear.py "
+        "rule_waves for the shared engine — 1024 AdaGrad / AdaGrad-RDA, 512 AdaGrad-L1 / elastic "
+        "net; seq_waves for the seq engine, which auto picks for the other general-learner "
+        "rules — 512 SGD / momentum / RMSprop / AdaDelta, 256 Adam / NAdam / AdamHD, 128 Eve)"),
 ] + CKPT_OPTS
 
 GENERAL_OPTS = [
@@ -368,7 +369,7 @@ class OnlineLinearLearner(Learner):
                 self.load_model_table(self._warm)
             return
         if self._use_seq(L, mb):
-            W = int(self.cl["shared_waves"]) or LO.SEQ_ENGINE_WAVES
+            W = int(self.cl["shared_waves"]) or LO.seq_waves(self.P)
             if int(self.cl["seq_spread"]) not in (1, 8):
                 raise UDFArgumentException(f"{self.NAME}: -seq_spread must be 1 or 8")
             self.state = LO.new_seq_state(dims, self.device, max(1, min(W, max(1, rows.n))),
@@ -379,6 +380,11 @@ class OnlineLinearLearner(Learner):
         if self._use_shared(R, L, dims, mb):
             try:
                 W = LO.shared_waves(rows.n, int(self.cl["shared_waves"]) or LO.rule_waves(self.P))
+                if W <= 16 and rows.n > 64 * W:
+                    log.warning("%s: the shared-table engine runs this rule with %d rows in flight "
+                                "(~%d M rows/s on one MI355X); -engine seq keeps the rows in flight "
+                                "on one XCD at 128-512 rows (ops/linear.py seq_waves)",
+                                self.NAME, W, max(1, W // 4))
                 # at a few rows in flight the read-modify-write window is no hazard: skip the
                 # state re-read before the update (+5 % at 8 rows, same parity:
                 # profiles/r4/linear_reload_ab_8rows.jsonl)

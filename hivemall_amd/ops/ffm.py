@@ -188,7 +188,7 @@ def new_state_tables(num_features: int, num_fields: int, kp: int, dtype, device,
             torch.zeros(shape, dtype=dtype, device=device))
 
 
-_DEFER: dict = {}   # device -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
+_DEFER: dict = {}   # (device, stream) -> int32 [1 + B] deferral buffer of multi-hot rows (csrc hm_ffm_step)
 # Global-bias FTRL state sharded over this many 128-B lines during a training launch (csrc/kernels/
 # ffm.hip FFMParams.bias_sh): one same-address pair of atomics per row held -w0 runs at 5.5 M
 # rows/s (profiles/r5/ffm_w0_rate.jsonl).  HM_FFM_BIAS_SHARDS=0: the single address (A/B only).
@@ -200,11 +200,19 @@ BIAS_EVERY = int(os.environ.get("HM_FFM_BIAS_EVERY", "32"))
 _BIAS_SH: dict = {}
 
 
+def _launch_key(device: torch.device):
+    """Scratch buffers (_DEFER, _BIAS_SH) are per (device, stream): two learners training on one
+    device from different streams must not share a deferral counter or bias shards (launches on
+    ONE stream are ordered, so they may)."""
+    return (device, _native.stream_of(device))
+
+
 def _bias_shards(device: torch.device) -> torch.Tensor:
-    sh = _BIAS_SH.get(device)
+    key = _launch_key(device)
+    sh = _BIAS_SH.get(key)
     if sh is None or sh.shape[0] != BIAS_SHARDS:
         sh = torch.zeros((BIAS_SHARDS, 32), dtype=torch.float32, device=device)
-        _BIAS_SH[device] = sh
+        _BIAS_SH[key] = sh
     return sh
 # HM_FFM_DEFER=0 (A/B only): no multi-hot detection in the pipelined kernels (a row with a
 # repeated field or feature is then updated slot by slot: racing stores of one address)
@@ -215,11 +223,31 @@ _LIN_DEFER = int(os.environ.get("HM_FFM_LIN_DEFER", "1") != "0")
 
 
 def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
-    buf = _DEFER.get(device)
+    key = _launch_key(device)
+    buf = _DEFER.get(key)
     if buf is None or buf.numel() < 1 + B:
         buf = torch.empty(1 + max(B, 1 << 16), dtype=torch.int32, device=device)
-        _DEFER[device] = buf
+        _DEFER[key] = buf
     return buf
+
+
+def _has_multihot(idx: torch.Tensor, fld: torch.Tensor | None) -> bool:
+    """Any row with a repeated feature or a repeated field (padding / invalid ids excluded)."""
+    if idx.numel() == 0 or idx.shape[1] < 2:
+        return False
+    big = torch.iinfo(torch.int32).max
+    pos = torch.arange(idx.shape[1], device=idx.device, dtype=torch.int32)
+
+    def rep(t: torch.Tensor, valid: torch.Tensor) -> bool:
+        # invalid entries get distinct sentinels, so they never compare equal
+        u = torch.where(valid, t, big - pos.unsqueeze(0))
+        s = u.sort(dim=1).values
+        return bool((s[:, 1:] == s[:, :-1]).any().item())
+
+    valid = idx >= 0
+    if rep(idx, valid):
+        return True
+    return fld is not None and rep(fld, valid & (fld >= 0))
 
 
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
@@ -250,6 +278,11 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
         assert pred.shape[0] >= B
     if loss is not None:
         assert loss.shape[0] >= B
+    if V.is_cuda and train and int(grid) == 1 and variant is None and _VARIANT == 0 and _has_multihot(idx, fld):
+        # one block is documented as the sequential learner: a multi-hot row would be deferred by
+        # the pipelined kernels until after the batch's other rows, so the whole launch
+        # goes to the generic kernel, which trains every row in order with grouped updates
+        variant = 1
     G = state["G"]
     bf16 = V.dtype == torch.bfloat16
     slot_g = G.dim() == 2

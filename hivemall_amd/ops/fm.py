@@ -84,9 +84,45 @@ def new_state_tables(dims: int, KP: int, dtype: torch.dtype, device) -> tuple:
     return w, V
 
 
+# Hot features' stores go out write-through (csrc/kernels/fm.hip P.hot): the per-XCD L2s are not
+# coherent, and with plain stores each XCD kept training its own copy of the hottest lines.  Every
+# store write-through (A/B variant 2) moved the grid-256 held-out gap vs Hivemall's 8-mapper average
+# from +3.1e-3 .. +3.7e-3 to -3.2e-3 .. -3.1e-3 (one learner over all rows loses nothing) at 0.4x
+# the rate (profiles/r6/fm_wt_parity.jsonl); a feature in at least HOT_FRAC of a batch's rows
+# (sampled) is hot.  HM_FM_HOT_WT=0: plain stores everywhere (A/B).
+HOT_FRAC = float(os.environ.get("HM_FM_HOT_FRAC", "0"))
+# a hot feature's store goes out write-through on one row in HOT_EVERY (a power of two; per-row
+# hash): the line is dropped from the writer's L2 that often, which bounds how many of its own
+# XCD's updates a stale copy can absorb while the memory side serialises 1 / HOT_EVERY of them
+HOT_EVERY = int(os.environ.get("HM_FM_HOT_EVERY", "1"))
+HOT_WT = os.environ.get("HM_FM_HOT_WT", "1") != "0"
+
+
+def hot_flags(state: dict, idx: torch.Tensor, n_rows: int, frac: float = None,
+              buf: torch.Tensor | None = None) -> torch.Tensor | None:
+    """uint8 [dims] flags of the features in >= ``frac`` of the rows, from a strided sample of the
+    indices (written into ``buf`` when it fits, else a new tensor)."""
+    V = state["V"]
+    dims = V.shape[0]
+    frac = HOT_FRAC if frac is None else frac
+    if not (HOT_WT and V.is_cuda) or n_rows <= 0 or idx.numel() == 0 or frac <= 0:
+        return None
+    stride = 17 if idx.numel() >= (1 << 20) else 1     # prime: every field position is sampled
+    ids = idx[::stride]
+    ids = ids[(ids >= 0) & (ids < dims)].long()
+    cnt = torch.bincount(ids, minlength=dims)
+    thr = max(2.0, frac * n_rows / stride)
+    hot = buf
+    if hot is None or hot.numel() != dims or hot.device != V.device:
+        hot = torch.zeros(dims, dtype=torch.uint8, device=V.device)
+    torch.ge(cnt, thr, out=hot.view(torch.bool))
+    return hot
+
+
 def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor | None,
             y: torch.Tensor | None, h: FMHyper, k: int, train: bool = True, t0: int = 0,
-            pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0) -> None:
+            pred: torch.Tensor | None = None, loss: torch.Tensor | None = None, grid: int = 0,
+            hot: torch.Tensor | None = None) -> None:
     """One fused pass over CSR rows.  state: w f32 [dims], V bf16|f32 [dims, KP], w0 f32:
     on the GPU the global bias is the SUM of S = numel/32 shards at stride 32 floats (every
     row's update is an atomic add into shard (wave % S) instead of one contended address);
@@ -110,7 +146,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
                    int(os.environ.get("HM_FM_VARIANT", "0")),
                    max(1, min(W0_EVERY_MAX, int(os.environ.get(
                        "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1))))),
-                   V.stride(0), w.stride(0), WPB],
+                   V.stride(0), w.stride(0), WPB, max(1, HOT_EVERY) - 1],
                   dtype=np.int32)
     assert V.stride(1) == 1 and V.stride(0) >= KP, "V rows must be contiguous"
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
@@ -120,7 +156,9 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     args = [ip.ctypes.data, hp.ctypes.data, C.c_int64(n), C.c_int64(t0), p(indptr), p(idx), p(val),
             p(y), p(w), p(V), p(w0), p(pred), p(loss)]
     if dev.type == "cuda":
-        rc = _native.hip().hm_fm_step(*args, _native.stream_of(dev))
+        if hot is not None:
+            assert hot.dtype == torch.uint8 and hot.numel() == dims and hot.device == dev
+        rc = _native.hip().hm_fm_step(*args, p(hot if train else None), _native.stream_of(dev))
         _native.check(rc, "hm_fm_step")
     else:
         assert not bf16, "CPU FM engine keeps V in fp32"
@@ -131,5 +169,5 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
 
 
 _P = _native.c_p
-_native.register_hip("hm_fm_step", [_P, _P, _native.c_i64, _native.c_i64] + [_P] * 9 + [_P])
+_native.register_hip("hm_fm_step", [_P, _P, _native.c_i64, _native.c_i64] + [_P] * 10 + [_P])
 _native.register_host("hm_fm_step_cpu", [_P, _P, _native.c_i64, _native.c_i64] + [_P] * 9)

@@ -225,17 +225,35 @@ def hot_owner_rule(P: LinParams) -> bool:
 SEQ_WAVES = 8
 
 
-# Rows in flight of the near-sequential engine (linear_seq_kernel, ``-engine seq``) by default.
-SEQ_ENGINE_WAVES = 32
+# Near-sequential engine (linear_seq_kernel, ``-engine seq``; round 6): W consecutive rows in
+# flight, all on ONE XCD.  Held-out logloss minus the sequential CPU engine's after one epoch of
+# 1 M Criteo-shaped rows at -dims 2^24, seeds 5 / 11 / 23 (profiles/r6/linear_seq_*.jsonl):
+#   on one XCD, 512 rows: SGD / momentum / Nesterov / RMSprop(-Graves) / AdaDelta -1.8e-3 ..
+#     +1.5e-3 (one AdaDelta run -3.3e-3, i.e. better than sequential) at 120-130 M rows/s;
+#     Adam +0.7e-3 .. +2.7e-3 at 84 M; at 256 rows Adam -0.3e-3 .. +1.4e-3 at 53 M;
+#   the same rows dealt over all 8 XCDs: +3e-3 .. +6e-3 at any W from 8 to 128 — the per-XCD
+#     L2s are not coherent, so an XCD keeps reading its own copy of a hot feature's line;
+#   AdaGrad (+0.5e-2 .. +2e-2) stays on the shared engine's hot-feature sums.
+SEQ_ENGINE_WAVES = 512
+_SEQ_WAVES_BY_OPT = {"adam": 256, "nadam": 256, "adam_hd": 256, "eve": 128}
 # HM_LINEAR_SEQ=0: the rules of seq_rule stay on the shared engine at SEQ_WAVES rows in flight
-_SEQ_AUTO = os.environ.get("HM_LINEAR_SEQ", "0") != "0"
+_SEQ_AUTO = os.environ.get("HM_LINEAR_SEQ", "1") != "0"
 
 
 def seq_rule(P: LinParams) -> bool:
     """Rules routed to the near-sequential engine by ``-engine auto``: the general learner's
-    rules that neither pre-aggregate (hot_rule) nor own (hot_owner_rule) their hot features."""
+    rules that neither pre-aggregate (hot_rule) nor own (hot_owner_rule) their hot features,
+    i.e. every optimizer but AdaGrad."""
     return (_SEQ_AUTO and P.algo == ALGOS["general"] and P.n_labels == 1 and not hot_rule(P)
-            and not hot_owner_rule(P))
+            and not hot_owner_rule(P) and P.opt != OPTIMIZERS["adagrad"])
+
+
+def seq_waves(P: LinParams) -> int:
+    """Default rows in flight of the near-sequential engine for the rule (table above)."""
+    for name, w in _SEQ_WAVES_BY_OPT.items():
+        if P.opt == OPTIMIZERS[name]:
+            return w
+    return SEQ_ENGINE_WAVES
 
 
 def rule_waves(P: LinParams) -> int:

@@ -52,6 +52,8 @@ _native.register_hip("hm_mix_pack3", [_native.c_p, _native.c_p, _native.c_i64, _
 _native.register_hip("hm_mix_merge3", [_native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_i64,
                                        _native.c_int, _native.c_int, _native.c_i64, _native.c_i64, _native.c_int,
                                        _native.c_p])
+_native.register_hip("hm_mix_unpack3", [_native.c_p, _native.c_p, _native.c_i64, _native.c_int, _native.c_int,
+                                        _native.c_i64, _native.c_i64, _native.c_int, _native.c_p])
 _native.register_hip("hm_mix_merge", [_native.c_p, _native.c_p, _native.c_p, _native.c_i64,
                                       _native.c_int, _native.c_i64, _native.c_int, _native.c_p])
 _native.register_hip("hm_mix_delta3", [_native.c_p, _native.c_p, _native.c_p, _native.c_p, _native.c_i64,
@@ -172,8 +174,9 @@ class _FlatGroup:
                 d.copy_(t)
 
     def unpack(self) -> None:
-        for k, t in enumerate(self.tensors):
-            t.copy_(self.seg(self.out, k))
+        """x <- out for every tensor (fused view kernel where the view allows, bit-exact)."""
+        ts = self.tensors
+        self.merge_rows([(k, 0, self.rows_of(k, t)[0]) for k, t in enumerate(ts) if t.numel()], delta=False)
 
     def _delta3(self, k: int, t: torch.Tensor, mode: int) -> bool:
         """One fused delta pass over tensor k (hm_mix_delta3); False when it does not apply."""
@@ -283,7 +286,14 @@ class _FlatGroup:
                 b.add_(m.to(torch.float32))
                 x.copy_(b.view(x.shape))
             else:
-                x.copy_(m.view(x.shape))
+                code = _dtype_code(self.dtype)
+                v3 = _view3(x) if x.is_cuda and code is not None and x.dtype == self.dtype else None
+                if v3 is not None:
+                    rc = _native.hip().hm_mix_unpack3(x.data_ptr(), m.data_ptr(), *v3, code,
+                                                      _native.stream_of(x.device))
+                    _native.check(rc, "hm_mix_unpack3")
+                else:
+                    x.copy_(m.view(x.shape))
 
     def _delta3_rows(self, k: int, t: torch.Tensor, mode: int, ra: int, rb: int, rl: int) -> bool:
         xc, wc = _dtype_code(t.dtype), _dtype_code(self.dtype)
@@ -458,9 +468,11 @@ class ModelMixer:
     def _gather(self, g: _FlatGroup, async_op: bool = False):
         return dist.all_gather_into_tensor(g.out, g.mean, async_op=async_op)
 
-    # wire bytes per bucket of the pipelined shard mean (SURVEY.md:739-742: 32-128 MB buckets);
+    # wire bytes per bucket of the pipelined shard mean (SURVEY.md:739-742: 32-128 MB buckets; on
+    # one card, where the collectives are device copies, 64 MB cost 1.81 vs 1.68 ms monolithic per
+    # fp32 delta mix and 32 MB 2.08: per-bucket launches, profiles/r6/mix_pipe_probe.jsonl);
     # 0 = one monolithic collective pair per dtype group (A/B, tests)
-    PIPE_BUCKET_MB = 32.0
+    PIPE_BUCKET_MB = 64.0
 
     def _pipelined(self, g: _FlatGroup, delta: bool) -> None:
         """Bucketed, software-pipelined shard mean of one flat group: bucket b+1's pack (compute

@@ -317,6 +317,46 @@ def test_ffm_gpu_single_block_is_exactly_sequential(adagrad, k):
 
 
 @pytest.mark.gpu
+def test_ffm_gpu_single_block_multihot_rows_train_in_order():
+    """with -grid 1 (one block = the sequential learner) a batch holding multi-hot rows
+    (hashed collisions at 2^12 ids: many rows repeat a feature) is trained in row order by the
+    generic kernel instead of deferring those rows to after the batch, so it equals the CPU
+    engine on exactly the rows the pipelined-kernel exactness test has to avoid."""
+    from hivemall_amd.models import ffm as ffm_model
+    from hivemall_amd.ops import ffm as ffm_op
+
+    idx, y = criteo_like(6000, hash_bits=12, seed=5)
+    eidx, ey = criteo_like(3000, hash_bits=12, seed=99)
+    assert ffm_op._has_multihot(idx, None)
+    yy = (ey > 0).float()
+    res = {}
+    old = ffm_model.RAMP_ROWS
+    ffm_model.RAMP_ROWS = 0
+    try:
+        for dev in ("cpu", "cuda"):
+            t = FFMTrainer("-classification -factors 4 -num_fields 39 -feature_hashing 12 -seed 1", device=dev)
+            t.grid = 1
+            t.fit(batch=FFMBatch(idx, None, None, y).to(dev))
+            p = t.predict_raw(batch=FFMBatch(eidx, None, None, None).to(dev)).cpu()
+            res[dev] = torch.nn.functional.binary_cross_entropy_with_logits(p, yy).item()
+    finally:
+        ffm_model.RAMP_ROWS = old
+    assert abs(res["cpu"] - res["cuda"]) < 1e-4, res
+
+
+def test_ffm_multihot_detection():
+    from hivemall_amd.ops.ffm import _has_multihot
+
+    idx = torch.tensor([[1, 2, 3], [4, 5, 6]], dtype=torch.int32)
+    assert not _has_multihot(idx, None)
+    assert _has_multihot(torch.tensor([[1, 2, 1]], dtype=torch.int32), None)
+    assert not _has_multihot(torch.tensor([[1, -1, -1]], dtype=torch.int32), None)   # padding
+    fld = torch.tensor([[0, 1, 2], [0, 0, 1]], dtype=torch.int32)
+    assert _has_multihot(idx, fld)
+    assert not _has_multihot(idx, fld[:1].repeat(2, 1))
+
+
+@pytest.mark.gpu
 def test_ffm_gpu_global_bias_loses_no_updates():
     """-w0: every block updates the one global bias; its FTRL state (z0, n0) is accumulated
     atomically, so n0 = sum over rows of the squared row gradient |kappa| = 1 - exp(-loss)
