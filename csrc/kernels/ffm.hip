@@ -1062,7 +1062,12 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // KV = 16-B quads per slot: 1 for k <= 4 (the 896-B blocks above), 2 for k <= 8 (32-B V slots,
 // 1,536-B blocks; the landing zone and the image double, 107 KB of LDS at 39 fields: one block
 // per CU, launched with 512 threads so that each SIMD still holds two waves).
-template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1>
+// KEEP = 1 (round 6): each slot's offsets, x_a x_b and live / written / repeat bits are derived
+// from the row metadata ONCE, in phase C (next to that row's DMA issue), and kept in registers
+// for the row's B / D / E phases; the other phases re-read both metadata entries of every slot from
+// LDS, and the (b)-side reads of 16-B entries conflict where b wraps from F - 1 to 0 inside a
+// 16-lane group (2.7 extra LDS cycles per such read at F = 39, profiles/r6/lds_conflict_model.txt).
+template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1, int KEEP = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1137,17 +1142,39 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
+    // KEEP: the slot data of the row whose DMA was issued last (nov / nog / nxab / bits), handed to
+    // the current-row registers (kov / kog / kxab / bits) at the end of each row
+    OT kov[KEEP ? NS : 1], kog[KEEP ? NS : 1], nov[KEEP ? NS : 1], nog[KEEP ? NS : 1];
+    float kxab[KEEP ? NS : 1], nxab[KEEP ? NS : 1];
+    uint32_t klive = 0u, kwr = 0u, nlive = 0u, nwr = 0u;
+    int krep = 0, nrep = 0;
     auto dma_slots = [&](int bf) {
+        if constexpr (KEEP) { nlive = 0u; nwr = 0u; nrep = 0; }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT ov, og;
             float xab;
-            slot(bf, j, ov, og, xab);
+            const uint32_t k = slot(bf, j, ov, og, xab);
+            if constexpr (KEEP) {
+                nov[j] = ov;
+                nog[j] = og;
+                nxab[j] = xab;
+                nlive |= (k & 1u) << j;
+                nwr |= (uint32_t)(k != 0u) << j;
+                if (P.defer) nrep |= (int)slot_repeats(SA(j), SB(j), s_m[bf][SA(j)], s_m[bf][SB(j)]);
+            }
 #pragma unroll
             for (int q = 0; q < KV; ++q)
                 __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + ov + 16u * q),
                                                  (lds_ptr_t)(s_rv + (q * NS + j) * TPB + wave * 64), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(gb + og), (lds_ptr_t)(s_rg + j * TPB + wave * 64), 4, 0, 0);
+        }
+    };
+    auto keep_rotate = [&]() {
+        if constexpr (KEEP) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) { kov[j] = nov[j]; kog[j] = nog[j]; kxab[j] = nxab[j]; }
+            klive = nlive; kwr = nwr; krep = nrep;
         }
     };
     // The linear state of the next row is DMA'd after this row's FTRL stores (phase F), so it is
@@ -1180,6 +1207,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     publish_meta(0);
     bar_raw();
     dma_slots(0);
+    keep_rotate();
     dma_lin(0);
     dma_meta(1, row + G);
 
@@ -1228,9 +1256,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 #pragma unroll
             for (int q = 0; q < KV; ++q) v[q] = s_rv[(q * NS + j) * TPB + tid];
             if (fwd >> j & 1u) {
-                OT ov, og;
-                float xq;
-                if (slot(cur, j, ov, og, xq) != 0u && ov == fo[j]) {
+                bool same;
+                if constexpr (KEEP) {
+                    same = (kwr >> j & 1u) && kov[j] == fo[j];
+                } else {
+                    OT ov, og;
+                    float xq;
+                    same = slot(cur, j, ov, og, xq) != 0u && ov == fo[j];
+                }
+                if (same) {
 #pragma unroll
                     for (int q = 0; q < KV; ++q) v[q] = fv[j][q];
                     cg[j] = fg[j];
@@ -1268,13 +1302,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         float xab[NS];
         float part = 0.f;
         int rep = 0;
+        if constexpr (KEEP) { live = klive; wr = kwr; rep = krep; }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            OT ov, og;
-            const uint32_t k = slot(cur, j, ov, og, xab[j]);
-            live |= (k & 1u) << j;
-            wr |= (uint32_t)(k != 0u) << j;
-            if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            if constexpr (KEEP) {
+                xab[j] = kxab[j];
+            } else {
+                OT ov, og;
+                const uint32_t k = slot(cur, j, ov, og, xab[j]);
+                live |= (k & 1u) << j;
+                wr |= (uint32_t)(k != 0u) << j;
+                if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            }
             const int s = tid + j * TPB;
             float dot = 0.f;
 #pragma unroll
@@ -1314,8 +1353,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             for (int j = 0; j < NS; ++j) {
                 if (!(wr >> j & 1u)) continue;
                 OT ov, og;
-                float xj;
-                slot(cur, j, ov, og, xj);
+                if constexpr (KEEP) {
+                    ov = kov[j];
+                    og = kog[j];
+                } else {
+                    float xj;
+                    slot(cur, j, ov, og, xj);
+                }
                 const int s = tid + j * TPB;
                 const float c = ks * xab[j];
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
@@ -1396,6 +1440,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
         if (more) dma_lin(nxt);
+        keep_rotate();
         bz = nbz;
         bn = nbn;
         ++bit;
@@ -1794,6 +1839,9 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
         else if (variant == 8 && P.hot) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 2>), dim3(blocks), \
+                                                  dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                  bias, pred, loss); \
+        else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \

@@ -559,3 +559,28 @@ def test_mix_pipelined_buckets_bit_identical_to_monolithic(world):
     for r in range(world):
         assert out[r][0] == [True] * 4, out[r][0]
         assert out[r][1] == out[0][1]                  # every rank bit-identical
+
+
+def test_bench_seq_reference_is_the_cpu_learner_on_the_same_stream():
+    """bench.py's default stream (rows drawn on the CPU) is exactly the one
+    benchmarks/ffm_seq_ref.py replays through the sequential engine: on the CPU, where bench.py's
+    learner IS that engine, its held-out logloss equals the reference (so a GPU run's
+    logloss_gap is the Hogwild / mixing gap alone); and the pinned table answers the driver's
+    configuration."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from benchmarks.ffm_seq_ref import load_refs, ref_key, run
+
+    ref = run(gpus=1, steps=2, warmup=1, batch=512, hash_bits=10, factors=4, resident=2, eval_rows=512)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "512",
+           "--hash-bits", "10", "--eval-rows", "512", "--device", "cpu", "--resident-batches", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["logloss_heldout"] == pytest.approx(ref["logloss_seq"], abs=2e-5), (d["logloss_heldout"], ref)
+    refs = load_refs()
+    for n in (1, 2, 4, 8):
+        assert ref_key(n, 20, 5, 262144, 20, 4, 8, 262144) in refs
+    args = bench.parse_args(["--steps", "20", "--warmup", "5"])
+    assert bench.seq_reference(args, 1) == pytest.approx(0.446395, abs=1e-5)
+    assert bench.seq_reference(bench.parse_args(["--steps", "20", "--warmup", "5", "--gen-device", "auto"]), 1) is None

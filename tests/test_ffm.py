@@ -383,8 +383,10 @@ def test_ffm_gpu_hogwild_logloss_parity_with_sequential():
     lookahead, ~1,000 rows in flight) measured 0.0117, the pipelined kernel 0.0195-0.0221
     (profiles/ffm_r3/hogwild_probe.log, profiles/r4/ffm_early_grid_curve.jsonl); the learner's
     default atomic-update ramp over the first 2^18 rows 0.0026.  With the linear records in the
-    feature blocks (round 5: a feature's lines stay longer in each XCD's L2, docs/compat.md) the
-    generic kernel measured 0.0164, the pipelined 0.0218 (profiles/r5/pytest_gpu_val_fail.log).
+    feature blocks the generic kernel measured 0.0152-0.0165 (one 16-B record access or three 4-B
+    words alike) against 0.0121-0.0124 with separate linear arrays, the pipelined 0.0215 vs
+    0.0195-0.0199: the cost is the layout (round 6, profiles/r6/ffm_generic_lin_layout.jsonl;
+    docs/compat.md "Test bounds"), which the headline keeps for +19 % rows/s.
     At the bench's 12.6 M rows the gap is +2.5e-3 .. +2.8e-3 (test_ffm_gpu_bench_scale_parity_pinned).
     Bounds = measurement + margin."""
     from hivemall_amd.models import ffm as ffm_model
