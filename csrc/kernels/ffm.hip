@@ -1062,11 +1062,14 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // KV = 16-B quads per slot: 1 for k <= 4 (the 896-B blocks above), 2 for k <= 8 (32-B V slots,
 // 1,536-B blocks; the landing zone and the image double, 107 KB of LDS at 39 fields: one block
 // per CU, launched with 512 threads so that each SIMD still holds two waves).
-// KEEP = 1 (round 6): each slot's offsets, x_a x_b and live / written / repeat bits are derived
+// KEEP = 1 (round 6, the default; variant 9 = KEEP 0 for A/B): each slot's offsets, x_a x_b and live / written / repeat bits are derived
 // from the row metadata ONCE, in phase C (next to that row's DMA issue), and kept in registers
 // for the row's B / D / E phases; the other phases re-read both metadata entries of every slot from
 // LDS, and the (b)-side reads of 16-B entries conflict where b wraps from F - 1 to 0 inside a
 // 16-lane group (2.7 extra LDS cycles per such read at F = 39, profiles/r6/lds_conflict_model.txt).
+// Measured (profiles/r6/keep_*): LDS bank-conflict cycles 210 M -> 30 M and LDS instructions 115 M
+// -> 72 M per 262,144-row dispatch; bench 93.0-93.3 vs 89.2-89.4 M rows/s fp32, same box,
+// interleaved x3; one block still equals the sequential engine to 3e-8 (k = 4) / 6e-8 (k = 8).
 template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1, int KEEP = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1456,7 +1459,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
 // per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
 // footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
-template <int NS, typename OT>
+// KEEP = 1 (round 6, default; variant 9 = 0): the slot data kept in registers from phase C, as in
+// ffm_pipe_sg32_kernel (the 16-B metadata reads of the b-side conflict where b wraps).
+template <int NS, typename OT, int KEEP = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1528,14 +1533,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         xab = live ? __int_as_float(ma.z) * __int_as_float(mb.z) : 0.f;
         return live ? 1u : (ok ? 2u : 0u);
     };
+    OT koff[KEEP ? NS : 1], noff[KEEP ? NS : 1];
+    float kxab[KEEP ? NS : 1], nxab[KEEP ? NS : 1];
+    uint32_t klive = 0u, kwr = 0u, nlive = 0u, nwr = 0u;
+    int krep = 0, nrep = 0;
     auto dma_slots = [&](int bf) {
+        if constexpr (KEEP) { nlive = 0u; nwr = 0u; nrep = 0; }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             OT off;
             float xab;
-            slot(bf, j, off, xab);
+            const uint32_t k = slot(bf, j, off, xab);
+            if constexpr (KEEP) {
+                noff[j] = off;
+                nxab[j] = xab;
+                nlive |= (k & 1u) << j;
+                nwr |= (uint32_t)(k != 0u) << j;
+                if (P.defer) nrep |= (int)slot_repeats(SA(j), SB(j), s_m[bf][SA(j)], s_m[bf][SB(j)]);
+            }
             __builtin_amdgcn_global_load_lds((glb_ptr_t)(vb + off), (lds_ptr_t)(s_raw + (j * 256 + wave * 64) * 4),
                                              12, 0, 0);
+        }
+    };
+    auto keep_rotate = [&]() {
+        if constexpr (KEEP) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) { koff[j] = noff[j]; kxab[j] = nxab[j]; }
+            klive = nlive; kwr = nwr; krep = nrep;
         }
     };
     auto dma_lin = [&](int bf) {
@@ -1562,6 +1586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     publish_meta(0);
     bar_raw();
     dma_slots(0);
+    keep_rotate();
     dma_lin(0);
     dma_meta(1, row + G);
 
@@ -1617,13 +1642,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         float xab[NS];
         float part = 0.f;
         int rep = 0;
+        if constexpr (KEEP) { live = klive; wr = kwr; rep = krep; }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            OT off;
-            const uint32_t k = slot(cur, j, off, xab[j]);
-            live |= (k & 1u) << j;
-            wr |= (uint32_t)(k != 0u) << j;
-            if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            if constexpr (KEEP) {
+                xab[j] = kxab[j];
+            } else {
+                OT off;
+                const uint32_t k = slot(cur, j, off, xab[j]);
+                live |= (k & 1u) << j;
+                wr |= (uint32_t)(k != 0u) << j;
+                if (P.defer) rep |= (int)slot_repeats(SA(j), SB(j), s_m[cur][SA(j)], s_m[cur][SB(j)]);
+            }
             const int s = tid + j * 256;
             const uint2 pv = s_t[s < FF ? s : 0];
             const uint2 cv = s_t[SB(j) * F + SA(j)];
@@ -1660,8 +1690,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             for (int j = 0; j < NS; ++j) {
                 if (!(wr >> j & 1u)) continue;
                 OT off;
-                float xj;
-                slot(cur, j, off, xj);
+                if constexpr (KEEP) {
+                    off = koff[j];
+                } else {
+                    float xj;
+                    slot(cur, j, off, xj);
+                }
                 const int s = tid + j * 256;
                 const uint2 pv = s_t[s];
                 const uint2 cv = s_t[SB(j) * F + SA(j)];
@@ -1718,6 +1752,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             }
         }
         if (more) dma_lin(nxt);
+        keep_rotate();
         bz = nbz;
         bn = nbn;
         ++bit;
@@ -1789,7 +1824,9 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
 #define HM_P12(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, \
+                                                  stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 1>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
@@ -1821,7 +1858,10 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 1, 2>), dim3(blocks), \
                                                   dim3(512), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 0, 2>), dim3(blocks), dim3(512), 0, stream, \
+        else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 0, 2>), dim3(blocks), \
+                                                  dim3(512), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                  bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 0, 2, 1>), dim3(blocks), dim3(512), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
         if (need <= 2) { HM_P32K8(2); }
         else if (need <= 3) { HM_P32K8(3); }
@@ -1841,10 +1881,9 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (variant == 8 && P.hot) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 2>), dim3(blocks), \
                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
-        else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), \
-                                                  dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
-                                                  bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, \
+                                                  stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
