@@ -1062,7 +1062,7 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // KV = 16-B quads per slot: 1 for k <= 4 (the 896-B blocks above), 2 for k <= 8 (32-B V slots,
 // 1,536-B blocks; the landing zone and the image double, 107 KB of LDS at 39 fields: one block
 // per CU, launched with 512 threads so that each SIMD still holds two waves).
-// KEEP = 1 (round 6, the default; variant 9 = KEEP 0 for A/B): each slot's offsets, x_a x_b and live / written / repeat bits are derived
+// KEEP >= 1 (round 6; the default is 2, variant 10 = 1, variant 9 = 0 for A/B): each slot's offsets, x_a x_b and live / written / repeat bits are derived
 // from the row metadata ONCE, in phase C (next to that row's DMA issue), and kept in registers
 // for the row's B / D / E phases; the other phases re-read both metadata entries of every slot from
 // LDS, and the (b)-side reads of 16-B entries conflict where b wraps from F - 1 to 0 inside a
@@ -1070,6 +1070,9 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // Measured (profiles/r6/keep_*): LDS bank-conflict cycles 210 M -> 30 M and LDS instructions 115 M
 // -> 72 M per 262,144-row dispatch; bench 93.0-93.3 vs 89.2-89.4 M rows/s fp32, same box,
 // interleaved x3; one block still equals the sequential engine to 3e-8 (k = 4) / 6e-8 (k = 8).
+// KEEP = 2 also keeps the forward pass's two image reads per slot for the update phase (the image
+// is not written between D and E): 94.2-97.6 vs 92.8-95.4 M rows/s fp32, 153.6-154.3 vs
+// 149.6-150.6 M bf16, same box, interleaved x3 (profiles/r6/keep/bench_keep2_ab.log).
 template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1, int KEEP = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1303,6 +1306,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
         float xab[NS];
+        float4 kpv[KEEP >= 2 ? NS : 1][KEEP >= 2 ? KV : 1], kcv[KEEP >= 2 ? NS : 1][KEEP >= 2 ? KV : 1];
         float part = 0.f;
         int rep = 0;
         if constexpr (KEEP) { live = klive; wr = kwr; rep = krep; }
@@ -1323,6 +1327,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             for (int q = 0; q < KV; ++q) {
                 const float4 pv = s_t[(s < FF ? s : 0) * KV + q];
                 const float4 cv = s_t[(SB(j) * F + SA(j)) * KV + q];
+                if constexpr (KEEP >= 2) { kpv[j][q] = pv; kcv[j][q] = cv; }
                 dot += cv.x * pv.x + cv.y * pv.y + cv.z * pv.z + cv.w * pv.w;
             }
             part += dot * xab[j];
@@ -1371,8 +1376,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 float gs = cg[j];
 #pragma unroll
                 for (int q = 0; q < KV; ++q) {
-                    const float4 pv = s_t[s * KV + q];
-                    const float4 cv = s_t[(SB(j) * F + SA(j)) * KV + q];
+                    // KEEP >= 2: the two image reads of the forward pass, kept in registers (the
+                    // image is not written between D and E)
+                    const float4 pv = KEEP >= 2 ? kpv[j][q] : s_t[s * KV + q];
+                    const float4 cv = KEEP >= 2 ? kcv[j][q] : s_t[(SB(j) * F + SA(j)) * KV + q];
                     o0[q] = f2{cv.x, cv.y};
                     o1[q] = f2{cv.z, cv.w};
                     const f2 p0 = f2{pv.x, pv.y}, p1 = f2{pv.z, pv.w};
@@ -1459,8 +1466,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 // {V | G | 0} slots need 5).  One 12-B LDS-DMA (global_load_lds_dwordx3) and one 12-B store
 // per slot; otherwise the schedule of ffm_pipe_sg32_kernel.  Access-pattern ceiling of this
 // footprint: 182 M rows/s (profiles/ffm_r3/roofline_sg.log, mode 6), 16-B slots 138 M.
-// KEEP = 1 (round 6, default; variant 9 = 0): the slot data kept in registers from phase C, as in
-// ffm_pipe_sg32_kernel (the 16-B metadata reads of the b-side conflict where b wraps).
+// KEEP (round 6; default 2, variant 10 = 1, variant 9 = 0): the slot data kept in registers from
+// phase C, and with 2 the forward's image reads kept for the update, as in ffm_pipe_sg32_kernel
+// (the 16-B metadata reads of the b-side conflict where b wraps).
 template <int NS, typename OT, int KEEP = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
@@ -1618,9 +1626,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            const uint32_t* q = s_raw + (j * 256 + tid) * 4;
-            cg[j] = __uint_as_float(q[2]);
-            if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = make_uint2(q[0], q[1]);
+            // one 16-B read per lane (contiguous: conflict-free); separate 4-B and 8-B reads at a
+            // 16-B lane stride were 4-way / 2-way bank conflicts
+            const uint4 q = *reinterpret_cast<const uint4*>(s_raw + (j * 256 + tid) * 4);
+            cg[j] = __uint_as_float(q.z);
+            if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = make_uint2(q.x, q.y);
         }
         if (more) publish_meta(nxt);
         bar_raw();
@@ -1640,6 +1650,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
         float xab[NS];
+        uint2 kpv[KEEP >= 2 ? NS : 1], kcv[KEEP >= 2 ? NS : 1];
         float part = 0.f;
         int rep = 0;
         if constexpr (KEEP) { live = klive; wr = kwr; rep = krep; }
@@ -1657,6 +1668,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             const int s = tid + j * 256;
             const uint2 pv = s_t[s < FF ? s : 0];
             const uint2 cv = s_t[SB(j) * F + SA(j)];
+            if constexpr (KEEP >= 2) { kpv[j] = pv; kcv[j] = cv; }
             part += dot2_bf16(cv.x, pv.x, dot2_bf16(cv.y, pv.y, 0.f)) * xab[j];
         }
         part *= 0.5f * scale * scale;
@@ -1697,8 +1709,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                     slot(cur, j, off, xj);
                 }
                 const int s = tid + j * 256;
-                const uint2 pv = s_t[s];
-                const uint2 cv = s_t[SB(j) * F + SA(j)];
+                const uint2 pv = KEEP >= 2 ? kpv[j] : s_t[s];
+                const uint2 cv = KEEP >= 2 ? kcv[j] : s_t[SB(j) * F + SA(j)];
                 const float c = ks * xab[j];
                 const float lj = (live >> j & 1u) ? P.lambda_v : 0.f;   // diagonal: zero step
                 const f2 cc = {c, c}, ll = {lj, lj};
@@ -1826,7 +1838,9 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                      P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
         else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, \
                                                   stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 1>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 1>), dim3(blocks), dim3(256), 0, \
+                                                   stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 2>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P12(2); }
     else if (need <= 4) { HM_P12(4); }
@@ -1883,7 +1897,10 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
                                                   bias, pred, loss); \
         else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, \
                                                   stream, P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
-        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), dim3(256), 0, stream, \
+        else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), \
+                                                   dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
+                                                   bias, pred, loss); \
+        else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 2>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
     else if (need <= 4) { HM_P32(4); }
