@@ -37,9 +37,12 @@ def heldout(m, test, dev):
 
 
 def fit(opts, rows, dev, timed=True):
-    from hivemall_amd.models.linear import TrainClassifier
+    """``opts``: train_classifier options, or "<learner>: options" for another SQL learner."""
+    from hivemall_amd.models.linear import LEARNERS
 
-    m = TrainClassifier(f"-loss logloss {opts} -dims 16777216 -iters 1", device=dev)
+    name, _, o = opts.partition(":") if ":" in opts else ("train_classifier", "", opts)
+    base = "-loss logloss " if name == "train_classifier" else ""
+    m = LEARNERS[name.strip()](f"{base}{o} -dims 16777216 -iters 1", device=dev)
     r = rows.to(dev)
     m._ensure_state(r)
     if dev == "cuda":
