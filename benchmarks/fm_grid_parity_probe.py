@@ -39,11 +39,14 @@ def main():
     hots = [float(h) for h in os.environ.get("PROBE_HOT", str(fm_ops.HOT_FRAC)).split(",")]
     # PROBE_HOT_EVERY="1,8,32": write-through on one hot update in N (ops/fm.py HOT_EVERY)
     evs = [int(e) for e in os.environ.get("PROBE_HOT_EVERY", str(fm_ops.HOT_EVERY)).split(",")]
+    # PROBE_XCDS="8,1,2": the waves on that many XCDs (ops/fm.py XCDS)
+    xcds = [int(x) for x in os.environ.get("PROBE_XCDS", "8").split(",")]
     for rep in range(reps):
         for g in grids:
-            for var, hot, ev in [(v, h, e) for v in variants for h in hots for e in evs]:
+            for var, hot, ev, xc in [(v, h, e, x) for v in variants for h in hots for e in evs for x in xcds]:
                 fm_ops.HOT_FRAC = hot
                 fm_ops.HOT_EVERY = ev
+                fm_ops.XCDS = xc
                 os.environ["HM_FM_VARIANT"] = var
                 torch.cuda.synchronize()
                 t = time.perf_counter()
@@ -52,7 +55,7 @@ def main():
                 dt = time.perf_counter() - t
                 os.environ["HM_FM_VARIANT"] = "0"
                 v = ll(m, "cuda")
-                print(json.dumps({"opts": extra, "variant": var, "hot_frac": hot, "hot_every": ev, "grid": g, "rep": rep, "gpu": round(v, 5),
+                print(json.dumps({"opts": extra, "variant": var, "hot_frac": hot, "hot_every": ev, "xcds": xc, "grid": g, "rep": rep, "gpu": round(v, 5),
                                   "delta_vs_mappers8": round(v - m8, 5), "rows_per_s": round(n / dt)}), flush=True)
 
 

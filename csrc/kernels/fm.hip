@@ -43,6 +43,8 @@ struct FMParams {
     const uint8_t* hot;       // per-feature flags (nullable): a hot feature's V row / w stores go
                               // out SC1 (write-through, dropped from the writer's XCD L2) ...
     uint32_t hot_mask;        // ... on the rows whose hash & hot_mask == 0 (0: every row)
+    int xcds;                 // fm_pipe_kernel: waves on this many of the 8 XCDs (8: all; fewer:
+                              // only blocks with blockIdx % 8 < xcds work — round-robin placement)
     long long vstride;        // V elements between feature rows (>= KP)
     long long wstride;        // floats between features' w (1: its own array; a record: inside
                               // the feature's V row, so the gather and the store touch one line)
@@ -318,8 +320,15 @@ __global__ __launch_bounds__(256) void fm_pipe_kernel(FMParams P, const int64_t*
                                                       void* __restrict__ V, float* __restrict__ w0,
                                                       float* __restrict__ pred, float* __restrict__ loss) {
     const int lane = hm::lane_id();
-    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + hm::wave_id();
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    // XCD confinement (P.xcds < 8): the launch has 8 / xcds x the blocks and only those with
+    // blockIdx % 8 < xcds work, i.e. every wave on xcds XCDs under round-robin placement (speed and
+    // staleness only, never correctness): one XCD's L2 is a coherent copy of the hot features
+    const int bx = (int)blockIdx.x;
+    if (P.xcds < 8 && (bx & 7) >= P.xcds) return;
+    const int64_t lbx = P.xcds < 8 ? (int64_t)(bx >> 3) * P.xcds + (bx & 7) : (int64_t)bx;
+    const int64_t lgrid = P.xcds < 8 ? (int64_t)(gridDim.x >> 3) * P.xcds : (int64_t)gridDim.x;
+    const int64_t gw = lbx * (blockDim.x / 64) + hm::wave_id();
+    const int64_t nw = lgrid * (blockDim.x / 64);
     if (gw >= n_rows) return;                                  // wave-uniform
     // pipeline registers: bounds of the current row, first-chunk (index, value) of it
     int64_t s = indptr[gw], e = indptr[gw + 1];
@@ -525,7 +534,8 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
     if (blocks < 1) blocks = 1;
     // `grid` counts 4-wave workgroups (the Hogwild rows in flight / 4); the waves are launched
     // wpb to a workgroup (1, 2 or 4), so the same rows in flight spread over more CUs
-    const int64_t lb = blocks * 4 / wpb;
+    int64_t lb = blocks * 4 / wpb;
+    if (P.xcds < 8 && variant != 1) lb = (lb + P.xcds - 1) / P.xcds * 8;   // see fm_pipe_kernel
     if (variant == 1)
         hipLaunchKernelGGL((fm_kernel<KP, BF16>), dim3((int)lb), dim3(64 * wpb), 0, st, P, indptr, idx,
                            val, y, n, t0, w, V, w0, pred, loss);
@@ -561,6 +571,7 @@ HM_API int hm_fm_step(const int32_t* ip, const float* hp, int64_t n_rows, int64_
     FMParams P;
     P.hot = hot;
     P.hot_mask = (uint32_t)ip[16];
+    P.xcds = ip[17] >= 1 && ip[17] <= 8 ? ip[17] : 8;
     P.dims = ip[0]; P.k = ip[1];
     const int KP = ip[2];
     P.classification = ip[3]; P.train = ip[4]; P.eta_kind = ip[5]; P.use_w0 = ip[6];

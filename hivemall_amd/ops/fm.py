@@ -96,6 +96,8 @@ HOT_FRAC = float(os.environ.get("HM_FM_HOT_FRAC", "0"))
 # XCD's updates a stale copy can absorb while the memory side serialises 1 / HOT_EVERY of them
 HOT_EVERY = int(os.environ.get("HM_FM_HOT_EVERY", "1"))
 HOT_WT = os.environ.get("HM_FM_HOT_WT", "1") != "0"
+# waves on this many of the 8 XCDs (csrc/kernels/fm.hip P.xcds; 8 = all)
+XCDS = 8
 
 
 def hot_flags(state: dict, idx: torch.Tensor, n_rows: int, frac: float = None,
@@ -146,7 +148,8 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
                    int(os.environ.get("HM_FM_VARIANT", "0")),
                    max(1, min(W0_EVERY_MAX, int(os.environ.get(
                        "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1))))),
-                   V.stride(0), w.stride(0), WPB, max(1, HOT_EVERY) - 1],
+                   V.stride(0), w.stride(0), WPB, max(1, HOT_EVERY) - 1,
+                   int(os.environ.get("HM_FM_XCDS", str(XCDS)))],
                   dtype=np.int32)
     assert V.stride(1) == 1 and V.stride(0) >= KP, "V rows must be contiguous"
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1
