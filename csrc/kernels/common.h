@@ -15,6 +15,7 @@
 #define HM_API extern "C" __attribute__((visibility("default")))
 
 #define HM_LAUNCH_RET() return (int)hipGetLastError()
+#define HM_LAUNCH_RET_IF_ERR() do { const hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 namespace hm {
 

@@ -75,6 +75,18 @@ struct FFMParams {
     // one 16-B store per feature instead of three scattered 4-B ones into three more lines.
     long long lstride;
     int lpack;
+    // lin_atomic (lpack records, ATOM = 0 pipelined kernels, grid > 1): each row ADDS its FTRL
+    // steps dz, g^2 to the record's (z, n) with float atomics instead of storing {w, z, n}, and w is
+    // derived as f(z, n) where it is read (ffm_lin_derive_kernel refreshes the stored w after the
+    // launch).  Round 6: a host model of W rows in flight (benchmarks/ffm_hogwild_sim.py) put 79 %
+    // of the same-stream gap on lost linear updates (+3.86e-3 -> +0.81e-3 at W = 1024 with only
+    // the linear (z, n) added, nothing else changed; the V / G slots' lost updates the rest).
+    int lin_atomic;
+    const int32_t* hidx;           // lin_atomic 4: hot index of each feature (-1: cold), [num_features]
+    const int32_t* hot_id;         // lin_atomic 4: feature of each hot index, [nhot]
+    float* hacc;                   // lin_atomic 4: {z, n, 0, 0} per hot index, [nhot][HACC_STRIDE]
+    int nhot;                      // <= HD_SIZE
+    int hacc_on;                   // set by the dispatch for a launch that uses the side table
     // Global-bias FTRL state sharded over bias_s 128-B lines during a training launch (sg32 /
     // sg12): z0 = sum of bias_sh[32 s], n0 = sum of bias_sh[32 s + 1]; a row adds its step to
     // shard (block % bias_s).  Null: the single {w0, z0, n0} address (every row's two atomics
@@ -139,6 +151,41 @@ __device__ __forceinline__ void bias_update_sh(const FFMParams& P, float g, floa
     acc[0] += dz;
     acc[1] += g * g;
 }
+
+// lin_atomic: the weight of a DMA'd {w, z, n, _} record is f(z, n) (its stored w lags: rows add
+// to (z, n) only); a record never stepped (n = 0) keeps its stored w
+__device__ __forceinline__ float lin_w(const FFMParams& P, float4 r) {
+    return r.z > 0.f ? ftrl_weight(r.y, r.z, P.alpha, P.beta, P.lambda1, P.lambda2) : r.x;
+}
+
+// lin_atomic: the row's FTRL step of feature i as two no-return float atomics on its record's
+// (z, n): dz = g - sigma w (the host engine's association: z + (g - sigma w)), dn = g^2
+__device__ __forceinline__ void lin_add(const FFMParams& P, float* w, int i, float g, float n0,
+                                        float n1, float wcur) {
+    atomicAdd(&LW(w, i) + 1, g - (sqrtf(n1) - sqrtf(n0)) / P.alpha * wcur);
+    atomicAdd(&LW(w, i) + 2, g * g);
+}
+
+// lin_atomic 4 (template LT of the pipelined kernels): the linear FTRL state (z, n) of the
+// P.nhot hot features lives in a dense side table P.hacc[h] = {z, n, 0, 0} (h = P.hidx[feature],
+// -1: cold) for the duration of a launch (ffm_hacc_kernel copies it out of / back into the
+// records around the launch).  A block sums its rows' steps of hot features in LDS, s_hd[h], and
+// adds them to P.hacc by float atomics when it ends; a row reads hacc[h] (DMA'd one row ahead,
+// like the record) plus the block's own sums.  Nothing is lost to a concurrent row, and the
+// atomics land in the side table, not in the hot features' blocks: atomics on the records
+// themselves drop those lines from L2 and took the kernel from 93 to 28 M rows/s
+// (profiles/r6/linhot/).  Cold features keep the plain record stores.
+constexpr int HD_SIZE = 2048;
+constexpr int HD12_SIZE = 1024;   // ffm_pipe_sg12_kernel (bf16 12-B slots)
+// one side-table entry per 128-B line (16-B entries, 8 to a line: 73.6 vs 76.0 M rows/s)
+constexpr int HACC_STRIDE = 32;
+// default grid of a side-table launch: a block's sums are flushed when it ends, so fewer, longer-
+// lived blocks add fewer atomics per row (distinct hot features per block grow slower than its
+// rows).  Measured (profiles/r6/linhot/): 8,192 blocks 76.0 M rows/s, 4,096 .., 2,048 84.5 M at
+// +0.96e-3 .. +1.01e-3; 1,024 (256 rows per block) diverges (+0.06 .. +0.11): every block walks
+// its own copy of a hot feature's weight toward the target for 256 rows and the sum of those walks
+// overshoots.
+constexpr int HACC_GRID = 2048;
 
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
@@ -481,7 +528,7 @@ __global__ __launch_bounds__(256) void ffm_row_kernel(
                     const float4 r = *rp;
                     float z = r.y, n = r.z;
                     const float nw = ftrl_update(&z, &n, r.x, kappa * xs * scale, P.alpha, P.beta, P.lambda1, P.lambda2);
-                    *rp = make_float4(nw, z, n, 0.f);
+                    *rp = make_float4(nw, z, n, r.w);
                 } else {
                     LW(w, i) = ftrl_update(&LW(wz, i), &LW(wn, i), LW(w, i), kappa * xs * scale, P.alpha, P.beta,
                                            P.lambda1, P.lambda2);
@@ -1073,7 +1120,7 @@ typedef uint32_t u3v_t __attribute__((ext_vector_type(3)));
 // KEEP = 2 also keeps the forward pass's two image reads per slot for the update phase (the image
 // is not written between D and E): 94.2-97.6 vs 92.8-95.4 M rows/s fp32, 153.6-154.3 vs
 // 149.6-150.6 M bf16, same box, interleaved x3 (profiles/r6/keep/bench_keep2_ab.log).
-template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1, int KEEP = 0>
+template <int NS, typename OT, int TPB = 256, int ATOM = 0, int KV = 1, int KEEP = 0, int LT = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))) void ffm_pipe_sg32_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1091,6 +1138,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     __shared__ int s_rep[TPB / 64];                                   // per wave: a multi-hot slot
     __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
     __shared__ float s_bcur[2];                                       // own bias steps since the read
+    // LT (lin_atomic 4, HD_SIZE above): the block's own linear steps of hot features, summed per
+    // hot index, and the rows' DMA of the side table
+    __shared__ float2 s_hd[LT ? HD_SIZE : 1];
+    __shared__ __attribute__((aligned(16))) float4 s_hacc[LT ? 2 : 1][48];
+    __shared__ __attribute__((aligned(16))) int s_nh[LT ? 2 : 1][48];   // DMA of the rows' hot indices
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1103,6 +1155,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     const int bid = (int)blockIdx.x;
     char* vb = reinterpret_cast<char*>(Vt);
     char* gb = reinterpret_cast<char*>(Gt);
+    // linear (z, n) steps by float atomics (FFMParams.lin_atomic; 2 / 3: only the features P.hot
+    // flags / does not flag, A/B); one block stores them (exact)
+    const bool latom = ATOM == 0 && !LT && P.lin_atomic == 1 && G > 1;
+    if constexpr (LT != 0) {
+        for (int t = tid; t < HD_SIZE; t += TPB) s_hd[t] = make_float2(0.f, 0.f);
+    }
+    int nh = -1, kh = -1;            // LT, W_LIN lanes: hot index of the next / current row's feature
 
     int ab[NS];
 #pragma unroll
@@ -1129,7 +1188,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
                 int rf = fld ? s_mr[bf][1][lane] : lane;
                 float rx = val ? __int_as_float(s_mr[bf][2][lane]) : 1.f;
                 if (ri < 0 || ri >= P.num_features || rf < 0 || rf >= P.num_fields) { ri = -1; rx = 0.f; rf = 0; }
-                const int hb = (ATOM == 2 && ri >= 0) ? (int)P.hot[ri] : 0;
+                const int hb = ((ATOM == 2 || (latom && P.lin_atomic >= 2)) && ri >= 0) ? (int)P.hot[ri] : 0;
                 s_m[bf][lane] = make_int4(ri, rf, __float_as_int(rx), hb);
                 sq = rx * rx;
             }
@@ -1188,12 +1247,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     // its older slot DMAs (vmcnt(NLIN)), and for the linear DMA right before its first read in D
     // (vmcnt(2 NS): only the next row's slot DMAs, issued in C, may still be in flight).  Every
     // lane < F issues the DMAs (an invalid feature reads w[0], unused), so the counts are exact.
-    const int nlin = (P.use_linear && P.lin_defer) ? ((P.lpack || !P.train) ? 1 : 3) : 0;
+    const int nlin = (P.use_linear && P.lin_defer) ? ((P.lpack || !P.train) ? 1 + (LT != 0) : 3) : 0;
     auto dma_lin = [&](int bf) {
         if (P.use_linear && wave == W_LIN && lane < F) {
             const int i = max(s_m[bf][lane].x, 0);
             if (P.lpack) {
                 __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin4[bf][0], 16, 0, 0);
+                if constexpr (LT != 0)   // every lane: the wave's DMA count stays exact
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(P.hacc + HACC_STRIDE * max(nh, 0)), (lds_ptr_t)&s_hacc[bf][0], 16, 0, 0);
                 return;
             }
             __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
@@ -1214,7 +1275,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
     bar_raw();
     dma_slots(0);
     keep_rotate();
+    if constexpr (LT != 0) {
+        if (wave == W_LIN && lane < F) nh = s_m[0][lane].x >= 0 ? P.hidx[s_m[0][lane].x] : -1;
+    }
     dma_lin(0);
+    kh = nh;
     dma_meta(1, row + G);
 
     // Forwarding of the block's own updates into its next row: the next row's slots are DMA'd
@@ -1241,6 +1306,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         const bool more = row + G < P.B;
         // ---- A: this wave's DMAs have landed, then every wave's ----
         if (wave == W_LIN && nlin == 3) __builtin_amdgcn_s_waitcnt(0x0F73);      // vmcnt(3)
+        else if (wave == W_LIN && nlin == 2) __builtin_amdgcn_s_waitcnt(0x0F72); // vmcnt(2)
         else if (wave == W_LIN && nlin == 1) __builtin_amdgcn_s_waitcnt(0x0F71); // vmcnt(1)
         else __builtin_amdgcn_s_waitcnt(0x0F70);                                // vmcnt(0)
         bar_raw();
@@ -1254,6 +1320,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             nbn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // ---- B: landing zone -> registers (G) and the transposed image (V); meta(row + G) ----
+        if constexpr (LT != 0) {
+            // the next row's hot indices by LDS-DMA from its raw meta (landed at A): older than the
+            // slot DMAs of phase C, so C's wait covers them and phase F reads them from LDS
+            if (more && wave == W_LIN && lane < F) {
+                const int ri = s_mr[nxt][0][lane];
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(P.hidx + (ri >= 0 && ri < P.num_features ? ri : 0)),
+                                                 (lds_ptr_t)&s_nh[nxt][0], 4, 0, 0);
+            }
+        }
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -1292,9 +1367,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
         const float scale = s_red[TPB / 64 + cur];
         int mi = -1;
         float mx = 0.f, lw = 0.f;
+        int hot = 0;                     // LT: this lane's feature is hot (kh >= 0)
+        float hz = 0.f, hn = 0.f;        // LT: its (z, n) as this block sees them
         if (wave == W_LIN && nlin) {
             // the linear DMA of this row has landed (older than the C-phase slot DMAs)
-            if (more) __builtin_amdgcn_s_waitcnt(VMCNT_ENC(2 * NS));
+            if (more) __builtin_amdgcn_s_waitcnt(VMCNT_ENC((KV + 1) * NS));
             else __builtin_amdgcn_s_waitcnt(0x0F70);
         }
         if (wave == W_LIN && lane < F) {
@@ -1302,6 +1379,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             mi = m.x;
             mx = __int_as_float(m.z);
             lw = P.lpack ? s_lin4[cur][lane].x : s_lin[cur][0][lane];
+            if (latom) lw = lin_w(P, s_lin4[cur][lane]);
+            if constexpr (LT != 0) {
+                if (P.hacc_on && mi >= 0 && kh >= 0) {
+                    // hot: the side table as DMA'd (the other blocks' flushed steps) + this block's own
+                    const float4 a = s_hacc[cur][lane];
+                    const float2 d = s_hd[kh];
+                    hz = a.x + d.x;
+                    hn = a.y + d.y;
+                    hot = 1;
+                    lw = hn > 0.f ? ftrl_weight(hz, hn, P.alpha, P.beta, P.lambda1, P.lambda2) : lw;
+                }
+            }
         }
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
@@ -1424,18 +1513,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             // profiles/r4/ffm_skip_diagonal_ab.log.)
             if (mi >= 0) {
                 if (P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                    const float lz = P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane];
-                    const float ln = P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane];
+                    const float lz = hot ? hz : (P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane]);
+                    const float ln = hot ? hn : (P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane]);
                     const float g = kappa * mx * scale;
                     const float n1 = ln + g * g;
                     const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
                     const float w1 = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
-                    if (ATOM == 1 || (ATOM == 2 && s_m[cur][lane].w != 0)) {
+                    if (LT && hot) {
+                        const float2 d = s_hd[kh];
+                        s_hd[kh] = make_float2(d.x + (g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw), d.y + g * g);
+                    } else if (ATOM == 1 || (ATOM == 2 && s_m[cur][lane].w != 0)) {
                         atomicAdd(&LW(wz, mi), z1 - lz);
                         atomicAdd(&LW(wn, mi), g * g);
                         LW(w, mi) = w1;
+                    } else if (latom && (P.lin_atomic == 1 || (P.lin_atomic == 2) == (s_m[cur][lane].w != 0))) {
+                        lin_add(P, w, mi, g, ln, n1, lw);
                     } else if (P.lpack) {
-                        *reinterpret_cast<float4*>(&LW(w, mi)) = make_float4(w1, z1, n1, 0.f);
+                        *reinterpret_cast<float4*>(&LW(w, mi)) = make_float4(w1, z1, n1, s_lin4[cur][lane].w);
                     } else {
                         LW(wz, mi) = z1;
                         LW(wn, mi) = n1;
@@ -1449,13 +1543,30 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
             }
         }
         // ---- F: linear state of the next row (after this row's FTRL stores) ----
+        if constexpr (LT != 0) {
+            if (more && wave == W_LIN && lane < F) nh = s_nh[nxt][lane];
+        }
         if (more) dma_lin(nxt);
+        kh = nh;
         keep_rotate();
         bz = nbz;
         bn = nbn;
         ++bit;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
+    if constexpr (LT != 0) {
+        // the block's summed hot steps -> the side table (every wave; the W_LIN wave's LDS adds
+        // are published by the barrier).  No-return atomics, not waited for: a wait here for their
+        // completion under every block's contention cost 89 -> 68 M rows/s (profiles/r6/linhot/)
+        bar_raw();
+        // Lanes 2e, 2e + 1 add z, n of entry e (one 8-B run per entry and instruction: 67 -> 76 M
+        // rows/s against one lane adding both)
+        if (P.hacc_on)
+            for (int t = tid; t < 2 * P.nhot; t += TPB) {
+                const float2 d = s_hd[t >> 1];
+                if (d.y != 0.f || d.x != 0.f) atomicAdd(P.hacc + HACC_STRIDE * (t >> 1) + (t & 1), (t & 1) ? d.y : d.x);
+            }
+    }
 #undef SA
 #undef SB
 }
@@ -1469,7 +1580,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB / 128))
 // KEEP (round 6; default 2, variant 10 = 1, variant 9 = 0): the slot data kept in registers from
 // phase C, and with 2 the forward's image reads kept for the update, as in ffm_pipe_sg32_kernel
 // (the 16-B metadata reads of the b-side conflict where b wraps).
-template <int NS, typename OT, int KEEP = 0>
+template <int NS, typename OT, int KEEP = 0, int LT = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ffm_pipe_sg12_kernel(
     FFMParams P, const int32_t* __restrict__ idx, const int32_t* __restrict__ fld,
     const float* __restrict__ val, const float* __restrict__ y, void* __restrict__ Vt,
@@ -1488,6 +1599,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     __shared__ int s_rep[4];                                                  // per wave: a multi-hot slot
     __shared__ float s_bias[4];                                       // the row's {w0, z0, n0}
     __shared__ float s_bcur[2];                                       // own bias steps since the read
+    // LT: the side table of ffm_pipe_sg32_kernel with at most HD12_SIZE hot features (8 KB of sums:
+    // 3 blocks per CU still fit)
+    __shared__ float2 s_hd[LT ? HD12_SIZE : 1];
+    __shared__ __attribute__((aligned(16))) float4 s_hacc[LT ? 2 : 1][48];
+    __shared__ __attribute__((aligned(16))) int s_nh[LT ? 2 : 1][48];
     const int F = P.F;
     const int FF = F * F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1495,6 +1611,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     const OT bs = (OT)P.gstride * 4u;                    // block bytes per feature
     const int G = gridDim.x;
     char* vb = reinterpret_cast<char*>(Vt);
+    const bool latom = !LT && P.lin_atomic == 1 && G > 1;   // as in ffm_pipe_sg32_kernel
+    if constexpr (LT != 0) {
+        for (int t = tid; t < HD12_SIZE; t += 256) s_hd[t] = make_float2(0.f, 0.f);
+    }
+    int nh = -1, kh = -1;            // LT, W_LIN lanes: hot index of the next / current row's feature
     // linear records inside the blocks (the first 16-B chunk after the 12-B slots), whether they
     // are accessed as one 16-B record (lpack) or as three 4-B words: the tail zeroing skips them
     const bool lin_in_tail = reinterpret_cast<const char*>(w) == vb + (size_t)P.vpad * 12;
@@ -1575,6 +1696,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             const int i = s_m[bf][lane].x;
             if (i >= 0 && P.lpack) {
                 __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin4[bf][0], 16, 0, 0);
+                if (LT && nh >= 0)
+                    __builtin_amdgcn_global_load_lds((glb_ptr_t)(P.hacc + HACC_STRIDE * nh), (lds_ptr_t)&s_hacc[bf][0], 16, 0, 0);
             } else if (i >= 0) {
                 __builtin_amdgcn_global_load_lds((glb_ptr_t)&LW(w, i), (lds_ptr_t)&s_lin[bf][0][0], 4, 0, 0);
                 if (P.train) {
@@ -1595,7 +1718,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
     bar_raw();
     dma_slots(0);
     keep_rotate();
+    if constexpr (LT != 0) {
+        if (P.hacc_on && wave == W_LIN && lane < F) nh = s_m[0][lane].x >= 0 ? P.hidx[s_m[0][lane].x] : -1;
+    }
     dma_lin(0);
+    kh = nh;
     dma_meta(1, row + G);
 
     const bool bsh = P.use_bias && P.bias_sh;
@@ -1623,6 +1750,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             nbn = __hip_atomic_load(P.bias_sh + lane * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // ---- B: landing zone -> G registers + transposed V image ----
+        if constexpr (LT != 0) {
+            // the next row's hot indices (as in ffm_pipe_sg32_kernel; waited for in C)
+            if (P.hacc_on && more && wave == W_LIN && lane < F) {
+                const int ri = s_mr[nxt][0][lane];
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(P.hidx + (ri >= 0 && ri < P.num_features ? ri : 0)),
+                                                 (lds_ptr_t)&s_nh[nxt][0], 4, 0, 0);
+            }
+        }
         float cg[NS];
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -1638,14 +1773,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             dma_slots(nxt);
             dma_meta(cur, row + 2 * G);
         }
+        if constexpr (LT != 0) {
+            if (P.hacc_on && more && wave == W_LIN) {
+                __builtin_amdgcn_s_waitcnt(VMCNT_ENC(NS));   // the B-phase DMA (older than the NS slot DMAs)
+                if (lane < F) nh = s_nh[nxt][lane];
+            }
+        }
         const float scale = s_red[4 + cur];
         int mi = -1;
         float mx = 0.f, lw = 0.f;
+        int hot = 0;
+        float hz = 0.f, hn = 0.f;
         if (wave == W_LIN && lane < F) {
             const int4 m = s_m[cur][lane];
             mi = m.x;
             mx = __int_as_float(m.z);
             lw = P.lpack ? s_lin4[cur][lane].x : s_lin[cur][0][lane];
+            if (latom) lw = lin_w(P, s_lin4[cur][lane]);
+            if constexpr (LT != 0) {
+                if (P.hacc_on && mi >= 0 && kh >= 0) {
+                    const float4 a = s_hacc[cur][lane];
+                    const float2 d = s_hd[kh];
+                    hz = a.x + d.x;
+                    hn = a.y + d.y;
+                    hot = 1;
+                    lw = hn > 0.f ? ftrl_weight(hz, hn, P.alpha, P.beta, P.lambda1, P.lambda2) : lw;
+                }
+            }
         }
         // ---- D: forward ----
         uint32_t live = 0u, wr = 0u;
@@ -1744,13 +1898,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
                 }
             }
             if (mi >= 0 && P.use_linear) {   // FTRL-proximal on the DMA'd (w, z, n)
-                const float lz = P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane];
-                const float ln = P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane];
+                const float lz = hot ? hz : (P.lpack ? s_lin4[cur][lane].y : s_lin[cur][1][lane]);
+                const float ln = hot ? hn : (P.lpack ? s_lin4[cur][lane].z : s_lin[cur][2][lane]);
                 const float g = kappa * mx * scale;
                 const float n1 = ln + g * g;
                 const float z1 = lz + g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw;
                 const float w1 = ftrl_weight(z1, n1, P.alpha, P.beta, P.lambda1, P.lambda2);
-                if (P.lpack) {
+                if (LT && hot) {
+                    const float2 d = s_hd[kh];
+                    s_hd[kh] = make_float2(d.x + (g - (sqrtf(n1) - sqrtf(ln)) / P.alpha * lw), d.y + g * g);
+                } else if (latom) {
+                    lin_add(P, w, mi, g, ln, n1, lw);
+                } else if (P.lpack) {
                     *reinterpret_cast<float4*>(&LW(w, mi)) = make_float4(w1, z1, n1, 0.f);
                 } else {
                     LW(wz, mi) = z1;
@@ -1764,12 +1923,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             }
         }
         if (more) dma_lin(nxt);
+        kh = nh;
         keep_rotate();
         bz = nbz;
         bn = nbn;
         ++bit;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // no LDS-DMA outstanding at exit
+    if constexpr (LT != 0) {
+        bar_raw();   // (as in ffm_pipe_sg32_kernel)
+        if (P.hacc_on)
+            for (int t = tid; t < 2 * P.nhot; t += 256) {
+                const float2 d = s_hd[t >> 1];
+                if (d.y != 0.f || d.x != 0.f) atomicAdd(P.hacc + HACC_STRIDE * (t >> 1) + (t & 1), (t & 1) ? d.y : d.x);
+            }
+    }
 #undef SA
 #undef SB
 }
@@ -1823,6 +1991,32 @@ int dispatch_lean(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     HM_LAUNCH_RET();
 }
 
+// lin_atomic 4: dir 0 copies the hot features' (z, n) from their records into the side table
+// before a launch, dir 1 writes them back (w = f(z, n)) after it.
+__global__ __launch_bounds__(256) void ffm_hacc_kernel(FFMParams P, float* __restrict__ w, int dir) {
+    const int h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= P.nhot) return;
+    float4* rp = reinterpret_cast<float4*>(&LW(w, P.hot_id[h]));
+    float4* ap = reinterpret_cast<float4*>(P.hacc + HACC_STRIDE * h);
+    const float4 r = *rp;
+    if (dir == 0) {
+        *ap = make_float4(r.y, r.z, 0.f, 0.f);
+    } else {
+        const float4 a = *ap;
+        const float nw = a.y > 0.f ? ftrl_weight(a.x, a.y, P.alpha, P.beta, P.lambda1, P.lambda2) : r.x;
+        *rp = make_float4(nw, a.x, a.y, r.w);
+    }
+}
+
+// lin_atomic: w <- f(z, n) for every feature record a row stepped (n > 0; a record never stepped
+// keeps its w, e.g. an imported model's).
+__global__ __launch_bounds__(256) void ffm_lin_derive_kernel(FFMParams P, float* __restrict__ w) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P.num_features) return;
+    const float4 r = *reinterpret_cast<const float4*>(&LW(w, i));
+    if (r.z > 0.f) LW(w, i) = ftrl_weight(r.y, r.z, P.alpha, P.beta, P.lambda1, P.lambda2);
+}
+
 // Per-slot-G in 12-B bf16 slots {V | G}, 512-B feature blocks (Kp == 4, F <= 45, table < 4 GiB).
 int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, const float* val,
                   const float* y, void* VG, float* w, float* wz, float* wn, float* bias,
@@ -1831,11 +2025,20 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     // tables of 4 GiB and more (-feature_hashing >= 23 at 512-B blocks): 64-bit slot offsets
     const bool wide = (size_t)P.num_features * (size_t)P.gstride * 4 >= ((size_t)1 << 32);
     const int need = (P.F * P.F + 255) / 256;
-    const int blocks = default_blocks(P.B, grid, 256 * 8 * 8);
+    int blocks = default_blocks(P.B, grid, 256 * 8 * 8);
     if (blocks <= 0) return 0;
+    FFMParams Q = P;
+    Q.hacc_on = P.lin_atomic == 4 && P.nhot <= HD12_SIZE && blocks > 1 && !wide && variant != 9 && variant != 10;
+    if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID);
+    if (Q.hacc_on) {
+        hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 0);
+        HM_LAUNCH_RET_IF_ERR();
+    }
 #define HM_P12(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
+        else if (Q.hacc_on) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 2, 1>), dim3(blocks), dim3(256), 0, \
+                                               stream, Q, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
         else if (variant == 9) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t>), dim3(blocks), dim3(256), 0, \
                                                   stream, P, idx, fld, val, y, VG, w, wz, wn, bias, pred, loss); \
         else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg12_kernel<NSV, uint32_t, 1>), dim3(blocks), dim3(256), 0, \
@@ -1847,6 +2050,10 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     else if (need <= 6) { HM_P12(6); }
     else { HM_P12(8); }
 #undef HM_P12
+    if (Q.hacc_on) {
+        HM_LAUNCH_RET_IF_ERR();
+        hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 1);
+    }
     HM_LAUNCH_RET();
 }
 
@@ -1884,8 +2091,17 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         HM_LAUNCH_RET();
     }
     const int need = (P.F * P.F + 255) / 256;
-    const int blocks = default_blocks(P.B, grid);
+    int blocks = default_blocks(P.B, grid);
     if (blocks <= 0) return 0;
+    // lin_atomic 4: the side table for a launch of more than one block (one block stores the
+    // records in row order: the sequential engine)
+    FFMParams Q = P;
+    Q.hacc_on = P.lin_atomic == 4 && blocks > 1 && variant != 6 && variant != 8 && variant != 9 && variant != 10;
+    if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID);
+    if (Q.hacc_on) {
+        hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 0);
+        HM_LAUNCH_RET_IF_ERR();
+    }
 #define HM_P32(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t>), dim3(blocks), dim3(256), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
@@ -1900,6 +2116,9 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (variant == 10) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 1>), dim3(blocks), \
                                                    dim3(256), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                    bias, pred, loss); \
+        else if (Q.hacc_on) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 2, 1>), dim3(blocks), \
+                                               dim3(256), 0, stream, Q, idx, fld, val, y, V, G, w, wz, wn, \
+                                               bias, pred, loss); \
         else hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 256, 0, 1, 2>), dim3(blocks), dim3(256), 0, stream, \
                                 P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); } while (0)
     if (need <= 2) { HM_P32(2); }
@@ -1907,6 +2126,10 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     else if (need <= 6) { HM_P32(6); }
     else { HM_P32(8); }
 #undef HM_P32
+    if (Q.hacc_on) {
+        HM_LAUNCH_RET_IF_ERR();
+        hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 1);
+    }
     HM_LAUNCH_RET();
 }
 
@@ -2000,7 +2223,8 @@ int launch_deferred(FFMParams P, const int32_t* idx, const int32_t* fld, const f
 // hp layout (floats): eta0, eps, lambda_v, alpha, beta, lambda1, lambda2, min_target, max_target
 // ip layout (ints)  : B, F, num_features, num_fields, Kp, classification, train, use_linear,
 //                     use_bias, norm, grid, reload, bf16_state, seed, packed, variant, fstride,
-//                     slot_g, gstride, vpad, tail16, gfstride, lin_defer, bias_every, lstride, lpack
+//                     slot_g, gstride, vpad, tail16, gfstride, lin_defer, bias_every, lstride, lpack,
+//                     lin_atomic
 // lstride = floats between consecutive features' w / wz / wn (1: separate arrays; the records of
 //           ops/ffm.py lin_record_views: the feature block's size); lpack = 1: {w, z, n} are one
 //           16-B record (wz = w + 1, wn = w + 2), DMA'd and stored as one 16-B access
@@ -2066,6 +2290,20 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     P.lin_defer = ip[22];
     P.lstride = ip[24] > 0 ? ip[24] : 1;
     P.lpack = ip[25];
+    P.lin_atomic = P.lpack ? ip[26] : 0;
+    P.hidx = nullptr; P.hot_id = nullptr; P.hacc = nullptr; P.nhot = 0; P.hacc_on = 0;
+
+    if (P.lin_atomic == 4) {
+        // aux[4..6] = hidx, hot_id, hacc; ip[27] = nhot
+        P.nhot = ip[27];
+        if (aux) {
+            P.hidx = reinterpret_cast<const int32_t*>(aux[4]);
+            P.hot_id = reinterpret_cast<const int32_t*>(aux[5]);
+            P.hacc = reinterpret_cast<float*>(aux[6]);
+        }
+        if (!P.hidx || !P.hot_id || !P.hacc || P.nhot <= 0 || P.nhot > HD_SIZE || !P.train || !P.use_linear)
+            P.lin_atomic = 0;
+    }
     if (P.lpack && (wz != w + 1 || wn != w + 2 || (P.lstride & 3) || (reinterpret_cast<uintptr_t>(w) & 15)))
         return (int)hipErrorInvalidValue;
     P.bias_sh = aux ? reinterpret_cast<float*>(aux[2]) : nullptr;
@@ -2110,7 +2348,15 @@ HM_API int hm_ffm_step(const int32_t* ip, const float* hp, const int32_t* idx, c
     int fast = 0;
     const int rc = bf16 ? dispatch<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast)
                         : dispatch<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, grid, packed, slot_g, variant, stream, &fast);
-    if (rc != 0 || !fast || !P.defer) return rc;
+    if (rc != 0) return rc;
+    if (fast && P.train && P.use_linear && P.lin_atomic == 1) {
+        // the stored w of every record a row stepped: w = f(z, n) (before the deferred rows, whose
+        // generic kernel reads w)
+        hipLaunchKernelGGL(ffm_lin_derive_kernel, dim3((P.num_features + 255) / 256), dim3(256), 0, stream, P, w);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    if (!fast || !P.defer) return rc;
     return bf16 ? launch_deferred<true>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, grid, stream)
                 : launch_deferred<false>(P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss, slot_g, grid, stream);
 }

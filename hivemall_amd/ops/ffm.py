@@ -220,6 +220,36 @@ _DEFER_ON = os.environ.get("HM_FFM_DEFER", "1") != "0"
 # HM_FFM_LIN_DEFER=0 (A/B only): the fp32 kernel's W_LIN wave waits for the next row's linear-state
 # DMA at phase A with the slot DMAs, instead of at its first use in the forward pass
 _LIN_DEFER = int(os.environ.get("HM_FFM_LIN_DEFER", "1") != "0")
+# Linear FTRL steps of the pipelined fp32 kernel without lost updates (HM_FFM_LIN_ATOMIC):
+#   4 (default): the top HM_FFM_LIN_HOT features (by frequency in the learner's first batch) keep
+#     (z, n) in a dense side table during a launch; each block sums its rows' steps of them in LDS
+#     and adds the sums by float atomics when it ends; the other features keep plain record stores
+#     (csrc/kernels/ffm.hip ffm_hacc_kernel).
+#   1: every row's (z, n) steps by float atomics on the records (A/B: 8.7 M rows/s — the atomics
+#     drop the hot features' block lines from L2)
+#   0: plain record stores (a concurrent row's step to the same feature is lost)
+# The host model benchmarks/ffm_hogwild_sim.py puts ~80 % of the same-stream gap on lost linear
+# steps (docs/perf_notes.md, round 6).
+_LIN_ATOMIC = int(os.environ.get("HM_FFM_LIN_ATOMIC", "4"))
+_LIN_HOT_N = min(int(os.environ.get("HM_FFM_LIN_HOT", "2048")), 2048)   # <= HD_SIZE of the kernel
+_LIN_HOT: dict = {}   # (device, w.data_ptr(), NF) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32])
+
+
+def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
+    """lin_atomic 4: the hot-feature side tables of this state, built from its first batch."""
+    w = state["w"]
+    nf = w.shape[0]
+    key = (w.device, w.data_ptr(), nf, nhot)
+    t = _LIN_HOT.get(key)
+    if t is None:
+        cnt = torch.bincount(idx.reshape(-1).long().clamp(0, nf - 1), minlength=nf)
+        top = torch.argsort(cnt, descending=True)[:nhot]
+        top = top[cnt[top] > 0].to(torch.int32)
+        hidx = torch.full((nf,), -1, dtype=torch.int32, device=w.device)
+        hidx[top.long()] = torch.arange(top.numel(), dtype=torch.int32, device=w.device)
+        hacc = torch.zeros(max(1, top.numel()), 32, dtype=torch.float32, device=w.device)  # HACC_STRIDE
+        t = _LIN_HOT[key] = (hidx, top, hacc)
+    return t
 
 
 def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:
@@ -324,7 +354,8 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
                    (hyper.seed * 1000003 + _CALLS) & 0x7FFFFFFF, int(packed),
                    _VARIANT if variant is None else int(variant),
                    field_stride(V), int(slot_g), gstride, block[0], block[1],
-                   G.stride(1) if slot_g else 0, _LIN_DEFER, BIAS_EVERY] + list(_lin_addressing(state)),
+                   G.stride(1) if slot_g else 0, _LIN_DEFER, BIAS_EVERY] + list(_lin_addressing(state))
+                  + [_LIN_ATOMIC, 0],
                   dtype=np.int32)
     hp = hyper.hp()
     p = _native.ptr
@@ -343,8 +374,17 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
             zn0 = b[1:3].clone()
             bsh.zero_()
             bsh[0, :2] = zn0
-        aux = (ctypes.c_void_p * 4)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
-                                    p(bsh), bsh.shape[0] if bsh is not None else 0)
+        lin_mode, hidx, hot_id, hacc = _LIN_ATOMIC, None, None, None
+        if lin_mode == 4:
+            if train and hyper.use_linear and _lin_addressing(state)[1]:
+                # the bf16 kernel's LDS holds the sums of 1,024 hot features (HD12_SIZE)
+                hidx, hot_id, hacc = _lin_hot_tables(state, idx, 1024 if bf16 else _LIN_HOT_N)
+            if hot_id is None or hot_id.numel() == 0:
+                lin_mode, hidx, hot_id, hacc = 0, None, None, None
+        ip[26], ip[27] = lin_mode, hot_id.numel() if hot_id is not None else 0
+        aux = (ctypes.c_void_p * 7)(p(hot), p(_defer_buffer(V.device, B)) if (train and _DEFER_ON) else None,
+                                    p(bsh), bsh.shape[0] if bsh is not None else 0,
+                                    p(hidx), p(hot_id), p(hacc))
         rc = _native.hip().hm_ffm_step(*args, ctypes.addressof(aux), _native.stream_of(V.device))
         _native.check(rc, "hm_ffm_step")
         if bsh is not None:

@@ -425,6 +425,50 @@ SEQ_BENCH_SCALE_LOGLOSS = 0.44501
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("state", ["", " -bf16_state"])
+def test_ffm_gpu_hot_linear_steps_are_not_lost(state, monkeypatch):
+    """The side-table linear mode (HM_FFM_LIN_ATOMIC=4, the default) loses no linear FTRL step at
+    full-chip concurrency.  With V frozen (-eta0 0, -lambda 0) and w pinned at 0 (-lambda1 1e9) every
+    row's kappa is fixed by the data alone, so whatever order and concurrency the kernel trains in,
+    each hot feature (the side table's: the 1,024 most frequent of the batch) must end with z = sum
+    of its rows' g and n = sum of g^2 — what the sequential engine computes.  (The other features
+    keep plain record stores: a concurrent row can still overwrite one of their steps.)  The plain
+    record stores (mode 0) lose most steps of the hot features at this concurrency; the test checks
+    that too, so it does not pass vacuously."""
+    from hivemall_amd.io.synthetic import criteo_ffm
+    from hivemall_amd.ops import ffm as ffm_ops
+
+    idx, fld, val, y = criteo_ffm(65536, hash_bits=20, seed=11)
+    single = torch.tensor([len(set(r)) == len(r) for r in idx.tolist()])   # no multi-hot rows
+    idx, fld, val, y = idx[single], fld[single], val[single], y[single]
+    opts = "-eta0 0 -lambda 0 -lambda1 1e9 -num_fields 39" + state
+    tc = _trainer("cpu", 1 << 20, 39, extra=opts)
+    tgs = {m: _trainer("cuda", 1 << 20, 39, extra=opts) for m in ("4", "0")}
+    for tg in tgs.values():
+        _copy_state(tc, tg)                 # the same (bf16-rounded) V everywhere
+    ffm_step(tc.state, idx, fld, val, y, tc.hyper)
+    n_ref = tc.state["wn"].double()
+    z_ref = tc.state["wz"].double()
+    cnt = torch.bincount(idx.reshape(-1).long(), minlength=1 << 20)
+    top = torch.argsort(cnt, descending=True)[:512]
+    res = {}
+    for mode, tg in tgs.items():
+        monkeypatch.setattr(ffm_ops, "_LIN_ATOMIC", int(mode))
+        ffm_ops._LIN_HOT.clear()
+        ffm_step(tg.state, idx.cuda(), fld.cuda(), val.cuda(), y.cuda(), tg.hyper)
+        torch.cuda.synchronize()
+        res[mode] = (tg.state["wn"].double().cpu(), tg.state["wz"].double().cpu(), tg.state["w"].cpu())
+    n4, z4, w4 = res["4"]
+    assert float(w4.abs().max()) == 0.0
+    hot = torch.argsort(cnt, descending=True)[:1024]      # in the side table of both kernels
+    np.testing.assert_allclose(n4[hot].numpy(), n_ref[hot].numpy(), rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(z4[hot].numpy(), z_ref[hot].numpy(), rtol=2e-3,
+                               atol=2e-3 * float(z_ref[hot].abs().max()))
+    n0 = res["0"][0]
+    assert float((n0[top] / n_ref[top]).median()) < 0.5   # plain stores: most hot steps lost
+
+
+@pytest.mark.gpu
 def test_ffm_gpu_bench_scale_parity_pinned():
     """The bench-scale parity record as a test, on the headline's own data: bench.py
     --gen-device cpu trains the same 12.6 M-row criteo_ffm stream as the sequential engine's
