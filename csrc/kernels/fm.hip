@@ -528,7 +528,10 @@ int launch(const FMParams& P, const int64_t* indptr, const int32_t* idx, const f
     // 256 +2.9e-3 .. +4.1e-3 (218-234 M rows/s on config 2), 192 +2.4e-3 .. +3.6e-3 (199 M),
     // 160 +2.2e-3 .. +2.9e-3 (180 M), 128 +1.9e-3 .. +2.6e-3 (164 M).  128 (512 rows in flight)
     // is the largest grid that stays inside SURVEY's bf16 3e-3 tolerance on every box measured.
-    int64_t blocks = grid > 0 ? grid : 128;
+    // Round 6: the waves confined to 6 of the 8 XCDs (P.xcds, the auto default) take 256 inside it:
+    // +2.06e-3 / +2.13e-3 at 188 M rows/s on config 2 (7 XCDs +2.65e-3 / +3.09e-3 at 191 M; 6 XCDs
+    // at 320: +2.35e-3 / +3.26e-3, 195 M; 8 XCDs at 128: 161 M; profiles/r6/fm_xcd/).
+    int64_t blocks = grid > 0 ? grid : (P.xcds < 8 ? 256 : 128);
     if (blocks > (n + 3) / 4) blocks = (n + 3) / 4;
     if (blocks > 256 * 8 * 4) blocks = 256 * 8 * 4;
     if (blocks < 1) blocks = 1;

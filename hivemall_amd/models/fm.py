@@ -81,8 +81,8 @@ FM_OPTS = [
     flag("fp32", None, "[engine] keep V in fp32 on the GPU (default bf16)"),
     opt("batch_size", None, 1 << 20, int, "[engine] rows per kernel launch"),
     opt("grid", None, 0, int, "[engine] kernel workgroups: the Hogwild rows in flight / 4 "
-                              "(0 = auto: 128, the largest grid measured inside the bf16 3e-3 parity "
-                              "tolerance on every box; docs/compat.md)"),
+                              "(0 = auto: 256 on 6 of the 8 XCDs, inside the bf16 3e-3 parity "
+                              "tolerance; 128 with HM_FM_XCDS=8; docs/compat.md)"),
     opt("engine", None, "rowwise", str, "[engine] rowwise (per-row Hogwild kernel) | minibatch "
         "(dense mini-batch GEMMs + AdaGrad; for low-dimensional dense rows, models/fm_dense.py)"),
     opt("mini_batch", None, 8192, int, "[engine] rows per step of -engine minibatch"),

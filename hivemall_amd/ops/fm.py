@@ -96,8 +96,10 @@ HOT_FRAC = float(os.environ.get("HM_FM_HOT_FRAC", "0"))
 # XCD's updates a stale copy can absorb while the memory side serialises 1 / HOT_EVERY of them
 HOT_EVERY = int(os.environ.get("HM_FM_HOT_EVERY", "1"))
 HOT_WT = os.environ.get("HM_FM_HOT_WT", "1") != "0"
-# waves on this many of the 8 XCDs (csrc/kernels/fm.hip P.xcds; 8 = all)
-XCDS = 8
+# waves on this many of the 8 XCDs (csrc/kernels/fm.hip P.xcds; 8 = all).  6 with the auto grid
+# (256 workgroups there): +17 % on config 2 at the same parity as 8 XCDs at 128 (round 6,
+# profiles/r6/fm_xcd/)
+XCDS = 6
 
 
 def hot_flags(state: dict, idx: torch.Tensor, n_rows: int, frac: float = None,
