@@ -471,14 +471,16 @@ def test_ffm_gpu_hot_linear_steps_are_not_lost(state, monkeypatch):
 @pytest.mark.gpu
 def test_ffm_gpu_bench_scale_parity_pinned():
     """The bench-scale parity record as a test, on the headline's own data: bench.py
-    --gen-device cpu trains the same 12.6 M-row criteo_ffm stream as the sequential engine's
-    reference run.  The same kernel on one block reproduces 0.44501 exactly
-    (profiles/r5/ffm_stream_gap_src.jsonl); at full-chip concurrency the fp32 run measures
-    +2.5e-3 .. +2.8e-3 with the linear records in the feature blocks (+2.3e-3 with separate
-    linear arrays, 19 % slower; lost Hogwild updates and XCD-L2 staleness; docs/compat.md "FFM
-    same-stream gap"), so the bound is 3e-3 — NOT SURVEY.md's 1e-3 fp32 tolerance, which this
-    kernel does not meet on criteo_ffm.  The bf16-state run measures +4.0e-3 .. +4.3e-3 (bound
-    5e-3; SURVEY's bf16 3e-3 is missed too; profiles/r5/bench_cpugen_linrec.log)."""
+    --gen-device cpu trains the same 12.6 M-row criteo_ffm stream (48 steps over 8 resident
+    batches) as the sequential engine's reference run.  The same kernel on one block reproduces
+    0.44501 exactly (profiles/r5/ffm_stream_gap_src.jsonl).  At full-chip concurrency, with the
+    hot features' linear steps in the side table (round 6, no linear step lost), the fp32 run
+    measures +1.85e-3 and bf16 +2.33e-3 (profiles/r6/linhot/); what is left is lost V-slot
+    updates, which grow with the epochs over the resident batches (the host model,
+    benchmarks/ffm_hogwild_sim.py: +0.8e-3 of slot gap after 25 steps, +2.0e-3 after 48).  Bounds:
+    fp32 2.5e-3 (SURVEY's 1e-3 is met on the driver's 25-step stream, +0.96e-3, not on this one),
+    bf16 3e-3 (SURVEY's bf16 tolerance).  Before the side table: fp32 +2.5e-3 .. +2.8e-3, bf16
+    +4.0e-3 .. +4.3e-3 (round 5)."""
     import json
     import os
     import subprocess
@@ -492,8 +494,8 @@ def test_ffm_gpu_bench_scale_parity_pinned():
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["rows_trained_per_rank"] == 12582912 and rec["dtype"] == "fp32"
     assert rec["config"]["early_ramp_warmup_steps"] == 1
-    assert 0.0 <= rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS <= 3.0e-3, rec["logloss_heldout"]
-    assert abs(rec["logloss_heldout_bf16"] - SEQ_BENCH_SCALE_LOGLOSS) <= 5e-3, rec["logloss_heldout_bf16"]
+    assert -1.0e-3 <= rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS <= 2.5e-3, rec["logloss_heldout"]
+    assert abs(rec["logloss_heldout_bf16"] - SEQ_BENCH_SCALE_LOGLOSS) <= 3e-3, rec["logloss_heldout_bf16"]
 
 
 def _copy_state(tc, tg, rows=None):
