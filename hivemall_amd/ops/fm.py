@@ -100,6 +100,11 @@ HOT_WT = os.environ.get("HM_FM_HOT_WT", "1") != "0"
 # (256 workgroups there): +17 % on config 2 at the same parity as 8 XCDs at 128 (round 6,
 # profiles/r6/fm_xcd/)
 XCDS = 6
+# ... except over a learner's first RAMP_ROWS rows (a launch that starts there), which take the
+# 8-XCD grid-128 setting: early training is the most staleness-sensitive regime, and the 6-XCD
+# 256 grid measured +0.0133 vs the 8-mapper average on 200 K early rows (tests/test_fm.py bound
+# 0.012; 8 XCDs at 128: +7.9e-3 / +9.8e-3)
+RAMP_ROWS = int(os.environ.get("HM_FM_RAMP_ROWS", str(1 << 20)))
 
 
 def hot_flags(state: dict, idx: torch.Tensor, n_rows: int, frac: float = None,
@@ -145,13 +150,16 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
         if t is not None:
             assert t.numel() >= n
     bf16 = V.dtype == torch.bfloat16
+    xcds = int(os.environ.get("HM_FM_XCDS", str(XCDS)))
+    if train and grid <= 0 and t0 < RAMP_ROWS and "HM_FM_XCDS" not in os.environ:
+        xcds, grid = 8, 128
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),
                    max(1, min(W0_EVERY_MAX, int(os.environ.get(
                        "HM_FM_W0_EVERY", str(W0_EVERY if t0 >= W0_WARM_ROWS else 1))))),
                    V.stride(0), w.stride(0), WPB, max(1, HOT_EVERY) - 1,
-                   int(os.environ.get("HM_FM_XCDS", str(XCDS)))],
+                   xcds],
                   dtype=np.int32)
     assert V.stride(1) == 1 and V.stride(0) >= KP, "V rows must be contiguous"
     assert (dev.type == "cuda" and w0.numel() % 32 == 0 and w0.numel() // 32 <= 64) or w0.numel() == 1

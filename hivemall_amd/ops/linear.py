@@ -234,8 +234,10 @@ SEQ_WAVES = 8
 #   the same rows dealt over all 8 XCDs: +3e-3 .. +6e-3 at any W from 8 to 128 — the per-XCD
 #     L2s are not coherent, so an XCD keeps reading its own copy of a hot feature's line;
 #   AdaGrad (+0.5e-2 .. +2e-2) stays on the shared engine's hot-feature sums.
+#   RMSprop-Graves at 512 rows measured -0.56e-3 on the sweep but +3.05e-3 once in the GPU test
+#     suite (profiles/r6/val3/pytest_gpu.log): it runs at 256 (-0.68e-3 at 78 M rows/s).
 SEQ_ENGINE_WAVES = 512
-_SEQ_WAVES_BY_OPT = {"adam": 256, "nadam": 256, "adam_hd": 256, "eve": 128}
+_SEQ_WAVES_BY_OPT = {"adam": 256, "nadam": 256, "adam_hd": 256, "rmspropgraves": 256, "eve": 128}
 # HM_LINEAR_SEQ=0: the rules of seq_rule stay on the shared engine at SEQ_WAVES rows in flight
 _SEQ_AUTO = os.environ.get("HM_LINEAR_SEQ", "1") != "0"
 

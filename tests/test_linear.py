@@ -370,7 +370,8 @@ def test_seq_engine_routing_table():
         assert not m._use_seq(1, 1)                   # CPU device
     assert waves["adagrad"] is None
     assert waves["sgd"] == waves["rmsprop"] == waves["adadelta"] == waves["momentum"] == 512
-    assert waves["adam"] == waves["nadam"] == waves["adam_hd"] == 256 and waves["eve"] == 128
+    assert waves["adam"] == waves["nadam"] == waves["adam_hd"] == waves["rmspropgraves"] == 256
+    assert waves["eve"] == 128
     assert LO.seq_rule(L.TrainClassifier("-loss logloss -opt adagrad -reg l1", device="cpu").P) is False
     with pytest.raises(UDFArgumentException):
         L.TrainClassifier("-engine seq", device="cpu")._use_seq(1, 1)
