@@ -2096,7 +2096,7 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     // lin_atomic 4: the side table for a launch of more than one block (one block stores the
     // records in row order: the sequential engine)
     FFMParams Q = P;
-    Q.hacc_on = P.lin_atomic == 4 && blocks > 1 && variant != 6 && variant != 8 && variant != 9 && variant != 10;
+    Q.hacc_on = P.lin_atomic == 4 && blocks > 1 && !wide && variant != 6 && variant != 8 && variant != 9 && variant != 10;
     if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID);
     if (Q.hacc_on) {
         hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 0);

@@ -593,12 +593,15 @@ def test_ffm_gpu_bf16_rows_wider_than_45_features():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lin", ["arrays", "records"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_ffm_gpu_tables_of_4gib_and_more(dtype):
+def test_ffm_gpu_tables_of_4gib_and_more(dtype, lin):
     """-feature_hashing 23: the bf16 12-B slot table is 4 GiB and the fp32 block table 7.5 GiB,
     past the 32-bit slot offsets; the pipelined kernels switch to 64-bit offsets.  The rows use
     features at the top of the id range (offsets > 4 GiB) and must match the sequential engine
-    run on a small table holding the same rows."""
+    run on a small table holding the same rows.  lin "records": the linear state in the feature
+    blocks (the learner's layout), where the side-table linear mode applies on 32-bit launches —
+    the 64-bit launches keep plain record stores, so no side-table copy may wrap them."""
     g = torch.Generator().manual_seed(9)
     B, F, NF = 256, 39, 1 << 23
     base = NF - B * F
@@ -610,7 +613,12 @@ def test_ffm_gpu_tables_of_4gib_and_more(dtype):
                     device="cuda")
     V, G = new_state_tables(NF, F, 4, dtype, "cuda", packed=True, slot_g=True)
     z = lambda: torch.zeros(NF, dtype=torch.float32, device="cuda")  # noqa: E731
-    tg.state = dict(V=V, G=G, w=z(), wz=z(), wn=z(), bias=torch.zeros(4, device="cuda"))
+    if lin == "records":
+        from hivemall_amd.ops.ffm import lin_record_views
+        w, wz, wn = lin_record_views(V, G)
+        tg.state = dict(V=V, G=G, w=w, wz=wz, wn=wn, bias=torch.zeros(4, device="cuda"))
+    else:
+        tg.state = dict(V=V, G=G, w=z(), wz=z(), wn=z(), bias=torch.zeros(4, device="cuda"))
     rows = slice(base, NF)
     _copy_state(tc, tg, rows)
     lc, lg = torch.empty(B), torch.empty(B, device="cuda")
