@@ -232,11 +232,16 @@ _LIN_DEFER = int(os.environ.get("HM_FFM_LIN_DEFER", "1") != "0")
 # steps (docs/perf_notes.md, round 6).
 _LIN_ATOMIC = int(os.environ.get("HM_FFM_LIN_ATOMIC", "4"))
 _LIN_HOT_N = min(int(os.environ.get("HM_FFM_LIN_HOT", "2048")), 2048)   # <= HD_SIZE of the kernel
-_LIN_HOT: dict = {}   # (device, w.data_ptr(), NF) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32])
+_LIN_HOT: dict = {}   # (device, w.data_ptr(), NF, H) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32])
+_LIN_HOT_KEEP = 8     # states whose tables are kept (4 MB index each at 2^20 features); an evicted
+                      # state rebuilds its table from its next batch (any hot set is exact: the
+                      # table only changes where the linear steps are summed, never what they are)
 
 
 def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
-    """lin_atomic 4: the hot-feature side tables of this state, built from its first batch."""
+    """lin_atomic 4: the hot-feature side tables of this state, built from its first batch (the
+    most frequent features of that batch; a later shift of the distribution only moves which
+    features are summed in the side table, not the result, which is exact for any choice)."""
     w = state["w"]
     nf = w.shape[0]
     key = (w.device, w.data_ptr(), nf, nhot)
@@ -248,6 +253,8 @@ def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
         hidx = torch.full((nf,), -1, dtype=torch.int32, device=w.device)
         hidx[top.long()] = torch.arange(top.numel(), dtype=torch.int32, device=w.device)
         hacc = torch.zeros(max(1, top.numel()), 32, dtype=torch.float32, device=w.device)  # HACC_STRIDE
+        while len(_LIN_HOT) >= _LIN_HOT_KEEP:        # the oldest states' tables go first
+            _LIN_HOT.pop(next(iter(_LIN_HOT)))
         t = _LIN_HOT[key] = (hidx, top, hacc)
     return t
 
