@@ -234,14 +234,14 @@ _LIN_ATOMIC = int(os.environ.get("HM_FFM_LIN_ATOMIC", "4"))
 _LIN_HOT_N = min(int(os.environ.get("HM_FFM_LIN_HOT", "2048")), 2048)   # <= HD_SIZE of the kernel
 _LIN_HOT: dict = {}   # (device, w.data_ptr(), NF, H) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32])
 _LIN_HOT_KEEP = 8     # states whose tables are kept (4 MB index each at 2^20 features); an evicted
-                      # state rebuilds its table from its next batch (any hot set is exact: the
-                      # table only changes where the linear steps are summed, never what they are)
+                      # state rebuilds its table from its next batch (its records hold the folded
+                      # state after every launch, so nothing is lost)
 
 
 def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
     """lin_atomic 4: the hot-feature side tables of this state, built from its first batch (the
-    most frequent features of that batch; a later shift of the distribution only moves which
-    features are summed in the side table, not the result, which is exact for any choice)."""
+    most frequent features of that batch; a later shift of the distribution leaves newly hot
+    features on the plain record stores, where concurrent rows can overwrite their steps)."""
     w = state["w"]
     nf = w.shape[0]
     key = (w.device, w.data_ptr(), nf, nhot)
