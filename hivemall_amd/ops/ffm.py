@@ -232,20 +232,29 @@ _LIN_DEFER = int(os.environ.get("HM_FFM_LIN_DEFER", "1") != "0")
 # steps (docs/perf_notes.md, round 6).
 _LIN_ATOMIC = int(os.environ.get("HM_FFM_LIN_ATOMIC", "4"))
 _LIN_HOT_N = min(int(os.environ.get("HM_FFM_LIN_HOT", "2048")), 2048)   # <= HD_SIZE of the kernel
-_LIN_HOT: dict = {}   # (device, w.data_ptr(), NF, H) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32])
+_LIN_HOT: dict = {}   # (device, w.data_ptr(), NF, H) -> (hidx int32 [NF], hot_id int32 [H], hacc f32 [H, 32], [launches])
 _LIN_HOT_KEEP = 8     # states whose tables are kept (4 MB index each at 2^20 features); an evicted
                       # state rebuilds its table from its next batch (its records hold the folded
                       # state after every launch, so nothing is lost)
 
 
+_LIN_HOT_REFRESH = int(os.environ.get("HM_FFM_LIN_HOT_REFRESH", "256"))   # launches between rebuilds
+
+
 def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
-    """lin_atomic 4: the hot-feature side tables of this state, built from its first batch (the
-    most frequent features of that batch; a later shift of the distribution leaves newly hot
-    features on the plain record stores, where concurrent rows can overwrite their steps)."""
+    """lin_atomic 4: the hot-feature side tables of this state: the nhot most frequent features of
+    its first batch, rebuilt from the current batch every _LIN_HOT_REFRESH launches (a stream whose
+    hot features drift; between launches every record holds its folded state, so a rebuild loses
+    nothing, and the bincount costs ~2 ms per rebuild)."""
     w = state["w"]
     nf = w.shape[0]
     key = (w.device, w.data_ptr(), nf, nhot)
     t = _LIN_HOT.get(key)
+    if t is not None:
+        t[3][0] += 1
+        if _LIN_HOT_REFRESH > 0 and t[3][0] % _LIN_HOT_REFRESH == 0:
+            del _LIN_HOT[key]
+            t = None
     if t is None:
         cnt = torch.bincount(idx.reshape(-1).long().clamp(0, nf - 1), minlength=nf)
         top = torch.argsort(cnt, descending=True)[:nhot]
@@ -255,8 +264,8 @@ def _lin_hot_tables(state: dict, idx: torch.Tensor, nhot: int):
         hacc = torch.zeros(max(1, top.numel()), 32, dtype=torch.float32, device=w.device)  # HACC_STRIDE
         while len(_LIN_HOT) >= _LIN_HOT_KEEP:        # the oldest states' tables go first
             _LIN_HOT.pop(next(iter(_LIN_HOT)))
-        t = _LIN_HOT[key] = (hidx, top, hacc)
-    return t
+        t = _LIN_HOT[key] = (hidx, top, hacc, [0])
+    return t[:3]
 
 
 def _defer_buffer(device: torch.device, B: int) -> torch.Tensor:

@@ -452,15 +452,20 @@ def test_ffm_gpu_hot_linear_steps_are_not_lost(state, monkeypatch):
     cnt = torch.bincount(idx.reshape(-1).long(), minlength=1 << 20)
     top = torch.argsort(cnt, descending=True)[:512]
     res = {}
+    # two launches with the hot set rebuilt at each (HM_FFM_LIN_HOT_REFRESH 1): every record holds
+    # its folded state between launches, so the rebuild loses nothing
+    monkeypatch.setattr(ffm_ops, "_LIN_HOT_REFRESH", 1)
+    half = idx.shape[0] // 2
     for mode, tg in tgs.items():
         monkeypatch.setattr(ffm_ops, "_LIN_ATOMIC", int(mode))
         ffm_ops._LIN_HOT.clear()
-        ffm_step(tg.state, idx.cuda(), fld.cuda(), val.cuda(), y.cuda(), tg.hyper)
+        for sl in (slice(0, half), slice(half, None)):
+            ffm_step(tg.state, idx[sl].cuda(), fld[sl].cuda(), val[sl].cuda(), y[sl].cuda(), tg.hyper)
         torch.cuda.synchronize()
         res[mode] = (tg.state["wn"].double().cpu(), tg.state["wz"].double().cpu(), tg.state["w"].cpu())
     n4, z4, w4 = res["4"]
     assert float(w4.abs().max()) == 0.0
-    hot = torch.argsort(cnt, descending=True)[:1024]      # in the side table of both kernels
+    hot = torch.argsort(cnt, descending=True)[:768]       # in both launches' side tables
     np.testing.assert_allclose(n4[hot].numpy(), n_ref[hot].numpy(), rtol=2e-4, atol=1e-6)
     np.testing.assert_allclose(z4[hot].numpy(), z_ref[hot].numpy(), rtol=2e-3,
                                atol=2e-3 * float(z_ref[hot].abs().max()))
