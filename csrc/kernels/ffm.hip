@@ -2071,11 +2071,22 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         // 32-B slots: 512-thread blocks, one per CU (107 KB of LDS at 39 fields)
         if (variant == 8) return -1;
         const int need = (P.F * P.F + 511) / 512;
-        const int blocks = default_blocks(P.B, grid);
+        int blocks = default_blocks(P.B, grid);
         if (blocks <= 0) return 0;
+        // lin_atomic 4 as for k = 4 below (the 16 KB of block sums still leave one block per CU)
+        FFMParams Q = P;
+        Q.hacc_on = P.lin_atomic == 4 && blocks > 1 && !wide && variant != 6 && variant != 9;
+        if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID);
+        if (Q.hacc_on) {
+            hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 0);
+            HM_LAUNCH_RET_IF_ERR();
+        }
 #define HM_P32K8(NSV) do { \
         if (wide) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint64_t, 512, 0, 2>), dim3(blocks), dim3(512), 0, stream, \
                                      P, idx, fld, val, y, V, G, w, wz, wn, bias, pred, loss); \
+        else if (Q.hacc_on) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 0, 2, 1, 1>), dim3(blocks), \
+                                               dim3(512), 0, stream, Q, idx, fld, val, y, V, G, w, wz, wn, \
+                                               bias, pred, loss); \
         else if (variant == 6) hipLaunchKernelGGL((ffm_pipe_sg32_kernel<NSV, uint32_t, 512, 1, 2>), dim3(blocks), \
                                                   dim3(512), 0, stream, P, idx, fld, val, y, V, G, w, wz, wn, \
                                                   bias, pred, loss); \
@@ -2088,6 +2099,10 @@ int dispatch_sg32(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
         else if (need <= 3) { HM_P32K8(3); }
         else { HM_P32K8(4); }
 #undef HM_P32K8
+        if (Q.hacc_on) {
+            HM_LAUNCH_RET_IF_ERR();
+            hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 1);
+        }
         HM_LAUNCH_RET();
     }
     const int need = (P.F * P.F + 255) / 256;
