@@ -173,16 +173,17 @@ __device__ __forceinline__ void lin_add(const FFMParams& P, float* w, int i, flo
 // adds them to P.hacc by float atomics when it ends; a row reads hacc[h] (DMA'd one row ahead,
 // like the record) plus the block's own sums.  Nothing is lost to a concurrent row, and the
 // atomics land in the side table, not in the hot features' blocks: atomics on the records
-// themselves drop those lines from L2 and took the kernel from 93 to 28 M rows/s
-// (profiles/r6/linhot/).  Cold features keep the plain record stores.
+// themselves drop those lines from L2, which every row reads (per-row atomics on the records: 8.7 M
+// rows/s, block sums flushed onto the records: 28 M, vs 93 M with plain stores;
+// profiles/r6/linhot/).  Cold features keep the plain record stores.
 constexpr int HD_SIZE = 2048;
 constexpr int HD12_SIZE = 1024;   // ffm_pipe_sg12_kernel (bf16 12-B slots)
 // one side-table entry per 128-B line (16-B entries, 8 to a line: 73.6 vs 76.0 M rows/s)
 constexpr int HACC_STRIDE = 32;
 // default grid of a side-table launch: a block's sums are flushed when it ends, so fewer, longer-
 // lived blocks add fewer atomics per row (distinct hot features per block grow slower than its
-// rows).  Measured (profiles/r6/linhot/): 8,192 blocks 76.0 M rows/s, 4,096 .., 2,048 84.5 M at
-// +0.96e-3 .. +1.01e-3; 1,024 (256 rows per block) diverges (+0.06 .. +0.11): every block walks
+// rows).  Measured (profiles/r6/linhot/): 8,192 blocks 76.0 M rows/s, 4,096 82.4 M (+0.90e-3),
+// 2,048 84.2-84.8 M at +0.96e-3 .. +1.01e-3; 1,024 (256 rows per block) diverges (+0.06 .. +0.11): every block walks
 // its own copy of a hot feature's weight toward the target for 256 rows and the sum of those walks
 // overshoots.
 constexpr int HACC_GRID = 2048;
