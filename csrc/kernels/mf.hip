@@ -397,9 +397,35 @@ __device__ __forceinline__ Trip bpr_resolve(const MFParams& P, Draw d, uint32_t 
     return t;
 }
 
-struct Gath { float pu, qi, qj, bi, bj; };
+template <int V>
+struct Gath { float pu[V], qi[V], qj[V]; float bi, bj; };
 
-template <int G>
+// V factors per lane (V = 4: 16-B loads and stores, G = 16 lanes per triple at k = 64, so a wave
+// instruction moves four triples' rows instead of one)
+template <int V>
+__device__ __forceinline__ void ldv(const MFParams& P, const float* p, float (&o)[V]) {
+    if constexpr (V == 4) {
+        // P.coherent: a non-temporal 16-B load, which also bypasses the CU's L1 (MI355X_MICROARCH.md)
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = P.coherent ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p))
+                                 : *reinterpret_cast<const f4v*>(p);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < V; ++q) o[q] = ldm(P, p + q);
+    }
+}
+template <int V>
+__device__ __forceinline__ void stv(float* p, const float (&o)[V]) {
+    if constexpr (V == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < V; ++q) p[q] = o[q];
+    }
+}
+
+template <int G, int V = 1>
 __global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t* __restrict__ tu,
                                                       const int32_t* __restrict__ ti,
                                                       const int32_t* __restrict__ tj, int64_t n,
@@ -421,13 +447,16 @@ __global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t*
         return r < n && t.u >= 0 && t.u < P.n_users && t.i >= 0 && t.i < P.n_items && t.j >= 0 &&
                t.j < P.n_items && t.i != t.j;
     };
-    auto gather = [&](int64_t r, const Trip& t) -> Gath {
-        Gath g{0.f, 0.f, 0.f, 0.f, 0.f};
+    auto gather = [&](int64_t r, const Trip& t) -> Gath<V> {
+        Gath<V> g;
+#pragma unroll
+        for (int q = 0; q < V; ++q) g.pu[q] = g.qi[q] = g.qj[q] = 0.f;
+        g.bi = g.bj = 0.f;
         const bool ok = valid(r, t);
-        if (ok && f < P.k) {
-            g.pu = ldm(P, Pu + (size_t)t.u * P.kp + f);
-            g.qi = ldm(P, Qi + (size_t)t.i * P.kp + f);
-            g.qj = ldm(P, Qi + (size_t)t.j * P.kp + f);
+        if (ok && f * V < P.k) {
+            ldv<V>(P, Pu + (size_t)t.u * P.kp + f * V, g.pu);
+            ldv<V>(P, Qi + (size_t)t.i * P.kp + f * V, g.qi);
+            ldv<V>(P, Qi + (size_t)t.j * P.kp + f * V, g.qj);
         }
         if (ok && P.use_bias) { g.bi = ldm(P, Bi + t.i); g.bj = ldm(P, Bi + t.j); }
         return g;
@@ -437,7 +466,7 @@ __global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t*
     Draw da = bpr_d1(P, r0, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
     Draw db = bpr_d1(P, r0 + stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
     Trip ta = bpr_resolve(P, da, bpr_d2(P, da, bitmap, sampled), bitmap, sampled);
-    Gath ga = gather(r0, ta);
+    Gath<V> ga = gather(r0, ta);
     uint32_t wb = bpr_d2(P, db, bitmap, sampled);
     Draw dc = bpr_d1(P, r0 + 2 * stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
     for (int64_t base = wave * PER; base < n; base += stride) {
@@ -446,10 +475,13 @@ __global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t*
         const Draw dn = bpr_d1(P, r + 3 * stride, n, t0, tu, ti, tj, uitems, pos_user, n_pos);
         const uint32_t wc = bpr_d2(P, dc, bitmap, sampled);
         const Trip tb = bpr_resolve(P, db, wb, bitmap, sampled);
-        const Gath gb = gather(r + stride, tb);
+        const Gath<V> gb = gather(r + stride, tb);
         // ---- compute triple r ----
         const bool ok = valid(r, ta);
-        const float d = group_sum<G>(ga.pu * (ga.qi - ga.qj));
+        float part = 0.f;
+#pragma unroll
+        for (int q = 0; q < V; ++q) part += ga.pu[q] * (ga.qi[q] - ga.qj[q]);
+        const float d = group_sum<G>(part);
         const float x = ga.bi - ga.bj + d;
         float z;
         if (P.loss == 2) { const float sg = hm::sigmoidf_(x); z = sg * (1.f - sg); }
@@ -457,10 +489,17 @@ __global__ __launch_bounds__(256) void bpr_pf3_kernel(MFParams P, const int32_t*
         if (ok && f == 0) lacc += (double)hm::log1pexp(-x);
         if (ok) {
             const float eta = eta_t(P, (float)(t0 + r + 1));
-            if (f < P.k) {
-                Pu[(size_t)ta.u * P.kp + f] = ga.pu + eta * (z * (ga.qi - ga.qj) - P.lambda_u * ga.pu);
-                Qi[(size_t)ta.i * P.kp + f] = ga.qi + eta * (z * ga.pu - P.lambda_i * ga.qi);
-                Qi[(size_t)ta.j * P.kp + f] = ga.qj + eta * (-z * ga.pu - P.lambda_j * ga.qj);
+            if (f * V < P.k) {
+                float nu[V], ni[V], nj[V];
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    nu[q] = ga.pu[q] + eta * (z * (ga.qi[q] - ga.qj[q]) - P.lambda_u * ga.pu[q]);
+                    ni[q] = ga.qi[q] + eta * (z * ga.pu[q] - P.lambda_i * ga.qi[q]);
+                    nj[q] = ga.qj[q] + eta * (-z * ga.pu[q] - P.lambda_j * ga.qj[q]);
+                }
+                stv<V>(Pu + (size_t)ta.u * P.kp + f * V, nu);
+                stv<V>(Qi + (size_t)ta.i * P.kp + f * V, ni);
+                stv<V>(Qi + (size_t)ta.j * P.kp + f * V, nj);
             }
             if (P.use_bias && f == 0) {
                 Bi[ta.i] = ga.bi + eta * (z - P.lambda_b * ga.bi);
@@ -563,6 +602,15 @@ HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, co
         hipLaunchKernelGGL((bpr_pf3_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, \
                            tu, ti, tj, n, uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap,        \
                            Pu, Qi, Bi, loss_sum)
+    // k in (32, 64] on 16-B-aligned rows: 16 lanes x 4 factors per triple (variant 4 or the
+    // default), the 64-lane form with variant 5 (A/B)
+    const bool v4 = P.k > 32 && (P.kp & 3) == 0 && variant != 1 && variant != 2 && variant != 5 &&
+                    (tu || bitmap);
+    if (v4) {
+        hipLaunchKernelGGL((bpr_pf3_kernel<16, 4>), dim3(grid_for(n, 4)), dim3(256), 0, stream, P, tu, ti, tj, n,
+                           uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap, Pu, Qi, Bi, loss_sum);
+        HM_LAUNCH_RET();
+    }
     if (P.k <= 8) HM_BPR(8);
     else if (P.k <= 16) HM_BPR(16);
     else if (P.k <= 32) HM_BPR(32);
