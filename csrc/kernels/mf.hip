@@ -602,13 +602,18 @@ HM_API int hm_bpr_step(const int32_t* ip, const float* hp, const int32_t* tu, co
         hipLaunchKernelGGL((bpr_pf3_kernel<GG>), dim3(grid_for(n, 64 / GG)), dim3(256), 0, stream, P, \
                            tu, ti, tj, n, uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap,        \
                            Pu, Qi, Bi, loss_sum)
-    // k in (32, 64] on 16-B-aligned rows: 16 lanes x 4 factors per triple (variant 4 or the
-    // default), the 64-lane form with variant 5 (A/B)
-    const bool v4 = P.k > 32 && (P.kp & 3) == 0 && variant != 1 && variant != 2 && variant != 5 &&
-                    (tu || bitmap);
+    // k in (16, 64] on 16-B-aligned rows: 4 factors per lane, k / 4 lanes per triple, so one wave
+    // instruction moves 64 / G triples' rows (the default).  Measured (profiles/r6/bpr_v4/): k = 64
+    // 3.31 vs 1.48-1.59 G triples/s, k = 32 4.99 vs 2.84 G; k = 16 4.18 vs 4.44 G and k = 10 4.35 vs
+    // 4.36 G keep the one-factor-per-lane forms (also variant 5, A/B)
+    const bool v4 = P.k > 16 && (P.kp & 3) == 0 && variant != 1 && variant != 2 && variant != 5 && (tu || bitmap);
     if (v4) {
-        hipLaunchKernelGGL((bpr_pf3_kernel<16, 4>), dim3(grid_for(n, 4)), dim3(256), 0, stream, P, tu, ti, tj, n,
-                           uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap, Pu, Qi, Bi, loss_sum);
+        if (P.k <= 32)
+            hipLaunchKernelGGL((bpr_pf3_kernel<8, 4>), dim3(grid_for(n, 8)), dim3(256), 0, stream, P, tu, ti, tj, n,
+                               uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap, Pu, Qi, Bi, loss_sum);
+        else
+            hipLaunchKernelGGL((bpr_pf3_kernel<16, 4>), dim3(grid_for(n, 4)), dim3(256), 0, stream, P, tu, ti, tj, n,
+                               uitems, pos_user, n_pos, t0, tu ? nullptr : bitmap, Pu, Qi, Bi, loss_sum);
         HM_LAUNCH_RET();
     }
     if (P.k <= 8) HM_BPR(8);
