@@ -100,11 +100,15 @@ HOT_WT = os.environ.get("HM_FM_HOT_WT", "1") != "0"
 # (256 workgroups there): +17 % on config 2 at the same parity as 8 XCDs at 128 (round 6,
 # profiles/r6/fm_xcd/)
 XCDS = 6
-# ... except over a learner's first RAMP_ROWS rows (a launch that starts there), which take the
-# 8-XCD grid-128 setting: early training is the most staleness-sensitive regime, and the 6-XCD
-# 256 grid measured +0.0133 vs the 8-mapper average on 200 K early rows (tests/test_fm.py bound
-# 0.012; 8 XCDs at 128: +7.9e-3 / +9.8e-3)
+# ... except over a learner's first RAMP_ROWS rows (a launch that starts there), which run on ONE
+# XCD at grid 128: early training is the most staleness-sensitive regime.  On the 200 K early
+# rows of test_fm_gpu_logloss_parity vs the 8-mapper average (profiles/r6/fm_xcd/fm_ramp_*):
+# 6 XCDs at 256 +0.0133; 8 XCDs at 128 +0.009 .. +0.0105 (fp32 / bf16); 2 XCDs at 128 +2.6e-3 ..
+# +6.6e-3; 1 XCD at 128 +0.0 .. +1.4e-3 fp32, +4.3e-3 .. +4.4e-3 bf16 — at ~31 M rows/s, i.e.
+# ~30 ms once per learner
 RAMP_ROWS = int(os.environ.get("HM_FM_RAMP_ROWS", str(1 << 20)))
+RAMP_GRID = int(os.environ.get("HM_FM_RAMP_GRID", "128"))
+RAMP_XCDS = int(os.environ.get("HM_FM_RAMP_XCDS", "1"))
 
 
 def hot_flags(state: dict, idx: torch.Tensor, n_rows: int, frac: float = None,
@@ -152,7 +156,7 @@ def fm_step(state: dict, indptr: torch.Tensor, idx: torch.Tensor, val: torch.Ten
     bf16 = V.dtype == torch.bfloat16
     xcds = int(os.environ.get("HM_FM_XCDS", str(XCDS)))
     if train and grid <= 0 and t0 < RAMP_ROWS and "HM_FM_XCDS" not in os.environ:
-        xcds, grid = 8, 128
+        xcds, grid = RAMP_XCDS, RAMP_GRID
     ip = np.array([dims, k, KP, int(h.classification), int(train), h.eta_kind, int(h.use_w0),
                    int(bf16), grid, h.seed & 0x7FFFFFFF, max(1, w0.numel() // 32),
                    int(os.environ.get("HM_FM_VARIANT", "0")),

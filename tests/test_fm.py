@@ -127,12 +127,14 @@ def test_fm_gpu_logloss_parity(fp32):
     ref = mapper_average_fm(opts, idx, y, 8, 262144)
     res = {"sequential": ll(seq, "cpu"), "mappers8": ll(ref, "cpu"), "gpu": ll(gpu, "cuda")}
     print(res)
-    # measured (profiles/fm_sweep_r1.log): the 256-block Hogwild grid landed ~0.01 above the
-    # 8-mapper average on these 200 K early-training rows; the 128-block default +7.9e-3 /
-    # +9.8e-3 (fp32 / bf16, profiles/r5/pytest_fm_zz.log).  Plain SGD (no AdaGrad) is the most
-    # staleness-sensitive learner, and early training the most sensitive regime (the steady
-    # state past 2^20 rows is bounded at SURVEY's 3e-3 below)
-    assert res["gpu"] <= res["mappers8"] + 0.012, res
+    # measured: the 256-block Hogwild grid landed ~0.01 above the 8-mapper average on these 200 K
+    # early-training rows (profiles/fm_sweep_r1.log); 8 XCDs at 128 blocks +7.9e-3 .. +0.0105
+    # (fp32 / bf16); since round 6 a learner's first 2^20 rows run on ONE XCD at 128 blocks (ops/fm.py
+    # RAMP_*): +0.0 .. +1.4e-3 fp32, +4.3e-3 .. +4.4e-3 bf16 (profiles/r6/fm_xcd/fm_ramp_*).  Plain
+    # SGD (no AdaGrad) is the most staleness-sensitive learner, and early training the most
+    # sensitive regime (the steady state past 2^20 rows is bounded at SURVEY's 3e-3 below).
+    # Bound 0.012 -> 0.007 (round 6, tightened).
+    assert res["gpu"] <= res["mappers8"] + 0.007, res
 
 
 @pytest.mark.gpu
