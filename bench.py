@@ -224,7 +224,8 @@ def run_schedule(args, ctx, idx, fld, val, y, state: str, data, metrics=None) ->
         ramp = i < ramp_steps
         ffm_step(st, idx[s:s + B], None if fld is None else fld[s:s + B],
                  None if val is None else val[s:s + B], y[s:s + B], hyper, train=True,
-                 grid=args.grid, loss=loss_buf, variant=ffm_model.RAMP_VARIANT if ramp else None)
+                 grid=args.grid, loss=loss_buf, variant=ffm_model.RAMP_VARIANT if ramp else None,
+                 lin_mode=ffm_model.dp_lin_mode(world))
         if loss_buf is not None:
             step_loss.append(loss_buf.mean())          # device scalar, read after timing
         if world > 1 and (i + 1) % args.mix_every == 0:

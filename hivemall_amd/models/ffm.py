@@ -98,6 +98,11 @@ DP_GUARD_RISE = 0.02
 DP_GUARD_POWER = 0.5
 
 
+def dp_lin_mode(world: int) -> int | None:
+    """ops.ffm.ffm_step's ``lin_mode`` for a replica of ``world`` ranks (FFMTrainer.lin_mode)."""
+    return 0 if world > 1 else None
+
+
 def dp_lr_scale(world: int, power: float = DP_LR_POWER) -> float:
     """Step-size factor of a data-parallel replica (1.0 on one rank)."""
     return float(world) ** float(power) if world > 1 else 1.0
@@ -193,6 +198,13 @@ class FFMTrainer(Learner):
     @dp_power.setter
     def dp_power(self, power: float) -> None:
         self._set_dp_power(float(power))
+
+    def lin_mode(self) -> int | None:
+        """The linear steps' form: the side table (module default) on one rank; the plain record
+        stores for replicas that mix during training (the N^p step rule was calibrated with them,
+        and an 8-rank rehearsal measured the side table no better there: +5.2e-3 vs +4.6e-3 against
+        the N = 8 sequential reference, profiles/r6/dp_side/)."""
+        return dp_lin_mode(self.mixer.world if self._dp() else 1)
 
     def _set_dp_power(self, power: float) -> None:
         sc = dp_lr_scale(self.mixer.world, power) if self._dp() else 1.0
@@ -324,7 +336,8 @@ class FFMTrainer(Learner):
                 ffm_step(self.state, part.idx, part.fld, part.val, part.y, self.hyper, train=True,
                          loss=None if lb is None else lb[r0:r1], grid=grid,
                          # (an explicit HM_FFM_VARIANT selects the kernel for every row)
-                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None)
+                         variant=RAMP_VARIANT if ramp and RAMP_VARIANT >= 0 and _ffm_ops._VARIANT == 0 else None,
+                         lin_mode=self.lin_mode())
             self.rows_seen += sub.n
             mi = int(self.cl["mix_interval"])
             if self.mixer is not None and mi > 0:

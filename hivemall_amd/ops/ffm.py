@@ -299,8 +299,10 @@ def _has_multihot(idx: torch.Tensor, fld: torch.Tensor | None) -> bool:
 def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torch.Tensor | None,
              y: torch.Tensor | None, hyper: FFMHyper, train: bool = True,
              pred: torch.Tensor | None = None, loss: torch.Tensor | None = None,
-             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None) -> None:
-    """One fused pass over a padded-ELL batch.
+             grid: int = 0, variant: int | None = None, hot: torch.Tensor | None = None,
+             lin_mode: int | None = None) -> None:
+    """One fused pass over a padded-ELL batch.  ``lin_mode``: the linear steps' form
+    (HM_FFM_LIN_ATOMIC values; None = the module default, the side table).
 
     state: dict with V, G ([NF, NFLD, Kp] f32 or bf16; either two contiguous tables or the two
     halves of one packed [NF, NFLD, 2, Kp] table, see :func:`is_packed`), w, wz, wn ([NF] f32),
@@ -390,7 +392,7 @@ def ffm_step(state: dict, idx: torch.Tensor, fld: torch.Tensor | None, val: torc
             zn0 = b[1:3].clone()
             bsh.zero_()
             bsh[0, :2] = zn0
-        lin_mode, hidx, hot_id, hacc = _LIN_ATOMIC, None, None, None
+        lin_mode, hidx, hot_id, hacc = _LIN_ATOMIC if lin_mode is None else int(lin_mode), None, None, None
         if lin_mode == 4:
             if train and hyper.use_linear and _lin_addressing(state)[1]:
                 # the bf16 kernel's LDS holds the sums of 1,024 hot features (HD12_SIZE)
