@@ -145,6 +145,11 @@ def self_launch(args, argv) -> int | None:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _dp_lin_mode(world: int):
+    from hivemall_amd.models.ffm import dp_lin_mode
+    return dp_lin_mode(world)
+
+
 def check_world(args, ctx) -> None:
     """Every rank: the job must really be N ranks (driver contract: value = whole-job rate)."""
     import torch.distributed as dist
@@ -441,6 +446,10 @@ def main(argv=None):
                 "mix_wire": main_run["mix_wire"],
                 "dp_lr_scale": round(main_run["dp_lr_scale"], 4),
                 "early_ramp_warmup_steps": main_run["ramp_steps"],
+                # FTRL linear steps: hot features' (z, n) in the side table (one rank, no step lost)
+                # or plain record stores (replicas that mix: the N^p step rule's calibration)
+                "linear_steps": ("side-table" if _dp_lin_mode(world) is None and dev.type == "cuda"
+                                 else "plain-stores"),
                 "resident_batches": nres,
             },
             "rccl_world": world if ctx.backend == "nccl" else None,
