@@ -1765,6 +1765,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
             // one 16-B read per lane (contiguous: conflict-free); separate 4-B and 8-B reads at a
             // 16-B lane stride were 4-way / 2-way bank conflicts
             const uint4 q = *reinterpret_cast<const uint4*>(s_raw + (j * 256 + tid) * 4);
+            // q.w is not needed, and without this use the compiler narrows the read back to the
+            // conflicting ds_read_b64 + ds_read_b32 pair
+            asm volatile("" :: "v"(q.w));
             cg[j] = __uint_as_float(q.z);
             if (tid + j * 256 < FF) s_t[SB(j) * F + SA(j)] = make_uint2(q.x, q.y);
         }
