@@ -271,6 +271,7 @@ def test_bench_self_launch_cpu_world2():
     assert d["n_gpus"] == 2 and d["world"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["dist_backend"] == "gloo" and d["rccl_world"] is None
     assert d["config"]["mixes_in_timed_region"] == 2
+    assert d["config"]["linear_steps"] == "plain-stores"   # replicas that mix (dp_lin_mode)
     assert d["mix_ms"] > 0 and d["mix_wire_bytes_per_rank"] > 0 and d["mix_bus_gbps"] > 0
 
 

@@ -499,6 +499,7 @@ def test_ffm_gpu_bench_scale_parity_pinned():
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["rows_trained_per_rank"] == 12582912 and rec["dtype"] == "fp32"
     assert rec["config"]["early_ramp_warmup_steps"] == 1
+    assert rec["config"]["linear_steps"] == "side-table"   # one rank keeps every hot linear step
     assert -1.0e-3 <= rec["logloss_heldout"] - SEQ_BENCH_SCALE_LOGLOSS <= 2.5e-3, rec["logloss_heldout"]
     assert abs(rec["logloss_heldout_bf16"] - SEQ_BENCH_SCALE_LOGLOSS) <= 3e-3, rec["logloss_heldout_bf16"]
 
