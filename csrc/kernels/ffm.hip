@@ -187,6 +187,12 @@ constexpr int HACC_STRIDE = 32;
 // its own copy of a hot feature's weight toward the target for 256 rows and the sum of those walks
 // overshoots.
 constexpr int HACC_GRID = 2048;
+// The bf16 kernel holds 3 blocks per CU (768 resident), so 2,048 blocks leave its last round 2/3
+// full: 2,304 (3 full rounds) 128.1-128.9 M bf16 rows/s at +1.58e-3 .. +1.67e-3 vs 125.8-125.9 M at
+// 2,048; 3,072 126.5-126.9 M; 1,536 (171 rows per block) 131.2-131.7 M but diverging (+8e-3 ..
+// +1.0e-2).  The fp32 kernel's 2 blocks per CU make 2,048 four full rounds (2,304: 81.5-81.8 M vs
+// 84.8-85.0 M).  profiles/r6/hacc_grid/
+constexpr int HACC_GRID12 = 2304;
 
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
@@ -2033,7 +2039,7 @@ int dispatch_sg12(const FFMParams& P, const int32_t* idx, const int32_t* fld, co
     if (blocks <= 0) return 0;
     FFMParams Q = P;
     Q.hacc_on = P.lin_atomic == 4 && P.nhot <= HD12_SIZE && blocks > 1 && !wide && variant != 9 && variant != 10;
-    if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID);
+    if (Q.hacc_on && grid <= 0) blocks = default_blocks(P.B, grid, HACC_GRID12);
     if (Q.hacc_on) {
         hipLaunchKernelGGL(ffm_hacc_kernel, dim3((P.nhot + 255) / 256), dim3(256), 0, stream, Q, w, 0);
         HM_LAUNCH_RET_IF_ERR();
