@@ -388,6 +388,17 @@ class BPRMF(_MFBase):
         self.grid = int(c["grid"])
         self.sharded = None        # {"P", "Q", "Bi"} ShardedTables with -shard_model
 
+    def _grid(self) -> int:
+        """The base rule (1 block per 32 items / users), rounded up to a power of two once it
+        reaches the 256 CUs: ML-20M-shaped k = 64 (16-lane float4 kernel, two boxes): 852 blocks
+        3.33-3.36 G triples/s, 1,024 3.66-3.67 G, 1,280 / 2,048 / 2,560 3.65-3.68 G, but 1,536 and
+        1,704 3.29-3.35 G; sampled AUC 0.7096-0.7101 at every grid up to 3,408
+        (profiles/r6/bpr_grid/)."""
+        g = super()._grid()
+        if int(self.cl["grid"]) > 0 or g < 256:
+            return g
+        return min(4096, 1 << (g - 1).bit_length())
+
     def init_state(self, n_users, n_items):
         self.n_users, self.n_items = int(n_users), int(n_items)
         g = torch.Generator().manual_seed(self.seed)
