@@ -201,3 +201,19 @@ def test_inert_option_warns(caplog):
     with caplog.at_level(logging.WARNING, logger="hivemall_amd"):
         MatrixFactorization("-factors 4 -scale 10", device="cpu")
     assert any("-scale" in r.getMessage() and "no effect" in r.getMessage() for r in caplog.records)
+
+
+def test_bpr_grid_rule_rounds_up_to_a_power_of_two():
+    """BPRMF._grid: 1 block per 32 items / users (the contention rule), rounded up to a power of
+    two once it reaches 256 blocks (ML-20M: 852 -> 1,024, profiles/r6/bpr_grid/); an explicit
+    -grid is kept as given."""
+    m = BPRMF("-factors 8")
+    m.n_users, m.n_items = 138493, 27278
+    assert m._grid() == 1024
+    m.n_users, m.n_items = 5000, 4000          # 125 blocks: below the rounding threshold
+    assert m._grid() == 125
+    m.n_users, m.n_items = 10 ** 7, 10 ** 7    # capped
+    assert m._grid() == 4096
+    m2 = BPRMF("-factors 8 -grid 852")
+    m2.n_users, m2.n_items = 138493, 27278
+    assert m2._grid() == 852
