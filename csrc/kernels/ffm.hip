@@ -191,7 +191,9 @@ constexpr int HACC_GRID = 2048;
 // full: 2,304 (3 full rounds) 128.1-128.9 M bf16 rows/s at +1.58e-3 .. +1.67e-3 vs 125.8-125.9 M at
 // 2,048; 3,072 126.5-126.9 M; 1,536 (171 rows per block) 131.2-131.7 M but diverging (+8e-3 ..
 // +1.0e-2).  The fp32 kernel's 2 blocks per CU make 2,048 four full rounds (2,304: 81.5-81.8 M vs
-// 84.8-85.0 M).  profiles/r6/hacc_grid/
+// 84.8-85.0 M).  profiles/r6/hacc_grid/.  More fp32 blocks do not buy a safer gap either:
+// 2,048 84.4-84.8 M at +0.95e-3 / +0.97e-3, 3,072 83.0-83.6 M at +0.90e-3 / +0.97e-3, 4,096
+// 81.5-82.2 M at +0.90e-3 / +0.96e-3 (one box, interleaved; profiles/r6/hacc_grid/fp32/).
 constexpr int HACC_GRID12 = 2304;
 
 __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
